@@ -1,0 +1,274 @@
+/* fd25519_fe.h -- GF(2^255-19) arithmetic for gfx950, one field element
+   per lane in ten signed 32-bit limbs (radix 2^25.5: limb i holds bits
+   [ceil(25.5 i), ceil(25.5 (i+1)) ), 26 bits for even i, 25 for odd).
+
+   Why this shape on MI355X: the products are 32x32->64 signed
+   multiply-accumulates, which hipcc lowers to one v_mad_i64_i32 each (a
+   VOP3 op that issues at half the rate of a plain VALU add on gfx950,
+   measured in tools/ubench/int_ubench.hip -- the same issue cost as a
+   24-bit multiply and cheaper than an f64 FMA).  A full product is 100 of
+   them plus a 12-step carry chain; a square 55.  Nothing here is a dense
+   contraction, so MFMA is not used.
+
+   Semantics follow the field API of the reference
+   (src/ballet/ed25519/fd_f25519.h:46-253): frombytes ignores bit 255 and
+   accepts non-canonical values (>= p), comparisons are on canonical
+   encodings.
+
+   Bound discipline (|limb| relative to 2^25 even / 2^24 odd):
+     tight  (outputs of mul/sq/carry, constants)  <= 1.01x
+     add/sub of two tight values                   <= 2.02x
+     add/sub of a tight and a 2.02x value          <= 3.03x
+   mul/sq accept inputs <= 3.3x (|limb| < 1.65*2^26 / 1.65*2^25): every
+   product term fits in a signed 32-bit operand (19*1.65*2^26 < 2^31) and
+   every 64-bit column sum stays below 2^63. */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FD_DEV __device__ __forceinline__
+
+struct fe { int32_t v[10]; };
+
+/* Constants in centered limbs (tight). */
+#define FE_D      {-10913610, 13857413, -15372611, 6949391, 114729, -8787816, -6275908, -3247719, -18696448, -12055116}
+#define FE_D2     {-21827239, -5839606, -30745221, 13898782, 229458, 15978800, -12551817, -6495438, 29715968, 9444199}
+#define FE_SQRTM1 {-32595792, -7943725, 9377950, 3500415, 12389472, -272473, -25146209, -2005654, 326686, 11406482}
+#define FE_BX     {-14297830, -7645148, 16144683, -16471763, 27570974, -2696100, -26142465, 8378389, 20764389, 8758491}
+#define FE_BY     {-26843541, -6710886, 13421773, -13421773, 26843546, 6710886, -13421773, 13421773, -26843546, -6710886}
+
+FD_DEV void fe_set_const(fe& h, const int32_t (&c)[10]) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = c[i];
+}
+
+FD_DEV void fe_0(fe& h) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = 0;
+}
+
+FD_DEV void fe_1(fe& h) {
+  fe_0(h);
+  h.v[0] = 1;
+}
+
+FD_DEV void fe_add(fe& h, const fe& f, const fe& g) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = f.v[i] + g.v[i];
+}
+
+FD_DEV void fe_sub(fe& h, const fe& f, const fe& g) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = f.v[i] - g.v[i];
+}
+
+FD_DEV void fe_neg(fe& h, const fe& f) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = -f.v[i];
+}
+
+/* h = c ? g : f  (per-lane select, no branch) */
+FD_DEV void fe_select(fe& h, const fe& f, const fe& g, bool c) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = c ? g.v[i] : f.v[i];
+}
+
+/* Column sums h[k] of a 10x10 product, reduced to tight limbs.  Carries
+   round to nearest (centered limbs) in two interleaved chains. */
+FD_DEV void fe_carry_wide(fe& h, int64_t (&a)[10]) {
+  int64_t c;
+  c = (a[0] + (1LL << 25)) >> 26; a[1] += c; a[0] -= c << 26;
+  c = (a[4] + (1LL << 25)) >> 26; a[5] += c; a[4] -= c << 26;
+  c = (a[1] + (1LL << 24)) >> 25; a[2] += c; a[1] -= c << 25;
+  c = (a[5] + (1LL << 24)) >> 25; a[6] += c; a[5] -= c << 25;
+  c = (a[2] + (1LL << 25)) >> 26; a[3] += c; a[2] -= c << 26;
+  c = (a[6] + (1LL << 25)) >> 26; a[7] += c; a[6] -= c << 26;
+  c = (a[3] + (1LL << 24)) >> 25; a[4] += c; a[3] -= c << 25;
+  c = (a[7] + (1LL << 24)) >> 25; a[8] += c; a[7] -= c << 25;
+  c = (a[4] + (1LL << 25)) >> 26; a[5] += c; a[4] -= c << 26;
+  c = (a[8] + (1LL << 25)) >> 26; a[9] += c; a[8] -= c << 26;
+  c = (a[9] + (1LL << 24)) >> 25; a[0] += c * 19; a[9] -= c << 25;
+  c = (a[0] + (1LL << 25)) >> 26; a[1] += c; a[0] -= c << 26;
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = (int32_t)a[i];
+}
+
+/* h = f*g.  Term (i,j) lands in column (i+j) mod 10; it is doubled when i
+   and j are both odd (the half-bit of the 25.5 radix) and multiplied by 19
+   when it wraps (2^255 = 19 mod p). */
+FD_DEV void fe_mul(fe& h, const fe& f, const fe& g) {
+  int64_t a[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) a[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      const int k = i + j;
+      const int32_t x = ((i & 1) && (j & 1)) ? 2 * f.v[i] : f.v[i];
+      const int32_t y = (k >= 10) ? 19 * g.v[j] : g.v[j];
+      a[k >= 10 ? k - 10 : k] += (int64_t)x * y;
+    }
+  }
+  fe_carry_wide(h, a);
+}
+
+/* h = f^2 (55 products): off-diagonal terms carry the factor 2 on the
+   left operand, the odd/odd and wrap factors (2, 19, 38) on the right. */
+FD_DEV void fe_sq(fe& h, const fe& f) {
+  int64_t a[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) a[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = i; j < 10; j++) {
+      const int k = i + j;
+      const int m = (((i & 1) && (j & 1)) ? 2 : 1) * ((k >= 10) ? 19 : 1);
+      const int32_t x = (i == j) ? f.v[i] : 2 * f.v[i];
+      const int32_t y = m * f.v[j];
+      a[k >= 10 ? k - 10 : k] += (int64_t)x * y;
+    }
+  }
+  fe_carry_wide(h, a);
+}
+
+/* h = 2 f^2 */
+FD_DEV void fe_sq2(fe& h, const fe& f) {
+  int64_t a[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) a[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = i; j < 10; j++) {
+      const int k = i + j;
+      const int m = (((i & 1) && (j & 1)) ? 2 : 1) * ((k >= 10) ? 19 : 1);
+      const int32_t x = (i == j) ? 2 * f.v[i] : 4 * f.v[i];
+      const int32_t y = m * f.v[j];
+      a[k >= 10 ? k - 10 : k] += (int64_t)x * y;
+    }
+  }
+  fe_carry_wide(h, a);
+}
+
+/* Re-tighten a 32-bit-limb element (e.g. the result of adds/subs). */
+FD_DEV void fe_carry(fe& h, const fe& f) {
+  int64_t a[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) a[i] = f.v[i];
+  fe_carry_wide(h, a);
+}
+
+/* Load 32 little-endian bytes given as 8 words; bit 255 is ignored and
+   values >= p are accepted (reduced implicitly by the arithmetic). */
+FD_DEV void fe_frombytes(fe& h, const uint32_t (&w)[8]) {
+  /* limb offsets 0,26,51,77,102,128,153,179,204,230 */
+  const uint32_t m26 = (1u << 26) - 1u, m25 = (1u << 25) - 1u;
+  h.v[0] = (int32_t)(w[0] & m26);
+  h.v[1] = (int32_t)(__builtin_amdgcn_alignbit(w[1], w[0], 26) & m25);
+  h.v[2] = (int32_t)(__builtin_amdgcn_alignbit(w[2], w[1], 19) & m26);
+  h.v[3] = (int32_t)(__builtin_amdgcn_alignbit(w[3], w[2], 13) & m25);
+  h.v[4] = (int32_t)((w[3] >> 6) & m26);
+  h.v[5] = (int32_t)(w[4] & m25);
+  h.v[6] = (int32_t)(__builtin_amdgcn_alignbit(w[5], w[4], 25) & m26);
+  h.v[7] = (int32_t)(__builtin_amdgcn_alignbit(w[6], w[5], 19) & m25);
+  h.v[8] = (int32_t)(__builtin_amdgcn_alignbit(w[7], w[6], 12) & m26);
+  h.v[9] = (int32_t)((w[7] >> 6) & m25);
+}
+
+/* Canonical little-endian encoding (value mod p, < p) as 8 words.  Any
+   input within the mul bounds is accepted: it is re-tightened first so the
+   quotient estimate below (valid for |h| < 2^254) is exact. */
+FD_DEV void fe_carry(fe& h, const fe& f);
+FD_DEV void fe_tobytes(uint32_t (&s)[8], const fe& f) {
+  fe g;
+  fe_carry(g, f);
+  int32_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) h[i] = g.v[i];
+  /* q = floor(h / p) in {0,1} once h is folded to [0, 2p) */
+  int32_t q = (19 * h[9] + (1 << 24)) >> 25;
+#pragma unroll
+  for (int i = 0; i < 10; i++) q = (h[i] + q) >> ((i & 1) ? 25 : 26);
+  h[0] += 19 * q;
+  int32_t c;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int sh = (i & 1) ? 25 : 26;
+    c = h[i] >> sh;
+    h[i + 1] += c;
+    h[i] -= c * (1 << sh);
+  }
+  c = h[9] >> 25;
+  h[9] -= c * (1 << 25);
+  /* pack: limbs are now in [0, 2^w) */
+  const uint32_t u0 = (uint32_t)h[0], u1 = (uint32_t)h[1], u2 = (uint32_t)h[2], u3 = (uint32_t)h[3],
+                 u4 = (uint32_t)h[4], u5 = (uint32_t)h[5], u6 = (uint32_t)h[6], u7 = (uint32_t)h[7],
+                 u8 = (uint32_t)h[8], u9 = (uint32_t)h[9];
+  s[0] = u0 | (u1 << 26);
+  s[1] = (u1 >> 6) | (u2 << 19);
+  s[2] = (u2 >> 13) | (u3 << 13);
+  s[3] = (u3 >> 19) | (u4 << 6);
+  s[4] = u5 | (u6 << 25);
+  s[5] = (u6 >> 7) | (u7 << 19);
+  s[6] = (u7 >> 13) | (u8 << 12);
+  s[7] = (u8 >> 20) | (u9 << 6);
+}
+
+FD_DEV bool fe_iszero(const fe& f) {
+  uint32_t s[8];
+  fe_tobytes(s, f);
+  return (s[0] | s[1] | s[2] | s[3] | s[4] | s[5] | s[6] | s[7]) == 0u;
+}
+
+/* parity of the canonical value (fd_f25519_sgn) */
+FD_DEV int fe_isodd(const fe& f) {
+  uint32_t s[8];
+  fe_tobytes(s, f);
+  return (int)(s[0] & 1u);
+}
+
+/* z^(2^252-3) -- same addition chain as fd_f25519_pow22523
+   (src/ballet/ed25519/fd_f25519.c:11-59): 250 squarings, 11 products. */
+FD_DEV void fe_sqn(fe& h, const fe& f, int n) {
+  fe_sq(h, f);
+#pragma clang loop unroll(disable)
+  for (int i = 1; i < n; i++) fe_sq(h, h);
+}
+
+FD_DEV void fe_pow22523(fe& out, const fe& z) {
+  fe t0, t1, t2;
+  fe_sq(t0, z);
+  fe_sqn(t1, t0, 2);
+  fe_mul(t1, z, t1);
+  fe_mul(t0, t0, t1);
+  fe_sq(t0, t0);
+  fe_mul(t0, t1, t0);
+  fe_sqn(t1, t0, 5);
+  fe_mul(t0, t1, t0);
+  fe_sqn(t1, t0, 10);
+  fe_mul(t1, t1, t0);
+  fe_sqn(t2, t1, 20);
+  fe_mul(t1, t2, t1);
+  fe_sqn(t1, t1, 10);
+  fe_mul(t0, t1, t0);
+  fe_sqn(t1, t0, 50);
+  fe_mul(t1, t1, t0);
+  fe_sqn(t2, t1, 100);
+  fe_mul(t1, t2, t1);
+  fe_sqn(t1, t1, 50);
+  fe_mul(t0, t1, t0);
+  fe_sqn(t0, t0, 2);
+  fe_mul(out, t0, z);
+}
+
+/* 1/z = z^(p-2) = (z^(2^252-3))^8 * z^3 */
+FD_DEV void fe_invert(fe& out, const fe& z) {
+  fe t, z2, z3;
+  fe_pow22523(t, z);
+  fe_sqn(t, t, 3);
+  fe_sq(z2, z);
+  fe_mul(z3, z2, z);
+  fe_mul(out, t, z3);
+}

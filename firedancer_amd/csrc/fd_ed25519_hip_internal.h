@@ -1,0 +1,78 @@
+/* fd_ed25519_hip_internal.h -- contract between the plain-C host runtime
+   (host/fd_ed25519_hip_engine.c) and the HIP kernel shim
+   (fd_ed25519_kernels.hip).  Only plain pointers and sizes cross it. */
+#ifndef FD_ED25519_HIP_INTERNAL_H
+#define FD_ED25519_HIP_INTERNAL_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Base-point table: [0..128] B in affine precomputed form (y+x, y-x, 2dxy),
+   36 int32 per entry (30 used), kept in LDS by the verify kernel. */
+#define FD_ED25519_BTAB_ENTRIES   129
+#define FD_ED25519_BTAB_STRIDE    36
+#define FD_ED25519_BTAB_INTS      (FD_ED25519_BTAB_ENTRIES * FD_ED25519_BTAB_STRIDE)
+
+/* Per-lane table of [0..8](-A) in cached form, in HBM: 9 entries x 40 int32
+   per lane, laid out [wave][entry][quad][lane] (int4 granules). */
+#define FD_ED25519_ATAB_BYTES_PER_WAVE (9UL * 10UL * 64UL * 16UL)
+
+#define FD_ED25519_VERIFY_BLOCK 256
+#ifndef FD_ED25519_DSM_WAVES_PER_SIMD
+#define FD_ED25519_DSM_WAVES_PER_SIMD 2
+#endif
+
+/* Work arrays handed between the phase kernels, per signature of a chunk
+   (SoA, [field][cap] so every access is one coalesced dword per lane):
+     k      [8][cap]     u32  k = SHA-512(R||A||M) mod L
+     sflag  [cap]        u8   S < L
+     pflag  [2][cap]     u8   per point (A, R): bit0 decode failure, bit1 small order
+     pts    [2][20][cap] i32  per point: x (10 limbs), y (10 limbs), radix 2^25.5
+   FD_ED25519_WORK_BYTES_PER_SIG bytes per signature of capacity. */
+#define FD_ED25519_WORK_BYTES_PER_SIG (8UL * 4UL + 1UL + 2UL + 2UL * 20UL * 4UL)
+
+typedef struct {
+  /* inputs (signature i = base + j for chunk-local j in [0,n)) */
+  uint8_t const *  msgs;     /* message bytes (any alignment)                 */
+  uint64_t const * msg_off;  /* [N] byte offset of message i in msgs          */
+  uint32_t const * msg_sz;   /* [N] message size                              */
+  uint8_t const *  sigs;     /* [N][64] R||S, 16-byte aligned                  */
+  uint8_t const *  pubs;     /* [N][32] A, 16-byte aligned                     */
+  int8_t *         out;      /* [N] FD_ED25519_SUCCESS / ERR_* codes           */
+  uint64_t         base;
+  uint64_t         n;        /* chunk size, <= cap                             */
+  /* work arrays */
+  uint32_t *       k;
+  uint8_t *        sflag;
+  uint8_t *        pflag;
+  int32_t *        pts;
+  uint64_t         cap;
+  int32_t const *  btab;     /* device base-point table (FD_ED25519_BTAB_INTS) */
+  void *           atab;     /* device scratch, waves * ATAB_BYTES_PER_WAVE    */
+  int              codes_portable; /* 0: AVX-512 backend codes, 1: portable  */
+} fd_ed25519_verify_params_t;
+
+/* All launchers are asynchronous on `stream` (a hipStream_t) and return a
+   hipError_t value (0 on success). */
+int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
+/* Enqueues hash, decode and dsm for one chunk; `grid` caps the persistent
+   dsm grid (its atab scratch must hold grid*VERIFY_BLOCK/64 waves). */
+int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t grid, void * stream );
+int fd_ed25519_hip_verify_occupancy( int * blocks_per_cu );
+
+/* Per-transaction combine with fd_ed25519_verify_batch_single_msg's
+   priority (src/ballet/ed25519/fd_ed25519_user.c:231-309): the first
+   phase-1 error (ERR_SIG/ERR_PUBKEY) in signature order wins, else ERR_MSG
+   if any equation fails, else SUCCESS; cnt==0 or cnt>16 -> ERR_SIG. */
+int fd_ed25519_hip_launch_txn_combine( int8_t const * d_sig_codes, uint32_t const * d_txn_first,
+                                       uint32_t const * d_txn_cnt, int8_t * d_txn_out, uint64_t ntxn,
+                                       void * stream );
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,479 @@
+/* fd_ed25519_kernels.hip -- gfx950 kernels behind libfd_ed25519_hip.
+
+   Verification of a batch: every step of fd_ed25519_verify
+   (src/ballet/ed25519/fd_ed25519_user.c:134-229) for every signature, with
+   the verdict computed as data (no early exits, so a wave never diverges on
+   an invalid signature), in three phase kernels (see "Phase kernels"):
+
+     1. S < L                          (fd_curve25519_scalar_validate)
+     2. decode A and R, reject on no square root (and, in AVX-512 code mode,
+        x == 0 with the sign bit set)  (fd_ed25519_point_frombytes_2x)
+     3. small-order A, then R          (fd_ed25519_affine_is_small_order)
+     4. k = SHA-512(R||A||M) mod L     (fd_sha512_*, fd_curve25519_scalar_reduce)
+     5. R' = [k](-A) + [S]B            (fd_ed25519_double_scalar_mul_base)
+     6. R' == R projectively           (fd_ed25519_point_eq_z1)
+
+   Step 5 uses fixed signed windows instead of the reference's sliding
+   wNAF so that every lane of a wave executes the same additions: k in
+   radix 16 (64 digits in [-8,8], table [0..8](-A) per lane in HBM) and S in
+   radix 256 (32 digits in [-128,128], table [0..128]B shared in LDS).  The
+   group element computed is the same, so the verdict is bit-identical.
+
+   The dsm kernel is persistent: its grid is sized to the resident occupancy
+   and each lane strides over signatures, so the per-lane -A table lives in
+   a fixed HBM scratch of waves x 90 KiB. */
+#include <hip/hip_runtime.h>
+#include "fd25519_ge.h"
+#include "fd25519_sc.h"
+#include "fd_sha512_dev.h"
+#include "fd_ed25519_hip_internal.h"
+
+#define FD_ED25519_SUCCESS 0
+#define FD_ED25519_ERR_SIG -1
+#define FD_ED25519_ERR_PUBKEY -2
+#define FD_ED25519_ERR_MSG -3
+
+/* ------------------------------------------------------------------------
+   Point decoding with the reference's acceptance rules. */
+
+struct decoded_pt {
+  fe x, y;
+  bool fail;   /* no square root, or (AVX-512 rule) x == 0 with sign set */
+  bool small;  /* small order: x == 0, y == 0, y == y0 or y == y1       */
+};
+
+FD_DEV void ge_decode(decoded_pt& d, const uint32_t (&s)[8], bool avx_rule) {
+  const fe one = {{1, 0, 0, 0, 0, 0, 0, 0, 0, 0}};
+  const fe cd = {FE_D}, sqrtm1 = {FE_SQRTM1};
+  fe u, v, v3, x, vxx, t;
+  fe_frombytes(d.y, s);
+  const uint32_t sign = s[7] >> 31;
+  fe_sq(u, d.y);
+  fe_mul(v, u, cd);
+  fe_sub(u, u, one);  /* u = y^2 - 1  */
+  fe_add(v, v, one);  /* v = d y^2 + 1 */
+  fe_sq(v3, v);
+  fe_mul(v3, v3, v);  /* v^3 */
+  fe_sq(x, v3);
+  fe_mul(x, x, v);
+  fe_mul(x, x, u);    /* u v^7 */
+  fe_pow22523(x, x);
+  fe_mul(x, x, v3);
+  fe_mul(x, x, u);    /* x = u v^3 (u v^7)^((p-5)/8) */
+  fe_sq(vxx, x);
+  fe_mul(vxx, vxx, v);
+  fe_sub(t, vxx, u);
+  const bool root = fe_iszero(t);
+  fe_add(t, vxx, u);
+  const bool iroot = fe_iszero(t);
+  fe xi;
+  fe_mul(xi, x, sqrtm1);
+  fe_select(x, x, xi, !root);
+  uint32_t xb[8];
+  fe_tobytes(xb, x);
+  const bool x0 = (xb[0] | xb[1] | xb[2] | xb[3] | xb[4] | xb[5] | xb[6] | xb[7]) == 0u;
+  const uint32_t par = xb[0] & 1u;
+  d.fail = !(root || iroot) || (avx_rule && x0 && sign);
+  fe xn;
+  fe_neg(xn, x);
+  fe_select(d.x, x, xn, par != sign);
+  /* small order on the canonical y */
+  uint32_t yb[8];
+  fe_tobytes(yb, d.y);
+  const uint32_t y0[8] = {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u,
+                          0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du};
+  const uint32_t y1[8] = {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du,
+                          0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u};
+  uint32_t z = 0, e0 = 0, e1 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    z |= yb[i];
+    e0 |= yb[i] ^ y0[i];
+    e1 |= yb[i] ^ y1[i];
+  }
+  d.small = x0 || z == 0u || e0 == 0u || e1 == 0u;
+}
+
+/* ------------------------------------------------------------------------
+   Signed fixed-window recoding, packed so the main loop can pop the most
+   significant digit with a shift (no dynamically indexed register arrays). */
+
+/* k < L < 2^253 -> 64 digits e_i in [-8,7] (e_63 in [0,2]), 4 bits each */
+FD_DEV void recode_radix16(uint32_t (&out)[8], const uint32_t (&k)[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      int e = (int)((k[w] >> (4 * j)) & 15u) + carry;
+      carry = (e + 8) >> 4;
+      e -= carry * 16;
+      packed |= ((uint32_t)e & 15u) << (4 * j);
+    }
+    out[w] = packed;
+  }
+}
+
+/* S < L -> 32 digits f_j in [-128,127] (f_31 in [0,17]), 8 bits each */
+FD_DEV void recode_radix256(uint32_t (&out)[8], const uint32_t (&s)[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      int f = (int)((s[w] >> (8 * j)) & 255u) + carry;
+      carry = (f + 128) >> 8;
+      f -= carry * 256;
+      packed |= ((uint32_t)f & 255u) << (8 * j);
+    }
+    out[w] = packed;
+  }
+}
+
+/* pop the top `bits` of the 256-bit value as a signed digit */
+template <int BITS>
+FD_DEV int pop_digit(uint32_t (&d)[8]) {
+  const int v = ((int32_t)d[7]) >> (32 - BITS);
+#pragma unroll
+  for (int w = 7; w > 0; w--) d[w] = __builtin_amdgcn_alignbit(d[w], d[w - 1], 32 - BITS);
+  d[0] <<= BITS;
+  return v;
+}
+
+/* ------------------------------------------------------------------------
+   Tables */
+
+FD_DEV void atab_store(int4* lane_tab, int e, const ge_cached& c) {
+  int v[40];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    v[i] = c.YplusX.v[i];
+    v[10 + i] = c.YminusX.v[i];
+    v[20 + i] = c.Z.v[i];
+    v[30 + i] = c.T2d.v[i];
+  }
+#pragma unroll
+  for (int q = 0; q < 10; q++)
+    lane_tab[(e * 10 + q) * 64] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+FD_DEV void atab_load(ge_cached& c, const int4* lane_tab, int e) {
+  int v[40];
+#pragma unroll
+  for (int q = 0; q < 10; q++) {
+    const int4 x = lane_tab[(e * 10 + q) * 64];
+    v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    c.YplusX.v[i] = v[i];
+    c.YminusX.v[i] = v[10 + i];
+    c.Z.v[i] = v[20 + i];
+    c.T2d.v[i] = v[30 + i];
+  }
+}
+
+FD_DEV void btab_load(ge_precomp& b, const int4* s_btab, int e) {
+  int v[32];
+  const int4* src = s_btab + e * (FD_ED25519_BTAB_STRIDE / 4);
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const int4 x = src[q];
+    v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    b.yplusx.v[i] = v[i];
+    b.yminusx.v[i] = v[10 + i];
+    b.xy2d.v[i] = v[20 + i];
+  }
+}
+
+/* ------------------------------------------------------------------------
+   Phase kernels.  A batch is verified by three launches on one stream,
+   each with its own register budget, handing ~200 B per signature through
+   the work arrays in HBM (fd_ed25519_verify_params_t):
+
+     hash    one lane per signature: S < L, k = SHA-512(R||A||M) mod L
+     decode  one lane per point (2n lanes: A then R): decompression and
+             the reference's acceptance / small-order rules
+     dsm     one lane per signature, persistent: [k](-A) + [S]B, compare
+             with R, fold every flag into the reference's error code */
+
+#define FD_PF_FAIL  1u
+#define FD_PF_SMALL 2u
+
+__global__ void __launch_bounds__(256)
+fd_ed25519_hash_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p.n) return;
+  const uint64_t i = p.base + j;
+  uint32_t r[8], S[8], a[8];
+  {
+    const uint4* sg = reinterpret_cast<const uint4*>(p.sigs + 64 * i);
+    const uint4* pk = reinterpret_cast<const uint4*>(p.pubs + 32 * i);
+    const uint4 q0 = sg[0], q1 = sg[1], q2 = sg[2], q3 = sg[3], q4 = pk[0], q5 = pk[1];
+    r[0] = q0.x; r[1] = q0.y; r[2] = q0.z; r[3] = q0.w; r[4] = q1.x; r[5] = q1.y; r[6] = q1.z; r[7] = q1.w;
+    S[0] = q2.x; S[1] = q2.y; S[2] = q2.z; S[3] = q2.w; S[4] = q3.x; S[5] = q3.y; S[6] = q3.z; S[7] = q3.w;
+    a[0] = q4.x; a[1] = q4.y; a[2] = q4.z; a[3] = q4.w; a[4] = q5.x; a[5] = q5.y; a[6] = q5.z; a[7] = q5.w;
+  }
+  const uintptr_t mp = reinterpret_cast<uintptr_t>(p.msgs + p.msg_off[i]);
+  sha_msg_src m;
+  m.base = reinterpret_cast<const uint32_t*>(mp & ~(uintptr_t)3);
+  m.shift = (uint32_t)(mp & 3);
+  m.sz = p.msg_sz[i];
+  uint32_t dig[16], k[8];
+  sha512_ram(dig, r, a, m);
+  sc_reduce512(k, dig);
+#pragma unroll
+  for (int w = 0; w < 8; w++) p.k[(uint64_t)w * p.cap + j] = k[w];
+  p.sflag[j] = sc_is_canonical(S) ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(256)
+fd_ed25519_decode_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * p.n) return;
+  const int which = t >= p.n;           /* 0: A (public key), 1: R */
+  const uint64_t j = which ? t - p.n : t;
+  const uint64_t i = p.base + j;
+  uint32_t s[8];
+  {
+    const uint4* src = which ? reinterpret_cast<const uint4*>(p.sigs + 64 * i)
+                             : reinterpret_cast<const uint4*>(p.pubs + 32 * i);
+    const uint4 q0 = src[0], q1 = src[1];
+    s[0] = q0.x; s[1] = q0.y; s[2] = q0.z; s[3] = q0.w; s[4] = q1.x; s[5] = q1.y; s[6] = q1.z; s[7] = q1.w;
+  }
+  decoded_pt d;
+  ge_decode(d, s, !p.codes_portable);
+  int32_t* dst = p.pts + (uint64_t)which * 20 * p.cap + j;
+#pragma unroll
+  for (int l = 0; l < 10; l++) {
+    dst[(uint64_t)l * p.cap] = d.x.v[l];
+    dst[(uint64_t)(10 + l) * p.cap] = d.y.v[l];
+  }
+  p.pflag[(uint64_t)which * p.cap + j] = (uint8_t)((d.fail ? FD_PF_FAIL : 0u) | (d.small ? FD_PF_SMALL : 0u));
+}
+
+FD_DEV void load_pt(fe& x, fe& y, const fd_ed25519_verify_params_t& p, int which, uint64_t j) {
+  const int32_t* src = p.pts + (uint64_t)which * 20 * p.cap + j;
+#pragma unroll
+  for (int l = 0; l < 10; l++) {
+    x.v[l] = src[(uint64_t)l * p.cap];
+    y.v[l] = src[(uint64_t)(10 + l) * p.cap];
+  }
+}
+
+FD_DEV int dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_tab, const int4* s_btab) {
+  const uint64_t i = p.base + j;
+  const uint32_t s_ok = p.sflag[j];
+  const uint32_t af = p.pflag[j], rf = p.pflag[p.cap + j];
+  int code;
+  if (!s_ok) code = FD_ED25519_ERR_SIG;
+  else if (af & FD_PF_FAIL) code = p.codes_portable ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;
+  else if (rf & FD_PF_FAIL) code = FD_ED25519_ERR_SIG;
+  else if (af & FD_PF_SMALL) code = FD_ED25519_ERR_PUBKEY;
+  else if (rf & FD_PF_SMALL) code = FD_ED25519_ERR_SIG;
+  else code = FD_ED25519_SUCCESS;  /* pending the group equation */
+
+  /* table [0..8](-A), cached form, in this lane's HBM slot */
+  {
+    fe ax, ay;
+    load_pt(ax, ay, p, 0, j);
+    ge_p3 nA;
+    fe_neg(nA.X, ax);
+    nA.Y = ay;
+    fe_1(nA.Z);
+    fe t;
+    fe_mul(t, ax, ay);
+    fe_neg(nA.T, t);
+    ge_cached c1, c;
+    c.YplusX = nA.Z; c.YminusX = nA.Z; c.Z = nA.Z; fe_0(c.T2d);  /* identity */
+    atab_store(lane_tab, 0, c);
+    ge_p3_to_cached(c1, nA);
+    atab_store(lane_tab, 1, c1);
+    ge_p3 cur = nA;
+    ge_p1p1 sum;
+#pragma clang loop unroll(disable)
+    for (int e = 2; e <= 8; e++) {
+      ge_add(sum, cur, c1);
+      ge_p1p1_to_p3(cur, sum);
+      ge_p3_to_cached(c, cur);
+      atab_store(lane_tab, e, c);
+    }
+  }
+
+  uint32_t kd[8], sd[8];
+  {
+    uint32_t k[8], S[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) k[w] = p.k[(uint64_t)w * p.cap + j];
+    const uint4* sg = reinterpret_cast<const uint4*>(p.sigs + 64 * i);
+    const uint4 q2 = sg[2], q3 = sg[3];
+    S[0] = q2.x; S[1] = q2.y; S[2] = q2.z; S[3] = q2.w; S[4] = q3.x; S[5] = q3.y; S[6] = q3.z; S[7] = q3.w;
+    /* a rejected S may be >= L; keep the recoding in range (the verdict is
+       already decided for this lane) */
+    if (!s_ok) {
+#pragma unroll
+      for (int w = 0; w < 8; w++) S[w] = 0;
+    }
+    recode_radix16(kd, k);
+    recode_radix256(sd, S);
+  }
+
+  ge_p3 P;
+  ge_p3_0(P);
+  ge_p1p1 Rt;
+  ge_p2 Q;
+#pragma clang loop unroll(disable)
+  for (int it = 63; it >= 0; it--) {
+    if (it != 63) {
+#pragma clang loop unroll(disable)
+      for (int dd = 0; dd < 4; dd++) {
+        ge_p2_dbl(Rt, Q);
+        if (dd < 3) ge_p1p1_to_p2(Q, Rt);
+      }
+      ge_p1p1_to_p3(P, Rt);
+    }
+    {
+      const int e = pop_digit<4>(kd);
+      ge_cached c;
+      atab_load(c, lane_tab, e < 0 ? -e : e);
+      ge_cached_cneg(c, e < 0);
+      ge_add(Rt, P, c);
+    }
+    if ((it & 1) == 0) {
+      ge_p1p1_to_p3(P, Rt);
+      const int f = pop_digit<8>(sd);
+      ge_precomp b;
+      btab_load(b, s_btab, f < 0 ? -f : f);
+      ge_precomp_cneg(b, f < 0);
+      ge_madd(Rt, P, b);
+    }
+    ge_p1p1_to_p2(Q, Rt);
+  }
+
+  /* R' == R with R.Z = 1: X' == x_R Z' and Y' == y_R Z' */
+  fe rx, ry, t1, t2;
+  load_pt(rx, ry, p, 1, j);
+  fe_mul(t1, rx, Q.Z);
+  fe_sub(t1, t1, Q.X);
+  fe_mul(t2, ry, Q.Z);
+  fe_sub(t2, t2, Q.Y);
+  const bool eq = fe_iszero(t1) && fe_iszero(t2);
+  if (code == FD_ED25519_SUCCESS && !eq) code = FD_ED25519_ERR_MSG;
+  return code;
+}
+
+__global__ void __launch_bounds__(FD_ED25519_VERIFY_BLOCK, FD_ED25519_DSM_WAVES_PER_SIMD)
+fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
+  __shared__ int4 s_btab[FD_ED25519_BTAB_INTS / 4];
+  const int4* g_btab = reinterpret_cast<const int4*>(p.btab);
+  for (int t = threadIdx.x; t < FD_ED25519_BTAB_INTS / 4; t += blockDim.x) s_btab[t] = g_btab[t];
+  __syncthreads();
+
+  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  int4* lane_tab = reinterpret_cast<int4*>(static_cast<char*>(p.atab) +
+                                           (gtid >> 6) * FD_ED25519_ATAB_BYTES_PER_WAVE) + (threadIdx.x & 63);
+  for (uint64_t j = gtid; j < p.n; j += stride) p.out[p.base + j] = (int8_t)dsm_one(p, j, lane_tab, s_btab);
+}
+
+/* ------------------------------------------------------------------------
+   Base table [0..128]B as (y+x, y-x, 2dxy), one entry per thread. */
+
+__global__ void fd_ed25519_gen_btab_kernel(int32_t* btab) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= FD_ED25519_BTAB_ENTRIES) return;
+  ge_p3 B, P;
+  const fe bx = {FE_BX}, by = {FE_BY}, d2 = {FE_D2};
+  B.X = bx; B.Y = by; fe_1(B.Z); fe_mul(B.T, bx, by);
+  ge_cached cb;
+  ge_p3_to_cached(cb, B);
+  ge_p3_0(P);
+  ge_p1p1 t;
+  for (int bit = 7; bit >= 0; bit--) {
+    ge_p3_dbl(t, P);
+    ge_p1p1_to_p3(P, t);
+    if ((e >> bit) & 1) {
+      ge_add(t, P, cb);
+      ge_p1p1_to_p3(P, t);
+    }
+  }
+  fe zi, x, y, ypx, ymx, xy2d;
+  fe_invert(zi, P.Z);
+  fe_mul(x, P.X, zi);
+  fe_mul(y, P.Y, zi);
+  fe_add(ypx, y, x); fe_carry(ypx, ypx);
+  fe_sub(ymx, y, x); fe_carry(ymx, ymx);
+  fe_mul(xy2d, x, y);
+  fe_mul(xy2d, xy2d, d2);
+  int32_t* o = btab + e * FD_ED25519_BTAB_STRIDE;
+  for (int i = 0; i < 10; i++) {
+    o[i] = ypx.v[i];
+    o[10 + i] = ymx.v[i];
+    o[20 + i] = xy2d.v[i];
+  }
+  for (int i = 30; i < FD_ED25519_BTAB_STRIDE; i++) o[i] = 0;
+}
+
+/* ------------------------------------------------------------------------
+   Per-transaction combine (fd_ed25519_verify_batch_single_msg priority). */
+
+__global__ void fd_ed25519_txn_combine_kernel(const int8_t* sig_codes, const uint32_t* txn_first,
+                                              const uint32_t* txn_cnt, int8_t* out, uint64_t ntxn) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntxn) return;
+  const uint32_t f = txn_first[t], n = txn_cnt[t];
+  int code = FD_ED25519_SUCCESS;
+  if (n == 0u || n > 16u) {
+    code = FD_ED25519_ERR_SIG;
+  } else {
+    bool msg_fail = false;
+    for (uint32_t j = 0; j < n; j++) {
+      const int c = sig_codes[f + j];
+      if (c == FD_ED25519_ERR_MSG) msg_fail = true;
+      else if (c != FD_ED25519_SUCCESS) { code = c; break; }
+    }
+    if (code == FD_ED25519_SUCCESS && msg_fail) code = FD_ED25519_ERR_MSG;
+  }
+  out[t] = (int8_t)code;
+}
+
+/* ------------------------------------------------------------------------
+   C-ABI launchers */
+
+extern "C" int fd_ed25519_hip_launch_gen_btab(int32_t* d_btab, void* stream) {
+  hipLaunchKernelGGL(fd_ed25519_gen_btab_kernel, dim3(3), dim3(64), 0, (hipStream_t)stream, d_btab);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fd_ed25519_hip_launch_verify(const fd_ed25519_verify_params_t* p, uint32_t grid, void* stream) {
+  if (!p->n) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t blk = 256;
+  hipLaunchKernelGGL(fd_ed25519_hash_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
+  hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((2 * p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
+  const uint64_t need = (p->n + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
+  const uint32_t g = (uint32_t)(need < grid ? need : grid);
+  hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fd_ed25519_hip_verify_occupancy(int* blocks_per_cu) {
+  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fd_ed25519_dsm_kernel,
+                                                           FD_ED25519_VERIFY_BLOCK, 0);
+}
+
+extern "C" int fd_ed25519_hip_launch_txn_combine(const int8_t* d_sig_codes, const uint32_t* d_txn_first,
+                                                 const uint32_t* d_txn_cnt, int8_t* d_txn_out, uint64_t ntxn,
+                                                 void* stream) {
+  if (!ntxn) return 0;
+  const uint32_t blk = 256;
+  const uint32_t grid = (uint32_t)((ntxn + blk - 1) / blk);
+  hipLaunchKernelGGL(fd_ed25519_txn_combine_kernel, dim3(grid), dim3(blk), 0, (hipStream_t)stream,
+                     d_sig_codes, d_txn_first, d_txn_cnt, d_txn_out, ntxn);
+  return (int)hipGetLastError();
+}

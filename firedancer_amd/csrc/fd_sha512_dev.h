@@ -1,0 +1,139 @@
+/* fd_sha512_dev.h -- SHA-512 of R || A || M for gfx950, one message per lane.
+
+   Computes the challenge hash of the verify equation,
+   k = SHA-512(R || A || M), as fd_ed25519_verify does with
+   fd_sha512_init/append/fini (src/ballet/ed25519/fd_ed25519_user.c:203-205;
+   core src/ballet/sha512/fd_sha512.c:128-231).  FIPS 180-4: 80 rounds of
+   64-bit big-endian arithmetic per 128-byte block; ceil((81+sz)/128)
+   blocks for a message of sz bytes.
+
+   Message bytes are read straight from the SoA message buffer in HBM with
+   32-bit loads from the enclosing aligned dword (any byte offset is
+   accepted) and realigned in registers (v_alignbyte_b32).  A lane never
+   loads a dword that holds none of its own message bytes, so the buffer
+   needs no padding.  Padding (0x80, zeros, 128-bit length) is synthesized
+   in registers. */
+#pragma once
+#include "fd25519_fe.h"
+
+__constant__ uint64_t fd_sha512_dev_k[80] = {
+  0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+  0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+  0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+  0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+  0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+  0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+  0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+  0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+  0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+  0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+  0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+  0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+  0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+  0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+  0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+  0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+  0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+  0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+  0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+  0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL,
+};
+
+FD_DEV uint64_t sha_ror(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+FD_DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+/* One compression: h <- h + F(h, w).  The schedule is kept as a rolling
+   16-word window; rounds are unrolled 16 at a time with the round constants
+   read through the scalar cache. */
+FD_DEV void sha512_block(uint64_t (&h)[8], uint64_t (&w)[16]) {
+  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int r0 = 0; r0 < 80; r0 += 16) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      if (r0 > 0) {
+        const uint64_t w15 = w[(r + 1) & 15], w2 = w[(r + 14) & 15];
+        const uint64_t s0 = sha_ror(w15, 1) ^ sha_ror(w15, 8) ^ (w15 >> 7);
+        const uint64_t s1 = sha_ror(w2, 19) ^ sha_ror(w2, 61) ^ (w2 >> 6);
+        w[r] += s0 + w[(r + 9) & 15] + s1;
+      }
+      const uint64_t S1 = sha_ror(e, 14) ^ sha_ror(e, 18) ^ sha_ror(e, 41);
+      const uint64_t ch = (e & f) ^ (~e & g);
+      const uint64_t t1 = hh + S1 + ch + fd_sha512_dev_k[r0 + r] + w[r];
+      const uint64_t S0 = sha_ror(a, 28) ^ sha_ror(a, 34) ^ sha_ror(a, 39);
+      const uint64_t mj = (a & b) ^ (c & (a ^ b));
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    }
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+/* Message dword at message byte position p (p % 4 == 0, may be >= sz),
+   padded: bytes >= sz are zero except byte sz = 0x80.  Returned in memory
+   (little-endian) byte order. */
+struct sha_msg_src {
+  const uint32_t* base;  /* aligned dword containing message byte 0 */
+  uint32_t shift;        /* message byte 0 is byte `shift` of base[0] */
+  uint32_t sz;
+};
+
+FD_DEV uint32_t sha_raw_dword(const sha_msg_src& m, int j) {
+  /* load only dwords holding at least one message byte */
+  return (4u * (uint32_t)j < m.shift + m.sz) ? __builtin_nontemporal_load(m.base + j) : 0u;
+}
+
+FD_DEV uint32_t sha_msg_dword(const sha_msg_src& m, int p, uint32_t lo, uint32_t hi) {
+  uint32_t d = __builtin_amdgcn_alignbyte(hi, lo, m.shift);
+  const int n = (int)m.sz - p;
+  const uint32_t keep = n >= 4 ? 0xffffffffu : (n > 0 ? (1u << (8 * n)) - 1u : 0u);
+  const uint32_t pad = (n >= 0 && n < 4) ? (0x80u << (8 * n)) : 0u;
+  return (d & keep) | pad;
+}
+
+/* digest (as 16 little-endian words of the 64-byte output) of
+   R(32) || A(32) || M(sz) */
+FD_DEV void sha512_ram(uint32_t (&out)[16], const uint32_t (&r)[8], const uint32_t (&a)[8],
+                       const sha_msg_src& m) {
+  uint64_t h[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                   0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                   0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  const uint32_t nblk = (m.sz + 208u) >> 7;  /* ceil((64+sz+17)/128) */
+  const uint64_t bitlen = (uint64_t)(64u + m.sz) << 3;
+  for (uint32_t b = 0; b < nblk; b++) {
+    uint64_t w[16];
+    /* message byte position of word t is 128 b + 8 t - 64 */
+    const int p0 = 128 * (int)b - 64;
+    int j0 = (p0 >> 2);  /* dword index of the first message dword in this block */
+    uint32_t prev = sha_raw_dword(m, j0 < 0 ? 0 : j0);
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+      const int p = p0 + 8 * t;
+      uint32_t d0, d1;
+      if (b == 0 && t < 8) {
+        /* R || A from registers */
+        const uint32_t x0 = t < 4 ? r[2 * t] : a[2 * t - 8];
+        const uint32_t x1 = t < 4 ? r[2 * t + 1] : a[2 * t - 7];
+        d0 = x0; d1 = x1;
+      } else {
+        const int j = p >> 2;
+        const uint32_t l1 = sha_raw_dword(m, j + 1);
+        const uint32_t l2 = sha_raw_dword(m, j + 2);
+        d0 = sha_msg_dword(m, p, prev, l1);
+        d1 = sha_msg_dword(m, p + 4, l1, l2);
+        prev = l2;
+      }
+      uint64_t word = ((uint64_t)bswap32(d0) << 32) | (uint64_t)bswap32(d1);
+      if (b + 1 == nblk) {
+        if (t == 14) word = 0;
+        if (t == 15) word = bitlen;
+      }
+      w[t] = word;
+    }
+    sha512_block(h, w);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    out[2 * i] = bswap32((uint32_t)(h[i] >> 32));
+    out[2 * i + 1] = bswap32((uint32_t)h[i]);
+  }
+}

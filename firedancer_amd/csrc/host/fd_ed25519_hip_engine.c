@@ -1,0 +1,454 @@
+/* fd_ed25519_hip_engine.c -- plain-C host runtime of libfd_ed25519_hip.
+
+   Owns the device, stream and memory of an engine, batches host requests
+   into pinned SoA staging buffers, and drives the HIP kernel shim
+   (fd_ed25519_kernels.hip) through the C-ABI in fd_ed25519_hip_internal.h.
+   Also provides the drop-in fd_ed25519_verify /
+   fd_ed25519_verify_batch_single_msg / fd_ed25519_strerror symbols on a
+   lazily created process-wide engine.
+
+   HBM layout of an engine (sized once at creation, no per-call device
+   allocation on the device-resident path):
+     btab   129 x 36 int32            base-point table [0..128]B (LDS image)
+     atab   dsm waves x 92160 B       per-lane [0..8](-A) tables
+     work   max_chunk x 195 B         k, flags and decoded points per signature
+     in/out staging for the host API  grown on demand */
+
+#define _GNU_SOURCE
+#include "../../../include/fd_ed25519_hip.h"
+#include "../fd_ed25519_hip_internal.h"
+
+#include <hip/hip_runtime_api.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+struct fd_ed25519_hip_engine {
+  int          device;
+  int          flags;
+  hipStream_t  stream;
+  int          cu_cnt;
+  int          dsm_blocks_per_cu;
+  uint32_t     dsm_grid;
+  uint64_t     max_chunk;
+  uint64_t     device_bytes;
+  char         arch[ 64 ];
+
+  int32_t *    d_btab;
+  void *       d_atab;
+  uint8_t *    d_work;       /* one allocation carved into the work arrays */
+  uint32_t *   d_k;
+  uint8_t *    d_sflag;
+  uint8_t *    d_pflag;
+  int32_t *    d_pts;
+
+  /* host-API staging (pinned host + device mirrors), grown on demand */
+  uint64_t     st_sig_cap;   /* signatures */
+  uint64_t     st_msg_cap;   /* message bytes */
+  uint64_t     st_txn_cap;   /* transactions */
+  uint8_t *    h_msgs;  uint8_t *  d_msgs;
+  uint64_t *   h_off;   uint64_t * d_off;
+  uint32_t *   h_sz;    uint32_t * d_sz;
+  uint8_t *    h_sigs;  uint8_t *  d_sigs;
+  uint8_t *    h_pubs;  uint8_t *  d_pubs;
+  int8_t *     h_out;   int8_t *   d_out;
+  uint32_t *   h_tfirst; uint32_t * d_tfirst;
+  uint32_t *   h_tcnt;  uint32_t * d_tcnt;
+  int8_t *     h_tout;  int8_t *   d_tout;
+};
+
+static __thread char fd_ed25519_hip_errbuf[ 256 ];
+
+char const *
+fd_ed25519_hip_last_error( void ) {
+  return fd_ed25519_hip_errbuf;
+}
+
+static int
+hip_fail( hipError_t err, char const * what ) {
+  snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "%s: %s (%d)", what,
+            hipGetErrorString( err ), (int)err );
+  return FD_ED25519_HIP_ERR_HIP - (int)err;
+}
+
+#define HIPCHK( call, what ) do {                     \
+    hipError_t _e = (call);                           \
+    if( _e!=hipSuccess ) return hip_fail( _e, what ); \
+  } while(0)
+
+char const *
+fd_ed25519_hip_strerror( int status ) {
+  if( status==FD_ED25519_HIP_OK        ) return "ok";
+  if( status==FD_ED25519_HIP_ERR_INVAL ) return "invalid argument";
+  if( status==FD_ED25519_HIP_ERR_NOMEM ) return "out of memory";
+  if( status<=FD_ED25519_HIP_ERR_HIP   ) return hipGetErrorString( (hipError_t)(FD_ED25519_HIP_ERR_HIP - status) );
+  return "unknown";
+}
+
+static void
+engine_free( fd_ed25519_hip_engine_t * e ) {
+  if( !e ) return;
+  hipSetDevice( e->device );
+  if( e->stream ) hipStreamSynchronize( e->stream );
+  hipFree( e->d_btab ); hipFree( e->d_atab ); hipFree( e->d_work );
+  hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
+  hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
+  hipHostFree( e->h_msgs ); hipHostFree( e->h_off ); hipHostFree( e->h_sz ); hipHostFree( e->h_sigs );
+  hipHostFree( e->h_pubs ); hipHostFree( e->h_out ); hipHostFree( e->h_tfirst ); hipHostFree( e->h_tcnt );
+  hipHostFree( e->h_tout );
+  if( e->stream ) hipStreamDestroy( e->stream );
+  free( e );
+}
+
+void
+fd_ed25519_hip_engine_delete( fd_ed25519_hip_engine_t * engine ) {
+  engine_free( engine );
+}
+
+static int
+engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int flags ) {
+  e->device    = device;
+  e->flags     = flags;
+  e->max_chunk = max_chunk ? max_chunk : (1UL<<20);
+  HIPCHK( hipSetDevice( device ), "hipSetDevice" );
+  hipDeviceProp_t prop;
+  HIPCHK( hipGetDeviceProperties( &prop, device ), "hipGetDeviceProperties" );
+  e->cu_cnt = prop.multiProcessorCount;
+  strncpy( e->arch, prop.gcnArchName, sizeof(e->arch)-1 );
+  if( strncmp( prop.gcnArchName, "gfx950", 6 ) ) {
+    snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf),
+              "device %d is %s; libfd_ed25519_hip is built for gfx950 only", device, prop.gcnArchName );
+    return FD_ED25519_HIP_ERR_INVAL;
+  }
+  HIPCHK( hipStreamCreateWithFlags( &e->stream, hipStreamNonBlocking ), "hipStreamCreate" );
+
+  int bpc = 0;
+  HIPCHK( (hipError_t)fd_ed25519_hip_verify_occupancy( &bpc ), "occupancy query" );
+  if( bpc<1 ) bpc = 1;
+  e->dsm_blocks_per_cu = bpc;
+  e->dsm_grid = (uint32_t)(bpc * e->cu_cnt);
+
+  size_t btab_sz = sizeof(int32_t) * FD_ED25519_BTAB_INTS;
+  size_t atab_sz = (size_t)e->dsm_grid * (FD_ED25519_VERIFY_BLOCK / 64) * FD_ED25519_ATAB_BYTES_PER_WAVE;
+  size_t work_sz = (size_t)e->max_chunk * FD_ED25519_WORK_BYTES_PER_SIG + 1024;
+  HIPCHK( hipMalloc( (void **)&e->d_btab, btab_sz ), "hipMalloc(btab)" );
+  HIPCHK( hipMalloc( &e->d_atab, atab_sz ), "hipMalloc(atab)" );
+  HIPCHK( hipMalloc( (void **)&e->d_work, work_sz ), "hipMalloc(work)" );
+  e->device_bytes = btab_sz + atab_sz + work_sz;
+  uint64_t c = e->max_chunk;
+  uint8_t * w = e->d_work;
+  e->d_k     = (uint32_t *)w; w += 8UL*4UL*c;
+  e->d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
+  e->d_sflag = w;             w += c;
+  e->d_pflag = w;             w += 2UL*c;
+
+  int err = fd_ed25519_hip_launch_gen_btab( e->d_btab, e->stream );
+  if( err ) return hip_fail( (hipError_t)err, "gen_btab launch" );
+  HIPCHK( hipStreamSynchronize( e->stream ), "gen_btab" );
+  return FD_ED25519_HIP_OK;
+}
+
+fd_ed25519_hip_engine_t *
+fd_ed25519_hip_engine_new( int device, unsigned long max_chunk, int flags ) {
+  fd_ed25519_hip_engine_t * e = (fd_ed25519_hip_engine_t *)calloc( 1, sizeof(fd_ed25519_hip_engine_t) );
+  if( !e ) { snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "calloc failed" ); return NULL; }
+  if( engine_init( e, device, max_chunk, flags ) ) { engine_free( e ); return NULL; }
+  return e;
+}
+
+int
+fd_ed25519_hip_engine_info( fd_ed25519_hip_engine_t const * e, fd_ed25519_hip_info_t * info ) {
+  if( !e || !info ) return FD_ED25519_HIP_ERR_INVAL;
+  memset( info, 0, sizeof(*info) );
+  info->device            = e->device;
+  info->cu_cnt            = e->cu_cnt;
+  info->dsm_blocks_per_cu = e->dsm_blocks_per_cu;
+  info->dsm_grid          = e->dsm_grid;
+  info->max_chunk         = e->max_chunk;
+  info->device_bytes      = e->device_bytes;
+  info->flags             = e->flags;
+  memcpy( info->arch, e->arch, sizeof(info->arch) );
+  return FD_ED25519_HIP_OK;
+}
+
+void *
+fd_ed25519_hip_engine_stream( fd_ed25519_hip_engine_t * e ) {
+  return e ? (void *)e->stream : NULL;
+}
+
+int
+fd_ed25519_hip_engine_sync( fd_ed25519_hip_engine_t * e ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipStreamSynchronize( e->stream ), "hipStreamSynchronize" );
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
+                           unsigned long n,
+                           unsigned char const * msgs, unsigned long const * msg_off, unsigned int const * msg_sz,
+                           unsigned char const * sigs, unsigned char const * pubs, signed char * out,
+                           void * stream ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  if( !n ) return FD_ED25519_HIP_OK;
+  if( !msg_off || !msg_sz || !sigs || !pubs || !out ) return FD_ED25519_HIP_ERR_INVAL;
+  if( ((uintptr_t)sigs & 15UL) || ((uintptr_t)pubs & 15UL) ) {
+    snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "sigs/pubs must be 16-byte aligned" );
+    return FD_ED25519_HIP_ERR_INVAL;
+  }
+  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  fd_ed25519_verify_params_t p;
+  memset( &p, 0, sizeof(p) );
+  p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz;
+  p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
+  p.k = e->d_k; p.sflag = e->d_sflag; p.pflag = e->d_pflag; p.pts = e->d_pts; p.cap = e->max_chunk;
+  p.btab = e->d_btab; p.atab = e->d_atab;
+  p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
+  for( uint64_t base=0UL; base<n; base+=e->max_chunk ) {
+    p.base = base;
+    p.n    = (n-base) < e->max_chunk ? (n-base) : e->max_chunk;
+    int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, st );
+    if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+  }
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_txn_combine_dev( fd_ed25519_hip_engine_t * e, unsigned long ntxn,
+                                signed char const * sig_codes, unsigned int const * txn_first,
+                                unsigned int const * txn_cnt, signed char * txn_out, void * stream ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  if( !ntxn ) return FD_ED25519_HIP_OK;
+  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  int err = fd_ed25519_hip_launch_txn_combine( (int8_t const *)sig_codes, txn_first, txn_cnt,
+                                               (int8_t *)txn_out, ntxn, st );
+  if( err ) return hip_fail( (hipError_t)err, "txn_combine launch" );
+  return FD_ED25519_HIP_OK;
+}
+
+/* ---- host staging ------------------------------------------------------ */
+
+static int
+grow_pair( void ** h, void ** d, uint64_t * cap, uint64_t need, uint64_t elem ) {
+  if( need<=*cap ) return FD_ED25519_HIP_OK;
+  uint64_t ncap = *cap ? *cap : 1024UL;
+  while( ncap<need ) ncap *= 2UL;
+  hipHostFree( *h ); hipFree( *d ); *h = NULL; *d = NULL; *cap = 0UL;
+  HIPCHK( hipHostMalloc( h, ncap*elem + 64UL, hipHostMallocDefault ), "hipHostMalloc" );
+  HIPCHK( hipMalloc( d, ncap*elem + 64UL ), "hipMalloc" );
+  *cap = ncap;
+  return FD_ED25519_HIP_OK;
+}
+
+static int
+stage_sigs( fd_ed25519_hip_engine_t * e, uint64_t n ) {
+  if( n<=e->st_sig_cap ) return FD_ED25519_HIP_OK;
+  uint64_t c0 = e->st_sig_cap, c = 0;
+  int err;
+  c = c0; if( (err = grow_pair( (void **)&e->h_off,  (void **)&e->d_off,  &c, n, 8UL  )) ) return err;
+  c = c0; if( (err = grow_pair( (void **)&e->h_sz,   (void **)&e->d_sz,   &c, n, 4UL  )) ) return err;
+  c = c0; if( (err = grow_pair( (void **)&e->h_sigs, (void **)&e->d_sigs, &c, n, 64UL )) ) return err;
+  c = c0; if( (err = grow_pair( (void **)&e->h_pubs, (void **)&e->d_pubs, &c, n, 32UL )) ) return err;
+  c = c0; if( (err = grow_pair( (void **)&e->h_out,  (void **)&e->d_out,  &c, n, 1UL  )) ) return err;
+  e->st_sig_cap = c;
+  return FD_ED25519_HIP_OK;
+}
+
+static int
+stage_msgs( fd_ed25519_hip_engine_t * e, uint64_t bytes ) {
+  return grow_pair( (void **)&e->h_msgs, (void **)&e->d_msgs, &e->st_msg_cap, bytes ? bytes : 1UL, 1UL );
+}
+
+static int
+stage_txns( fd_ed25519_hip_engine_t * e, uint64_t ntxn ) {
+  if( ntxn<=e->st_txn_cap ) return FD_ED25519_HIP_OK;
+  uint64_t c0 = e->st_txn_cap, c = 0;
+  int err;
+  c = c0; if( (err = grow_pair( (void **)&e->h_tfirst, (void **)&e->d_tfirst, &c, ntxn, 4UL )) ) return err;
+  c = c0; if( (err = grow_pair( (void **)&e->h_tcnt,   (void **)&e->d_tcnt,   &c, ntxn, 4UL )) ) return err;
+  c = c0; if( (err = grow_pair( (void **)&e->h_tout,   (void **)&e->d_tout,   &c, ntxn, 1UL )) ) return err;
+  e->st_txn_cap = c;
+  return FD_ED25519_HIP_OK;
+}
+
+static int
+upload_and_verify( fd_ed25519_hip_engine_t * e, uint64_t n, uint64_t msg_bytes ) {
+  hipStream_t st = e->stream;
+  HIPCHK( hipMemcpyAsync( e->d_msgs, e->h_msgs, msg_bytes ? msg_bytes : 1UL, hipMemcpyHostToDevice, st ), "H2D msgs" );
+  HIPCHK( hipMemcpyAsync( e->d_off,  e->h_off,  8UL*n,  hipMemcpyHostToDevice, st ), "H2D off" );
+  HIPCHK( hipMemcpyAsync( e->d_sz,   e->h_sz,   4UL*n,  hipMemcpyHostToDevice, st ), "H2D sz" );
+  HIPCHK( hipMemcpyAsync( e->d_sigs, e->h_sigs, 64UL*n, hipMemcpyHostToDevice, st ), "H2D sigs" );
+  HIPCHK( hipMemcpyAsync( e->d_pubs, e->h_pubs, 32UL*n, hipMemcpyHostToDevice, st ), "H2D pubs" );
+  return fd_ed25519_hip_verify_dev( e, n, e->d_msgs, (unsigned long const *)e->d_off, e->d_sz, e->d_sigs,
+                                    e->d_pubs, (signed char *)e->d_out, st );
+}
+
+int
+fd_ed25519_hip_verify_host( fd_ed25519_hip_engine_t * e, unsigned long n,
+                            unsigned char const * msgs, unsigned long const * msg_off, unsigned int const * msg_sz,
+                            unsigned char const * sigs, unsigned char const * pubs, signed char * out ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  if( !n ) return FD_ED25519_HIP_OK;
+  if( !msg_off || !msg_sz || !sigs || !pubs || !out ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  int err;
+  if( (err = stage_sigs( e, n )) ) return err;
+  uint64_t bytes = 0UL;
+  for( uint64_t i=0UL; i<n; i++ ) bytes += msg_sz[i];
+  if( (err = stage_msgs( e, bytes )) ) return err;
+  /* pack messages contiguously (pinned), rewrite offsets */
+  uint64_t pos = 0UL;
+  for( uint64_t i=0UL; i<n; i++ ) {
+    if( msg_sz[i] ) memcpy( e->h_msgs + pos, msgs + msg_off[i], msg_sz[i] );
+    e->h_off[i] = pos;
+    e->h_sz [i] = msg_sz[i];
+    pos += msg_sz[i];
+  }
+  memcpy( e->h_sigs, sigs, 64UL*n );
+  memcpy( e->h_pubs, pubs, 32UL*n );
+  if( (err = upload_and_verify( e, n, bytes )) ) return err;
+  HIPCHK( hipMemcpyAsync( e->h_out, e->d_out, n, hipMemcpyDeviceToHost, e->stream ), "D2H out" );
+  HIPCHK( hipStreamSynchronize( e->stream ), "verify" );
+  memcpy( out, e->h_out, n );
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_verify_txns_host( fd_ed25519_hip_engine_t * e, unsigned long ntxn,
+                                 unsigned char const * msgs, unsigned long const * txn_msg_off,
+                                 unsigned int const * txn_msg_sz, unsigned int const * txn_first,
+                                 unsigned int const * txn_cnt, unsigned char const * sigs,
+                                 unsigned char const * pubs, signed char * out_txn, signed char * out_sig ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  if( !ntxn ) return FD_ED25519_HIP_OK;
+  if( !txn_msg_off || !txn_msg_sz || !txn_first || !txn_cnt || !out_txn ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  /* signatures actually verified: those of transactions with 1..16 signers
+     (others are ERR_SIG without reading their inputs, as the reference) */
+  uint64_t n = 0UL, bytes = 0UL;
+  for( uint64_t t=0UL; t<ntxn; t++ ) {
+    if( txn_cnt[t]>=1U && txn_cnt[t]<=16U ) n += txn_cnt[t];
+    bytes += txn_msg_sz[t];
+  }
+  int err;
+  if( (err = stage_sigs( e, n ? n : 1UL )) ) return err;
+  if( (err = stage_msgs( e, bytes )) ) return err;
+  if( (err = stage_txns( e, ntxn )) ) return err;
+  uint64_t pos = 0UL, k = 0UL;
+  for( uint64_t t=0UL; t<ntxn; t++ ) {
+    uint64_t moff = pos;
+    if( txn_msg_sz[t] ) memcpy( e->h_msgs + pos, msgs + txn_msg_off[t], txn_msg_sz[t] );
+    pos += txn_msg_sz[t];
+    uint32_t cnt = txn_cnt[t];
+    e->h_tfirst[t] = (uint32_t)k;
+    e->h_tcnt  [t] = cnt;
+    if( cnt<1U || cnt>16U ) continue;
+    for( uint32_t j=0U; j<cnt; j++, k++ ) {
+      uint64_t s = (uint64_t)txn_first[t] + j;
+      e->h_off[k] = moff;
+      e->h_sz [k] = txn_msg_sz[t];
+      memcpy( e->h_sigs + 64UL*k, sigs + 64UL*s, 64UL );
+      memcpy( e->h_pubs + 32UL*k, pubs + 32UL*s, 32UL );
+    }
+  }
+  if( n && (err = upload_and_verify( e, n, bytes )) ) return err;
+  HIPCHK( hipMemcpyAsync( e->d_tfirst, e->h_tfirst, 4UL*ntxn, hipMemcpyHostToDevice, e->stream ), "H2D tfirst" );
+  HIPCHK( hipMemcpyAsync( e->d_tcnt,   e->h_tcnt,   4UL*ntxn, hipMemcpyHostToDevice, e->stream ), "H2D tcnt" );
+  if( (err = fd_ed25519_hip_txn_combine_dev( e, ntxn, (signed char const *)e->d_out, e->d_tfirst, e->d_tcnt,
+                                             (signed char *)e->d_tout, e->stream )) ) return err;
+  HIPCHK( hipMemcpyAsync( e->h_tout, e->d_tout, ntxn, hipMemcpyDeviceToHost, e->stream ), "D2H tout" );
+  if( out_sig && n ) HIPCHK( hipMemcpyAsync( e->h_out, e->d_out, n, hipMemcpyDeviceToHost, e->stream ), "D2H out" );
+  HIPCHK( hipStreamSynchronize( e->stream ), "verify_txns" );
+  memcpy( out_txn, e->h_tout, ntxn );
+  if( out_sig ) {
+    /* scatter per-signature codes back to the caller's indexing */
+    for( uint64_t t=0UL; t<ntxn; t++ ) {
+      uint32_t cnt = txn_cnt[t];
+      for( uint32_t j=0U; j<cnt; j++ )
+        out_sig[ txn_first[t] + j ] = (cnt>=1U && cnt<=16U) ? e->h_out[ e->h_tfirst[t] + j ] : (signed char)FD_ED25519_ERR_SIG;
+    }
+  }
+  return FD_ED25519_HIP_OK;
+}
+
+/* ---- drop-in API ------------------------------------------------------- */
+
+static pthread_once_t           default_once = PTHREAD_ONCE_INIT;
+static pthread_mutex_t          default_lock = PTHREAD_MUTEX_INITIALIZER;
+static fd_ed25519_hip_engine_t * default_engine;
+
+static void
+default_init( void ) {
+  char const * dev_s   = getenv( "FD_ED25519_HIP_DEVICE" );
+  char const * codes_s = getenv( "FD_ED25519_HIP_CODES" );
+  int dev   = dev_s ? atoi( dev_s ) : 0;
+  int flags = (codes_s && !strcmp( codes_s, "portable" )) ? FD_ED25519_HIP_FLAG_CODES_PORTABLE : 0;
+  default_engine = fd_ed25519_hip_engine_new( dev, 1UL<<16, flags );
+}
+
+static fd_ed25519_hip_engine_t *
+default_get( void ) {
+  pthread_once( &default_once, default_init );
+  if( !default_engine ) {
+    fprintf( stderr, "libfd_ed25519_hip: FATAL: cannot create the GPU engine: %s\n", fd_ed25519_hip_last_error() );
+    abort();
+  }
+  return default_engine;
+}
+
+static void
+dropin_fatal( int err ) {
+  fprintf( stderr, "libfd_ed25519_hip: FATAL: GPU verify failed: %s (%s)\n", fd_ed25519_hip_strerror( err ),
+           fd_ed25519_hip_last_error() );
+  abort();
+}
+
+int
+fd_ed25519_verify( unsigned char const msg[], unsigned long msg_sz, unsigned char const sig[ 64 ],
+                   unsigned char const public_key[ 32 ], fd_sha512_t * sha ) {
+  (void)sha;
+  fd_ed25519_hip_engine_t * e = default_get();
+  unsigned long off = 0UL;
+  unsigned int  sz  = (unsigned int)msg_sz;
+  signed char   out = 0;
+  static unsigned char const empty[1] = {0};
+  pthread_mutex_lock( &default_lock );
+  int err = fd_ed25519_hip_verify_host( e, 1UL, msg ? msg : empty, &off, &sz, sig, public_key, &out );
+  pthread_mutex_unlock( &default_lock );
+  if( err ) dropin_fatal( err );
+  return (int)out;
+}
+
+int
+fd_ed25519_verify_batch_single_msg( unsigned char const msg[], unsigned long const msg_sz,
+                                    unsigned char const signatures[], unsigned char const pubkeys[],
+                                    fd_sha512_t * shas[], unsigned char const batch_sz ) {
+  (void)shas;
+  if( batch_sz==0 || batch_sz>16 ) return FD_ED25519_ERR_SIG;
+  fd_ed25519_hip_engine_t * e = default_get();
+  unsigned long off = 0UL;
+  unsigned int  sz = (unsigned int)msg_sz, first = 0U, cnt = batch_sz;
+  signed char   out = 0;
+  static unsigned char const empty[1] = {0};
+  pthread_mutex_lock( &default_lock );
+  int err = fd_ed25519_hip_verify_txns_host( e, 1UL, msg ? msg : empty, &off, &sz, &first, &cnt, signatures,
+                                             pubkeys, &out, NULL );
+  pthread_mutex_unlock( &default_lock );
+  if( err ) dropin_fatal( err );
+  return (int)out;
+}
+
+char const *
+fd_ed25519_strerror( int err ) {
+  switch( err ) {
+  case FD_ED25519_SUCCESS:    return "success";
+  case FD_ED25519_ERR_SIG:    return "bad signature";
+  case FD_ED25519_ERR_PUBKEY: return "bad public key";
+  case FD_ED25519_ERR_MSG:    return "bad message";
+  default: break;
+  }
+  return "unknown";
+}

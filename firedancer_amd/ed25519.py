@@ -1,0 +1,179 @@
+"""Python mirror of the reference's ed25519 verify interface, backed by the
+MI355X library libfd_ed25519_hip (C-ABI, include/fd_ed25519_hip.h).
+
+Mirrors src/ballet/ed25519/fd_ed25519.h:96-138 of tigarcia/firedancer:
+
+    verify(msg, sig, public_key)                    -> fd_ed25519_verify
+    verify_batch_single_msg(msg, signatures, pubs)  -> fd_ed25519_verify_batch_single_msg
+    strerror(err)                                   -> fd_ed25519_strerror
+
+with the same argument meaning and return codes (SUCCESS 0, ERR_SIG -1,
+ERR_PUBKEY -2, ERR_MSG -3), plus the batch Engine the verify tile and
+bench.py drive.  There is no CPU fallback: importing this module without the
+built library raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+SUCCESS = 0
+ERR_SIG = -1
+ERR_PUBKEY = -2
+ERR_MSG = -3
+
+FLAG_CODES_PORTABLE = 1
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FD_ED25519_HIP_LIB", os.path.join(_HERE, "_lib", "libfd_ed25519_hip.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libfd_ed25519_hip not built: {LIB_PATH} missing "
+                      "(run `python -c 'import __graft_entry__ as g; g.build()'`); there is no CPU fallback")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+_u8p = ctypes.c_void_p
+_lib.fd_ed25519_verify.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
+_lib.fd_ed25519_verify.restype = ctypes.c_int
+_lib.fd_ed25519_verify_batch_single_msg.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p,
+                                                    ctypes.c_void_p, ctypes.c_ubyte]
+_lib.fd_ed25519_verify_batch_single_msg.restype = ctypes.c_int
+_lib.fd_ed25519_strerror.argtypes = [ctypes.c_int]
+_lib.fd_ed25519_strerror.restype = ctypes.c_char_p
+_lib.fd_ed25519_hip_engine_new.argtypes = [ctypes.c_int, ctypes.c_ulong, ctypes.c_int]
+_lib.fd_ed25519_hip_engine_new.restype = ctypes.c_void_p
+_lib.fd_ed25519_hip_engine_delete.argtypes = [ctypes.c_void_p]
+_lib.fd_ed25519_hip_engine_stream.argtypes = [ctypes.c_void_p]
+_lib.fd_ed25519_hip_engine_stream.restype = ctypes.c_void_p
+_lib.fd_ed25519_hip_engine_sync.argtypes = [ctypes.c_void_p]
+_lib.fd_ed25519_hip_verify_dev.argtypes = [ctypes.c_void_p, ctypes.c_ulong] + [_u8p] * 7
+_lib.fd_ed25519_hip_txn_combine_dev.argtypes = [ctypes.c_void_p, ctypes.c_ulong] + [_u8p] * 5
+_lib.fd_ed25519_hip_verify_host.argtypes = [ctypes.c_void_p, ctypes.c_ulong] + [_u8p] * 6
+_lib.fd_ed25519_hip_verify_txns_host.argtypes = [ctypes.c_void_p, ctypes.c_ulong] + [_u8p] * 9
+_lib.fd_ed25519_hip_strerror.argtypes = [ctypes.c_int]
+_lib.fd_ed25519_hip_strerror.restype = ctypes.c_char_p
+_lib.fd_ed25519_hip_last_error.restype = ctypes.c_char_p
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("cu_cnt", ctypes.c_int), ("dsm_blocks_per_cu", ctypes.c_int),
+                ("dsm_grid", ctypes.c_uint), ("max_chunk", ctypes.c_ulong), ("device_bytes", ctypes.c_ulong),
+                ("flags", ctypes.c_int), ("arch", ctypes.c_char * 64)]
+
+
+_lib.fd_ed25519_hip_engine_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Info)]
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc:
+        raise HipError(f"{_lib.fd_ed25519_hip_strerror(rc).decode()} ({_lib.fd_ed25519_hip_last_error().decode()})")
+
+
+def library():
+    """The loaded ctypes library (for callers that need raw entry points)."""
+    return _lib
+
+
+def strerror(err):
+    return _lib.fd_ed25519_strerror(int(err)).decode()
+
+
+def verify(msg, sig, public_key):
+    """fd_ed25519_verify drop-in (synchronous, default engine)."""
+    assert len(sig) == 64 and len(public_key) == 32
+    msg = bytes(msg)
+    return _lib.fd_ed25519_verify(msg, len(msg), bytes(sig), bytes(public_key), None)
+
+
+def verify_batch_single_msg(msg, signatures, pubkeys, batch_sz=None):
+    """fd_ed25519_verify_batch_single_msg drop-in: signatures is 64*n bytes,
+    pubkeys 32*n bytes."""
+    signatures, pubkeys, msg = bytes(signatures), bytes(pubkeys), bytes(msg)
+    n = len(signatures) // 64 if batch_sz is None else batch_sz
+    return _lib.fd_ed25519_verify_batch_single_msg(msg, len(msg), signatures or b"\0" * 64, pubkeys or b"\0" * 32,
+                                                   None, n & 0xFF)
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class Engine:
+    """A libfd_ed25519_hip engine bound to one GPU."""
+
+    def __init__(self, device=0, max_chunk=0, codes="avx512"):
+        flags = FLAG_CODES_PORTABLE if codes == "portable" else 0
+        self._h = _lib.fd_ed25519_hip_engine_new(int(device), int(max_chunk), flags)
+        if not self._h:
+            raise HipError(f"engine_new failed: {_lib.fd_ed25519_hip_last_error().decode()}")
+        self.codes = codes
+
+    def close(self):
+        if self._h:
+            _lib.fd_ed25519_hip_engine_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        i = _Info()
+        _check(_lib.fd_ed25519_hip_engine_info(self._h, ctypes.byref(i)))
+        return {f: (getattr(i, f).decode() if f == "arch" else getattr(i, f)) for f, _ in _Info._fields_}
+
+    @property
+    def stream(self):
+        return _lib.fd_ed25519_hip_engine_stream(self._h)
+
+    def sync(self):
+        _check(_lib.fd_ed25519_hip_engine_sync(self._h))
+
+    def verify_host(self, msgs, msg_off, msg_sz, sigs, pubs):
+        """SoA host batch -> int8 codes (synchronous)."""
+        n = len(msg_sz)
+        out = np.zeros(n, dtype=np.int8)
+        if n == 0:
+            return out
+        msgs = _c(msgs, np.uint8) if len(msgs) else np.zeros(1, np.uint8)
+        off, sz = _c(msg_off, np.uint64), _c(msg_sz, np.uint32)
+        sigs, pubs = _c(sigs, np.uint8).reshape(-1), _c(pubs, np.uint8).reshape(-1)
+        assert len(sigs) >= 64 * n and len(pubs) >= 32 * n
+        _check(_lib.fd_ed25519_hip_verify_host(self._h, n, _ptr(msgs), _ptr(off), _ptr(sz), _ptr(sigs), _ptr(pubs),
+                                               _ptr(out)))
+        return out
+
+    def verify_txns_host(self, msgs, txn_msg_off, txn_msg_sz, txn_first, txn_cnt, sigs, pubs, want_sig_codes=False):
+        """batch_single_msg semantics per transaction -> (txn codes, sig codes|None)."""
+        ntxn = len(txn_cnt)
+        out = np.zeros(ntxn, dtype=np.int8)
+        nsig = len(sigs) if np.ndim(sigs) == 2 else len(sigs) // 64
+        osig = np.zeros(max(nsig, 1), dtype=np.int8) if want_sig_codes else None
+        if ntxn == 0:
+            return out, osig
+        msgs = _c(msgs, np.uint8) if len(msgs) else np.zeros(1, np.uint8)
+        sigs = _c(sigs, np.uint8).reshape(-1) if nsig else np.zeros(64, np.uint8)
+        pubs = _c(pubs, np.uint8).reshape(-1) if nsig else np.zeros(32, np.uint8)
+        _check(_lib.fd_ed25519_hip_verify_txns_host(
+            self._h, ntxn, _ptr(msgs), _ptr(_c(txn_msg_off, np.uint64)), _ptr(_c(txn_msg_sz, np.uint32)),
+            _ptr(_c(txn_first, np.uint32)), _ptr(_c(txn_cnt, np.uint32)), _ptr(sigs), _ptr(pubs), _ptr(out),
+            _ptr(osig)))
+        return out, osig
+
+    def verify_dev(self, n, d_msgs, d_off, d_sz, d_sigs, d_pubs, d_out, stream=None):
+        """Device-resident batch: arguments are device addresses (ints); async."""
+        _check(_lib.fd_ed25519_hip_verify_dev(self._h, int(n), d_msgs, d_off, d_sz, d_sigs, d_pubs, d_out, stream))
+
+    def txn_combine_dev(self, ntxn, d_sig_codes, d_first, d_cnt, d_out, stream=None):
+        _check(_lib.fd_ed25519_hip_txn_combine_dev(self._h, int(ntxn), d_sig_codes, d_first, d_cnt, d_out, stream))

@@ -1,0 +1,193 @@
+#ifndef HEADER_fd_ed25519_hip_h
+#define HEADER_fd_ed25519_hip_h
+
+/* libfd_ed25519_hip -- MI355X (gfx950) ed25519 signature verification for
+   Firedancer, as a C-ABI shared library.
+
+   Part 1 is a drop-in for the reference's verify API
+   (tigarcia/firedancer src/ballet/ed25519/fd_ed25519.h:96-138): the same
+   symbols, prototypes, argument meaning and return codes, so a binary that
+   links libfd_ed25519_hip ahead of libfd_ballet.a resolves them here.
+
+   Part 2 is the batch engine the drop-ins sit on.  A synchronous per-call
+   API cannot feed a GPU; callers that batch (the verify
+   tile, bench.py) use the SoA entry points below, either with host buffers
+   (staged through pinned memory) or with device-resident buffers (enqueued
+   asynchronously on a HIP stream).
+
+   Verdicts and error codes are bit-identical to fd_ed25519_verify of the
+   reference's AVX-512 backend (the production build); an engine created with
+   FD_ED25519_HIP_FLAG_CODES_PORTABLE reproduces the portable backend's codes
+   instead (they differ only in the code returned for an undecodable public
+   key). */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Reference codes, src/ballet/ed25519/fd_ed25519.h:11-14 */
+#define FD_ED25519_SUCCESS    ( 0)
+#define FD_ED25519_ERR_SIG    (-1)
+#define FD_ED25519_ERR_PUBKEY (-2)
+#define FD_ED25519_ERR_MSG    (-3)
+
+/* The reference's sha512 calculator (src/ballet/sha512/fd_sha512.h:15-16,
+   56-77: 256 bytes, 128-byte aligned) is opaque here: the drop-ins accept
+   the caller's handle and do not touch it (the hash runs on the GPU). */
+#ifndef FD_SHA512_ALIGN
+typedef struct fd_sha512_private fd_sha512_t;
+#endif
+
+/* ---- Part 1: drop-in verify API ------------------------------------- */
+
+/* Replaces fd_ed25519_verify (src/ballet/ed25519/fd_ed25519.h:96-101,
+   implementation src/ballet/ed25519/fd_ed25519_user.c:134-229).  msg may be
+   NULL if msg_sz==0.  Returns FD_ED25519_SUCCESS or FD_ED25519_ERR_*.
+   Synchronous; runs on the process-wide default engine (device from
+   $FD_ED25519_HIP_DEVICE, default 0; codes from $FD_ED25519_HIP_CODES =
+   "avx512" (default) | "portable").  A GPU failure aborts the process with a
+   message on stderr: this path never silently falls back to the CPU. */
+int
+fd_ed25519_verify( unsigned char const   msg[],
+                   unsigned long         msg_sz,
+                   unsigned char const   sig[ 64 ],
+                   unsigned char const   public_key[ 32 ],
+                   fd_sha512_t *         sha );
+
+/* Replaces fd_ed25519_verify_batch_single_msg (src/ballet/ed25519/fd_ed25519.h:124-130,
+   implementation src/ballet/ed25519/fd_ed25519_user.c:231-309): batch_sz
+   signatures (64 B each, contiguous) by batch_sz public keys (32 B each,
+   contiguous) over one message.  batch_sz==0 or >16 -> FD_ED25519_ERR_SIG.
+   Otherwise the first phase-1 error (bad S, undecodable or small-order key
+   or R) in signature order wins, then FD_ED25519_ERR_MSG if any equation
+   fails. */
+int
+fd_ed25519_verify_batch_single_msg( unsigned char const   msg[],
+                                    unsigned long const   msg_sz,
+                                    unsigned char const   signatures[],
+                                    unsigned char const   pubkeys[],
+                                    fd_sha512_t *         shas[],
+                                    unsigned char const   batch_sz );
+
+/* Replaces fd_ed25519_strerror (src/ballet/ed25519/fd_ed25519_user.c:311-321). */
+char const *
+fd_ed25519_strerror( int err );
+
+/* ---- Part 2: batch engine -------------------------------------------- */
+
+typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
+
+/* Engine API status codes (not verdicts). */
+#define FD_ED25519_HIP_OK          (0)
+#define FD_ED25519_HIP_ERR_INVAL   (-22)   /* bad argument / misaligned device buffer */
+#define FD_ED25519_HIP_ERR_NOMEM   (-12)   /* host or device allocation failed        */
+#define FD_ED25519_HIP_ERR_HIP     (-1000) /* HIP runtime error: -1000 - hipError_t    */
+
+#define FD_ED25519_HIP_FLAG_CODES_PORTABLE (1)  /* portable-backend error codes */
+
+/* Creates an engine on HIP device `device`.  max_chunk is the number of
+   signatures processed per kernel sequence (0 = default 1<<20); larger
+   batches are processed in chunks.  Returns NULL on failure (reason via
+   fd_ed25519_hip_last_error()). */
+fd_ed25519_hip_engine_t *
+fd_ed25519_hip_engine_new( int device, unsigned long max_chunk, int flags );
+
+void
+fd_ed25519_hip_engine_delete( fd_ed25519_hip_engine_t * engine );
+
+typedef struct {
+  int           device;
+  int           cu_cnt;
+  int           dsm_blocks_per_cu;
+  unsigned      dsm_grid;
+  unsigned long max_chunk;
+  unsigned long device_bytes;   /* device memory held by the engine */
+  int           flags;
+  char          arch[ 64 ];
+} fd_ed25519_hip_info_t;
+
+int
+fd_ed25519_hip_engine_info( fd_ed25519_hip_engine_t const * engine, fd_ed25519_hip_info_t * info );
+
+/* The engine's HIP stream (a hipStream_t). */
+void *
+fd_ed25519_hip_engine_stream( fd_ed25519_hip_engine_t * engine );
+
+/* Device-resident batch: every pointer is a device pointer.  Signature i
+   is sigs[64 i .. 64 i + 64) = R || S over message msgs[msg_off[i] ..
+   msg_off[i] + msg_sz[i]) by public key pubs[32 i .. 32 i + 32); out[i]
+   receives its code.  sigs and pubs must be 16-byte aligned; messages may
+   start at any byte.  Enqueued on `stream` (NULL = the engine's stream) and
+   returns immediately; the engine's work arrays are reused by the next
+   call, so calls on one engine must be ordered on one stream. */
+int
+fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * engine,
+                           unsigned long             n,
+                           unsigned char const *     msgs,
+                           unsigned long const *     msg_off,
+                           unsigned int const *      msg_sz,
+                           unsigned char const *     sigs,
+                           unsigned char const *     pubs,
+                           signed char *             out,
+                           void *                    stream );
+
+/* Per-transaction combine on the device (fd_ed25519_verify_batch_single_msg
+   priority), for transactions whose signatures were verified with
+   fd_ed25519_hip_verify_dev: txn t owns signatures [txn_first[t],
+   txn_first[t] + txn_cnt[t]). */
+int
+fd_ed25519_hip_txn_combine_dev( fd_ed25519_hip_engine_t * engine,
+                                unsigned long             ntxn,
+                                signed char const *       sig_codes,
+                                unsigned int const *      txn_first,
+                                unsigned int const *      txn_cnt,
+                                signed char *             txn_out,
+                                void *                    stream );
+
+/* Host-buffer batch, synchronous: messages are packed into pinned staging
+   memory (any offsets / aliasing allowed), copied, verified, and the codes
+   copied back to out[0..n). */
+int
+fd_ed25519_hip_verify_host( fd_ed25519_hip_engine_t * engine,
+                            unsigned long             n,
+                            unsigned char const *     msgs,
+                            unsigned long const *     msg_off,
+                            unsigned int const *      msg_sz,
+                            unsigned char const *     sigs,
+                            unsigned char const *     pubs,
+                            signed char *             out );
+
+/* Host-buffer transactions (fd_ed25519_verify_batch_single_msg semantics
+   for each): txn t has message msgs[txn_msg_off[t] .. + txn_msg_sz[t]) and
+   signatures/keys [txn_first[t], txn_first[t] + txn_cnt[t]) of sigs/pubs.
+   out_txn[t] receives the transaction's code; out_sig (optional, may be
+   NULL) the per-signature codes. */
+int
+fd_ed25519_hip_verify_txns_host( fd_ed25519_hip_engine_t * engine,
+                                 unsigned long             ntxn,
+                                 unsigned char const *     msgs,
+                                 unsigned long const *     txn_msg_off,
+                                 unsigned int const *      txn_msg_sz,
+                                 unsigned int const *      txn_first,
+                                 unsigned int const *      txn_cnt,
+                                 unsigned char const *     sigs,
+                                 unsigned char const *     pubs,
+                                 signed char *             out_txn,
+                                 signed char *             out_sig );
+
+/* Waits for all work enqueued on the engine's stream. */
+int
+fd_ed25519_hip_engine_sync( fd_ed25519_hip_engine_t * engine );
+
+/* Human-readable form of an engine status code / of the last failure. */
+char const *
+fd_ed25519_hip_strerror( int status );
+
+char const *
+fd_ed25519_hip_last_error( void );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEADER_fd_ed25519_hip_h */

@@ -1,0 +1,183 @@
+"""Parity of the MI355X engine (through the C-ABI library) with the reference:
+golden fixtures produced by the reference itself (tests/golden/), and the
+oracle restatement on seeded random / adversarial inputs.  Bit-exact codes."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from conftest import oracle_many
+
+pytestmark = pytest.mark.gpu
+
+L = 2**252 + 27742317777372353535851937790883648493
+
+
+@pytest.fixture(scope="module")
+def fd():
+    from firedancer_amd import ed25519
+    return ed25519
+
+
+@pytest.fixture(scope="module")
+def eng(fd):
+    e = fd.Engine(0, max_chunk=1 << 16)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def eng_portable(fd):
+    e = fd.Engine(0, max_chunk=1 << 14, codes="portable")
+    yield e
+    e.close()
+
+
+def _check(got, want, tags=None):
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [((str(tags[i]) if tags is not None else i), int(got[i]), int(want[i])) for i in bad[:12]]
+
+
+def _run(e, d):
+    return e.verify_host(d["msgs"], d["msg_off"], d["msg_sz"], d["sigs"], d["pubs"])
+
+
+def test_engine_info(eng):
+    info = eng.info()
+    assert info["arch"].startswith("gfx950")
+    assert info["cu_cnt"] > 0 and info["dsm_grid"] > 0
+
+
+def test_reference_vectors(eng, vectors):
+    _check(_run(eng, vectors), vectors["codes_avx512"], vectors["tags"])
+
+
+def test_reference_vectors_accept_reject(eng, vectors):
+    got = _run(eng, vectors)
+    sel = vectors["ok"] >= 0
+    assert np.array_equal((got[sel] == 0).astype(np.int8), vectors["ok"][sel])
+
+
+def test_reference_vectors_portable_codes(eng_portable, vectors):
+    _check(_run(eng_portable, vectors), vectors["codes_portable"], vectors["tags"])
+
+
+def test_adversarial(eng, adversarial):
+    _check(_run(eng, adversarial), adversarial["codes_avx512"], adversarial["tags"])
+
+
+def test_adversarial_portable_codes(eng_portable, adversarial):
+    _check(_run(eng_portable, adversarial), adversarial["codes_portable"], adversarial["tags"])
+
+
+def test_batch_single_msg_txns(eng, batch):
+    out, _ = eng.verify_txns_host(batch["msgs"], batch["txn_msg_off"], batch["txn_msg_sz"], batch["txn_first"],
+                                  batch["txn_cnt"], batch["sigs"], batch["pubs"])
+    _check(out, batch["codes_avx512"], batch["tags"])
+
+
+def test_batch_single_msg_txns_portable(eng_portable, batch):
+    out, _ = eng_portable.verify_txns_host(batch["msgs"], batch["txn_msg_off"], batch["txn_msg_sz"],
+                                           batch["txn_first"], batch["txn_cnt"], batch["sigs"], batch["pubs"])
+    _check(out, batch["codes_portable"], batch["tags"])
+
+
+def _random_set(oracle, n, seed, sizes=None, mutate=True):
+    rng = random.Random(seed)
+    msgs = bytearray()
+    off, sz, sigs, pubs = [], [], bytearray(), bytearray()
+    keys = []
+    for _ in range(32):
+        priv = bytes(rng.getrandbits(8) for _ in range(32))
+        pub = ctypes.create_string_buffer(32)
+        oracle.oracle_ed25519_public_from_private(pub, priv)
+        keys.append((priv, pub.raw))
+    for i in range(n):
+        priv, pub = keys[i % len(keys)]
+        m = bytes(rng.getrandbits(8) for _ in range(sizes(i, rng) if sizes else rng.randrange(0, 1233)))
+        s = ctypes.create_string_buffer(64)
+        oracle.oracle_ed25519_sign(s, m, len(m), pub, priv)
+        sig, pk = bytearray(s.raw), bytearray(pub)
+        if mutate:
+            r = rng.random()
+            if r < 0.05:
+                sig[rng.randrange(64)] ^= 1 << rng.randrange(8)
+            elif r < 0.08:
+                pk[rng.randrange(32)] ^= 1 << rng.randrange(8)
+            elif r < 0.10 and m:
+                mm = bytearray(m); mm[rng.randrange(len(m))] ^= 1; m = bytes(mm)
+        # misalign message starts on purpose
+        msgs += bytes(rng.randrange(0, 4))
+        off.append(len(msgs)); sz.append(len(m)); msgs += m
+        sigs += sig; pubs += pk
+    return dict(msgs=np.frombuffer(bytes(msgs) or b"\0", dtype=np.uint8), msg_off=np.array(off, np.uint64),
+                msg_sz=np.array(sz, np.uint32), sigs=np.frombuffer(bytes(sigs), np.uint8).reshape(-1, 64),
+                pubs=np.frombuffer(bytes(pubs), np.uint8).reshape(-1, 32))
+
+
+def test_random_vs_oracle(eng, oracle):
+    d = _random_set(oracle, 3000, seed=11)
+    want = oracle_many(oracle, d, 0)
+    assert (want == 0).sum() > 2500
+    _check(_run(eng, d), want)
+
+
+def test_every_message_size_vs_oracle(eng, oracle):
+    """All sizes 0..400 (every SHA-512 block boundary and padding split) and
+    the Solana MTU."""
+    d = _random_set(oracle, 402, seed=12, sizes=lambda i, rng: i if i <= 400 else 1232, mutate=False)
+    want = oracle_many(oracle, d, 0)
+    assert (want == 0).all()
+    _check(_run(eng, d), want)
+
+
+def test_scalar_edges(eng, oracle):
+    """S around L and all-ones; S+kL for small k."""
+    d = _random_set(oracle, 64, seed=13, mutate=False)
+    sigs = d["sigs"].copy()
+    for i in range(64):
+        S = int.from_bytes(sigs[i, 32:].tobytes(), "little")
+        choice = [S, S + L, L - 1, L, L + 1, 2**256 - 1, 0, 2**253, S + 2 * L, 2**255 + S][i % 10]
+        sigs[i, 32:] = np.frombuffer((choice % 2**256).to_bytes(32, "little"), np.uint8)
+    d["sigs"] = sigs
+    for codes in (0, 1):
+        pass
+    want = oracle_many(oracle, d, 0)
+    _check(_run(eng, d), want)
+
+
+def test_chunking(fd, oracle):
+    """A batch larger than max_chunk goes through several kernel sequences."""
+    e = fd.Engine(0, max_chunk=700)
+    d = _random_set(oracle, 2500, seed=14)
+    _check(_run(e, d), oracle_many(oracle, d, 0))
+    e.close()
+
+
+def test_empty_batch(eng):
+    out = eng.verify_host(np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
+                          np.zeros((0, 64), np.uint8), np.zeros((0, 32), np.uint8))
+    assert out.shape == (0,)
+
+
+def test_dropin_single(fd, vectors):
+    """fd_ed25519_verify drop-in on the default engine."""
+    for i in range(0, len(vectors["msg_sz"]), 37):
+        off, sz = int(vectors["msg_off"][i]), int(vectors["msg_sz"][i])
+        m = bytes(vectors["msgs"][off:off + sz])
+        got = fd.verify(m, vectors["sigs"][i].tobytes(), vectors["pubs"][i].tobytes())
+        assert got == int(vectors["codes_avx512"][i]), str(vectors["tags"][i])
+
+
+def test_dropin_batch_single_msg(fd, batch):
+    for t in range(0, len(batch["txn_cnt"]), 7):
+        off, sz = int(batch["txn_msg_off"][t]), int(batch["txn_msg_sz"][t])
+        f, n = int(batch["txn_first"][t]), int(batch["txn_cnt"][t])
+        m = bytes(batch["msgs"][off:off + sz])
+        got = fd.verify_batch_single_msg(m, batch["sigs"][f:f + n].tobytes(), batch["pubs"][f:f + n].tobytes(), n)
+        assert got == int(batch["codes_avx512"][t]), (t, str(batch["tags"][t]))
+
+
+def test_strerror(fd):
+    assert fd.strerror(0) == "success" and fd.strerror(-3) == "bad message" and fd.strerror(5) == "unknown"
