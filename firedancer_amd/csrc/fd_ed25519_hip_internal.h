@@ -72,6 +72,39 @@ int fd_ed25519_hip_launch_txn_combine( int8_t const * d_sig_codes, uint32_t cons
                                        uint32_t const * d_txn_cnt, int8_t * d_txn_out, uint64_t ntxn,
                                        void * stream );
 
+/* ---- generator (fd_ed25519_gen.hip) ---- */
+
+typedef struct {
+  uint8_t const *  msgs;
+  uint64_t const * msg_off;
+  uint32_t const * msg_sz;
+  uint8_t const *  privs;      /* [n][32], 16-byte aligned; NULL: derive from (seed, index_base+i) */
+  uint8_t *        sigs;       /* [n][64] out */
+  uint8_t *        pubs;       /* [n][32] out */
+  uint64_t         n;
+  uint64_t         seed;
+  uint64_t         index_base;
+  int32_t const *  btab;
+} fd_ed25519_sign_params_t;
+
+typedef struct {
+  uint8_t *        msgs;
+  uint64_t const * msg_off;
+  uint32_t const * msg_sz;
+  uint8_t *        sigs;
+  uint8_t *        pubs;
+  uint64_t         n;
+  uint64_t         seed;
+  uint64_t         index_base;
+  uint32_t         ppm;        /* corrupted fraction, parts per million */
+  int8_t *         expect;     /* [n] out (optional): reference AVX-512 code */
+  uint8_t *        cls;        /* [n] out (optional): class 0..7 */
+} fd_ed25519_corrupt_params_t;
+
+int fd_ed25519_hip_launch_fill_random( uint8_t * d, uint64_t nbytes, uint64_t seed, void * stream );
+int fd_ed25519_hip_launch_sign( fd_ed25519_sign_params_t const * p, void * stream );
+int fd_ed25519_hip_launch_corrupt( fd_ed25519_corrupt_params_t const * p, void * stream );
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,29 +91,32 @@ FD_DEV uint32_t sha_msg_dword(const sha_msg_src& m, int p, uint32_t lo, uint32_t
 }
 
 /* digest (as 16 little-endian words of the 64-byte output) of
-   R(32) || A(32) || M(sz) */
-FD_DEV void sha512_ram(uint32_t (&out)[16], const uint32_t (&r)[8], const uint32_t (&a)[8],
-                       const sha_msg_src& m) {
+   PRE || M(sz), where PRE is NPRE 32-bit words (8: a 32-byte prefix, e.g.
+   the signing nonce prefix; 16: R || A) held in registers as little-endian
+   words. */
+template <int NPRE>
+FD_DEV void sha512_pre(uint32_t (&out)[16], const uint32_t (&pre)[NPRE], const sha_msg_src& m) {
+  static_assert(NPRE == 8 || NPRE == 16, "prefix is 32 or 64 bytes");
+  constexpr int PB = 4 * NPRE;   /* prefix bytes */
+  constexpr int PW = NPRE / 2;   /* prefix 64-bit words */
   uint64_t h[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
                    0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
                    0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
-  const uint32_t nblk = (m.sz + 208u) >> 7;  /* ceil((64+sz+17)/128) */
-  const uint64_t bitlen = (uint64_t)(64u + m.sz) << 3;
+  const uint32_t nblk = (m.sz + PB + 17u + 127u) >> 7;
+  const uint64_t bitlen = (uint64_t)(PB + m.sz) << 3;
   for (uint32_t b = 0; b < nblk; b++) {
     uint64_t w[16];
-    /* message byte position of word t is 128 b + 8 t - 64 */
-    const int p0 = 128 * (int)b - 64;
-    int j0 = (p0 >> 2);  /* dword index of the first message dword in this block */
+    /* message byte position of word t is 128 b + 8 t - PB */
+    const int p0 = 128 * (int)b - PB;
+    const int j0 = (p0 >> 2);
     uint32_t prev = sha_raw_dword(m, j0 < 0 ? 0 : j0);
 #pragma unroll
     for (int t = 0; t < 16; t++) {
       const int p = p0 + 8 * t;
       uint32_t d0, d1;
-      if (b == 0 && t < 8) {
-        /* R || A from registers */
-        const uint32_t x0 = t < 4 ? r[2 * t] : a[2 * t - 8];
-        const uint32_t x1 = t < 4 ? r[2 * t + 1] : a[2 * t - 7];
-        d0 = x0; d1 = x1;
+      if (t < PW && b == 0) {
+        d0 = pre[2 * t];
+        d1 = pre[2 * t + 1];
       } else {
         const int j = p >> 2;
         const uint32_t l1 = sha_raw_dword(m, j + 1);
@@ -136,4 +139,16 @@ FD_DEV void sha512_ram(uint32_t (&out)[16], const uint32_t (&r)[8], const uint32
     out[2 * i] = bswap32((uint32_t)(h[i] >> 32));
     out[2 * i + 1] = bswap32((uint32_t)h[i]);
   }
+}
+
+/* digest of R(32) || A(32) || M(sz): the verify challenge */
+FD_DEV void sha512_ram(uint32_t (&out)[16], const uint32_t (&r)[8], const uint32_t (&a)[8],
+                       const sha_msg_src& m) {
+  uint32_t pre[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    pre[i] = r[i];
+    pre[8 + i] = a[i];
+  }
+  sha512_pre<16>(out, pre, m);
 }

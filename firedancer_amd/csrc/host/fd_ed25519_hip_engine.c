@@ -229,6 +229,58 @@ fd_ed25519_hip_txn_combine_dev( fd_ed25519_hip_engine_t * e, unsigned long ntxn,
   return FD_ED25519_HIP_OK;
 }
 
+int
+fd_ed25519_hip_sign_dev( fd_ed25519_hip_engine_t * e, unsigned long n,
+                         unsigned char const * msgs, unsigned long const * msg_off, unsigned int const * msg_sz,
+                         unsigned char const * privs, unsigned char * sigs, unsigned char * pubs, void * stream ) {
+  if( !e || (!privs && n) ) return FD_ED25519_HIP_ERR_INVAL;
+  if( !n ) return FD_ED25519_HIP_OK;
+  if( ((uintptr_t)sigs & 15UL) || ((uintptr_t)pubs & 15UL) || ((uintptr_t)privs & 15UL) ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  fd_ed25519_sign_params_t p;
+  memset( &p, 0, sizeof(p) );
+  p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz; p.privs = privs;
+  p.sigs = sigs; p.pubs = pubs; p.n = n; p.btab = e->d_btab;
+  int err = fd_ed25519_hip_launch_sign( &p, stream ? stream : (void *)e->stream );
+  if( err ) return hip_fail( (hipError_t)err, "sign launch" );
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_gen_dev( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned long seed, unsigned long index_base,
+                        unsigned char * msgs, unsigned long msg_bytes, unsigned long const * msg_off,
+                        unsigned int const * msg_sz, unsigned char * sigs, unsigned char * pubs, void * stream ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  if( ((uintptr_t)sigs & 15UL) || ((uintptr_t)pubs & 15UL) ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  void * st = stream ? stream : (void *)e->stream;
+  int err = fd_ed25519_hip_launch_fill_random( msgs, msg_bytes, seed, st );
+  if( err ) return hip_fail( (hipError_t)err, "fill launch" );
+  fd_ed25519_sign_params_t p;
+  memset( &p, 0, sizeof(p) );
+  p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz; p.privs = NULL;
+  p.sigs = sigs; p.pubs = pubs; p.n = n; p.seed = seed; p.index_base = index_base; p.btab = e->d_btab;
+  if( (err = fd_ed25519_hip_launch_sign( &p, st )) ) return hip_fail( (hipError_t)err, "sign launch" );
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_corrupt_dev( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned long seed,
+                            unsigned long index_base, unsigned int ppm, unsigned char * msgs,
+                            unsigned long const * msg_off, unsigned int const * msg_sz, unsigned char * sigs,
+                            unsigned char * pubs, signed char * expect, unsigned char * cls, void * stream ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  if( ((uintptr_t)sigs & 15UL) || ((uintptr_t)pubs & 15UL) ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  fd_ed25519_corrupt_params_t p;
+  memset( &p, 0, sizeof(p) );
+  p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz; p.sigs = sigs; p.pubs = pubs;
+  p.n = n; p.seed = seed; p.index_base = index_base; p.ppm = ppm; p.expect = (int8_t *)expect; p.cls = cls;
+  int err = fd_ed25519_hip_launch_corrupt( &p, stream ? stream : (void *)e->stream );
+  if( err ) return hip_fail( (hipError_t)err, "corrupt launch" );
+  return FD_ED25519_HIP_OK;
+}
+
 /* ---- host staging ------------------------------------------------------ */
 
 static int

@@ -175,6 +175,61 @@ fd_ed25519_hip_verify_txns_host( fd_ed25519_hip_engine_t * engine,
                                  signed char *             out_txn,
                                  signed char *             out_sig );
 
+/* ---- Part 3: batched signing and the synthetic workload generator ------ */
+
+/* Batched fd_ed25519_public_from_private + fd_ed25519_sign on the device
+   (src/ballet/ed25519/fd_ed25519_user.c:4-132): for each i, pubs[32 i..]
+   and sigs[64 i..] receive the public key of privs[32 i..] and its
+   signature of msgs[msg_off[i] .. + msg_sz[i]).  Device pointers; privs,
+   sigs and pubs 16-byte aligned.  Async on `stream` (NULL = engine). */
+int
+fd_ed25519_hip_sign_dev( fd_ed25519_hip_engine_t * engine,
+                         unsigned long             n,
+                         unsigned char const *     msgs,
+                         unsigned long const *     msg_off,
+                         unsigned int const *      msg_sz,
+                         unsigned char const *     privs,
+                         unsigned char *           sigs,
+                         unsigned char *           pubs,
+                         void *                    stream );
+
+/* Deterministic synthetic workload (bench.py): fills
+   msgs[0..msg_bytes) with bytes derived from `seed`, derives the private
+   key of signature g = index_base + i from (seed, g) and writes its public
+   key and signature of message i.  Same (seed, g) -> same bytes on any GPU
+   (firedancer_amd/workload.py recomputes them on the host). */
+int
+fd_ed25519_hip_gen_dev( fd_ed25519_hip_engine_t * engine,
+                        unsigned long             n,
+                        unsigned long             seed,
+                        unsigned long             index_base,
+                        unsigned char *           msgs,
+                        unsigned long             msg_bytes,
+                        unsigned long const *     msg_off,
+                        unsigned int const *      msg_sz,
+                        unsigned char *           sigs,
+                        unsigned char *           pubs,
+                        void *                    stream );
+
+/* Corrupts about ppm/10^6 of the signatures in place with the invalid
+   classes of SURVEY.md §8(d) C2 (bad S, small-order A/R, undecodable A/R,
+   non-canonical A, flipped message bit); expect[i] (optional) receives the
+   code the reference's AVX-512 build returns, cls[i] (optional) the class. */
+int
+fd_ed25519_hip_corrupt_dev( fd_ed25519_hip_engine_t * engine,
+                            unsigned long             n,
+                            unsigned long             seed,
+                            unsigned long             index_base,
+                            unsigned int              ppm,
+                            unsigned char *           msgs,
+                            unsigned long const *     msg_off,
+                            unsigned int const *      msg_sz,
+                            unsigned char *           sigs,
+                            unsigned char *           pubs,
+                            signed char *             expect,
+                            unsigned char *           cls,
+                            void *                    stream );
+
 /* Waits for all work enqueued on the engine's stream. */
 int
 fd_ed25519_hip_engine_sync( fd_ed25519_hip_engine_t * engine );
