@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark: ed25519 batch verification on MI355X.
+
+A step is one verification pass (hash, decode, dsm kernels) over this rank's
+batch of BASELINE.json's C2 workload -- 1,048,576 signatures, messages of
+64-1232 B, 2% invalid -- resident in HBM (generated on the device by the
+library's own batch signer, firedancer_amd/workload.py).  With N GPUs each
+rank verifies its own shard (different signatures, no collective: weak
+scaling); value = signatures verified by all ranks / max-over-ranks time.
+
+Printed on rank 0 as one JSON line, with:
+  roofline      INT32 VALU roofline of the dominant kernel (dsm), from the
+                SURVEY.md §8(d) frozen per-verify op count and the kernel's
+                mean duration measured with HIP events on its stream
+  cpu_baseline  the reference's own fd_ed25519_verify (compiled from its
+                sources into oracle/_ref) on this host's cores, over a bounded
+                sample of the same workload (rank 0, N=1 only)
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "ed25519 verifies/sec at 1/8 GPUs; % INT32 VALU roofline; p99 batch latency"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup(gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return rank, local, world
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def allreduce_max(x, world):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(x, world):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def cpu_has(flag):
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    return flag in line.split()
+    except OSError:
+        pass
+    return False
+
+
+def cpu_baseline(wl, gpu_codes, sample, reps):
+    """Reference CPU verify (oracle/_ref) on `sample` signatures of the workload,
+    one pthread per core of this process's share.  Also checks the reference's
+    verdicts against the GPU's on the sample."""
+    from firedancer_amd import workload  # noqa: F401
+    ref_dir = os.path.join(REPO, "oracle", "_ref")
+    flavour = "avx512" if cpu_has("avx512ifma") and cpu_has("avx512vbmi") else "portable"
+    path = os.path.join(ref_dir, f"libfdref_{flavour}.so")
+    kind = "reference"
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.fdref_verify_many.restype = ctypes.c_long
+    lib.fdref_verify_many.argtypes = [ctypes.c_ulong] + [ctypes.c_void_p] * 6 + [ctypes.c_int, ctypes.c_ulong]
+    n = min(sample, wl.n)
+    sizes = wl.sizes[:n].astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    np.cumsum(sizes[:-1], out=off[1:])
+    nbytes = int(sizes.sum())
+    msgs = wl.msgs.download(np.uint8, max(nbytes, 1))
+    sigs = wl.sigs.download(np.uint8, 64 * n)
+    pubs = wl.pubs.download(np.uint8, 32 * n)
+    sz = wl.sizes[:n].astype(np.uint32)
+    out = np.zeros(n, np.int8)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    ns = lib.fdref_verify_many(n, msgs.ctypes.data, off.ctypes.data, sz.ctypes.data, sigs.ctypes.data,
+                               pubs.ctypes.data, out.ctypes.data, threads, reps)
+    if ns <= 0:
+        return None
+    rate = n * reps / (ns * 1e-9)
+    return {"value": rate, "unit": "verifies/s", "cores": threads, "kind": kind,
+            "sample": f"first {n} signatures of the C2 workload x {reps} passes, fd_ed25519_verify of the "
+                      f"reference's {flavour} backend (compiled from its sources), {threads} pthreads",
+            "seconds": ns * 1e-9, "per_core": rate / threads,
+            "verdicts_equal_gpu": bool(np.array_equal(out, gpu_codes[:n]))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--n", type=int, default=0, help="signatures per GPU (default: the config's)")
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--cpu-sample", type=int, default=262144)
+    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, local, world = dist_setup(args.gpus)
+    from firedancer_amd import ed25519, workload
+
+    cfg = dict(workload.CONFIGS[args.config])
+    n = args.n or cfg["n"]
+    eng = ed25519.Engine(device=local, max_chunk=min(n, 1 << 20))
+    info = eng.info()
+    log(f"[rank {rank}] engine {info}")
+
+    t = time.perf_counter()
+    wl = ed25519.DeviceWorkload(eng, n, cfg["lo"], cfg["hi"], cfg["ppm"], seed=args.seed, index_base=rank * n)
+    gen_s = time.perf_counter() - t
+    log(f"[rank {rank}] generated {n} signatures ({wl.msg_bytes / 1e6:.1f} MB of messages) in {gen_s:.2f} s")
+
+    for _ in range(args.warmup):
+        wl.verify()
+    eng.sync()
+
+    eng.timing(True)
+    barrier(world)
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.verify()
+    eng.sync()
+    t1 = time.perf_counter()
+    barrier(world)
+    phase_ms, launches = eng.timing_read()
+    eng.timing(False)
+    elapsed = allreduce_max(t1 - t0, world)
+
+    # full-size verdict check: every code equals the class label's reference code
+    out = wl.out.download(np.int8, n)
+    expect = wl.expect.download(np.int8, n)
+    mism = int((out != expect).sum())
+    mism_all = int(allreduce_sum(mism, world))
+    if mism:
+        log(f"[rank {rank}] VERDICT MISMATCH on {mism} of {n} signatures")
+
+    total = world * n * args.steps
+    value = total / elapsed
+    ms_step = elapsed * 1e3 / args.steps
+
+    # roofline (dsm = dominant kernel)
+    ops = workload.ops_per_verify(wl.sizes)
+    clock = eng.clock_mhz() * 1e6
+    peak = clock * info["cu_cnt"] * 64 * 2 / 1e12
+    per_launch = {k: v / max(launches, 1) for k, v in phase_ms.items()}
+    dsm_ops = float(ops["dsm"].sum())
+    achieved = dsm_ops / (per_launch["dsm"] * 1e-3) / 1e12 if per_launch["dsm"] > 0 else None
+    path_ms = sum(per_launch.values())
+    path_ops = float(ops["total"].sum())
+    path_achieved = path_ops / (path_ms * 1e-3) / 1e12 if path_ms > 0 else None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(wl, out, args.cpu_sample, args.cpu_reps)
+        except Exception as ex:  # reported, never fatal for the GPU number
+            log(f"cpu baseline failed: {ex!r}")
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic: seeded keys/messages generated and signed on the GPU (fd_ed25519_hip_gen_dev), "
+                    "2% corrupted by class (fd_ed25519_hip_corrupt_dev)",
+            "config": {"workload": f"{args.config}: {n} signatures per GPU, message size uniform "
+                                   f"[{cfg['lo']},{cfg['hi']}] B, {cfg['ppm'] / 1e4:.1f}% invalid",
+                       "signatures_per_gpu": n, "parallelism": f"shard x{world} (independent batches, no collective)",
+                       "codes": "reference AVX-512 backend"},
+            "roofline": {"bound": "valu-int32", "kernel": "fd_ed25519_dsm_kernel",
+                         "achieved": achieved, "peak": peak, "unit": "TOPS",
+                         "frac": (achieved / peak) if achieved else None, "traffic": None,
+                         "ops_per_launch": dsm_ops, "launch_ms": per_launch["dsm"],
+                         "path": {"achieved": path_achieved, "frac": (path_achieved / peak) if path_achieved else None,
+                                  "ops_per_verify_mean": path_ops / n, "ms_per_launch": path_ms}},
+            "kernel_ms_per_launch": per_launch,
+            "cpu_baseline": cpu,
+            "gpu_over_cpu": (value / cpu["value"]) if cpu else None,
+            "verdicts_match_reference_labels": mism_all == 0,
+            "verdict_mismatches": mism_all,
+            "invalid_fraction": float((expect != 0).mean()),
+            "gen_seconds": gen_s,
+        }
+        print(json.dumps(line), flush=True)
+    wl.free()
+    eng.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0 if mism_all == 0 else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -62,6 +62,13 @@ int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
 /* Enqueues hash, decode and dsm for one chunk; `grid` caps the persistent
    dsm grid (its atab scratch must hold grid*VERIFY_BLOCK/64 waves). */
 int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t grid, void * stream );
+
+/* The same, one phase at a time (so the host can bracket each with events). */
+#define FD_ED25519_PHASE_HASH   0
+#define FD_ED25519_PHASE_DECODE 1
+#define FD_ED25519_PHASE_DSM    2
+#define FD_ED25519_PHASE_CNT    3
+int fd_ed25519_hip_launch_phase( fd_ed25519_verify_params_t const * p, int phase, uint32_t grid, void * stream );
 int fd_ed25519_hip_verify_occupancy( int * blocks_per_cu );
 
 /* Per-transaction combine with fd_ed25519_verify_batch_single_msg's

@@ -287,16 +287,36 @@ extern "C" int fd_ed25519_hip_launch_gen_btab(int32_t* d_btab, void* stream) {
   return (int)hipGetLastError();
 }
 
-extern "C" int fd_ed25519_hip_launch_verify(const fd_ed25519_verify_params_t* p, uint32_t grid, void* stream) {
+extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, int phase, uint32_t grid,
+                                           void* stream) {
   if (!p->n) return 0;
   hipStream_t st = (hipStream_t)stream;
   const uint32_t blk = 256;
-  hipLaunchKernelGGL(fd_ed25519_hash_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
-  hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((2 * p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
-  const uint64_t need = (p->n + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
-  const uint32_t g = (uint32_t)(need < grid ? need : grid);
-  hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
+  switch (phase) {
+  case FD_ED25519_PHASE_HASH:
+    hipLaunchKernelGGL(fd_ed25519_hash_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
+    break;
+  case FD_ED25519_PHASE_DECODE:
+    hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((2 * p->n + blk - 1) / blk)), dim3(blk), 0, st,
+                       *p);
+    break;
+  case FD_ED25519_PHASE_DSM: {
+    const uint64_t need = (p->n + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
+    const uint32_t g = (uint32_t)(need < grid ? need : grid);
+    hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
+  } break;
+  default:
+    return (int)hipErrorInvalidValue;
+  }
   return (int)hipGetLastError();
+}
+
+extern "C" int fd_ed25519_hip_launch_verify(const fd_ed25519_verify_params_t* p, uint32_t grid, void* stream) {
+  for (int ph = 0; ph < FD_ED25519_PHASE_CNT; ph++) {
+    const int err = fd_ed25519_hip_launch_phase(p, ph, grid, stream);
+    if (err) return err;
+  }
+  return 0;
 }
 
 extern "C" int fd_ed25519_hip_verify_occupancy(int* blocks_per_cu) {

@@ -24,6 +24,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#define FD_ED25519_HIP_TIMING_MAX 256
+
 struct fd_ed25519_hip_engine {
   int          device;
   int          flags;
@@ -56,6 +58,12 @@ struct fd_ed25519_hip_engine {
   uint32_t *   h_tfirst; uint32_t * d_tfirst;
   uint32_t *   h_tcnt;  uint32_t * d_tcnt;
   int8_t *     h_tout;  int8_t *   d_tout;
+
+  /* per-phase event timing (bench / profiling) */
+  int          timing;
+  int          tm_ev_init;
+  int          tm_cnt;
+  hipEvent_t   tm_ev[ FD_ED25519_HIP_TIMING_MAX ][ FD_ED25519_PHASE_CNT+1 ];
 };
 
 static __thread char fd_ed25519_hip_errbuf[ 256 ];
@@ -97,6 +105,9 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   hipHostFree( e->h_msgs ); hipHostFree( e->h_off ); hipHostFree( e->h_sz ); hipHostFree( e->h_sigs );
   hipHostFree( e->h_pubs ); hipHostFree( e->h_out ); hipHostFree( e->h_tfirst ); hipHostFree( e->h_tcnt );
   hipHostFree( e->h_tout );
+  if( e->tm_ev_init )
+    for( int i=0; i<FD_ED25519_HIP_TIMING_MAX; i++ )
+      for( int j=0; j<=FD_ED25519_PHASE_CNT; j++ ) hipEventDestroy( e->tm_ev[i][j] );
   if( e->stream ) hipStreamDestroy( e->stream );
   free( e );
 }
@@ -209,10 +220,93 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   for( uint64_t base=0UL; base<n; base+=e->max_chunk ) {
     p.base = base;
     p.n    = (n-base) < e->max_chunk ? (n-base) : e->max_chunk;
-    int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, st );
-    if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+    if( e->timing && e->tm_cnt<FD_ED25519_HIP_TIMING_MAX ) {
+      /* events bracket each phase kernel on the stream it runs on */
+      hipEvent_t * ev = e->tm_ev[ e->tm_cnt++ ];
+      HIPCHK( hipEventRecord( ev[0], st ), "hipEventRecord" );
+      for( int ph=0; ph<FD_ED25519_PHASE_CNT; ph++ ) {
+        int err = fd_ed25519_hip_launch_phase( &p, ph, e->dsm_grid, st );
+        if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+        HIPCHK( hipEventRecord( ev[ph+1], st ), "hipEventRecord" );
+      }
+    } else {
+      int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, st );
+      if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+    }
   }
   return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_engine_timing( fd_ed25519_hip_engine_t * e, int enable ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  if( enable && !e->tm_ev_init ) {
+    for( int i=0; i<FD_ED25519_HIP_TIMING_MAX; i++ )
+      for( int j=0; j<=FD_ED25519_PHASE_CNT; j++ )
+        HIPCHK( hipEventCreate( &e->tm_ev[i][j] ), "hipEventCreate" );
+    e->tm_ev_init = 1;
+  }
+  e->timing = enable;
+  e->tm_cnt = 0;
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * e, double * phase_ms, unsigned long * launches ) {
+  if( !e || !phase_ms ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  for( int ph=0; ph<FD_ED25519_PHASE_CNT; ph++ ) phase_ms[ph] = 0.0;
+  for( int i=0; i<e->tm_cnt; i++ ) {
+    HIPCHK( hipEventSynchronize( e->tm_ev[i][FD_ED25519_PHASE_CNT] ), "hipEventSynchronize" );
+    for( int ph=0; ph<FD_ED25519_PHASE_CNT; ph++ ) {
+      float ms = 0.f;
+      HIPCHK( hipEventElapsedTime( &ms, e->tm_ev[i][ph], e->tm_ev[i][ph+1] ), "hipEventElapsedTime" );
+      phase_ms[ph] += (double)ms;
+    }
+  }
+  if( launches ) *launches = (unsigned long)e->tm_cnt;
+  e->tm_cnt = 0;
+  return FD_ED25519_HIP_OK;
+}
+
+/* ---- device memory helpers (the engine's HIP runtime) ---------------- */
+
+void *
+fd_ed25519_hip_dev_alloc( fd_ed25519_hip_engine_t * e, unsigned long bytes ) {
+  if( !e ) return NULL;
+  if( hipSetDevice( e->device )!=hipSuccess ) return NULL;
+  void * p = NULL;
+  hipError_t err = hipMalloc( &p, bytes ? bytes : 1UL );
+  if( err!=hipSuccess ) { hip_fail( err, "hipMalloc" ); return NULL; }
+  return p;
+}
+
+int
+fd_ed25519_hip_dev_free( fd_ed25519_hip_engine_t * e, void * p ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  HIPCHK( hipFree( p ), "hipFree" );
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_memcpy( fd_ed25519_hip_engine_t * e, void * dst, void const * src, unsigned long bytes, int dir ) {
+  if( !e ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  hipMemcpyKind k = dir==FD_ED25519_HIP_H2D ? hipMemcpyHostToDevice
+                  : dir==FD_ED25519_HIP_D2H ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+  HIPCHK( hipMemcpyAsync( dst, src, bytes, k, e->stream ), "hipMemcpyAsync" );
+  HIPCHK( hipStreamSynchronize( e->stream ), "hipStreamSynchronize" );
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_device_clock_mhz( fd_ed25519_hip_engine_t * e ) {
+  if( !e ) return 0;
+  hipDeviceProp_t prop;
+  if( hipGetDeviceProperties( &prop, e->device )!=hipSuccess ) return 0;
+  return prop.clockRate / 1000;
 }
 
 int

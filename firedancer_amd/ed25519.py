@@ -51,6 +51,20 @@ _lib.fd_ed25519_hip_verify_dev.argtypes = [ctypes.c_void_p, ctypes.c_ulong] + [_
 _lib.fd_ed25519_hip_txn_combine_dev.argtypes = [ctypes.c_void_p, ctypes.c_ulong] + [_u8p] * 5
 _lib.fd_ed25519_hip_verify_host.argtypes = [ctypes.c_void_p, ctypes.c_ulong] + [_u8p] * 6
 _lib.fd_ed25519_hip_verify_txns_host.argtypes = [ctypes.c_void_p, ctypes.c_ulong] + [_u8p] * 9
+_lib.fd_ed25519_hip_sign_dev.argtypes = [ctypes.c_void_p, ctypes.c_ulong] + [_u8p] * 7
+_lib.fd_ed25519_hip_gen_dev.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong, _u8p,
+                                        ctypes.c_ulong] + [_u8p] * 5
+_lib.fd_ed25519_hip_corrupt_dev.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong,
+                                            ctypes.c_uint] + [_u8p] * 8
+_lib.fd_ed25519_hip_engine_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+_lib.fd_ed25519_hip_engine_timing_read.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                                   ctypes.POINTER(ctypes.c_ulong)]
+_lib.fd_ed25519_hip_dev_alloc.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
+_lib.fd_ed25519_hip_dev_alloc.restype = ctypes.c_void_p
+_lib.fd_ed25519_hip_dev_free.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+_lib.fd_ed25519_hip_memcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
+                                       ctypes.c_int]
+_lib.fd_ed25519_hip_device_clock_mhz.argtypes = [ctypes.c_void_p]
 _lib.fd_ed25519_hip_strerror.argtypes = [ctypes.c_int]
 _lib.fd_ed25519_hip_strerror.restype = ctypes.c_char_p
 _lib.fd_ed25519_hip_last_error.restype = ctypes.c_char_p
@@ -177,3 +191,101 @@ class Engine:
 
     def txn_combine_dev(self, ntxn, d_sig_codes, d_first, d_cnt, d_out, stream=None):
         _check(_lib.fd_ed25519_hip_txn_combine_dev(self._h, int(ntxn), d_sig_codes, d_first, d_cnt, d_out, stream))
+
+
+    # ---- batched signing / synthetic workloads -------------------------
+    def sign_dev(self, n, d_msgs, d_off, d_sz, d_privs, d_sigs, d_pubs, stream=None):
+        _check(_lib.fd_ed25519_hip_sign_dev(self._h, int(n), d_msgs, d_off, d_sz, d_privs, d_sigs, d_pubs, stream))
+
+    def gen_dev(self, n, seed, index_base, d_msgs, msg_bytes, d_off, d_sz, d_sigs, d_pubs, stream=None):
+        _check(_lib.fd_ed25519_hip_gen_dev(self._h, int(n), int(seed), int(index_base), d_msgs, int(msg_bytes), d_off,
+                                           d_sz, d_sigs, d_pubs, stream))
+
+    def corrupt_dev(self, n, seed, index_base, ppm, d_msgs, d_off, d_sz, d_sigs, d_pubs, d_expect=None, d_cls=None,
+                    stream=None):
+        _check(_lib.fd_ed25519_hip_corrupt_dev(self._h, int(n), int(seed), int(index_base), int(ppm), d_msgs, d_off,
+                                               d_sz, d_sigs, d_pubs, d_expect, d_cls, stream))
+
+    # ---- measurement ------------------------------------------------------
+    def timing(self, enable=True):
+        _check(_lib.fd_ed25519_hip_engine_timing(self._h, 1 if enable else 0))
+
+    def timing_read(self):
+        ms = (ctypes.c_double * 3)()
+        cnt = ctypes.c_ulong(0)
+        _check(_lib.fd_ed25519_hip_engine_timing_read(self._h, ms, ctypes.byref(cnt)))
+        return {"hash": ms[0], "decode": ms[1], "dsm": ms[2]}, cnt.value
+
+    def clock_mhz(self):
+        return _lib.fd_ed25519_hip_device_clock_mhz(self._h)
+
+    # ---- device memory ----------------------------------------------------
+    def alloc(self, nbytes):
+        return DeviceBuffer(self, nbytes)
+
+
+class DeviceBuffer:
+    """Device memory owned by an engine's HIP runtime."""
+
+    def __init__(self, engine, nbytes):
+        self.engine, self.nbytes = engine, int(nbytes)
+        self.ptr = _lib.fd_ed25519_hip_dev_alloc(engine._h, max(self.nbytes, 1))
+        if not self.ptr:
+            raise HipError(f"dev_alloc({nbytes}) failed: {_lib.fd_ed25519_hip_last_error().decode()}")
+
+    def upload(self, arr):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        _check(_lib.fd_ed25519_hip_memcpy(self.engine._h, self.ptr, arr.ctypes.data, arr.nbytes, 0))
+        return self
+
+    def download(self, dtype, count, offset_bytes=0):
+        out = np.empty(count, dtype=dtype)
+        assert offset_bytes + out.nbytes <= self.nbytes
+        _check(_lib.fd_ed25519_hip_memcpy(self.engine._h, out.ctypes.data, self.ptr + offset_bytes, out.nbytes, 1))
+        return out
+
+    def free(self):
+        if self.ptr:
+            _lib.fd_ed25519_hip_dev_free(self.engine._h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DeviceWorkload:
+    """A signature batch resident in HBM (SoA), generated on the device."""
+
+    def __init__(self, engine, n, lo, hi, ppm, seed, index_base=0):
+        from . import workload
+        self.n = n
+        sizes = workload.msg_sizes(seed, index_base, n, lo, hi)
+        off = workload.msg_offsets(sizes)
+        self.msg_bytes = int(sizes.astype(np.uint64).sum())
+        self.sizes = sizes
+        self.msgs = engine.alloc(self.msg_bytes + 16)
+        self.off = engine.alloc(8 * n).upload(off)
+        self.sz = engine.alloc(4 * n).upload(sizes)
+        self.sigs = engine.alloc(64 * n)
+        self.pubs = engine.alloc(32 * n)
+        self.out = engine.alloc(n)
+        self.expect = engine.alloc(n)
+        self.cls = engine.alloc(n)
+        engine.gen_dev(n, seed, index_base, self.msgs.ptr, self.msg_bytes, self.off.ptr, self.sz.ptr, self.sigs.ptr,
+                       self.pubs.ptr)
+        engine.corrupt_dev(n, seed, index_base, ppm, self.msgs.ptr, self.off.ptr, self.sz.ptr, self.sigs.ptr,
+                           self.pubs.ptr, self.expect.ptr, self.cls.ptr)
+        engine.sync()
+        self.engine = engine
+
+    def verify(self, stream=None):
+        self.engine.verify_dev(self.n, self.msgs.ptr, self.off.ptr, self.sz.ptr, self.sigs.ptr, self.pubs.ptr,
+                               self.out.ptr, stream)
+
+    def free(self):
+        for b in (self.msgs, self.off, self.sz, self.sigs, self.pubs, self.out, self.expect, self.cls):
+            b.free()

@@ -1,0 +1,95 @@
+"""Synthetic workloads of SURVEY.md §8(d), shared by bench.py and the tests.
+
+Every byte is a pure function of (seed, global signature index), computed by
+a counter-based mixer (the splitmix64 finalizer), so a shard of a stream can
+be produced on any GPU (fd_ed25519_hip_gen_dev / _corrupt_dev) and the same
+bytes recomputed here on the host.  Definitions must match
+firedancer_amd/csrc/fd_ed25519_gen.hip.
+
+  C2  1,048,576 signatures, message size uniform in [64, 1232] B, 2% invalid
+      (S+L, small-order A/R, undecodable A/R, non-canonical A, message bit
+      flip), messages packed back to back at arbitrary byte offsets.
+  C4  the C2 distribution as a 64M-signature stream, sharded over ranks.
+"""
+import numpy as np
+
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+MSG_SALT = np.uint64(0xA0761D6478BD642F)
+BAD_SALT = np.uint64(0xE7037ED1A0B428DB)
+SIZE_SALT = np.uint64(0xD1B54A32D192ED03)
+
+CONFIGS = {
+    "C1": dict(n=16384, lo=200, hi=200, ppm=0),
+    "C2": dict(n=1 << 20, lo=64, hi=1232, ppm=20000),
+}
+
+# invalid classes of fd_ed25519_corrupt_kernel -> reference AVX-512 code
+CLASS_NAMES = ["valid", "S_plus_L", "A_small_order", "R_small_order", "A_undecodable", "R_undecodable",
+               "A_noncanonical_y", "msg_bitflip"]
+
+
+def mix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def _ctr(salted_seed, idx):
+    with np.errstate(over="ignore"):
+        return np.uint64(salted_seed) + GOLDEN * (np.asarray(idx, dtype=np.uint64) + np.uint64(1))
+
+
+def msg_sizes(seed, index_base, n, lo, hi):
+    g = np.arange(index_base, index_base + n, dtype=np.uint64)
+    x = mix64(_ctr(np.uint64(seed) ^ SIZE_SALT, g))
+    return (np.uint64(lo) + x % np.uint64(hi - lo + 1)).astype(np.uint32)
+
+
+def msg_offsets(sizes):
+    off = np.zeros(len(sizes), dtype=np.uint64)
+    if len(sizes) > 1:
+        np.cumsum(sizes[:-1], dtype=np.uint64, out=off[1:])
+    return off
+
+
+def msg_buffer(seed, nbytes):
+    """Host recomputation of the message buffer fd_ed25519_fill_random_kernel writes."""
+    words = (nbytes + 7) // 8
+    x = mix64(_ctr(np.uint64(seed) ^ MSG_SALT, np.arange(words, dtype=np.uint64)))
+    return x.astype("<u8").view(np.uint8)[:nbytes].copy()
+
+
+def private_keys(seed, index_base, n):
+    """Host recomputation of the derived private keys ([n][32] bytes)."""
+    g = np.arange(index_base, index_base + n, dtype=np.uint64)
+    ctr = (g[:, None] * np.uint64(4) + np.arange(4, dtype=np.uint64)[None, :])
+    x = mix64(_ctr(np.uint64(seed), ctr))
+    return x.astype("<u8").view(np.uint8).reshape(n, 32)
+
+
+def corruption(seed, index_base, n, ppm):
+    """(class[n], selector[n]) as fd_ed25519_corrupt_kernel draws them."""
+    g = np.arange(index_base, index_base + n, dtype=np.uint64)
+    x = mix64(_ctr(np.uint64(seed) ^ BAD_SALT, g))
+    bad = (x % np.uint64(1000000)) < np.uint64(ppm)
+    cls = np.where(bad, 1 + ((x >> np.uint64(32)) % np.uint64(7)), 0).astype(np.uint8)
+    return cls, (x >> np.uint64(40)).astype(np.uint64)
+
+
+def ops_per_verify(msg_sz):
+    """SURVEY.md §8(d) frozen algorithmic INT32 op count per verify, split by
+    phase kernel.  Unit costs (radix 2^25.5): mul 130, sqr 85, carried
+    add/sub 30, uncarried add/sub 10, SHA-512 block 5400, misc 2000.
+    Totals: 1381 mul + 1520 sqr + 806.5 add/sub + 1265.8 add_nr + SHA + misc.
+      hash   = SHA-512 blocks of R||A||M + mod-L reduction (1000)
+      decode = two square roots: 2 x (pow22523 = 251 sqr + 11 mul, + 10 mul, 2 sqr)
+      dsm    = the rest (double-scalar multiplication, table, compare)."""
+    msg_sz = np.asarray(msg_sz, dtype=np.float64)
+    blocks = np.ceil((81.0 + msg_sz) / 128.0)
+    total = 1381 * 130 + 1520 * 85 + 806.5 * 30 + 1265.8 * 10 + 5400 * blocks + 2000
+    hash_ = 5400 * blocks + 1000
+    decode = 2 * (253 * 85 + 21 * 130)
+    dsm = total - hash_ - decode
+    return dict(total=total, hash=hash_, decode=np.full_like(total, decode), dsm=dsm)

@@ -230,6 +230,38 @@ fd_ed25519_hip_corrupt_dev( fd_ed25519_hip_engine_t * engine,
                             unsigned char *           cls,
                             void *                    stream );
 
+/* ---- Part 4: measurement and device-memory helpers ------------------ */
+
+/* Phase timing: while enabled, fd_ed25519_hip_verify_dev brackets each of
+   its phase kernels (0 hash, 1 decode, 2 dsm) with HIP events on the stream
+   they run on (up to 256 chunk launches); _timing_read waits for them and
+   returns the summed milliseconds per phase and the number of chunk
+   launches, then resets.  Enabling resets too. */
+int
+fd_ed25519_hip_engine_timing( fd_ed25519_hip_engine_t * engine, int enable );
+
+int
+fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * engine, double phase_ms[ 3 ], unsigned long * launches );
+
+/* Device memory from the engine's HIP runtime (so callers need not link a
+   second runtime).  memcpy is synchronous on the engine's stream. */
+#define FD_ED25519_HIP_H2D (0)
+#define FD_ED25519_HIP_D2H (1)
+#define FD_ED25519_HIP_D2D (2)
+
+void *
+fd_ed25519_hip_dev_alloc( fd_ed25519_hip_engine_t * engine, unsigned long bytes );
+
+int
+fd_ed25519_hip_dev_free( fd_ed25519_hip_engine_t * engine, void * ptr );
+
+int
+fd_ed25519_hip_memcpy( fd_ed25519_hip_engine_t * engine, void * dst, void const * src, unsigned long bytes, int dir );
+
+/* Peak shader clock of the engine's device in MHz (hipDeviceProp clockRate). */
+int
+fd_ed25519_hip_device_clock_mhz( fd_ed25519_hip_engine_t * engine );
+
 /* Waits for all work enqueued on the engine's stream. */
 int
 fd_ed25519_hip_engine_sync( fd_ed25519_hip_engine_t * engine );
