@@ -134,14 +134,14 @@ FD_DEV void atab_store(int4* lane_tab, int e, const ge_cached& c) {
   }
 #pragma unroll
   for (int q = 0; q < 10; q++)
-    lane_tab[(e * 10 + q) * 64] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    lane_tab[e * 10 + q] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
 }
 
 FD_DEV void atab_load(ge_cached& c, const int4* lane_tab, int e) {
   int v[40];
 #pragma unroll
   for (int q = 0; q < 10; q++) {
-    const int4 x = lane_tab[(e * 10 + q) * 64];
+    const int4 x = lane_tab[e * 10 + q];
     v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
   }
 #pragma unroll

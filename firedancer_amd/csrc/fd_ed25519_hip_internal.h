@@ -18,7 +18,10 @@ extern "C" {
 #define FD_ED25519_BTAB_INTS      (FD_ED25519_BTAB_ENTRIES * FD_ED25519_BTAB_STRIDE)
 
 /* Per-lane table of [0..8](-A) in cached form, in HBM: 9 entries x 40 int32
-   per lane, laid out [wave][entry][quad][lane] (int4 granules). */
+   per lane, laid out [wave][lane][entry][quad] (int4 granules): a lookup
+   reads 160 contiguous bytes of the lane's own table, so every fetched line
+   is fully used (the [entry][quad][lane] layout fetched ~2.4x the table
+   bytes from HBM because lanes pick different entries). */
 #define FD_ED25519_ATAB_BYTES_PER_WAVE (9UL * 10UL * 64UL * 16UL)
 
 #define FD_ED25519_VERIFY_BLOCK 256

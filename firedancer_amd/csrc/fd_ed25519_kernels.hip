@@ -214,7 +214,7 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   int4* lane_tab = reinterpret_cast<int4*>(static_cast<char*>(p.atab) +
-                                           (gtid >> 6) * FD_ED25519_ATAB_BYTES_PER_WAVE) + (threadIdx.x & 63);
+                                           (gtid >> 6) * FD_ED25519_ATAB_BYTES_PER_WAVE) + (threadIdx.x & 63) * 90;
   for (uint64_t j = gtid; j < p.n; j += stride) p.out[p.base + j] = (int8_t)dsm_one(p, j, lane_tab, s_btab);
 }
 
