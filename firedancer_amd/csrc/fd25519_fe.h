@@ -73,24 +73,31 @@ FD_DEV void fe_select(fe& h, const fe& f, const fe& g, bool c) {
   for (int i = 0; i < 10; i++) h.v[i] = c ? g.v[i] : f.v[i];
 }
 
-/* Column sums h[k] of a 10x10 product, reduced to tight limbs.  Carries
-   round to nearest (centered limbs) in two interleaved chains. */
+/* Rounding bias of column k: the carry out of a centered limb is
+   (a + 2^(w-1)) >> w.  Accumulators start at this bias (it rides along the
+   multiply-accumulate chain for free), so each carry step is one 64-bit
+   shift and one 64-bit add, and the limb is (low bits) - bias. */
+#define FE_BIAS(k) (((k) & 1) ? (1LL << 24) : (1LL << 25))
+
+/* Column sums a[k] (each pre-biased with FE_BIAS(k)) of a 10x10 product,
+   reduced to tight centered limbs in two interleaved chains (limbs 4 and 0
+   are carried twice; between their two carries they are kept in biased
+   form, so the result equals carrying (a + 2^(w-1)) >> w step by step). */
 FD_DEV void fe_carry_wide(fe& h, int64_t (&a)[10]) {
+  const int64_t m26 = (1LL << 26) - 1, m25 = (1LL << 25) - 1;
   int64_t c;
-  c = (a[0] + (1LL << 25)) >> 26; a[1] += c; a[0] -= c << 26;
-  c = (a[4] + (1LL << 25)) >> 26; a[5] += c; a[4] -= c << 26;
-  c = (a[1] + (1LL << 24)) >> 25; a[2] += c; a[1] -= c << 25;
-  c = (a[5] + (1LL << 24)) >> 25; a[6] += c; a[5] -= c << 25;
-  c = (a[2] + (1LL << 25)) >> 26; a[3] += c; a[2] -= c << 26;
-  c = (a[6] + (1LL << 25)) >> 26; a[7] += c; a[6] -= c << 26;
-  c = (a[3] + (1LL << 24)) >> 25; a[4] += c; a[3] -= c << 25;
-  c = (a[7] + (1LL << 24)) >> 25; a[8] += c; a[7] -= c << 25;
-  c = (a[4] + (1LL << 25)) >> 26; a[5] += c; a[4] -= c << 26;
-  c = (a[8] + (1LL << 25)) >> 26; a[9] += c; a[8] -= c << 26;
-  c = (a[9] + (1LL << 24)) >> 25; a[0] += c * 19; a[9] -= c << 25;
-  c = (a[0] + (1LL << 25)) >> 26; a[1] += c; a[0] -= c << 26;
-#pragma unroll
-  for (int i = 0; i < 10; i++) h.v[i] = (int32_t)a[i];
+  c = a[0] >> 26; a[1] += c; a[0] &= m26;                    /* a0 stays biased */
+  c = a[4] >> 26; a[5] += c; a[4] &= m26;                    /* a4 stays biased */
+  c = a[1] >> 25; a[2] += c; h.v[1] = (int32_t)(a[1] & m25) - (1 << 24);
+  c = a[5] >> 25; a[6] += c; h.v[5] = (int32_t)(a[5] & m25) - (1 << 24);
+  c = a[2] >> 26; a[3] += c; h.v[2] = (int32_t)(a[2] & m26) - (1 << 25);
+  c = a[6] >> 26; a[7] += c; h.v[6] = (int32_t)(a[6] & m26) - (1 << 25);
+  c = a[3] >> 25; a[4] += c; h.v[3] = (int32_t)(a[3] & m25) - (1 << 24);
+  c = a[7] >> 25; a[8] += c; h.v[7] = (int32_t)(a[7] & m25) - (1 << 24);
+  c = a[4] >> 26; h.v[5] += (int32_t)c; h.v[4] = (int32_t)(a[4] & m26) - (1 << 25);
+  c = a[8] >> 26; a[9] += c; h.v[8] = (int32_t)(a[8] & m26) - (1 << 25);
+  c = a[9] >> 25; a[0] += c * 19; h.v[9] = (int32_t)(a[9] & m25) - (1 << 24);
+  c = a[0] >> 26; h.v[1] += (int32_t)c; h.v[0] = (int32_t)(a[0] & m26) - (1 << 25);
 }
 
 /* h = f*g.  Term (i,j) lands in column (i+j) mod 10; it is doubled when i
@@ -99,7 +106,7 @@ FD_DEV void fe_carry_wide(fe& h, int64_t (&a)[10]) {
 FD_DEV void fe_mul(fe& h, const fe& f, const fe& g) {
   int64_t a[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) a[k] = 0;
+  for (int k = 0; k < 10; k++) a[k] = FE_BIAS(k);
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -118,7 +125,7 @@ FD_DEV void fe_mul(fe& h, const fe& f, const fe& g) {
 FD_DEV void fe_sq(fe& h, const fe& f) {
   int64_t a[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) a[k] = 0;
+  for (int k = 0; k < 10; k++) a[k] = FE_BIAS(k);
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -137,7 +144,7 @@ FD_DEV void fe_sq(fe& h, const fe& f) {
 FD_DEV void fe_sq2(fe& h, const fe& f) {
   int64_t a[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) a[k] = 0;
+  for (int k = 0; k < 10; k++) a[k] = FE_BIAS(k);
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -156,7 +163,7 @@ FD_DEV void fe_sq2(fe& h, const fe& f) {
 FD_DEV void fe_carry(fe& h, const fe& f) {
   int64_t a[10];
 #pragma unroll
-  for (int i = 0; i < 10; i++) a[i] = f.v[i];
+  for (int i = 0; i < 10; i++) a[i] = (int64_t)f.v[i] + FE_BIAS(i);
   fe_carry_wide(h, a);
 }
 
