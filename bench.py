@@ -122,6 +122,45 @@ def cpu_baseline(wl, gpu_codes, sample, reps):
             "verdicts_equal_gpu": bool(np.array_equal(out, gpu_codes[:n]))}
 
 
+def batch_latency(eng, wl, batch, iters):
+    """C5 (closed loop): `batch`-signature batches through the host-buffer
+    API (pack into pinned memory, H2D, hash/decode/dsm, D2H) one at a time;
+    per-batch wall latency percentiles."""
+    n = min(wl.n, batch * 64)
+    sizes = wl.sizes[:n].astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    np.cumsum(sizes[:-1], out=off[1:])
+    msgs = wl.msgs.download(np.uint8, max(int(sizes.sum()), 1))
+    sigs = wl.sigs.download(np.uint8, 64 * n).reshape(n, 64)
+    pubs = wl.pubs.download(np.uint8, 32 * n).reshape(n, 32)
+    expect = wl.expect.download(np.int8, n)
+    lat = []
+    ok = True
+    for it in range(iters):
+        s = (it * batch) % (n - batch + 1)
+        t = time.perf_counter()
+        out = eng.verify_host(msgs, off[s:s + batch], wl.sizes[s:s + batch], sigs[s:s + batch], pubs[s:s + batch])
+        lat.append(time.perf_counter() - t)
+        ok &= bool(np.array_equal(out, expect[s:s + batch]))
+    lat = np.array(lat[max(1, iters // 20):]) * 1e3  # drop warm-up calls
+    return {"batch": batch, "iters": len(lat), "p50_ms": float(np.percentile(lat, 50)),
+            "p99_ms": float(np.percentile(lat, 99)), "mean_ms": float(lat.mean()),
+            "verifies_per_s_closed_loop": batch / (lat.mean() * 1e-3), "verdicts_ok": ok,
+            "mode": "closed loop, one batch in flight, host buffers (pinned staging + H2D + kernels + D2H)"}
+
+
+def pmc_traffic(n):
+    """HBM bytes per dsm launch from the committed PMC summary (rocprofv3
+    FETCH_SIZE + WRITE_SIZE passes, tools/pmc_summary.py), scaled to n."""
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(path))["fd_ed25519_dsm_kernel"]
+        per_sig = d["hbm_read_bytes_per_signature"] + d["hbm_write_bytes_per_signature"]
+        return per_sig * n, os.path.relpath(path, REPO)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -133,6 +172,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=262144)
     ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--latency-batch", type=int, default=256)
+    ap.add_argument("--latency-iters", type=int, default=400)
     args = ap.parse_args()
 
     rank, local, world = dist_setup(args.gpus)
@@ -140,7 +181,8 @@ def main():
 
     cfg = dict(workload.CONFIGS[args.config])
     n = args.n or cfg["n"]
-    eng = ed25519.Engine(device=local, max_chunk=min(n, 1 << 20))
+    ndev = max(ed25519.device_count(), 1)
+    eng = ed25519.Engine(device=local % ndev, max_chunk=min(n, 1 << 20))
     info = eng.info()
     log(f"[rank {rank}] engine {info}")
 
@@ -195,6 +237,10 @@ def main():
             cpu = cpu_baseline(wl, out, args.cpu_sample, args.cpu_reps)
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"cpu baseline failed: {ex!r}")
+    lat = None
+    if rank == 0 and args.latency_iters > 0:
+        lat = batch_latency(eng, wl, args.latency_batch, args.latency_iters)
+    traffic, traffic_src = pmc_traffic(n)
 
     if rank == 0:
         line = {
@@ -217,13 +263,16 @@ def main():
                        "codes": "reference AVX-512 backend"},
             "roofline": {"bound": "valu-int32", "kernel": "fd_ed25519_dsm_kernel",
                          "achieved": achieved, "peak": peak, "unit": "TOPS",
-                         "frac": (achieved / peak) if achieved else None, "traffic": None,
+                         "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+                         "traffic_unit": "bytes per launch (HBM read+write, rocprofv3 FETCH_SIZE+WRITE_SIZE)",
+                         "traffic_source": traffic_src,
                          "ops_per_launch": dsm_ops, "launch_ms": per_launch["dsm"],
                          "path": {"achieved": path_achieved, "frac": (path_achieved / peak) if path_achieved else None,
                                   "ops_per_verify_mean": path_ops / n, "ms_per_launch": path_ms}},
             "kernel_ms_per_launch": per_launch,
             "cpu_baseline": cpu,
             "gpu_over_cpu": (value / cpu["value"]) if cpu else None,
+            "batch_latency": lat,
             "verdicts_match_reference_labels": mism_all == 0,
             "verdict_mismatches": mism_all,
             "invalid_fraction": float((expect != 0).mean()),

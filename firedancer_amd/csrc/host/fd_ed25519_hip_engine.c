@@ -126,10 +126,10 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   hipDeviceProp_t prop;
   HIPCHK( hipGetDeviceProperties( &prop, device ), "hipGetDeviceProperties" );
   e->cu_cnt = prop.multiProcessorCount;
-  strncpy( e->arch, prop.gcnArchName, sizeof(e->arch)-1 );
+  snprintf( e->arch, sizeof(e->arch), "%.63s", prop.gcnArchName );
   if( strncmp( prop.gcnArchName, "gfx950", 6 ) ) {
     snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf),
-              "device %d is %s; libfd_ed25519_hip is built for gfx950 only", device, prop.gcnArchName );
+              "device %d is %.63s; libfd_ed25519_hip is built for gfx950 only", device, prop.gcnArchName );
     return FD_ED25519_HIP_ERR_INVAL;
   }
   HIPCHK( hipStreamCreateWithFlags( &e->stream, hipStreamNonBlocking ), "hipStreamCreate" );
@@ -307,6 +307,13 @@ fd_ed25519_hip_device_clock_mhz( fd_ed25519_hip_engine_t * e ) {
   hipDeviceProp_t prop;
   if( hipGetDeviceProperties( &prop, e->device )!=hipSuccess ) return 0;
   return prop.clockRate / 1000;
+}
+
+int
+fd_ed25519_hip_device_count( void ) {
+  int n = 0;
+  if( hipGetDeviceCount( &n )!=hipSuccess ) return 0;
+  return n;
 }
 
 int

@@ -289,3 +289,11 @@ class DeviceWorkload:
     def free(self):
         for b in (self.msgs, self.off, self.sz, self.sigs, self.pubs, self.out, self.expect, self.cls):
             b.free()
+
+
+_lib.fd_ed25519_hip_device_count.restype = ctypes.c_int
+
+
+def device_count():
+    """Visible HIP devices, from the library's own runtime."""
+    return _lib.fd_ed25519_hip_device_count()

@@ -241,7 +241,7 @@ int
 fd_ed25519_hip_engine_timing( fd_ed25519_hip_engine_t * engine, int enable );
 
 int
-fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * engine, double phase_ms[ 3 ], unsigned long * launches );
+fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * engine, double * phase_ms /* [3] */, unsigned long * launches );
 
 /* Device memory from the engine's HIP runtime (so callers need not link a
    second runtime).  memcpy is synchronous on the engine's stream. */
@@ -257,6 +257,10 @@ fd_ed25519_hip_dev_free( fd_ed25519_hip_engine_t * engine, void * ptr );
 
 int
 fd_ed25519_hip_memcpy( fd_ed25519_hip_engine_t * engine, void * dst, void const * src, unsigned long bytes, int dir );
+
+/* Number of visible HIP devices (0 if none / no driver). */
+int
+fd_ed25519_hip_device_count( void );
 
 /* Peak shader clock of the engine's device in MHz (hipDeviceProp clockRate). */
 int
