@@ -25,9 +25,18 @@ extern "C" {
 #define FD_ED25519_ATAB_BYTES_PER_WAVE (9UL * 10UL * 64UL * 16UL)
 
 #define FD_ED25519_VERIFY_BLOCK 256
+/* Occupancy targets (waves per SIMD) of the phase kernels; each caps the
+   kernel's register allocation (512 / waves VGPRs). */
 #ifndef FD_ED25519_DSM_WAVES_PER_SIMD
 #define FD_ED25519_DSM_WAVES_PER_SIMD 2
 #endif
+#ifndef FD_ED25519_HASH_WAVES_PER_SIMD
+#define FD_ED25519_HASH_WAVES_PER_SIMD 2  /* measured: 2 (200 VGPR, no spill) beats 3 (spills) */
+#endif
+#ifndef FD_ED25519_DECODE_WAVES_PER_SIMD
+#define FD_ED25519_DECODE_WAVES_PER_SIMD 2
+#endif
+#define FD_ED25519_SORT_BUCKETS 64
 
 /* Work arrays handed between the phase kernels, per signature of a chunk
    (SoA, [field][cap] so every access is one coalesced dword per lane):
@@ -36,7 +45,7 @@ extern "C" {
      pflag  [2][cap]     u8   per point (A, R): bit0 decode failure, bit1 small order
      pts    [2][20][cap] i32  per point: x (10 limbs), y (10 limbs), radix 2^25.5
    FD_ED25519_WORK_BYTES_PER_SIG bytes per signature of capacity. */
-#define FD_ED25519_WORK_BYTES_PER_SIG (8UL * 4UL + 1UL + 2UL + 2UL * 20UL * 4UL)
+#define FD_ED25519_WORK_BYTES_PER_SIG (8UL * 4UL + 1UL + 2UL + 2UL * 20UL * 4UL + 4UL)
 
 typedef struct {
   /* inputs (signature i = base + j for chunk-local j in [0,n)) */
@@ -53,6 +62,8 @@ typedef struct {
   uint8_t *        sflag;
   uint8_t *        pflag;
   int32_t *        pts;
+  uint32_t *       perm;     /* [cap] hash order (length-sorted), NULL: identity */
+  uint32_t *       hist;     /* [2*SORT_BUCKETS] counting-sort scratch          */
   uint64_t         cap;
   int32_t const *  btab;     /* device base-point table (FD_ED25519_BTAB_INTS) */
   void *           atab;     /* device scratch, waves * ATAB_BYTES_PER_WAVE    */

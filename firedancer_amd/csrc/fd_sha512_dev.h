@@ -8,11 +8,10 @@
    blocks for a message of sz bytes.
 
    Message bytes are read straight from the SoA message buffer in HBM with
-   32-bit loads from the enclosing aligned dword (any byte offset is
-   accepted) and realigned in registers (v_alignbyte_b32).  A lane never
-   loads a dword that holds none of its own message bytes, so the buffer
-   needs no padding.  Padding (0x80, zeros, 128-bit length) is synthesized
-   in registers. */
+   dword-aligned 16-byte loads (any message byte offset is accepted) and
+   realigned in registers (v_alignbyte_b32); the next block's loads are in
+   flight while the current block is compressed.  Padding (0x80, zeros,
+   128-bit length) is synthesized in registers. */
 #pragma once
 #include "fd25519_fe.h"
 
@@ -68,20 +67,28 @@ FD_DEV void sha512_block(uint64_t (&h)[8], uint64_t (&w)[16]) {
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
 
-/* Message dword at message byte position p (p % 4 == 0, may be >= sz),
-   padded: bytes >= sz are zero except byte sz = 0x80.  Returned in memory
-   (little-endian) byte order. */
+/* A lane's message: base is the aligned dword holding message byte 0,
+   which is byte `shift` of it. */
 struct sha_msg_src {
-  const uint32_t* base;  /* aligned dword containing message byte 0 */
-  uint32_t shift;        /* message byte 0 is byte `shift` of base[0] */
+  const uint32_t* base;
+  uint32_t shift;
   uint32_t sz;
 };
 
-FD_DEV uint32_t sha_raw_dword(const sha_msg_src& m, int j) {
-  /* load only dwords holding at least one message byte */
-  return (4u * (uint32_t)j < m.shift + m.sz) ? __builtin_nontemporal_load(m.base + j) : 0u;
+/* 16-byte load of base dwords [j, j+4); skipped (zero) unless it holds a
+   message byte.  Dword-aligned global_load_dwordx4 (gfx950 unaligned mode).
+   A chunk that holds the last message byte may read up to 15 bytes past
+   the message; callers keep message buffers readable that far (the
+   engine's staging and generator buffers are padded). */
+FD_DEV uint4 sha_chunk(const sha_msg_src& m, int j) {
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (j >= 0 && 4u * (uint32_t)j < m.shift + m.sz) __builtin_memcpy(&v, m.base + j, 16);
+  return v;
 }
 
+/* Message dword at message byte position p (p % 4 == 0), from the two base
+   dwords covering it, padded: bytes >= sz are zero except byte sz = 0x80.
+   Little-endian (memory) byte order. */
 FD_DEV uint32_t sha_msg_dword(const sha_msg_src& m, int p, uint32_t lo, uint32_t hi) {
   uint32_t d = __builtin_amdgcn_alignbyte(hi, lo, m.shift);
   const int n = (int)m.sz - p;
@@ -90,48 +97,78 @@ FD_DEV uint32_t sha_msg_dword(const sha_msg_src& m, int p, uint32_t lo, uint32_t
   return (d & keep) | pad;
 }
 
+#define SHA_CHUNKS 9  /* 36 dwords cover a 128-byte block at any byte shift */
+
+FD_DEV void sha_load_block(uint4 (&c)[SHA_CHUNKS], const sha_msg_src& m, int j0) {
+#pragma unroll
+  for (int q = 0; q < SHA_CHUNKS; q++) c[q] = sha_chunk(m, j0 + 4 * q);
+}
+
+FD_DEV uint32_t sha_chunk_dword(const uint4 (&c)[SHA_CHUNKS], int i) {
+  const uint4 v = c[i >> 2];
+  return (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
+}
+
 /* digest (as 16 little-endian words of the 64-byte output) of
    PRE || M(sz), where PRE is NPRE 32-bit words (8: a 32-byte prefix, e.g.
    the signing nonce prefix; 16: R || A) held in registers as little-endian
-   words. */
+   words.  Block b covers stream dwords [32 b, 32 b + 32), i.e. message
+   dwords from j0 = 32 b - NPRE; its 9 chunk loads are issued before the
+   previous block is compressed, so the load latency hides under 80 rounds. */
+/* Message schedule words of block b from its chunks (and, for the first
+   block, the register prefix), with padding and the length in the last. */
+template <int NPRE, bool FIRST>
+FD_DEV void sha_build_w(uint64_t (&w)[16], const uint4 (&c)[SHA_CHUNKS], const uint32_t (&pre)[NPRE],
+                        const sha_msg_src& m, uint32_t b, uint32_t nblk, uint64_t bitlen) {
+  constexpr int PB = 4 * NPRE;
+  constexpr int PW = NPRE / 2;
+  const int p0 = 128 * (int)b - PB;  /* message byte position of word 0 */
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    uint32_t d0, d1;
+    if (FIRST && t < PW) {
+      d0 = pre[2 * t];
+      d1 = pre[2 * t + 1];
+    } else {
+      const int p = p0 + 8 * t;
+      d0 = sha_msg_dword(m, p, sha_chunk_dword(c, 2 * t), sha_chunk_dword(c, 2 * t + 1));
+      d1 = sha_msg_dword(m, p + 4, sha_chunk_dword(c, 2 * t + 1), sha_chunk_dword(c, 2 * t + 2));
+    }
+    uint64_t word = ((uint64_t)bswap32(d0) << 32) | (uint64_t)bswap32(d1);
+    if (b + 1 == nblk) {
+      if (t == 14) word = 0;
+      if (t == 15) word = bitlen;
+    }
+    w[t] = word;
+  }
+}
+
+/* digest (as 16 little-endian words of the 64-byte output) of
+   PRE || M(sz), where PRE is NPRE 32-bit words (8: a 32-byte prefix, e.g.
+   the signing nonce prefix; 16: R || A) held in registers as little-endian
+   words.  Block b covers stream dwords [32 b, 32 b + 32), i.e. message
+   dwords from j0 = 32 b - NPRE.  Once a block's schedule is built, its chunk
+   registers receive the next block's loads, in flight during the 80
+   rounds.  The first block (prefix + message head) is peeled so the prefix
+   registers die before the loop. */
 template <int NPRE>
 FD_DEV void sha512_pre(uint32_t (&out)[16], const uint32_t (&pre)[NPRE], const sha_msg_src& m) {
   static_assert(NPRE == 8 || NPRE == 16, "prefix is 32 or 64 bytes");
   constexpr int PB = 4 * NPRE;   /* prefix bytes */
-  constexpr int PW = NPRE / 2;   /* prefix 64-bit words */
   uint64_t h[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
                    0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
                    0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
   const uint32_t nblk = (m.sz + PB + 17u + 127u) >> 7;
   const uint64_t bitlen = (uint64_t)(PB + m.sz) << 3;
-  for (uint32_t b = 0; b < nblk; b++) {
-    uint64_t w[16];
-    /* message byte position of word t is 128 b + 8 t - PB */
-    const int p0 = 128 * (int)b - PB;
-    const int j0 = (p0 >> 2);
-    uint32_t prev = sha_raw_dword(m, j0 < 0 ? 0 : j0);
-#pragma unroll
-    for (int t = 0; t < 16; t++) {
-      const int p = p0 + 8 * t;
-      uint32_t d0, d1;
-      if (t < PW && b == 0) {
-        d0 = pre[2 * t];
-        d1 = pre[2 * t + 1];
-      } else {
-        const int j = p >> 2;
-        const uint32_t l1 = sha_raw_dword(m, j + 1);
-        const uint32_t l2 = sha_raw_dword(m, j + 2);
-        d0 = sha_msg_dword(m, p, prev, l1);
-        d1 = sha_msg_dword(m, p + 4, l1, l2);
-        prev = l2;
-      }
-      uint64_t word = ((uint64_t)bswap32(d0) << 32) | (uint64_t)bswap32(d1);
-      if (b + 1 == nblk) {
-        if (t == 14) word = 0;
-        if (t == 15) word = bitlen;
-      }
-      w[t] = word;
-    }
+  uint4 cur[SHA_CHUNKS];
+  uint64_t w[16];
+  sha_load_block(cur, m, -NPRE);
+  sha_build_w<NPRE, true>(w, cur, pre, m, 0u, nblk, bitlen);
+  if (nblk > 1) sha_load_block(cur, m, 32 - NPRE);
+  sha512_block(h, w);
+  for (uint32_t b = 1; b < nblk; b++) {
+    sha_build_w<NPRE, false>(w, cur, pre, m, b, nblk, bitlen);
+    if (b + 1 < nblk) sha_load_block(cur, m, 32 * (int)(b + 1) - NPRE);
     sha512_block(h, w);
   }
 #pragma unroll

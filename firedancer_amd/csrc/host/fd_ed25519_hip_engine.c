@@ -44,6 +44,9 @@ struct fd_ed25519_hip_engine {
   uint8_t *    d_sflag;
   uint8_t *    d_pflag;
   int32_t *    d_pts;
+  uint32_t *   d_perm;       /* hash order (length-sorted) */
+  uint32_t *   d_hist;       /* counting-sort scratch      */
+  int          sort;         /* sort the hash phase by SHA-512 block count */
 
   /* host-API staging (pinned host + device mirrors), grown on demand */
   uint64_t     st_sig_cap;   /* signatures */
@@ -151,8 +154,13 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   uint8_t * w = e->d_work;
   e->d_k     = (uint32_t *)w; w += 8UL*4UL*c;
   e->d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
+  e->d_perm  = (uint32_t *)w; w += 4UL*c;
   e->d_sflag = w;             w += c;
   e->d_pflag = w;             w += 2UL*c;
+  w = (uint8_t *)(((uintptr_t)w + 255UL) & ~(uintptr_t)255UL);
+  e->d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words inside the 1024-byte slack */
+  char const * ns = getenv( "FD_ED25519_HIP_NOSORT" );
+  e->sort = !(ns && ns[0]=='1');
 
   int err = fd_ed25519_hip_launch_gen_btab( e->d_btab, e->stream );
   if( err ) return hip_fail( (hipError_t)err, "gen_btab launch" );
@@ -215,6 +223,7 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz;
   p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
   p.k = e->d_k; p.sflag = e->d_sflag; p.pflag = e->d_pflag; p.pts = e->d_pts; p.cap = e->max_chunk;
+  p.perm = e->sort ? e->d_perm : NULL; p.hist = e->d_hist;
   p.btab = e->d_btab; p.atab = e->d_atab;
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   for( uint64_t base=0UL; base<n; base+=e->max_chunk ) {
