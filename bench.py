@@ -169,8 +169,8 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--n", type=int, default=0, help="signatures per GPU (default: the config's)")
     ap.add_argument("--seed", type=int, default=0x5EED)
-    ap.add_argument("--cpu-sample", type=int, default=262144)
-    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=1048576)
+    ap.add_argument("--cpu-reps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-batch", type=int, default=256)
     ap.add_argument("--latency-iters", type=int, default=400)
