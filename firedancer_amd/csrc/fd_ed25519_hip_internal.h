@@ -40,12 +40,23 @@ extern "C" {
 
 /* Work arrays handed between the phase kernels, per signature of a chunk
    (SoA, [field][cap] so every access is one coalesced dword per lane):
-     k      [8][cap]     u32  k = SHA-512(R||A||M) mod L
-     sflag  [cap]        u8   S < L
-     pflag  [2][cap]     u8   per point (A, R): bit0 decode failure, bit1 small order
-     pts    [2][20][cap] i32  per point: x (10 limbs), y (10 limbs), radix 2^25.5
+     k        [8][cap]   u32  k = SHA-512(R||A||M) mod L
+     sflag    [cap]      u8   S < L
+     pflag    [cap]      u8   A: bit0 decode failure, bit1 small order
+     pts      [20][cap]  i32  A: x (10 limbs), y (10 limbs), radix 2^25.5
+     proj     [30][cap]  i32  R' = [k](-A) + [S]B projective (X, Y, Z)
+     st       [cap]      i8   dsm status: a decided code (< 0), FD_ST_CHECK or FD_ST_ASMALL
+     perm     [cap]      u32  hash order (length-sorted)
+     fix_list [cap]      u32  signatures whose R must be decoded (fin -> rfix)
    FD_ED25519_WORK_BYTES_PER_SIG bytes per signature of capacity. */
-#define FD_ED25519_WORK_BYTES_PER_SIG (8UL * 4UL + 1UL + 2UL + 2UL * 20UL * 4UL + 4UL)
+#define FD_ED25519_WORK_BYTES_PER_SIG (8UL * 4UL + 1UL + 1UL + 20UL * 4UL + 30UL * 4UL + 1UL + 4UL + 4UL)
+
+/* dsm status values besides the decided (negative) codes */
+#define FD_ST_CHECK  1  /* compare R' with R's encoding                         */
+#define FD_ST_ASMALL 2  /* A small order: ERR_PUBKEY unless R fails to decode */
+
+/* fin: signatures per lane of the batched inversion (Montgomery's trick) */
+#define FD_ED25519_FIN_M 8
 
 typedef struct {
   /* inputs (signature i = base + j for chunk-local j in [0,n)) */
@@ -62,6 +73,10 @@ typedef struct {
   uint8_t *        sflag;
   uint8_t *        pflag;
   int32_t *        pts;
+  int32_t *        proj;
+  int8_t *         st;
+  uint32_t *       fix_list;
+  uint32_t *       fix_cnt;  /* 1 word: entries of fix_list                   */
   uint32_t *       perm;     /* [cap] hash order (length-sorted), NULL: identity */
   uint32_t *       hist;     /* [2*SORT_BUCKETS] counting-sort scratch          */
   uint64_t         cap;
@@ -81,7 +96,8 @@ int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t
 #define FD_ED25519_PHASE_HASH   0
 #define FD_ED25519_PHASE_DECODE 1
 #define FD_ED25519_PHASE_DSM    2
-#define FD_ED25519_PHASE_CNT    3
+#define FD_ED25519_PHASE_FIN    3
+#define FD_ED25519_PHASE_CNT    4
 int fd_ed25519_hip_launch_phase( fd_ed25519_verify_params_t const * p, int phase, uint32_t grid, void * stream );
 int fd_ed25519_hip_verify_occupancy( int * blocks_per_cu );
 

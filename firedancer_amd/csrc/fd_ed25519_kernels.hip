@@ -120,56 +120,63 @@ fd_ed25519_hash_kernel(fd_ed25519_verify_params_t p) {
   p.sflag[j] = sc_is_canonical(S) ? 1 : 0;
 }
 
+/* One lane per public key A: decompression with the reference's acceptance
+   rules and the small-order test.  R is never decompressed on the common
+   path: fin compares the encoding of R' = [k](-A) + [S]B with R's bytes
+   (see fd_ed25519_fin_kernel). */
 __global__ void __launch_bounds__(256, FD_ED25519_DECODE_WAVES_PER_SIMD)
 fd_ed25519_decode_kernel(fd_ed25519_verify_params_t p) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * p.n) return;
-  const int which = t >= p.n;           /* 0: A (public key), 1: R */
-  const uint64_t j = which ? t - p.n : t;
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p.n) return;
   const uint64_t i = p.base + j;
   uint32_t s[8];
   {
-    const uint4* src = which ? reinterpret_cast<const uint4*>(p.sigs + 64 * i)
-                             : reinterpret_cast<const uint4*>(p.pubs + 32 * i);
+    const uint4* src = reinterpret_cast<const uint4*>(p.pubs + 32 * i);
     const uint4 q0 = src[0], q1 = src[1];
     s[0] = q0.x; s[1] = q0.y; s[2] = q0.z; s[3] = q0.w; s[4] = q1.x; s[5] = q1.y; s[6] = q1.z; s[7] = q1.w;
   }
   decoded_pt d;
   ge_decode(d, s, !p.codes_portable);
-  int32_t* dst = p.pts + (uint64_t)which * 20 * p.cap + j;
+  int32_t* dst = p.pts + j;
 #pragma unroll
   for (int l = 0; l < 10; l++) {
     dst[(uint64_t)l * p.cap] = d.x.v[l];
     dst[(uint64_t)(10 + l) * p.cap] = d.y.v[l];
   }
-  p.pflag[(uint64_t)which * p.cap + j] = (uint8_t)((d.fail ? FD_PF_FAIL : 0u) | (d.small ? FD_PF_SMALL : 0u));
+  p.pflag[j] = (uint8_t)((d.fail ? FD_PF_FAIL : 0u) | (d.small ? FD_PF_SMALL : 0u));
 }
 
-FD_DEV void load_pt(fe& x, fe& y, const fd_ed25519_verify_params_t& p, int which, uint64_t j) {
-  const int32_t* src = p.pts + (uint64_t)which * 20 * p.cap + j;
+FD_DEV void load_fe(fe& x, const int32_t* src, uint64_t cap) {
 #pragma unroll
-  for (int l = 0; l < 10; l++) {
-    x.v[l] = src[(uint64_t)l * p.cap];
-    y.v[l] = src[(uint64_t)(10 + l) * p.cap];
-  }
+  for (int l = 0; l < 10; l++) x.v[l] = src[(uint64_t)l * cap];
 }
 
-FD_DEV int dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_tab, const int4* s_btab) {
+FD_DEV void store_fe(int32_t* dst, uint64_t cap, const fe& x) {
+#pragma unroll
+  for (int l = 0; l < 10; l++) dst[(uint64_t)l * cap] = x.v[l];
+}
+
+/* R' = [k](-A) + [S]B for signature j, written to proj as (X:Y:Z), plus the
+   status that fin finishes.  The reference's checks in order
+   (fd_ed25519_user.c:134-229): S < L, A and R decode (an undecodable A is
+   ERR_SIG with AVX-512 codes, ERR_PUBKEY with portable ones; R: ERR_SIG),
+   A small order (ERR_PUBKEY), R small order (ERR_SIG), the group equation
+   (ERR_MSG).  Here S and A are decided; everything about R is left to fin. */
+FD_DEV void dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_tab, const int4* s_btab) {
   const uint64_t i = p.base + j;
   const uint32_t s_ok = p.sflag[j];
-  const uint32_t af = p.pflag[j], rf = p.pflag[p.cap + j];
-  int code;
-  if (!s_ok) code = FD_ED25519_ERR_SIG;
-  else if (af & FD_PF_FAIL) code = p.codes_portable ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;
-  else if (rf & FD_PF_FAIL) code = FD_ED25519_ERR_SIG;
-  else if (af & FD_PF_SMALL) code = FD_ED25519_ERR_PUBKEY;
-  else if (rf & FD_PF_SMALL) code = FD_ED25519_ERR_SIG;
-  else code = FD_ED25519_SUCCESS;  /* pending the group equation */
+  const uint32_t af = p.pflag[j];
+  int st;
+  if (!s_ok) st = FD_ED25519_ERR_SIG;
+  else if (af & FD_PF_FAIL) st = p.codes_portable ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;
+  else if (af & FD_PF_SMALL) st = FD_ST_ASMALL;
+  else st = FD_ST_CHECK;
 
   /* table [0..8](-A), cached form, in this lane's HBM slot */
   {
     fe ax, ay;
-    load_pt(ax, ay, p, 0, j);
+    load_fe(ax, p.pts + j, p.cap);
+    load_fe(ay, p.pts + 10 * p.cap + j, p.cap);
     ge_p3 nA;
     fe_neg(nA.X, ax);
     nA.Y = ay;
@@ -243,16 +250,19 @@ FD_DEV int dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_t
     ge_p1p1_to_p2(Q, Rt);
   }
 
-  /* R' == R with R.Z = 1: X' == x_R Z' and Y' == y_R Z' */
-  fe rx, ry, t1, t2;
-  load_pt(rx, ry, p, 1, j);
-  fe_mul(t1, rx, Q.Z);
-  fe_sub(t1, t1, Q.X);
-  fe_mul(t2, ry, Q.Z);
-  fe_sub(t2, t2, Q.Y);
-  const bool eq = fe_iszero(t1) && fe_iszero(t2);
-  if (code == FD_ED25519_SUCCESS && !eq) code = FD_ED25519_ERR_MSG;
-  return code;
+  /* A decided lane publishes Z = 1 so that it cannot zero fin's batched
+     inversion (an undecodable A is not a curve point, so its R' is not
+     either).  For a curve point the complete formulas never give Z = 0. */
+  if (st < 0) {
+    fe_0(Q.X);
+    fe_1(Q.Y);
+    fe_1(Q.Z);
+  }
+  int32_t* dst = p.proj + j;
+  store_fe(dst, p.cap, Q.X);
+  store_fe(dst + 10 * p.cap, p.cap, Q.Y);
+  store_fe(dst + 20 * p.cap, p.cap, Q.Z);
+  p.st[j] = (int8_t)st;
 }
 
 __global__ void __launch_bounds__(FD_ED25519_VERIFY_BLOCK, FD_ED25519_DSM_WAVES_PER_SIMD)
@@ -266,7 +276,156 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   int4* lane_tab = reinterpret_cast<int4*>(static_cast<char*>(p.atab) +
                                            (gtid >> 6) * FD_ED25519_ATAB_BYTES_PER_WAVE) + (threadIdx.x & 63) * 90;
-  for (uint64_t j = gtid; j < p.n; j += stride) p.out[p.base + j] = (int8_t)dsm_one(p, j, lane_tab, s_btab);
+  for (uint64_t j = gtid; j < p.n; j += stride) dsm_one(p, j, lane_tab, s_btab);
+}
+
+/* ------------------------------------------------------------------------
+   fin: the group equation without decompressing R.
+
+   The reference decodes R (a square root, ~265 field operations) and tests
+   R' == R projectively (fd_ed25519_point_eq_z1).  Equivalently: R decodes
+   to R' exactly when R's bytes are the encoding of R' with y taken mod p
+   (decoding y gives x up to sign; R' on the curve proves the root exists;
+   the sign bit picks x's parity -- x = 0 with the sign bit set never
+   matches, which is the AVX-512 decoder's rejection).  So each signature
+   needs R' in affine form, and the inversions are batched per lane with
+   Montgomery's trick: FIN_M signatures share one inversion (3 (M-1)
+   multiplications + 1 inversion instead of M inversions).
+
+   If the encodings match, R is decodable and equal to R': the verdict is
+   ERR_SIG if R has small order (y in {0, 1, -1, y0, y1} -- x = 0 iff
+   y = +-1 on the curve) and SUCCESS otherwise.  Otherwise -- and whenever A
+   has small order, where the verdict depends on whether R decodes -- the
+   signature goes to fix_list and rfix decodes R the reference's way.  Only
+   invalid signatures take that path. */
+
+FD_DEV bool r_encoding_small(const uint32_t (&y)[8]) {
+  const uint32_t y0[8] = {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u,
+                          0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du};
+  const uint32_t y1[8] = {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du,
+                          0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u};
+  uint32_t hi = 0, e0 = 0, e1 = 0, ones = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    if (w) hi |= y[w];
+    e0 |= y[w] ^ y0[w];
+    e1 |= y[w] ^ y1[w];
+    if (w && w < 7) ones |= ~y[w];
+  }
+  const bool y01 = hi == 0u && y[0] <= 1u;                               /* 0, 1  */
+  const bool ym1 = ones == 0u && y[7] == 0x7fffffffu && y[0] == 0xffffffecu;  /* p - 1 */
+  return y01 || ym1 || e0 == 0u || e1 == 0u;
+}
+
+__global__ void __launch_bounds__(256)
+fd_ed25519_fin_kernel(fd_ed25519_verify_params_t p) {
+  constexpr int M = FD_ED25519_FIN_M;
+  const uint64_t lanes = (p.n + M - 1) / M;
+  const uint64_t L = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (L >= lanes) return;
+  const int32_t* PX = p.proj;
+  const int32_t* PY = p.proj + 10 * p.cap;
+  const int32_t* PZ = p.proj + 20 * p.cap;
+
+  fe pre[M];  /* prefix products of Z */
+#pragma unroll
+  for (int t = 0; t < M; t++) {
+    const uint64_t j = L + (uint64_t)t * lanes;
+    fe z;
+    if (j < p.n) load_fe(z, PZ + j, p.cap);
+    else fe_1(z);
+    if (t == 0) pre[0] = z;
+    else fe_mul(pre[t], pre[t - 1], z);
+  }
+  fe inv;
+  fe_invert(inv, pre[M - 1]);
+
+#pragma unroll
+  for (int t = M - 1; t >= 0; t--) {
+    const uint64_t j = L + (uint64_t)t * lanes;
+    const bool live = j < p.n;
+    fe zi;
+    if (t > 0) {
+      fe_mul(zi, inv, pre[t - 1]);
+      fe z;
+      if (live) load_fe(z, PZ + j, p.cap);
+      else fe_1(z);
+      fe_mul(inv, inv, z);
+    } else {
+      zi = inv;
+    }
+    if (!live) continue;
+    const int st = p.st[j];
+    int code;
+    if (st < 0) {
+      code = st;
+    } else if (st == FD_ST_ASMALL) {
+      code = 1;  /* R decode needed */
+    } else {
+      fe x, y, X, Y;
+      load_fe(X, PX + j, p.cap);
+      load_fe(Y, PY + j, p.cap);
+      fe_mul(x, X, zi);
+      fe_mul(y, Y, zi);
+      uint32_t xb[8], yb[8], r[8];
+      fe_tobytes(xb, x);
+      fe_tobytes(yb, y);
+      {
+        const uint4* sg = reinterpret_cast<const uint4*>(p.sigs + 64 * (p.base + j));
+        const uint4 q0 = sg[0], q1 = sg[1];
+        r[0] = q0.x; r[1] = q0.y; r[2] = q0.z; r[3] = q0.w; r[4] = q1.x; r[5] = q1.y; r[6] = q1.z; r[7] = q1.w;
+      }
+      const uint32_t sign = r[7] >> 31;
+      r[7] &= 0x7fffffffu;
+      /* y >= p (only 2^255-19 .. 2^255-1) is taken mod p, as the decoder does */
+      uint32_t allf = 0xffffffffu;
+#pragma unroll
+      for (int w = 1; w < 7; w++) allf &= r[w];
+      const bool ge_p = allf == 0xffffffffu && r[7] == 0x7fffffffu && r[0] >= 0xffffffedu;
+      if (ge_p) {
+        r[0] -= 0xffffffedu;
+#pragma unroll
+        for (int w = 1; w < 8; w++) r[w] = 0u;
+      }
+      uint32_t diff = (xb[0] & 1u) ^ sign;
+#pragma unroll
+      for (int w = 0; w < 8; w++) diff |= yb[w] ^ r[w];
+      if (diff == 0u) code = r_encoding_small(yb) ? FD_ED25519_ERR_SIG : FD_ED25519_SUCCESS;
+      else code = 1;
+    }
+    if (code == 1) {
+      const uint32_t slot = atomicAdd(p.fix_cnt, 1u);
+      p.fix_list[slot] = (uint32_t)j;
+    } else {
+      p.out[p.base + j] = (int8_t)code;
+    }
+  }
+}
+
+/* rfix: decode R the reference's way for the signatures fin could not
+   settle (invalid ones, and those with a small-order A).  Persistent grid;
+   the list length is read on the device. */
+__global__ void __launch_bounds__(256, FD_ED25519_DECODE_WAVES_PER_SIMD)
+fd_ed25519_rfix_kernel(fd_ed25519_verify_params_t p) {
+  const uint32_t cnt = *p.fix_cnt;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < cnt;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t j = p.fix_list[t];
+    uint32_t s[8];
+    {
+      const uint4* sg = reinterpret_cast<const uint4*>(p.sigs + 64 * (p.base + j));
+      const uint4 q0 = sg[0], q1 = sg[1];
+      s[0] = q0.x; s[1] = q0.y; s[2] = q0.z; s[3] = q0.w; s[4] = q1.x; s[5] = q1.y; s[6] = q1.z; s[7] = q1.w;
+    }
+    decoded_pt d;
+    ge_decode(d, s, !p.codes_portable);
+    int code;
+    if (d.fail) code = FD_ED25519_ERR_SIG;
+    else if (p.st[j] == FD_ST_ASMALL) code = FD_ED25519_ERR_PUBKEY;
+    else if (d.small) code = FD_ED25519_ERR_SIG;
+    else code = FD_ED25519_ERR_MSG;  /* R decodes, is not small, and R' != R */
+    p.out[p.base + j] = (int8_t)code;
+  }
 }
 
 /* ------------------------------------------------------------------------
@@ -356,13 +515,20 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
     hipLaunchKernelGGL(fd_ed25519_hash_kernel, g, dim3(blk), 0, st, *p);
   } break;
   case FD_ED25519_PHASE_DECODE:
-    hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((2 * p->n + blk - 1) / blk)), dim3(blk), 0, st,
-                       *p);
+    hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
     break;
   case FD_ED25519_PHASE_DSM: {
     const uint64_t need = (p->n + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
     const uint32_t g = (uint32_t)(need < grid ? need : grid);
     hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
+  } break;
+  case FD_ED25519_PHASE_FIN: {
+    const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return (int)e;
+    const uint64_t lanes = (p->n + FD_ED25519_FIN_M - 1) / FD_ED25519_FIN_M;
+    hipLaunchKernelGGL(fd_ed25519_fin_kernel, dim3((uint32_t)((lanes + blk - 1) / blk)), dim3(blk), 0, st, *p);
+    const uint64_t need = (p->n + blk - 1) / blk;
+    hipLaunchKernelGGL(fd_ed25519_rfix_kernel, dim3((uint32_t)(need < 1024 ? need : 1024)), dim3(blk), 0, st, *p);
   } break;
   default:
     return (int)hipErrorInvalidValue;

@@ -26,6 +26,8 @@
 
 #define FD_ED25519_HIP_TIMING_MAX 256
 
+_Static_assert( FD_ED25519_HIP_PHASE_CNT==FD_ED25519_PHASE_CNT, "public and internal phase counts differ" );
+
 struct fd_ed25519_hip_engine {
   int          device;
   int          flags;
@@ -44,6 +46,9 @@ struct fd_ed25519_hip_engine {
   uint8_t *    d_sflag;
   uint8_t *    d_pflag;
   int32_t *    d_pts;
+  int32_t *    d_proj;       /* R' per signature (dsm -> fin) */
+  int8_t *     d_st;         /* dsm status per signature      */
+  uint32_t *   d_fix;        /* fin -> rfix list              */
   uint32_t *   d_perm;       /* hash order (length-sorted) */
   uint32_t *   d_hist;       /* counting-sort scratch      */
   int          sort;         /* sort the hash phase by SHA-512 block count */
@@ -153,12 +158,15 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   uint64_t c = e->max_chunk;
   uint8_t * w = e->d_work;
   e->d_k     = (uint32_t *)w; w += 8UL*4UL*c;
-  e->d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
+  e->d_pts   = (int32_t  *)w; w += 20UL*4UL*c;
+  e->d_proj  = (int32_t  *)w; w += 30UL*4UL*c;
   e->d_perm  = (uint32_t *)w; w += 4UL*c;
+  e->d_fix   = (uint32_t *)w; w += 4UL*c;
   e->d_sflag = w;             w += c;
-  e->d_pflag = w;             w += 2UL*c;
+  e->d_pflag = w;             w += c;
+  e->d_st    = (int8_t *)w;   w += c;
   w = (uint8_t *)(((uintptr_t)w + 255UL) & ~(uintptr_t)255UL);
-  e->d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words inside the 1024-byte slack */
+  e->d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words + fix count inside the 1024-byte slack */
   char const * ns = getenv( "FD_ED25519_HIP_NOSORT" );
   e->sort = !(ns && ns[0]=='1');
 
@@ -223,6 +231,7 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz;
   p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
   p.k = e->d_k; p.sflag = e->d_sflag; p.pflag = e->d_pflag; p.pts = e->d_pts; p.cap = e->max_chunk;
+  p.proj = e->d_proj; p.st = e->d_st; p.fix_list = e->d_fix; p.fix_cnt = e->d_hist + 2*FD_ED25519_SORT_BUCKETS;
   p.perm = e->sort ? e->d_perm : NULL; p.hist = e->d_hist;
   p.btab = e->d_btab; p.atab = e->d_atab;
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;

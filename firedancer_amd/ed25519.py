@@ -24,6 +24,9 @@ ERR_MSG = -3
 
 FLAG_CODES_PORTABLE = 1
 
+# phases of a verify launch (FD_ED25519_HIP_PHASE_CNT, include/fd_ed25519_hip.h)
+PHASES = ("hash", "decode", "dsm", "fin")
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FD_ED25519_HIP_LIB", os.path.join(_HERE, "_lib", "libfd_ed25519_hip.so"))
 
@@ -211,10 +214,10 @@ class Engine:
         _check(_lib.fd_ed25519_hip_engine_timing(self._h, 1 if enable else 0))
 
     def timing_read(self):
-        ms = (ctypes.c_double * 3)()
+        ms = (ctypes.c_double * len(PHASES))()
         cnt = ctypes.c_ulong(0)
         _check(_lib.fd_ed25519_hip_engine_timing_read(self._h, ms, ctypes.byref(cnt)))
-        return {"hash": ms[0], "decode": ms[1], "dsm": ms[2]}, cnt.value
+        return {name: ms[i] for i, name in enumerate(PHASES)}, cnt.value
 
     def clock_mhz(self):
         return _lib.fd_ed25519_hip_device_clock_mhz(self._h)

@@ -233,15 +233,18 @@ fd_ed25519_hip_corrupt_dev( fd_ed25519_hip_engine_t * engine,
 /* ---- Part 4: measurement and device-memory helpers ------------------ */
 
 /* Phase timing: while enabled, fd_ed25519_hip_verify_dev brackets each of
-   its phase kernels (0 hash, 1 decode, 2 dsm) with HIP events on the stream
+   its phases (0 hash, 1 decode, 2 dsm, 3 fin) with HIP events on the stream
    they run on (up to 256 chunk launches); _timing_read waits for them and
    returns the summed milliseconds per phase and the number of chunk
    launches, then resets.  Enabling resets too. */
+#define FD_ED25519_HIP_PHASE_CNT (4)
+
 int
 fd_ed25519_hip_engine_timing( fd_ed25519_hip_engine_t * engine, int enable );
 
 int
-fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * engine, double * phase_ms /* [3] */, unsigned long * launches );
+fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * engine,
+                                   double * phase_ms /* [FD_ED25519_HIP_PHASE_CNT] */, unsigned long * launches );
 
 /* Device memory from the engine's HIP runtime (so callers need not link a
    second runtime).  memcpy is synchronous on the engine's stream. */

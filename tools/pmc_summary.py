@@ -45,10 +45,9 @@ def main():
             d["hbm_read_bytes_x2_upper"] = per["FETCH_SIZE"] * 2048
         if "WRITE_SIZE" in per:
             d["hbm_write_bytes"] = per["WRITE_SIZE"] * 1024
-        if n and k in ("fd_ed25519_dsm_kernel", "fd_ed25519_hash_kernel"):
+        if n and k in ("fd_ed25519_dsm_kernel", "fd_ed25519_hash_kernel", "fd_ed25519_decode_kernel",
+                       "fd_ed25519_fin_kernel"):
             lanes = n
-        elif n and k == "fd_ed25519_decode_kernel":
-            lanes = 2 * n
         else:
             lanes = None
         if lanes:
