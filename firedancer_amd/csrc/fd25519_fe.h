@@ -79,6 +79,31 @@ FD_DEV void fe_select(fe& h, const fe& f, const fe& g, bool c) {
    shift and one 64-bit add, and the limb is (low bits) - bias. */
 #define FE_BIAS(k) (((k) & 1) ? (1LL << 24) : (1LL << 25))
 
+/* One 32x32->64 signed multiply-accumulate, v_mad_i64_i32, written as
+   inline asm so that LLVM cannot reassociate the column sums: left to
+   itself it moves the (constant) bias of every column to a separate 64-bit
+   add, one extra v_lshl_add_u64 per column and product.  fe_mad_init
+   starts a column with its bias as the addend (an SGPR pair).  The carry-out
+   SGPR pair the instruction writes is a dead scratch output.
+   FE_ASM_MAD=0 restores the plain C (for A/B builds). */
+#ifndef FE_ASM_MAD
+#define FE_ASM_MAD 1
+#endif
+
+FD_DEV void fe_mad(int64_t& acc, int32_t x, int32_t y) {
+  acc += (int64_t)x * y;
+#if FE_ASM_MAD
+  asm("" : "+v"(acc));
+#endif
+}
+
+FD_DEV void fe_mad_init(int64_t& acc, int32_t x, int32_t y, int k) {
+  acc = FE_BIAS(k) + (int64_t)x * y;
+#if FE_ASM_MAD
+  asm("" : "+v"(acc));
+#endif
+}
+
 /* Column sums a[k] (each pre-biased with FE_BIAS(k)) of a 10x10 product,
    reduced to tight centered limbs in two interleaved chains (limbs 4 and 0
    are carried twice; between their two carries they are kept in biased
@@ -106,15 +131,14 @@ FD_DEV void fe_carry_wide(fe& h, int64_t (&a)[10]) {
 FD_DEV void fe_mul(fe& h, const fe& f, const fe& g) {
   int64_t a[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) a[k] = FE_BIAS(k);
-#pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
     for (int j = 0; j < 10; j++) {
       const int k = i + j;
       const int32_t x = ((i & 1) && (j & 1)) ? 2 * f.v[i] : f.v[i];
       const int32_t y = (k >= 10) ? 19 * g.v[j] : g.v[j];
-      a[k >= 10 ? k - 10 : k] += (int64_t)x * y;
+      if (i == 0) fe_mad_init(a[k], x, y, k);
+      else fe_mad(a[k >= 10 ? k - 10 : k], x, y);
     }
   }
   fe_carry_wide(h, a);
@@ -125,8 +149,6 @@ FD_DEV void fe_mul(fe& h, const fe& f, const fe& g) {
 FD_DEV void fe_sq(fe& h, const fe& f) {
   int64_t a[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) a[k] = FE_BIAS(k);
-#pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
     for (int j = i; j < 10; j++) {
@@ -134,7 +156,8 @@ FD_DEV void fe_sq(fe& h, const fe& f) {
       const int m = (((i & 1) && (j & 1)) ? 2 : 1) * ((k >= 10) ? 19 : 1);
       const int32_t x = (i == j) ? f.v[i] : 2 * f.v[i];
       const int32_t y = m * f.v[j];
-      a[k >= 10 ? k - 10 : k] += (int64_t)x * y;
+      if (i == 0) fe_mad_init(a[k], x, y, k);
+      else fe_mad(a[k >= 10 ? k - 10 : k], x, y);
     }
   }
   fe_carry_wide(h, a);
@@ -144,8 +167,6 @@ FD_DEV void fe_sq(fe& h, const fe& f) {
 FD_DEV void fe_sq2(fe& h, const fe& f) {
   int64_t a[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) a[k] = FE_BIAS(k);
-#pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
     for (int j = i; j < 10; j++) {
@@ -153,7 +174,8 @@ FD_DEV void fe_sq2(fe& h, const fe& f) {
       const int m = (((i & 1) && (j & 1)) ? 2 : 1) * ((k >= 10) ? 19 : 1);
       const int32_t x = (i == j) ? 2 * f.v[i] : 4 * f.v[i];
       const int32_t y = m * f.v[j];
-      a[k >= 10 ? k - 10 : k] += (int64_t)x * y;
+      if (i == 0) fe_mad_init(a[k], x, y, k);
+      else fe_mad(a[k >= 10 ? k - 10 : k], x, y);
     }
   }
   fe_carry_wide(h, a);
