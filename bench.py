@@ -122,31 +122,34 @@ def cpu_baseline(wl, gpu_codes, sample, reps):
             "verdicts_equal_gpu": bool(np.array_equal(out, gpu_codes[:n]))}
 
 
-def batch_latency(eng, wl, batch, iters):
-    """C5 (closed loop): `batch`-signature batches through the host-buffer
-    API (pack into pinned memory, H2D, hash/decode/dsm, D2H) one at a time;
-    per-batch wall latency percentiles."""
-    n = min(wl.n, batch * 64)
-    sizes = wl.sizes[:n].astype(np.uint64)
-    off = np.zeros(n, np.uint64)
-    np.cumsum(sizes[:-1], out=off[1:])
-    msgs = wl.msgs.download(np.uint8, max(int(sizes.sum()), 1))
-    sigs = wl.sigs.download(np.uint8, 64 * n).reshape(n, 64)
-    pubs = wl.pubs.download(np.uint8, 32 * n).reshape(n, 32)
-    expect = wl.expect.download(np.int8, n)
-    lat = []
-    ok = True
-    for it in range(iters):
-        s = (it * batch) % (n - batch + 1)
-        t = time.perf_counter()
-        out = eng.verify_host(msgs, off[s:s + batch], wl.sizes[s:s + batch], sigs[s:s + batch], pubs[s:s + batch])
-        lat.append(time.perf_counter() - t)
-        ok &= bool(np.array_equal(out, expect[s:s + batch]))
-    lat = np.array(lat[max(1, iters // 20):]) * 1e3  # drop warm-up calls
-    return {"batch": batch, "iters": len(lat), "p50_ms": float(np.percentile(lat, 50)),
-            "p99_ms": float(np.percentile(lat, 99)), "mean_ms": float(lat.mean()),
-            "verifies_per_s_closed_loop": batch / (lat.mean() * 1e-3), "verdicts_ok": ok,
-            "mode": "closed loop, one batch in flight, host buffers (pinned staging + H2D + kernels + D2H)"}
+def latency_mode(eng, args, device):
+    """C5: the verify tile's latency mode.  Signed single-signer Solana
+    transactions (~200-byte messages, GPU-signed) are published into a
+    tango-style mcache/dcache ring by a producer thread at a fixed offered
+    load; the verify-tile core (fd_ed25519_hip_vtile: parse, dedup,
+    batch_single_msg verify) pulls them and submits batches of up to
+    `batch` signatures (sooner when the ring is drained and a slot is free).
+    Latency = due publish time -> verdict on the host.  Peak = the same
+    loop unpaced; then 50/80/95% of it."""
+    from firedancer_amd import tile, workload
+    n = args.latency_txns
+    pay, _ = workload.txn_payloads(eng, n, args.seed + 77, msg_sz=200)
+    lat, v, res = tile.latency_run(pay, 0.0, device=device, slot_cnt=args.latency_slots,
+                                   batch_sigs=args.latency_batch, ring_depth=4096)
+    peak = res["achieved_txn_per_s"]
+    out = {"batch_sigs": args.latency_batch, "slots_in_flight": args.latency_slots, "txns_per_run": n,
+           "msg_sz": 200, "peak_txn_per_s": peak, "ring": "tango-style mcache/dcache, depth 4096",
+           "verdicts_ok": bool((v == 0).all()), "loads": []}
+    for frac in (0.5, 0.8, 0.95):
+        lat, v, res = tile.latency_run(pay, frac * peak, device=device, slot_cnt=args.latency_slots,
+                                       batch_sigs=args.latency_batch, ring_depth=4096)
+        ms = lat * 1e3
+        out["loads"].append({"offered_frac_of_peak": frac, "offered_txn_per_s": res["offered_txn_per_s"],
+                             "achieved_txn_per_s": res["achieved_txn_per_s"], "p50_ms": float(np.percentile(ms, 50)),
+                             "p99_ms": float(np.percentile(ms, 99)), "max_ms": float(ms.max()),
+                             "batches": res["batches"], "ring_overruns": res["ring_overruns"]})
+        out["verdicts_ok"] &= bool((v == 0).all())
+    return out
 
 
 def pmc_traffic(n):
@@ -173,7 +176,8 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-batch", type=int, default=256)
-    ap.add_argument("--latency-iters", type=int, default=400)
+    ap.add_argument("--latency-slots", type=int, default=4)
+    ap.add_argument("--latency-txns", type=int, default=100000, help="0 disables the latency mode")
     args = ap.parse_args()
 
     rank, local, world = dist_setup(args.gpus)
@@ -238,8 +242,8 @@ def main():
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"cpu baseline failed: {ex!r}")
     lat = None
-    if rank == 0 and args.latency_iters > 0:
-        lat = batch_latency(eng, wl, args.latency_batch, args.latency_iters)
+    if rank == 0 and args.latency_txns > 0:
+        lat = latency_mode(eng, args, local % ndev)
     traffic, traffic_src = pmc_traffic(n)
 
     if rank == 0:
@@ -272,7 +276,7 @@ def main():
             "kernel_ms_per_launch": per_launch,
             "cpu_baseline": cpu,
             "gpu_over_cpu": (value / cpu["value"]) if cpu else None,
-            "batch_latency": lat,
+            "latency_mode": lat,
             "verdicts_match_reference_labels": mism_all == 0,
             "verdict_mismatches": mism_all,
             "invalid_fraction": float((expect != 0).mean()),

@@ -11,7 +11,7 @@
    allocation on the device-resident path):
      btab   129 x 36 int32            base-point table [0..128]B (LDS image)
      atab   dsm waves x 92160 B       per-lane [0..8](-A) tables
-     work   max_chunk x 195 B         k, flags and decoded points per signature
+     work   max_chunk x 243 B         k, flags, decoded A, R' and lists per signature
      in/out staging for the host API  grown on demand */
 
 #define _GNU_SOURCE
@@ -79,6 +79,12 @@ static __thread char fd_ed25519_hip_errbuf[ 256 ];
 char const *
 fd_ed25519_hip_last_error( void ) {
   return fd_ed25519_hip_errbuf;
+}
+
+/* for the other host files of the library (fd_ed25519_hip_tile.c) */
+void
+fd_ed25519_hip_private_set_error( char const * msg ) {
+  snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "%s", msg );
 }
 
 static int

@@ -1,0 +1,912 @@
+/* fd_ed25519_hip_tile.c -- host runtime between Firedancer's verify tile
+   and the GPU engine (include/fd_ed25519_hip_tile.h): the asynchronous
+   pipe, the transaction parser and tcache the verify tile needs, the
+   batched verify-tile core, a tango-style ring for the latency mode, and
+   the multi-GPU pool with one feeder thread per device.  Plain C11 +
+   pthreads over the HIP runtime. */
+
+#define _GNU_SOURCE
+#include "../../../include/fd_ed25519_hip_tile.h"
+
+#include <hip/hip_runtime_api.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+/* engine.c's error buffer is thread-local there; this file reports through
+   its own setter so that fd_ed25519_hip_last_error() sees both */
+extern char const * fd_ed25519_hip_last_error( void );
+void fd_ed25519_hip_private_set_error( char const * msg );
+
+static double
+now_s( void ) {
+  struct timespec ts;
+  clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static int
+tile_fail( char const * what, hipError_t err ) {
+  char buf[ 256 ];
+  snprintf( buf, sizeof(buf), "%s: %s (%d)", what, hipGetErrorString( err ), (int)err );
+  fd_ed25519_hip_private_set_error( buf );
+  return FD_ED25519_HIP_ERR_HIP - (int)err;
+}
+
+#define TCHK( call, what ) do {                       \
+    hipError_t _e = (call);                           \
+    if( _e!=hipSuccess ) return tile_fail( what, _e ); \
+  } while(0)
+
+/* ======================================================================
+   pipe */
+
+#define PIPE_SLOT_MAX 8
+
+#define SLOT_FREE 0
+#define SLOT_FILL 1
+#define SLOT_BUSY 2
+#define SLOT_DONE 3
+
+typedef struct {
+  fd_ed25519_hip_slot_t     pub;     /* first member: the public handle */
+  fd_ed25519_hip_engine_t * eng;
+  hipEvent_t                ev;
+  int                       state;
+  unsigned char *           d_msgs;
+  unsigned long *           d_off;
+  unsigned int *            d_sz;
+  unsigned char *           d_sigs;
+  unsigned char *           d_pubs;
+  signed char *             d_out;
+  unsigned int *            d_tfirst;
+  unsigned int *            d_tcnt;
+  signed char *             d_tout;
+} pipe_slot_t;
+
+struct fd_ed25519_hip_pipe {
+  int           device;
+  unsigned      slot_cnt;
+  unsigned long next_acq;    /* ring index of the next slot to acquire */
+  unsigned long next_poll;   /* ring index of the oldest submitted slot */
+  unsigned long seq;
+  unsigned      in_flight;
+  pipe_slot_t   slot[ PIPE_SLOT_MAX ];
+};
+
+static void
+pipe_slot_free( pipe_slot_t * s ) {
+  fd_ed25519_hip_slot_t * p = &s->pub;
+  hipHostFree( p->msgs ); hipHostFree( p->msg_off ); hipHostFree( p->msg_sz ); hipHostFree( p->sigs );
+  hipHostFree( p->pubs ); hipHostFree( p->txn_first ); hipHostFree( p->txn_sig_cnt ); hipHostFree( p->sig_out );
+  hipHostFree( p->txn_out );
+  hipFree( s->d_msgs ); hipFree( s->d_off ); hipFree( s->d_sz ); hipFree( s->d_sigs ); hipFree( s->d_pubs );
+  hipFree( s->d_out ); hipFree( s->d_tfirst ); hipFree( s->d_tcnt ); hipFree( s->d_tout );
+  if( s->ev ) hipEventDestroy( s->ev );
+  if( s->eng ) fd_ed25519_hip_engine_delete( s->eng );
+}
+
+void
+fd_ed25519_hip_pipe_delete( fd_ed25519_hip_pipe_t * pipe ) {
+  if( !pipe ) return;
+  hipSetDevice( pipe->device );
+  for( unsigned i=0U; i<pipe->slot_cnt; i++ ) {
+    if( pipe->slot[i].eng ) fd_ed25519_hip_engine_sync( pipe->slot[i].eng );
+    pipe_slot_free( &pipe->slot[i] );
+  }
+  free( pipe );
+}
+
+static int
+pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned long msg_cap, unsigned long txn_cap,
+                int flags ) {
+  s->eng = fd_ed25519_hip_engine_new( device, sig_cap, flags );
+  if( !s->eng ) return FD_ED25519_HIP_ERR_INVAL;
+  fd_ed25519_hip_slot_t * p = &s->pub;
+  p->sig_cap = sig_cap; p->msg_cap = msg_cap; p->txn_cap = txn_cap;
+  unsigned long tc = txn_cap ? txn_cap : 1UL;
+  TCHK( hipHostMalloc( (void **)&p->msgs,        msg_cap + 64UL, hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&p->msg_off,     8UL*sig_cap,    hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&p->msg_sz,      4UL*sig_cap,    hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&p->sigs,        64UL*sig_cap,   hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&p->pubs,        32UL*sig_cap,   hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&p->sig_out,     sig_cap,        hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&p->txn_first,   4UL*tc,         hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&p->txn_sig_cnt, 4UL*tc,         hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&p->txn_out,     tc,             hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_msgs,   msg_cap + 64UL ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_off,    8UL*sig_cap    ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_sz,     4UL*sig_cap    ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_sigs,   64UL*sig_cap   ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_pubs,   32UL*sig_cap   ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_out,    sig_cap        ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_tfirst, 4UL*tc         ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_tcnt,   4UL*tc         ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_tout,   tc             ), "hipMalloc" );
+  TCHK( hipEventCreateWithFlags( &s->ev, hipEventDisableTiming ), "hipEventCreate" );
+  s->state = SLOT_FREE;
+  return FD_ED25519_HIP_OK;
+}
+
+fd_ed25519_hip_pipe_t *
+fd_ed25519_hip_pipe_new( int device, unsigned slot_cnt, unsigned long sig_cap, unsigned long msg_cap,
+                         unsigned long txn_cap, int flags ) {
+  if( slot_cnt<1U || slot_cnt>PIPE_SLOT_MAX || !sig_cap ) {
+    fd_ed25519_hip_private_set_error( "pipe_new: slot_cnt must be 1..8 and sig_cap > 0" );
+    return NULL;
+  }
+  fd_ed25519_hip_pipe_t * pipe = (fd_ed25519_hip_pipe_t *)calloc( 1, sizeof(fd_ed25519_hip_pipe_t) );
+  if( !pipe ) { fd_ed25519_hip_private_set_error( "pipe_new: calloc failed" ); return NULL; }
+  pipe->device   = device;
+  pipe->slot_cnt = slot_cnt;
+  if( hipSetDevice( device )!=hipSuccess ) { tile_fail( "hipSetDevice", hipErrorInvalidDevice ); free( pipe ); return NULL; }
+  for( unsigned i=0U; i<slot_cnt; i++ ) {
+    if( pipe_slot_init( &pipe->slot[i], device, sig_cap, msg_cap, txn_cap, flags ) ) {
+      fd_ed25519_hip_pipe_delete( pipe );
+      return NULL;
+    }
+  }
+  return pipe;
+}
+
+fd_ed25519_hip_slot_t *
+fd_ed25519_hip_pipe_acquire( fd_ed25519_hip_pipe_t * pipe ) {
+  pipe_slot_t * s = &pipe->slot[ pipe->next_acq % pipe->slot_cnt ];
+  if( s->state!=SLOT_FREE ) return NULL;
+  s->state = SLOT_FILL;
+  pipe->next_acq++;
+  s->pub.sig_cnt = 0UL; s->pub.msg_bytes = 0UL; s->pub.txn_cnt = 0UL;
+  return &s->pub;
+}
+
+int
+fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot,
+                            unsigned long sig_cnt, unsigned long msg_bytes, unsigned long txn_cnt ) {
+  pipe_slot_t * s = (pipe_slot_t *)slot;
+  if( s->state!=SLOT_FILL || sig_cnt>slot->sig_cap || msg_bytes>slot->msg_cap || txn_cnt>slot->txn_cap )
+    return FD_ED25519_HIP_ERR_INVAL;
+  TCHK( hipSetDevice( pipe->device ), "hipSetDevice" );
+  hipStream_t st = (hipStream_t)fd_ed25519_hip_engine_stream( s->eng );
+  slot->sig_cnt = sig_cnt; slot->msg_bytes = msg_bytes; slot->txn_cnt = txn_cnt;
+  slot->seq = pipe->seq++;
+  slot->t_submit = now_s();
+  if( sig_cnt ) {
+    TCHK( hipMemcpyAsync( s->d_msgs, slot->msgs,    msg_bytes ? msg_bytes : 1UL, hipMemcpyHostToDevice, st ), "H2D msgs" );
+    TCHK( hipMemcpyAsync( s->d_off,  slot->msg_off, 8UL*sig_cnt,  hipMemcpyHostToDevice, st ), "H2D off" );
+    TCHK( hipMemcpyAsync( s->d_sz,   slot->msg_sz,  4UL*sig_cnt,  hipMemcpyHostToDevice, st ), "H2D sz" );
+    TCHK( hipMemcpyAsync( s->d_sigs, slot->sigs,    64UL*sig_cnt, hipMemcpyHostToDevice, st ), "H2D sigs" );
+    TCHK( hipMemcpyAsync( s->d_pubs, slot->pubs,    32UL*sig_cnt, hipMemcpyHostToDevice, st ), "H2D pubs" );
+    int err = fd_ed25519_hip_verify_dev( s->eng, sig_cnt, s->d_msgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs,
+                                         s->d_out, st );
+    if( err ) return err;
+  }
+  if( txn_cnt ) {
+    TCHK( hipMemcpyAsync( s->d_tfirst, slot->txn_first,   4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tfirst" );
+    TCHK( hipMemcpyAsync( s->d_tcnt,   slot->txn_sig_cnt, 4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tcnt" );
+    int err = fd_ed25519_hip_txn_combine_dev( s->eng, txn_cnt, s->d_out, s->d_tfirst, s->d_tcnt, s->d_tout, st );
+    if( err ) return err;
+    TCHK( hipMemcpyAsync( slot->txn_out, s->d_tout, txn_cnt, hipMemcpyDeviceToHost, st ), "D2H tout" );
+  }
+  if( sig_cnt ) TCHK( hipMemcpyAsync( slot->sig_out, s->d_out, sig_cnt, hipMemcpyDeviceToHost, st ), "D2H out" );
+  TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
+  s->state = SLOT_BUSY;
+  pipe->in_flight++;
+  return FD_ED25519_HIP_OK;
+}
+
+fd_ed25519_hip_slot_t *
+fd_ed25519_hip_pipe_poll( fd_ed25519_hip_pipe_t * pipe, int wait ) {
+  pipe_slot_t * s = &pipe->slot[ pipe->next_poll % pipe->slot_cnt ];
+  if( s->state!=SLOT_BUSY ) return NULL;
+  hipError_t e = wait ? hipEventSynchronize( s->ev ) : hipEventQuery( s->ev );
+  if( e==hipErrorNotReady ) return NULL;
+  if( e!=hipSuccess ) {
+    /* a failed batch is unrecoverable for the pipe: report loudly */
+    fprintf( stderr, "libfd_ed25519_hip: FATAL: batch %lu failed on the GPU: %s\n", s->pub.seq, hipGetErrorString( e ) );
+    abort();
+  }
+  s->pub.t_done = now_s();
+  s->state = SLOT_DONE;
+  pipe->next_poll++;
+  pipe->in_flight--;
+  return &s->pub;
+}
+
+void
+fd_ed25519_hip_pipe_release( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot ) {
+  (void)pipe;
+  pipe_slot_t * s = (pipe_slot_t *)slot;
+  if( s->state==SLOT_DONE ) s->state = SLOT_FREE;
+}
+
+unsigned
+fd_ed25519_hip_pipe_in_flight( fd_ed25519_hip_pipe_t const * pipe ) {
+  return pipe->in_flight;
+}
+
+/* ======================================================================
+   txn: fd_txn_parse restated (src/ballet/txn/fd_txn_parse.c:6-244).
+   Each rule below is the reference's CHECK at the cited line; a payload is
+   accepted iff every rule holds.  Offsets are only read after the bytes are
+   known to be present. */
+
+/* compact-u16 (src/ballet/txn/fd_compact_u16.h): 1-3 bytes, 7 bits per
+   byte little-endian, minimal encoding required; returns the encoded size
+   (0: malformed / truncated) */
+static unsigned long
+cu16_decode( unsigned char const * b, unsigned long avail, unsigned * val ) {
+  if( avail>=1UL && !(b[0] & 0x80U) ) { *val = b[0]; return 1UL; }
+  if( avail>=2UL && !(b[1] & 0x80U) ) {
+    if( !b[1] ) return 0UL;                                      /* non-minimal */
+    *val = (b[0] & 0x7FU) | ((unsigned)b[1] << 7);
+    return 2UL;
+  }
+  if( avail>=3UL && !(b[2] & 0xFCU) ) {
+    if( !b[2] ) return 0UL;                                      /* non-minimal */
+    *val = (b[0] & 0x7FU) | ((unsigned)(b[1] & 0x7FU) << 7) | ((unsigned)b[2] << 14);
+    return 3UL;
+  }
+  return 0UL;
+}
+
+#define TXN_SIG_MAX       127UL
+#define TXN_ACCT_MAX      128UL
+#define TXN_INSTR_MAX      64UL
+#define TXN_LUT_MAX       127UL
+
+int
+fd_ed25519_hip_txn_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn_t * out ) {
+  unsigned long i = 0UL, n;
+  unsigned v;
+#define HAVE( k ) ( (unsigned long)(k) <= sz - i )
+#define CU16( dst ) do { n = cu16_decode( p + i, sz - i, &v ); if( !n ) return 0; (dst) = v; i += n; } while(0)
+  if( sz>FD_ED25519_HIP_TXN_MTU ) return 0;                                             /* :85 */
+  if( !HAVE( 1 ) ) return 0;
+  unsigned sig_cnt = p[ i++ ];
+  if( sig_cnt<1U || sig_cnt>TXN_SIG_MAX ) return 0;                                    /* :94 */
+  if( !HAVE( 64UL*sig_cnt ) ) return 0;
+  unsigned long sig_off = i;  i += 64UL*sig_cnt;
+  unsigned long msg_off = i;
+  if( !HAVE( 1 ) ) return 0;
+  unsigned b0 = p[ i++ ];
+  unsigned char ver;
+  if( b0 & 0x80U ) {                                                                     /* :102-107 */
+    ver = (unsigned char)(b0 & 0x7FU);
+    if( ver!=0U ) return 0;
+    if( !HAVE( 1 ) ) return 0;
+    if( p[ i ]!=sig_cnt ) return 0;
+    i++;
+  } else {
+    ver = 0xFF;
+    if( b0!=sig_cnt ) return 0;                                                          /* :110 */
+  }
+  if( !HAVE( 1 ) ) return 0;
+  unsigned ro_signed = p[ i++ ];
+  if( !(ro_signed<sig_cnt) ) return 0;                                                   /* :114 */
+  if( !HAVE( 1 ) ) return 0;
+  unsigned ro_unsigned = p[ i++ ];
+  unsigned acct_cnt;  CU16( acct_cnt );
+  if( !(sig_cnt<=acct_cnt && acct_cnt<=TXN_ACCT_MAX) ) return 0;                         /* :120 */
+  if( sig_cnt + ro_unsigned > acct_cnt ) return 0;                                       /* :121 */
+  if( !HAVE( 32UL*acct_cnt ) ) return 0;
+  unsigned long acct_off = i;  i += 32UL*acct_cnt;
+  if( !HAVE( 32 ) ) return 0;
+  unsigned long bh_off = i;  i += 32UL;
+  unsigned instr_cnt;  CU16( instr_cnt );
+  if( instr_cnt>TXN_INSTR_MAX ) return 0;                                                /* :132 */
+  if( !HAVE( 3UL*instr_cnt ) ) return 0;                                                 /* :133 */
+  if( !(acct_cnt > (instr_cnt ? 1U : 0U)) ) return 0;                                    /* :136 */
+  unsigned max_acct = 0U;
+  for( unsigned j=0U; j<instr_cnt; j++ ) {
+    if( !HAVE( 3 ) ) return 0;
+    unsigned prog = p[ i++ ];
+    unsigned ia; CU16( ia );
+    if( !HAVE( ia ) ) return 0;
+    for( unsigned k=0U; k<ia; k++ ) if( p[ i+k ]>max_acct ) max_acct = p[ i+k ];
+    i += ia;
+    unsigned dsz; CU16( dsz );
+    if( !HAVE( dsz ) ) return 0;
+    i += dsz;
+    if( !(0U<prog && prog<acct_cnt) ) return 0;                                          /* :175 */
+  }
+  unsigned lut_cnt = 0U;
+  unsigned long adtl = 0UL, adtl_w = 0UL;
+  if( ver==0U ) {
+    CU16( lut_cnt );
+    if( lut_cnt>TXN_LUT_MAX ) return 0;                                                  /* :199 */
+    if( !HAVE( 34UL*lut_cnt ) ) return 0;
+    for( unsigned j=0U; j<lut_cnt; j++ ) {
+      if( !HAVE( 32 ) ) return 0;
+      i += 32UL;
+      unsigned w, r;
+      CU16( w );  if( !HAVE( w ) ) return 0;  i += w;
+      CU16( r );  if( !HAVE( r ) ) return 0;  i += r;
+      if( w > TXN_ACCT_MAX - acct_cnt ) return 0;                                        /* :212 */
+      if( r > TXN_ACCT_MAX - acct_cnt ) return 0;
+      if( w + r < 1U ) return 0;
+      adtl_w += w;
+      adtl   += (unsigned long)w + r;
+    }
+  }
+  if( i!=sz ) return 0;                                                                  /* :229 */
+  if( acct_cnt + adtl > TXN_ACCT_MAX ) return 0;                                         /* :231 */
+  if( !(max_acct < acct_cnt + adtl) ) return 0;                                          /* :234 */
+#undef HAVE
+#undef CU16
+  if( out ) {
+    out->transaction_version          = ver;
+    out->signature_cnt                = (unsigned char)sig_cnt;
+    out->signature_off                = (unsigned short)sig_off;
+    out->message_off                  = (unsigned short)msg_off;
+    out->readonly_signed_cnt          = (unsigned char)ro_signed;
+    out->readonly_unsigned_cnt        = (unsigned char)ro_unsigned;
+    out->acct_addr_cnt                = (unsigned short)acct_cnt;
+    out->acct_addr_off                = (unsigned short)acct_off;
+    out->recent_blockhash_off         = (unsigned short)bh_off;
+    out->instr_cnt                    = (unsigned short)instr_cnt;
+    out->addr_table_lookup_cnt        = (unsigned char)lut_cnt;
+    out->addr_table_adtl_writable_cnt = (unsigned char)adtl_w;
+    out->addr_table_adtl_cnt          = (unsigned char)adtl;
+  }
+  return 1;
+}
+
+/* ======================================================================
+   tcache: a ring of the last `depth` tags plus an open-addressed map
+   (linear probing from tag & (map_cnt-1), tag 0 = empty slot), with the
+   reference's semantics (src/tango/tcache/fd_tcache.h:259-404): query stops
+   at the tag or at an empty slot -- so tag 0 always "hits" an empty slot;
+   insert of a present tag changes nothing; otherwise the tag goes in and
+   the tag `depth` inserts older is removed from the map with backward-shift
+   deletion. */
+
+struct fd_ed25519_hip_tcache {
+  unsigned long depth, map_cnt, oldest;
+  unsigned long * ring;
+  unsigned long * map;
+};
+
+fd_ed25519_hip_tcache_t *
+fd_ed25519_hip_tcache_new( unsigned long depth, unsigned long map_cnt ) {
+  if( !depth || !map_cnt || (map_cnt & (map_cnt-1UL)) || map_cnt<depth+2UL ) return NULL;
+  fd_ed25519_hip_tcache_t * tc = (fd_ed25519_hip_tcache_t *)calloc( 1, sizeof(*tc) );
+  if( !tc ) return NULL;
+  tc->depth = depth; tc->map_cnt = map_cnt;
+  tc->ring = (unsigned long *)calloc( depth, sizeof(unsigned long) );
+  tc->map  = (unsigned long *)calloc( map_cnt, sizeof(unsigned long) );
+  if( !tc->ring || !tc->map ) { fd_ed25519_hip_tcache_delete( tc ); return NULL; }
+  return tc;
+}
+
+void
+fd_ed25519_hip_tcache_delete( fd_ed25519_hip_tcache_t * tc ) {
+  if( !tc ) return;
+  free( tc->ring ); free( tc->map ); free( tc );
+}
+
+static unsigned long
+tc_probe( fd_ed25519_hip_tcache_t const * tc, unsigned long tag, int * found ) {
+  unsigned long m = tc->map_cnt - 1UL, idx = tag & m;
+  for( ;; ) {
+    unsigned long t = tc->map[ idx ];
+    if( t==tag ) { *found = 1; return idx; }
+    if( !t )     { *found = 0; return idx; }
+    idx = (idx+1UL) & m;
+  }
+}
+
+int
+fd_ed25519_hip_tcache_query( fd_ed25519_hip_tcache_t const * tc, unsigned long tag ) {
+  int found;
+  tc_probe( tc, tag, &found );
+  return found;
+}
+
+static void
+tc_remove( fd_ed25519_hip_tcache_t * tc, unsigned long tag ) {
+  if( !tag ) return;
+  int found;
+  unsigned long slot = tc_probe( tc, tag, &found );
+  if( !found ) return;
+  unsigned long m = tc->map_cnt - 1UL;
+  for( ;; ) {
+    tc->map[ slot ] = 0UL;
+    unsigned long hole = slot;
+    for( ;; ) {
+      slot = (slot+1UL) & m;
+      unsigned long t = tc->map[ slot ];
+      if( !t ) return;
+      unsigned long home = t & m;
+      /* t may stay iff its home lies cyclically in (hole, slot] */
+      int stays = hole<=slot ? (hole<home && home<=slot) : (hole<home || home<=slot);
+      if( !stays ) break;
+    }
+    tc->map[ hole ] = tc->map[ slot ];
+  }
+}
+
+int
+fd_ed25519_hip_tcache_insert( fd_ed25519_hip_tcache_t * tc, unsigned long tag ) {
+  int found;
+  unsigned long idx = tc_probe( tc, tag, &found );
+  if( found ) return 1;
+  tc->map[ idx ] = tag;
+  unsigned long evict = tc->ring[ tc->oldest ];
+  tc->ring[ tc->oldest ] = tag;
+  tc->oldest = tc->oldest+1UL==tc->depth ? 0UL : tc->oldest+1UL;
+  tc_remove( tc, evict );
+  return 0;
+}
+
+/* ======================================================================
+   vtile: fd_txn_verify batched.
+
+   Every frag becomes a record in a FIFO.  Parse failures are answered at
+   once (after_frag filters them, fd_verify.c:117-121); parsed transactions
+   are staged into the open pipe slot.  When a batch completes, its records
+   are resolved in frag order with exactly fd_txn_verify's sequence
+   (fd_verify.h:65-87): tcache query -> DEDUP; else batch_single_msg code !=
+   SUCCESS -> FAILED; else tcache insert -> DEDUP if it was a duplicate, else
+   SUCCESS.  Because batches complete in submission order and no frag's
+   outcome is decided before the ones ahead of it, the verdict stream is the
+   one the reference tile produces on the same frags. */
+
+typedef struct {
+  unsigned long cookie;
+  unsigned long tag;
+  unsigned long slot_seq;   /* submission seq of its batch (pending)  */
+  unsigned      txn_idx;    /* index in its batch                      */
+  signed char   verdict;
+  unsigned char resolved;
+} vrec_t;
+
+struct fd_ed25519_hip_vtile {
+  fd_ed25519_hip_pipe_t *   pipe;
+  fd_ed25519_hip_tcache_t * tc;
+  fd_ed25519_hip_slot_t *   open;       /* acquired, not yet submitted */
+  unsigned long             open_seq;   /* seq the open slot will get   */
+  unsigned long             batch_sigs;
+  vrec_t *                  q;          /* circular FIFO of records */
+  unsigned long             q_cap, q_head, q_cnt;
+  unsigned long             resolved_head;  /* records [q_head, q_head+resolved_head) are resolved */
+};
+
+fd_ed25519_hip_vtile_t *
+fd_ed25519_hip_vtile_new( int device, unsigned slot_cnt, unsigned long batch_sigs, unsigned long tcache_depth,
+                          unsigned long tcache_map_cnt, int flags ) {
+  fd_ed25519_hip_vtile_t * vt = (fd_ed25519_hip_vtile_t *)calloc( 1, sizeof(*vt) );
+  if( !vt ) return NULL;
+  vt->batch_sigs = batch_sigs ? batch_sigs : 4096UL;
+  vt->pipe = fd_ed25519_hip_pipe_new( device, slot_cnt, vt->batch_sigs, vt->batch_sigs*FD_ED25519_HIP_TXN_MTU,
+                                      vt->batch_sigs, flags );
+  vt->tc   = fd_ed25519_hip_tcache_new( tcache_depth, tcache_map_cnt );
+  vt->q_cap = 1024UL;
+  vt->q = (vrec_t *)malloc( vt->q_cap*sizeof(vrec_t) );
+  if( !vt->pipe || !vt->tc || !vt->q ) {
+    if( !vt->tc ) fd_ed25519_hip_private_set_error( "vtile_new: bad tcache geometry" );
+    fd_ed25519_hip_vtile_delete( vt );
+    return NULL;
+  }
+  return vt;
+}
+
+void
+fd_ed25519_hip_vtile_delete( fd_ed25519_hip_vtile_t * vt ) {
+  if( !vt ) return;
+  fd_ed25519_hip_pipe_delete( vt->pipe );
+  fd_ed25519_hip_tcache_delete( vt->tc );
+  free( vt->q );
+  free( vt );
+}
+
+static vrec_t *
+vq_at( fd_ed25519_hip_vtile_t * vt, unsigned long k ) {
+  return &vt->q[ (vt->q_head + k) % vt->q_cap ];
+}
+
+static vrec_t *
+vq_push( fd_ed25519_hip_vtile_t * vt ) {
+  if( vt->q_cnt==vt->q_cap ) {
+    unsigned long ncap = 2UL*vt->q_cap;
+    vrec_t * nq = (vrec_t *)malloc( ncap*sizeof(vrec_t) );
+    if( !nq ) { fprintf( stderr, "libfd_ed25519_hip: FATAL: vtile queue allocation failed\n" ); abort(); }
+    for( unsigned long k=0UL; k<vt->q_cnt; k++ ) nq[k] = *vq_at( vt, k );
+    free( vt->q );
+    vt->q = nq; vt->q_cap = ncap; vt->q_head = 0UL;
+  }
+  vrec_t * r = &vt->q[ (vt->q_head + vt->q_cnt) % vt->q_cap ];
+  vt->q_cnt++;
+  memset( r, 0, sizeof(*r) );
+  return r;
+}
+
+/* advance resolved_head over the resolved prefix of the FIFO */
+static void
+vt_advance( fd_ed25519_hip_vtile_t * vt ) {
+  while( vt->resolved_head<vt->q_cnt && vq_at( vt, vt->resolved_head )->resolved ) vt->resolved_head++;
+}
+
+/* resolve the records of a completed batch, in frag order (records ahead
+   of them are resolved already: earlier batches completed first, parse
+   failures at once) */
+static void
+vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
+  for( unsigned long k=vt->resolved_head; k<vt->q_cnt; k++ ) {
+    vrec_t * r = vq_at( vt, k );
+    if( r->resolved ) continue;
+    if( r->slot_seq!=s->seq ) break;
+    int code = s->txn_out[ r->txn_idx ];
+    int v;
+    if( fd_ed25519_hip_tcache_query( vt->tc, r->tag ) )      v = FD_ED25519_HIP_TXN_VERIFY_DEDUP;
+    else if( code!=FD_ED25519_SUCCESS )                       v = FD_ED25519_HIP_TXN_VERIFY_FAILED;
+    else if( fd_ed25519_hip_tcache_insert( vt->tc, r->tag ) ) v = FD_ED25519_HIP_TXN_VERIFY_DEDUP;
+    else                                                      v = FD_ED25519_HIP_TXN_VERIFY_SUCCESS;
+    r->verdict  = (signed char)v;
+    r->resolved = 1;
+  }
+  vt_advance( vt );
+}
+
+static int
+vt_drain_one( fd_ed25519_hip_vtile_t * vt, int wait ) {
+  fd_ed25519_hip_slot_t * s = fd_ed25519_hip_pipe_poll( vt->pipe, wait );
+  if( !s ) return 0;
+  vt_resolve( vt, s );
+  fd_ed25519_hip_pipe_release( vt->pipe, s );
+  return 1;
+}
+
+static int
+vt_submit_open( fd_ed25519_hip_vtile_t * vt ) {
+  fd_ed25519_hip_slot_t * s = vt->open;
+  if( !s || !s->txn_cnt ) return 0;
+  int err = fd_ed25519_hip_pipe_submit( vt->pipe, s, s->sig_cnt, s->msg_bytes, s->txn_cnt );
+  if( err ) {
+    fprintf( stderr, "libfd_ed25519_hip: FATAL: vtile submit failed: %s (%s)\n", fd_ed25519_hip_strerror( err ),
+             fd_ed25519_hip_last_error() );
+    abort();
+  }
+  vt->open = NULL;
+  return 1;
+}
+
+static void
+vt_open( fd_ed25519_hip_vtile_t * vt ) {
+  if( vt->open ) return;
+  for( ;; ) {
+    vt->open = fd_ed25519_hip_pipe_acquire( vt->pipe );  /* counts start at 0 */
+    if( vt->open ) break;
+    vt_drain_one( vt, 1 );  /* every slot in flight: wait for the oldest */
+  }
+  vt->open_seq = vt->pipe->seq;
+}
+
+int
+fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
+                           unsigned long cookie ) {
+  fd_ed25519_hip_txn_t t;
+  if( !fd_ed25519_hip_txn_parse( payload, payload_sz, &t ) ) {
+    vrec_t * r = vq_push( vt );
+    r->cookie = cookie; r->verdict = FD_ED25519_HIP_TXN_PARSE_FAILED; r->resolved = 1;
+    vt_advance( vt );
+    return 0;
+  }
+  unsigned long nsig   = (t.signature_cnt>=1U && t.signature_cnt<=16U) ? t.signature_cnt : 0UL;
+  unsigned long msg_sz = payload_sz - t.message_off;
+  vt_open( vt );
+  fd_ed25519_hip_slot_t * s = vt->open;
+  if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap || s->msg_bytes+msg_sz>s->msg_cap ) ) {
+    vt_submit_open( vt );
+    vt_open( vt );
+    s = vt->open;
+  }
+  unsigned long moff = s->msg_bytes;
+  memcpy( s->msgs + moff, payload + t.message_off, msg_sz );
+  s->msg_bytes += msg_sz;
+  unsigned long first = s->sig_cnt;
+  for( unsigned long j=0UL; j<nsig; j++ ) {
+    unsigned long k = first + j;
+    s->msg_off[ k ] = moff;
+    s->msg_sz [ k ] = (unsigned int)msg_sz;
+    memcpy( s->sigs + 64UL*k, payload + t.signature_off + 64UL*j, 64UL );
+    memcpy( s->pubs + 32UL*k, payload + t.acct_addr_off + 32UL*j, 32UL );
+  }
+  s->sig_cnt += nsig;
+  unsigned long ti = s->txn_cnt++;
+  s->txn_first  [ ti ] = (unsigned int)first;
+  s->txn_sig_cnt[ ti ] = t.signature_cnt;   /* 17..127 -> ERR_SIG, no signatures staged */
+  vrec_t * r = vq_push( vt );
+  r->cookie   = cookie;
+  memcpy( &r->tag, payload + t.signature_off, 8UL );  /* ha_dedup_tag, fd_verify.h:65 */
+  r->slot_seq = vt->open_seq;
+  r->txn_idx  = (unsigned)ti;
+  if( s->sig_cnt>=s->sig_cap || s->txn_cnt>=s->txn_cap ) vt_submit_open( vt );
+  return 1;
+}
+
+int
+fd_ed25519_hip_vtile_flush( fd_ed25519_hip_vtile_t * vt, int wait ) {
+  (void)wait;
+  return vt_submit_open( vt );
+}
+
+unsigned long
+fd_ed25519_hip_vtile_poll( fd_ed25519_hip_vtile_t * vt, int wait, unsigned long max, unsigned long * cookie,
+                           signed char * verdict, unsigned long * tag ) {
+  while( vt_drain_one( vt, 0 ) ) {}
+  if( wait && !vt->resolved_head && vt->q_cnt && fd_ed25519_hip_pipe_in_flight( vt->pipe ) ) vt_drain_one( vt, 1 );
+  unsigned long n = 0UL;
+  while( n<max && vt->resolved_head ) {
+    vrec_t * r = vq_at( vt, 0UL );
+    if( cookie  ) cookie [ n ] = r->cookie;
+    if( verdict ) verdict[ n ] = r->verdict;
+    if( tag     ) tag    [ n ] = r->tag;
+    n++;
+    vt->q_head = (vt->q_head+1UL) % vt->q_cap;
+    vt->q_cnt--;
+    vt->resolved_head--;
+  }
+  return n;
+}
+
+unsigned long
+fd_ed25519_hip_vtile_pending( fd_ed25519_hip_vtile_t const * vt ) {
+  return vt->q_cnt;
+}
+
+/* ======================================================================
+   ring: a single-producer single-consumer tango-style mcache / dcache.
+   The frag metadata is fd_frag_meta_t's layout (src/tango/fd_tango_base.h:
+   123-203, 32 bytes: seq, sig, chunk, sz, ctl, tsorig, tspub); the producer
+   invalidates a line (seq-1), writes the body, then publishes seq with
+   release order; the consumer reads seq with acquire order, copies the
+   payload, and re-reads seq to detect being overrun.  Payloads live in a
+   dcache of 64-byte chunks, allocated compactly with wrap-around. */
+
+typedef struct {
+  _Atomic uint64_t seq;
+  uint64_t         sig;
+  uint32_t         chunk;
+  uint16_t         sz;
+  uint16_t         ctl;
+  uint32_t         tsorig;
+  uint32_t         tspub;
+} ring_meta_t;
+
+typedef struct {
+  ring_meta_t *   mcache;
+  unsigned long   depth;
+  unsigned char * dcache;
+  unsigned long   chunk_cnt;
+} ring_t;
+
+#define RING_CHUNK 64UL
+#define RING_MTU_CHUNKS ((FD_ED25519_HIP_TXN_MTU + RING_CHUNK - 1UL) / RING_CHUNK)
+
+typedef struct {
+  ring_t *              ring;
+  unsigned char const * payloads;
+  unsigned long const * off;
+  unsigned int const *  sz;
+  unsigned long         n;
+  double                rate;
+  double *              t_pub;
+  _Atomic int           go;
+  _Atomic uint64_t      consumed;   /* frags the consumer has taken (credits) */
+  double                t0;
+} producer_t;
+
+static void *
+producer_main( void * arg ) {
+  producer_t * pr = (producer_t *)arg;
+  ring_t * rg = pr->ring;
+  while( !atomic_load_explicit( &pr->go, memory_order_acquire ) ) {}
+  unsigned long chunk = 0UL;
+  double t0 = now_s();
+  pr->t0 = t0;
+  for( unsigned long i=0UL; i<pr->n; i++ ) {
+    /* the time frag i is due: latency counts from here, so time a frag
+       waits for credits is part of it (no coordinated omission) */
+    double due = t0;
+    if( pr->rate>0.0 ) {
+      due = t0 + (double)i / pr->rate;
+      while( now_s()<due ) {}
+    } else {
+      due = now_s();
+    }
+    while( i - atomic_load_explicit( &pr->consumed, memory_order_acquire ) >= rg->depth ) {}
+    unsigned long sz = pr->sz[ i ];
+    unsigned long nch = (sz + RING_CHUNK - 1UL) / RING_CHUNK;
+    if( chunk + RING_MTU_CHUNKS > rg->chunk_cnt ) chunk = 0UL;   /* compact wrap */
+    ring_meta_t * m = &rg->mcache[ i & (rg->depth-1UL) ];
+    atomic_store_explicit( &m->seq, i-1UL, memory_order_relaxed );
+    atomic_thread_fence( memory_order_release );
+    memcpy( rg->dcache + chunk*RING_CHUNK, pr->payloads + pr->off[ i ], sz );
+    m->sig = i; m->chunk = (uint32_t)chunk; m->sz = (uint16_t)sz; m->ctl = 0; m->tsorig = 0; m->tspub = 0;
+    pr->t_pub[ i ] = due;
+    atomic_store_explicit( &m->seq, i, memory_order_release );
+    chunk += nch;
+  }
+  return NULL;
+}
+
+int
+fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_sigs,
+                            unsigned char const * payloads, unsigned long const * payload_off,
+                            unsigned int const * payload_sz, unsigned long txn_cnt, double offered_txn_per_s,
+                            unsigned long ring_depth, double * lat_s, signed char * verdict,
+                            fd_ed25519_hip_latency_result_t * res ) {
+  if( !txn_cnt || !ring_depth || (ring_depth & (ring_depth-1UL)) || !lat_s || !verdict || !res )
+    return FD_ED25519_HIP_ERR_INVAL;
+  for( unsigned long i=0UL; i<txn_cnt; i++ )
+    if( payload_sz[ i ]>FD_ED25519_HIP_TXN_MTU ) return FD_ED25519_HIP_ERR_INVAL;
+  memset( res, 0, sizeof(*res) );
+  fd_ed25519_hip_vtile_t * vt = fd_ed25519_hip_vtile_new( device, slot_cnt, batch_sigs, 16UL, 64UL, 0 );
+  if( !vt ) return FD_ED25519_HIP_ERR_INVAL;
+  ring_t rg;
+  rg.depth     = ring_depth;
+  rg.chunk_cnt = (ring_depth + 2UL) * RING_MTU_CHUNKS;
+  rg.mcache    = (ring_meta_t *)aligned_alloc( 64, ring_depth*sizeof(ring_meta_t) );
+  rg.dcache    = (unsigned char *)aligned_alloc( 64, rg.chunk_cnt*RING_CHUNK );
+  double * t_pub = (double *)malloc( txn_cnt*sizeof(double) );
+  unsigned long * ck = (unsigned long *)malloc( 4096UL*sizeof(unsigned long) );
+  signed char *   vd = (signed char *)malloc( 4096UL );
+  unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_TXN_MTU );
+  if( !rg.mcache || !rg.dcache || !t_pub || !ck || !vd || !buf ) {
+    free( rg.mcache ); free( rg.dcache ); free( t_pub ); free( ck ); free( vd ); free( buf );
+    fd_ed25519_hip_vtile_delete( vt );
+    return FD_ED25519_HIP_ERR_NOMEM;
+  }
+  for( unsigned long k=0UL; k<ring_depth; k++ ) atomic_store( &rg.mcache[k].seq, (uint64_t)(k - ring_depth) );
+
+  producer_t pr;
+  memset( &pr, 0, sizeof(pr) );
+  pr.ring = &rg; pr.payloads = payloads; pr.off = payload_off; pr.sz = payload_sz; pr.n = txn_cnt;
+  pr.rate = offered_txn_per_s; pr.t_pub = t_pub;
+  pthread_t th;
+  if( pthread_create( &th, NULL, producer_main, &pr ) ) {
+    free( rg.mcache ); free( rg.dcache ); free( t_pub ); free( ck ); free( vd ); free( buf );
+    fd_ed25519_hip_vtile_delete( vt );
+    return FD_ED25519_HIP_ERR_NOMEM;
+  }
+  atomic_store_explicit( &pr.go, 1, memory_order_release );
+
+  unsigned long next = 0UL, done = 0UL, sigs = 0UL;
+  unsigned long batches0 = 0UL;
+  while( done<txn_cnt ) {
+    /* pull every frag that is ready (after_frag) */
+    int pulled = 0;
+    while( next<txn_cnt ) {
+      ring_meta_t * m = &rg.mcache[ next & (ring_depth-1UL) ];
+      uint64_t s0 = atomic_load_explicit( &m->seq, memory_order_acquire );
+      if( (int64_t)(s0 - next)<0 ) break;                 /* not yet published */
+      if( s0!=next ) { res->ring_overruns++; verdict[ next ] = FD_ED25519_HIP_TXN_PARSE_FAILED; lat_s[ next ] = -1.0;
+                       next++; done++; continue; }
+      unsigned long sz = m->sz, cookie = m->sig;
+      memcpy( buf, rg.dcache + (unsigned long)m->chunk*RING_CHUNK, sz );
+      atomic_thread_fence( memory_order_acquire );
+      if( atomic_load_explicit( &m->seq, memory_order_relaxed )!=s0 ) {
+        res->ring_overruns++; verdict[ next ] = FD_ED25519_HIP_TXN_PARSE_FAILED; lat_s[ next ] = -1.0;
+        next++; done++; continue;
+      }
+      fd_ed25519_hip_txn_t t;
+      if( fd_ed25519_hip_txn_parse( buf, sz, &t ) && t.signature_cnt<=16U ) sigs += t.signature_cnt;
+      fd_ed25519_hip_vtile_frag( vt, buf, sz, cookie );
+      next++;
+      atomic_store_explicit( &pr.consumed, next, memory_order_release );
+      pulled = 1;
+      if( vt->pipe->seq!=batches0 ) break;                /* a full batch went out: go collect */
+    }
+    batches0 = vt->pipe->seq;
+    /* ring drained: send the open batch if a slot can take it */
+    if( !pulled && vt->open && vt->open->txn_cnt &&
+        ( slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<slot_cnt || next==txn_cnt ) )
+      fd_ed25519_hip_vtile_flush( vt, 0 );
+    unsigned long got = fd_ed25519_hip_vtile_poll( vt, 0, 4096UL, ck, vd, NULL );
+    double t = now_s();
+    for( unsigned long k=0UL; k<got; k++ ) {
+      lat_s  [ ck[k] ] = t - t_pub[ ck[k] ];
+      verdict[ ck[k] ] = vd[k];
+    }
+    done += got;
+  }
+  double t_end = now_s();
+  pthread_join( th, NULL );
+  res->offered_txn_per_s  = offered_txn_per_s;
+  res->seconds            = t_end - pr.t0;
+  res->txn_cnt            = txn_cnt;
+  res->sig_cnt            = sigs;
+  res->achieved_txn_per_s = (double)txn_cnt / res->seconds;
+  res->achieved_sig_per_s = (double)sigs / res->seconds;
+  res->batches            = vt->pipe->seq;
+  free( rg.mcache ); free( rg.dcache ); free( t_pub ); free( ck ); free( vd ); free( buf );
+  fd_ed25519_hip_vtile_delete( vt );
+  return FD_ED25519_HIP_OK;
+}
+
+/* ======================================================================
+   pool: one feeder thread + pipe per device, batches dealt round-robin. */
+
+typedef struct {
+  int                   device;
+  unsigned              slot_cnt;
+  unsigned              rank, ranks;
+  unsigned long         batch_sigs, n;
+  unsigned char const * msgs;
+  unsigned long const * msg_off;
+  unsigned int const *  msg_sz;
+  unsigned char const * sigs;
+  unsigned char const * pubs;
+  signed char *         out;
+  int                   err;
+} pool_job_t;
+
+static void *
+pool_main( void * arg ) {
+  pool_job_t * j = (pool_job_t *)arg;
+  unsigned long nb = (j->n + j->batch_sigs - 1UL) / j->batch_sigs;
+  unsigned long msg_cap = 1UL;
+  for( unsigned long b=j->rank; b<nb; b+=j->ranks ) {
+    unsigned long i0 = b*j->batch_sigs, i1 = i0+j->batch_sigs < j->n ? i0+j->batch_sigs : j->n, bytes = 0UL;
+    for( unsigned long i=i0; i<i1; i++ ) bytes += j->msg_sz[i];
+    if( bytes>msg_cap ) msg_cap = bytes;
+  }
+  fd_ed25519_hip_pipe_t * pipe = fd_ed25519_hip_pipe_new( j->device, j->slot_cnt, j->batch_sigs, msg_cap, 0UL, 0 );
+  if( !pipe ) { j->err = FD_ED25519_HIP_ERR_INVAL; return NULL; }
+  unsigned long b_sub = j->rank, b_done = j->rank;
+  while( b_done<nb ) {
+    fd_ed25519_hip_slot_t * s = b_sub<nb ? fd_ed25519_hip_pipe_acquire( pipe ) : NULL;
+    if( s ) {
+      unsigned long i0 = b_sub*j->batch_sigs, i1 = i0+j->batch_sigs < j->n ? i0+j->batch_sigs : j->n, pos = 0UL;
+      for( unsigned long i=i0; i<i1; i++ ) {
+        unsigned long k = i-i0;
+        memcpy( s->msgs + pos, j->msgs + j->msg_off[i], j->msg_sz[i] );
+        s->msg_off[k] = pos; s->msg_sz[k] = j->msg_sz[i];
+        pos += j->msg_sz[i];
+      }
+      memcpy( s->sigs, j->sigs + 64UL*i0, 64UL*(i1-i0) );
+      memcpy( s->pubs, j->pubs + 32UL*i0, 32UL*(i1-i0) );
+      s->user = b_sub;
+      int err = fd_ed25519_hip_pipe_submit( pipe, s, i1-i0, pos, 0UL );
+      if( err ) { j->err = err; break; }
+      b_sub += j->ranks;
+      continue;
+    }
+    fd_ed25519_hip_slot_t * d = fd_ed25519_hip_pipe_poll( pipe, 1 );
+    if( !d ) break;
+    memcpy( j->out + d->user*j->batch_sigs, d->sig_out, d->sig_cnt );
+    fd_ed25519_hip_pipe_release( pipe, d );
+    b_done += j->ranks;
+  }
+  fd_ed25519_hip_pipe_delete( pipe );
+  return NULL;
+}
+
+int
+fd_ed25519_hip_pool_verify( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
+                            unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
+                            unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
+                            signed char * out, double * seconds ) {
+  if( !devices || !device_cnt || device_cnt>64U || !batch_sigs || !out ) return FD_ED25519_HIP_ERR_INVAL;
+  pool_job_t job[ 64 ];
+  pthread_t  th[ 64 ];
+  double t0 = now_s();
+  for( unsigned r=0U; r<device_cnt; r++ ) {
+    job[r] = (pool_job_t){ devices[r], slot_cnt, r, device_cnt, batch_sigs, n, msgs, msg_off, msg_sz, sigs, pubs, out, 0 };
+    if( pthread_create( &th[r], NULL, pool_main, &job[r] ) ) {
+      for( unsigned q=0U; q<r; q++ ) pthread_join( th[q], NULL );
+      return FD_ED25519_HIP_ERR_NOMEM;
+    }
+  }
+  int err = 0;
+  for( unsigned r=0U; r<device_cnt; r++ ) {
+    pthread_join( th[r], NULL );
+    if( job[r].err && !err ) err = job[r].err;
+  }
+  if( seconds ) *seconds = now_s() - t0;
+  return err;
+}

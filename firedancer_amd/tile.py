@@ -1,0 +1,199 @@
+"""Python mirror of the verify-tile side of libfd_ed25519_hip
+(include/fd_ed25519_hip_tile.h): the transaction parser, the tcache, the
+batched verify-tile core, the latency mode and the multi-GPU pool.
+
+Names follow the reference: txn_parse ~ fd_txn_parse
+(src/ballet/txn/fd_txn_parse.c), TCache ~ fd_tcache
+(src/tango/tcache/fd_tcache.h), VerifyTile.frag / .poll ~ the verify tile's
+after_frag + fd_txn_verify (src/app/fdctl/run/tiles/fd_verify.{c,h}), with
+the verdicts TXN_VERIFY_SUCCESS / FAILED / DEDUP (fd_verify.h:9-11).
+"""
+import ctypes
+
+import numpy as np
+
+from .ed25519 import HipError, _c, _check, _lib, _ptr
+
+TXN_VERIFY_SUCCESS = 0
+TXN_VERIFY_FAILED = -1
+TXN_VERIFY_DEDUP = -2
+TXN_PARSE_FAILED = -3
+
+TXN_MTU = 1232
+
+
+class Txn(ctypes.Structure):
+    _fields_ = [("transaction_version", ctypes.c_ubyte), ("signature_cnt", ctypes.c_ubyte),
+                ("signature_off", ctypes.c_ushort), ("message_off", ctypes.c_ushort),
+                ("readonly_signed_cnt", ctypes.c_ubyte), ("readonly_unsigned_cnt", ctypes.c_ubyte),
+                ("acct_addr_cnt", ctypes.c_ushort), ("acct_addr_off", ctypes.c_ushort),
+                ("recent_blockhash_off", ctypes.c_ushort), ("instr_cnt", ctypes.c_ushort),
+                ("addr_table_lookup_cnt", ctypes.c_ubyte), ("addr_table_adtl_writable_cnt", ctypes.c_ubyte),
+                ("addr_table_adtl_cnt", ctypes.c_ubyte)]
+
+    FIELDS = [f for f, _ in _fields_]
+
+    def as_tuple(self):
+        return tuple(getattr(self, f) for f in self.FIELDS)
+
+
+class LatencyResult(ctypes.Structure):
+    _fields_ = [("offered_txn_per_s", ctypes.c_double), ("achieved_txn_per_s", ctypes.c_double),
+                ("achieved_sig_per_s", ctypes.c_double), ("seconds", ctypes.c_double),
+                ("txn_cnt", ctypes.c_ulong), ("sig_cnt", ctypes.c_ulong), ("batches", ctypes.c_ulong),
+                ("ring_overruns", ctypes.c_ulong)]
+
+
+_v = ctypes.c_void_p
+_lib.fd_ed25519_hip_txn_parse.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.POINTER(Txn)]
+_lib.fd_ed25519_hip_txn_parse.restype = ctypes.c_int
+_lib.fd_ed25519_hip_tcache_new.argtypes = [ctypes.c_ulong, ctypes.c_ulong]
+_lib.fd_ed25519_hip_tcache_new.restype = _v
+_lib.fd_ed25519_hip_tcache_delete.argtypes = [_v]
+_lib.fd_ed25519_hip_tcache_query.argtypes = [_v, ctypes.c_ulong]
+_lib.fd_ed25519_hip_tcache_insert.argtypes = [_v, ctypes.c_ulong]
+_lib.fd_ed25519_hip_vtile_new.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong,
+                                          ctypes.c_int]
+_lib.fd_ed25519_hip_vtile_new.restype = _v
+_lib.fd_ed25519_hip_vtile_delete.argtypes = [_v]
+_lib.fd_ed25519_hip_vtile_frag.argtypes = [_v, ctypes.c_char_p, ctypes.c_ulong, ctypes.c_ulong]
+_lib.fd_ed25519_hip_vtile_flush.argtypes = [_v, ctypes.c_int]
+_lib.fd_ed25519_hip_vtile_poll.argtypes = [_v, ctypes.c_int, ctypes.c_ulong, _v, _v, _v]
+_lib.fd_ed25519_hip_vtile_poll.restype = ctypes.c_ulong
+_lib.fd_ed25519_hip_vtile_pending.argtypes = [_v]
+_lib.fd_ed25519_hip_vtile_pending.restype = ctypes.c_ulong
+_lib.fd_ed25519_hip_latency_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, _v, _v, _v, ctypes.c_ulong,
+                                            ctypes.c_double, ctypes.c_ulong, _v, _v, ctypes.POINTER(LatencyResult)]
+_lib.fd_ed25519_hip_pool_verify.argtypes = [_v, ctypes.c_uint, ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, _v, _v,
+                                            _v, _v, _v, _v, ctypes.POINTER(ctypes.c_double)]
+
+
+def txn_parse(payload):
+    """fd_txn_parse: the parsed fields as a dict, or None if rejected."""
+    t = Txn()
+    payload = bytes(payload)
+    if not _lib.fd_ed25519_hip_txn_parse(payload, len(payload), ctypes.byref(t)):
+        return None
+    return {f: getattr(t, f) for f in Txn.FIELDS}
+
+
+class TCache:
+    def __init__(self, depth=16, map_cnt=64):
+        self._h = _lib.fd_ed25519_hip_tcache_new(depth, map_cnt)
+        if not self._h:
+            raise ValueError("bad tcache geometry (map_cnt must be a power of two >= depth+2)")
+
+    def query(self, tag):
+        return bool(_lib.fd_ed25519_hip_tcache_query(self._h, int(tag)))
+
+    def insert(self, tag):
+        """1 if tag was a duplicate (nothing inserted)."""
+        return bool(_lib.fd_ed25519_hip_tcache_insert(self._h, int(tag)))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.fd_ed25519_hip_tcache_delete(self._h)
+            self._h = None
+
+
+class VerifyTile:
+    """The verify tile's batched core on one GPU."""
+
+    def __init__(self, device=0, slot_cnt=3, batch_sigs=4096, tcache_depth=16, tcache_map_cnt=64, codes="avx512"):
+        flags = 1 if codes == "portable" else 0
+        self._h = _lib.fd_ed25519_hip_vtile_new(int(device), int(slot_cnt), int(batch_sigs), int(tcache_depth),
+                                                int(tcache_map_cnt), flags)
+        if not self._h:
+            raise HipError(f"vtile_new failed: {_lib.fd_ed25519_hip_last_error().decode()}")
+
+    def frag(self, payload, cookie):
+        payload = bytes(payload)
+        return _lib.fd_ed25519_hip_vtile_frag(self._h, payload, len(payload), int(cookie))
+
+    def flush(self):
+        return _lib.fd_ed25519_hip_vtile_flush(self._h, 1)
+
+    def poll(self, wait=False, max_n=1 << 16):
+        ck = np.zeros(max_n, np.uint64)
+        vd = np.zeros(max_n, np.int8)
+        tg = np.zeros(max_n, np.uint64)
+        n = _lib.fd_ed25519_hip_vtile_poll(self._h, 1 if wait else 0, max_n, _ptr(ck), _ptr(vd), _ptr(tg))
+        return ck[:n], vd[:n], tg[:n]
+
+    def pending(self):
+        return _lib.fd_ed25519_hip_vtile_pending(self._h)
+
+    def run(self, payloads):
+        """Every payload through the tile in order -> (verdicts, tags) by index."""
+        n = len(payloads)
+        verdict = np.full(n, 99, np.int8)
+        tags = np.zeros(n, np.uint64)
+        for i, p in enumerate(payloads):
+            self.frag(p, i)
+            ck, vd, tg = self.poll(False)
+            verdict[ck] = vd
+            tags[ck] = tg
+        self.flush()
+        while self.pending():
+            ck, vd, tg = self.poll(True)
+            verdict[ck] = vd
+            tags[ck] = tg
+        return verdict, tags
+
+    def close(self):
+        if self._h:
+            _lib.fd_ed25519_hip_vtile_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pack_payloads(payloads):
+    sz = np.array([len(p) for p in payloads], np.uint32)
+    off = np.zeros(len(payloads), np.uint64)
+    if len(payloads) > 1:
+        np.cumsum(sz[:-1], dtype=np.uint64, out=off[1:])
+    buf = np.frombuffer(b"".join(bytes(p) for p in payloads) or b"\0", np.uint8).copy()
+    return buf, off, sz
+
+
+def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=256, ring_depth=4096):
+    """Latency mode (C5): a producer thread publishes the payloads into a
+    tango-style ring at the offered rate; the verify tile consumes them.
+    payloads: a list of byte strings, or a uint8 array [n][size] of
+    equal-size payloads.  Returns (per-txn latency seconds, verdicts,
+    result dict)."""
+    if isinstance(payloads, np.ndarray) and payloads.ndim == 2:
+        n, size = payloads.shape
+        buf = np.ascontiguousarray(payloads).reshape(-1)
+        off = np.arange(n, dtype=np.uint64) * np.uint64(size)
+        sz = np.full(n, size, np.uint32)
+    else:
+        buf, off, sz = pack_payloads(payloads)
+        n = len(payloads)
+    lat = np.zeros(n, np.float64)
+    verdict = np.zeros(n, np.int8)
+    res = LatencyResult()
+    _check(_lib.fd_ed25519_hip_latency_run(int(device), int(slot_cnt), int(batch_sigs), _ptr(buf), _ptr(off), _ptr(sz),
+                                           n, float(offered_txn_per_s), int(ring_depth), _ptr(lat), _ptr(verdict),
+                                           ctypes.byref(res)))
+    return lat, verdict, {f: getattr(res, f) for f, _ in LatencyResult._fields_}
+
+
+def pool_verify(devices, msgs, msg_off, msg_sz, sigs, pubs, batch_sigs=65536, slot_cnt=3):
+    """Signatures dealt round-robin in batches over `devices` (one host thread
+    and pipe per entry) -> (codes, seconds)."""
+    devs = np.ascontiguousarray(devices, np.int32)
+    n = len(msg_sz)
+    out = np.zeros(max(n, 1), np.int8)
+    msgs = _c(msgs, np.uint8) if len(msgs) else np.zeros(1, np.uint8)
+    sec = ctypes.c_double(0.0)
+    _check(_lib.fd_ed25519_hip_pool_verify(_ptr(devs), len(devs), int(slot_cnt), int(batch_sigs), n, _ptr(msgs),
+                                           _ptr(_c(msg_off, np.uint64)), _ptr(_c(msg_sz, np.uint32)),
+                                           _ptr(_c(sigs, np.uint8).reshape(-1)), _ptr(_c(pubs, np.uint8).reshape(-1)),
+                                           _ptr(out), ctypes.byref(sec)))
+    return out[:n], sec.value

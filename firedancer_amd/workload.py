@@ -78,6 +78,66 @@ def corruption(seed, index_base, n, ppm):
     return cls, (x >> np.uint64(40)).astype(np.uint64)
 
 
+def _cu16(v):
+    out = bytearray()
+    while True:
+        b, v = v & 0x7F, v >> 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+def txn_payloads(engine, n, seed, msg_sz=200, index_base=0, signers=1):
+    """n legacy Solana transactions (the verify tile's input format,
+    src/ballet/txn/fd_txn.h) with `signers` signatures over a msg_sz-byte
+    message each, keys derived from (seed, index), signed on the GPU
+    (fd_ed25519_hip_sign_dev).  Message: header (signers, 0, 1), signers+2
+    accounts (the signers' keys first), blockhash, one instruction with
+    padding data.  Returns (payloads uint8 [n][size], size)."""
+    k = signers
+    head = bytes([k, 0, 1]) + _cu16(k + 2)
+    fixed = len(head) + 32 * (k + 2) + 32 + 1 + 1 + 1 + 2
+    data_len = msg_sz - fixed - len(_cu16(max(msg_sz - fixed - 1, 0)))
+    assert data_len >= 0, "message too short"
+    tail_hdr = bytes([1, k + 1, 2, 0, 1]) + _cu16(data_len)
+    m_len = len(head) + 32 * (k + 2) + 32 + len(tail_hdr) + data_len
+    rng = np.random.default_rng(seed)
+    privs = private_keys(seed, index_base, n * k).reshape(n, k, 32)
+    # public keys first (signing an empty message yields them)
+    d_priv = engine.alloc(32 * n * k).upload(privs.reshape(-1))
+    d_off = engine.alloc(8 * n * k).upload(np.zeros(n * k, np.uint64))
+    d_sz = engine.alloc(4 * n * k).upload(np.zeros(n * k, np.uint32))
+    d_msg = engine.alloc(16)
+    d_sig, d_pub = engine.alloc(64 * n * k), engine.alloc(32 * n * k)
+    engine.sign_dev(n * k, d_msg.ptr, d_off.ptr, d_sz.ptr, d_priv.ptr, d_sig.ptr, d_pub.ptr)
+    engine.sync()
+    pubs = d_pub.download(np.uint8, 32 * n * k).reshape(n, k, 32)
+    msgs = np.zeros((n, m_len), np.uint8)
+    p = 0
+    msgs[:, p:p + len(head)] = np.frombuffer(head, np.uint8); p += len(head)
+    msgs[:, p:p + 32 * k] = pubs.reshape(n, 32 * k); p += 32 * k
+    msgs[:, p:p + 64] = rng.integers(0, 256, (n, 64), dtype=np.uint8); p += 64    # 2 more accounts
+    msgs[:, p:p + 32] = rng.integers(0, 256, (n, 32), dtype=np.uint8); p += 32    # blockhash
+    msgs[:, p:p + len(tail_hdr)] = np.frombuffer(tail_hdr, np.uint8); p += len(tail_hdr)
+    msgs[:, p:] = rng.integers(0, 256, (n, m_len - p), dtype=np.uint8)
+    # every signer signs its transaction's message
+    d_m = engine.alloc(n * m_len).upload(msgs.reshape(-1))
+    off = np.repeat(np.arange(n, dtype=np.uint64) * np.uint64(m_len), k)
+    d_off2 = engine.alloc(8 * n * k).upload(off)
+    d_sz2 = engine.alloc(4 * n * k).upload(np.full(n * k, m_len, np.uint32))
+    engine.sign_dev(n * k, d_m.ptr, d_off2.ptr, d_sz2.ptr, d_priv.ptr, d_sig.ptr, d_pub.ptr)
+    engine.sync()
+    sigs = d_sig.download(np.uint8, 64 * n * k).reshape(n, 64 * k)
+    for b in (d_priv, d_off, d_sz, d_msg, d_sig, d_pub, d_m, d_off2, d_sz2):
+        b.free()
+    size = 1 + 64 * k + m_len
+    pay = np.empty((n, size), np.uint8)
+    pay[:, 0] = k
+    pay[:, 1:1 + 64 * k] = sigs
+    pay[:, 1 + 64 * k:] = msgs
+    return pay, size
+
+
 def ops_per_verify(msg_sz):
     """SURVEY.md §8(d) frozen algorithmic INT32 op count per verify, split by
     phase kernel.  Unit costs (radix 2^25.5): mul 130, sqr 85, carried

@@ -1,0 +1,230 @@
+#ifndef HEADER_fd_ed25519_hip_tile_h
+#define HEADER_fd_ed25519_hip_tile_h
+
+/* libfd_ed25519_hip, part 2: the host runtime that feeds the GPU from the
+   verify tile's side of Firedancer (SURVEY.md §8(b) "Needed extension for
+   GPU throughput", §8(e), §8(f) rows 1-2).  Plain C over the engine of
+   fd_ed25519_hip.h; every entry point is a C-ABI function of
+   libfd_ed25519_hip.so.
+
+     pipe    asynchronous submit / poll of pinned SoA batches, several in
+             flight per GPU (H2D, kernels and D2H of one batch overlap the
+             next batch's packing)
+     txn     fd_txn_parse restated for the fields the verify tile uses
+             (src/ballet/txn/fd_txn_parse.c:6-244), and the verify tile's
+             tcache dedup (src/tango/tcache/fd_tcache.h:259-404)
+     vtile   the verify tile's per-transaction logic, fd_txn_verify
+             (src/app/fdctl/run/tiles/fd_verify.h:43-88), batched: frags
+             are parsed and staged as they arrive, verified a batch at a
+             time, and their verdicts released in arrival order with the
+             reference's dedup semantics
+     ring    a tango-style mcache / dcache (src/tango/fd_tango_base.h:123-203)
+             between a producer thread and the vtile, for the latency mode
+     pool    one host feeder thread and pipe per GPU, batches dealt
+             round-robin (the analogue of seq % verify_tile_count,
+             src/app/fdctl/run/tiles/fd_verify.c:36-47) */
+
+#include "fd_ed25519_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- pipe ------------------------------------------------------------- */
+
+typedef struct fd_ed25519_hip_pipe fd_ed25519_hip_pipe_t;
+
+/* One batch of a pipe.  Between acquire and submit the caller fills the
+   pinned host arrays in place (no extra copy): signature i is sigs[64 i..]
+   by pubs[32 i..] over msgs[msg_off[i] .. + msg_sz[i]).  Optionally, with
+   txn_cnt > 0 at submit, transactions group consecutive signatures:
+   transaction t owns [txn_first[t], txn_first[t] + txn_sig_cnt[t]) and
+   gets fd_ed25519_verify_batch_single_msg's code in txn_out[t] (a count of
+   0 or > 16 gives ERR_SIG, such transactions stage no signatures).  After
+   poll returns the slot, sig_out / txn_out hold the codes. */
+typedef struct {
+  unsigned char *  msgs;
+  unsigned long *  msg_off;
+  unsigned int *   msg_sz;
+  unsigned char *  sigs;
+  unsigned char *  pubs;
+  unsigned int *   txn_first;
+  unsigned int *   txn_sig_cnt;
+  signed char *    sig_out;
+  signed char *    txn_out;
+  unsigned long    sig_cap;
+  unsigned long    msg_cap;
+  unsigned long    txn_cap;
+  /* set by submit */
+  unsigned long    sig_cnt;
+  unsigned long    msg_bytes;
+  unsigned long    txn_cnt;
+  unsigned long    seq;        /* submission number, 0, 1, 2, ...         */
+  double           t_submit;   /* CLOCK_MONOTONIC seconds at submit        */
+  double           t_done;     /* ... when poll saw the batch complete     */
+  unsigned long    user;       /* caller cookie, untouched                 */
+} fd_ed25519_hip_slot_t;
+
+/* slot_cnt batches (1..8) of up to sig_cap signatures, msg_cap message
+   bytes and txn_cap transactions each, on HIP device `device`; each slot
+   owns an engine (its own stream and work arrays), so the batches in
+   flight run concurrently.  NULL on failure (fd_ed25519_hip_last_error). */
+fd_ed25519_hip_pipe_t *
+fd_ed25519_hip_pipe_new( int device, unsigned slot_cnt, unsigned long sig_cap, unsigned long msg_cap,
+                         unsigned long txn_cap, int flags );
+
+void
+fd_ed25519_hip_pipe_delete( fd_ed25519_hip_pipe_t * pipe );
+
+/* The next slot in ring order if it is free, else NULL. */
+fd_ed25519_hip_slot_t *
+fd_ed25519_hip_pipe_acquire( fd_ed25519_hip_pipe_t * pipe );
+
+/* Enqueues H2D, verification (and the per-transaction combine if
+   txn_cnt>0) and D2H of an acquired slot; returns immediately. */
+int
+fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot,
+                            unsigned long sig_cnt, unsigned long msg_bytes, unsigned long txn_cnt );
+
+/* The oldest submitted slot once its results are on the host (wait != 0:
+   block until it is), else NULL.  Slots come back in submission order. */
+fd_ed25519_hip_slot_t *
+fd_ed25519_hip_pipe_poll( fd_ed25519_hip_pipe_t * pipe, int wait );
+
+/* Returns a polled slot to the free ring. */
+void
+fd_ed25519_hip_pipe_release( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot );
+
+unsigned
+fd_ed25519_hip_pipe_in_flight( fd_ed25519_hip_pipe_t const * pipe );
+
+/* ---- txn -------------------------------------------------------------- */
+
+/* The fields of fd_txn_t (src/ballet/txn/fd_txn.h) the verify tile reads. */
+typedef struct {
+  unsigned char  transaction_version;   /* 0xFF legacy, 0x00 v0 */
+  unsigned char  signature_cnt;
+  unsigned short signature_off;
+  unsigned short message_off;
+  unsigned char  readonly_signed_cnt;
+  unsigned char  readonly_unsigned_cnt;
+  unsigned short acct_addr_cnt;
+  unsigned short acct_addr_off;
+  unsigned short recent_blockhash_off;
+  unsigned short instr_cnt;
+  unsigned char  addr_table_lookup_cnt;
+  unsigned char  addr_table_adtl_writable_cnt;
+  unsigned char  addr_table_adtl_cnt;
+} fd_ed25519_hip_txn_t;
+
+#define FD_ED25519_HIP_TXN_MTU (1232UL)
+
+/* Accepts exactly the payloads fd_txn_parse(payload, sz, out, NULL)
+   accepts (fd_txn_parse_core with allow_zero_signatures=0 and no trailing
+   bytes), returning 1 and the fields, else 0. */
+int
+fd_ed25519_hip_txn_parse( unsigned char const * payload, unsigned long payload_sz, fd_ed25519_hip_txn_t * out );
+
+/* tcache: the verify tile's HA dedup cache of the last `depth` tags
+   (map_cnt a power of two >= depth+2; the tile uses 16 / 64). */
+typedef struct fd_ed25519_hip_tcache fd_ed25519_hip_tcache_t;
+
+fd_ed25519_hip_tcache_t * fd_ed25519_hip_tcache_new( unsigned long depth, unsigned long map_cnt );
+void fd_ed25519_hip_tcache_delete( fd_ed25519_hip_tcache_t * tc );
+/* 1 if tag is present (FD_TCACHE_QUERY) */
+int  fd_ed25519_hip_tcache_query( fd_ed25519_hip_tcache_t const * tc, unsigned long tag );
+/* FD_TCACHE_INSERT: 1 if tag was already present (nothing changes), else
+   inserts it, evicting the oldest of depth tags, and returns 0 */
+int  fd_ed25519_hip_tcache_insert( fd_ed25519_hip_tcache_t * tc, unsigned long tag );
+
+/* ---- vtile ------------------------------------------------------------ */
+
+/* Verdicts of fd_txn_verify (src/app/fdctl/run/tiles/fd_verify.h:9-11),
+   plus the filters after_frag applies before it. */
+#define FD_ED25519_HIP_TXN_VERIFY_SUCCESS (0)
+#define FD_ED25519_HIP_TXN_VERIFY_FAILED  (-1)
+#define FD_ED25519_HIP_TXN_VERIFY_DEDUP   (-2)
+#define FD_ED25519_HIP_TXN_PARSE_FAILED   (-3)  /* after_frag: fd_txn_parse failed -> filtered */
+
+typedef struct fd_ed25519_hip_vtile fd_ed25519_hip_vtile_t;
+
+/* A verify tile's batched core on `device`: batches of up to batch_sigs
+   signatures, slot_cnt in flight, tcache of tcache_depth / tcache_map_cnt
+   (the reference: 16 / 64, fd_verify.h:6-7). */
+fd_ed25519_hip_vtile_t *
+fd_ed25519_hip_vtile_new( int device, unsigned slot_cnt, unsigned long batch_sigs, unsigned long tcache_depth,
+                          unsigned long tcache_map_cnt, int flags );
+
+void
+fd_ed25519_hip_vtile_delete( fd_ed25519_hip_vtile_t * vt );
+
+/* after_frag for one transaction payload: parse and stage it (copying the
+   payload into the open batch).  `cookie` comes back with its verdict.
+   Returns 1 if staged, 0 if it was answered immediately (parse failure:
+   the verdict is queued for the next vtile_poll in order).  May submit the
+   open batch when it is full; blocks only if every slot is in flight. */
+int
+fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
+                           unsigned long cookie );
+
+/* Submits the open batch if it holds any transaction and a slot is free
+   (wait != 0: waits for one).  Returns 1 if a batch was submitted. */
+int
+fd_ed25519_hip_vtile_flush( fd_ed25519_hip_vtile_t * vt, int wait );
+
+/* Completed verdicts, in frag order: up to max entries of (cookie,
+   verdict, dedup tag = first 8 signature bytes).  wait != 0 blocks for
+   the oldest batch in flight.  Returns the number written. */
+unsigned long
+fd_ed25519_hip_vtile_poll( fd_ed25519_hip_vtile_t * vt, int wait, unsigned long max, unsigned long * cookie,
+                           signed char * verdict, unsigned long * tag );
+
+/* Transactions staged or in flight whose verdicts have not been polled. */
+unsigned long
+fd_ed25519_hip_vtile_pending( fd_ed25519_hip_vtile_t const * vt );
+
+/* ---- ring + latency mode ------------------------------------------- */
+
+/* Latency mode: a producer thread publishes the txn
+   payloads into a tango-style mcache/dcache ring at a fixed offered rate
+   (txns/s; 0 = as fast as possible) with a publish timestamp; the vtile
+   thread pulls frags, stages them, submits a batch once it holds
+   batch_sigs signatures or the ring is drained and a slot is free, and
+   timestamps each verdict when the batch completes.  lat_s[i] is txn i's
+   publish -> verdict latency in seconds; verdict[i] its verdict. */
+typedef struct {
+  double        offered_txn_per_s;
+  double        achieved_txn_per_s;
+  double        achieved_sig_per_s;
+  double        seconds;
+  unsigned long txn_cnt;
+  unsigned long sig_cnt;
+  unsigned long batches;
+  unsigned long ring_overruns;     /* frags the consumer lost (must be 0) */
+} fd_ed25519_hip_latency_result_t;
+
+int
+fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_sigs,
+                            unsigned char const * payloads, unsigned long const * payload_off,
+                            unsigned int const * payload_sz, unsigned long txn_cnt, double offered_txn_per_s,
+                            unsigned long ring_depth, double * lat_s, signed char * verdict,
+                            fd_ed25519_hip_latency_result_t * res );
+
+/* ---- pool ------------------------------------------------------------- */
+
+/* Verifies n signatures (host SoA as in fd_ed25519_hip_verify_host) on
+   device_cnt GPUs: batches of batch_sigs signatures are dealt round-robin,
+   batch b to device devices[b % device_cnt]; one host thread per device
+   packs its batches into its pipe (slot_cnt in flight) and writes the
+   codes into out.  Returns 0 or an engine status; *seconds (optional) is
+   the wall time of the whole call. */
+int
+fd_ed25519_hip_pool_verify( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
+                            unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
+                            unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
+                            signed char * out, double * seconds );
+
+#ifdef __cplusplus
+}
+#endif
+#endif

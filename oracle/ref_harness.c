@@ -9,9 +9,16 @@
    Entry points wrap:
      fd_ed25519_verify                  src/ballet/ed25519/fd_ed25519.h:96-101
      fd_ed25519_verify_batch_single_msg src/ballet/ed25519/fd_ed25519.h:124-130
-     fd_ed25519_sign / public_from_private src/ballet/ed25519/fd_ed25519.h:41-73 */
+     fd_ed25519_sign / public_from_private src/ballet/ed25519/fd_ed25519.h:41-73
+     fd_txn_parse                       src/ballet/txn/fd_txn.h, fd_txn_parse.c
+     the verify tile's after_frag + fd_txn_verify, sequentially
+                                        src/app/fdctl/run/tiles/fd_verify.c:85-155,
+                                        src/app/fdctl/run/tiles/fd_verify.h:43-88 */
 
 #include "ballet/ed25519/fd_ed25519.h"
+#include "ballet/txn/fd_txn.h"
+#include "tango/tcache/fd_tcache.h"
+#include <stdlib.h>
 #include <pthread.h>
 #include <time.h>
 
@@ -85,4 +92,52 @@ fdref_verify_many( ulong n, uchar const * msgs, ulong const * off, uint const * 
   for( int t=0; t<nthreads; t++ ) pthread_join( th[t], NULL );
   clock_gettime( CLOCK_MONOTONIC, &t1 );
   return (t1.tv_sec - t0.tv_sec)*1000000000L + (t1.tv_nsec - t0.tv_nsec);
+}
+
+/* fd_txn_parse of one payload: returns the footprint (0 = rejected) and the
+   parsed fields the verify tile uses in fields[0..12]. */
+ulong
+fdref_txn_parse( uchar const * payload, ulong sz, ulong * fields ) {
+  static __thread uchar buf[ FD_TXN_MAX_SZ ] __attribute__((aligned(16)));
+  ulong r = fd_txn_parse( payload, sz, buf, NULL );
+  if( !r ) return 0UL;
+  fd_txn_t const * t = (fd_txn_t const *)buf;
+  fields[ 0] = t->transaction_version;   fields[ 1] = t->signature_cnt;        fields[ 2] = t->signature_off;
+  fields[ 3] = t->message_off;           fields[ 4] = t->readonly_signed_cnt;  fields[ 5] = t->readonly_unsigned_cnt;
+  fields[ 6] = t->acct_addr_cnt;         fields[ 7] = t->acct_addr_off;        fields[ 8] = t->recent_blockhash_off;
+  fields[ 9] = t->instr_cnt;             fields[10] = t->addr_table_lookup_cnt;
+  fields[11] = t->addr_table_adtl_writable_cnt;                                 fields[12] = t->addr_table_adtl_cnt;
+  return r;
+}
+
+/* The verify tile over n frags in order, as one tile sees them: after_frag's
+   parse filter (-3), then fd_txn_verify: tcache query (-2 DEDUP), batch
+   verify (-1 FAILED), tcache insert (-2 DEDUP on a duplicate, else 0). */
+void
+fdref_vtile_seq( ulong n, uchar const * payloads, ulong const * off, uint const * sz, ulong depth, ulong map_cnt,
+                 schar * verdict, ulong * tag_out ) {
+  ulong * ring = (ulong *)calloc( depth, sizeof(ulong) );
+  ulong * map  = (ulong *)calloc( map_cnt, sizeof(ulong) );
+  ulong oldest = 0UL;
+  static __thread uchar buf[ FD_TXN_MAX_SZ ] __attribute__((aligned(16)));
+  tsha();
+  for( ulong i=0UL; i<n; i++ ) {
+    uchar const * p = payloads + off[i];
+    tag_out[i] = 0UL;
+    if( !fd_txn_parse( p, sz[i], buf, NULL ) ) { verdict[i] = -3; continue; }
+    fd_txn_t const * t = (fd_txn_t const *)buf;
+    uchar const * signatures = p + t->signature_off;
+    ulong tag = *(ulong const *)signatures;
+    tag_out[i] = tag;
+    int dup; ulong map_idx;
+    FD_TCACHE_QUERY( dup, map_idx, map, map_cnt, tag );
+    (void)map_idx;
+    if( dup ) { verdict[i] = -2; continue; }
+    int res = fd_ed25519_verify_batch_single_msg( p + t->message_off, (ulong)sz[i] - t->message_off, signatures,
+                                                  p + t->acct_addr_off, tl_shas, t->signature_cnt );
+    if( res!=FD_ED25519_SUCCESS ) { verdict[i] = -1; continue; }
+    FD_TCACHE_INSERT( dup, oldest, ring, depth, map, map_cnt, tag );
+    verdict[i] = dup ? (schar)-2 : (schar)0;
+  }
+  free( ring ); free( map );
 }

@@ -1,0 +1,125 @@
+"""GPU parity of the verify-tile layer (include/fd_ed25519_hip_tile.h): the
+batched tile's verdict stream against the reference tile replayed
+sequentially on the same frags (oracle/_ref: fd_txn_parse + FD_TCACHE_* +
+fd_ed25519_verify_batch_single_msg), the latency mode through the ring,
+the pipe, and the multi-device pool."""
+import random
+
+import numpy as np
+import pytest
+
+from txn_util import Signer, random_txn, ref_lib, ref_vtile, tile_workload
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def tile():
+    from firedancer_amd import tile as t
+    return t
+
+
+@pytest.fixture(scope="module")
+def ref():
+    lib = ref_lib()
+    if lib is None:
+        pytest.skip("oracle/_ref not built")
+    return lib
+
+
+@pytest.fixture(scope="module")
+def frags(oracle):
+    return tile_workload(oracle, 2024, 3000)
+
+
+@pytest.mark.parametrize("batch_sigs,slot_cnt", [(64, 3), (1000, 2), (16, 1), (4096, 4)])
+def test_vtile_matches_reference_tile(tile, ref, frags, batch_sigs, slot_cnt):
+    want, want_tags = ref_vtile(ref, frags)
+    vt = tile.VerifyTile(0, slot_cnt=slot_cnt, batch_sigs=batch_sigs)
+    got, tags = vt.run(frags)
+    vt.close()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:10]]
+    ok = want != -3
+    assert np.array_equal(tags[ok], want_tags[ok])
+
+
+def test_vtile_dedup_across_batches(tile, ref, oracle):
+    """Duplicates of a transaction in an earlier batch and in the same batch,
+    and copies that come back after the tcache (depth 16) evicted them."""
+    rng = random.Random(1)
+    signer = Signer(oracle, 1)
+    base = [random_txn(signer, rng, 1) for _ in range(40)]
+    seq = base[:5] + [base[0]] + base[5:21] + [base[4]] + base[21:38] + [base[20], base[21], base[30], base[38],
+                                                                         base[38]]
+    want, _ = ref_vtile(ref, seq)
+    vt = tile.VerifyTile(0, slot_cnt=2, batch_sigs=4)
+    got, _ = vt.run(seq)
+    vt.close()
+    assert got.tolist() == want.tolist()
+    assert want.tolist()[5] == -2 and want.tolist()[-3:] == [-2, 0, -2]  # dups of base[0], base[30], base[38]
+    assert want.tolist()[22] == 0                                         # base[4] came back after eviction
+
+
+def test_latency_run(tile, ref, frags):
+    frags = [p for p in frags if len(p) <= tile.TXN_MTU]  # a dcache frag is at most the TPU MTU
+    want, _ = ref_vtile(ref, frags)
+    lat, got, res = tile.latency_run(frags, offered_txn_per_s=20000.0, batch_sigs=256, slot_cnt=3, ring_depth=1024)
+    assert res["ring_overruns"] == 0
+    assert np.array_equal(got, want)
+    assert (lat > 0).all() and res["batches"] > 1
+    assert res["achieved_txn_per_s"] > 0.5 * 20000.0
+
+
+def test_latency_run_unpaced(tile, ref, frags):
+    frags = [p for p in frags if len(p) <= tile.TXN_MTU]
+    want, _ = ref_vtile(ref, frags)
+    lat, got, res = tile.latency_run(frags, offered_txn_per_s=0.0, batch_sigs=512, slot_cnt=4, ring_depth=256)
+    assert res["ring_overruns"] == 0
+    assert np.array_equal(got, want)
+
+
+def test_pool_matches_engine(tile, oracle):
+    from firedancer_amd import ed25519
+    rng = random.Random(9)
+    signer = Signer(oracle, 9)
+    n = 3000
+    msgs, off, sz, sigs, pubs = bytearray(), [], [], bytearray(), bytearray()
+    for i in range(n):
+        priv, pub = signer.key() if i % 50 == 0 else signer.keys[-1]
+        m = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 300)))
+        s = bytearray(signer.sign(m, priv, pub))
+        if i % 9 == 4:
+            s[rng.randrange(64)] ^= 1
+        off.append(len(msgs)); sz.append(len(m)); msgs += m; sigs += s; pubs += pub
+    msgs = np.frombuffer(bytes(msgs), np.uint8)
+    off, sz = np.array(off, np.uint64), np.array(sz, np.uint32)
+    sigs, pubs = np.frombuffer(bytes(sigs), np.uint8), np.frombuffer(bytes(pubs), np.uint8)
+    eng = ed25519.Engine(0, max_chunk=1 << 12)
+    want = eng.verify_host(msgs, off, sz, sigs, pubs)
+    eng.close()
+    for devices, batch in [([0], 1000), ([0, 0], 256), ([0, 0, 0], 7)]:
+        got, sec = tile.pool_verify(devices, msgs, off, sz, sigs, pubs, batch_sigs=batch, slot_cnt=2)
+        assert np.array_equal(got, want), devices
+        assert sec > 0
+    assert (want != 0).sum() > 0
+
+
+def test_txn_payload_generator(tile, ref):
+    """bench.py's C5 transactions: GPU-signed, parseable, all valid, and the
+    reference tile agrees."""
+    from firedancer_amd import ed25519, workload
+    eng = ed25519.Engine(0, max_chunk=1 << 12)
+    for signers in (1, 3):
+        pay, size = workload.txn_payloads(eng, 300, 5, msg_sz=200 + 64 * signers, signers=signers)
+        payloads = [bytes(p) for p in pay]
+        t = tile.txn_parse(payloads[0])
+        assert t is not None and t["signature_cnt"] == signers
+        assert size - t["message_off"] == 200 + 64 * signers
+        want, _ = ref_vtile(ref, payloads)
+        assert (want == 0).all()
+        vt = tile.VerifyTile(0, slot_cnt=2, batch_sigs=128)
+        got, _ = vt.run(payloads)
+        vt.close()
+        assert (got == 0).all()
+    eng.close()
