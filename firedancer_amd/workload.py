@@ -21,6 +21,8 @@ SIZE_SALT = np.uint64(0xD1B54A32D192ED03)
 CONFIGS = {
     "C1": dict(n=16384, lo=200, hi=200, ppm=0),
     "C2": dict(n=1 << 20, lo=64, hi=1232, ppm=20000),
+    # the C2 distribution as one 64M stream split over the ranks (strong scaling)
+    "C4": dict(n=64 << 20, lo=64, hi=1232, ppm=20000, total=True),
 }
 
 # invalid classes of fd_ed25519_corrupt_kernel -> reference AVX-512 code
