@@ -114,9 +114,21 @@ def mutate(rng, p):
     return bytes(p)
 
 
-def ref_lib():
-    """The reference compiled from its sources (oracle/_ref), or None."""
-    path = os.path.join(REPO, "oracle", "_ref", "libfdref_portable.so")
+def cpu_has_avx512ifma():
+    try:
+        flags = next(l for l in open("/proc/cpuinfo") if l.startswith("flags")).split()
+        return "avx512ifma" in flags and "avx512vbmi" in flags
+    except (OSError, StopIteration):
+        return False
+
+
+def ref_lib(flavour="portable"):
+    """The reference compiled from its sources (oracle/_ref), or None.
+    flavour: "portable" (fiat backend) or "avx512" (the production r43x6
+    backend; None if this CPU lacks AVX-512 IFMA)."""
+    if flavour == "avx512" and not cpu_has_avx512ifma():
+        return None
+    path = os.path.join(REPO, "oracle", "_ref", f"libfdref_{flavour}.so")
     if not os.path.exists(path):
         return None
     lib = ctypes.CDLL(path)
