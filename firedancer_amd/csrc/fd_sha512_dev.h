@@ -38,7 +38,35 @@ __constant__ uint64_t fd_sha512_dev_k[80] = {
   0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL,
 };
 
-FD_DEV uint64_t sha_ror(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+/* 64-bit words live in VGPR pairs; the rotations, shifts and 3-input
+   boolean functions are written on the 32-bit halves so that each costs
+   one full-rate op per half: a rotation is two v_alignbit_b32 (funnel
+   shifts), xor3 / maj / ch one v_bitop3_b32 each (gfx950's 3-input LUT op,
+   truth-table index = a<<2 | b<<1 | c).  Left to itself LLVM builds the
+   rotations from 64-bit shifts and ors. */
+FD_DEV uint32_t sha_lo(uint64_t x) { return (uint32_t)x; }
+FD_DEV uint32_t sha_hi(uint64_t x) { return (uint32_t)(x >> 32); }
+FD_DEV uint64_t sha_pair(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
+
+FD_DEV uint64_t sha_ror(uint64_t x, int n) {
+  const uint32_t lo = sha_lo(x), hi = sha_hi(x);
+  if (n < 32) return sha_pair(__builtin_amdgcn_alignbit(lo, hi, n), __builtin_amdgcn_alignbit(hi, lo, n));
+  return sha_pair(__builtin_amdgcn_alignbit(hi, lo, n - 32), __builtin_amdgcn_alignbit(lo, hi, n - 32));
+}
+
+FD_DEV uint64_t sha_shr(uint64_t x, int n) {  /* n < 32 */
+  const uint32_t lo = sha_lo(x), hi = sha_hi(x);
+  return sha_pair(hi >> n, __builtin_amdgcn_alignbit(hi, lo, n));
+}
+
+template <int LUT>
+FD_DEV uint64_t sha_bitop3(uint64_t a, uint64_t b, uint64_t c) {
+  return sha_pair(__builtin_amdgcn_bitop3_b32(sha_hi(a), sha_hi(b), sha_hi(c), LUT),
+                  __builtin_amdgcn_bitop3_b32(sha_lo(a), sha_lo(b), sha_lo(c), LUT));
+}
+#define SHA_XOR3 0x96
+#define SHA_MAJ  0xE8
+#define SHA_CH   0xCA
 
 FD_DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -52,15 +80,15 @@ FD_DEV void sha512_block(uint64_t (&h)[8], uint64_t (&w)[16]) {
     for (int r = 0; r < 16; r++) {
       if (r0 > 0) {
         const uint64_t w15 = w[(r + 1) & 15], w2 = w[(r + 14) & 15];
-        const uint64_t s0 = sha_ror(w15, 1) ^ sha_ror(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = sha_ror(w2, 19) ^ sha_ror(w2, 61) ^ (w2 >> 6);
+        const uint64_t s0 = sha_bitop3<SHA_XOR3>(sha_ror(w15, 1), sha_ror(w15, 8), sha_shr(w15, 7));
+        const uint64_t s1 = sha_bitop3<SHA_XOR3>(sha_ror(w2, 19), sha_ror(w2, 61), sha_shr(w2, 6));
         w[r] += s0 + w[(r + 9) & 15] + s1;
       }
-      const uint64_t S1 = sha_ror(e, 14) ^ sha_ror(e, 18) ^ sha_ror(e, 41);
-      const uint64_t ch = (e & f) ^ (~e & g);
+      const uint64_t S1 = sha_bitop3<SHA_XOR3>(sha_ror(e, 14), sha_ror(e, 18), sha_ror(e, 41));
+      const uint64_t ch = sha_bitop3<SHA_CH>(e, f, g);
       const uint64_t t1 = hh + S1 + ch + fd_sha512_dev_k[r0 + r] + w[r];
-      const uint64_t S0 = sha_ror(a, 28) ^ sha_ror(a, 34) ^ sha_ror(a, 39);
-      const uint64_t mj = (a & b) ^ (c & (a ^ b));
+      const uint64_t S0 = sha_bitop3<SHA_XOR3>(sha_ror(a, 28), sha_ror(a, 34), sha_ror(a, 39));
+      const uint64_t mj = sha_bitop3<SHA_MAJ>(a, b, c);
       hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
     }
   }
