@@ -13,6 +13,9 @@
      5. R' = [k](-A) + [S]B            (fd_ed25519_double_scalar_mul_base)
      6. R' == R projectively           (fd_ed25519_point_eq_z1)
 
+   Steps 2-3 for R and step 6 are done together, without decompressing R,
+   by comparing the encoding of R' with R's bytes (fin, below).
+
    Step 5 uses fixed signed windows instead of the reference's sliding
    wNAF so that every lane of a wave executes the same additions: k in
    radix 16 (64 digits in [-8,8], table [0..8](-A) per lane in HBM) and S in
@@ -29,15 +32,17 @@
 
 
 /* ------------------------------------------------------------------------
-   Phase kernels.  A batch is verified by three launches on one stream,
-   each with its own register budget, handing ~200 B per signature through
-   the work arrays in HBM (fd_ed25519_verify_params_t):
+   Phase kernels.  A batch is verified by four phases on one stream, each
+   kernel with its own register budget, handing ~240 B per signature
+   through the work arrays in HBM (fd_ed25519_verify_params_t):
 
      hash    one lane per signature: S < L, k = SHA-512(R||A||M) mod L
-     decode  one lane per point (2n lanes: A then R): decompression and
-             the reference's acceptance / small-order rules
-     dsm     one lane per signature, persistent: [k](-A) + [S]B, compare
-             with R, fold every flag into the reference's error code */
+     decode  one lane per public key A: decompression and the reference's
+             acceptance / small-order rules
+     dsm     one lane per signature, persistent: R' = [k](-A) + [S]B,
+             written projective with the S / A status
+     fin     R' in affine by per-lane batched inversion, compared with R's
+             encoding; rfix decodes R for the few signatures that need it */
 
 #define FD_PF_FAIL  1u
 #define FD_PF_SMALL 2u

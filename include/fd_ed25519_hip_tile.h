@@ -129,13 +129,20 @@ fd_ed25519_hip_txn_parse( unsigned char const * payload, unsigned long payload_s
    (map_cnt a power of two >= depth+2; the tile uses 16 / 64). */
 typedef struct fd_ed25519_hip_tcache fd_ed25519_hip_tcache_t;
 
-fd_ed25519_hip_tcache_t * fd_ed25519_hip_tcache_new( unsigned long depth, unsigned long map_cnt );
-void fd_ed25519_hip_tcache_delete( fd_ed25519_hip_tcache_t * tc );
+fd_ed25519_hip_tcache_t *
+fd_ed25519_hip_tcache_new( unsigned long depth, unsigned long map_cnt );
+
+void
+fd_ed25519_hip_tcache_delete( fd_ed25519_hip_tcache_t * tc );
+
 /* 1 if tag is present (FD_TCACHE_QUERY) */
-int  fd_ed25519_hip_tcache_query( fd_ed25519_hip_tcache_t const * tc, unsigned long tag );
+int
+fd_ed25519_hip_tcache_query( fd_ed25519_hip_tcache_t const * tc, unsigned long tag );
+
 /* FD_TCACHE_INSERT: 1 if tag was already present (nothing changes), else
    inserts it, evicting the oldest of depth tags, and returns 0 */
-int  fd_ed25519_hip_tcache_insert( fd_ed25519_hip_tcache_t * tc, unsigned long tag );
+int
+fd_ed25519_hip_tcache_insert( fd_ed25519_hip_tcache_t * tc, unsigned long tag );
 
 /* ---- vtile ------------------------------------------------------------ */
 
