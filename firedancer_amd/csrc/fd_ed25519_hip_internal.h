@@ -109,6 +109,31 @@ int fd_ed25519_hip_launch_txn_combine( int8_t const * d_sig_codes, uint32_t cons
                                        uint32_t const * d_txn_cnt, int8_t * d_txn_out, uint64_t ntxn,
                                        void * stream );
 
+/* ---- raw transactions (fd_ed25519_txn.hip) ---- */
+
+/* per-transaction code for a payload fd_txn_parse rejects (never an
+   ed25519 code) */
+#define FD_ED25519_TXN_PARSE_FAILED_CODE (-4)
+
+typedef struct {
+  uint8_t const *  payloads;   /* payload bytes, readable 16 B past each   */
+  uint64_t const * pay_off;    /* [ntxn]                                   */
+  uint32_t const * pay_sz;     /* [ntxn]                                   */
+  uint32_t const * txn_first;  /* [ntxn] first signature slot               */
+  uint32_t const * txn_cnt;    /* [ntxn] payload byte 0 (slots: 1..16 -> cnt, else 0) */
+  uint64_t         ntxn;
+  uint8_t *        sigs;       /* [slots][64] out, 16-B aligned            */
+  uint8_t *        pubs;       /* [slots][32] out                          */
+  uint64_t *       msg_off;    /* [slots] out: into payloads                */
+  uint32_t *       msg_sz;     /* [slots] out                               */
+  uint8_t *        parse_ok;   /* [ntxn] out                                */
+} fd_ed25519_txn_stage_params_t;
+
+int fd_ed25519_hip_launch_txn_stage( fd_ed25519_txn_stage_params_t const * p, void * stream );
+int fd_ed25519_hip_launch_txn_finish( int8_t const * d_sig_codes, uint32_t const * d_txn_first,
+                                      uint32_t const * d_txn_cnt, uint8_t const * d_parse_ok, int8_t * d_txn_out,
+                                      uint64_t ntxn, void * stream );
+
 /* ---- generator (fd_ed25519_gen.hip) ---- */
 
 typedef struct {

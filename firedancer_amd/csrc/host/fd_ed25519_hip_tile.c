@@ -7,6 +7,7 @@
 
 #define _GNU_SOURCE
 #include "../../../include/fd_ed25519_hip_tile.h"
+#include "../fd_ed25519_hip_internal.h"
 
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
@@ -66,6 +67,9 @@ typedef struct {
   unsigned int *            d_tfirst;
   unsigned int *            d_tcnt;
   signed char *             d_tout;
+  unsigned long *           d_toff;    /* raw mode: per-transaction payload offset */
+  unsigned int *            d_tsz;     /* raw mode: per-transaction payload size   */
+  unsigned char *           d_pok;     /* raw mode: fd_txn_parse accepted          */
 } pipe_slot_t;
 
 struct fd_ed25519_hip_pipe {
@@ -86,6 +90,7 @@ pipe_slot_free( pipe_slot_t * s ) {
   hipHostFree( p->txn_out );
   hipFree( s->d_msgs ); hipFree( s->d_off ); hipFree( s->d_sz ); hipFree( s->d_sigs ); hipFree( s->d_pubs );
   hipFree( s->d_out ); hipFree( s->d_tfirst ); hipFree( s->d_tcnt ); hipFree( s->d_tout );
+  hipFree( s->d_toff ); hipFree( s->d_tsz ); hipFree( s->d_pok );
   if( s->ev ) hipEventDestroy( s->ev );
   if( s->eng ) fd_ed25519_hip_engine_delete( s->eng );
 }
@@ -127,6 +132,9 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   TCHK( hipMalloc( (void **)&s->d_tfirst, 4UL*tc         ), "hipMalloc" );
   TCHK( hipMalloc( (void **)&s->d_tcnt,   4UL*tc         ), "hipMalloc" );
   TCHK( hipMalloc( (void **)&s->d_tout,   tc             ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_toff,   8UL*tc         ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_tsz,    4UL*tc         ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_pok,    tc             ), "hipMalloc" );
   TCHK( hipEventCreateWithFlags( &s->ev, hipEventDisableTiming ), "hipEventCreate" );
   s->state = SLOT_FREE;
   return FD_ED25519_HIP_OK;
@@ -198,6 +206,54 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   return FD_ED25519_HIP_OK;
 }
 
+int
+fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot,
+                                 unsigned long txn_cnt, unsigned long payload_bytes ) {
+  pipe_slot_t * s = (pipe_slot_t *)slot;
+  if( s->state!=SLOT_FILL || txn_cnt>slot->txn_cap || txn_cnt>slot->sig_cap || payload_bytes>slot->msg_cap )
+    return FD_ED25519_HIP_ERR_INVAL;
+  /* signature slots from byte 0 of each payload (its signature count if
+     fd_txn_parse accepts it; 0 or > 16 reserve none) */
+  unsigned long slots = 0UL;
+  for( unsigned long t=0UL; t<txn_cnt; t++ ) {
+    unsigned int c = slot->msg_sz[ t ] ? slot->msgs[ slot->msg_off[ t ] ] : 0U;
+    slot->txn_first  [ t ] = (unsigned int)slots;
+    slot->txn_sig_cnt[ t ] = c;
+    if( c>=1U && c<=16U ) slots += c;
+  }
+  if( slots>slot->sig_cap ) return FD_ED25519_HIP_ERR_INVAL;
+  TCHK( hipSetDevice( pipe->device ), "hipSetDevice" );
+  hipStream_t st = (hipStream_t)fd_ed25519_hip_engine_stream( s->eng );
+  slot->sig_cnt = slots; slot->msg_bytes = payload_bytes; slot->txn_cnt = txn_cnt;
+  slot->seq = pipe->seq++;
+  slot->t_submit = now_s();
+  if( txn_cnt ) {
+    TCHK( hipMemcpyAsync( s->d_msgs,   slot->msgs,        payload_bytes ? payload_bytes : 1UL, hipMemcpyHostToDevice, st ), "H2D payloads" );
+    TCHK( hipMemcpyAsync( s->d_toff,   slot->msg_off,     8UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D toff" );
+    TCHK( hipMemcpyAsync( s->d_tsz,    slot->msg_sz,      4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tsz" );
+    TCHK( hipMemcpyAsync( s->d_tfirst, slot->txn_first,   4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tfirst" );
+    TCHK( hipMemcpyAsync( s->d_tcnt,   slot->txn_sig_cnt, 4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tcnt" );
+    fd_ed25519_txn_stage_params_t sp;
+    sp.payloads = s->d_msgs; sp.pay_off = s->d_toff; sp.pay_sz = s->d_tsz; sp.txn_first = s->d_tfirst;
+    sp.txn_cnt = s->d_tcnt; sp.ntxn = txn_cnt; sp.sigs = s->d_sigs; sp.pubs = s->d_pubs; sp.msg_off = s->d_off;
+    sp.msg_sz = s->d_sz; sp.parse_ok = s->d_pok;
+    int err = fd_ed25519_hip_launch_txn_stage( &sp, st );
+    if( err ) return tile_fail( "txn_stage launch", (hipError_t)err );
+    if( slots ) {
+      err = fd_ed25519_hip_verify_dev( s->eng, slots, s->d_msgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
+      if( err ) return err;
+    }
+    err = fd_ed25519_hip_launch_txn_finish( s->d_out, s->d_tfirst, s->d_tcnt, s->d_pok, s->d_tout, txn_cnt, st );
+    if( err ) return tile_fail( "txn_finish launch", (hipError_t)err );
+    TCHK( hipMemcpyAsync( slot->txn_out, s->d_tout, txn_cnt, hipMemcpyDeviceToHost, st ), "D2H tout" );
+    if( slots ) TCHK( hipMemcpyAsync( slot->sig_out, s->d_out, slots, hipMemcpyDeviceToHost, st ), "D2H out" );
+  }
+  TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
+  s->state = SLOT_BUSY;
+  pipe->in_flight++;
+  return FD_ED25519_HIP_OK;
+}
+
 fd_ed25519_hip_slot_t *
 fd_ed25519_hip_pipe_poll( fd_ed25519_hip_pipe_t * pipe, int wait ) {
   pipe_slot_t * s = &pipe->slot[ pipe->next_poll % pipe->slot_cnt ];
@@ -229,130 +285,14 @@ fd_ed25519_hip_pipe_in_flight( fd_ed25519_hip_pipe_t const * pipe ) {
 }
 
 /* ======================================================================
-   txn: fd_txn_parse restated (src/ballet/txn/fd_txn_parse.c:6-244).
-   Each rule below is the reference's CHECK at the cited line; a payload is
-   accepted iff every rule holds.  Offsets are only read after the bytes are
-   known to be present. */
+   txn: fd_txn_parse restated once in fd_txn_parse_core.h (shared with the
+   device staging kernel, fd_ed25519_txn.hip). */
 
-/* compact-u16 (src/ballet/txn/fd_compact_u16.h): 1-3 bytes, 7 bits per
-   byte little-endian, minimal encoding required; returns the encoded size
-   (0: malformed / truncated) */
-static unsigned long
-cu16_decode( unsigned char const * b, unsigned long avail, unsigned * val ) {
-  if( avail>=1UL && !(b[0] & 0x80U) ) { *val = b[0]; return 1UL; }
-  if( avail>=2UL && !(b[1] & 0x80U) ) {
-    if( !b[1] ) return 0UL;                                      /* non-minimal */
-    *val = (b[0] & 0x7FU) | ((unsigned)b[1] << 7);
-    return 2UL;
-  }
-  if( avail>=3UL && !(b[2] & 0xFCU) ) {
-    if( !b[2] ) return 0UL;                                      /* non-minimal */
-    *val = (b[0] & 0x7FU) | ((unsigned)(b[1] & 0x7FU) << 7) | ((unsigned)b[2] << 14);
-    return 3UL;
-  }
-  return 0UL;
-}
-
-#define TXN_SIG_MAX       127UL
-#define TXN_ACCT_MAX      128UL
-#define TXN_INSTR_MAX      64UL
-#define TXN_LUT_MAX       127UL
+#include "../fd_txn_parse_core.h"
 
 int
 fd_ed25519_hip_txn_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn_t * out ) {
-  unsigned long i = 0UL, n;
-  unsigned v;
-#define HAVE( k ) ( (unsigned long)(k) <= sz - i )
-#define CU16( dst ) do { n = cu16_decode( p + i, sz - i, &v ); if( !n ) return 0; (dst) = v; i += n; } while(0)
-  if( sz>FD_ED25519_HIP_TXN_MTU ) return 0;                                             /* :85 */
-  if( !HAVE( 1 ) ) return 0;
-  unsigned sig_cnt = p[ i++ ];
-  if( sig_cnt<1U || sig_cnt>TXN_SIG_MAX ) return 0;                                    /* :94 */
-  if( !HAVE( 64UL*sig_cnt ) ) return 0;
-  unsigned long sig_off = i;  i += 64UL*sig_cnt;
-  unsigned long msg_off = i;
-  if( !HAVE( 1 ) ) return 0;
-  unsigned b0 = p[ i++ ];
-  unsigned char ver;
-  if( b0 & 0x80U ) {                                                                     /* :102-107 */
-    ver = (unsigned char)(b0 & 0x7FU);
-    if( ver!=0U ) return 0;
-    if( !HAVE( 1 ) ) return 0;
-    if( p[ i ]!=sig_cnt ) return 0;
-    i++;
-  } else {
-    ver = 0xFF;
-    if( b0!=sig_cnt ) return 0;                                                          /* :110 */
-  }
-  if( !HAVE( 1 ) ) return 0;
-  unsigned ro_signed = p[ i++ ];
-  if( !(ro_signed<sig_cnt) ) return 0;                                                   /* :114 */
-  if( !HAVE( 1 ) ) return 0;
-  unsigned ro_unsigned = p[ i++ ];
-  unsigned acct_cnt;  CU16( acct_cnt );
-  if( !(sig_cnt<=acct_cnt && acct_cnt<=TXN_ACCT_MAX) ) return 0;                         /* :120 */
-  if( sig_cnt + ro_unsigned > acct_cnt ) return 0;                                       /* :121 */
-  if( !HAVE( 32UL*acct_cnt ) ) return 0;
-  unsigned long acct_off = i;  i += 32UL*acct_cnt;
-  if( !HAVE( 32 ) ) return 0;
-  unsigned long bh_off = i;  i += 32UL;
-  unsigned instr_cnt;  CU16( instr_cnt );
-  if( instr_cnt>TXN_INSTR_MAX ) return 0;                                                /* :132 */
-  if( !HAVE( 3UL*instr_cnt ) ) return 0;                                                 /* :133 */
-  if( !(acct_cnt > (instr_cnt ? 1U : 0U)) ) return 0;                                    /* :136 */
-  unsigned max_acct = 0U;
-  for( unsigned j=0U; j<instr_cnt; j++ ) {
-    if( !HAVE( 3 ) ) return 0;
-    unsigned prog = p[ i++ ];
-    unsigned ia; CU16( ia );
-    if( !HAVE( ia ) ) return 0;
-    for( unsigned k=0U; k<ia; k++ ) if( p[ i+k ]>max_acct ) max_acct = p[ i+k ];
-    i += ia;
-    unsigned dsz; CU16( dsz );
-    if( !HAVE( dsz ) ) return 0;
-    i += dsz;
-    if( !(0U<prog && prog<acct_cnt) ) return 0;                                          /* :175 */
-  }
-  unsigned lut_cnt = 0U;
-  unsigned long adtl = 0UL, adtl_w = 0UL;
-  if( ver==0U ) {
-    CU16( lut_cnt );
-    if( lut_cnt>TXN_LUT_MAX ) return 0;                                                  /* :199 */
-    if( !HAVE( 34UL*lut_cnt ) ) return 0;
-    for( unsigned j=0U; j<lut_cnt; j++ ) {
-      if( !HAVE( 32 ) ) return 0;
-      i += 32UL;
-      unsigned w, r;
-      CU16( w );  if( !HAVE( w ) ) return 0;  i += w;
-      CU16( r );  if( !HAVE( r ) ) return 0;  i += r;
-      if( w > TXN_ACCT_MAX - acct_cnt ) return 0;                                        /* :212 */
-      if( r > TXN_ACCT_MAX - acct_cnt ) return 0;
-      if( w + r < 1U ) return 0;
-      adtl_w += w;
-      adtl   += (unsigned long)w + r;
-    }
-  }
-  if( i!=sz ) return 0;                                                                  /* :229 */
-  if( acct_cnt + adtl > TXN_ACCT_MAX ) return 0;                                         /* :231 */
-  if( !(max_acct < acct_cnt + adtl) ) return 0;                                          /* :234 */
-#undef HAVE
-#undef CU16
-  if( out ) {
-    out->transaction_version          = ver;
-    out->signature_cnt                = (unsigned char)sig_cnt;
-    out->signature_off                = (unsigned short)sig_off;
-    out->message_off                  = (unsigned short)msg_off;
-    out->readonly_signed_cnt          = (unsigned char)ro_signed;
-    out->readonly_unsigned_cnt        = (unsigned char)ro_unsigned;
-    out->acct_addr_cnt                = (unsigned short)acct_cnt;
-    out->acct_addr_off                = (unsigned short)acct_off;
-    out->recent_blockhash_off         = (unsigned short)bh_off;
-    out->instr_cnt                    = (unsigned short)instr_cnt;
-    out->addr_table_lookup_cnt        = (unsigned char)lut_cnt;
-    out->addr_table_adtl_writable_cnt = (unsigned char)adtl_w;
-    out->addr_table_adtl_cnt          = (unsigned char)adtl;
-  }
-  return 1;
+  return fd_txn_core_parse( p, sz, out );
 }
 
 /* ======================================================================
@@ -470,6 +410,7 @@ struct fd_ed25519_hip_vtile {
   fd_ed25519_hip_slot_t *   open;       /* acquired, not yet submitted */
   unsigned long             open_seq;   /* seq the open slot will get   */
   unsigned long             batch_sigs;
+  int                       gpu_parse;  /* FD_ED25519_HIP_VTILE_GPU_PARSE: raw payloads to the device */
   vrec_t *                  q;          /* circular FIFO of records */
   unsigned long             q_cap, q_head, q_cnt;
   unsigned long             resolved_head;  /* records [q_head, q_head+resolved_head) are resolved */
@@ -481,8 +422,9 @@ fd_ed25519_hip_vtile_new( int device, unsigned slot_cnt, unsigned long batch_sig
   fd_ed25519_hip_vtile_t * vt = (fd_ed25519_hip_vtile_t *)calloc( 1, sizeof(*vt) );
   if( !vt ) return NULL;
   vt->batch_sigs = batch_sigs ? batch_sigs : 4096UL;
+  vt->gpu_parse  = !!(flags & FD_ED25519_HIP_VTILE_GPU_PARSE);
   vt->pipe = fd_ed25519_hip_pipe_new( device, slot_cnt, vt->batch_sigs, vt->batch_sigs*FD_ED25519_HIP_TXN_MTU,
-                                      vt->batch_sigs, flags );
+                                      vt->batch_sigs, flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE );
   vt->tc   = fd_ed25519_hip_tcache_new( tcache_depth, tcache_map_cnt );
   vt->q_cap = 1024UL;
   vt->q = (vrec_t *)malloc( vt->q_cap*sizeof(vrec_t) );
@@ -541,7 +483,8 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
     if( r->slot_seq!=s->seq ) break;
     int code = s->txn_out[ r->txn_idx ];
     int v;
-    if( fd_ed25519_hip_tcache_query( vt->tc, r->tag ) )      v = FD_ED25519_HIP_TXN_VERIFY_DEDUP;
+    if( code==FD_ED25519_HIP_TXN_CODE_PARSE_FAILED )          v = FD_ED25519_HIP_TXN_PARSE_FAILED;  /* device parse */
+    else if( fd_ed25519_hip_tcache_query( vt->tc, r->tag ) )  v = FD_ED25519_HIP_TXN_VERIFY_DEDUP;
     else if( code!=FD_ED25519_SUCCESS )                       v = FD_ED25519_HIP_TXN_VERIFY_FAILED;
     else if( fd_ed25519_hip_tcache_insert( vt->tc, r->tag ) ) v = FD_ED25519_HIP_TXN_VERIFY_DEDUP;
     else                                                      v = FD_ED25519_HIP_TXN_VERIFY_SUCCESS;
@@ -564,7 +507,8 @@ static int
 vt_submit_open( fd_ed25519_hip_vtile_t * vt ) {
   fd_ed25519_hip_slot_t * s = vt->open;
   if( !s || !s->txn_cnt ) return 0;
-  int err = fd_ed25519_hip_pipe_submit( vt->pipe, s, s->sig_cnt, s->msg_bytes, s->txn_cnt );
+  int err = vt->gpu_parse ? fd_ed25519_hip_pipe_submit_txns( vt->pipe, s, s->txn_cnt, s->msg_bytes )
+                          : fd_ed25519_hip_pipe_submit( vt->pipe, s, s->sig_cnt, s->msg_bytes, s->txn_cnt );
   if( err ) {
     fprintf( stderr, "libfd_ed25519_hip: FATAL: vtile submit failed: %s (%s)\n", fd_ed25519_hip_strerror( err ),
              fd_ed25519_hip_last_error() );
@@ -585,9 +529,45 @@ vt_open( fd_ed25519_hip_vtile_t * vt ) {
   vt->open_seq = vt->pipe->seq;
 }
 
+/* GPU-parse mode: the payload goes to the device as is; the host reads
+   only byte 0 (the signature count, to reserve slots) and bytes 1..8 (the
+   dedup tag, valid whenever the device's parse accepts the payload). */
+static int
+vt_frag_raw( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
+             unsigned long cookie ) {
+  if( !payload_sz || payload_sz>FD_ED25519_HIP_TXN_MTU ) {   /* fd_txn_parse rejects these before reading */
+    vrec_t * r = vq_push( vt );
+    r->cookie = cookie; r->verdict = FD_ED25519_HIP_TXN_PARSE_FAILED; r->resolved = 1;
+    vt_advance( vt );
+    return 0;
+  }
+  unsigned long c = payload[0], nsig = (c>=1UL && c<=16UL) ? c : 0UL;
+  vt_open( vt );
+  fd_ed25519_hip_slot_t * s = vt->open;
+  if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap || s->msg_bytes+payload_sz>s->msg_cap ) ) {
+    vt_submit_open( vt );
+    vt_open( vt );
+    s = vt->open;
+  }
+  unsigned long ti = s->txn_cnt++;
+  memcpy( s->msgs + s->msg_bytes, payload, payload_sz );
+  s->msg_off[ ti ] = s->msg_bytes;
+  s->msg_sz [ ti ] = (unsigned int)payload_sz;
+  s->msg_bytes += payload_sz;
+  s->sig_cnt   += nsig;
+  vrec_t * r = vq_push( vt );
+  r->cookie = cookie;
+  if( payload_sz>=9UL ) memcpy( &r->tag, payload + 1, 8UL );
+  r->slot_seq = vt->open_seq;
+  r->txn_idx  = (unsigned)ti;
+  if( s->sig_cnt>=s->sig_cap || s->txn_cnt>=s->txn_cap ) vt_submit_open( vt );
+  return 1;
+}
+
 int
 fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
                            unsigned long cookie ) {
+  if( vt->gpu_parse ) return vt_frag_raw( vt, payload, payload_sz, cookie );
   fd_ed25519_hip_txn_t t;
   if( !fd_ed25519_hip_txn_parse( payload, payload_sz, &t ) ) {
     vrec_t * r = vq_push( vt );
@@ -738,14 +718,14 @@ int
 fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_sigs,
                             unsigned char const * payloads, unsigned long const * payload_off,
                             unsigned int const * payload_sz, unsigned long txn_cnt, double offered_txn_per_s,
-                            unsigned long ring_depth, double * lat_s, signed char * verdict,
+                            unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
                             fd_ed25519_hip_latency_result_t * res ) {
   if( !txn_cnt || !ring_depth || (ring_depth & (ring_depth-1UL)) || !lat_s || !verdict || !res )
     return FD_ED25519_HIP_ERR_INVAL;
   for( unsigned long i=0UL; i<txn_cnt; i++ )
     if( payload_sz[ i ]>FD_ED25519_HIP_TXN_MTU ) return FD_ED25519_HIP_ERR_INVAL;
   memset( res, 0, sizeof(*res) );
-  fd_ed25519_hip_vtile_t * vt = fd_ed25519_hip_vtile_new( device, slot_cnt, batch_sigs, 16UL, 64UL, 0 );
+  fd_ed25519_hip_vtile_t * vt = fd_ed25519_hip_vtile_new( device, slot_cnt, batch_sigs, 16UL, 64UL, flags );
   if( !vt ) return FD_ED25519_HIP_ERR_INVAL;
   ring_t rg;
   rg.depth     = ring_depth;
@@ -793,8 +773,7 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
         res->ring_overruns++; verdict[ next ] = FD_ED25519_HIP_TXN_PARSE_FAILED; lat_s[ next ] = -1.0;
         next++; done++; continue;
       }
-      fd_ed25519_hip_txn_t t;
-      if( fd_ed25519_hip_txn_parse( buf, sz, &t ) && t.signature_cnt<=16U ) sigs += t.signature_cnt;
+      if( sz && buf[0]<=16U ) sigs += buf[0];
       fd_ed25519_hip_vtile_frag( vt, buf, sz, cookie );
       next++;
       atomic_store_explicit( &pr.consumed, next, memory_order_release );

@@ -20,6 +20,7 @@ TXN_VERIFY_DEDUP = -2
 TXN_PARSE_FAILED = -3
 
 TXN_MTU = 1232
+VTILE_GPU_PARSE = 2   # FD_ED25519_HIP_VTILE_GPU_PARSE: fd_txn_parse on the device
 
 
 class Txn(ctypes.Structure):
@@ -63,7 +64,8 @@ _lib.fd_ed25519_hip_vtile_poll.restype = ctypes.c_ulong
 _lib.fd_ed25519_hip_vtile_pending.argtypes = [_v]
 _lib.fd_ed25519_hip_vtile_pending.restype = ctypes.c_ulong
 _lib.fd_ed25519_hip_latency_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, _v, _v, _v, ctypes.c_ulong,
-                                            ctypes.c_double, ctypes.c_ulong, _v, _v, ctypes.POINTER(LatencyResult)]
+                                            ctypes.c_double, ctypes.c_ulong, ctypes.c_int, _v, _v,
+                                            ctypes.POINTER(LatencyResult)]
 _lib.fd_ed25519_hip_pool_verify.argtypes = [_v, ctypes.c_uint, ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, _v, _v,
                                             _v, _v, _v, _v, ctypes.POINTER(ctypes.c_double)]
 
@@ -99,8 +101,9 @@ class TCache:
 class VerifyTile:
     """The verify tile's batched core on one GPU."""
 
-    def __init__(self, device=0, slot_cnt=3, batch_sigs=4096, tcache_depth=16, tcache_map_cnt=64, codes="avx512"):
-        flags = 1 if codes == "portable" else 0
+    def __init__(self, device=0, slot_cnt=3, batch_sigs=4096, tcache_depth=16, tcache_map_cnt=64, codes="avx512",
+                 gpu_parse=False):
+        flags = (1 if codes == "portable" else 0) | (VTILE_GPU_PARSE if gpu_parse else 0)
         self._h = _lib.fd_ed25519_hip_vtile_new(int(device), int(slot_cnt), int(batch_sigs), int(tcache_depth),
                                                 int(tcache_map_cnt), flags)
         if not self._h:
@@ -161,7 +164,7 @@ def pack_payloads(payloads):
     return buf, off, sz
 
 
-def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=256, ring_depth=4096):
+def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=256, ring_depth=4096, gpu_parse=False):
     """Latency mode (C5): a producer thread publishes the payloads into a
     tango-style ring at the offered rate; the verify tile consumes them.
     payloads: a list of byte strings, or a uint8 array [n][size] of
@@ -179,7 +182,8 @@ def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=25
     verdict = np.zeros(n, np.int8)
     res = LatencyResult()
     _check(_lib.fd_ed25519_hip_latency_run(int(device), int(slot_cnt), int(batch_sigs), _ptr(buf), _ptr(off), _ptr(sz),
-                                           n, float(offered_txn_per_s), int(ring_depth), _ptr(lat), _ptr(verdict),
+                                           n, float(offered_txn_per_s), int(ring_depth),
+                                           VTILE_GPU_PARSE if gpu_parse else 0, _ptr(lat), _ptr(verdict),
                                            ctypes.byref(res)))
     return lat, verdict, {f: getattr(res, f) for f, _ in LatencyResult._fields_}
 

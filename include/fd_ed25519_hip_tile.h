@@ -86,6 +86,21 @@ int
 fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot,
                             unsigned long sig_cnt, unsigned long msg_bytes, unsigned long txn_cnt );
 
+/* Raw transactions: the caller copies txn_cnt
+   payloads (the TPU wire format fd_txn_parse reads) into msgs, with
+   msg_off[t] / msg_sz[t] per transaction.  The device parses them
+   (fd_txn_parse's exact acceptance), gathers signatures and signer keys,
+   verifies, and writes txn_out[t]: fd_ed25519_verify_batch_single_msg's
+   code, or FD_ED25519_HIP_TXN_CODE_PARSE_FAILED.  txn_first / txn_sig_cnt
+   are filled by the pipe (from payload byte 0, the signature count).  The
+   signature slots (counts of 1..16) must fit sig_cap, payloads msg_cap
+   (the buffer is readable 64 bytes past the end, as the kernels need). */
+#define FD_ED25519_HIP_TXN_CODE_PARSE_FAILED (-4)
+
+int
+fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot,
+                                 unsigned long txn_cnt, unsigned long payload_bytes );
+
 /* The oldest submitted slot once its results are on the host (wait != 0:
    block until it is), else NULL.  Slots come back in submission order. */
 fd_ed25519_hip_slot_t *
@@ -157,7 +172,12 @@ typedef struct fd_ed25519_hip_vtile fd_ed25519_hip_vtile_t;
 
 /* A verify tile's batched core on `device`: batches of up to batch_sigs
    signatures, slot_cnt in flight, tcache of tcache_depth / tcache_map_cnt
-   (the reference: 16 / 64, fd_verify.h:6-7). */
+   (the reference: 16 / 64, fd_verify.h:6-7).  flags: the engine flags
+   (FD_ED25519_HIP_FLAG_CODES_PORTABLE) and FD_ED25519_HIP_VTILE_GPU_PARSE:
+   payloads go to the device as they are and fd_txn_parse runs there
+   (fd_ed25519_hip_pipe_submit_txns); the verdicts are the same. */
+#define FD_ED25519_HIP_VTILE_GPU_PARSE (2)
+
 fd_ed25519_hip_vtile_t *
 fd_ed25519_hip_vtile_new( int device, unsigned slot_cnt, unsigned long batch_sigs, unsigned long tcache_depth,
                           unsigned long tcache_map_cnt, int flags );
@@ -198,7 +218,8 @@ fd_ed25519_hip_vtile_pending( fd_ed25519_hip_vtile_t const * vt );
    thread pulls frags, stages them, submits a batch once it holds
    batch_sigs signatures or the ring is drained and a slot is free, and
    timestamps each verdict when the batch completes.  lat_s[i] is txn i's
-   publish -> verdict latency in seconds; verdict[i] its verdict. */
+   publish -> verdict latency in seconds; verdict[i] its verdict.  flags as
+   for fd_ed25519_hip_vtile_new. */
 typedef struct {
   double        offered_txn_per_s;
   double        achieved_txn_per_s;
@@ -214,7 +235,7 @@ int
 fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_sigs,
                             unsigned char const * payloads, unsigned long const * payload_off,
                             unsigned int const * payload_sz, unsigned long txn_cnt, double offered_txn_per_s,
-                            unsigned long ring_depth, double * lat_s, signed char * verdict,
+                            unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
                             fd_ed25519_hip_latency_result_t * res );
 
 /* ---- pool ------------------------------------------------------------- */

@@ -32,10 +32,11 @@ def frags(oracle):
     return tile_workload(oracle, 2024, 3000)
 
 
+@pytest.mark.parametrize("gpu_parse", [False, True])
 @pytest.mark.parametrize("batch_sigs,slot_cnt", [(64, 3), (1000, 2), (16, 1), (4096, 4)])
-def test_vtile_matches_reference_tile(tile, ref, frags, batch_sigs, slot_cnt):
+def test_vtile_matches_reference_tile(tile, ref, frags, batch_sigs, slot_cnt, gpu_parse):
     want, want_tags = ref_vtile(ref, frags)
-    vt = tile.VerifyTile(0, slot_cnt=slot_cnt, batch_sigs=batch_sigs)
+    vt = tile.VerifyTile(0, slot_cnt=slot_cnt, batch_sigs=batch_sigs, gpu_parse=gpu_parse)
     got, tags = vt.run(frags)
     vt.close()
     bad = np.nonzero(got != want)[0]
@@ -61,10 +62,12 @@ def test_vtile_dedup_across_batches(tile, ref, oracle):
     assert want.tolist()[22] == 0                                         # base[4] came back after eviction
 
 
-def test_latency_run(tile, ref, frags):
+@pytest.mark.parametrize("gpu_parse", [False, True])
+def test_latency_run(tile, ref, frags, gpu_parse):
     frags = [p for p in frags if len(p) <= tile.TXN_MTU]  # a dcache frag is at most the TPU MTU
     want, _ = ref_vtile(ref, frags)
-    lat, got, res = tile.latency_run(frags, offered_txn_per_s=20000.0, batch_sigs=256, slot_cnt=3, ring_depth=1024)
+    lat, got, res = tile.latency_run(frags, offered_txn_per_s=20000.0, batch_sigs=256, slot_cnt=3, ring_depth=1024,
+                                     gpu_parse=gpu_parse)
     assert res["ring_overruns"] == 0
     assert np.array_equal(got, want)
     assert (lat > 0).all() and res["batches"] > 1
@@ -123,3 +126,31 @@ def test_txn_payload_generator(tile, ref):
         vt.close()
         assert (got == 0).all()
     eng.close()
+
+
+def test_device_parse_on_mutated_fixtures(tile, ref):
+    """fd_txn_parse on the device (GPU-parse tile) against the reference's
+    parser: the reference's 6 fixtures and 9000 mutations of them, plus the
+    whole verdict (parse, dedup, verify) against the reference tile."""
+    import glob
+    import os
+    from conftest import GOLDEN
+    from txn_util import mutate, ref_parse
+    fx = [open(p, "rb").read() for p in sorted(glob.glob(os.path.join(GOLDEN, "txn", "*.bin")))]
+    rng = random.Random(7)
+    corpus = list(fx)
+    for p in fx:
+        for _ in range(1500):
+            q = p
+            for _ in range(rng.randrange(1, 4)):
+                q = mutate(rng, q)
+            corpus.append(q)
+    want, _ = ref_vtile(ref, corpus)
+    vt = tile.VerifyTile(0, slot_cnt=3, batch_sigs=512, gpu_parse=True)
+    got, _ = vt.run(corpus)
+    vt.close()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:10]]
+    parsed = np.array([ref_parse(ref, p)[0] is not None for p in corpus])
+    assert np.array_equal(got != tile.TXN_PARSE_FAILED, parsed)
+    assert 500 < parsed.sum() < len(corpus) - 500
