@@ -85,7 +85,7 @@ def cpu_has(flag):
     return False
 
 
-def cpu_baseline(wl, gpu_codes, sample, reps):
+def cpu_baseline(wl, gpu_codes, sample, reps, workload_name="C2"):
     """Reference CPU verify (oracle/_ref) on `sample` signatures of the workload,
     one pthread per core of this process's share.  Also checks the reference's
     verdicts against the GPU's on the sample."""
@@ -116,10 +116,33 @@ def cpu_baseline(wl, gpu_codes, sample, reps):
         return None
     rate = n * reps / (ns * 1e-9)
     return {"value": rate, "unit": "verifies/s", "cores": threads, "kind": kind,
-            "sample": f"first {n} signatures of the C2 workload x {reps} passes, fd_ed25519_verify of the "
+            "sample": f"first {n} signatures of the {workload_name} workload x {reps} passes, fd_ed25519_verify of the "
                       f"reference's {flavour} backend (compiled from its sources), {threads} pthreads",
             "seconds": ns * 1e-9, "per_core": rate / threads,
             "verdicts_equal_gpu": bool(np.array_equal(out, gpu_codes[:n]))}
+
+
+def config_c1(eng, args):
+    """C1 (BASELINE.json configs[0]): 16,384 single-signer ~200-byte
+    signatures, all valid -- the reference's own CPU case.  The reference's
+    fd_ed25519_verify on this host's cores (20 passes) next to this engine
+    on one GPU (20 launches of the 16K batch, device-resident)."""
+    from firedancer_amd import ed25519
+    wl = ed25519.DeviceWorkload(eng, 16384, 200, 200, 0, seed=args.seed + 1)
+    for _ in range(3):
+        wl.verify()
+    eng.sync()
+    t = time.perf_counter()
+    for _ in range(20):
+        wl.verify()
+    eng.sync()
+    gpu_s = time.perf_counter() - t
+    out = wl.out.download(np.int8, wl.n)
+    cpu = cpu_baseline(wl, out, wl.n, 20, workload_name="C1")
+    wl.free()
+    return {"signatures": 16384, "msg_sz": 200, "gpu_verifies_per_s": 20 * 16384 / gpu_s,
+            "gpu_ms_per_batch": gpu_s * 1e3 / 20, "all_valid": bool((out == 0).all()),
+            "cpu_reference": cpu}
 
 
 def latency_mode(eng, args, device):
@@ -241,10 +264,11 @@ def main():
     path_ops = float(ops["total"].sum()) / chunks
     path_achieved = path_ops / (path_ms * 1e-3) / 1e12 if path_ms > 0 else None
 
-    cpu = None
+    cpu = c1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(wl, out, args.cpu_sample, args.cpu_reps)
+            c1 = config_c1(eng, args)
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"cpu baseline failed: {ex!r}")
     lat = None
@@ -285,6 +309,7 @@ def main():
             "cpu_baseline": cpu,
             "gpu_over_cpu": (value / cpu["value"]) if cpu else None,
             "latency_mode": lat,
+            "config_c1": c1,
             "verdicts_match_reference_labels": mism_all == 0,
             "verdict_mismatches": mism_all,
             "invalid_fraction": float((expect != 0).mean()),
