@@ -110,6 +110,23 @@ FD_DEV void recode_radix256(uint32_t (&out)[8], const uint32_t (&s)[8]) {
   }
 }
 
+/* S < L -> 16 digits g_j in [-2^15, 2^15] (g_15 in [0, 2^13+1]), 16 bits each */
+FD_DEV void recode_radix65536(uint32_t (&out)[8], const uint32_t (&s)[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      int g = (int)((s[w] >> (16 * j)) & 0xffffu) + carry;
+      carry = (g + 32768) >> 16;
+      g -= carry * 65536;
+      packed |= ((uint32_t)g & 0xffffu) << (16 * j);
+    }
+    out[w] = packed;
+  }
+}
+
 /* pop the top `bits` of the 256-bit value as a signed digit */
 template <int BITS>
 FD_DEV int pop_digit(uint32_t (&d)[8]) {
@@ -169,6 +186,22 @@ FD_DEV void btab_load(ge_precomp& b, const int4* s_btab, int e) {
   }
 }
 
+/* entry e of the wide B table in global memory (128-byte entries) */
+FD_DEV void btab16_load(ge_precomp& b, const int4* g_btab, int e) {
+  int v[32];
+  const int4* src = g_btab + e * (FD_ED25519_BTAB16_STRIDE / 4);
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const int4 x = src[q];
+    v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    b.yplusx.v[i] = v[i];
+    b.yminusx.v[i] = v[10 + i];
+    b.xy2d.v[i] = v[20 + i];
+  }
+}
 
 /* ------------------------------------------------------------------------
    Fixed-base scalar multiplication [s]B, s < L, with the [0..128]B table in

@@ -17,6 +17,17 @@ extern "C" {
 #define FD_ED25519_BTAB_STRIDE    36
 #define FD_ED25519_BTAB_INTS      (FD_ED25519_BTAB_ENTRIES * FD_ED25519_BTAB_STRIDE)
 
+/* Window (bits) of S in the verify kernel's double-scalar multiplication.
+   16: signed radix-2^16 digits (16 mixed additions of B), table
+   [0..2^15]B of 128-byte entries (4.2 MB) read from HBM / L2 / MALL with
+   the entry prefetched a k-window ahead; 8: radix 2^8 (32 additions) from
+   the 129-entry LDS table above. */
+#ifndef FD_ED25519_BWIN
+#define FD_ED25519_BWIN 16
+#endif
+#define FD_ED25519_BTAB16_ENTRIES ((1 << 15) + 1)
+#define FD_ED25519_BTAB16_STRIDE  32
+
 /* Per-lane table of [0..8](-A) in cached form, in HBM: 9 entries x 40 int32
    per lane, laid out [wave][lane][entry][quad] (int4 granules): a lookup
    reads 160 contiguous bytes of the lane's own table, so every fetched line
@@ -81,6 +92,7 @@ typedef struct {
   uint32_t *       hist;     /* [2*SORT_BUCKETS] counting-sort scratch          */
   uint64_t         cap;
   int32_t const *  btab;     /* device base-point table (FD_ED25519_BTAB_INTS) */
+  int32_t const *  btab16;   /* [FD_ED25519_BTAB16_ENTRIES][32] (BWIN 16)      */
   void *           atab;     /* device scratch, waves * ATAB_BYTES_PER_WAVE    */
   int              codes_portable; /* 0: AVX-512 backend codes, 1: portable  */
 } fd_ed25519_verify_params_t;
@@ -88,6 +100,7 @@ typedef struct {
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a
    hipError_t value (0 on success). */
 int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
+int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, void * stream );
 /* Enqueues hash, decode and dsm for one chunk; `grid` caps the persistent
    dsm grid (its atab scratch must hold grid*VERIFY_BLOCK/64 waves). */
 int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t grid, void * stream );

@@ -220,8 +220,15 @@ FD_DEV void dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_
       for (int w = 0; w < 8; w++) S[w] = 0;
     }
     recode_radix16(kd, k);
+#if FD_ED25519_BWIN == 16
+    recode_radix65536(sd, S);
+#else
     recode_radix256(sd, S);
+#endif
   }
+#if FD_ED25519_BWIN == 16
+  const int4* g_btab16 = reinterpret_cast<const int4*>(p.btab16);
+#endif
 
   ge_p3 P;
   ge_p3_0(P);
@@ -229,6 +236,20 @@ FD_DEV void dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_
   ge_p2 Q;
 #pragma clang loop unroll(disable)
   for (int it = 63; it >= 0; it--) {
+#if FD_ED25519_BWIN == 16
+    /* every 4th k-window adds a B entry: its HBM/L2 load is issued here,
+       before the window's doublings, so their ~28 field operations cover
+       the latency */
+    const bool badd = (it & 3) == 0;
+    int f = 0;
+    ge_precomp b;
+    if (badd) {
+      f = pop_digit<16>(sd);
+      btab16_load(b, g_btab16, f < 0 ? -f : f);
+    }
+#else
+    const bool badd = (it & 1) == 0;
+#endif
     if (it != 63) {
 #pragma clang loop unroll(disable)
       for (int dd = 0; dd < 4; dd++) {
@@ -244,11 +265,13 @@ FD_DEV void dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_
       ge_cached_cneg(c, e < 0);
       ge_add(Rt, P, c);
     }
-    if ((it & 1) == 0) {
+    if (badd) {
       ge_p1p1_to_p3(P, Rt);
+#if FD_ED25519_BWIN != 16
       const int f = pop_digit<8>(sd);
       ge_precomp b;
       btab_load(b, s_btab, f < 0 ? -f : f);
+#endif
       ge_precomp_cneg(b, f < 0);
       ge_madd(Rt, P, b);
     }
@@ -272,10 +295,14 @@ FD_DEV void dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_
 
 __global__ void __launch_bounds__(FD_ED25519_VERIFY_BLOCK, FD_ED25519_DSM_WAVES_PER_SIMD)
 fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
+#if FD_ED25519_BWIN == 16
+  const int4* s_btab = nullptr;  /* the wide table is read from global memory */
+#else
   __shared__ int4 s_btab[FD_ED25519_BTAB_INTS / 4];
   const int4* g_btab = reinterpret_cast<const int4*>(p.btab);
   for (int t = threadIdx.x; t < FD_ED25519_BTAB_INTS / 4; t += blockDim.x) s_btab[t] = g_btab[t];
   __syncthreads();
+#endif
 
   const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -434,11 +461,12 @@ fd_ed25519_rfix_kernel(fd_ed25519_verify_params_t p) {
 }
 
 /* ------------------------------------------------------------------------
-   Base table [0..128]B as (y+x, y-x, 2dxy), one entry per thread. */
+   Base tables [0..entries)B as (y+x, y-x, 2dxy), one entry per lane:
+   [e]B by double-and-add over `bits` bits, then affine. */
 
-__global__ void fd_ed25519_gen_btab_kernel(int32_t* btab) {
+__global__ void fd_ed25519_gen_btab_kernel(int32_t* btab, int entries, int stride, int bits) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= FD_ED25519_BTAB_ENTRIES) return;
+  if (e >= entries) return;
   ge_p3 B, P;
   const fe bx = {FE_BX}, by = {FE_BY}, d2 = {FE_D2};
   B.X = bx; B.Y = by; fe_1(B.Z); fe_mul(B.T, bx, by);
@@ -446,7 +474,7 @@ __global__ void fd_ed25519_gen_btab_kernel(int32_t* btab) {
   ge_p3_to_cached(cb, B);
   ge_p3_0(P);
   ge_p1p1 t;
-  for (int bit = 7; bit >= 0; bit--) {
+  for (int bit = bits - 1; bit >= 0; bit--) {
     ge_p3_dbl(t, P);
     ge_p1p1_to_p3(P, t);
     if ((e >> bit) & 1) {
@@ -462,13 +490,13 @@ __global__ void fd_ed25519_gen_btab_kernel(int32_t* btab) {
   fe_sub(ymx, y, x); fe_carry(ymx, ymx);
   fe_mul(xy2d, x, y);
   fe_mul(xy2d, xy2d, d2);
-  int32_t* o = btab + e * FD_ED25519_BTAB_STRIDE;
+  int32_t* o = btab + (int64_t)e * stride;
   for (int i = 0; i < 10; i++) {
     o[i] = ypx.v[i];
     o[10 + i] = ymx.v[i];
     o[20 + i] = xy2d.v[i];
   }
-  for (int i = 30; i < FD_ED25519_BTAB_STRIDE; i++) o[i] = 0;
+  for (int i = 30; i < stride; i++) o[i] = 0;
 }
 
 /* ------------------------------------------------------------------------
@@ -498,7 +526,15 @@ __global__ void fd_ed25519_txn_combine_kernel(const int8_t* sig_codes, const uin
    C-ABI launchers */
 
 extern "C" int fd_ed25519_hip_launch_gen_btab(int32_t* d_btab, void* stream) {
-  hipLaunchKernelGGL(fd_ed25519_gen_btab_kernel, dim3(3), dim3(64), 0, (hipStream_t)stream, d_btab);
+  hipLaunchKernelGGL(fd_ed25519_gen_btab_kernel, dim3(3), dim3(64), 0, (hipStream_t)stream, d_btab,
+                     FD_ED25519_BTAB_ENTRIES, FD_ED25519_BTAB_STRIDE, 8);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fd_ed25519_hip_launch_gen_btab16(int32_t* d_btab16, void* stream) {
+  const int entries = FD_ED25519_BTAB16_ENTRIES;
+  hipLaunchKernelGGL(fd_ed25519_gen_btab_kernel, dim3((entries + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     d_btab16, entries, FD_ED25519_BTAB16_STRIDE, 16);
   return (int)hipGetLastError();
 }
 

@@ -9,7 +9,8 @@
 
    HBM layout of an engine (sized once at creation, no per-call device
    allocation on the device-resident path):
-     btab   129 x 36 int32            base-point table [0..128]B (LDS image)
+     btab   129 x 36 int32            base-point table [0..128]B (LDS image, signing)
+     btab16 32769 x 32 int32          base-point table [0..2^15]B (verify, 4.2 MB)
      atab   dsm waves x 92160 B       per-lane [0..8](-A) tables
      work   max_chunk x 243 B         k, flags, decoded A, R' and lists per signature
      in/out staging for the host API  grown on demand */
@@ -40,6 +41,7 @@ struct fd_ed25519_hip_engine {
   char         arch[ 64 ];
 
   int32_t *    d_btab;
+  int32_t *    d_btab16;     /* [0..2^15]B, the verify kernel's wide B table */
   void *       d_atab;
   uint8_t *    d_work;       /* one allocation carved into the work arrays */
   uint32_t *   d_k;
@@ -113,7 +115,7 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   if( !e ) return;
   hipSetDevice( e->device );
   if( e->stream ) hipStreamSynchronize( e->stream );
-  hipFree( e->d_btab ); hipFree( e->d_atab ); hipFree( e->d_work );
+  hipFree( e->d_btab ); hipFree( e->d_btab16 ); hipFree( e->d_atab ); hipFree( e->d_work );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
   hipHostFree( e->h_msgs ); hipHostFree( e->h_off ); hipHostFree( e->h_sz ); hipHostFree( e->h_sigs );
@@ -155,12 +157,14 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   e->dsm_grid = (uint32_t)(bpc * e->cu_cnt);
 
   size_t btab_sz = sizeof(int32_t) * FD_ED25519_BTAB_INTS;
+  size_t btab16_sz = sizeof(int32_t) * (size_t)FD_ED25519_BTAB16_ENTRIES * FD_ED25519_BTAB16_STRIDE;
   size_t atab_sz = (size_t)e->dsm_grid * (FD_ED25519_VERIFY_BLOCK / 64) * FD_ED25519_ATAB_BYTES_PER_WAVE;
   size_t work_sz = (size_t)e->max_chunk * FD_ED25519_WORK_BYTES_PER_SIG + 1024;
   HIPCHK( hipMalloc( (void **)&e->d_btab, btab_sz ), "hipMalloc(btab)" );
+  HIPCHK( hipMalloc( (void **)&e->d_btab16, btab16_sz ), "hipMalloc(btab16)" );
   HIPCHK( hipMalloc( &e->d_atab, atab_sz ), "hipMalloc(atab)" );
   HIPCHK( hipMalloc( (void **)&e->d_work, work_sz ), "hipMalloc(work)" );
-  e->device_bytes = btab_sz + atab_sz + work_sz;
+  e->device_bytes = btab_sz + btab16_sz + atab_sz + work_sz;
   uint64_t c = e->max_chunk;
   uint8_t * w = e->d_work;
   e->d_k     = (uint32_t *)w; w += 8UL*4UL*c;
@@ -178,6 +182,8 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
 
   int err = fd_ed25519_hip_launch_gen_btab( e->d_btab, e->stream );
   if( err ) return hip_fail( (hipError_t)err, "gen_btab launch" );
+  err = fd_ed25519_hip_launch_gen_btab16( e->d_btab16, e->stream );
+  if( err ) return hip_fail( (hipError_t)err, "gen_btab16 launch" );
   HIPCHK( hipStreamSynchronize( e->stream ), "gen_btab" );
   return FD_ED25519_HIP_OK;
 }
@@ -239,7 +245,7 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   p.k = e->d_k; p.sflag = e->d_sflag; p.pflag = e->d_pflag; p.pts = e->d_pts; p.cap = e->max_chunk;
   p.proj = e->d_proj; p.st = e->d_st; p.fix_list = e->d_fix; p.fix_cnt = e->d_hist + 2*FD_ED25519_SORT_BUCKETS;
   p.perm = e->sort ? e->d_perm : NULL; p.hist = e->d_hist;
-  p.btab = e->d_btab; p.atab = e->d_atab;
+  p.btab = e->d_btab; p.btab16 = e->d_btab16; p.atab = e->d_atab;
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   for( uint64_t base=0UL; base<n; base+=e->max_chunk ) {
     p.base = base;
