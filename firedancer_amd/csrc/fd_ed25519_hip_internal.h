@@ -17,15 +17,11 @@ extern "C" {
 #define FD_ED25519_BTAB_STRIDE    36
 #define FD_ED25519_BTAB_INTS      (FD_ED25519_BTAB_ENTRIES * FD_ED25519_BTAB_STRIDE)
 
-/* Window (bits) of S in the verify kernel's double-scalar multiplication.
-   16: signed radix-2^16 digits (16 mixed additions of B), table
-   [0..2^15]B of 128-byte entries (4.2 MB) read from HBM / L2 / MALL with
-   the entry prefetched a k-window ahead; 8: radix 2^8 (32 additions) from
-   the 129-entry LDS table above. */
-#ifndef FD_ED25519_BWIN
-#define FD_ED25519_BWIN 16
-#endif
+/* Wide base-point tables of the verify kernels: [0..2^15]B and
+   [0..2^15][2^132]B (signed radix-2^16 digits), 128-byte entries, 4.2 MB
+   each, read from HBM / L2 / MALL with each entry loaded a window ahead. */
 #define FD_ED25519_BTAB16_ENTRIES ((1 << 15) + 1)
+#define FD_ED25519_BTAB16B_SHIFT  132
 #define FD_ED25519_BTAB16_STRIDE  32
 
 /* Per-lane table of [0..8](-A) in cached form, in HBM: 9 entries x 40 int32
@@ -33,7 +29,7 @@ extern "C" {
    reads 160 contiguous bytes of the lane's own table, so every fetched line
    is fully used (the [entry][quad][lane] layout fetched ~2.4x the table
    bytes from HBM because lanes pick different entries). */
-#define FD_ED25519_ATAB_BYTES_PER_WAVE (9UL * 10UL * 64UL * 16UL)
+#define FD_ED25519_ATAB_BYTES_PER_WAVE (2UL * 9UL * 10UL * 64UL * 16UL)  /* -A and -+R tables */
 
 #define FD_ED25519_VERIFY_BLOCK 256
 /* Occupancy targets (waves per SIMD) of the phase kernels; each caps the
@@ -53,21 +49,14 @@ extern "C" {
    (SoA, [field][cap] so every access is one coalesced dword per lane):
      k        [8][cap]   u32  k = SHA-512(R||A||M) mod L
      sflag    [cap]      u8   S < L
-     pflag    [cap]      u8   A: bit0 decode failure, bit1 small order
-     pts      [20][cap]  i32  A: x (10 limbs), y (10 limbs), radix 2^25.5
-     proj     [30][cap]  i32  R' = [k](-A) + [S]B projective (X, Y, Z)
-     st       [cap]      i8   dsm status: a decided code (< 0), FD_ST_CHECK or FD_ST_ASMALL
+     pflag    [2][cap]   u8   A, R: bit0 decode failure, bit1 small order
+     pts      [2][20][cap] i32 A, R: x (10 limbs), y (10 limbs), radix 2^25.5
+     hs       [19][cap]  u32  half-size scalars: c, |d|, s_lo (5 words), s_hi (4)
+     hflag    [cap]      u8   bit0 d < 0, bit1 no half-size pair (full-length form)
      perm     [cap]      u32  hash order (length-sorted)
-     fix_list [cap]      u32  signatures whose R must be decoded (fin -> rfix)
+     fix_list [cap]      u32  signatures for the full-length form (scalar -> dsm)
    FD_ED25519_WORK_BYTES_PER_SIG bytes per signature of capacity. */
-#define FD_ED25519_WORK_BYTES_PER_SIG (8UL * 4UL + 1UL + 1UL + 20UL * 4UL + 30UL * 4UL + 1UL + 4UL + 4UL)
-
-/* dsm status values besides the decided (negative) codes */
-#define FD_ST_CHECK  1  /* compare R' with R's encoding                         */
-#define FD_ST_ASMALL 2  /* A small order: ERR_PUBKEY unless R fails to decode */
-
-/* fin: signatures per lane of the batched inversion (Montgomery's trick) */
-#define FD_ED25519_FIN_M 8
+#define FD_ED25519_WORK_BYTES_PER_SIG (8UL * 4UL + 1UL + 2UL + 2UL * 20UL * 4UL + 19UL * 4UL + 1UL + 4UL + 4UL)
 
 typedef struct {
   /* inputs (signature i = base + j for chunk-local j in [0,n)) */
@@ -84,15 +73,17 @@ typedef struct {
   uint8_t *        sflag;
   uint8_t *        pflag;
   int32_t *        pts;
-  int32_t *        proj;
-  int8_t *         st;
+  uint32_t *       hs;
+  uint8_t *        hflag;
   uint32_t *       fix_list;
   uint32_t *       fix_cnt;  /* 1 word: entries of fix_list                   */
+  uint32_t *       work_ctr; /* 1 word: dsm items handed out (fix_cnt + 1)    */
   uint32_t *       perm;     /* [cap] hash order (length-sorted), NULL: identity */
   uint32_t *       hist;     /* [2*SORT_BUCKETS] counting-sort scratch          */
   uint64_t         cap;
   int32_t const *  btab;     /* device base-point table (FD_ED25519_BTAB_INTS) */
-  int32_t const *  btab16;   /* [FD_ED25519_BTAB16_ENTRIES][32] (BWIN 16)      */
+  int32_t const *  btab16;   /* [0..2^15]B,          [FD_ED25519_BTAB16_ENTRIES][32] */
+  int32_t const *  btab16b;  /* [0..2^15][2^132]B,   same layout                     */
   void *           atab;     /* device scratch, waves * ATAB_BYTES_PER_WAVE    */
   int              codes_portable; /* 0: AVX-512 backend codes, 1: portable  */
 } fd_ed25519_verify_params_t;
@@ -100,16 +91,16 @@ typedef struct {
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a
    hipError_t value (0 on success). */
 int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
-int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, void * stream );
+int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, int base_doublings, void * stream );
 /* Enqueues hash, decode and dsm for one chunk; `grid` caps the persistent
    dsm grid (its atab scratch must hold grid*VERIFY_BLOCK/64 waves). */
 int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t grid, void * stream );
 
 /* The same, one phase at a time (so the host can bracket each with events). */
 #define FD_ED25519_PHASE_HASH   0
-#define FD_ED25519_PHASE_DECODE 1
-#define FD_ED25519_PHASE_DSM    2
-#define FD_ED25519_PHASE_FIN    3
+#define FD_ED25519_PHASE_SCALAR 1
+#define FD_ED25519_PHASE_DECODE 2
+#define FD_ED25519_PHASE_DSM    3
 #define FD_ED25519_PHASE_CNT    4
 int fd_ed25519_hip_launch_phase( fd_ed25519_verify_params_t const * p, int phase, uint32_t grid, void * stream );
 int fd_ed25519_hip_verify_occupancy( int * blocks_per_cu );

@@ -29,23 +29,28 @@
 #include "fd25519_dsm.h"
 #include "fd25519_sc.h"
 #include "fd_sha512_dev.h"
+#define FD_HALF_FN __device__ static inline
+#include "fd25519_half.h"
 
 
 /* ------------------------------------------------------------------------
    Phase kernels.  A batch is verified by four phases on one stream, each
-   kernel with its own register budget, handing ~240 B per signature
+   kernel with its own register budget, handing ~280 B per signature
    through the work arrays in HBM (fd_ed25519_verify_params_t):
 
      hash    one lane per signature: S < L, k = SHA-512(R||A||M) mod L
-     decode  one lane per public key A: decompression and the reference's
+     scalar  one lane per signature: half-size scalars c, d (c == d k mod
+             8L) and s' = d S mod L
+     decode  one lane per point (A, R): decompression and the reference's
              acceptance / small-order rules
-     dsm     one lane per signature, persistent: R' = [k](-A) + [S]B,
-             written projective with the S / A status
-     fin     R' in affine by per-lane batched inversion, compared with R's
-             encoding; rfix decodes R for the few signatures that need it */
+     dsm     persistent, dynamically scheduled: the group equation as
+             [c](-A) + [d](-R) + [dS]B == 0, and the full-length form for
+             the ~0.13% of signatures whose k has no half-size pair */
 
 #define FD_PF_FAIL  1u
 #define FD_PF_SMALL 2u
+#define FD_HF_DNEG  1u   /* hflag: d < 0                        */
+#define FD_HF_FULL  2u   /* hflag: no half-size pair, full form */
 
 /* ------------------------------------------------------------------------
    Length sort for the hash phase.  A wave runs as many SHA-512 blocks as
@@ -125,30 +130,32 @@ fd_ed25519_hash_kernel(fd_ed25519_verify_params_t p) {
   p.sflag[j] = sc_is_canonical(S) ? 1 : 0;
 }
 
-/* One lane per public key A: decompression with the reference's acceptance
-   rules and the small-order test.  R is never decompressed on the common
-   path: fin compares the encoding of R' = [k](-A) + [S]B with R's bytes
-   (see fd_ed25519_fin_kernel). */
+/* One lane per point (2n lanes: A, then R): decompression with the
+   reference's acceptance rules (fd_ed25519_point_frombytes_2x) and the
+   small-order test (fd_ed25519_affine_is_small_order). */
 __global__ void __launch_bounds__(256, FD_ED25519_DECODE_WAVES_PER_SIMD)
 fd_ed25519_decode_kernel(fd_ed25519_verify_params_t p) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= p.n) return;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * p.n) return;
+  const int which = t >= p.n;           /* 0: A (public key), 1: R */
+  const uint64_t j = which ? t - p.n : t;
   const uint64_t i = p.base + j;
   uint32_t s[8];
   {
-    const uint4* src = reinterpret_cast<const uint4*>(p.pubs + 32 * i);
+    const uint4* src = which ? reinterpret_cast<const uint4*>(p.sigs + 64 * i)
+                             : reinterpret_cast<const uint4*>(p.pubs + 32 * i);
     const uint4 q0 = src[0], q1 = src[1];
     s[0] = q0.x; s[1] = q0.y; s[2] = q0.z; s[3] = q0.w; s[4] = q1.x; s[5] = q1.y; s[6] = q1.z; s[7] = q1.w;
   }
   decoded_pt d;
   ge_decode(d, s, !p.codes_portable);
-  int32_t* dst = p.pts + j;
+  int32_t* dst = p.pts + (uint64_t)which * 20 * p.cap + j;
 #pragma unroll
   for (int l = 0; l < 10; l++) {
     dst[(uint64_t)l * p.cap] = d.x.v[l];
     dst[(uint64_t)(10 + l) * p.cap] = d.y.v[l];
   }
-  p.pflag[j] = (uint8_t)((d.fail ? FD_PF_FAIL : 0u) | (d.small ? FD_PF_SMALL : 0u));
+  p.pflag[(uint64_t)which * p.cap + j] = (uint8_t)((d.fail ? FD_PF_FAIL : 0u) | (d.small ? FD_PF_SMALL : 0u));
 }
 
 FD_DEV void load_fe(fe& x, const int32_t* src, uint64_t cap) {
@@ -156,55 +163,298 @@ FD_DEV void load_fe(fe& x, const int32_t* src, uint64_t cap) {
   for (int l = 0; l < 10; l++) x.v[l] = src[(uint64_t)l * cap];
 }
 
-FD_DEV void store_fe(int32_t* dst, uint64_t cap, const fe& x) {
-#pragma unroll
-  for (int l = 0; l < 10; l++) dst[(uint64_t)l * cap] = x.v[l];
+FD_DEV void load_pt(fe& x, fe& y, const fd_ed25519_verify_params_t& p, int which, uint64_t j) {
+  const int32_t* src = p.pts + (uint64_t)which * 20 * p.cap + j;
+  load_fe(x, src, p.cap);
+  load_fe(y, src + 10 * p.cap, p.cap);
 }
 
-/* R' = [k](-A) + [S]B for signature j, written to proj as (X:Y:Z), plus the
-   status that fin finishes.  The reference's checks in order
-   (fd_ed25519_user.c:134-229): S < L, A and R decode (an undecodable A is
-   ERR_SIG with AVX-512 codes, ERR_PUBKEY with portable ones; R: ERR_SIG),
-   A small order (ERR_PUBKEY), R small order (ERR_SIG), the group equation
-   (ERR_MSG).  Here S and A are decided; everything about R is left to fin. */
-FD_DEV void dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_tab, const int4* s_btab) {
-  const uint64_t i = p.base + j;
+/* The reference's checks before the group equation, in its order
+   (fd_ed25519_user.c:134-229): S < L; A and R decode (an undecodable A is
+   ERR_SIG with AVX-512 codes, ERR_PUBKEY with portable ones; R: ERR_SIG);
+   A small order (ERR_PUBKEY); R small order (ERR_SIG).  1 = pending. */
+#define FD_PENDING 1
+FD_DEV int precheck(const fd_ed25519_verify_params_t& p, uint64_t j) {
   const uint32_t s_ok = p.sflag[j];
-  const uint32_t af = p.pflag[j];
-  int st;
-  if (!s_ok) st = FD_ED25519_ERR_SIG;
-  else if (af & FD_PF_FAIL) st = p.codes_portable ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;
-  else if (af & FD_PF_SMALL) st = FD_ST_ASMALL;
-  else st = FD_ST_CHECK;
+  const uint32_t af = p.pflag[j], rf = p.pflag[p.cap + j];
+  if (!s_ok) return FD_ED25519_ERR_SIG;
+  if (af & FD_PF_FAIL) return p.codes_portable ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;
+  if (rf & FD_PF_FAIL) return FD_ED25519_ERR_SIG;
+  if (af & FD_PF_SMALL) return FD_ED25519_ERR_PUBKEY;
+  if (rf & FD_PF_SMALL) return FD_ED25519_ERR_SIG;
+  return FD_PENDING;
+}
 
-  /* table [0..8](-A), cached form, in this lane's HBM slot */
-  {
-    fe ax, ay;
-    load_fe(ax, p.pts + j, p.cap);
-    load_fe(ay, p.pts + 10 * p.cap + j, p.cap);
-    ge_p3 nA;
-    fe_neg(nA.X, ax);
-    nA.Y = ay;
-    fe_1(nA.Z);
-    fe t;
-    fe_mul(t, ax, ay);
-    fe_neg(nA.T, t);
-    ge_cached c1, c;
-    c.YplusX = nA.Z; c.YminusX = nA.Z; c.Z = nA.Z; fe_0(c.T2d);  /* identity */
-    atab_store(lane_tab, 0, c);
-    ge_p3_to_cached(c1, nA);
-    atab_store(lane_tab, 1, c1);
-    ge_p3 cur = nA;
-    ge_p1p1 sum;
+/* [0..8](sign P) in cached form for the affine point (x, y), into a lane's
+   9-entry table */
+FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
+  ge_p3 P0;
+  fe xn;
+  fe_neg(xn, x);
+  fe_select(P0.X, x, xn, negate);
+  P0.Y = y;
+  fe_1(P0.Z);
+  fe_mul(P0.T, P0.X, y);
+  ge_cached c1, c;
+  c.YplusX = P0.Z; c.YminusX = P0.Z; c.Z = P0.Z; fe_0(c.T2d);  /* identity */
+  atab_store(tab, 0, c);
+  ge_p3_to_cached(c1, P0);
+  atab_store(tab, 1, c1);
+  ge_p3 cur = P0;
+  ge_p1p1 sum;
 #pragma clang loop unroll(disable)
-    for (int e = 2; e <= 8; e++) {
-      ge_add(sum, cur, c1);
-      ge_p1p1_to_p3(cur, sum);
-      ge_p3_to_cached(c, cur);
-      atab_store(lane_tab, e, c);
+  for (int e = 2; e <= 8; e++) {
+    ge_add(sum, cur, c1);
+    ge_p1p1_to_p3(cur, sum);
+    ge_p3_to_cached(c, cur);
+    atab_store(tab, e, c);
+  }
+}
+
+FD_DEV void table_add(ge_p1p1& Rt, const ge_p3& P, const int4* tab, int e) {
+  ge_cached c;
+  atab_load(c, tab, e < 0 ? -e : e);
+  ge_cached_cneg(c, e < 0);
+  ge_add(Rt, P, c);
+}
+
+FD_DEV void btab_add(ge_p1p1& Rt, const ge_p3& P, ge_precomp& b, int f) {
+  ge_precomp_cneg(b, f < 0);
+  ge_madd(Rt, P, b);
+}
+
+/* ------------------------------------------------------------------------
+   scalar: the half-size scalars (fd25519_half.h) of every signature, one
+   lane per signature, before the points are decoded:
+
+       c == d k (mod 8L), d odd, 0 <= c, |d| < 2^131,
+       s' = d S mod L = s_lo + 2^132 s_hi
+
+   written to hs[19][cap] (c, |d|, s_lo: 5 words each, s_hi: 4) with d's
+   sign in hflag.  Signatures whose k has no such pair (~0.13% of random k)
+   are flagged and queued on fix_list for the full-length form. */
+
+__global__ void __launch_bounds__(256)
+fd_ed25519_scalar_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p.n) return;
+  const uint64_t i = p.base + j;
+  uint32_t k[8], S[8];
+#pragma unroll
+  for (int w = 0; w < 8; w++) k[w] = p.k[(uint64_t)w * p.cap + j];
+  {
+    const uint4* sg = reinterpret_cast<const uint4*>(p.sigs + 64 * i);
+    const uint4 q2 = sg[2], q3 = sg[3];
+    S[0] = q2.x; S[1] = q2.y; S[2] = q2.z; S[3] = q2.w; S[4] = q3.x; S[5] = q3.y; S[6] = q3.z; S[7] = q3.w;
+  }
+  uint32_t cw[FD_HALF_TW], dm[FD_HALF_TW];
+  int dneg = 0;
+  int ok = fd_half_scalars(k, cw, dm, &dneg);
+  if (!p.sflag[j]) ok = 1;   /* S >= L: decided without the equation, any scalars do */
+
+  /* s' = d S mod L */
+  uint32_t sp[8];
+  {
+    uint32_t prod[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) prod[w] = 0u;
+#pragma unroll
+    for (int a = 0; a < FD_HALF_TW; a++) {
+      uint64_t carry = 0;
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const uint64_t t = (uint64_t)dm[a] * S[b] + prod[a + b] + carry;
+        prod[a + b] = (uint32_t)t;
+        carry = t >> 32;
+      }
+      prod[a + 8] = (uint32_t)carry;
+    }
+    sc_reduce512(sp, prod);
+    if (dneg) {   /* L - sp (mod L) */
+      const uint32_t l[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0u, 0u, 0u, 0x10000000u};
+      uint32_t nz = 0;
+#pragma unroll
+      for (int w = 0; w < 8; w++) nz |= sp[w];
+      uint64_t br = 0;
+#pragma unroll
+      for (int w = 0; w < 8; w++) {
+        const uint64_t t = (uint64_t)l[w] - sp[w] - br;
+        br = (t >> 63) & 1u;
+        sp[w] = nz ? (uint32_t)t : 0u;
+      }
     }
   }
+  uint32_t* hs = p.hs + j;
+  const uint64_t c = p.cap;
+#pragma unroll
+  for (int w = 0; w < 5; w++) {
+    hs[(uint64_t)w * c] = cw[w];
+    hs[(uint64_t)(5 + w) * c] = dm[w];
+    hs[(uint64_t)(10 + w) * c] = w < 4 ? sp[w] : (sp[4] & 0xfu);               /* bits 0..131   */
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++)
+    hs[(uint64_t)(15 + w) * c] = __builtin_amdgcn_alignbit(sp[w + 5], sp[w + 4], 4);  /* bits 132..   */
+  p.hflag[j] = (uint8_t)((dneg ? FD_HF_DNEG : 0u) | (ok ? 0u : FD_HF_FULL));
+  if (!ok) {
+    const uint32_t slot = atomicAdd(p.fix_cnt, 1u);
+    p.fix_list[slot] = (uint32_t)j;
+  }
+}
 
+/* x << SH for a 160-bit value known to stay below 2^160 */
+template <int SH>
+FD_DEV void shl160(uint32_t (&out)[5], const uint32_t (&x)[5]) {
+  constexpr int W = SH / 32, B = SH % 32;
+#pragma unroll
+  for (int i = 4; i >= 0; i--) {
+    const uint32_t hi = i - W >= 0 ? x[i - W] : 0u;
+    const uint32_t lo = i - W - 1 >= 0 ? x[i - W - 1] : 0u;
+    out[i] = B ? __builtin_amdgcn_alignbit(hi, lo, 32 - B) : hi;
+  }
+}
+
+/* signed recoding of a 160-bit value in radix 2^BITS, digits packed as
+   BITS-bit two's complement (the carry out of the top digit is dropped:
+   the caller reads the top digit unsigned where it may reach 2^(BITS-1)) */
+template <int BITS>
+FD_DEV void recode160(uint32_t (&out)[5], const uint32_t (&x)[5]) {
+  constexpr uint32_t M = (1u << BITS) - 1u;
+  constexpr int PER = 32 / BITS;
+  int carry = 0;
+#pragma unroll
+  for (int w = 0; w < 5; w++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      int e = (int)((x[w] >> (BITS * q)) & M) + carry;
+      carry = (e + (1 << (BITS - 1))) >> BITS;
+      e -= carry << BITS;
+      packed |= ((uint32_t)e & M) << (BITS * q);
+    }
+    out[w] = packed;
+  }
+}
+
+template <int BITS>
+FD_DEV int pop160(uint32_t (&d)[5]) {
+  const int v = ((int32_t)d[4]) >> (32 - BITS);
+#pragma unroll
+  for (int w = 4; w > 0; w--) d[w] = __builtin_amdgcn_alignbit(d[w], d[w - 1], 32 - BITS);
+  d[0] <<= BITS;
+  return v;
+}
+
+FD_DEV void load_hs(uint32_t (&x)[5], const fd_ed25519_verify_params_t& p, int row, int words, uint64_t j) {
+#pragma unroll
+  for (int w = 0; w < 5; w++) x[w] = w < words ? p.hs[(uint64_t)(row + w) * p.cap + j] : 0u;
+}
+
+/* ------------------------------------------------------------------------
+   dsm: the group equation with half-size scalars.
+
+   E = [S]B - R - [k]A == 0 is tested as [d]E == 0, i.e.
+
+       [c](-A) + [|d|](-sign(d) R) + [s_lo]B + [s_hi]B' == 0,   B' = [2^132]B
+
+   exactly equivalent (fd25519_half.h: the group has order 8L and [d] is
+   invertible on it).  A four-scalar Straus loop over 33 signed 4-bit
+   windows: 128 doublings (against 252 for the reference's double-scalar
+   form), 33 additions from each lane's [0..8](-A) and [0..8](-+R) tables
+   (HBM, lane-contiguous 160-byte entries) and 9 + 9 mixed additions from
+   the two radix-2^16 base tables (HBM/L2).  Every table entry is loaded
+   one step ahead of its use: the -A entry before the window's doublings,
+   the R entry before the -A addition, the base entries before the R
+   addition.  The result is compared with the identity (X == 0, Y == Z). */
+
+FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* tabA, int4* tabR) {
+  int code = precheck(p, j);
+  const uint32_t hf = p.hflag[j];
+
+  /* lane tables: [0..8](-A) and [0..8](-sign(d) R) */
+  {
+    fe x, y;
+    load_pt(x, y, p, 0, j);
+    table_build(tabA, x, y, true);
+    load_pt(x, y, p, 1, j);
+    table_build(tabR, x, y, !(hf & FD_HF_DNEG));
+  }
+  /* digits, most significant first, top-aligned in 160 bits: c, |d| in
+     radix 16 (33 digits, the top one in [0,8]), s_lo, s_hi in radix 2^16
+     (9 digits) */
+  uint32_t cd[5], dd[5], ld[5], hd[5];
+  {
+    uint32_t x[5], t[5];
+    load_hs(x, p, 0, 5, j);  shl160<28>(t, x); recode160<4>(cd, t);
+    load_hs(x, p, 5, 5, j);  shl160<28>(t, x); recode160<4>(dd, t);
+    load_hs(x, p, 10, 5, j); shl160<16>(t, x); recode160<16>(ld, t);
+    load_hs(x, p, 15, 4, j); shl160<16>(t, x); recode160<16>(hd, t);
+  }
+  const int4* g_btab = reinterpret_cast<const int4*>(p.btab16);
+  const int4* g_btab2 = reinterpret_cast<const int4*>(p.btab16b);
+
+  ge_p3 P;
+  ge_p3_0(P);
+  ge_p1p1 Rt;
+  ge_p2 Q;
+#pragma clang loop unroll(disable)
+  for (int it = 32; it >= 0; it--) {
+    int ea = pop160<4>(cd), er = pop160<4>(dd);
+    if (it == 32) { ea &= 15; er &= 15; }   /* top digits in [0,8] */
+    ge_cached ca, cr;
+    atab_load(ca, tabA, ea < 0 ? -ea : ea);
+    if (it != 32) {
+#pragma clang loop unroll(disable)
+      for (int dbl = 0; dbl < 4; dbl++) {
+        ge_p2_dbl(Rt, Q);
+        if (dbl < 3) ge_p1p1_to_p2(Q, Rt);
+      }
+      ge_p1p1_to_p3(P, Rt);
+    }
+    atab_load(cr, tabR, er < 0 ? -er : er);
+    ge_cached_cneg(ca, ea < 0);
+    ge_add(Rt, P, ca);
+    ge_p1p1_to_p3(P, Rt);
+    const bool badd = (it & 3) == 0;
+    int f = 0, g = 0;
+    ge_precomp b1, b2;
+    if (badd) {
+      f = pop160<16>(ld);
+      g = pop160<16>(hd);
+      btab16_load(b1, g_btab, f < 0 ? -f : f);
+      btab16_load(b2, g_btab2, g < 0 ? -g : g);
+    }
+    ge_cached_cneg(cr, er < 0);
+    ge_add(Rt, P, cr);
+    if (badd) {
+      ge_p1p1_to_p3(P, Rt);
+      btab_add(Rt, P, b1, f);
+      ge_p1p1_to_p3(P, Rt);
+      btab_add(Rt, P, b2, g);
+    }
+    ge_p1p1_to_p2(Q, Rt);
+  }
+  /* identity: X == 0 and Y == Z */
+  fe t;
+  fe_sub(t, Q.Y, Q.Z);
+  const bool ident = fe_iszero(Q.X) && fe_iszero(t);
+  if (code == FD_PENDING) code = ident ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  return code;
+}
+
+/* The reference's own form, for the few signatures whose k has no
+   half-size pair: R' = [k](-A) + [S]B with k in radix 16 (252 doublings,
+   64 additions of [0..8](-A)) and S in radix 2^16 (16 mixed additions),
+   then R' == R projectively (fd_ed25519_point_eq_z1: X' == x_R Z',
+   Y' == y_R Z'). */
+FD_DEV int dsm_full_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* tabA) {
+  const uint64_t i = p.base + j;
+  const int code = precheck(p, j);
+  {
+    fe x, y;
+    load_pt(x, y, p, 0, j);
+    table_build(tabA, x, y, true);
+  }
   uint32_t kd[8], sd[8];
   {
     uint32_t k[8], S[8];
@@ -213,250 +463,75 @@ FD_DEV void dsm_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* lane_
     const uint4* sg = reinterpret_cast<const uint4*>(p.sigs + 64 * i);
     const uint4 q2 = sg[2], q3 = sg[3];
     S[0] = q2.x; S[1] = q2.y; S[2] = q2.z; S[3] = q2.w; S[4] = q3.x; S[5] = q3.y; S[6] = q3.z; S[7] = q3.w;
-    /* a rejected S may be >= L; keep the recoding in range (the verdict is
-       already decided for this lane) */
-    if (!s_ok) {
-#pragma unroll
-      for (int w = 0; w < 8; w++) S[w] = 0;
-    }
     recode_radix16(kd, k);
-#if FD_ED25519_BWIN == 16
     recode_radix65536(sd, S);
-#else
-    recode_radix256(sd, S);
-#endif
   }
-#if FD_ED25519_BWIN == 16
-  const int4* g_btab16 = reinterpret_cast<const int4*>(p.btab16);
-#endif
-
+  const int4* g_btab = reinterpret_cast<const int4*>(p.btab16);
   ge_p3 P;
   ge_p3_0(P);
   ge_p1p1 Rt;
   ge_p2 Q;
 #pragma clang loop unroll(disable)
   for (int it = 63; it >= 0; it--) {
-#if FD_ED25519_BWIN == 16
-    /* every 4th k-window adds a B entry: its HBM/L2 load is issued here,
-       before the window's doublings, so their ~28 field operations cover
-       the latency */
     const bool badd = (it & 3) == 0;
     int f = 0;
     ge_precomp b;
     if (badd) {
       f = pop_digit<16>(sd);
-      btab16_load(b, g_btab16, f < 0 ? -f : f);
+      btab16_load(b, g_btab, f < 0 ? -f : f);
     }
-#else
-    const bool badd = (it & 1) == 0;
-#endif
     if (it != 63) {
 #pragma clang loop unroll(disable)
-      for (int dd = 0; dd < 4; dd++) {
+      for (int dbl = 0; dbl < 4; dbl++) {
         ge_p2_dbl(Rt, Q);
-        if (dd < 3) ge_p1p1_to_p2(Q, Rt);
+        if (dbl < 3) ge_p1p1_to_p2(Q, Rt);
       }
       ge_p1p1_to_p3(P, Rt);
     }
-    {
-      const int e = pop_digit<4>(kd);
-      ge_cached c;
-      atab_load(c, lane_tab, e < 0 ? -e : e);
-      ge_cached_cneg(c, e < 0);
-      ge_add(Rt, P, c);
-    }
+    table_add(Rt, P, tabA, pop_digit<4>(kd));
     if (badd) {
       ge_p1p1_to_p3(P, Rt);
-#if FD_ED25519_BWIN != 16
-      const int f = pop_digit<8>(sd);
-      ge_precomp b;
-      btab_load(b, s_btab, f < 0 ? -f : f);
-#endif
-      ge_precomp_cneg(b, f < 0);
-      ge_madd(Rt, P, b);
+      btab_add(Rt, P, b, f);
     }
     ge_p1p1_to_p2(Q, Rt);
   }
-
-  /* A decided lane publishes Z = 1 so that it cannot zero fin's batched
-     inversion (an undecodable A is not a curve point, so its R' is not
-     either).  For a curve point the complete formulas never give Z = 0. */
-  if (st < 0) {
-    fe_0(Q.X);
-    fe_1(Q.Y);
-    fe_1(Q.Z);
-  }
-  int32_t* dst = p.proj + j;
-  store_fe(dst, p.cap, Q.X);
-  store_fe(dst + 10 * p.cap, p.cap, Q.Y);
-  store_fe(dst + 20 * p.cap, p.cap, Q.Z);
-  p.st[j] = (int8_t)st;
+  fe rx, ry, t1, t2;
+  load_pt(rx, ry, p, 1, j);
+  fe_mul(t1, rx, Q.Z);
+  fe_sub(t1, t1, Q.X);
+  fe_mul(t2, ry, Q.Z);
+  fe_sub(t2, t2, Q.Y);
+  const bool eq = fe_iszero(t1) && fe_iszero(t2);
+  if (code != FD_PENDING) return code;
+  return eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
+/* Persistent over fix_cnt + n items, handed out 64 at a time (one atomic
+   per wave): the full-length items first, then the chunk's signatures
+   (those queued as full-length skipped), so the ~2x longer full-length
+   work is spread over the grid instead of forming a tail. */
 __global__ void __launch_bounds__(FD_ED25519_VERIFY_BLOCK, FD_ED25519_DSM_WAVES_PER_SIMD)
 fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
-#if FD_ED25519_BWIN == 16
-  const int4* s_btab = nullptr;  /* the wide table is read from global memory */
-#else
-  __shared__ int4 s_btab[FD_ED25519_BTAB_INTS / 4];
-  const int4* g_btab = reinterpret_cast<const int4*>(p.btab);
-  for (int t = threadIdx.x; t < FD_ED25519_BTAB_INTS / 4; t += blockDim.x) s_btab[t] = g_btab[t];
-  __syncthreads();
-#endif
-
-  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  int4* lane_tab = reinterpret_cast<int4*>(static_cast<char*>(p.atab) +
-                                           (gtid >> 6) * FD_ED25519_ATAB_BYTES_PER_WAVE) + (threadIdx.x & 63) * 90;
-  for (uint64_t j = gtid; j < p.n; j += stride) dsm_one(p, j, lane_tab, s_btab);
-}
-
-/* ------------------------------------------------------------------------
-   fin: the group equation without decompressing R.
-
-   The reference decodes R (a square root, ~265 field operations) and tests
-   R' == R projectively (fd_ed25519_point_eq_z1).  Equivalently: R decodes
-   to R' exactly when R's bytes are the encoding of R' with y taken mod p
-   (decoding y gives x up to sign; R' on the curve proves the root exists;
-   the sign bit picks x's parity -- x = 0 with the sign bit set never
-   matches, which is the AVX-512 decoder's rejection).  So each signature
-   needs R' in affine form, and the inversions are batched per lane with
-   Montgomery's trick: FIN_M signatures share one inversion (3 (M-1)
-   multiplications + 1 inversion instead of M inversions).
-
-   If the encodings match, R is decodable and equal to R': the verdict is
-   ERR_SIG if R has small order (y in {0, 1, -1, y0, y1} -- x = 0 iff
-   y = +-1 on the curve) and SUCCESS otherwise.  Otherwise -- and whenever A
-   has small order, where the verdict depends on whether R decodes -- the
-   signature goes to fix_list and rfix decodes R the reference's way.  Only
-   invalid signatures take that path. */
-
-FD_DEV bool r_encoding_small(const uint32_t (&y)[8]) {
-  const uint32_t y0[8] = {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u,
-                          0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du};
-  const uint32_t y1[8] = {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du,
-                          0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u};
-  uint32_t hi = 0, e0 = 0, e1 = 0, ones = 0;
-#pragma unroll
-  for (int w = 0; w < 8; w++) {
-    if (w) hi |= y[w];
-    e0 |= y[w] ^ y0[w];
-    e1 |= y[w] ^ y1[w];
-    if (w && w < 7) ones |= ~y[w];
-  }
-  const bool y01 = hi == 0u && y[0] <= 1u;                               /* 0, 1  */
-  const bool ym1 = ones == 0u && y[7] == 0x7fffffffu && y[0] == 0xffffffecu;  /* p - 1 */
-  return y01 || ym1 || e0 == 0u || e1 == 0u;
-}
-
-__global__ void __launch_bounds__(256)
-fd_ed25519_fin_kernel(fd_ed25519_verify_params_t p) {
-  constexpr int M = FD_ED25519_FIN_M;
-  const uint64_t lanes = (p.n + M - 1) / M;
-  const uint64_t L = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (L >= lanes) return;
-  const int32_t* PX = p.proj;
-  const int32_t* PY = p.proj + 10 * p.cap;
-  const int32_t* PZ = p.proj + 20 * p.cap;
-
-  fe pre[M];  /* prefix products of Z */
-#pragma unroll
-  for (int t = 0; t < M; t++) {
-    const uint64_t j = L + (uint64_t)t * lanes;
-    fe z;
-    if (j < p.n) load_fe(z, PZ + j, p.cap);
-    else fe_1(z);
-    if (t == 0) pre[0] = z;
-    else fe_mul(pre[t], pre[t - 1], z);
-  }
-  fe inv;
-  fe_invert(inv, pre[M - 1]);
-
-#pragma unroll
-  for (int t = M - 1; t >= 0; t--) {
-    const uint64_t j = L + (uint64_t)t * lanes;
-    const bool live = j < p.n;
-    fe zi;
-    if (t > 0) {
-      fe_mul(zi, inv, pre[t - 1]);
-      fe z;
-      if (live) load_fe(z, PZ + j, p.cap);
-      else fe_1(z);
-      fe_mul(inv, inv, z);
-    } else {
-      zi = inv;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + wave * FD_ED25519_ATAB_BYTES_PER_WAVE) +
+               lane * 180;
+  int4* tabR = tabA + 90;
+  const uint64_t nfix = *p.fix_cnt;
+  const uint64_t total = nfix + p.n;
+  for (;;) {
+    uint32_t b = 0u;
+    if (lane == 0u) b = atomicAdd(p.work_ctr, 64u);
+    b = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)b, 0));
+    if ((uint64_t)b >= total) break;
+    const uint64_t t = (uint64_t)b + lane;
+    if (t < nfix) {
+      const uint64_t j = p.fix_list[t];
+      p.out[p.base + j] = (int8_t)dsm_full_one(p, j, tabA);
+    } else if (t < total) {
+      const uint64_t j = t - nfix;
+      if (!(p.hflag[j] & FD_HF_FULL)) p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
     }
-    if (!live) continue;
-    const int st = p.st[j];
-    int code;
-    if (st < 0) {
-      code = st;
-    } else if (st == FD_ST_ASMALL) {
-      code = 1;  /* R decode needed */
-    } else {
-      fe x, y, X, Y;
-      load_fe(X, PX + j, p.cap);
-      load_fe(Y, PY + j, p.cap);
-      fe_mul(x, X, zi);
-      fe_mul(y, Y, zi);
-      uint32_t xb[8], yb[8], r[8];
-      fe_tobytes(xb, x);
-      fe_tobytes(yb, y);
-      {
-        const uint4* sg = reinterpret_cast<const uint4*>(p.sigs + 64 * (p.base + j));
-        const uint4 q0 = sg[0], q1 = sg[1];
-        r[0] = q0.x; r[1] = q0.y; r[2] = q0.z; r[3] = q0.w; r[4] = q1.x; r[5] = q1.y; r[6] = q1.z; r[7] = q1.w;
-      }
-      const uint32_t sign = r[7] >> 31;
-      r[7] &= 0x7fffffffu;
-      /* y >= p (only 2^255-19 .. 2^255-1) is taken mod p, as the decoder does */
-      uint32_t allf = 0xffffffffu;
-#pragma unroll
-      for (int w = 1; w < 7; w++) allf &= r[w];
-      const bool ge_p = allf == 0xffffffffu && r[7] == 0x7fffffffu && r[0] >= 0xffffffedu;
-      if (ge_p) {
-        r[0] -= 0xffffffedu;
-#pragma unroll
-        for (int w = 1; w < 8; w++) r[w] = 0u;
-      }
-      uint32_t diff = (xb[0] & 1u) ^ sign;
-#pragma unroll
-      for (int w = 0; w < 8; w++) diff |= yb[w] ^ r[w];
-      if (diff == 0u) code = r_encoding_small(yb) ? FD_ED25519_ERR_SIG : FD_ED25519_SUCCESS;
-      else code = 1;
-    }
-    if (code == 1) {
-      const uint32_t slot = atomicAdd(p.fix_cnt, 1u);
-      p.fix_list[slot] = (uint32_t)j;
-    } else {
-      p.out[p.base + j] = (int8_t)code;
-    }
-  }
-}
-
-/* rfix: decode R the reference's way for the signatures fin could not
-   settle (invalid ones, and those with a small-order A).  Persistent grid;
-   the list length is read on the device. */
-__global__ void __launch_bounds__(256, FD_ED25519_DECODE_WAVES_PER_SIMD)
-fd_ed25519_rfix_kernel(fd_ed25519_verify_params_t p) {
-  const uint32_t cnt = *p.fix_cnt;
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < cnt;
-       t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t j = p.fix_list[t];
-    uint32_t s[8];
-    {
-      const uint4* sg = reinterpret_cast<const uint4*>(p.sigs + 64 * (p.base + j));
-      const uint4 q0 = sg[0], q1 = sg[1];
-      s[0] = q0.x; s[1] = q0.y; s[2] = q0.z; s[3] = q0.w; s[4] = q1.x; s[5] = q1.y; s[6] = q1.z; s[7] = q1.w;
-    }
-    decoded_pt d;
-    ge_decode(d, s, !p.codes_portable);
-    int code;
-    if (d.fail) code = FD_ED25519_ERR_SIG;
-    else if (p.st[j] == FD_ST_ASMALL) code = FD_ED25519_ERR_PUBKEY;
-    else if (d.small) code = FD_ED25519_ERR_SIG;
-    else code = FD_ED25519_ERR_MSG;  /* R decodes, is not small, and R' != R */
-    p.out[p.base + j] = (int8_t)code;
   }
 }
 
@@ -464,12 +539,17 @@ fd_ed25519_rfix_kernel(fd_ed25519_verify_params_t p) {
    Base tables [0..entries)B as (y+x, y-x, 2dxy), one entry per lane:
    [e]B by double-and-add over `bits` bits, then affine. */
 
-__global__ void fd_ed25519_gen_btab_kernel(int32_t* btab, int entries, int stride, int bits) {
+__global__ void fd_ed25519_gen_btab_kernel(int32_t* btab, int entries, int stride, int bits, int base_dbl) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= entries) return;
   ge_p3 B, P;
   const fe bx = {FE_BX}, by = {FE_BY}, d2 = {FE_D2};
   B.X = bx; B.Y = by; fe_1(B.Z); fe_mul(B.T, bx, by);
+  for (int i = 0; i < base_dbl; i++) {   /* the table's base: [2^base_dbl]B */
+    ge_p1p1 t2;
+    ge_p3_dbl(t2, B);
+    ge_p1p1_to_p3(B, t2);
+  }
   ge_cached cb;
   ge_p3_to_cached(cb, B);
   ge_p3_0(P);
@@ -527,14 +607,14 @@ __global__ void fd_ed25519_txn_combine_kernel(const int8_t* sig_codes, const uin
 
 extern "C" int fd_ed25519_hip_launch_gen_btab(int32_t* d_btab, void* stream) {
   hipLaunchKernelGGL(fd_ed25519_gen_btab_kernel, dim3(3), dim3(64), 0, (hipStream_t)stream, d_btab,
-                     FD_ED25519_BTAB_ENTRIES, FD_ED25519_BTAB_STRIDE, 8);
+                     FD_ED25519_BTAB_ENTRIES, FD_ED25519_BTAB_STRIDE, 8, 0);
   return (int)hipGetLastError();
 }
 
-extern "C" int fd_ed25519_hip_launch_gen_btab16(int32_t* d_btab16, void* stream) {
+extern "C" int fd_ed25519_hip_launch_gen_btab16(int32_t* d_btab16, int base_dbl, void* stream) {
   const int entries = FD_ED25519_BTAB16_ENTRIES;
   hipLaunchKernelGGL(fd_ed25519_gen_btab_kernel, dim3((entries + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     d_btab16, entries, FD_ED25519_BTAB16_STRIDE, 16);
+                     d_btab16, entries, FD_ED25519_BTAB16_STRIDE, 16, base_dbl);
   return (int)hipGetLastError();
 }
 
@@ -555,21 +635,20 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
     }
     hipLaunchKernelGGL(fd_ed25519_hash_kernel, g, dim3(blk), 0, st, *p);
   } break;
+  case FD_ED25519_PHASE_SCALAR: {
+    /* fix_cnt and the dsm work counter, adjacent words */
+    const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 2 * sizeof(uint32_t), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(fd_ed25519_scalar_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
+  } break;
   case FD_ED25519_PHASE_DECODE:
-    hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
+    hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((2 * p->n + blk - 1) / blk)), dim3(blk), 0, st,
+                       *p);
     break;
   case FD_ED25519_PHASE_DSM: {
     const uint64_t need = (p->n + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
     const uint32_t g = (uint32_t)(need < grid ? need : grid);
     hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
-  } break;
-  case FD_ED25519_PHASE_FIN: {
-    const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, sizeof(uint32_t), st);
-    if (e != hipSuccess) return (int)e;
-    const uint64_t lanes = (p->n + FD_ED25519_FIN_M - 1) / FD_ED25519_FIN_M;
-    hipLaunchKernelGGL(fd_ed25519_fin_kernel, dim3((uint32_t)((lanes + blk - 1) / blk)), dim3(blk), 0, st, *p);
-    const uint64_t need = (p->n + blk - 1) / blk;
-    hipLaunchKernelGGL(fd_ed25519_rfix_kernel, dim3((uint32_t)(need < 1024 ? need : 1024)), dim3(blk), 0, st, *p);
   } break;
   default:
     return (int)hipErrorInvalidValue;

@@ -10,9 +10,9 @@
    HBM layout of an engine (sized once at creation, no per-call device
    allocation on the device-resident path):
      btab   129 x 36 int32            base-point table [0..128]B (LDS image, signing)
-     btab16 32769 x 32 int32          base-point table [0..2^15]B (verify, 4.2 MB)
-     atab   dsm waves x 92160 B       per-lane [0..8](-A) tables
-     work   max_chunk x 243 B         k, flags, decoded A, R' and lists per signature
+     btab16 32769 x 32 int32          base-point tables [0..2^15]B, [0..2^15][2^132]B (verify, 2 x 4.2 MB)
+     atab   dsm waves x 184320 B      per-lane [0..8](-A), [0..8](-+R) tables
+     work   max_chunk x 280 B         k, flags, half-size scalars, decoded A and R, lists per signature
      in/out staging for the host API  grown on demand */
 
 #define _GNU_SOURCE
@@ -41,16 +41,17 @@ struct fd_ed25519_hip_engine {
   char         arch[ 64 ];
 
   int32_t *    d_btab;
-  int32_t *    d_btab16;     /* [0..2^15]B, the verify kernel's wide B table */
+  int32_t *    d_btab16;     /* [0..2^15]B, the verify kernels' wide B table  */
+  int32_t *    d_btab16b;    /* [0..2^15][2^132]B                             */
   void *       d_atab;
   uint8_t *    d_work;       /* one allocation carved into the work arrays */
   uint32_t *   d_k;
   uint8_t *    d_sflag;
   uint8_t *    d_pflag;
   int32_t *    d_pts;
-  int32_t *    d_proj;       /* R' per signature (dsm -> fin) */
-  int8_t *     d_st;         /* dsm status per signature      */
-  uint32_t *   d_fix;        /* fin -> rfix list              */
+  uint32_t *   d_fix;        /* scalar -> dsm full-length list */
+  uint32_t *   d_hs;         /* half-size scalars             */
+  uint8_t *    d_hflag;
   uint32_t *   d_perm;       /* hash order (length-sorted) */
   uint32_t *   d_hist;       /* counting-sort scratch      */
   int          sort;         /* sort the hash phase by SHA-512 block count */
@@ -115,7 +116,7 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   if( !e ) return;
   hipSetDevice( e->device );
   if( e->stream ) hipStreamSynchronize( e->stream );
-  hipFree( e->d_btab ); hipFree( e->d_btab16 ); hipFree( e->d_atab ); hipFree( e->d_work );
+  hipFree( e->d_btab ); hipFree( e->d_btab16 ); hipFree( e->d_btab16b ); hipFree( e->d_atab ); hipFree( e->d_work );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
   hipHostFree( e->h_msgs ); hipHostFree( e->h_off ); hipHostFree( e->h_sz ); hipHostFree( e->h_sigs );
@@ -162,19 +163,20 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   size_t work_sz = (size_t)e->max_chunk * FD_ED25519_WORK_BYTES_PER_SIG + 1024;
   HIPCHK( hipMalloc( (void **)&e->d_btab, btab_sz ), "hipMalloc(btab)" );
   HIPCHK( hipMalloc( (void **)&e->d_btab16, btab16_sz ), "hipMalloc(btab16)" );
+  HIPCHK( hipMalloc( (void **)&e->d_btab16b, btab16_sz ), "hipMalloc(btab16b)" );
   HIPCHK( hipMalloc( &e->d_atab, atab_sz ), "hipMalloc(atab)" );
   HIPCHK( hipMalloc( (void **)&e->d_work, work_sz ), "hipMalloc(work)" );
-  e->device_bytes = btab_sz + btab16_sz + atab_sz + work_sz;
+  e->device_bytes = btab_sz + 2UL*btab16_sz + atab_sz + work_sz;
   uint64_t c = e->max_chunk;
   uint8_t * w = e->d_work;
   e->d_k     = (uint32_t *)w; w += 8UL*4UL*c;
-  e->d_pts   = (int32_t  *)w; w += 20UL*4UL*c;
-  e->d_proj  = (int32_t  *)w; w += 30UL*4UL*c;
+  e->d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
+  e->d_hs    = (uint32_t *)w; w += 19UL*4UL*c;
   e->d_perm  = (uint32_t *)w; w += 4UL*c;
   e->d_fix   = (uint32_t *)w; w += 4UL*c;
   e->d_sflag = w;             w += c;
-  e->d_pflag = w;             w += c;
-  e->d_st    = (int8_t *)w;   w += c;
+  e->d_pflag = w;             w += 2UL*c;
+  e->d_hflag = w;             w += c;
   w = (uint8_t *)(((uintptr_t)w + 255UL) & ~(uintptr_t)255UL);
   e->d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words + fix count inside the 1024-byte slack */
   char const * ns = getenv( "FD_ED25519_HIP_NOSORT" );
@@ -182,8 +184,10 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
 
   int err = fd_ed25519_hip_launch_gen_btab( e->d_btab, e->stream );
   if( err ) return hip_fail( (hipError_t)err, "gen_btab launch" );
-  err = fd_ed25519_hip_launch_gen_btab16( e->d_btab16, e->stream );
+  err = fd_ed25519_hip_launch_gen_btab16( e->d_btab16, 0, e->stream );
   if( err ) return hip_fail( (hipError_t)err, "gen_btab16 launch" );
+  err = fd_ed25519_hip_launch_gen_btab16( e->d_btab16b, FD_ED25519_BTAB16B_SHIFT, e->stream );
+  if( err ) return hip_fail( (hipError_t)err, "gen_btab16b launch" );
   HIPCHK( hipStreamSynchronize( e->stream ), "gen_btab" );
   return FD_ED25519_HIP_OK;
 }
@@ -243,9 +247,10 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz;
   p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
   p.k = e->d_k; p.sflag = e->d_sflag; p.pflag = e->d_pflag; p.pts = e->d_pts; p.cap = e->max_chunk;
-  p.proj = e->d_proj; p.st = e->d_st; p.fix_list = e->d_fix; p.fix_cnt = e->d_hist + 2*FD_ED25519_SORT_BUCKETS;
+  p.fix_list = e->d_fix; p.fix_cnt = e->d_hist + 2*FD_ED25519_SORT_BUCKETS;
+  p.work_ctr = p.fix_cnt + 1; p.hs = e->d_hs; p.hflag = e->d_hflag;
   p.perm = e->sort ? e->d_perm : NULL; p.hist = e->d_hist;
-  p.btab = e->d_btab; p.btab16 = e->d_btab16; p.atab = e->d_atab;
+  p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab16b = e->d_btab16b; p.atab = e->d_atab;
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   for( uint64_t base=0UL; base<n; base+=e->max_chunk ) {
     p.base = base;

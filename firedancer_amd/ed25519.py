@@ -25,7 +25,7 @@ ERR_MSG = -3
 FLAG_CODES_PORTABLE = 1
 
 # phases of a verify launch (FD_ED25519_HIP_PHASE_CNT, include/fd_ed25519_hip.h)
-PHASES = ("hash", "decode", "dsm", "fin")
+PHASES = ("hash", "scalar", "decode", "dsm")
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FD_ED25519_HIP_LIB", os.path.join(_HERE, "_lib", "libfd_ed25519_hip.so"))

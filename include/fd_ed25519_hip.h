@@ -233,7 +233,7 @@ fd_ed25519_hip_corrupt_dev( fd_ed25519_hip_engine_t * engine,
 /* ---- Part 4: measurement and device-memory helpers ------------------ */
 
 /* Phase timing: while enabled, fd_ed25519_hip_verify_dev brackets each of
-   its phases (0 hash, 1 decode, 2 dsm, 3 fin) with HIP events on the stream
+   its phases (0 hash, 1 scalar, 2 decode, 3 dsm) with HIP events on the stream
    they run on (up to 256 chunk launches); _timing_read waits for them and
    returns the summed milliseconds per phase and the number of chunk
    launches, then resets.  Enabling resets too. */

@@ -45,8 +45,7 @@ def main():
             d["hbm_read_bytes_x2_upper"] = per["FETCH_SIZE"] * 2048
         if "WRITE_SIZE" in per:
             d["hbm_write_bytes"] = per["WRITE_SIZE"] * 1024
-        if n and k in ("fd_ed25519_dsm_kernel", "fd_ed25519_hash_kernel", "fd_ed25519_decode_kernel",
-                       "fd_ed25519_fin_kernel"):
+        if n and k in ("fd_ed25519_dsm_kernel", "fd_ed25519_hash_kernel", "fd_ed25519_decode_kernel"):
             lanes = n
         else:
             lanes = None
