@@ -33,6 +33,7 @@ struct fe { int32_t v[10]; };
 /* Constants in centered limbs (tight). */
 #define FE_D      {-10913610, 13857413, -15372611, 6949391, 114729, -8787816, -6275908, -3247719, -18696448, -12055116}
 #define FE_D2     {-21827239, -5839606, -30745221, 13898782, 229458, 15978800, -12551817, -6495438, 29715968, 9444199}
+#define FE_DINV   {30013526, 3972531, -24787780, 12719051, 2979674, -4599962, -15693209, -3644061, 18959709, -16629253}
 #define FE_SQRTM1 {-32595792, -7943725, 9377950, 3500415, 12389472, -272473, -25146209, -2005654, 326686, 11406482}
 #define FE_BX     {-14297830, -7645148, 16144683, -16471763, 27570974, -2696100, -26142465, 8378389, 20764389, 8758491}
 #define FE_BY     {-26843541, -6710886, 13421773, -13421773, 26843546, 6710886, -13421773, 13421773, -26843546, -6710886}

@@ -71,6 +71,20 @@ FD_DEV void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
   fe_mul(r.T2d, p.T, d2);
 }
 
+/* the cached point back in extended form, scaled by 2:
+   (Y+X) - (Y-X) = 2X, (Y+X) + (Y-X) = 2Y, 2Z, 2dT / d = 2T */
+FD_DEV void ge_cached_to_p3(ge_p3& r, const ge_cached& c) {
+  const fe dinv = {FE_DINV};
+  fe t;
+  fe_sub(t, c.YplusX, c.YminusX);
+  fe_carry(r.X, t);
+  fe_add(t, c.YplusX, c.YminusX);
+  fe_carry(r.Y, t);
+  fe_add(t, c.Z, c.Z);
+  fe_carry(r.Z, t);
+  fe_mul(r.T, c.T2d, dinv);
+}
+
 /* r = p + q */
 FD_DEV void ge_add(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
   fe a, b, c, zz, t0;

@@ -29,8 +29,9 @@
    random k) the caller falls back to the full-length multiplication.
 
    The Euclidean steps run Lehmer-style (Knuth, TAOCP 4.5.2, Algorithm L):
-   quotients are found from 52 leading bits in double precision (exact
-   there) and verified by the two-sided test, the cofactor matrix is
+   quotients are found from 52 leading bits, every value an exact integer
+   in double precision (FMA remainders), and verified by the two-sided
+   test, the cofactor matrix is
    applied to the full-length values once per round; the last steps near
    2^131 and rounds with an unverifiable quotient use single conservative
    steps (a quotient estimate never above the true one, so a step may be
@@ -180,11 +181,21 @@ FD_HALF_FN void fd_half_single(uint32_t (&a)[8], uint32_t (&b)[8], uint32_t (&ta
   fd_half_swap(a, b, ta, tb, fd_half_lt(a, b));
 }
 
-/* floor(x / y) for 0 <= x < 2^53, 0 < y < 2^53 */
-FD_HALF_FN int64_t fd_half_fdiv(int64_t x, int64_t y) {
-  int64_t q = (int64_t)((double)x / (double)y);
-  if (q * y > x) q--;
-  else if ((q + 1) * y <= x) q++;
+/* floor(x / y) for integers 0 <= x < 2^53, 0 < y < 2^53 held in doubles:
+   an estimate from a refined reciprocal, then exact remainder corrections
+   (fma(-q, y, x) is exact on these integers) */
+#ifndef FD_HALF_RCP
+#define FD_HALF_RCP(y) (1.0 / (y))
+#endif
+FD_HALF_FN double fd_half_fdiv(double x, double y) {
+  double r = FD_HALF_RCP(y);
+  r = __builtin_fma(r, __builtin_fma(-y, r, 1.0), r);
+  double q = __builtin_floor(x * r);
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const double rem = __builtin_fma(-q, y, x);
+    q = rem < 0.0 ? q - 1.0 : (rem >= y ? q + 1.0 : q);
+  }
   return q;
 }
 
@@ -219,21 +230,24 @@ FD_HALF_FN int fd_half_scalars(const uint32_t (&k)[8], uint32_t (&c)[FD_HALF_TW]
   while (fd_half_bitlen<8>(b) > FD_HALF_BITS + FD_HALF_LEHMER_MARGIN) {
     if (++it > 200) { ok = 0; break; }
     const int s = fd_half_bitlen<8>(a) - 52;   /* a > 2^137: s > 0 */
-    int64_t uh = (int64_t)fd_half_shr64(a, s), vh = (int64_t)fd_half_shr64(b, s);
+    /* leading 52 bits and the cosequences, all exact integers in doubles */
+    double uh = (double)fd_half_shr64(a, s), vh = (double)fd_half_shr64(b, s);
     /* the emulated remainder must stay above the margin (Knuth L with a floor) */
     const int fl = FD_HALF_BITS + FD_HALF_LEHMER_MARGIN - s;
-    const int64_t floor_v = fl > 0 ? ((int64_t)1 << (fl < 62 ? fl : 62)) : 0;
-    int64_t A = 1, B = 0, C = 0, D = 1;
+    const double floor_v = fl > 0 ? (double)((uint64_t)1 << (fl < 62 ? fl : 62)) : 0.0;
+    double Af = 1.0, Bf = 0.0, Cf = 0.0, Df = 1.0;
     for (int inner = 0; inner < 64; inner++) {
-      if (vh + C <= 0 || vh + D <= 0 || uh + A < 0 || uh + B < 0) break;
-      const int64_t q = fd_half_fdiv(uh + A, vh + C);
-      if (q != fd_half_fdiv(uh + B, vh + D)) break;
-      const int64_t nv = uh - q * vh;
+      const double x1 = uh + Af, y1 = vh + Cf, x2 = uh + Bf, y2 = vh + Df;
+      if (!(y1 > 0.0 && y2 > 0.0 && x1 >= 0.0 && x2 >= 0.0)) break;
+      const double q = fd_half_fdiv(x1, y1);
+      if (q != fd_half_fdiv(x2, y2)) break;
+      const double nv = __builtin_fma(-q, vh, uh);
       if (nv < floor_v) break;
-      int64_t T = A - q * C; A = C; C = T;
-      T = B - q * D; B = D; D = T;
+      double T = __builtin_fma(-q, Cf, Af); Af = Cf; Cf = T;
+      T = __builtin_fma(-q, Df, Bf); Bf = Df; Df = T;
       uh = vh; vh = nv;
     }
+    const int64_t A = (int64_t)Af, B = (int64_t)Bf, C = (int64_t)Cf, D = (int64_t)Df;
     if (B == 0) {
       fd_half_single(a, b, ta, tb);
     } else {

@@ -30,6 +30,7 @@
 #include "fd25519_sc.h"
 #include "fd_sha512_dev.h"
 #define FD_HALF_FN __device__ static inline
+#define FD_HALF_RCP(y) __builtin_amdgcn_rcp(y)
 #include "fd25519_half.h"
 
 
@@ -200,11 +201,14 @@ FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
   atab_store(tab, 0, c);
   ge_p3_to_cached(c1, P0);
   atab_store(tab, 1, c1);
+  /* P0 is affine: the multiples by mixed additions (3 multiplications) */
+  ge_precomp pre;
+  pre.yplusx = c1.YplusX; pre.yminusx = c1.YminusX; pre.xy2d = c1.T2d;
   ge_p3 cur = P0;
   ge_p1p1 sum;
 #pragma clang loop unroll(disable)
   for (int e = 2; e <= 8; e++) {
-    ge_add(sum, cur, c1);
+    ge_madd(sum, cur, pre);
     ge_p1p1_to_p3(cur, sum);
     ge_p3_to_cached(c, cur);
     atab_store(tab, e, c);
@@ -402,6 +406,9 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     int ea = pop160<4>(cd), er = pop160<4>(dd);
     if (it == 32) { ea &= 15; er &= 15; }   /* top digits in [0,8] */
     ge_cached ca, cr;
+    const bool badd = (it & 3) == 0;
+    int f = 0, g = 0;
+    ge_precomp b1, b2;
     atab_load(ca, tabA, ea < 0 ? -ea : ea);
     if (it != 32) {
 #pragma clang loop unroll(disable)
@@ -415,9 +422,6 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     ge_cached_cneg(ca, ea < 0);
     ge_add(Rt, P, ca);
     ge_p1p1_to_p3(P, Rt);
-    const bool badd = (it & 3) == 0;
-    int f = 0, g = 0;
-    ge_precomp b1, b2;
     if (badd) {
       f = pop160<16>(ld);
       g = pop160<16>(hd);
