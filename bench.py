@@ -187,6 +187,17 @@ def pmc_traffic(n):
         return None, None
 
 
+def pmc_valu_per_sig():
+    """Executed INT32+INT64 VALU instructions per signature (= per lane:
+    one signature per lane) of the dsm kernel (rocprofv3
+    SQ_INSTS_VALU_INT32/INT64 x 64 / signatures, committed summary)."""
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", "pmc_latest.json")))["fd_ed25519_dsm_kernel"]
+        return d["SQ_INSTS_VALU_INT32_per_signature"] + d["SQ_INSTS_VALU_INT64_per_signature"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -275,6 +286,12 @@ def main():
     if rank == 0 and args.latency_txns > 0:
         lat = latency_mode(eng, args, local % ndev)
     traffic, traffic_src = pmc_traffic(min(n, info["max_chunk"]))
+    # executed (not algorithmic) instruction rate of the dsm kernel: the
+    # half-size formulation executes fewer operations than the reference's
+    # algorithm counted above, so both are reported
+    valu = pmc_valu_per_sig()
+    sig_launch = min(n, info["max_chunk"])
+    executed = (valu * sig_launch / (per_launch["dsm"] * 1e-3) / 1e12) if valu and per_launch["dsm"] > 0 else None
 
     if rank == 0:
         line = {
@@ -302,6 +319,9 @@ def main():
                          "traffic_unit": "bytes per launch (HBM read+write, rocprofv3 FETCH_SIZE+WRITE_SIZE)",
                          "traffic_source": traffic_src,
                          "ops_per_launch": dsm_ops, "launch_ms": per_launch["dsm"],
+                         "executed": {"achieved": executed, "frac": (executed / peak) if executed else None,
+                                      "unit": "TOPS (INT32+INT64 VALU lane-instructions / s)",
+                                      "valu_per_signature": valu, "source": traffic_src},
                          "path": {"achieved": path_achieved, "frac": (path_achieved / peak) if path_achieved else None,
                                   "ops_per_verify_mean": path_ops * chunks / n, "ms_per_launch": path_ms},
                          "signatures_per_launch": min(n, info["max_chunk"])},
