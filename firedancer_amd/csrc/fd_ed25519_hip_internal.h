@@ -40,6 +40,9 @@ extern "C" {
 #ifndef FD_ED25519_HASH_WAVES_PER_SIMD
 #define FD_ED25519_HASH_WAVES_PER_SIMD 2  /* measured: 2 (200 VGPR, no spill) beats 3 (spills) */
 #endif
+#ifndef FD_ED25519_SCALAR_WAVES_PER_SIMD
+#define FD_ED25519_SCALAR_WAVES_PER_SIMD 4
+#endif
 #ifndef FD_ED25519_DECODE_WAVES_PER_SIMD
 #define FD_ED25519_DECODE_WAVES_PER_SIMD 2
 #endif

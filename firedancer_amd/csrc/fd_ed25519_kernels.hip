@@ -238,7 +238,7 @@ FD_DEV void btab_add(ge_p1p1& Rt, const ge_p3& P, ge_precomp& b, int f) {
    sign in hflag.  Signatures whose k has no such pair (~0.13% of random k)
    are flagged and queued on fix_list for the full-length form. */
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, FD_ED25519_SCALAR_WAVES_PER_SIMD)
 fd_ed25519_scalar_kernel(fd_ed25519_verify_params_t p) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= p.n) return;

@@ -73,3 +73,8 @@ def oracle_many(oracle, d, codes=0, nthreads=8):
                                    pubs.ctypes.data, out.ctypes.data, codes, nthreads)
     assert rc == 0
     return out
+
+
+@pytest.fixture(scope="session")
+def halfsize():
+    return load_golden("halfsize")

@@ -181,3 +181,33 @@ def test_dropin_batch_single_msg(fd, batch):
 
 def test_strerror(fd):
     assert fd.strerror(0) == "success" and fd.strerror(-3) == "bad message" and fd.strerror(5) == "unknown"
+
+
+def test_halfsize_fallback(eng, halfsize):
+    """k with no half-size pair: the dsm kernel's full-length items."""
+    _check(_run(eng, halfsize), halfsize["codes_avx512"], halfsize["tags"])
+
+
+def test_halfsize_fallback_portable(eng_portable, halfsize):
+    _check(_run(eng_portable, halfsize), halfsize["codes_portable"], halfsize["tags"])
+
+
+def test_halfsize_fallback_scattered(eng, halfsize, adversarial):
+    """The full-length items scattered through a larger chunk (they are
+    handed out first by the dsm work counter, the rest after them)."""
+    rng = np.random.default_rng(11)
+    reps = 24
+    parts = [halfsize] * reps + [adversarial] * 4
+    order = rng.permutation(sum(len(p["msg_sz"]) for p in parts))
+    msgs, off, sz, sigs, pubs, want = [], [], [], [], [], []
+    base = 0
+    for p in parts:
+        msgs.append(p["msgs"])
+        off.append(p["msg_off"].astype(np.uint64) + np.uint64(base))
+        base += len(p["msgs"])
+        sz.append(p["msg_sz"]); sigs.append(p["sigs"]); pubs.append(p["pubs"]); want.append(p["codes_avx512"])
+    msgs = np.concatenate(msgs)
+    off, sz = np.concatenate(off)[order], np.concatenate(sz)[order]
+    sigs, pubs, want = np.concatenate(sigs)[order], np.concatenate(pubs)[order], np.concatenate(want)[order]
+    got = eng.verify_host(msgs, off, sz, sigs, pubs)
+    _check(got, want)

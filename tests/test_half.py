@@ -103,3 +103,20 @@ def test_matches_exact_euclid(half):
             agree += (c, d) == (rc, rd)
         assert ok or not rok or True
     assert agree > 2900, agree
+
+
+def test_fixture_k_have_no_half_pair(half):
+    """tests/golden/halfsize.npz (gen_halfsize.py) holds signatures whose k
+    takes the full-length form: check that property on the fixture."""
+    import hashlib
+    import numpy as np
+    from conftest import load_golden
+    d = load_golden("halfsize")
+    for i in range(len(d["msg_sz"])):
+        off, sz = int(d["msg_off"][i]), int(d["msg_sz"][i])
+        m = bytes(d["msgs"][off:off + sz])
+        k = int.from_bytes(hashlib.sha512(d["sigs"][i][:32].tobytes() + d["pubs"][i].tobytes() + m).digest(),
+                           "little") % L
+        ok, _, _ = run(half, k)
+        assert not ok, (i, str(d["tags"][i]))
+    assert len(set(d["codes_avx512"].tolist())) == 4 and np.any(d["codes_avx512"] == 0)

@@ -97,3 +97,11 @@ def test_empty_message_null(oracle):
     """msg==NULL with sz==0 is fine (src/ballet/ed25519/fd_ed25519.h:78-80)."""
     d = json.load(open(os.path.join(GOLDEN, "sign_kat.json")))[0]
     assert oracle.oracle_ed25519_verify(None, 0, bytes.fromhex(d["sig"]), bytes.fromhex(d["pub"]), 0) == 0
+
+
+@pytest.mark.parametrize("codes,key", [(0, "codes_avx512"), (1, "codes_portable")])
+def test_halfsize_fallback_codes(oracle, halfsize, codes, key):
+    """Signatures whose k has no half-size pair (gen_halfsize.py)."""
+    got = oracle_many(oracle, halfsize, codes)
+    bad = np.nonzero(got != halfsize[key])[0]
+    assert len(bad) == 0, [(str(halfsize["tags"][i]), int(got[i]), int(halfsize[key][i])) for i in bad[:10]]
