@@ -50,7 +50,9 @@
 
 #define FD_HALF_BITS 131   /* 0 <= c < 2^FD_HALF_BITS, |d| < 2^FD_HALF_BITS */
 #define FD_HALF_TW   5     /* t values: 160-bit two's complement */
-#define FD_HALF_LEHMER_MARGIN 6  /* Lehmer rounds stop this many bits above 2^FD_HALF_BITS */
+#ifndef FD_HALF_LEHMER_MARGIN
+#define FD_HALF_LEHMER_MARGIN 0  /* Lehmer rounds stop this many bits above 2^FD_HALF_BITS (0: measured fastest, same fallback rate) */
+#endif
 
 /* 8L, little-endian 32-bit words */
 #define FD_HALF_N8L {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0u, 0u, 0u, 0x80000000u}
