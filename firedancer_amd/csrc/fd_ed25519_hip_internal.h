@@ -17,12 +17,17 @@ extern "C" {
 #define FD_ED25519_BTAB_STRIDE    36
 #define FD_ED25519_BTAB_INTS      (FD_ED25519_BTAB_ENTRIES * FD_ED25519_BTAB_STRIDE)
 
-/* Wide base-point tables of the verify kernels: [0..2^15]B and
-   [0..2^15][2^132]B (signed radix-2^16 digits), 128-byte entries, 4.2 MB
-   each, read from HBM / L2 / MALL with each entry loaded a window ahead. */
+/* Wide base-point tables of the verify kernels, 128-byte entries
+   (y+x, y-x, 2dxy, pad), read from HBM / L2 / MALL with each entry loaded
+   ahead of its use:
+     btab16   [0..2^15]B, signed radix-2^16 digits of S (full-length form), 4.2 MB
+     btab20   [0..2^20)B, unsigned radix-2^20 digits of s_lo (half-size form), 128 MB
+     btab20b  [0..2^20)[2^132]B, digits of s_hi, 128 MB
+   The two 128 MB tables are shared by all engines of a device. */
 #define FD_ED25519_BTAB16_ENTRIES ((1 << 15) + 1)
-#define FD_ED25519_BTAB16B_SHIFT  132
 #define FD_ED25519_BTAB16_STRIDE  32
+#define FD_ED25519_BTAB20_ENTRIES (1 << 20)
+#define FD_ED25519_BTAB20B_SHIFT  132
 
 /* Per-lane table of [0..8](-A) in cached form, in HBM: 9 entries x 40 int32
    per lane, laid out [wave][lane][entry][quad] (int4 granules): a lookup
@@ -86,7 +91,8 @@ typedef struct {
   uint64_t         cap;
   int32_t const *  btab;     /* device base-point table (FD_ED25519_BTAB_INTS) */
   int32_t const *  btab16;   /* [0..2^15]B,          [FD_ED25519_BTAB16_ENTRIES][32] */
-  int32_t const *  btab16b;  /* [0..2^15][2^132]B,   same layout                     */
+  int32_t const *  btab20;   /* [0..2^20)B,          [FD_ED25519_BTAB20_ENTRIES][32] */
+  int32_t const *  btab20b;  /* [0..2^20)[2^132]B,   same layout                     */
   void *           atab;     /* device scratch, waves * ATAB_BYTES_PER_WAVE    */
   int              codes_portable; /* 0: AVX-512 backend codes, 1: portable  */
 } fd_ed25519_verify_params_t;
@@ -95,6 +101,9 @@ typedef struct {
    hipError_t value (0 on success). */
 int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
 int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, int base_doublings, void * stream );
+/* [0..2^20)[2^base_doublings]B into d_tab; d_scratch holds
+   FD_ED25519_BTAB20_ENTRIES*10 + 40 int32 */
+int fd_ed25519_hip_launch_gen_btab20( int32_t * d_tab, int base_doublings, int32_t * d_scratch, void * stream );
 /* Enqueues hash, decode and dsm for one chunk; `grid` caps the persistent
    dsm grid (its atab scratch must hold grid*VERIFY_BLOCK/64 waves). */
 int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t grid, void * stream );

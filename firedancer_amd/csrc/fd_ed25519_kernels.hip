@@ -341,6 +341,15 @@ FD_DEV void recode160(uint32_t (&out)[5], const uint32_t (&x)[5]) {
 }
 
 template <int BITS>
+FD_DEV uint32_t pop160u(uint32_t (&d)[5]) {
+  const uint32_t v = d[4] >> (32 - BITS);
+#pragma unroll
+  for (int w = 4; w > 0; w--) d[w] = __builtin_amdgcn_alignbit(d[w], d[w - 1], 32 - BITS);
+  d[0] <<= BITS;
+  return v;
+}
+
+template <int BITS>
 FD_DEV int pop160(uint32_t (&d)[5]) {
   const int v = ((int32_t)d[4]) >> (32 - BITS);
 #pragma unroll
@@ -365,8 +374,9 @@ FD_DEV void load_hs(uint32_t (&x)[5], const fd_ed25519_verify_params_t& p, int r
    invertible on it).  A four-scalar Straus loop over 33 signed 4-bit
    windows: 128 doublings (against 252 for the reference's double-scalar
    form), 33 additions from each lane's [0..8](-A) and [0..8](-+R) tables
-   (HBM, lane-contiguous 160-byte entries) and 9 + 9 mixed additions from
-   the two radix-2^16 base tables (HBM/L2).  Every table entry is loaded
+   (HBM, lane-contiguous 160-byte entries) and 7 + 7 mixed additions from
+   the two unsigned radix-2^20 base tables [0..2^20)B and [0..2^20)B'
+   (128 MB each, HBM/MALL).  Every table entry is loaded
    one step ahead of its use: the -A entry before the window's doublings,
    the R entry before the -A addition, the base entries before the R
    addition.  The result is compared with the identity (X == 0, Y == Z). */
@@ -384,18 +394,18 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     table_build(tabR, x, y, !(hf & FD_HF_DNEG));
   }
   /* digits, most significant first, top-aligned in 160 bits: c, |d| in
-     radix 16 (33 digits, the top one in [0,8]), s_lo, s_hi in radix 2^16
-     (9 digits) */
+     radix 16 (33 signed digits, the top one in [0,8]), s_lo, s_hi in
+     radix 2^20 (7 unsigned digits: no recoding, no negation) */
   uint32_t cd[5], dd[5], ld[5], hd[5];
   {
     uint32_t x[5], t[5];
     load_hs(x, p, 0, 5, j);  shl160<28>(t, x); recode160<4>(cd, t);
     load_hs(x, p, 5, 5, j);  shl160<28>(t, x); recode160<4>(dd, t);
-    load_hs(x, p, 10, 5, j); shl160<16>(t, x); recode160<16>(ld, t);
-    load_hs(x, p, 15, 4, j); shl160<16>(t, x); recode160<16>(hd, t);
+    load_hs(x, p, 10, 5, j); shl160<20>(ld, x);
+    load_hs(x, p, 15, 4, j); shl160<20>(hd, x);
   }
-  const int4* g_btab = reinterpret_cast<const int4*>(p.btab16);
-  const int4* g_btab2 = reinterpret_cast<const int4*>(p.btab16b);
+  const int4* g_btab = reinterpret_cast<const int4*>(p.btab20);
+  const int4* g_btab2 = reinterpret_cast<const int4*>(p.btab20b);
 
   ge_p3 P;
   ge_p3_0(P);
@@ -406,8 +416,8 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     int ea = pop160<4>(cd), er = pop160<4>(dd);
     if (it == 32) { ea &= 15; er &= 15; }   /* top digits in [0,8] */
     ge_cached ca, cr;
-    const bool badd = (it & 3) == 0;
-    int f = 0, g = 0;
+    const bool badd = it % 5 == 0;           /* base digits at bits 20m: windows 30, 25, .., 0 */
+    uint32_t f = 0, g = 0;
     ge_precomp b1, b2;
     atab_load(ca, tabA, ea < 0 ? -ea : ea);
     if (it != 32) {
@@ -423,18 +433,18 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     ge_add(Rt, P, ca);
     ge_p1p1_to_p3(P, Rt);
     if (badd) {
-      f = pop160<16>(ld);
-      g = pop160<16>(hd);
-      btab16_load(b1, g_btab, f < 0 ? -f : f);
-      btab16_load(b2, g_btab2, g < 0 ? -g : g);
+      f = pop160u<20>(ld);
+      g = pop160u<20>(hd);
+      btab16_load(b1, g_btab, (int)f);
+      btab16_load(b2, g_btab2, (int)g);
     }
     ge_cached_cneg(cr, er < 0);
     ge_add(Rt, P, cr);
     if (badd) {
       ge_p1p1_to_p3(P, Rt);
-      btab_add(Rt, P, b1, f);
+      ge_madd(Rt, P, b1);
       ge_p1p1_to_p3(P, Rt);
-      btab_add(Rt, P, b2, g);
+      ge_madd(Rt, P, b2);
     }
     ge_p1p1_to_p2(Q, Rt);
   }
@@ -583,6 +593,90 @@ __global__ void fd_ed25519_gen_btab_kernel(int32_t* btab, int entries, int strid
   for (int i = 30; i < stride; i++) o[i] = 0;
 }
 
+/* Wide unsigned-digit tables [0..2^20)[2^base_dbl]B.  The base is computed
+   once (gen_base), then each thread produces a run of consecutive entries
+   by additions and puts them in affine form with one inversion per run
+   (Montgomery's trick: prefix products of Z in `scratch`). */
+#define FD_BTAB_RUN 32
+
+__global__ void fd_ed25519_gen_base_kernel(int32_t* base, int base_dbl) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  ge_p3 B;
+  const fe bx = {FE_BX}, by = {FE_BY};
+  B.X = bx; B.Y = by; fe_1(B.Z); fe_mul(B.T, bx, by);
+  for (int i = 0; i < base_dbl; i++) {
+    ge_p1p1 t2;
+    ge_p3_dbl(t2, B);
+    ge_p1p1_to_p3(B, t2);
+  }
+  for (int i = 0; i < 10; i++) {
+    base[i] = B.X.v[i]; base[10 + i] = B.Y.v[i]; base[20 + i] = B.Z.v[i]; base[30 + i] = B.T.v[i];
+  }
+}
+
+FD_DEV void fe_st(int32_t* o, const fe& a) {
+  for (int i = 0; i < 10; i++) o[i] = a.v[i];
+}
+FD_DEV void fe_ld(fe& a, const int32_t* o) {
+  for (int i = 0; i < 10; i++) a.v[i] = o[i];
+}
+
+__global__ void __launch_bounds__(256)
+fd_ed25519_gen_btab_run_kernel(int32_t* tab, int entries, const int32_t* base, int32_t* scratch) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e0 = t * FD_BTAB_RUN;
+  if (e0 >= entries) return;
+  const int e1 = e0 + FD_BTAB_RUN < entries ? e0 + FD_BTAB_RUN : entries;
+  ge_p3 B, P;
+  fe_ld(B.X, base); fe_ld(B.Y, base + 10); fe_ld(B.Z, base + 20); fe_ld(B.T, base + 30);
+  ge_cached cb;
+  ge_p3_to_cached(cb, B);
+  ge_p3_0(P);
+  ge_p1p1 r;
+  for (int bit = 20; bit >= 0; bit--) {   /* P = [e0] base */
+    ge_p3_dbl(r, P);
+    ge_p1p1_to_p3(P, r);
+    if ((e0 >> bit) & 1) {
+      ge_add(r, P, cb);
+      ge_p1p1_to_p3(P, r);
+    }
+  }
+  fe acc;
+  fe_1(acc);
+  for (int e = e0; e < e1; e++) {   /* projective entries, prefix products of Z */
+    int32_t* o = tab + (int64_t)e * FD_ED25519_BTAB16_STRIDE;
+    fe_st(o, P.X); fe_st(o + 10, P.Y); fe_st(o + 20, P.Z);
+    fe_mul(acc, acc, P.Z);
+    fe_st(scratch + (int64_t)e * 10, acc);
+    ge_add(r, P, cb);
+    ge_p1p1_to_p3(P, r);
+  }
+  fe inv;
+  fe_invert(inv, acc);
+  const fe d2 = {FE_D2};
+  for (int e = e1 - 1; e >= e0; e--) {
+    int32_t* o = tab + (int64_t)e * FD_ED25519_BTAB16_STRIDE;
+    fe X, Y, Z, zi, x, y, ypx, ymx, xy2d;
+    fe_ld(X, o); fe_ld(Y, o + 10); fe_ld(Z, o + 20);
+    if (e > e0) {
+      fe prev;
+      fe_ld(prev, scratch + (int64_t)(e - 1) * 10);
+      fe_mul(zi, inv, prev);
+    } else {
+      zi = inv;
+    }
+    fe_mul(inv, inv, Z);
+    fe_mul(x, X, zi);
+    fe_mul(y, Y, zi);
+    fe_add(ypx, y, x); fe_carry(ypx, ypx);
+    fe_sub(ymx, y, x); fe_carry(ymx, ymx);
+    fe_mul(xy2d, x, y);
+    fe_mul(xy2d, xy2d, d2);
+    fe_st(o, ypx); fe_st(o + 10, ymx); fe_st(o + 20, xy2d);
+    o[30] = 0; o[31] = 0;
+  }
+}
+
 /* ------------------------------------------------------------------------
    Per-transaction combine (fd_ed25519_verify_batch_single_msg priority). */
 
@@ -619,6 +713,16 @@ extern "C" int fd_ed25519_hip_launch_gen_btab16(int32_t* d_btab16, int base_dbl,
   const int entries = FD_ED25519_BTAB16_ENTRIES;
   hipLaunchKernelGGL(fd_ed25519_gen_btab_kernel, dim3((entries + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      d_btab16, entries, FD_ED25519_BTAB16_STRIDE, 16, base_dbl);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fd_ed25519_hip_launch_gen_btab20(int32_t* d_tab, int base_dbl, int32_t* d_scratch, void* stream) {
+  const int entries = FD_ED25519_BTAB20_ENTRIES;
+  int32_t* base = d_scratch + (size_t)entries * 10;   /* 40 ints after the prefix products */
+  hipLaunchKernelGGL(fd_ed25519_gen_base_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, base, base_dbl);
+  const int threads = (entries + FD_BTAB_RUN - 1) / FD_BTAB_RUN;
+  hipLaunchKernelGGL(fd_ed25519_gen_btab_run_kernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     d_tab, entries, (const int32_t*)base, d_scratch);
   return (int)hipGetLastError();
 }
 
