@@ -211,3 +211,22 @@ def test_halfsize_fallback_scattered(eng, halfsize, adversarial):
     sigs, pubs, want = np.concatenate(sigs)[order], np.concatenate(pubs)[order], np.concatenate(want)[order]
     got = eng.verify_host(msgs, off, sz, sigs, pubs)
     _check(got, want)
+
+
+def test_engines_share_base_tables(fd, adversarial):
+    """The 2 x 128 MB base tables are shared by the engines of a device and
+    freed with the last one: engines created and destroyed in overlapping
+    order all verify correctly, including after a full release."""
+    want = adversarial["codes_avx512"]
+    a = fd.Engine(0, max_chunk=1 << 12)
+    b = fd.Engine(0, max_chunk=1 << 12)
+    _check(_run(a, adversarial), want)
+    a.close()
+    _check(_run(b, adversarial), want)
+    c = fd.Engine(0, max_chunk=1 << 12)
+    b.close()
+    _check(_run(c, adversarial), want)
+    c.close()
+    d = fd.Engine(0, max_chunk=1 << 12)   # the module's engines may still hold them; either way correct
+    _check(_run(d, adversarial), want)
+    d.close()
