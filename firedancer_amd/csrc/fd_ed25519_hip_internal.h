@@ -29,8 +29,9 @@ extern "C" {
 #define FD_ED25519_BTAB20_ENTRIES (1 << 20)
 #define FD_ED25519_BTAB20B_SHIFT  132
 
-/* Per-lane table of [0..8](-A) in cached form, in HBM: 9 entries x 40 int32
-   per lane, laid out [wave][lane][entry][quad] (int4 granules): a lookup
+/* Per-lane tables [0..8](-A) and [0..8](-+R) in cached form, in HBM: 2 x 9
+   entries x 40 int32 per lane, laid out [wave][lane][entry][quad] (int4
+   granules, lane stride 180 int4): a lookup
    reads 160 contiguous bytes of the lane's own table, so every fetched line
    is fully used (the [entry][quad][lane] layout fetched ~2.4x the table
    bytes from HBM because lanes pick different entries). */
