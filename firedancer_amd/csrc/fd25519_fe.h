@@ -145,6 +145,30 @@ FD_DEV void fe_mul(fe& h, const fe& f, const fe& g) {
   fe_carry_wide(h, a);
 }
 
+/* 19 g (limbs 1..9; limb 0 never wraps), for products that share g */
+FD_DEV void fe_19(fe& g19, const fe& g) {
+  g19.v[0] = 0;
+#pragma unroll
+  for (int j = 1; j < 10; j++) g19.v[j] = 19 * g.v[j];
+}
+
+/* h = f*g with 19 g given */
+FD_DEV void fe_mul19(fe& h, const fe& f, const fe& g, const fe& g19) {
+  int64_t a[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      const int k = i + j;
+      const int32_t x = ((i & 1) && (j & 1)) ? 2 * f.v[i] : f.v[i];
+      const int32_t y = (k >= 10) ? g19.v[j] : g.v[j];
+      if (i == 0) fe_mad_init(a[k], x, y, k);
+      else fe_mad(a[k >= 10 ? k - 10 : k], x, y);
+    }
+  }
+  fe_carry_wide(h, a);
+}
+
 /* h = f^2 (55 products): off-diagonal terms carry the factor 2 on the
    left operand, the odd/odd and wrap factors (2, 19, 38) on the right. */
 FD_DEV void fe_sq(fe& h, const fe& f) {

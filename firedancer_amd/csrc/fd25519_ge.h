@@ -30,17 +30,41 @@ FD_DEV void ge_p3_0(ge_p3& h) {
   fe_0(h.X); fe_1(h.Y); fe_1(h.Z); fe_0(h.T);
 }
 
+#ifndef FD_GE_SHARE19
+#define FD_GE_SHARE19 1
+#endif
+
+/* The conversions share each right operand between two products, so its
+   19-multiples (the wrapped terms) are computed once. */
 FD_DEV void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
+#if FD_GE_SHARE19
+  fe t19;
+  fe_19(t19, p.T);
+  fe_mul19(r.X, p.X, p.T, t19);
+  fe_mul19(r.Z, p.Z, p.T, t19);
+  fe_mul(r.Y, p.Y, p.Z);
+#else
   fe_mul(r.X, p.X, p.T);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
+#endif
 }
 
 FD_DEV void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
+#if FD_GE_SHARE19
+  fe t19, y19;
+  fe_19(t19, p.T);
+  fe_mul19(r.X, p.X, p.T, t19);
+  fe_mul19(r.Z, p.Z, p.T, t19);
+  fe_19(y19, p.Y);
+  fe_mul19(r.Y, p.Z, p.Y, y19);
+  fe_mul19(r.T, p.X, p.Y, y19);
+#else
   fe_mul(r.X, p.X, p.T);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
   fe_mul(r.T, p.X, p.Y);
+#endif
 }
 
 /* r = 2p  (4 squarings) */
