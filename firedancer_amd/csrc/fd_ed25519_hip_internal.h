@@ -126,6 +126,10 @@ int fd_ed25519_hip_launch_txn_combine( int8_t const * d_sig_codes, uint32_t cons
                                        uint32_t const * d_txn_cnt, int8_t * d_txn_out, uint64_t ntxn,
                                        void * stream );
 
+/* diagnostic: fd_half_scalars on the device, 12 words out per k (see
+   fd_ed25519_hip_diag_half_scalars) */
+int fd_ed25519_hip_launch_diag_half( uint32_t const * d_k, uint32_t * d_out, uint64_t n, void * stream );
+
 /* ---- raw transactions (fd_ed25519_txn.hip) ---- */
 
 /* per-transaction code for a payload fd_txn_parse rejects (never an

@@ -716,6 +716,26 @@ extern "C" int fd_ed25519_hip_launch_gen_btab16(int32_t* d_btab16, int base_dbl,
   return (int)hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) fd_ed25519_diag_half_kernel(const uint32_t* kin, uint32_t* out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8], c[FD_HALF_TW], d[FD_HALF_TW];
+  for (int w = 0; w < 8; w++) k[w] = kin[8 * i + w];
+  int neg = 0;
+  const int ok = fd_half_scalars(k, c, d, &neg);
+  uint32_t* o = out + 12 * i;
+  o[0] = (uint32_t)ok;
+  o[1] = (uint32_t)neg;
+  for (int w = 0; w < FD_HALF_TW; w++) { o[2 + w] = c[w]; o[7 + w] = d[w]; }
+}
+
+extern "C" int fd_ed25519_hip_launch_diag_half(const uint32_t* d_k, uint32_t* d_out, uint64_t n, void* stream) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(fd_ed25519_diag_half_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     d_k, d_out, n);
+  return (int)hipGetLastError();
+}
+
 extern "C" int fd_ed25519_hip_launch_gen_btab20(int32_t* d_tab, int base_dbl, int32_t* d_scratch, void* stream) {
   const int entries = FD_ED25519_BTAB20_ENTRIES;
   int32_t* base = d_scratch + (size_t)entries * 10;   /* 40 ints after the prefix products */

@@ -68,6 +68,7 @@ _lib.fd_ed25519_hip_dev_free.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 _lib.fd_ed25519_hip_memcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
                                        ctypes.c_int]
 _lib.fd_ed25519_hip_device_clock_mhz.argtypes = [ctypes.c_void_p]
+_lib.fd_ed25519_hip_diag_half_scalars.argtypes = [ctypes.c_void_p, _u8p, ctypes.c_ulong, _u8p]
 _lib.fd_ed25519_hip_strerror.argtypes = [ctypes.c_int]
 _lib.fd_ed25519_hip_strerror.restype = ctypes.c_char_p
 _lib.fd_ed25519_hip_last_error.restype = ctypes.c_char_p
@@ -218,6 +219,16 @@ class Engine:
         cnt = ctypes.c_ulong(0)
         _check(_lib.fd_ed25519_hip_engine_timing_read(self._h, ms, ctypes.byref(cnt)))
         return {name: ms[i] for i, name in enumerate(PHASES)}, cnt.value
+
+    def diag_half_scalars(self, k_words):
+        """Diagnostic: the device's half-size scalar search for k given as
+        uint32 [n][8]; returns uint32 [n][12] (ok, d<0, c[5], |d|[5])."""
+        k = np.ascontiguousarray(k_words, dtype=np.uint32).reshape(-1, 8)
+        out = np.zeros((len(k), 12), dtype=np.uint32)
+        if len(k):
+            _check(_lib.fd_ed25519_hip_diag_half_scalars(self._h, k.ctypes.data_as(_u8p), len(k),
+                                                         out.ctypes.data_as(_u8p)))
+        return out
 
     def clock_mhz(self):
         return _lib.fd_ed25519_hip_device_clock_mhz(self._h)

@@ -273,6 +273,18 @@ fd_ed25519_hip_device_clock_mhz( fd_ed25519_hip_engine_t * engine );
 int
 fd_ed25519_hip_engine_sync( fd_ed25519_hip_engine_t * engine );
 
+/* Diagnostic: the verify kernels' half-size scalar search
+   (csrc/fd25519_half.h) run on the device for n scalars k (8 little-endian
+   32-bit words each, k < L), host buffers in and out.  out[12*i]: 1 if a
+   pair was found, out[12*i+1]: d < 0, out[12*i+2..6]: c, out[12*i+7..11]:
+   |d| (5 words each).  Synchronous.  For tests: the device search must
+   agree with the host build of the same header. */
+int
+fd_ed25519_hip_diag_half_scalars( fd_ed25519_hip_engine_t * engine,
+                                  unsigned int const *      k,
+                                  unsigned long             n,
+                                  unsigned int *            out );
+
 /* Human-readable form of an engine status code / of the last failure. */
 char const *
 fd_ed25519_hip_strerror( int status );
