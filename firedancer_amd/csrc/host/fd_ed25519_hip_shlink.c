@@ -1,0 +1,185 @@
+/* fd_ed25519_hip_shlink.c -- a tango-style link in POSIX shared memory,
+   so that the verify tile (inside its write/fsync-only sandbox,
+   src/app/fdctl/run/tiles/verify.seccomppolicy) and a GPU process outside
+   it exchange frags with memory operations only.
+
+   One shm object per direction holds the header, an mcache of
+   fd_frag_meta_t-shaped lines (src/tango/fd_tango_base.h:123-203: seq,
+   sig, chunk, sz, ctl, tsorig, tspub) and a dcache of 64-byte chunks.
+   Single producer, single consumer.  The producer invalidates a line
+   (seq - 1), writes the payload and the metadata, then publishes seq with
+   release order; the consumer reads seq with acquire order, copies, and
+   re-reads seq to detect an overrun.  Flow control is credit based: the
+   consumer publishes how many frags it has taken, and the producer never
+   runs more than depth frags ahead (the reference's fctl / fseq pair,
+   reduced to one counter).
+
+   No HIP: this file is also linked into the standalone sandboxed producer
+   (tools/shlink_producer.c). */
+#define _GNU_SOURCE
+#include "../../../include/fd_ed25519_hip_tile.h"
+
+#include <fcntl.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#define SHLINK_MAGIC 0xfd25519517a4c0deUL
+#define SHLINK_CHUNK 64UL
+
+typedef struct {
+  _Atomic uint64_t seq;
+  uint64_t         sig;
+  uint32_t         chunk;
+  uint16_t         sz;
+  uint16_t         ctl;
+  uint32_t         tsorig;
+  uint32_t         tspub;
+} shlink_meta_t;
+
+typedef struct {
+  uint64_t         magic;
+  uint64_t         depth;       /* mcache lines, power of 2 */
+  uint64_t         chunk_cnt;   /* dcache chunks */
+  uint64_t         mtu;
+  uint64_t         pad0[4];
+  _Atomic uint64_t consumed;    /* consumer -> producer credits (own line) */
+  uint64_t         pad1[7];
+} shlink_hdr_t;
+
+struct fd_ed25519_hip_shlink {
+  shlink_hdr_t *  hdr;
+  shlink_meta_t * mcache;
+  unsigned char * dcache;
+  size_t          map_sz;
+  char            name[ 128 ];
+  /* process-local cursor: the next seq to publish (producer) or take
+     (consumer), and the producer's next dcache chunk */
+  uint64_t        seq;
+  uint64_t        chunk;
+};
+
+static size_t
+shlink_footprint( uint64_t depth, uint64_t chunk_cnt ) {
+  return sizeof(shlink_hdr_t) + depth * sizeof(shlink_meta_t) + chunk_cnt * SHLINK_CHUNK;
+}
+
+static fd_ed25519_hip_shlink_t *
+shlink_map( char const * name, int fd, size_t sz ) {
+  void * m = mmap( NULL, sz, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0 );
+  close( fd );
+  if( m==MAP_FAILED ) return NULL;
+  fd_ed25519_hip_shlink_t * l = (fd_ed25519_hip_shlink_t *)calloc( 1, sizeof(*l) );
+  if( !l ) { munmap( m, sz ); return NULL; }
+  l->hdr    = (shlink_hdr_t *)m;
+  l->mcache = (shlink_meta_t *)( (unsigned char *)m + sizeof(shlink_hdr_t) );
+  l->map_sz = sz;
+  snprintf( l->name, sizeof(l->name), "%s", name );
+  return l;
+}
+
+fd_ed25519_hip_shlink_t *
+fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
+  if( !name || !depth || (depth & (depth-1UL)) || strlen( name )>=120 ) return NULL;
+  uint64_t mtu_chunks = (FD_ED25519_HIP_TXN_MTU + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
+  uint64_t chunk_cnt  = (depth + 2UL) * mtu_chunks;
+  size_t   sz         = shlink_footprint( depth, chunk_cnt );
+  int fd = shm_open( name, O_RDWR | O_CREAT | O_EXCL, 0600 );
+  if( fd<0 ) return NULL;
+  if( ftruncate( fd, (off_t)sz ) ) { close( fd ); shm_unlink( name ); return NULL; }
+  fd_ed25519_hip_shlink_t * l = shlink_map( name, fd, sz );
+  if( !l ) { shm_unlink( name ); return NULL; }
+  l->dcache = (unsigned char *)l->mcache + depth * sizeof(shlink_meta_t);
+  for( uint64_t k=0UL; k<depth; k++ ) {
+    atomic_store_explicit( &l->mcache[ k ].seq, k - depth, memory_order_relaxed );
+  }
+  l->hdr->depth     = depth;
+  l->hdr->chunk_cnt = chunk_cnt;
+  l->hdr->mtu       = FD_ED25519_HIP_TXN_MTU;
+  atomic_store_explicit( &l->hdr->consumed, 0UL, memory_order_relaxed );
+  atomic_thread_fence( memory_order_release );
+  l->hdr->magic = SHLINK_MAGIC;
+  return l;
+}
+
+fd_ed25519_hip_shlink_t *
+fd_ed25519_hip_shlink_join( char const * name ) {
+  if( !name ) return NULL;
+  int fd = shm_open( name, O_RDWR, 0600 );
+  if( fd<0 ) return NULL;
+  struct stat st;
+  if( fstat( fd, &st ) || (size_t)st.st_size<sizeof(shlink_hdr_t) ) { close( fd ); return NULL; }
+  fd_ed25519_hip_shlink_t * l = shlink_map( name, fd, (size_t)st.st_size );
+  if( !l ) return NULL;
+  if( l->hdr->magic!=SHLINK_MAGIC ||
+      shlink_footprint( l->hdr->depth, l->hdr->chunk_cnt )!=l->map_sz ) {
+    munmap( l->hdr, l->map_sz ); free( l ); return NULL;
+  }
+  l->dcache = (unsigned char *)l->mcache + l->hdr->depth * sizeof(shlink_meta_t);
+  return l;
+}
+
+void
+fd_ed25519_hip_shlink_leave( fd_ed25519_hip_shlink_t * l, int unlink ) {
+  if( !l ) return;
+  if( unlink ) shm_unlink( l->name );
+  munmap( l->hdr, l->map_sz );
+  free( l );
+}
+
+unsigned long
+fd_ed25519_hip_shlink_depth( fd_ed25519_hip_shlink_t const * l ) {
+  return l ? l->hdr->depth : 0UL;
+}
+
+int
+fd_ed25519_hip_shlink_publish( fd_ed25519_hip_shlink_t * l, unsigned char const * payload, unsigned long sz,
+                               unsigned long sig, unsigned int ctl ) {
+  shlink_hdr_t * h = l->hdr;
+  if( sz>h->mtu ) return FD_ED25519_HIP_ERR_INVAL;
+  uint64_t seq = l->seq;
+  if( seq - atomic_load_explicit( &h->consumed, memory_order_acquire )>=h->depth ) return 1;   /* no credit */
+  uint64_t mtu_chunks = (h->mtu + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
+  if( l->chunk + mtu_chunks>h->chunk_cnt ) l->chunk = 0UL;   /* compact wrap */
+  shlink_meta_t * m = &l->mcache[ seq & (h->depth-1UL) ];
+  atomic_store_explicit( &m->seq, seq-1UL, memory_order_relaxed );
+  atomic_thread_fence( memory_order_release );
+  if( sz ) memcpy( l->dcache + l->chunk*SHLINK_CHUNK, payload, sz );
+  m->sig    = sig;
+  m->chunk  = (uint32_t)l->chunk;
+  m->sz     = (uint16_t)sz;
+  m->ctl    = (uint16_t)ctl;
+  m->tsorig = 0U;
+  m->tspub  = 0U;
+  atomic_store_explicit( &m->seq, seq, memory_order_release );
+  l->chunk += (sz + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
+  l->seq    = seq + 1UL;
+  return 0;
+}
+
+int
+fd_ed25519_hip_shlink_consume( fd_ed25519_hip_shlink_t * l, unsigned char * payload, unsigned long * sz,
+                               unsigned long * sig, unsigned int * ctl ) {
+  shlink_hdr_t * h = l->hdr;
+  uint64_t seq = l->seq;
+  shlink_meta_t * m = &l->mcache[ seq & (h->depth-1UL) ];
+  uint64_t s0 = atomic_load_explicit( &m->seq, memory_order_acquire );
+  if( (int64_t)(s0 - seq)<0 ) return 1;                      /* not yet published */
+  if( s0!=seq ) return -1;                                    /* overrun */
+  unsigned long n = m->sz;
+  unsigned long sg = m->sig;
+  unsigned int  c  = m->ctl;
+  if( n>h->mtu ) return -1;
+  if( n ) memcpy( payload, l->dcache + (unsigned long)m->chunk*SHLINK_CHUNK, n );
+  atomic_thread_fence( memory_order_acquire );
+  if( atomic_load_explicit( &m->seq, memory_order_relaxed )!=s0 ) return -1;   /* overrun during the copy */
+  *sz = n; *sig = sg; *ctl = c;
+  l->seq = seq + 1UL;
+  atomic_store_explicit( &h->consumed, l->seq, memory_order_release );
+  return 0;
+}

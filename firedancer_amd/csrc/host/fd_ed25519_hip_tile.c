@@ -808,6 +808,72 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
 }
 
 /* ======================================================================
+   vservice: the GPU process behind a sandboxed verify tile (shlink in,
+   shlink out). */
+
+int
+fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+                             fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
+                             fd_ed25519_hip_vservice_stats_t * stats ) {
+  if( !in || !out ) return FD_ED25519_HIP_ERR_INVAL;
+  fd_ed25519_hip_vtile_t * vt = fd_ed25519_hip_vtile_new( device, slot_cnt, batch_sigs, 16UL, 64UL, flags );
+  if( !vt ) return FD_ED25519_HIP_ERR_INVAL;
+  enum { QMAX = 4096 };
+  unsigned long * ck  = (unsigned long *)malloc( QMAX*sizeof(unsigned long) );
+  signed char *   vd  = (signed char *)malloc( QMAX );
+  unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_TXN_MTU );
+  if( !ck || !vd || !buf ) {
+    free( ck ); free( vd ); free( buf ); fd_ed25519_hip_vtile_delete( vt );
+    return FD_ED25519_HIP_ERR_NOMEM;
+  }
+  double t0 = now_s();
+  unsigned long txns = 0UL, qn = 0UL, qi = 0UL;
+  int eos = 0, rc = FD_ED25519_HIP_OK;
+  for(;;) {
+    /* verdicts already collected go out first, as far as credits allow */
+    while( qi<qn ) {
+      unsigned char v = (unsigned char)vd[ qi ];
+      int r = fd_ed25519_hip_shlink_publish( out, &v, 1UL, ck[ qi ], 0U );
+      if( r==1 ) break;
+      if( r ) { rc = r; goto done; }
+      qi++;
+    }
+    if( qi==qn ) {
+      qi = qn = 0UL;
+      qn = fd_ed25519_hip_vtile_poll( vt, 0, QMAX, ck, vd, NULL );
+    }
+    if( eos && !qn && !fd_ed25519_hip_vtile_pending( vt ) ) break;
+    /* after_frag for every frag that is ready */
+    int pulled = 0;
+    while( !eos ) {
+      unsigned long sz = 0UL, sig = 0UL;
+      unsigned int ctl = 0U;
+      int r = fd_ed25519_hip_shlink_consume( in, buf, &sz, &sig, &ctl );
+      if( r==1 ) break;
+      if( r ) { rc = FD_ED25519_HIP_ERR_INVAL; goto done; }   /* overrun: cannot happen with credits */
+      if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { eos = 1; break; }
+      fd_ed25519_hip_vtile_frag( vt, buf, sz, sig );
+      txns++;
+      pulled = 1;
+    }
+    /* `in` drained: send the open batch if a slot can take it (all of it at the end) */
+    if( !pulled && vt->open && vt->open->txn_cnt &&
+        ( eos || slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<slot_cnt ) )
+      fd_ed25519_hip_vtile_flush( vt, eos );
+  }
+  while( fd_ed25519_hip_shlink_publish( out, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {}
+done:
+  if( stats ) {
+    stats->txn_cnt = txns;
+    stats->batches = vt->pipe->seq;
+    stats->seconds = now_s() - t0;
+  }
+  free( ck ); free( vd ); free( buf );
+  fd_ed25519_hip_vtile_delete( vt );
+  return rc;
+}
+
+/* ======================================================================
    pool: one feeder thread + pipe per device, batches dealt round-robin. */
 
 typedef struct {

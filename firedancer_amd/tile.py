@@ -201,3 +201,97 @@ def pool_verify(devices, msgs, msg_off, msg_sz, sigs, pubs, batch_sigs=65536, sl
                                            _ptr(_c(sigs, np.uint8).reshape(-1)), _ptr(_c(pubs, np.uint8).reshape(-1)),
                                            _ptr(out), ctypes.byref(sec)))
     return out[:n], sec.value
+
+
+# ---- shlink + verify service (the GPU process behind a sandboxed tile) ----
+
+SHLINK_CTL_EOS = 1
+PRODUCER_BIN = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)),
+                                          "_lib", "fd_shlink_producer")
+
+
+class VServiceStats(ctypes.Structure):
+    _fields_ = [("txn_cnt", ctypes.c_ulong), ("batches", ctypes.c_ulong), ("seconds", ctypes.c_double)]
+
+
+_lib.fd_ed25519_hip_shlink_create.argtypes = [ctypes.c_char_p, ctypes.c_ulong]
+_lib.fd_ed25519_hip_shlink_create.restype = _v
+_lib.fd_ed25519_hip_shlink_join.argtypes = [ctypes.c_char_p]
+_lib.fd_ed25519_hip_shlink_join.restype = _v
+_lib.fd_ed25519_hip_shlink_leave.argtypes = [_v, ctypes.c_int]
+_lib.fd_ed25519_hip_shlink_depth.argtypes = [_v]
+_lib.fd_ed25519_hip_shlink_depth.restype = ctypes.c_ulong
+_lib.fd_ed25519_hip_shlink_publish.argtypes = [_v, ctypes.c_char_p, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_uint]
+_lib.fd_ed25519_hip_shlink_publish.restype = ctypes.c_int
+_lib.fd_ed25519_hip_shlink_consume.argtypes = [_v, _v, ctypes.POINTER(ctypes.c_ulong), ctypes.POINTER(ctypes.c_ulong),
+                                               ctypes.POINTER(ctypes.c_uint)]
+_lib.fd_ed25519_hip_shlink_consume.restype = ctypes.c_int
+_lib.fd_ed25519_hip_vservice_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, ctypes.c_int, _v, _v,
+                                             ctypes.POINTER(VServiceStats)]
+
+
+class ShLink:
+    """fd_ed25519_hip_shlink: a tango-style mcache/dcache in POSIX shared
+    memory, one producer and one consumer process (one handle per side)."""
+
+    def __init__(self, name, depth=0, create=False):
+        self.name = name
+        h = (_lib.fd_ed25519_hip_shlink_create(name.encode(), int(depth)) if create
+             else _lib.fd_ed25519_hip_shlink_join(name.encode()))
+        if not h:
+            raise HipError(-1, f"shlink {'create' if create else 'join'} {name} failed")
+        self._h, self._owner = h, create
+        self._buf = ctypes.create_string_buffer(TXN_MTU)
+
+    @property
+    def depth(self):
+        return _lib.fd_ed25519_hip_shlink_depth(self._h)
+
+    def publish(self, payload, sig, ctl=0):
+        """True if published, False if no credit (retry)."""
+        r = _lib.fd_ed25519_hip_shlink_publish(self._h, bytes(payload), len(payload), int(sig), int(ctl))
+        if r < 0:
+            _check(r)
+        return r == 0
+
+    def consume(self):
+        """(payload, sig, ctl), or None if nothing is published yet."""
+        sz, sig, ctl = ctypes.c_ulong(), ctypes.c_ulong(), ctypes.c_uint()
+        r = _lib.fd_ed25519_hip_shlink_consume(self._h, self._buf, ctypes.byref(sz), ctypes.byref(sig),
+                                               ctypes.byref(ctl))
+        if r == 1:
+            return None
+        if r:
+            raise HipError(r, "shlink overrun")
+        return self._buf.raw[:sz.value], sig.value, ctl.value
+
+    def close(self, unlink=None):
+        if self._h:
+            _lib.fd_ed25519_hip_shlink_leave(self._h, int(self._owner if unlink is None else unlink))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def vservice_run(in_link, out_link, device=0, slot_cnt=3, batch_sigs=4096, gpu_parse=True, codes="avx512"):
+    """The GPU side of a sandboxed verify tile: serves in_link -> out_link
+    until the EOS frag (fd_ed25519_hip_vservice_run).  Returns its stats."""
+    from .ed25519 import FLAG_CODES_PORTABLE
+    flags = (VTILE_GPU_PARSE if gpu_parse else 0) | (FLAG_CODES_PORTABLE if codes == "portable" else 0)
+    st = VServiceStats()
+    _check(_lib.fd_ed25519_hip_vservice_run(int(device), int(slot_cnt), int(batch_sigs), flags, in_link._h,
+                                            out_link._h, ctypes.byref(st)))
+    return {f: getattr(st, f) for f, _ in VServiceStats._fields_}
+
+
+def write_payload_file(path, payloads):
+    """The producer tool's input: u64 n, n x u32 sizes, the payloads."""
+    with open(path, "wb") as f:
+        f.write(np.uint64(len(payloads)).tobytes())
+        f.write(np.array([len(p) for p in payloads], np.uint32).tobytes())
+        for p in payloads:
+            f.write(bytes(p))

@@ -22,7 +22,12 @@
              between a producer thread and the vtile, for the latency mode
      pool    one host feeder thread and pipe per GPU, batches dealt
              round-robin (the analogue of seq % verify_tile_count,
-             src/app/fdctl/run/tiles/fd_verify.c:36-47) */
+             src/app/fdctl/run/tiles/fd_verify.c:36-47)
+     shlink  the same mcache / dcache in POSIX shared memory, between
+             processes, and the GPU-side verify service behind it: the
+             verify tile keeps its write/fsync-only sandbox
+             (src/app/fdctl/run/tiles/verify.seccomppolicy) and talks to
+             the GPU process with memory operations only */
 
 #include "fd_ed25519_hip.h"
 
@@ -237,6 +242,68 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
                             unsigned int const * payload_sz, unsigned long txn_cnt, double offered_txn_per_s,
                             unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
                             fd_ed25519_hip_latency_result_t * res );
+
+/* ---- shlink + verify service (GPU process outside the sandbox) -------- */
+
+/* A single-producer single-consumer tango-style link in a POSIX shm object
+   `name` (e.g. "/fd_verify_in"): an mcache of depth (power of 2)
+   fd_frag_meta_t-shaped lines and a dcache of 64-byte chunks for payloads
+   of up to FD_ED25519_HIP_TXN_MTU bytes, with credit-based flow control.
+   create makes the object (it must not exist), join maps an existing one;
+   each process keeps its own cursor, so one handle per side.  After the
+   mapping, publish / consume are memory operations only (they may run
+   under seccomp strict mode). */
+typedef struct fd_ed25519_hip_shlink fd_ed25519_hip_shlink_t;
+
+fd_ed25519_hip_shlink_t *
+fd_ed25519_hip_shlink_create( char const * name, unsigned long depth );
+
+fd_ed25519_hip_shlink_t *
+fd_ed25519_hip_shlink_join( char const * name );
+
+/* Unmaps (and with unlink != 0 removes the name). */
+void
+fd_ed25519_hip_shlink_leave( fd_ed25519_hip_shlink_t * link, int unlink );
+
+unsigned long
+fd_ed25519_hip_shlink_depth( fd_ed25519_hip_shlink_t const * link );
+
+/* Producer: publishes one frag (payload of sz bytes, sig, ctl).  Returns
+   0, 1 if the consumer has not returned a credit yet (retry), or an
+   error status. */
+int
+fd_ed25519_hip_shlink_publish( fd_ed25519_hip_shlink_t * link, unsigned char const * payload, unsigned long sz,
+                               unsigned long sig, unsigned int ctl );
+
+/* Consumer: takes the next frag into payload (FD_ED25519_HIP_TXN_MTU
+   bytes of room).  Returns 0, 1 if none is published yet, -1 if the
+   producer overran the consumer. */
+int
+fd_ed25519_hip_shlink_consume( fd_ed25519_hip_shlink_t * link, unsigned char * payload, unsigned long * sz,
+                               unsigned long * sig, unsigned int * ctl );
+
+/* ctl bit of the last frag of a stream, both directions */
+#define FD_ED25519_HIP_SHLINK_CTL_EOS (1U)
+
+typedef struct {
+  unsigned long txn_cnt;
+  unsigned long batches;
+  double        seconds;
+} fd_ed25519_hip_vservice_stats_t;
+
+/* The GPU side of a sandboxed verify tile: consumes transaction payload
+   frags from `in` (sig = the tile's cookie), runs them through a vtile
+   (slot_cnt, batch_sigs, flags as for fd_ed25519_hip_vtile_new) and
+   publishes one frag per transaction to `out` in frag order: sig = cookie,
+   a 1-byte payload with the verdict (FD_ED25519_HIP_TXN_VERIFY_* /
+   FD_ED25519_HIP_TXN_PARSE_FAILED).  A frag with ctl EOS ends the stream:
+   the service answers everything before it, publishes an EOS frag and
+   returns.  A batch is submitted when full, or when `in` is drained and a
+   slot is free. */
+int
+fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+                             fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
+                             fd_ed25519_hip_vservice_stats_t * stats );
 
 /* ---- pool ------------------------------------------------------------- */
 

@@ -154,3 +154,46 @@ def test_device_parse_on_mutated_fixtures(tile, ref):
     parsed = np.array([ref_parse(ref, p)[0] is not None for p in corpus])
     assert np.array_equal(got != tile.TXN_PARSE_FAILED, parsed)
     assert 500 < parsed.sum() < len(corpus) - 500
+
+
+@pytest.mark.parametrize("gpu_parse", [False, True])
+def test_sandboxed_tile_with_gpu_service(tile, ref, frags, tmp_path, gpu_parse):
+    """the verify tile in seccomp strict mode (the
+    standalone producer: memory operations, write and _exit only) and the
+    GPU in a separate service process, connected by two shared-memory
+    links.  The verdict stream equals the reference tile's."""
+    import subprocess
+    import sys
+    import uuid
+    frags = [p for p in frags if len(p) <= tile.TXN_MTU]
+    want, _ = ref_vtile(ref, frags)
+    path = str(tmp_path / "payloads.bin")
+    tile.write_payload_file(path, frags)
+    tag = uuid.uuid4().hex[:12]
+    txl = tile.ShLink(f"/fdg_tx_{tag}", 256, create=True)
+    vdl = tile.ShLink(f"/fdg_vd_{tag}", 256, create=True)
+    repo = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); from firedancer_amd import tile; "
+            "a = tile.ShLink(%r); b = tile.ShLink(%r); "
+            "print(tile.vservice_run(a, b, batch_sigs=256, slot_cnt=3, gpu_parse=%r))"
+            % (repo, txl.name, vdl.name, gpu_parse))
+    svc = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    prod = subprocess.Popen([tile.PRODUCER_BIN, txl.name, vdl.name, path], stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE)
+    try:
+        out, perr = prod.communicate(timeout=90)
+        sout, serr = svc.communicate(timeout=30)
+    finally:
+        for p in (prod, svc):
+            if p.poll() is None:
+                p.kill()
+        txl.close()
+        vdl.close()
+    if prod.returncode == 3:
+        pytest.skip(f"seccomp strict mode unavailable: {perr.decode()}")
+    assert svc.returncode == 0, serr.decode()
+    assert prod.returncode == 0, perr.decode()
+    got = np.frombuffer(out, np.int8)
+    bad = np.nonzero(got != want)[0]
+    assert len(got) == len(want) and len(bad) == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:10]]
+    assert b"'txn_cnt': %d" % len(frags) in sout

@@ -1,0 +1,97 @@
+/* shlink_producer -- the verify tile's side of the sandboxed integration,
+   standalone: maps two shared-memory links (txn frags out, verdict frags
+   in), then enters seccomp strict mode (only read, write, _exit and
+   sigreturn remain -- stricter than the verify tile's write/fsync policy,
+   src/app/fdctl/run/tiles/verify.seccomppolicy) and runs the whole stream
+   with memory operations only.  Any other system call would kill it.
+
+     shlink_producer IN_LINK OUT_LINK PAYLOAD_FILE [--no-sandbox]
+
+   PAYLOAD_FILE: u64 n, n x u32 sizes, the payloads back to back.  Frag i
+   carries sig = i; after the last one an EOS frag.  Verdict frags are
+   consumed whenever a publish finds no credit, and after the EOS until
+   the service's EOS.  Output on stdout: n verdict bytes in frag order
+   (checked against the sig of every verdict frag), via write(2); exit
+   status 0, or 2 on a protocol error, 3 if strict mode is unavailable. */
+#define _GNU_SOURCE
+#include "../include/fd_ed25519_hip_tile.h"
+
+#include <linux/seccomp.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/prctl.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+static void
+leave( int status ) {   /* exit(2) itself: exit_group is not allowed in strict mode */
+  syscall( SYS_exit, status );
+  for(;;) {}
+}
+
+static int
+take_verdicts( fd_ed25519_hip_shlink_t * in, unsigned char * buf, signed char * verdict, unsigned long n,
+               unsigned long * next, int * eos ) {
+  for(;;) {
+    unsigned long sz = 0UL, sig = 0UL;
+    unsigned int ctl = 0U;
+    int r = fd_ed25519_hip_shlink_consume( in, buf, &sz, &sig, &ctl );
+    if( r==1 ) return 0;
+    if( r ) return -1;
+    if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { *eos = 1; return 0; }
+    if( sz!=1UL || sig!=*next || *next>=n ) return -1;
+    verdict[ (*next)++ ] = (signed char)buf[ 0 ];
+  }
+}
+
+int
+main( int argc, char ** argv ) {
+  if( argc<4 ) { fprintf( stderr, "usage: %s IN_LINK OUT_LINK PAYLOAD_FILE [--no-sandbox]\n", argv[0] ); return 1; }
+  int sandbox = !(argc>4 && !strcmp( argv[4], "--no-sandbox" ));
+  FILE * f = fopen( argv[3], "rb" );
+  if( !f ) { perror( "payload file" ); return 1; }
+  unsigned long n = 0UL;
+  if( fread( &n, 8, 1, f )!=1 ) return 1;
+  unsigned int * sz = (unsigned int *)malloc( 4UL*(n+1UL) );
+  unsigned long * off = (unsigned long *)malloc( 8UL*(n+1UL) );
+  if( !sz || !off || fread( sz, 4, n, f )!=n ) return 1;
+  unsigned long total = 0UL;
+  for( unsigned long i=0UL; i<n; i++ ) { off[ i ] = total; total += sz[ i ]; }
+  unsigned char * pay = (unsigned char *)malloc( total + 1UL );
+  if( !pay || fread( pay, 1, total, f )!=total ) return 1;
+  fclose( f );
+  signed char * verdict = (signed char *)malloc( n + 1UL );
+  unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_TXN_MTU );
+  fd_ed25519_hip_shlink_t * txl = fd_ed25519_hip_shlink_join( argv[1] );
+  fd_ed25519_hip_shlink_t * vdl = fd_ed25519_hip_shlink_join( argv[2] );
+  if( !verdict || !buf || !txl || !vdl ) { fprintf( stderr, "cannot join the links\n" ); return 1; }
+  fflush( stdout ); fflush( stderr );
+
+  if( sandbox && prctl( PR_SET_SECCOMP, SECCOMP_MODE_STRICT ) ) { perror( "seccomp strict" ); return 3; }
+
+  /* from here on: memory operations, write(2) and _exit(2) only */
+  unsigned long i = 0UL, got = 0UL;
+  int eos = 0;
+  while( i<n ) {
+    int r = fd_ed25519_hip_shlink_publish( txl, pay + off[ i ], sz[ i ], i, 0U );
+    if( r==0 ) { i++; continue; }
+    if( r!=1 ) leave( 2 );
+    if( take_verdicts( vdl, buf, verdict, n, &got, &eos ) || eos ) leave( 2 );
+  }
+  while( fd_ed25519_hip_shlink_publish( txl, NULL, 0UL, n, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
+    if( take_verdicts( vdl, buf, verdict, n, &got, &eos ) || eos ) leave( 2 );
+  }
+  while( !eos ) {
+    if( take_verdicts( vdl, buf, verdict, n, &got, &eos ) ) leave( 2 );
+  }
+  if( got!=n ) leave( 2 );
+  unsigned long w = 0UL;
+  while( w<n ) {
+    long k = write( 1, verdict + w, n - w );
+    if( k<=0 ) leave( 2 );
+    w += (unsigned long)k;
+  }
+  leave( 0 );
+  return 0;
+}
