@@ -177,11 +177,15 @@ def latency_mode(eng, args, device):
 
 def pmc_traffic(n):
     """HBM bytes per dsm launch from the committed PMC summary (rocprofv3
-    FETCH_SIZE + WRITE_SIZE passes, tools/pmc_summary.py), scaled to n."""
+    FETCH_SIZE + WRITE_SIZE passes, tools/pmc_summary.py), scaled to n.
+    The dsm kernel's loads are 16 B per lane (global_load_dwordx4), for
+    which gfx950's FETCH_SIZE reports half the bytes
+    (MI355X_MICROARCH.md, HBM): reads are doubled; WRITE_SIZE is exact for
+    16-B stores."""
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
     try:
         d = json.load(open(path))["fd_ed25519_dsm_kernel"]
-        per_sig = d["hbm_read_bytes_per_signature"] + d["hbm_write_bytes_per_signature"]
+        per_sig = 2.0 * d["hbm_read_bytes_per_signature"] + d["hbm_write_bytes_per_signature"]
         return per_sig * n, os.path.relpath(path, REPO)
     except (OSError, KeyError, ValueError):
         return None, None
@@ -316,7 +320,8 @@ def main():
             "roofline": {"bound": "valu-int32", "kernel": "fd_ed25519_dsm_kernel",
                          "achieved": achieved, "peak": peak, "unit": "TOPS",
                          "frac": (achieved / peak) if achieved else None, "traffic": traffic,
-                         "traffic_unit": "bytes per launch (HBM read+write, rocprofv3 FETCH_SIZE+WRITE_SIZE)",
+                         "traffic_unit": "bytes per launch (HBM read+write: rocprofv3 2 x FETCH_SIZE (gfx950 16-B/lane "
+                                         "correction) + WRITE_SIZE)",
                          "traffic_source": traffic_src,
                          "ops_per_launch": dsm_ops, "launch_ms": per_launch["dsm"],
                          "executed": {"achieved": executed, "frac": (executed / peak) if executed else None,
