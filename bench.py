@@ -213,6 +213,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1048576)
     ap.add_argument("--cpu-reps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--half", default="extended", choices=["extended", "strict"],
+                    help="half-size scalar bound (A/B only; same verdicts)")
     ap.add_argument("--latency-batch", type=int, default=256)
     ap.add_argument("--latency-slots", type=int, default=4)
     ap.add_argument("--latency-txns", type=int, default=100000, help="0 disables the latency mode")
@@ -227,7 +229,7 @@ def main():
     if strong:  # cfg n is the whole stream: this rank verifies its contiguous share
         n = (n + world - 1) // world
     ndev = max(ed25519.device_count(), 1)
-    eng = ed25519.Engine(device=local % ndev, max_chunk=min(n, 1 << 20))
+    eng = ed25519.Engine(device=local % ndev, max_chunk=min(n, 1 << 20), half=args.half)
     info = eng.info()
     log(f"[rank {rank}] engine {info}")
 

@@ -25,8 +25,12 @@
    (t_i even: t_{i-1} is odd, consecutive t being coprime) the vector
    (r_{i-1} - m r_i, t_{i-1} - m t_i) with the least m that brings the
    first coordinate below 2^131 (every t of that family is odd, and the
-   least m gives the smallest |t|).  When even that is too long (~0.15% of
-   random k) the caller falls back to the full-length multiplication.
+   least m gives the smallest |t|).  That |d| may exceed 2^131 (~0.16% of
+   random k: the lattice is unbalanced, its short vector has an even d);
+   the caller states how long a d it accepts (dbits: 131 for the strict
+   half-size form, up to FD_HALF_DBITS_MAX for the extended one, whose
+   multiplication simply runs a few more windows) and falls back to the
+   full-length multiplication beyond that (~1e-6 of random k at 151 bits).
 
    The Euclidean steps run Lehmer-style (Knuth, TAOCP 4.5.2, Algorithm L):
    quotients are found from 52 leading bits, every value an exact integer
@@ -48,7 +52,8 @@
 #define FD_HALF_FN static inline
 #endif
 
-#define FD_HALF_BITS 131   /* 0 <= c < 2^FD_HALF_BITS, |d| < 2^FD_HALF_BITS */
+#define FD_HALF_BITS 131   /* 0 <= c < 2^FD_HALF_BITS, |d| < 2^dbits, dbits >= FD_HALF_BITS */
+#define FD_HALF_DBITS_MAX 151  /* longest |d| the dsm kernel takes (38 windows of 4 bits) */
 #define FD_HALF_TW   5     /* t values: 160-bit two's complement */
 #ifndef FD_HALF_LEHMER_MARGIN
 #define FD_HALF_LEHMER_MARGIN 0  /* Lehmer rounds stop this many bits above 2^FD_HALF_BITS (0: measured fastest, same fallback rate) */
@@ -215,11 +220,12 @@ FD_HALF_FN int fd_half_abs(uint32_t (&mag)[FD_HALF_TW], const uint32_t (&x)[FD_H
   return neg;
 }
 
-/* Finds c, d with c == d k (mod 8L), d odd, 0 <= c < 2^131, |d| < 2^131,
-   for 0 <= k < L.  Returns 1 and c (5 words), |d| (5 words), d's sign;
-   0 if no such pair was found within the bounds / iteration caps. */
+/* Finds c, d with c == d k (mod 8L), d odd, 0 <= c < 2^131, |d| < 2^dbits
+   (FD_HALF_BITS <= dbits <= FD_HALF_DBITS_MAX), for 0 <= k < L.  Returns 1
+   and c (5 words), |d| (5 words), d's sign; 0 if no such pair was found
+   within the bounds / iteration caps. */
 FD_HALF_FN int fd_half_scalars(const uint32_t (&k)[8], uint32_t (&c)[FD_HALF_TW], uint32_t (&dmag)[FD_HALF_TW],
-                               int* dneg) {
+                               int* dneg, int dbits) {
   uint32_t a[8] = FD_HALF_N8L, b[8];
   uint32_t ta[FD_HALF_TW] = {0u, 0u, 0u, 0u, 0u}, tb[FD_HALF_TW] = {1u, 0u, 0u, 0u, 0u};
 #pragma unroll
@@ -302,6 +308,14 @@ FD_HALF_FN int fd_half_scalars(const uint32_t (&k)[8], uint32_t (&c)[FD_HALF_TW]
       m += q;
     }
     if (big) m += 1;
+    /* |t_{i-1} - m t_i| = |t_{i-1}| + m |t_i| must not wrap the 160-bit t
+       (|t_{i-1}| <= |t_i| < 2^125): require m |t_i| < 2^155 */
+    {
+      uint32_t tm[FD_HALF_TW];
+      fd_half_abs(tm, tb);
+      const int mb = m ? 64 - __builtin_clzll(m) : 0;
+      if (mb + fd_half_bitlen<FD_HALF_TW>(tm) > 155) ok = 0;
+    }
     fd_half_lin<8>(cw, a, b, 1, -(int64_t)m);
     fd_half_lin<FD_HALF_TW>(dw, ta, tb, 1, -(int64_t)m);
   }
@@ -311,7 +325,7 @@ FD_HALF_FN int fd_half_scalars(const uint32_t (&k)[8], uint32_t (&c)[FD_HALF_TW]
   uint32_t chi = 0u;
 #pragma unroll
   for (int i = FD_HALF_TW; i < 8; i++) chi |= cw[i];
-  if (chi || fd_half_bitlen<FD_HALF_TW>(c) > FD_HALF_BITS || fd_half_bitlen<FD_HALF_TW>(dmag) > FD_HALF_BITS ||
+  if (chi || fd_half_bitlen<FD_HALF_TW>(c) > FD_HALF_BITS || fd_half_bitlen<FD_HALF_TW>(dmag) > dbits ||
       !(dw[0] & 1u))
     ok = 0;
   return ok;

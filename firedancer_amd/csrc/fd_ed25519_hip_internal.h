@@ -96,6 +96,7 @@ typedef struct {
   int32_t const *  btab20b;  /* [0..2^20)[2^132]B,   same layout                     */
   void *           atab;     /* device scratch, waves * ATAB_BYTES_PER_WAVE    */
   int              codes_portable; /* 0: AVX-512 backend codes, 1: portable  */
+  int              half_dbits;     /* longest |d| of the half-size form (fd25519_half.h) */
 } fd_ed25519_verify_params_t;
 
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a
@@ -128,7 +129,7 @@ int fd_ed25519_hip_launch_txn_combine( int8_t const * d_sig_codes, uint32_t cons
 
 /* diagnostic: fd_half_scalars on the device, 12 words out per k (see
    fd_ed25519_hip_diag_half_scalars) */
-int fd_ed25519_hip_launch_diag_half( uint32_t const * d_k, uint32_t * d_out, uint64_t n, void * stream );
+int fd_ed25519_hip_launch_diag_half( uint32_t const * d_k, uint32_t * d_out, uint64_t n, int dbits, void * stream );
 
 /* ---- raw transactions (fd_ed25519_txn.hip) ---- */
 

@@ -231,12 +231,13 @@ FD_DEV void btab_add(ge_p1p1& Rt, const ge_p3& P, ge_precomp& b, int f) {
    scalar: the half-size scalars (fd25519_half.h) of every signature, one
    lane per signature, before the points are decoded:
 
-       c == d k (mod 8L), d odd, 0 <= c, |d| < 2^131,
+       c == d k (mod 8L), d odd, 0 <= c < 2^131, |d| < 2^half_dbits,
        s' = d S mod L = s_lo + 2^132 s_hi
 
    written to hs[19][cap] (c, |d|, s_lo: 5 words each, s_hi: 4) with d's
-   sign in hflag.  Signatures whose k has no such pair (~0.13% of random k)
-   are flagged and queued on fix_list for the full-length form. */
+   sign in hflag.  Signatures whose k has no such pair (~1e-6 of random k
+   at 151 bits, ~0.16% at 131) are flagged and queued on fix_list for the
+   full-length form. */
 
 __global__ void __launch_bounds__(256, FD_ED25519_SCALAR_WAVES_PER_SIMD)
 fd_ed25519_scalar_kernel(fd_ed25519_verify_params_t p) {
@@ -253,7 +254,7 @@ fd_ed25519_scalar_kernel(fd_ed25519_verify_params_t p) {
   }
   uint32_t cw[FD_HALF_TW], dm[FD_HALF_TW];
   int dneg = 0;
-  int ok = fd_half_scalars(k, cw, dm, &dneg);
+  int ok = fd_half_scalars(k, cw, dm, &dneg, p.half_dbits);
   if (!p.sflag[j]) ok = 1;   /* S >= L: decided without the equation, any scalars do */
 
   /* s' = d S mod L */
@@ -318,6 +319,13 @@ FD_DEV void shl160(uint32_t (&out)[5], const uint32_t (&x)[5]) {
   }
 }
 
+/* x << s for 0 < s < 32 (wave-uniform s), the value staying below 2^160 */
+FD_DEV void shl160v(uint32_t (&out)[5], const uint32_t (&x)[5], int s) {
+#pragma unroll
+  for (int i = 4; i > 0; i--) out[i] = __builtin_amdgcn_alignbit(x[i], x[i - 1], 32 - s);
+  out[0] = x[0] << s;
+}
+
 /* signed recoding of a 160-bit value in radix 2^BITS, digits packed as
    BITS-bit two's complement (the carry out of the top digit is dropped:
    the caller reads the top digit unsigned where it may reach 2^(BITS-1)) */
@@ -371,9 +379,12 @@ FD_DEV void load_hs(uint32_t (&x)[5], const fd_ed25519_verify_params_t& p, int r
        [c](-A) + [|d|](-sign(d) R) + [s_lo]B + [s_hi]B' == 0,   B' = [2^132]B
 
    exactly equivalent (fd25519_half.h: the group has order 8L and [d] is
-   invertible on it).  A four-scalar Straus loop over 33 signed 4-bit
-   windows: 128 doublings (against 252 for the reference's double-scalar
-   form), 33 additions from each lane's [0..8](-A) and [0..8](-+R) tables
+   invertible on it).  A four-scalar Straus loop over W signed 4-bit
+   windows, W = 33 unless a lane of the wave has |d| >= 2^131 (~0.16% of
+   signatures; then up to 38, the same W for the whole wave, the other
+   lanes' top digits being 0): 4(W-1) = 128 doublings (against 252 for the
+   reference's double-scalar form), W additions from each lane's
+   [0..8](-A) and [0..8](-+R) tables
    (HBM, lane-contiguous 160-byte entries) and 7 + 7 mixed additions from
    the two unsigned radix-2^20 base tables [0..2^20)B and [0..2^20)B'
    (128 MB each, HBM/MALL).  Every table entry is loaded
@@ -394,13 +405,20 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     table_build(tabR, x, y, !(hf & FD_HF_DNEG));
   }
   /* digits, most significant first, top-aligned in 160 bits: c, |d| in
-     radix 16 (33 signed digits, the top one in [0,8]), s_lo, s_hi in
+     radix 16 (W signed digits, the top one in [0,8]), s_lo, s_hi in
      radix 2^20 (7 unsigned digits: no recoding, no negation) */
   uint32_t cd[5], dd[5], ld[5], hd[5];
+  int W = 33;
   {
     uint32_t x[5], t[5];
-    load_hs(x, p, 0, 5, j);  shl160<28>(t, x); recode160<4>(cd, t);
-    load_hs(x, p, 5, 5, j);  shl160<28>(t, x); recode160<4>(dd, t);
+    load_hs(x, p, 5, 5, j);
+    /* windows this lane needs: |d| < 2^(4W-1); the wave takes the max */
+    const int wl = (fd_half_bitlen<5>(x) + 4) >> 2;
+#pragma unroll
+    for (int w = 34; w <= (FD_HALF_DBITS_MAX + 4) / 4; w++) W += __ballot(wl >= w) != 0ull;
+    const int sh = 160 - 4 * W;
+    shl160v(t, x, sh); recode160<4>(dd, t);
+    load_hs(x, p, 0, 5, j);  shl160v(t, x, sh); recode160<4>(cd, t);
     load_hs(x, p, 10, 5, j); shl160<20>(ld, x);
     load_hs(x, p, 15, 4, j); shl160<20>(hd, x);
   }
@@ -412,15 +430,15 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
   ge_p1p1 Rt;
   ge_p2 Q;
 #pragma clang loop unroll(disable)
-  for (int it = 32; it >= 0; it--) {
+  for (int it = W - 1; it >= 0; it--) {
     int ea = pop160<4>(cd), er = pop160<4>(dd);
-    if (it == 32) { ea &= 15; er &= 15; }   /* top digits in [0,8] */
+    if (it == W - 1) { ea &= 15; er &= 15; }   /* top digits in [0,8] */
     ge_cached ca, cr;
-    const bool badd = it % 5 == 0;           /* base digits at bits 20m: windows 30, 25, .., 0 */
+    const bool badd = it <= 30 && it % 5 == 0;   /* base digits at bits 20m: windows 30, 25, .., 0 */
     uint32_t f = 0, g = 0;
     ge_precomp b1, b2;
     atab_load(ca, tabA, ea < 0 ? -ea : ea);
-    if (it != 32) {
+    if (it != W - 1) {
 #pragma clang loop unroll(disable)
       for (int dbl = 0; dbl < 4; dbl++) {
         ge_p2_dbl(Rt, Q);
@@ -520,10 +538,12 @@ FD_DEV int dsm_full_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
   return eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
-/* Persistent over fix_cnt + n items, handed out 64 at a time (one atomic
-   per wave): the full-length items first, then the chunk's signatures
-   (those queued as full-length skipped), so the ~2x longer full-length
-   work is spread over the grid instead of forming a tail. */
+/* Persistent over fix_cnt (rounded up to whole waves) + n items, handed
+   out 64 at a time (one atomic per wave): the full-length items first, in
+   waves of their own (a wave mixing both forms would run both), then the
+   chunk's signatures (those queued as full-length skipped), so the ~2x
+   longer full-length work is spread over the grid instead of forming a
+   tail. */
 __global__ void __launch_bounds__(FD_ED25519_VERIFY_BLOCK, FD_ED25519_DSM_WAVES_PER_SIMD)
 fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -532,7 +552,8 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
                lane * 180;
   int4* tabR = tabA + 90;
   const uint64_t nfix = *p.fix_cnt;
-  const uint64_t total = nfix + p.n;
+  const uint64_t nfix64 = (nfix + 63u) & ~(uint64_t)63u;
+  const uint64_t total = nfix64 + p.n;
   for (;;) {
     uint32_t b = 0u;
     if (lane == 0u) b = atomicAdd(p.work_ctr, 64u);
@@ -542,8 +563,8 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
     if (t < nfix) {
       const uint64_t j = p.fix_list[t];
       p.out[p.base + j] = (int8_t)dsm_full_one(p, j, tabA);
-    } else if (t < total) {
-      const uint64_t j = t - nfix;
+    } else if (t >= nfix64 && t < total) {
+      const uint64_t j = t - nfix64;
       if (!(p.hflag[j] & FD_HF_FULL)) p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
     }
   }
@@ -716,23 +737,25 @@ extern "C" int fd_ed25519_hip_launch_gen_btab16(int32_t* d_btab16, int base_dbl,
   return (int)hipGetLastError();
 }
 
-__global__ void __launch_bounds__(256) fd_ed25519_diag_half_kernel(const uint32_t* kin, uint32_t* out, uint64_t n) {
+__global__ void __launch_bounds__(256) fd_ed25519_diag_half_kernel(const uint32_t* kin, uint32_t* out, uint64_t n,
+                                                                   int dbits) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k[8], c[FD_HALF_TW], d[FD_HALF_TW];
   for (int w = 0; w < 8; w++) k[w] = kin[8 * i + w];
   int neg = 0;
-  const int ok = fd_half_scalars(k, c, d, &neg);
+  const int ok = fd_half_scalars(k, c, d, &neg, dbits);
   uint32_t* o = out + 12 * i;
   o[0] = (uint32_t)ok;
   o[1] = (uint32_t)neg;
   for (int w = 0; w < FD_HALF_TW; w++) { o[2 + w] = c[w]; o[7 + w] = d[w]; }
 }
 
-extern "C" int fd_ed25519_hip_launch_diag_half(const uint32_t* d_k, uint32_t* d_out, uint64_t n, void* stream) {
+extern "C" int fd_ed25519_hip_launch_diag_half(const uint32_t* d_k, uint32_t* d_out, uint64_t n, int dbits,
+                                               void* stream) {
   if (!n) return 0;
   hipLaunchKernelGGL(fd_ed25519_diag_half_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     d_k, d_out, n);
+                     d_k, d_out, n, dbits);
   return (int)hipGetLastError();
 }
 
@@ -774,7 +797,9 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
                        *p);
     break;
   case FD_ED25519_PHASE_DSM: {
-    const uint64_t need = (p->n + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
+    /* one wave more than the chunk needs: the full-length items (counted on
+       the device) run in waves of their own, in parallel with the rest */
+    const uint64_t need = (p->n + 64 + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
     const uint32_t g = (uint32_t)(need < grid ? need : grid);
     hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
   } break;

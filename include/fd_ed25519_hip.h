@@ -84,6 +84,11 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
 #define FD_ED25519_HIP_ERR_HIP     (-1000) /* HIP runtime error: -1000 - hipError_t    */
 
 #define FD_ED25519_HIP_FLAG_CODES_PORTABLE (1)  /* portable-backend error codes */
+/* Half-size scalars with |d| < 2^131 only (the strict form): signatures
+   whose k has no such pair take the full-length multiplication.  Default:
+   |d| up to 2^151 with a few more windows, the full-length form only for
+   ~1e-6 of random k.  Same verdicts either way; for tests and A/B. */
+#define FD_ED25519_HIP_FLAG_HALF_STRICT    (2)
 
 /* Creates an engine on HIP device `device`.  max_chunk is the number of
    signatures processed per kernel sequence (0 = default 1<<20); larger

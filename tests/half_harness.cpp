@@ -1,10 +1,10 @@
 // CPU harness (tests only): the product's half-size scalar search
 // (firedancer_amd/csrc/fd25519_half.h) compiled for the host.
 #include "fd25519_half.h"
-extern "C" int half_scalars(const uint32_t* k, uint32_t* c, uint32_t* dmag, int* dneg) {
+extern "C" int half_scalars(const uint32_t* k, uint32_t* c, uint32_t* dmag, int* dneg, int dbits) {
   uint32_t kk[8], cc[FD_HALF_TW], dd[FD_HALF_TW];
   for (int i = 0; i < 8; i++) kk[i] = k[i];
-  int ok = fd_half_scalars(kk, cc, dd, dneg);
+  int ok = fd_half_scalars(kk, cc, dd, dneg, dbits);
   for (int i = 0; i < FD_HALF_TW; i++) c[i] = cc[i];
   for (int i = 0; i < FD_HALF_TW; i++) dmag[i] = dd[i];
   return ok;

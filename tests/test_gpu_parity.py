@@ -183,18 +183,43 @@ def test_strerror(fd):
     assert fd.strerror(0) == "success" and fd.strerror(-3) == "bad message" and fd.strerror(5) == "unknown"
 
 
+@pytest.fixture(scope="module")
+def eng_strict(fd):
+    e = fd.Engine(0, max_chunk=1 << 14, half="strict")
+    yield e
+    e.close()
+
+
 def test_halfsize_fallback(eng, halfsize):
-    """k with no half-size pair: the dsm kernel's full-length items."""
+    """k with no strict half-size pair (|d| >= 2^131): by default the
+    extended-window form (W > 33 for the waves holding them)."""
     _check(_run(eng, halfsize), halfsize["codes_avx512"], halfsize["tags"])
+
+
+def test_halfsize_fallback_strict(eng_strict, halfsize):
+    """The same signatures under FLAG_HALF_STRICT: the dsm kernel's
+    full-length items (waves of their own)."""
+    _check(_run(eng_strict, halfsize), halfsize["codes_avx512"], halfsize["tags"])
 
 
 def test_halfsize_fallback_portable(eng_portable, halfsize):
     _check(_run(eng_portable, halfsize), halfsize["codes_portable"], halfsize["tags"])
 
 
-def test_halfsize_fallback_scattered(eng, halfsize, adversarial):
-    """The full-length items scattered through a larger chunk (they are
-    handed out first by the dsm work counter, the rest after them)."""
+def test_halfsize_fallback_portable_strict(fd, halfsize):
+    e = fd.Engine(0, max_chunk=1 << 12, codes="portable", half="strict")
+    try:
+        _check(_run(e, halfsize), halfsize["codes_portable"], halfsize["tags"])
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("mode", ["extended", "strict"])
+def test_halfsize_fallback_scattered(fd, eng, eng_strict, halfsize, adversarial, mode):
+    """Those signatures scattered through a larger chunk: extended-window
+    lanes mixed into ordinary waves, or (strict) full-length items handed
+    out first by the dsm work counter, the rest after them."""
+    e = eng if mode == "extended" else eng_strict
     rng = np.random.default_rng(11)
     reps = 24
     parts = [halfsize] * reps + [adversarial] * 4
@@ -209,7 +234,7 @@ def test_halfsize_fallback_scattered(eng, halfsize, adversarial):
     msgs = np.concatenate(msgs)
     off, sz = np.concatenate(off)[order], np.concatenate(sz)[order]
     sigs, pubs, want = np.concatenate(sigs)[order], np.concatenate(pubs)[order], np.concatenate(want)[order]
-    got = eng.verify_host(msgs, off, sz, sigs, pubs)
+    got = e.verify_host(msgs, off, sz, sigs, pubs)
     _check(got, want)
 
 
