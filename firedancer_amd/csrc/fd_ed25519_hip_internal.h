@@ -38,6 +38,7 @@ extern "C" {
 #define FD_ED25519_ATAB_BYTES_PER_WAVE (2UL * 9UL * 10UL * 64UL * 16UL)  /* -A and -+R tables */
 
 #define FD_ED25519_VERIFY_BLOCK 256
+#define FD_ED25519_QUAD_LANE_BYTES 864UL   /* dsm4 lane tables: 2 x 9 entries x 48 B */
 /* Occupancy targets (waves per SIMD) of the phase kernels; each caps the
    kernel's register allocation (512 / waves VGPRs). */
 #ifndef FD_ED25519_DSM_WAVES_PER_SIMD
@@ -97,6 +98,8 @@ typedef struct {
   void *           atab;     /* device scratch, waves * ATAB_BYTES_PER_WAVE    */
   int              codes_portable; /* 0: AVX-512 backend codes, 1: portable  */
   int              half_dbits;     /* longest |d| of the half-size form (fd25519_half.h) */
+  int              dsm_quad;       /* dsm phase: a quad of lanes per signature (dsm4)  */
+  int              dsm_fix_only;   /* dsm kernel: the full-length items only           */
 } fd_ed25519_verify_params_t;
 
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a

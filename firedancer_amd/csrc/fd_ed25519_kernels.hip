@@ -27,6 +27,7 @@
    a fixed HBM scratch of waves x 90 KiB. */
 #include <hip/hip_runtime.h>
 #include "fd25519_dsm.h"
+#include "fd25519_ge4.h"
 #include "fd25519_sc.h"
 #include "fd_sha512_dev.h"
 #define FD_HALF_FN __device__ static inline
@@ -553,7 +554,7 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   int4* tabR = tabA + 90;
   const uint64_t nfix = *p.fix_cnt;
   const uint64_t nfix64 = (nfix + 63u) & ~(uint64_t)63u;
-  const uint64_t total = nfix64 + p.n;
+  const uint64_t total = p.dsm_fix_only ? nfix : nfix64 + p.n;
   for (;;) {
     uint32_t b = 0u;
     if (lane == 0u) b = atomicAdd(p.work_ctr, 64u);
@@ -568,6 +569,149 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
       if (!(p.hflag[j] & FD_HF_FULL)) p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
     }
   }
+}
+
+/* ------------------------------------------------------------------------
+   dsm4: the same half-size group equation with a quad of lanes per
+   signature (fd25519_ge4.h), for small chunks: the verify tile's latency
+   mode, where a one-lane-per-signature launch leaves the chip idle and the
+   batch waits for one lane's serial chain.  Same digits, tables (in qc
+   layout: each lane stores its coordinate of every entry, 48-byte entries,
+   FD_ED25519_QUAD_LANE_BYTES per lane) and addition order as
+   dsm_half_one, each group operation in one multiplication's time.  A
+   negative table digit adds -Q as -((-P) + Q) (negating P costs no DPP,
+   swapping Q's coordinates would).  Full-length items are left to the dsm
+   kernel (launched after this one in fix-only mode). */
+
+FD_DEV void tab4_store(int4* tab, int e, const fe& c) {
+  int4* d = tab + 3 * e;
+  d[0] = make_int4(c.v[0], c.v[1], c.v[2], c.v[3]);
+  d[1] = make_int4(c.v[4], c.v[5], c.v[6], c.v[7]);
+  d[2] = make_int4(c.v[8], c.v[9], 0, 0);
+}
+
+FD_DEV void tab4_load(fe& c, const int4* tab, int e) {
+  const int4* s = tab + 3 * e;
+  const int4 a = s[0], b = s[1], d = s[2];
+  c.v[0] = a.x; c.v[1] = a.y; c.v[2] = a.z; c.v[3] = a.w;
+  c.v[4] = b.x; c.v[5] = b.y; c.v[6] = b.z; c.v[7] = b.w;
+  c.v[8] = d.x; c.v[9] = d.y;
+}
+
+/* this lane's coordinate of base entry e as qc: (y-x, y+x, 2dxy, 2) */
+FD_DEV void btab4_load(fe& c, const int32_t* g_btab, int e, const qmask_t& m) {
+  const int off = m.l0 ? 10 : (m.l1 ? 0 : 20);
+  const int2* s = reinterpret_cast<const int2*>(g_btab + (size_t)e * FD_ED25519_BTAB16_STRIDE + off);
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const int2 x = s[q];
+    c.v[2 * q] = x.x;
+    c.v[2 * q + 1] = x.y;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) c.v[i] = m.l3 ? (i == 0 ? 2 : 0) : c.v[i];
+}
+
+/* [0..8](sign P) as qc entries for the affine point (x, y) */
+FD_DEV void table4_build(int4* tab, const fe& x, const fe& y, bool negate, const qmask_t& m) {
+  fe xs, xy, p0, c1, c, r, cur;
+#pragma unroll
+  for (int i = 0; i < 10; i++) xs.v[i] = negate ? -x.v[i] : x.v[i];
+  fe_mul(xy, xs, y);
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    p0.v[i] = m.l0 ? xs.v[i] : (m.l1 ? y.v[i] : (m.l2 ? (i == 0 ? 1 : 0) : xy.v[i]));
+    c.v[i] = i == 0 ? (m.l2 ? 0 : (m.l3 ? 2 : 1)) : 0;   /* the identity (1, 1, 0, 2) */
+  }
+  tab4_store(tab, 0, c);
+  ge4_to_qc(c1, p0, m);
+  tab4_store(tab, 1, c1);
+  cur = p0;
+#pragma clang loop unroll(disable)
+  for (int e = 2; e <= 8; e++) {
+    ge4_add(r, cur, c1, m);
+    ge4_to_p3(cur, r);
+    ge4_to_qc(c, cur, m);
+    tab4_store(tab, e, c);
+  }
+}
+
+__global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t j = gid >> 2;   /* a quad per signature: all four lanes take the same branches */
+  if (j >= p.n) return;
+  const uint32_t hf = p.hflag[j];
+  if (hf & FD_HF_FULL) return;
+  const qmask_t m = quad_masks();
+  int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + gid * FD_ED25519_QUAD_LANE_BYTES);
+  int4* tabR = tabA + 27;
+  int code = precheck(p, j);
+  {
+    fe x, y;
+    load_pt(x, y, p, 0, j);
+    table4_build(tabA, x, y, true, m);
+    load_pt(x, y, p, 1, j);
+    table4_build(tabR, x, y, !(hf & FD_HF_DNEG), m);
+  }
+  uint32_t cd[5], dd[5], ld[5], hd[5];
+  int W = 33;
+  {
+    uint32_t x[5], t[5];
+    load_hs(x, p, 5, 5, j);
+    const int wl = (fd_half_bitlen<5>(x) + 4) >> 2;
+#pragma unroll
+    for (int w = 34; w <= (FD_HALF_DBITS_MAX + 4) / 4; w++) W += __ballot(wl >= w) != 0ull;
+    const int sh = 160 - 4 * W;
+    shl160v(t, x, sh); recode160<4>(dd, t);
+    load_hs(x, p, 0, 5, j);  shl160v(t, x, sh); recode160<4>(cd, t);
+    load_hs(x, p, 10, 5, j); shl160<20>(ld, x);
+    load_hs(x, p, 15, 4, j); shl160<20>(hd, x);
+  }
+  fe P, Rt;
+#pragma unroll
+  for (int i = 0; i < 10; i++) P.v[i] = (i == 0 && (m.l1 | m.l2)) ? 1 : 0;   /* identity (0, 1, 1, 0) */
+#pragma clang loop unroll(disable)
+  for (int it = W - 1; it >= 0; it--) {
+    int ea = pop160<4>(cd), er = pop160<4>(dd);
+    if (it == W - 1) { ea &= 15; er &= 15; }
+    const bool badd = it <= 30 && it % 5 == 0;
+    fe ca, cr, b1, b2;
+    tab4_load(ca, tabA, ea < 0 ? -ea : ea);
+    if (it != W - 1) {
+#pragma clang loop unroll(disable)
+      for (int dbl = 0; dbl < 4; dbl++) {
+        ge4_dbl(Rt, P, m);
+        ge4_to_p3(P, Rt);
+      }
+    }
+    tab4_load(cr, tabR, er < 0 ? -er : er);
+    ge4_cneg(P, m.l03, ea < 0);
+    ge4_add(Rt, P, ca, m);
+    ge4_cneg(Rt, m.l0, ea < 0);
+    ge4_to_p3(P, Rt);
+    if (badd) {
+      btab4_load(b1, p.btab20, (int)pop160u<20>(ld), m);
+      btab4_load(b2, p.btab20b, (int)pop160u<20>(hd), m);
+    }
+    ge4_cneg(P, m.l03, er < 0);
+    ge4_add(Rt, P, cr, m);
+    ge4_cneg(Rt, m.l0, er < 0);
+    ge4_to_p3(P, Rt);
+    if (badd) {
+      ge4_add(Rt, P, b1, m);
+      ge4_to_p3(P, Rt);
+      ge4_add(Rt, P, b2, m);
+      ge4_to_p3(P, Rt);
+    }
+  }
+  /* identity: X == 0 and Y == Z (on lane 0) */
+  fe y1, z1, t;
+  fe_qp<FD_QP(1, 1, 1, 1)>(y1, P);
+  fe_qp<FD_QP(2, 2, 2, 2)>(z1, P);
+  fe_sub(t, y1, z1);
+  const bool ident = fe_iszero(P) && fe_iszero(t);
+  if (code == FD_PENDING) code = ident ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  if (m.l0) p.out[p.base + j] = (int8_t)code;
 }
 
 /* ------------------------------------------------------------------------
@@ -797,6 +941,15 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
                        *p);
     break;
   case FD_ED25519_PHASE_DSM: {
+    if (p->dsm_quad) {
+      /* a quad per signature, then the (rare) full-length items */
+      hipLaunchKernelGGL(fd_ed25519_dsm4_kernel, dim3((uint32_t)((4 * p->n + 255) / 256)), dim3(256), 0, st, *p);
+      fd_ed25519_verify_params_t q = *p;
+      q.dsm_fix_only = 1;
+      const uint32_t g = grid < 16u ? grid : 16u;
+      hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, q);
+      break;
+    }
     /* one wave more than the chunk needs: the full-length items (counted on
        the device) run in waves of their own, in parallel with the rest */
     const uint64_t need = (p->n + 64 + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;

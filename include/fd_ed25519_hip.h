@@ -89,6 +89,13 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    |d| up to 2^151 with a few more windows, the full-length form only for
    ~1e-6 of random k.  Same verdicts either way; for tests and A/B. */
 #define FD_ED25519_HIP_FLAG_HALF_STRICT    (2)
+/* The dsm phase runs one signature per lane (throughput) or, for chunks of
+   at most FD_ED25519_HIP_QUAD_MAX_DEFAULT signatures ($FD_ED25519_HIP_QUAD_MAX),
+   one per quad of lanes (latency: each group operation in one
+   multiplication's time).  These force either form (tests / A-B). */
+#define FD_ED25519_HIP_FLAG_DSM_QUAD       (4)
+#define FD_ED25519_HIP_FLAG_DSM_WIDE       (8)
+#define FD_ED25519_HIP_QUAD_MAX_DEFAULT    (32768UL)
 
 /* Creates an engine on HIP device `device`.  max_chunk is the number of
    signatures processed per kernel sequence (0 = default 1<<20); larger

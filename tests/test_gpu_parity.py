@@ -20,16 +20,19 @@ def fd():
     return ed25519
 
 
-@pytest.fixture(scope="module")
-def eng(fd):
-    e = fd.Engine(0, max_chunk=1 << 16)
+# Every engine test runs with both dsm forms: a quad of lanes per signature
+# (what chunks of up to FD_ED25519_HIP_QUAD_MAX_DEFAULT signatures use) and
+# one lane per signature (larger chunks).
+@pytest.fixture(scope="module", params=["quad", "wide"])
+def eng(fd, request):
+    e = fd.Engine(0, max_chunk=1 << 16, dsm=request.param)
     yield e
     e.close()
 
 
-@pytest.fixture(scope="module")
-def eng_portable(fd):
-    e = fd.Engine(0, max_chunk=1 << 14, codes="portable")
+@pytest.fixture(scope="module", params=["quad", "wide"])
+def eng_portable(fd, request):
+    e = fd.Engine(0, max_chunk=1 << 14, codes="portable", dsm=request.param)
     yield e
     e.close()
 
@@ -155,6 +158,17 @@ def test_chunking(fd, oracle):
     e.close()
 
 
+def test_dsm_form_by_size(fd, oracle, monkeypatch):
+    """The automatic choice: a chunk at the quad limit and one above it
+    (FD_ED25519_HIP_QUAD_MAX lowered so the test stays small) in one batch,
+    against the oracle."""
+    monkeypatch.setenv("FD_ED25519_HIP_QUAD_MAX", "600")
+    e = fd.Engine(0, max_chunk=1000)
+    d = _random_set(oracle, 1600, seed=15)   # chunks of 1000 (wide) and 600 (quad)
+    _check(_run(e, d), oracle_many(oracle, d, 0))
+    e.close()
+
+
 def test_empty_batch(eng):
     out = eng.verify_host(np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
                           np.zeros((0, 64), np.uint8), np.zeros((0, 32), np.uint8))
@@ -183,9 +197,9 @@ def test_strerror(fd):
     assert fd.strerror(0) == "success" and fd.strerror(-3) == "bad message" and fd.strerror(5) == "unknown"
 
 
-@pytest.fixture(scope="module")
-def eng_strict(fd):
-    e = fd.Engine(0, max_chunk=1 << 14, half="strict")
+@pytest.fixture(scope="module", params=["quad", "wide"])
+def eng_strict(fd, request):
+    e = fd.Engine(0, max_chunk=1 << 14, half="strict", dsm=request.param)
     yield e
     e.close()
 

@@ -26,8 +26,9 @@ def main():
     ap.add_argument("--batches", type=int, default=40)
     ap.add_argument("--msg", type=int, default=200)
     ap.add_argument("--half", default="extended")
+    ap.add_argument("--dsm", default="auto")
     args = ap.parse_args()
-    eng = ed25519.Engine(0, max_chunk=1 << 16, half=args.half)
+    eng = ed25519.Engine(0, max_chunk=1 << 16, half=args.half, dsm=args.dsm)
     for n in [int(x) for x in args.sizes.split(",")]:
         wall, dsm, other = [], [], []
         for b in range(args.batches):
@@ -46,7 +47,7 @@ def main():
             other.append(ph["hash"] + ph["scalar"] + ph["decode"])
             w.free()
         pct = lambda a, q: float(np.percentile(np.array(a), q))  # noqa: E731
-        print(json.dumps({"n": n, "half": args.half, "batches": args.batches,
+        print(json.dumps({"n": n, "half": args.half, "dsm": args.dsm, "batches": args.batches,
                           "wall_ms": {"p50": pct(wall, 50), "p90": pct(wall, 90), "max": max(wall)},
                           "dsm_ms": {"p50": pct(dsm, 50), "p90": pct(dsm, 90), "max": max(dsm)},
                           "hash_scalar_decode_ms_p50": pct(other, 50)}), flush=True)
