@@ -104,11 +104,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_sort_scatter_kernel(fd_ed25519
   if (j < p.n) p.perm[base[b] + r] = (uint32_t)j;
 }
 
-__global__ void __launch_bounds__(256, FD_ED25519_HASH_WAVES_PER_SIMD)
-fd_ed25519_hash_kernel(fd_ed25519_verify_params_t p) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= p.n) return;
-  const uint64_t j = p.perm ? (uint64_t)p.perm[t] : t;
+FD_DEV void hash_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
   const uint64_t i = p.base + j;
   uint32_t r[8], S[8], a[8];
   {
@@ -132,15 +128,17 @@ fd_ed25519_hash_kernel(fd_ed25519_verify_params_t p) {
   p.sflag[j] = sc_is_canonical(S) ? 1 : 0;
 }
 
+__global__ void __launch_bounds__(256, FD_ED25519_HASH_WAVES_PER_SIMD)
+fd_ed25519_hash_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.n) return;
+  hash_one(p, p.perm ? (uint64_t)p.perm[t] : t);
+}
+
 /* One lane per point (2n lanes: A, then R): decompression with the
    reference's acceptance rules (fd_ed25519_point_frombytes_2x) and the
    small-order test (fd_ed25519_affine_is_small_order). */
-__global__ void __launch_bounds__(256, FD_ED25519_DECODE_WAVES_PER_SIMD)
-fd_ed25519_decode_kernel(fd_ed25519_verify_params_t p) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * p.n) return;
-  const int which = t >= p.n;           /* 0: A (public key), 1: R */
-  const uint64_t j = which ? t - p.n : t;
+FD_DEV void decode_one(const fd_ed25519_verify_params_t& p, int which /* 0: A (public key), 1: R */, uint64_t j) {
   const uint64_t i = p.base + j;
   uint32_t s[8];
   {
@@ -158,6 +156,14 @@ fd_ed25519_decode_kernel(fd_ed25519_verify_params_t p) {
     dst[(uint64_t)(10 + l) * p.cap] = d.y.v[l];
   }
   p.pflag[(uint64_t)which * p.cap + j] = (uint8_t)((d.fail ? FD_PF_FAIL : 0u) | (d.small ? FD_PF_SMALL : 0u));
+}
+
+__global__ void __launch_bounds__(256, FD_ED25519_DECODE_WAVES_PER_SIMD)
+fd_ed25519_decode_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * p.n) return;
+  const int which = t >= p.n;
+  decode_one(p, which, which ? t - p.n : t);
 }
 
 FD_DEV void load_fe(fe& x, const int32_t* src, uint64_t cap) {
@@ -240,10 +246,7 @@ FD_DEV void btab_add(ge_p1p1& Rt, const ge_p3& P, ge_precomp& b, int f) {
    at 151 bits, ~0.16% at 131) are flagged and queued on fix_list for the
    full-length form. */
 
-__global__ void __launch_bounds__(256, FD_ED25519_SCALAR_WAVES_PER_SIMD)
-fd_ed25519_scalar_kernel(fd_ed25519_verify_params_t p) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= p.n) return;
+FD_DEV void scalar_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
   const uint64_t i = p.base + j;
   uint32_t k[8], S[8];
 #pragma unroll
@@ -302,9 +305,34 @@ fd_ed25519_scalar_kernel(fd_ed25519_verify_params_t p) {
   for (int w = 0; w < 4; w++)
     hs[(uint64_t)(15 + w) * c] = __builtin_amdgcn_alignbit(sp[w + 5], sp[w + 4], 4);  /* bits 132..   */
   p.hflag[j] = (uint8_t)((dneg ? FD_HF_DNEG : 0u) | (ok ? 0u : FD_HF_FULL));
-  if (!ok) {
+  if (!ok && !p.small) {   /* small chunks: the dsm scan finds them by hflag */
     const uint32_t slot = atomicAdd(p.fix_cnt, 1u);
     p.fix_list[slot] = (uint32_t)j;
+  }
+}
+
+__global__ void __launch_bounds__(256, FD_ED25519_SCALAR_WAVES_PER_SIMD)
+fd_ed25519_scalar_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p.n) return;
+  scalar_one(p, j);
+}
+
+/* Small chunks (the latency regime): hash, scalar and decode in one launch,
+   specialised by wave so no wave diverges: per 64 signatures, wave 0 hashes
+   and then finds the half-size scalars, waves 1 and 2 decode A and R, all
+   three at once on different SIMDs (the path is the longer of the two
+   chains instead of their sum, and two launches and the counting sort are
+   gone). */
+__global__ void __launch_bounds__(192) fd_ed25519_prep_kernel(fd_ed25519_verify_params_t p) {
+  const uint32_t w = threadIdx.x >> 6;
+  const uint64_t j = (uint64_t)blockIdx.x * 64u + (threadIdx.x & 63u);
+  if (j >= p.n) return;
+  if (w == 0) {
+    hash_one(p, j);
+    scalar_one(p, j);
+  } else {
+    decode_one(p, (int)w - 1, j);
   }
 }
 
@@ -552,9 +580,17 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + wave * FD_ED25519_ATAB_BYTES_PER_WAVE) +
                lane * 180;
   int4* tabR = tabA + 90;
+  if (p.small) {
+    /* after dsm4: the full-length items only, found by their flag (a
+       static stride: the work counter is not reset for small chunks) */
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < p.n; t += stride)
+      if (p.hflag[t] & FD_HF_FULL) p.out[p.base + t] = (int8_t)dsm_full_one(p, t, tabA);
+    return;
+  }
   const uint64_t nfix = *p.fix_cnt;
   const uint64_t nfix64 = (nfix + 63u) & ~(uint64_t)63u;
-  const uint64_t total = p.dsm_fix_only ? nfix : nfix64 + p.n;
+  const uint64_t total = nfix64 + p.n;
   for (;;) {
     uint32_t b = 0u;
     if (lane == 0u) b = atomicAdd(p.work_ctr, 64u);
@@ -920,6 +956,10 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
   const uint32_t blk = 256;
   switch (phase) {
   case FD_ED25519_PHASE_HASH: {
+    if (p->small) {
+      hipLaunchKernelGGL(fd_ed25519_prep_kernel, dim3((uint32_t)((p->n + 63) / 64)), dim3(192), 0, st, *p);
+      break;
+    }
     const dim3 g((uint32_t)((p->n + blk - 1) / blk));
     if (p->perm) {
       const hipError_t e = hipMemsetAsync(p->hist, 0, 2 * FD_ED25519_SORT_BUCKETS * sizeof(uint32_t), st);
@@ -931,23 +971,25 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
     hipLaunchKernelGGL(fd_ed25519_hash_kernel, g, dim3(blk), 0, st, *p);
   } break;
   case FD_ED25519_PHASE_SCALAR: {
+    if (p->small) break;   /* in the prep kernel */
     /* fix_cnt and the dsm work counter, adjacent words */
     const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 2 * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(fd_ed25519_scalar_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
   } break;
   case FD_ED25519_PHASE_DECODE:
+    if (p->small) break;   /* in the prep kernel */
     hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((2 * p->n + blk - 1) / blk)), dim3(blk), 0, st,
                        *p);
     break;
   case FD_ED25519_PHASE_DSM: {
-    if (p->dsm_quad) {
-      /* a quad per signature, then the (rare) full-length items */
+    if (p->small) {
+      /* a quad per signature, then the (rare) full-length items, found by
+         a scan of the flags */
       hipLaunchKernelGGL(fd_ed25519_dsm4_kernel, dim3((uint32_t)((4 * p->n + 255) / 256)), dim3(256), 0, st, *p);
-      fd_ed25519_verify_params_t q = *p;
-      q.dsm_fix_only = 1;
-      const uint32_t g = grid < 16u ? grid : 16u;
-      hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, q);
+      const uint64_t need = (p->n + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
+      const uint32_t g = (uint32_t)(need < grid ? need : grid);
+      hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
       break;
     }
     /* one wave more than the chunk needs: the full-length items (counted on
