@@ -78,3 +78,8 @@ def oracle_many(oracle, d, codes=0, nthreads=8):
 @pytest.fixture(scope="session")
 def halfsize():
     return load_golden("halfsize")
+
+
+@pytest.fixture(scope="session")
+def longd():
+    return load_golden("longd")

@@ -30,16 +30,18 @@ def half_lib():
                            os.path.join(REPO, "firedancer_amd", "csrc"),
                            os.path.join(REPO, "tests", "half_harness.cpp"), "-o", out])
     lib = ctypes.CDLL(out)
-    lib.half_scalars.argtypes = [ctypes.c_void_p] * 4
+    lib.half_scalars.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int]
     lib.half_scalars.restype = ctypes.c_int
     return lib
 
 
-def has_half(lib, r, a, m):
+def has_half(lib, r, a, m, dbits=131):
+    """a pair with |d| < 2^dbits (131: the strict half-size form)"""
     k = int.from_bytes(hashlib.sha512(r + a + m).digest(), "little") % L
     kb = (ctypes.c_uint32 * 8)(*[(k >> (32 * i)) & 0xffffffff for i in range(8)])
     c, d, neg = (ctypes.c_uint32 * 5)(), (ctypes.c_uint32 * 5)(), ctypes.c_int()
-    return lib.half_scalars(ctypes.addressof(kb), ctypes.addressof(c), ctypes.addressof(d), ctypes.addressof(neg))
+    return lib.half_scalars(ctypes.addressof(kb), ctypes.addressof(c), ctypes.addressof(d), ctypes.addressof(neg),
+                            dbits)
 
 
 def main():

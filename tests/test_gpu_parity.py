@@ -216,6 +216,37 @@ def test_halfsize_fallback_strict(eng_strict, halfsize):
     _check(_run(eng_strict, halfsize), halfsize["codes_avx512"], halfsize["tags"])
 
 
+def test_long_d_windows(eng, longd):
+    """k whose half-size pair needs |d| up to 2^151: waves of 36..38 windows."""
+    _check(_run(eng, longd), longd["codes_avx512"], longd["tags"])
+
+
+def test_long_d_strict(eng_strict, longd):
+    """The same under FLAG_HALF_STRICT: the full-length form."""
+    _check(_run(eng_strict, longd), longd["codes_avx512"], longd["tags"])
+
+
+def test_long_d_mixed_into_waves(eng, longd, adversarial):
+    """One long-d signature in each wave of an otherwise ordinary chunk: the
+    other lanes run the longer window count with zero top digits."""
+    parts_m, off, sz, sigs, pubs, want = [], [], [], [], [], []
+    base = 0
+    for i in range(len(longd["msg_sz"])):
+        for d, j in ((longd, i), (adversarial, None)):
+            if j is None:
+                sel = np.arange(63 * i, 63 * i + 63) % len(d["msg_sz"])
+            else:
+                sel = np.array([j])
+            for t in sel:
+                o, n = int(d["msg_off"][t]), int(d["msg_sz"][t])
+                parts_m.append(d["msgs"][o:o + n])
+                off.append(base); sz.append(n); base += n
+                sigs.append(d["sigs"][t]); pubs.append(d["pubs"][t]); want.append(d["codes_avx512"][t])
+    msgs = np.concatenate(parts_m) if base else np.zeros(1, np.uint8)
+    got = eng.verify_host(msgs, np.array(off, np.uint64), np.array(sz, np.uint32), np.stack(sigs), np.stack(pubs))
+    _check(got, np.array(want, np.int8))
+
+
 def test_halfsize_fallback_portable(eng_portable, halfsize):
     _check(_run(eng_portable, halfsize), halfsize["codes_portable"], halfsize["tags"])
 

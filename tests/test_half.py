@@ -152,3 +152,22 @@ def test_fixture_k_have_no_half_pair(half):
         ok, _, dd = run(half, k, DBITS_EXT)
         assert ok and abs(dd) >= 2**BITS, (i, str(d["tags"][i]))
     assert len(set(d["codes_avx512"].tolist())) == 4 and np.any(d["codes_avx512"] == 0)
+
+
+def test_fixture_k_need_long_d(half):
+    """tests/golden/longd.npz (gen_longd.py): k whose pair needs
+    2^139 <= |d| < 2^151, i.e. 36..38 dsm windows as tagged."""
+    import hashlib
+    from conftest import load_golden
+    d = load_golden("longd")
+    for i in range(len(d["msg_sz"])):
+        off, sz = int(d["msg_off"][i]), int(d["msg_sz"][i])
+        m = bytes(d["msgs"][off:off + sz])
+        k = int.from_bytes(hashlib.sha512(d["sigs"][i][:32].tobytes() + d["pubs"][i].tobytes() + m).digest(),
+                           "little") % L
+        tag = str(d["tags"][i])
+        w = int(tag.split("_")[1][1:])
+        ok, c, dd = run(half, k, DBITS_EXT)
+        assert ok and (c - dd * k) % N8L == 0 and 0 <= c < 2**BITS, tag
+        assert (abs(dd).bit_length() + 4) // 4 == w, (tag, abs(dd).bit_length())
+        assert not run(half, k, 139)[0], tag
