@@ -98,9 +98,9 @@ typedef struct {
   void *           atab;     /* device scratch, waves * ATAB_BYTES_PER_WAVE    */
   int              codes_portable; /* 0: AVX-512 backend codes, 1: portable  */
   int              half_dbits;     /* longest |d| of the half-size form (fd25519_half.h) */
-  int              small;          /* small chunk: fused prep kernel, no sort, dsm4 (a
-                                      quad of lanes per signature), full-length items
-                                      by a scan of hflag                             */
+  int              small;          /* small chunk: fused prep kernel, no sort, dsm4 (1: a
+                                      quad of lanes per signature) or dsm8 (2: two quads),
+                                      full-length items by a scan of hflag          */
 } fd_ed25519_verify_params_t;
 
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a

@@ -750,6 +750,90 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
   if (m.l0) p.out[p.base + j] = (int8_t)code;
 }
 
+/* dsm8: two quads per signature for the smallest chunks.  The four-scalar
+   sum splits into two Straus halves over the same windows,
+
+       quad 0: [c](-A) + [s_lo]B        quad 1: [|d|](-+R) + [s_hi]B',
+
+   each quad building only its own [0..8] table and doing one table
+   addition (plus one base addition every 5th window) per 4 doublings;
+   quad 1 then hands its point to quad 0 (DPP row shift) for one last
+   addition and the identity test.  ~22% less latency than dsm4 for ~57%
+   more lane work. */
+__global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t j = gid >> 3;                 /* 8 lanes per signature, the same branches */
+  if (j >= p.n) return;
+  const uint32_t hf = p.hflag[j];
+  if (hf & FD_HF_FULL) return;
+  const int half = (int)((threadIdx.x >> 2) & 1u);   /* 0: -A and B, 1: -+R and B' */
+  const qmask_t m = quad_masks();
+  int4* tab = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + gid * (FD_ED25519_QUAD_LANE_BYTES / 2));
+  int code = precheck(p, j);
+  {
+    fe x, y;
+    load_pt(x, y, p, half, j);
+    table4_build(tab, x, y, half ? !(hf & FD_HF_DNEG) : true, m);
+  }
+  uint32_t sd[5], bd[5];
+  int W = 33;
+  {
+    uint32_t x[5], t[5];
+    load_hs(x, p, 5, 5, j);
+    const int wl = (fd_half_bitlen<5>(x) + 4) >> 2;
+#pragma unroll
+    for (int w = 34; w <= (FD_HALF_DBITS_MAX + 4) / 4; w++) W += __ballot(wl >= w) != 0ull;
+    if (!half) load_hs(x, p, 0, 5, j);
+    shl160v(t, x, 160 - 4 * W); recode160<4>(sd, t);
+    if (half) load_hs(x, p, 15, 4, j);
+    else load_hs(x, p, 10, 5, j);
+    shl160<20>(bd, x);
+  }
+  const int32_t* btab = half ? p.btab20b : p.btab20;
+  fe P, Rt;
+#pragma unroll
+  for (int i = 0; i < 10; i++) P.v[i] = (i == 0 && (m.l1 | m.l2)) ? 1 : 0;   /* identity (0, 1, 1, 0) */
+#pragma clang loop unroll(disable)
+  for (int it = W - 1; it >= 0; it--) {
+    int e = pop160<4>(sd);
+    if (it == W - 1) e &= 15;
+    const bool badd = it <= 30 && it % 5 == 0;
+    fe ce, b;
+    tab4_load(ce, tab, e < 0 ? -e : e);
+    if (it != W - 1) {
+#pragma clang loop unroll(disable)
+      for (int dbl = 0; dbl < 4; dbl++) {
+        ge4_dbl(Rt, P, m);
+        ge4_to_p3(P, Rt);
+      }
+    }
+    if (badd) btab4_load(b, btab, (int)pop160u<20>(bd), m);
+    ge4_cneg(P, m.l03, e < 0);
+    ge4_add(Rt, P, ce, m);
+    ge4_cneg(Rt, m.l0, e < 0);
+    ge4_to_p3(P, Rt);
+    if (badd) {
+      ge4_add(Rt, P, b, m);
+      ge4_to_p3(P, Rt);
+    }
+  }
+  /* quad 1's point as an addend, moved 4 lanes down */
+  fe q, qs;
+  ge4_to_qc(q, P, m);
+#pragma unroll
+  for (int i = 0; i < 10; i++) qs.v[i] = __shfl_down(q.v[i], 4);
+  ge4_add(Rt, P, qs, m);
+  ge4_to_p3(P, Rt);
+  /* identity: X == 0 and Y == Z (on lane 0 of quad 0) */
+  fe y1, z1, t;
+  fe_qp<FD_QP(1, 1, 1, 1)>(y1, P);
+  fe_qp<FD_QP(2, 2, 2, 2)>(z1, P);
+  fe_sub(t, y1, z1);
+  const bool ident = fe_iszero(P) && fe_iszero(t);
+  if (code == FD_PENDING) code = ident ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  if (m.l0 && !half) p.out[p.base + j] = (int8_t)code;
+}
+
 /* ------------------------------------------------------------------------
    Base tables [0..entries)B as (y+x, y-x, 2dxy), one entry per lane:
    [e]B by double-and-add over `bits` bits, then affine. */
@@ -986,7 +1070,10 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
     if (p->small) {
       /* a quad per signature, then the (rare) full-length items, found by
          a scan of the flags */
-      hipLaunchKernelGGL(fd_ed25519_dsm4_kernel, dim3((uint32_t)((4 * p->n + 255) / 256)), dim3(256), 0, st, *p);
+      if (p->small == 2)
+        hipLaunchKernelGGL(fd_ed25519_dsm8_kernel, dim3((uint32_t)((8 * p->n + 255) / 256)), dim3(256), 0, st, *p);
+      else
+        hipLaunchKernelGGL(fd_ed25519_dsm4_kernel, dim3((uint32_t)((4 * p->n + 255) / 256)), dim3(256), 0, st, *p);
       const uint64_t need = (p->n + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
       const uint32_t g = (uint32_t)(need < grid ? need : grid);
       hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);

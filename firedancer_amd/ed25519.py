@@ -26,6 +26,7 @@ FLAG_CODES_PORTABLE = 1
 FLAG_HALF_STRICT = 2     # half-size |d| < 2^131 only (full-length form for the rest): tests / A-B
 FLAG_DSM_QUAD = 4        # dsm with a quad of lanes per signature at every chunk size
 FLAG_DSM_WIDE = 8        # dsm with one lane per signature at every chunk size
+FLAG_DSM_OCT = 16        # dsm with two quads of lanes per signature at every chunk size
 
 # phases of a verify launch (FD_ED25519_HIP_PHASE_CNT, include/fd_ed25519_hip.h)
 PHASES = ("hash", "scalar", "decode", "dsm")
@@ -134,7 +135,7 @@ class Engine:
     def __init__(self, device=0, max_chunk=0, codes="avx512", half="extended", dsm="auto"):
         flags = FLAG_CODES_PORTABLE if codes == "portable" else 0
         flags |= FLAG_HALF_STRICT if half == "strict" else 0
-        flags |= {"auto": 0, "quad": FLAG_DSM_QUAD, "wide": FLAG_DSM_WIDE}[dsm]
+        flags |= {"auto": 0, "quad": FLAG_DSM_QUAD, "wide": FLAG_DSM_WIDE, "oct": FLAG_DSM_OCT}[dsm]
         self._h = _lib.fd_ed25519_hip_engine_new(int(device), int(max_chunk), flags)
         if not self._h:
             raise HipError(f"engine_new failed: {_lib.fd_ed25519_hip_last_error().decode()}")

@@ -92,10 +92,14 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
 /* The dsm phase runs one signature per lane (throughput) or, for chunks of
    at most FD_ED25519_HIP_QUAD_MAX_DEFAULT signatures ($FD_ED25519_HIP_QUAD_MAX),
    one per quad of lanes (latency: each group operation in one
-   multiplication's time).  These force either form (tests / A-B). */
+   multiplication's time), and for at most FD_ED25519_HIP_OCT_MAX_DEFAULT
+   ($FD_ED25519_HIP_OCT_MAX) one per two quads (the two halves of the
+   multi-scalar sum in parallel).  These force one form (tests / A-B). */
 #define FD_ED25519_HIP_FLAG_DSM_QUAD       (4)
 #define FD_ED25519_HIP_FLAG_DSM_WIDE       (8)
+#define FD_ED25519_HIP_FLAG_DSM_OCT        (16)
 #define FD_ED25519_HIP_QUAD_MAX_DEFAULT    (32768UL)
+#define FD_ED25519_HIP_OCT_MAX_DEFAULT     (8192UL)
 
 /* Creates an engine on HIP device `device`.  max_chunk is the number of
    signatures processed per kernel sequence (0 = default 1<<20); larger

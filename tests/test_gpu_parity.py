@@ -20,17 +20,17 @@ def fd():
     return ed25519
 
 
-# Every engine test runs with both dsm forms: a quad of lanes per signature
-# (what chunks of up to FD_ED25519_HIP_QUAD_MAX_DEFAULT signatures use) and
-# one lane per signature (larger chunks).
-@pytest.fixture(scope="module", params=["quad", "wide"])
+# Every engine test runs with each dsm form: two quads of lanes per
+# signature (chunks of up to FD_ED25519_HIP_OCT_MAX_DEFAULT signatures), a
+# quad (up to FD_ED25519_HIP_QUAD_MAX_DEFAULT) and one lane per signature.
+@pytest.fixture(scope="module", params=["oct", "quad", "wide"])
 def eng(fd, request):
     e = fd.Engine(0, max_chunk=1 << 16, dsm=request.param)
     yield e
     e.close()
 
 
-@pytest.fixture(scope="module", params=["quad", "wide"])
+@pytest.fixture(scope="module", params=["oct", "quad", "wide"])
 def eng_portable(fd, request):
     e = fd.Engine(0, max_chunk=1 << 14, codes="portable", dsm=request.param)
     yield e
@@ -159,13 +159,15 @@ def test_chunking(fd, oracle):
 
 
 def test_dsm_form_by_size(fd, oracle, monkeypatch):
-    """The automatic choice: a chunk at the quad limit and one above it
-    (FD_ED25519_HIP_QUAD_MAX lowered so the test stays small) in one batch,
-    against the oracle."""
+    """The automatic choice by chunk size (thresholds lowered through the
+    environment so the test stays small): a batch of two chunks (1000 wide,
+    600 quad), one of 600 (quad) and one of 300 (oct), against the oracle."""
     monkeypatch.setenv("FD_ED25519_HIP_QUAD_MAX", "600")
+    monkeypatch.setenv("FD_ED25519_HIP_OCT_MAX", "300")
     e = fd.Engine(0, max_chunk=1000)
-    d = _random_set(oracle, 1600, seed=15)   # chunks of 1000 (wide) and 600 (quad)
-    _check(_run(e, d), oracle_many(oracle, d, 0))
+    for n, seed in ((1600, 15), (600, 16), (300, 17)):
+        d = _random_set(oracle, n, seed=seed)
+        _check(_run(e, d), oracle_many(oracle, d, 0))
     e.close()
 
 
@@ -197,7 +199,7 @@ def test_strerror(fd):
     assert fd.strerror(0) == "success" and fd.strerror(-3) == "bad message" and fd.strerror(5) == "unknown"
 
 
-@pytest.fixture(scope="module", params=["quad", "wide"])
+@pytest.fixture(scope="module", params=["oct", "quad", "wide"])
 def eng_strict(fd, request):
     e = fd.Engine(0, max_chunk=1 << 14, half="strict", dsm=request.param)
     yield e
