@@ -58,6 +58,15 @@ typedef struct {
   fd_ed25519_hip_engine_t * eng;
   hipEvent_t                ev;
   int                       state;
+  /* staging: the public host arrays live in one pinned block laid out as
+     [sigs | pubs | msg_off | msg_sz | txn_first | txn_sig_cnt | msgs], its
+     device mirror has the same layout, so a batch goes over in one copy;
+     the codes come back the same way ([sig_out | txn_out]) */
+  unsigned char *           h_in;
+  unsigned char *           d_in;
+  unsigned long             in_msgs;    /* offset of msgs in both blocks */
+  signed char *             h_outb;
+  signed char *             d_outb;
   unsigned char *           d_msgs;
   unsigned long *           d_off;
   unsigned int *            d_sz;
@@ -67,9 +76,9 @@ typedef struct {
   unsigned int *            d_tfirst;
   unsigned int *            d_tcnt;
   signed char *             d_tout;
-  unsigned long *           d_toff;    /* raw mode: per-transaction payload offset */
-  unsigned int *            d_tsz;     /* raw mode: per-transaction payload size   */
-  unsigned char *           d_pok;     /* raw mode: fd_txn_parse accepted          */
+  unsigned long *           d_soff;    /* raw mode: per-signature message offset (device-made) */
+  unsigned int *            d_ssz;     /* raw mode: per-signature message size             */
+  unsigned char *           d_pok;     /* raw mode: fd_txn_parse accepted                  */
 } pipe_slot_t;
 
 struct fd_ed25519_hip_pipe {
@@ -84,13 +93,9 @@ struct fd_ed25519_hip_pipe {
 
 static void
 pipe_slot_free( pipe_slot_t * s ) {
-  fd_ed25519_hip_slot_t * p = &s->pub;
-  hipHostFree( p->msgs ); hipHostFree( p->msg_off ); hipHostFree( p->msg_sz ); hipHostFree( p->sigs );
-  hipHostFree( p->pubs ); hipHostFree( p->txn_first ); hipHostFree( p->txn_sig_cnt ); hipHostFree( p->sig_out );
-  hipHostFree( p->txn_out );
-  hipFree( s->d_msgs ); hipFree( s->d_off ); hipFree( s->d_sz ); hipFree( s->d_sigs ); hipFree( s->d_pubs );
-  hipFree( s->d_out ); hipFree( s->d_tfirst ); hipFree( s->d_tcnt ); hipFree( s->d_tout );
-  hipFree( s->d_toff ); hipFree( s->d_tsz ); hipFree( s->d_pok );
+  hipHostFree( s->h_in ); hipHostFree( s->h_outb );
+  hipFree( s->d_in ); hipFree( s->d_outb );
+  hipFree( s->d_soff ); hipFree( s->d_ssz ); hipFree( s->d_pok );
   if( s->ev ) hipEventDestroy( s->ev );
   if( s->eng ) fd_ed25519_hip_engine_delete( s->eng );
 }
@@ -114,27 +119,34 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   fd_ed25519_hip_slot_t * p = &s->pub;
   p->sig_cap = sig_cap; p->msg_cap = msg_cap; p->txn_cap = txn_cap;
   unsigned long tc = txn_cap ? txn_cap : 1UL;
-  TCHK( hipHostMalloc( (void **)&p->msgs,        msg_cap + 64UL, hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&p->msg_off,     8UL*sig_cap,    hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&p->msg_sz,      4UL*sig_cap,    hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&p->sigs,        64UL*sig_cap,   hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&p->pubs,        32UL*sig_cap,   hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&p->sig_out,     sig_cap,        hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&p->txn_first,   4UL*tc,         hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&p->txn_sig_cnt, 4UL*tc,         hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&p->txn_out,     tc,             hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_msgs,   msg_cap + 64UL ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_off,    8UL*sig_cap    ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_sz,     4UL*sig_cap    ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_sigs,   64UL*sig_cap   ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_pubs,   32UL*sig_cap   ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_out,    sig_cap        ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_tfirst, 4UL*tc         ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_tcnt,   4UL*tc         ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_tout,   tc             ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_toff,   8UL*tc         ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_tsz,    4UL*tc         ), "hipMalloc" );
-  TCHK( hipMalloc( (void **)&s->d_pok,    tc             ), "hipMalloc" );
+  /* per-signature (and, raw mode, per-transaction) offsets and sizes share
+     the msg_off / msg_sz arrays: size them for the larger count */
+  unsigned long oc = sig_cap > tc ? sig_cap : tc;
+  unsigned long o_sigs = 0UL;
+  unsigned long o_pubs = o_sigs + 64UL*sig_cap;
+  unsigned long o_off  = o_pubs + 32UL*sig_cap;
+  unsigned long o_sz   = (o_off + 8UL*oc + 15UL) & ~15UL;
+  unsigned long o_tf   = (o_sz  + 4UL*oc + 15UL) & ~15UL;
+  unsigned long o_tc   = (o_tf  + 4UL*tc + 15UL) & ~15UL;
+  unsigned long o_msgs = (o_tc  + 4UL*tc + 255UL) & ~255UL;
+  unsigned long in_sz  = o_msgs + msg_cap + 64UL;
+  s->in_msgs = o_msgs;
+  TCHK( hipHostMalloc( (void **)&s->h_in,   in_sz,               hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&s->h_outb, sig_cap + tc,        hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipMalloc(     (void **)&s->d_in,   in_sz                                     ), "hipMalloc" );
+  TCHK( hipMalloc(     (void **)&s->d_outb, sig_cap + tc                              ), "hipMalloc" );
+  p->sigs        = s->h_in + o_sigs;                   s->d_sigs   = s->d_in + o_sigs;
+  p->pubs        = s->h_in + o_pubs;                   s->d_pubs   = s->d_in + o_pubs;
+  p->msg_off     = (unsigned long *)(s->h_in + o_off); s->d_off    = (unsigned long *)(s->d_in + o_off);
+  p->msg_sz      = (unsigned int  *)(s->h_in + o_sz);  s->d_sz     = (unsigned int  *)(s->d_in + o_sz);
+  p->txn_first   = (unsigned int  *)(s->h_in + o_tf);  s->d_tfirst = (unsigned int  *)(s->d_in + o_tf);
+  p->txn_sig_cnt = (unsigned int  *)(s->h_in + o_tc);  s->d_tcnt   = (unsigned int  *)(s->d_in + o_tc);
+  p->msgs        = s->h_in + o_msgs;                   s->d_msgs   = s->d_in + o_msgs;
+  p->sig_out     = s->h_outb;                          s->d_out    = s->d_outb;
+  p->txn_out     = s->h_outb + sig_cap;                s->d_tout   = s->d_outb + sig_cap;
+  TCHK( hipMalloc( (void **)&s->d_soff, 8UL*sig_cap ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_ssz,  4UL*sig_cap ), "hipMalloc" );
+  TCHK( hipMalloc( (void **)&s->d_pok,  tc          ), "hipMalloc" );
   TCHK( hipEventCreateWithFlags( &s->ev, hipEventDisableTiming ), "hipEventCreate" );
   s->state = SLOT_FREE;
   return FD_ED25519_HIP_OK;
@@ -161,6 +173,47 @@ fd_ed25519_hip_pipe_new( int device, unsigned slot_cnt, unsigned long sig_cap, u
   return pipe;
 }
 
+/* H2D of a batch: one copy of the staging block's prefix (every array at
+   full capacity, then the used message bytes) unless the unused capacity
+   would cost more to move than the per-array copies' overhead; sig_cnt
+   counts the signature arrays in use, oc_cnt the msg_off/msg_sz entries. */
+#define SLOT_ONE_COPY_SLACK (256UL << 10)
+
+static int
+slot_h2d( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt, unsigned long msg_bytes ) {
+  fd_ed25519_hip_slot_t * p = &s->pub;
+  unsigned long oc_cnt = sig_cnt > txn_cnt ? sig_cnt : txn_cnt;
+  unsigned long used = 96UL*sig_cnt + 12UL*oc_cnt + 8UL*txn_cnt + msg_bytes;
+  unsigned long whole = s->in_msgs + msg_bytes;
+  if( whole - used <= SLOT_ONE_COPY_SLACK ) {
+    TCHK( hipMemcpyAsync( s->d_in, s->h_in, whole ? whole : 1UL, hipMemcpyHostToDevice, st ), "H2D batch" );
+    return FD_ED25519_HIP_OK;
+  }
+  if( msg_bytes ) TCHK( hipMemcpyAsync( s->d_msgs, p->msgs, msg_bytes, hipMemcpyHostToDevice, st ), "H2D msgs" );
+  if( oc_cnt ) {
+    TCHK( hipMemcpyAsync( s->d_off, p->msg_off, 8UL*oc_cnt, hipMemcpyHostToDevice, st ), "H2D off" );
+    TCHK( hipMemcpyAsync( s->d_sz,  p->msg_sz,  4UL*oc_cnt, hipMemcpyHostToDevice, st ), "H2D sz" );
+  }
+  if( sig_cnt ) {
+    TCHK( hipMemcpyAsync( s->d_sigs, p->sigs, 64UL*sig_cnt, hipMemcpyHostToDevice, st ), "H2D sigs" );
+    TCHK( hipMemcpyAsync( s->d_pubs, p->pubs, 32UL*sig_cnt, hipMemcpyHostToDevice, st ), "H2D pubs" );
+  }
+  if( txn_cnt ) {
+    TCHK( hipMemcpyAsync( s->d_tfirst, p->txn_first,   4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tfirst" );
+    TCHK( hipMemcpyAsync( s->d_tcnt,   p->txn_sig_cnt, 4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tcnt" );
+  }
+  return FD_ED25519_HIP_OK;
+}
+
+/* D2H of the codes: [sig_out | txn_out] in one copy when transactions are
+   combined (txn_out sits after sig_cap signature codes), else sig_out */
+static int
+slot_d2h( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt ) {
+  unsigned long n = txn_cnt ? s->pub.sig_cap + txn_cnt : sig_cnt;
+  if( n ) TCHK( hipMemcpyAsync( s->h_outb, s->d_outb, n, hipMemcpyDeviceToHost, st ), "D2H codes" );
+  return FD_ED25519_HIP_OK;
+}
+
 fd_ed25519_hip_slot_t *
 fd_ed25519_hip_pipe_acquire( fd_ed25519_hip_pipe_t * pipe ) {
   pipe_slot_t * s = &pipe->slot[ pipe->next_acq % pipe->slot_cnt ];
@@ -182,24 +235,18 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   slot->sig_cnt = sig_cnt; slot->msg_bytes = msg_bytes; slot->txn_cnt = txn_cnt;
   slot->seq = pipe->seq++;
   slot->t_submit = now_s();
+  int err = slot_h2d( s, st, sig_cnt, txn_cnt, msg_bytes );
+  if( err ) return err;
   if( sig_cnt ) {
-    TCHK( hipMemcpyAsync( s->d_msgs, slot->msgs,    msg_bytes ? msg_bytes : 1UL, hipMemcpyHostToDevice, st ), "H2D msgs" );
-    TCHK( hipMemcpyAsync( s->d_off,  slot->msg_off, 8UL*sig_cnt,  hipMemcpyHostToDevice, st ), "H2D off" );
-    TCHK( hipMemcpyAsync( s->d_sz,   slot->msg_sz,  4UL*sig_cnt,  hipMemcpyHostToDevice, st ), "H2D sz" );
-    TCHK( hipMemcpyAsync( s->d_sigs, slot->sigs,    64UL*sig_cnt, hipMemcpyHostToDevice, st ), "H2D sigs" );
-    TCHK( hipMemcpyAsync( s->d_pubs, slot->pubs,    32UL*sig_cnt, hipMemcpyHostToDevice, st ), "H2D pubs" );
-    int err = fd_ed25519_hip_verify_dev( s->eng, sig_cnt, s->d_msgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs,
-                                         s->d_out, st );
+    err = fd_ed25519_hip_verify_dev( s->eng, sig_cnt, s->d_msgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
     if( err ) return err;
   }
   if( txn_cnt ) {
-    TCHK( hipMemcpyAsync( s->d_tfirst, slot->txn_first,   4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tfirst" );
-    TCHK( hipMemcpyAsync( s->d_tcnt,   slot->txn_sig_cnt, 4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tcnt" );
-    int err = fd_ed25519_hip_txn_combine_dev( s->eng, txn_cnt, s->d_out, s->d_tfirst, s->d_tcnt, s->d_tout, st );
+    err = fd_ed25519_hip_txn_combine_dev( s->eng, txn_cnt, s->d_out, s->d_tfirst, s->d_tcnt, s->d_tout, st );
     if( err ) return err;
-    TCHK( hipMemcpyAsync( slot->txn_out, s->d_tout, txn_cnt, hipMemcpyDeviceToHost, st ), "D2H tout" );
   }
-  if( sig_cnt ) TCHK( hipMemcpyAsync( slot->sig_out, s->d_out, sig_cnt, hipMemcpyDeviceToHost, st ), "D2H out" );
+  err = slot_d2h( s, st, sig_cnt, txn_cnt );
+  if( err ) return err;
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
   s->state = SLOT_BUSY;
   pipe->in_flight++;
@@ -228,25 +275,26 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
   slot->seq = pipe->seq++;
   slot->t_submit = now_s();
   if( txn_cnt ) {
-    TCHK( hipMemcpyAsync( s->d_msgs,   slot->msgs,        payload_bytes ? payload_bytes : 1UL, hipMemcpyHostToDevice, st ), "H2D payloads" );
-    TCHK( hipMemcpyAsync( s->d_toff,   slot->msg_off,     8UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D toff" );
-    TCHK( hipMemcpyAsync( s->d_tsz,    slot->msg_sz,      4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tsz" );
-    TCHK( hipMemcpyAsync( s->d_tfirst, slot->txn_first,   4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tfirst" );
-    TCHK( hipMemcpyAsync( s->d_tcnt,   slot->txn_sig_cnt, 4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tcnt" );
+    /* the per-transaction offsets / sizes travel in msg_off / msg_sz; the
+       device writes the per-signature ones (and the signatures and keys)
+       into arrays of its own */
+    int err = slot_h2d( s, st, 0UL, txn_cnt, payload_bytes );
+    if( err ) return err;
     fd_ed25519_txn_stage_params_t sp;
-    sp.payloads = s->d_msgs; sp.pay_off = s->d_toff; sp.pay_sz = s->d_tsz; sp.txn_first = s->d_tfirst;
-    sp.txn_cnt = s->d_tcnt; sp.ntxn = txn_cnt; sp.sigs = s->d_sigs; sp.pubs = s->d_pubs; sp.msg_off = s->d_off;
-    sp.msg_sz = s->d_sz; sp.parse_ok = s->d_pok;
-    int err = fd_ed25519_hip_launch_txn_stage( &sp, st );
+    sp.payloads = s->d_msgs; sp.pay_off = s->d_off; sp.pay_sz = s->d_sz; sp.txn_first = s->d_tfirst;
+    sp.txn_cnt = s->d_tcnt; sp.ntxn = txn_cnt; sp.sigs = s->d_sigs; sp.pubs = s->d_pubs; sp.msg_off = s->d_soff;
+    sp.msg_sz = s->d_ssz; sp.parse_ok = s->d_pok;
+    err = fd_ed25519_hip_launch_txn_stage( &sp, st );
     if( err ) return tile_fail( "txn_stage launch", (hipError_t)err );
     if( slots ) {
-      err = fd_ed25519_hip_verify_dev( s->eng, slots, s->d_msgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
+      err = fd_ed25519_hip_verify_dev( s->eng, slots, s->d_msgs, s->d_soff, s->d_ssz, s->d_sigs, s->d_pubs, s->d_out,
+                                       st );
       if( err ) return err;
     }
     err = fd_ed25519_hip_launch_txn_finish( s->d_out, s->d_tfirst, s->d_tcnt, s->d_pok, s->d_tout, txn_cnt, st );
     if( err ) return tile_fail( "txn_finish launch", (hipError_t)err );
-    TCHK( hipMemcpyAsync( slot->txn_out, s->d_tout, txn_cnt, hipMemcpyDeviceToHost, st ), "D2H tout" );
-    if( slots ) TCHK( hipMemcpyAsync( slot->sig_out, s->d_out, slots, hipMemcpyDeviceToHost, st ), "D2H out" );
+    err = slot_d2h( s, st, slots, txn_cnt );
+    if( err ) return err;
   }
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
   s->state = SLOT_BUSY;
