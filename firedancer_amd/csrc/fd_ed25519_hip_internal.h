@@ -101,6 +101,8 @@ typedef struct {
   int              small;          /* small chunk: fused prep kernel, no sort, dsm4 (1: a
                                       quad of lanes per signature) or dsm8 (2: two quads),
                                       full-length items by a scan of hflag          */
+  int              fused;          /* large chunk: hash + scalar and decode in the
+                                      wave-specialised prep kernel                   */
 } fd_ed25519_verify_params_t;
 
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a

@@ -326,13 +326,14 @@ fd_ed25519_scalar_kernel(fd_ed25519_verify_params_t p) {
    gone). */
 __global__ void __launch_bounds__(192) fd_ed25519_prep_kernel(fd_ed25519_verify_params_t p) {
   const uint32_t w = threadIdx.x >> 6;
-  const uint64_t j = (uint64_t)blockIdx.x * 64u + (threadIdx.x & 63u);
-  if (j >= p.n) return;
+  const uint64_t t = (uint64_t)blockIdx.x * 64u + (threadIdx.x & 63u);
+  if (t >= p.n) return;
   if (w == 0) {
+    const uint64_t j = p.perm ? (uint64_t)p.perm[t] : t;   /* hash order (length-sorted) */
     hash_one(p, j);
     scalar_one(p, j);
   } else {
-    decode_one(p, (int)w - 1, j);
+    decode_one(p, (int)w - 1, t);
   }
 }
 
@@ -1045,6 +1046,19 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
       break;
     }
     const dim3 g((uint32_t)((p->n + blk - 1) / blk));
+    if (p->fused) {
+      if (p->perm) {
+        const hipError_t e = hipMemsetAsync(p->hist, 0, 2 * FD_ED25519_SORT_BUCKETS * sizeof(uint32_t), st);
+        if (e != hipSuccess) return (int)e;
+        hipLaunchKernelGGL(fd_ed25519_sort_hist_kernel, g, dim3(blk), 0, st, *p);
+        hipLaunchKernelGGL(fd_ed25519_sort_scan_kernel, dim3(1), dim3(64), 0, st, *p);
+        hipLaunchKernelGGL(fd_ed25519_sort_scatter_kernel, g, dim3(blk), 0, st, *p);
+      }
+      const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 2 * sizeof(uint32_t), st);
+      if (e != hipSuccess) return (int)e;
+      hipLaunchKernelGGL(fd_ed25519_prep_kernel, dim3((uint32_t)((p->n + 63) / 64)), dim3(192), 0, st, *p);
+      break;
+    }
     if (p->perm) {
       const hipError_t e = hipMemsetAsync(p->hist, 0, 2 * FD_ED25519_SORT_BUCKETS * sizeof(uint32_t), st);
       if (e != hipSuccess) return (int)e;
@@ -1055,14 +1069,14 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
     hipLaunchKernelGGL(fd_ed25519_hash_kernel, g, dim3(blk), 0, st, *p);
   } break;
   case FD_ED25519_PHASE_SCALAR: {
-    if (p->small) break;   /* in the prep kernel */
+    if (p->small || p->fused) break;   /* in the prep kernel */
     /* fix_cnt and the dsm work counter, adjacent words */
     const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 2 * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(fd_ed25519_scalar_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
   } break;
   case FD_ED25519_PHASE_DECODE:
-    if (p->small) break;   /* in the prep kernel */
+    if (p->small || p->fused) break;   /* in the prep kernel */
     hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((2 * p->n + blk - 1) / blk)), dim3(blk), 0, st,
                        *p);
     break;
