@@ -201,6 +201,44 @@ __global__ void k_mix_mad_add(uint64_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+
+// 32-bit ops used by SHA-512, the DPP exchanges and the carry chains
+#define UB_K32(NAME, ASM)                                                        \
+__global__ void NAME(uint64_t* out, uint32_t seed) {                               \
+  uint32_t a = threadIdx.x + seed, b = seed * 3;                                   \
+  uint32_t acc[NCHAIN];                                                            \
+  _Pragma("unroll") for (int i = 0; i < NCHAIN; i++) acc[i] = a + i;                \
+  for (int it = 0; it < ITERS; it++) {                                             \
+    _Pragma("unroll") for (int i = 0; i < NCHAIN; i++)                             \
+      asm volatile(ASM : "+v"(acc[i]) : "v"(a), "v"(b));                           \
+  }                                                                                \
+  uint32_t s = 0;                                                                  \
+  _Pragma("unroll") for (int i = 0; i < NCHAIN; i++) s ^= acc[i];                  \
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                  \
+}
+UB_K32(k_alignbit, "v_alignbit_b32 %0, %0, %1, %2")
+UB_K32(k_bitop3, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96")
+UB_K32(k_xor, "v_xor_b32 %0, %0, %1")
+UB_K32(k_lshl_add_u32, "v_lshl_add_u32 %0, %0, 3, %1")
+UB_K32(k_dpp_qp, "v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+UB_K32(k_cndmask, "v_cndmask_b32_e64 %0, %0, %1, s[0:1]")
+
+// 64-bit arithmetic shift (the carry extraction)
+__global__ void k_ashr_i64(uint64_t* out, uint32_t seed) {
+  int64_t a = threadIdx.x + seed;
+  int64_t acc[NCHAIN];
+#pragma unroll
+  for (int i = 0; i < NCHAIN; i++) acc[i] = a + i;
+  for (int it = 0; it < ITERS; it++) {
+#pragma unroll
+    for (int i = 0; i < NCHAIN; i++) asm volatile("v_ashrrev_i64 %0, 1, %0" : "+v"(acc[i]));
+  }
+  int64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < NCHAIN; i++) s ^= acc[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)s;
+}
+
 typedef void (*kfn)(uint64_t*, uint32_t);
 
 int main() {
@@ -225,6 +263,13 @@ int main() {
       {"v_fma_f64", k_fma_f64, 1},
       {"v_fma_f32", k_fma_f32, 1},
       {"mad_u64+2add", k_mix_mad_add, 3},
+      {"v_alignbit_b32", k_alignbit, 1},
+      {"v_bitop3_b32", k_bitop3, 1},
+      {"v_xor_b32", k_xor, 1},
+      {"v_lshl_add_u32", k_lshl_add_u32, 1},
+      {"v_mov_b32_dpp", k_dpp_qp, 1},
+      {"v_cndmask_b32", k_cndmask, 1},
+      {"v_ashrrev_i64", k_ashr_i64, 1},
   };
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
