@@ -171,6 +171,16 @@ def test_dsm_form_by_size(fd, oracle, monkeypatch):
     e.close()
 
 
+def test_fused_prep_large_chunks(fd, oracle, monkeypatch):
+    """$FD_ED25519_HIP_FUSED=1 (A/B path): the wave-specialised prep kernel
+    with the length sort for one-lane-per-signature chunks."""
+    monkeypatch.setenv("FD_ED25519_HIP_FUSED", "1")
+    e = fd.Engine(0, max_chunk=1 << 12, dsm="wide")
+    d = _random_set(oracle, 1500, seed=18)
+    _check(_run(e, d), oracle_many(oracle, d, 0))
+    e.close()
+
+
 def test_empty_batch(eng):
     out = eng.verify_host(np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
                           np.zeros((0, 64), np.uint8), np.zeros((0, 32), np.uint8))
