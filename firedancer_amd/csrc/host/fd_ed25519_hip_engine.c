@@ -48,17 +48,26 @@ struct fd_ed25519_hip_engine {
   int32_t *    d_btab;
   int32_t *    d_btab16;     /* [0..2^15]B, the verify kernels' wide B table  */
   int32_t *    btab20[2];    /* shared per device: [0..2^20)B, [0..2^20)[2^132]B */
-  void *       d_atab;
-  uint8_t *    d_work;       /* one allocation carved into the work arrays */
-  uint32_t *   d_k;
-  uint8_t *    d_sflag;
-  uint8_t *    d_pflag;
-  int32_t *    d_pts;
-  uint32_t *   d_fix;        /* scalar -> dsm full-length list */
-  uint32_t *   d_hs;         /* half-size scalars             */
-  uint8_t *    d_hflag;
-  uint32_t *   d_perm;       /* hash order (length-sorted) */
-  uint32_t *   d_hist;       /* counting-sort scratch      */
+  /* work sets: the per-chunk scratch of one chunk in flight.  Set 1 and
+     stream2 exist only with `dual`: a large batch then runs as two chunks,
+     one per (stream, work set), whose kernels overlap on the device (one
+     chunk's phase tails fill with the other's work). */
+  struct {
+    void *     d_atab;       /* dsm lane tables (and the dsm4 quad tables)  */
+    uint8_t *  d_work;       /* one allocation carved into the work arrays */
+    uint32_t * d_k;
+    uint8_t *  d_sflag;
+    uint8_t *  d_pflag;
+    int32_t *  d_pts;
+    uint32_t * d_fix;        /* scalar -> dsm full-length list */
+    uint32_t * d_hs;         /* half-size scalars             */
+    uint8_t *  d_hflag;
+    uint32_t * d_perm;       /* hash order (length-sorted) */
+    uint32_t * d_hist;       /* counting-sort scratch      */
+  } ws[2];
+  int          dual;
+  hipStream_t  stream2;
+  hipEvent_t   ev_fork, ev_join;
   int          sort;         /* sort the hash phase by SHA-512 block count */
 
   /* host-API staging (pinned host + device mirrors), grown on demand */
@@ -179,7 +188,9 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   if( !e ) return;
   hipSetDevice( e->device );
   if( e->stream ) hipStreamSynchronize( e->stream );
-  hipFree( e->d_btab ); hipFree( e->d_btab16 ); hipFree( e->d_atab ); hipFree( e->d_work );
+  if( e->stream2 ) hipStreamSynchronize( e->stream2 );
+  hipFree( e->d_btab ); hipFree( e->d_btab16 );
+  for( int i=0; i<2; i++ ) { hipFree( e->ws[i].d_atab ); hipFree( e->ws[i].d_work ); }
   if( e->btab20[0] ) btab20_release( e->device );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
@@ -189,6 +200,10 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   if( e->tm_ev_init )
     for( int i=0; i<FD_ED25519_HIP_TIMING_MAX; i++ )
       for( int j=0; j<=FD_ED25519_PHASE_CNT; j++ ) hipEventDestroy( e->tm_ev[i][j] );
+  if( e->stream2 ) {
+    hipEventDestroy( e->ev_fork ); hipEventDestroy( e->ev_join );
+    hipStreamDestroy( e->stream2 );
+  }
   if( e->stream ) hipStreamDestroy( e->stream );
   free( e );
 }
@@ -227,21 +242,32 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   size_t work_sz = (size_t)e->max_chunk * FD_ED25519_WORK_BYTES_PER_SIG + 1024;
   HIPCHK( hipMalloc( (void **)&e->d_btab, btab_sz ), "hipMalloc(btab)" );
   HIPCHK( hipMalloc( (void **)&e->d_btab16, btab16_sz ), "hipMalloc(btab16)" );
-  HIPCHK( hipMalloc( &e->d_atab, atab_sz ), "hipMalloc(atab)" );
-  HIPCHK( hipMalloc( (void **)&e->d_work, work_sz ), "hipMalloc(work)" );
-  e->device_bytes = btab_sz + btab16_sz + atab_sz + work_sz;   /* + 2 x 128 MB shared per device */
-  uint64_t c = e->max_chunk;
-  uint8_t * w = e->d_work;
-  e->d_k     = (uint32_t *)w; w += 8UL*4UL*c;
-  e->d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
-  e->d_hs    = (uint32_t *)w; w += 19UL*4UL*c;
-  e->d_perm  = (uint32_t *)w; w += 4UL*c;
-  e->d_fix   = (uint32_t *)w; w += 4UL*c;
-  e->d_sflag = w;             w += c;
-  e->d_pflag = w;             w += 2UL*c;
-  e->d_hflag = w;             w += c;
-  w = (uint8_t *)(((uintptr_t)w + 255UL) & ~(uintptr_t)255UL);
-  e->d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words + fix count inside the 1024-byte slack */
+  char const * ds = getenv( "FD_ED25519_HIP_DUAL" );
+  e->dual = ds ? ds[0]=='1' : FD_ED25519_HIP_DUAL_DEFAULT;
+  if( flags & FD_ED25519_HIP_FLAG_SINGLE ) e->dual = 0;
+  int nws = e->dual ? 2 : 1;
+  e->device_bytes = btab_sz + btab16_sz + (size_t)nws * (atab_sz + work_sz);   /* + 2 x 128 MB shared per device */
+  for( int i=0; i<nws; i++ ) {
+    HIPCHK( hipMalloc( &e->ws[i].d_atab, atab_sz ), "hipMalloc(atab)" );
+    HIPCHK( hipMalloc( (void **)&e->ws[i].d_work, work_sz ), "hipMalloc(work)" );
+    uint64_t c = e->max_chunk;
+    uint8_t * w = e->ws[i].d_work;
+    e->ws[i].d_k     = (uint32_t *)w; w += 8UL*4UL*c;
+    e->ws[i].d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
+    e->ws[i].d_hs    = (uint32_t *)w; w += 19UL*4UL*c;
+    e->ws[i].d_perm  = (uint32_t *)w; w += 4UL*c;
+    e->ws[i].d_fix   = (uint32_t *)w; w += 4UL*c;
+    e->ws[i].d_sflag = w;             w += c;
+    e->ws[i].d_pflag = w;             w += 2UL*c;
+    e->ws[i].d_hflag = w;             w += c;
+    w = (uint8_t *)(((uintptr_t)w + 255UL) & ~(uintptr_t)255UL);
+    e->ws[i].d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words + fix count inside the 1024-byte slack */
+  }
+  if( e->dual ) {
+    HIPCHK( hipStreamCreateWithFlags( &e->stream2, hipStreamNonBlocking ), "hipStreamCreate" );
+    HIPCHK( hipEventCreateWithFlags( &e->ev_fork, hipEventDisableTiming ), "hipEventCreate" );
+    HIPCHK( hipEventCreateWithFlags( &e->ev_join, hipEventDisableTiming ), "hipEventCreate" );
+  }
   char const * ns = getenv( "FD_ED25519_HIP_NOSORT" );
   e->sort = !(ns && ns[0]=='1');
   /* dsm4 (a quad of lanes per signature) below the size where one lane
@@ -349,32 +375,52 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   memset( &p, 0, sizeof(p) );
   p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz;
   p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
-  p.k = e->d_k; p.sflag = e->d_sflag; p.pflag = e->d_pflag; p.pts = e->d_pts; p.cap = e->max_chunk;
-  p.fix_list = e->d_fix; p.fix_cnt = e->d_hist + 2*FD_ED25519_SORT_BUCKETS;
-  p.work_ctr = p.fix_cnt + 1; p.hs = e->d_hs; p.hflag = e->d_hflag;
-  p.perm = e->sort ? e->d_perm : NULL; p.hist = e->d_hist;
-  p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab20 = e->btab20[0]; p.btab20b = e->btab20[1]; p.atab = e->d_atab;
+  p.cap = e->max_chunk;
+  p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab20 = e->btab20[0]; p.btab20b = e->btab20[1];
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   p.half_dbits     = engine_half_dbits( e );
-  for( uint64_t base=0UL; base<n; base+=e->max_chunk ) {
+  /* dual: chunks alternate between (st, set 0) and (stream2, set 1); at
+     least two chunks, each above the small-chunk size */
+  uint64_t chunk = e->max_chunk;
+  int dual = 0;
+  if( e->dual && !e->timing && (n+1UL)/2UL > e->quad_max ) {
+    dual = 1;
+    if( (n+1UL)/2UL < chunk ) chunk = (n+1UL)/2UL;
+  }
+  if( dual ) {
+    HIPCHK( hipEventRecord( e->ev_fork, st ), "hipEventRecord" );
+    HIPCHK( hipStreamWaitEvent( e->stream2, e->ev_fork, 0 ), "hipStreamWaitEvent" );
+  }
+  uint64_t ci = 0UL;
+  for( uint64_t base=0UL; base<n; base+=chunk, ci++ ) {
+    int          wi = dual ? (int)(ci & 1UL) : 0;
+    hipStream_t  cs = wi ? e->stream2 : st;
+    p.k = e->ws[wi].d_k; p.sflag = e->ws[wi].d_sflag; p.pflag = e->ws[wi].d_pflag; p.pts = e->ws[wi].d_pts;
+    p.fix_list = e->ws[wi].d_fix; p.fix_cnt = e->ws[wi].d_hist + 2*FD_ED25519_SORT_BUCKETS;
+    p.work_ctr = p.fix_cnt + 1; p.hs = e->ws[wi].d_hs; p.hflag = e->ws[wi].d_hflag;
+    p.hist = e->ws[wi].d_hist; p.atab = e->ws[wi].d_atab;
     p.base = base;
-    p.n    = (n-base) < e->max_chunk ? (n-base) : e->max_chunk;
+    p.n    = (n-base) < chunk ? (n-base) : chunk;
     p.small = p.n > e->quad_max ? 0 : (p.n <= e->oct_max ? 2 : 1);
     p.fused = e->fused;
-    p.perm  = (e->sort && !p.small) ? e->d_perm : NULL;
+    p.perm  = (e->sort && !p.small) ? e->ws[wi].d_perm : NULL;
     if( e->timing && e->tm_cnt<FD_ED25519_HIP_TIMING_MAX ) {
       /* events bracket each phase kernel on the stream it runs on */
       hipEvent_t * ev = e->tm_ev[ e->tm_cnt++ ];
-      HIPCHK( hipEventRecord( ev[0], st ), "hipEventRecord" );
+      HIPCHK( hipEventRecord( ev[0], cs ), "hipEventRecord" );
       for( int ph=0; ph<FD_ED25519_PHASE_CNT; ph++ ) {
-        int err = fd_ed25519_hip_launch_phase( &p, ph, e->dsm_grid, st );
+        int err = fd_ed25519_hip_launch_phase( &p, ph, e->dsm_grid, cs );
         if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-        HIPCHK( hipEventRecord( ev[ph+1], st ), "hipEventRecord" );
+        HIPCHK( hipEventRecord( ev[ph+1], cs ), "hipEventRecord" );
       }
     } else {
-      int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, st );
+      int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, cs );
       if( err ) return hip_fail( (hipError_t)err, "verify launch" );
     }
+  }
+  if( dual ) {
+    HIPCHK( hipEventRecord( e->ev_join, e->stream2 ), "hipEventRecord" );
+    HIPCHK( hipStreamWaitEvent( st, e->ev_join, 0 ), "hipStreamWaitEvent" );
   }
   return FD_ED25519_HIP_OK;
 }

@@ -100,6 +100,13 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
 #define FD_ED25519_HIP_FLAG_DSM_OCT        (16)
 #define FD_ED25519_HIP_QUAD_MAX_DEFAULT    (32768UL)
 #define FD_ED25519_HIP_OCT_MAX_DEFAULT     (8192UL)
+/* Dual: a batch larger than 2 x FD_ED25519_HIP_QUAD_MAX_DEFAULT runs as two
+   chunks on two streams with their own scratch, so the kernels of one fill
+   the other's phase tails ($FD_ED25519_HIP_DUAL=0/1 overrides the default).
+   Per-phase timing (fd_ed25519_hip_engine_timing) runs the single-stream
+   sequence.  FLAG_SINGLE never allocates the second set. */
+#define FD_ED25519_HIP_FLAG_SINGLE         (32)
+#define FD_ED25519_HIP_DUAL_DEFAULT        (0)
 
 /* Creates an engine on HIP device `device`.  max_chunk is the number of
    signatures processed per kernel sequence (0 = default 1<<20); larger
