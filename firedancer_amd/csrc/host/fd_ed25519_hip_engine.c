@@ -68,6 +68,11 @@ struct fd_ed25519_hip_engine {
   int          dual;
   hipStream_t  stream2;
   hipEvent_t   ev_fork, ev_join;
+  /* overlap: a large chunk's decode (A and R need neither the hash nor the
+     scalars) runs on a side stream beside hash + scalar, dsm after both */
+  int          overlap;
+  hipStream_t  side;
+  hipEvent_t   ev_dfork, ev_djoin;
   int          sort;         /* sort the hash phase by SHA-512 block count */
 
   /* host-API staging (pinned host + device mirrors), grown on demand */
@@ -204,6 +209,11 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
     hipEventDestroy( e->ev_fork ); hipEventDestroy( e->ev_join );
     hipStreamDestroy( e->stream2 );
   }
+  if( e->side ) {
+    hipStreamSynchronize( e->side );
+    hipEventDestroy( e->ev_dfork ); hipEventDestroy( e->ev_djoin );
+    hipStreamDestroy( e->side );
+  }
   if( e->stream ) hipStreamDestroy( e->stream );
   free( e );
 }
@@ -268,6 +278,8 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
     HIPCHK( hipEventCreateWithFlags( &e->ev_fork, hipEventDisableTiming ), "hipEventCreate" );
     HIPCHK( hipEventCreateWithFlags( &e->ev_join, hipEventDisableTiming ), "hipEventCreate" );
   }
+  char const * ovs = getenv( "FD_ED25519_HIP_OVERLAP" );
+  e->overlap = ovs ? ovs[0]=='1' : FD_ED25519_HIP_OVERLAP_DEFAULT;
   char const * ns = getenv( "FD_ED25519_HIP_NOSORT" );
   e->sort = !(ns && ns[0]=='1');
   /* dsm4 (a quad of lanes per signature) below the size where one lane
@@ -413,6 +425,27 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
         if( err ) return hip_fail( (hipError_t)err, "verify launch" );
         HIPCHK( hipEventRecord( ev[ph+1], cs ), "hipEventRecord" );
       }
+    } else if( e->overlap && !dual && !p.small && !p.fused ) {
+      if( !e->side ) {
+        /* created on the first large chunk only: an engine that only sees
+           small batches (a tile slot) keeps to one stream, since the
+           device's few hardware queues are shared by every stream of the
+           process and extra streams serialise the slots */
+        HIPCHK( hipStreamCreateWithFlags( &e->side, hipStreamNonBlocking ), "hipStreamCreate" );
+        HIPCHK( hipEventCreateWithFlags( &e->ev_dfork, hipEventDisableTiming ), "hipEventCreate" );
+        HIPCHK( hipEventCreateWithFlags( &e->ev_djoin, hipEventDisableTiming ), "hipEventCreate" );
+      }
+      HIPCHK( hipEventRecord( e->ev_dfork, cs ), "hipEventRecord" );
+      HIPCHK( hipStreamWaitEvent( e->side, e->ev_dfork, 0 ), "hipStreamWaitEvent" );
+      int err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DECODE, e->dsm_grid, e->side );
+      if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+      HIPCHK( hipEventRecord( e->ev_djoin, e->side ), "hipEventRecord" );
+      err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_HASH, e->dsm_grid, cs );
+      if( !err ) err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_SCALAR, e->dsm_grid, cs );
+      if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+      HIPCHK( hipStreamWaitEvent( cs, e->ev_djoin, 0 ), "hipStreamWaitEvent" );
+      err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, cs );
+      if( err ) return hip_fail( (hipError_t)err, "verify launch" );
     } else {
       int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, cs );
       if( err ) return hip_fail( (hipError_t)err, "verify launch" );
