@@ -66,6 +66,7 @@ struct fd_ed25519_hip_engine {
     uint32_t * d_hist;       /* counting-sort scratch      */
   } ws[2];
   int          dual;
+  int          dual_skew;  /* chunk 1 starts after this many phases of chunk 0 */
   hipStream_t  stream2;
   hipEvent_t   ev_fork, ev_join;
   /* overlap: a large chunk's decode (A and R need neither the hash nor the
@@ -255,6 +256,9 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   char const * ds = getenv( "FD_ED25519_HIP_DUAL" );
   e->dual = ds ? ds[0]=='1' : FD_ED25519_HIP_DUAL_DEFAULT;
   if( flags & FD_ED25519_HIP_FLAG_SINGLE ) e->dual = 0;
+  char const * sks = getenv( "FD_ED25519_HIP_DUAL_SKEW" );
+  e->dual_skew = sks ? atoi( sks ) : 0;
+  if( e->dual_skew<0 || e->dual_skew>=FD_ED25519_PHASE_CNT ) e->dual_skew = 0;
   int nws = e->dual ? 2 : 1;
   e->device_bytes = btab_sz + btab16_sz + (size_t)nws * (atab_sz + work_sz);   /* + 2 x 128 MB shared per device */
   for( int i=0; i<nws; i++ ) {
@@ -399,7 +403,7 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
     dual = 1;
     if( (n+1UL)/2UL < chunk ) chunk = (n+1UL)/2UL;
   }
-  if( dual ) {
+  if( dual && !e->dual_skew ) {
     HIPCHK( hipEventRecord( e->ev_fork, st ), "hipEventRecord" );
     HIPCHK( hipStreamWaitEvent( e->stream2, e->ev_fork, 0 ), "hipStreamWaitEvent" );
   }
@@ -424,6 +428,16 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
         int err = fd_ed25519_hip_launch_phase( &p, ph, e->dsm_grid, cs );
         if( err ) return hip_fail( (hipError_t)err, "verify launch" );
         HIPCHK( hipEventRecord( ev[ph+1], cs ), "hipEventRecord" );
+      }
+    } else if( dual && e->dual_skew && ci==0UL ) {
+      /* skewed start: the second chunk's phases trail the first's */
+      for( int ph=0; ph<FD_ED25519_PHASE_CNT; ph++ ) {
+        if( ph==e->dual_skew ) {
+          HIPCHK( hipEventRecord( e->ev_fork, cs ), "hipEventRecord" );
+          HIPCHK( hipStreamWaitEvent( e->stream2, e->ev_fork, 0 ), "hipStreamWaitEvent" );
+        }
+        int err = fd_ed25519_hip_launch_phase( &p, ph, e->dsm_grid, cs );
+        if( err ) return hip_fail( (hipError_t)err, "verify launch" );
       }
     } else if( e->overlap && !dual && !p.small && !p.fused ) {
       if( !e->side ) {
