@@ -103,11 +103,18 @@ typedef struct {
                                       full-length items by a scan of hflag          */
   int              fused;          /* large chunk: hash + scalar and decode in the
                                       wave-specialised prep kernel                   */
+  uint64_t         tail;           /* large chunk: the dsm kernel leaves the last `tail`
+                                      half-size items to a dsm4 launch that fills its
+                                      drain (0: none)                                 */
+  uint64_t         qbase;          /* dsm4: first item (0, or n - tail for the drain) */
 } fd_ed25519_verify_params_t;
 
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a
    hipError_t value (0 on success). */
 int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
+/* dsm4 over items [p->qbase, p->n) of a large chunk (the drain of the dsm
+   kernel when p->tail > 0; p->atab: the drain's own quad tables) */
+int fd_ed25519_hip_launch_dsm4( fd_ed25519_verify_params_t const * p, void * stream );
 int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, int base_doublings, void * stream );
 /* [0..2^20)[2^base_doublings]B into d_tab; d_scratch holds
    FD_ED25519_BTAB20_ENTRIES*10 + 40 int32 */

@@ -591,7 +591,7 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   }
   const uint64_t nfix = *p.fix_cnt;
   const uint64_t nfix64 = (nfix + 63u) & ~(uint64_t)63u;
-  const uint64_t total = nfix64 + p.n;
+  const uint64_t total = nfix64 + p.n - p.tail;   /* the last `tail` items: the dsm4 drain */
   for (;;) {
     uint32_t b = 0u;
     if (lane == 0u) b = atomicAdd(p.work_ctr, 64u);
@@ -675,7 +675,7 @@ FD_DEV void table4_build(int4* tab, const fe& x, const fe& y, bool negate, const
 
 __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_params_t p) {
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t j = gid >> 2;   /* a quad per signature: all four lanes take the same branches */
+  const uint64_t j = (gid >> 2) + p.qbase;   /* a quad per signature: all four lanes take the same branches */
   if (j >= p.n) return;
   const uint32_t hf = p.hflag[j];
   if (hf & FD_HF_FULL) return;
@@ -1102,6 +1102,13 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
   default:
     return (int)hipErrorInvalidValue;
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int fd_ed25519_hip_launch_dsm4(const fd_ed25519_verify_params_t* p, void* stream) {
+  if (p->qbase >= p->n) return 0;
+  hipLaunchKernelGGL(fd_ed25519_dsm4_kernel, dim3((uint32_t)((4 * (p->n - p->qbase) + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, *p);
   return (int)hipGetLastError();
 }
 

@@ -73,7 +73,12 @@ struct fd_ed25519_hip_engine {
      scalars) runs on a side stream beside hash + scalar, dsm after both */
   int          overlap;
   hipStream_t  side;
-  hipEvent_t   ev_dfork, ev_djoin;
+  hipEvent_t   ev_dfork, ev_djoin, ev_sjoin;
+  /* drain: with the overlap, the last `tail` items of a large chunk go to a
+     dsm4 launch on the (low-priority) side stream, whose blocks take the
+     slots the persistent dsm kernel's waves free as its work runs out */
+  uint64_t     tail;
+  void *       d_qtab;     /* the drain's quad tables, tail x 4 lanes */
   int          sort;         /* sort the hash phase by SHA-512 block count */
 
   /* host-API staging (pinned host + device mirrors), grown on demand */
@@ -197,6 +202,7 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   if( e->stream2 ) hipStreamSynchronize( e->stream2 );
   hipFree( e->d_btab ); hipFree( e->d_btab16 );
   for( int i=0; i<2; i++ ) { hipFree( e->ws[i].d_atab ); hipFree( e->ws[i].d_work ); }
+  hipFree( e->d_qtab );
   if( e->btab20[0] ) btab20_release( e->device );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
@@ -212,7 +218,7 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   }
   if( e->side ) {
     hipStreamSynchronize( e->side );
-    hipEventDestroy( e->ev_dfork ); hipEventDestroy( e->ev_djoin );
+    hipEventDestroy( e->ev_dfork ); hipEventDestroy( e->ev_djoin ); hipEventDestroy( e->ev_sjoin );
     hipStreamDestroy( e->side );
   }
   if( e->stream ) hipStreamDestroy( e->stream );
@@ -284,6 +290,13 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   }
   char const * ovs = getenv( "FD_ED25519_HIP_OVERLAP" );
   e->overlap = ovs ? ovs[0]=='1' : FD_ED25519_HIP_OVERLAP_DEFAULT;
+  char const * tls = getenv( "FD_ED25519_HIP_TAIL" );
+  e->tail = tls ? strtoul( tls, NULL, 0 ) : FD_ED25519_HIP_TAIL_DEFAULT;
+  if( !e->overlap ) e->tail = 0UL;
+  if( e->tail ) {
+    HIPCHK( hipMalloc( &e->d_qtab, e->tail * 4UL * FD_ED25519_QUAD_LANE_BYTES ), "hipMalloc(qtab)" );
+    e->device_bytes += e->tail * 4UL * FD_ED25519_QUAD_LANE_BYTES;
+  }
   char const * ns = getenv( "FD_ED25519_HIP_NOSORT" );
   e->sort = !(ns && ns[0]=='1');
   /* dsm4 (a quad of lanes per signature) below the size where one lane
@@ -445,10 +458,15 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
            small batches (a tile slot) keeps to one stream, since the
            device's few hardware queues are shared by every stream of the
            process and extra streams serialise the slots */
-        HIPCHK( hipStreamCreateWithFlags( &e->side, hipStreamNonBlocking ), "hipStreamCreate" );
+        int least = 0, greatest = 0;
+        HIPCHK( hipDeviceGetStreamPriorityRange( &least, &greatest ), "hipDeviceGetStreamPriorityRange" );
+        HIPCHK( hipStreamCreateWithPriority( &e->side, hipStreamNonBlocking, e->tail ? least : 0 ),
+                "hipStreamCreate" );
         HIPCHK( hipEventCreateWithFlags( &e->ev_dfork, hipEventDisableTiming ), "hipEventCreate" );
         HIPCHK( hipEventCreateWithFlags( &e->ev_djoin, hipEventDisableTiming ), "hipEventCreate" );
+        HIPCHK( hipEventCreateWithFlags( &e->ev_sjoin, hipEventDisableTiming ), "hipEventCreate" );
       }
+      uint64_t tail = (e->tail && p.n > 4UL*e->tail) ? e->tail : 0UL;
       HIPCHK( hipEventRecord( e->ev_dfork, cs ), "hipEventRecord" );
       HIPCHK( hipStreamWaitEvent( e->side, e->ev_dfork, 0 ), "hipStreamWaitEvent" );
       int err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DECODE, e->dsm_grid, e->side );
@@ -458,8 +476,23 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
       if( !err ) err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_SCALAR, e->dsm_grid, cs );
       if( err ) return hip_fail( (hipError_t)err, "verify launch" );
       HIPCHK( hipStreamWaitEvent( cs, e->ev_djoin, 0 ), "hipStreamWaitEvent" );
+      if( tail ) {
+        HIPCHK( hipEventRecord( e->ev_sjoin, cs ), "hipEventRecord" );
+        HIPCHK( hipStreamWaitEvent( e->side, e->ev_sjoin, 0 ), "hipStreamWaitEvent" );
+      }
+      p.tail = tail;
       err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, cs );
       if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+      if( tail ) {
+        fd_ed25519_verify_params_t q = p;
+        q.atab  = e->d_qtab;
+        q.qbase = p.n - tail;
+        err = fd_ed25519_hip_launch_dsm4( &q, e->side );
+        if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+        HIPCHK( hipEventRecord( e->ev_djoin, e->side ), "hipEventRecord" );
+        HIPCHK( hipStreamWaitEvent( cs, e->ev_djoin, 0 ), "hipStreamWaitEvent" );
+      }
+      p.tail = 0UL;
     } else {
       int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, cs );
       if( err ) return hip_fail( (hipError_t)err, "verify launch" );

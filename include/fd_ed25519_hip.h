@@ -112,6 +112,10 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    after both: +1% at 1M, measured.  Per-phase timing runs the phases in
    sequence.  ($FD_ED25519_HIP_OVERLAP=0/1 overrides.) */
 #define FD_ED25519_HIP_OVERLAP_DEFAULT     (1)
+/* Drain (with the overlap): the last $FD_ED25519_HIP_TAIL signatures of a
+   large chunk are verified a quad of lanes per signature on the side stream,
+   in the slots the one-lane dsm kernel frees as its work runs out. */
+#define FD_ED25519_HIP_TAIL_DEFAULT        (0UL)
 
 /* Creates an engine on HIP device `device`.  max_chunk is the number of
    signatures processed per kernel sequence (0 = default 1<<20); larger
