@@ -181,6 +181,30 @@ def test_fused_prep_large_chunks(fd, oracle, monkeypatch):
     e.close()
 
 
+@pytest.mark.parametrize("env", [
+    {"FD_ED25519_HIP_OVERLAP": "0"},
+    {"FD_ED25519_HIP_DUAL": "1"},
+    {"FD_ED25519_HIP_DUAL": "1", "FD_ED25519_HIP_DUAL_SKEW": "1"},
+    {"FD_ED25519_HIP_DUAL": "1", "FD_ED25519_HIP_DUAL_SKEW": "3"},
+    {"FD_ED25519_HIP_TAIL": "200"},
+], ids=["sequential", "dual", "dual-skew1", "dual-skew3", "drain"])
+def test_launch_options_large_chunks(fd, oracle, monkeypatch, env):
+    """The engine's launch options for one-lane-per-signature chunks (the
+    small-chunk threshold lowered so the batches stay small): phases in
+    sequence on one stream, two chunks on two streams with their own
+    scratch (optionally the second started behind the first), and the dsm4
+    drain of a chunk's last items on the side stream -- each against the
+    oracle, over a batch of two chunks."""
+    monkeypatch.setenv("FD_ED25519_HIP_QUAD_MAX", "300")
+    monkeypatch.setenv("FD_ED25519_HIP_OCT_MAX", "100")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = fd.Engine(0, max_chunk=1000)
+    d = _random_set(oracle, 1700, seed=19)
+    _check(_run(e, d), oracle_many(oracle, d, 0))
+    e.close()
+
+
 def test_empty_batch(eng):
     out = eng.verify_host(np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
                           np.zeros((0, 64), np.uint8), np.zeros((0, 32), np.uint8))
