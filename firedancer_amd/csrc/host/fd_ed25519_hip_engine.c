@@ -460,8 +460,11 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
            process and extra streams serialise the slots */
         int least = 0, greatest = 0;
         HIPCHK( hipDeviceGetStreamPriorityRange( &least, &greatest ), "hipDeviceGetStreamPriorityRange" );
-        HIPCHK( hipStreamCreateWithPriority( &e->side, hipStreamNonBlocking, e->tail ? least : 0 ),
-                "hipStreamCreate" );
+        int prio = e->tail ? least : 0;
+        char const * ps = getenv( "FD_ED25519_HIP_SIDE_PRIO" );   /* A/B: "high" | "low" */
+        if( ps && !strcmp( ps, "high" ) ) prio = greatest;
+        if( ps && !strcmp( ps, "low"  ) ) prio = least;
+        HIPCHK( hipStreamCreateWithPriority( &e->side, hipStreamNonBlocking, prio ), "hipStreamCreate" );
         HIPCHK( hipEventCreateWithFlags( &e->ev_dfork, hipEventDisableTiming ), "hipEventCreate" );
         HIPCHK( hipEventCreateWithFlags( &e->ev_djoin, hipEventDisableTiming ), "hipEventCreate" );
         HIPCHK( hipEventCreateWithFlags( &e->ev_sjoin, hipEventDisableTiming ), "hipEventCreate" );

@@ -16,7 +16,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from firedancer_amd import ed25519, workload  # noqa: E402
 
-VARS = ("FD_ED25519_HIP_DUAL", "FD_ED25519_HIP_DUAL_SKEW", "FD_ED25519_HIP_OVERLAP", "FD_ED25519_HIP_TAIL")
+VARS = ("FD_ED25519_HIP_DUAL", "FD_ED25519_HIP_DUAL_SKEW", "FD_ED25519_HIP_OVERLAP", "FD_ED25519_HIP_TAIL", "FD_ED25519_HIP_SIDE_PRIO")
 
 
 def run(spec, n, steps, cfg):
