@@ -77,10 +77,15 @@ __global__ void __launch_bounds__(256) fd_ed25519_sort_hist_kernel(fd_ed25519_ve
   if (threadIdx.x < FD_ED25519_SORT_BUCKETS && h[threadIdx.x]) atomicAdd(&p.hist[threadIdx.x], h[threadIdx.x]);
 }
 
+#ifndef FD_ED25519_SORT_DESC
+#define FD_ED25519_SORT_DESC 1   /* longest hashes first: hash 1.05 -> 1.01 ms per 1M */
+#endif
+
 __global__ void fd_ed25519_sort_scan_kernel(fd_ed25519_verify_params_t p) {
   if (threadIdx.x == 0) {
     uint32_t acc = 0;
-    for (int b = 0; b < FD_ED25519_SORT_BUCKETS; b++) {
+    for (int i = 0; i < FD_ED25519_SORT_BUCKETS; i++) {
+      const int b = FD_ED25519_SORT_DESC ? FD_ED25519_SORT_BUCKETS - 1 - i : i;
       p.hist[FD_ED25519_SORT_BUCKETS + b] = acc;  /* cursor = exclusive prefix */
       acc += p.hist[b];
     }
