@@ -87,7 +87,9 @@ typedef struct {
   uint8_t *        hflag;
   uint32_t *       fix_list;
   uint32_t *       fix_cnt;  /* 1 word: entries of fix_list                   */
-  uint32_t *       work_ctr; /* 1 word: dsm items handed out (fix_cnt + 1)    */
+  uint32_t *       work_ctr; /* 1 word: dsm items handed out (fix_cnt + 1); the
+                                next word counts the long-|d| items queued at the
+                                back of fix_list                                 */
   uint32_t *       perm;     /* [cap] hash order (length-sorted), NULL: identity */
   uint32_t *       hist;     /* [2*SORT_BUCKETS] counting-sort scratch          */
   uint64_t         cap;

@@ -53,6 +53,8 @@
 #define FD_PF_SMALL 2u
 #define FD_HF_DNEG  1u   /* hflag: d < 0                        */
 #define FD_HF_FULL  2u   /* hflag: no half-size pair, full form */
+#define FD_HF_LONG  4u   /* hflag: |d| >= 2^131 (more than 33 windows), queued
+                            at the back of fix_list (large chunks)  */
 
 /* ------------------------------------------------------------------------
    Length sort for the hash phase.  A wave runs as many SHA-512 blocks as
@@ -76,6 +78,10 @@ __global__ void __launch_bounds__(256) fd_ed25519_sort_hist_kernel(fd_ed25519_ve
   __syncthreads();
   if (threadIdx.x < FD_ED25519_SORT_BUCKETS && h[threadIdx.x]) atomicAdd(&p.hist[threadIdx.x], h[threadIdx.x]);
 }
+
+#ifndef FD_ED25519_LONG_LIST
+#define FD_ED25519_LONG_LIST 0   /* A/B: no measurable difference (profiles/r1_long_list_ab.txt) */
+#endif
 
 #ifndef FD_ED25519_SORT_DESC
 #define FD_ED25519_SORT_DESC 1   /* longest hashes first: hash 1.05 -> 1.01 ms per 1M */
@@ -309,10 +315,18 @@ FD_DEV void scalar_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
 #pragma unroll
   for (int w = 0; w < 4; w++)
     hs[(uint64_t)(15 + w) * c] = __builtin_amdgcn_alignbit(sp[w + 5], sp[w + 4], 4);  /* bits 132..   */
-  p.hflag[j] = (uint8_t)((dneg ? FD_HF_DNEG : 0u) | (ok ? 0u : FD_HF_FULL));
+  /* large chunks: the ~0.16% with |d| >= 2^131 are gathered into waves of
+     their own (else ~10% of the dsm waves would run extra windows for one
+     lane each) */
+  const bool lng = ok && !p.small && FD_ED25519_LONG_LIST && fd_half_bitlen<FD_HALF_TW>(dm) > 131;
+  p.hflag[j] = (uint8_t)((dneg ? FD_HF_DNEG : 0u) | (ok ? 0u : FD_HF_FULL) | (lng ? FD_HF_LONG : 0u));
   if (!ok && !p.small) {   /* small chunks: the dsm scan finds them by hflag */
     const uint32_t slot = atomicAdd(p.fix_cnt, 1u);
     p.fix_list[slot] = (uint32_t)j;
+  }
+  if (lng) {
+    const uint32_t slot = atomicAdd(p.work_ctr + 1, 1u);
+    p.fix_list[p.cap - 1u - slot] = (uint32_t)j;
   }
 }
 
@@ -596,7 +610,9 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   }
   const uint64_t nfix = *p.fix_cnt;
   const uint64_t nfix64 = (nfix + 63u) & ~(uint64_t)63u;
-  const uint64_t total = nfix64 + p.n - p.tail;   /* the last `tail` items: the dsm4 drain */
+  const uint64_t nlong = p.work_ctr[1];
+  const uint64_t head = nfix64 + ((nlong + 63u) & ~(uint64_t)63u);
+  const uint64_t total = head + p.n - p.tail;   /* the last `tail` items: the dsm4 drain */
   for (;;) {
     uint32_t b = 0u;
     if (lane == 0u) b = atomicAdd(p.work_ctr, 64u);
@@ -606,9 +622,12 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
     if (t < nfix) {
       const uint64_t j = p.fix_list[t];
       p.out[p.base + j] = (int8_t)dsm_full_one(p, j, tabA);
-    } else if (t >= nfix64 && t < total) {
-      const uint64_t j = t - nfix64;
-      if (!(p.hflag[j] & FD_HF_FULL)) p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
+    } else if (t >= nfix64 && t < nfix64 + nlong) {
+      const uint64_t j = p.fix_list[p.cap - 1u - (t - nfix64)];
+      p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
+    } else if (t >= head && t < total) {
+      const uint64_t j = t - head;
+      if (!(p.hflag[j] & (FD_HF_FULL | FD_HF_LONG))) p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
     }
   }
 }
@@ -683,7 +702,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
   const uint64_t j = (gid >> 2) + p.qbase;   /* a quad per signature: all four lanes take the same branches */
   if (j >= p.n) return;
   const uint32_t hf = p.hflag[j];
-  if (hf & FD_HF_FULL) return;
+  if (hf & (FD_HF_FULL | FD_HF_LONG)) return;   /* the dsm kernel's (large-chunk drain) */
   const qmask_t m = quad_masks();
   int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + gid * FD_ED25519_QUAD_LANE_BYTES);
   int4* tabR = tabA + 27;
@@ -771,7 +790,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
   const uint64_t j = gid >> 3;                 /* 8 lanes per signature, the same branches */
   if (j >= p.n) return;
   const uint32_t hf = p.hflag[j];
-  if (hf & FD_HF_FULL) return;
+  if (hf & (FD_HF_FULL | FD_HF_LONG)) return;   /* the dsm kernel's (large-chunk drain) */
   const int half = (int)((threadIdx.x >> 2) & 1u);   /* 0: -A and B, 1: -+R and B' */
   const qmask_t m = quad_masks();
   int4* tab = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + gid * (FD_ED25519_QUAD_LANE_BYTES / 2));
@@ -1059,7 +1078,7 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
         hipLaunchKernelGGL(fd_ed25519_sort_scan_kernel, dim3(1), dim3(64), 0, st, *p);
         hipLaunchKernelGGL(fd_ed25519_sort_scatter_kernel, g, dim3(blk), 0, st, *p);
       }
-      const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 2 * sizeof(uint32_t), st);
+      const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 3 * sizeof(uint32_t), st);
       if (e != hipSuccess) return (int)e;
       hipLaunchKernelGGL(fd_ed25519_prep_kernel, dim3((uint32_t)((p->n + 63) / 64)), dim3(192), 0, st, *p);
       break;
@@ -1075,8 +1094,8 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
   } break;
   case FD_ED25519_PHASE_SCALAR: {
     if (p->small || p->fused) break;   /* in the prep kernel */
-    /* fix_cnt and the dsm work counter, adjacent words */
-    const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 2 * sizeof(uint32_t), st);
+    /* fix_cnt, the dsm work counter and the long-|d| count, adjacent words */
+    const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 3 * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(fd_ed25519_scalar_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
   } break;
