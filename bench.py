@@ -17,6 +17,13 @@ Printed on rank 0 as one JSON line, with:
                 sample of the same workload (rank 0, N=1 only)
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+
+With --gpus N > 1 and no launcher environment (WORLD_SIZE unset), bench.py
+starts its N ranks itself, as child processes created before anything
+touches a GPU (rank r on device r, gloo for the barrier and the
+max-over-ranks); under torchrun it uses the launcher's ranks.  Every rank
+must hold a distinct device (checked by PCI address) unless
+--allow-shared-device is given (a one-GPU rehearsal).
 """
 import argparse
 import ctypes
@@ -37,15 +44,56 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def spawn_ranks(gpus):
+    """--gpus N without a launcher: N child processes of this script, rank r
+    on device r, started before this process touches any GPU; returns the
+    exit code (the worst rank's)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def dist_setup(gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != gpus:
+        log(f"[rank {rank}] --gpus {gpus} but the launcher started {world} ranks")
+        sys.exit(2)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo reports its connections on stdout: keep stdout for the one
+        # JSON line (fd 1 points at stderr while the group forms)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     return rank, local, world
+
+
+def all_gather(obj, world):
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def barrier(world):
@@ -89,7 +137,7 @@ def cpu_baseline(wl, gpu_codes, sample, reps, workload_name="C2"):
     """Reference CPU verify (oracle/_ref) on `sample` signatures of the workload,
     one pthread per core of this process's share.  Also checks the reference's
     verdicts against the GPU's on the sample."""
-    from firedancer_amd import workload  # noqa: F401
+    from firedancer_amd import workload
     ref_dir = os.path.join(REPO, "oracle", "_ref")
     flavour = "avx512" if cpu_has("avx512ifma") and cpu_has("avx512vbmi") else "portable"
     path = os.path.join(ref_dir, f"libfdref_{flavour}.so")
@@ -109,7 +157,7 @@ def cpu_baseline(wl, gpu_codes, sample, reps, workload_name="C2"):
     pubs = wl.pubs.download(np.uint8, 32 * n)
     sz = wl.sizes[:n].astype(np.uint32)
     out = np.zeros(n, np.int8)
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads, cores_src = workload.host_cores()
     ns = lib.fdref_verify_many(n, msgs.ctypes.data, off.ctypes.data, sz.ctypes.data, sigs.ctypes.data,
                                pubs.ctypes.data, out.ctypes.data, threads, reps)
     if ns <= 0:
@@ -118,6 +166,8 @@ def cpu_baseline(wl, gpu_codes, sample, reps, workload_name="C2"):
     return {"value": rate, "unit": "verifies/s", "cores": threads, "kind": kind,
             "sample": f"first {n} signatures of the {workload_name} workload x {reps} passes, fd_ed25519_verify of the "
                       f"reference's {flavour} backend (compiled from its sources), {threads} pthreads",
+            "cores_source": cores_src,
+            "scope": "this process's CPU share of the GPU box (one GPU's lease), not the whole node",
             "seconds": ns * 1e-9, "per_core": rate / threads,
             "verdicts_equal_gpu": bool(np.array_equal(out, gpu_codes[:n]))}
 
@@ -175,6 +225,54 @@ def latency_mode(eng, args, device):
     return out
 
 
+def host_fed(wl, device, world, reps, batch, slots):
+    """The host-fed path: the same C2 signatures from host memory (page-
+    locked, as a deployment registers its dcache once), through the pool's
+    feeder thread: per batch, H2D of the messages' byte range and of
+    msg_off / msg_sz / sigs / pubs, verify, D2H of the codes into the
+    caller's array, `slots` batches in flight.  Reported beside the
+    device-resident value (never as it), with the PCIe bound it is up
+    against: achieved H2D bytes/s, and the H2D rate of a plain pinned
+    copy."""
+    from firedancer_amd import tile
+    n = wl.n
+    msgs = wl.msgs.download(np.uint8, wl.msg_bytes + 16)
+    off = wl.off.download(np.uint64, n)
+    sz = wl.sizes.astype(np.uint32)
+    sigs = wl.sigs.download(np.uint8, 64 * n)
+    pubs = wl.pubs.download(np.uint8, 32 * n)
+    expect = wl.expect.download(np.int8, n)
+    out = np.zeros(n, np.int8)
+    t = time.perf_counter()
+    with tile.HostRegistration(msgs, off, sz, sigs, pubs, out):
+        reg_s = time.perf_counter() - t
+        tile.pool_verify([device], msgs, off, sz, sigs, pubs, batch_sigs=batch, slot_cnt=slots, out=out)  # warm-up
+        barrier(world)
+        t0 = time.perf_counter()
+        st = None
+        for _ in range(reps):
+            _, _, st = tile.pool_verify([device], msgs, off, sz, sigs, pubs, batch_sigs=batch, slot_cnt=slots,
+                                        out=out, stats=True)
+        dt = time.perf_counter() - t0
+        barrier(world)
+    ok = bool(np.array_equal(out, expect))
+    dt_max = allreduce_max(dt, world)
+    ok_all = allreduce_sum(0 if ok else 1, world) == 0
+    h2d = tile.h2d_gbps(device, 256 << 20, 8)
+    bytes_per_sig = st["h2d_bytes"] / n
+    bound = h2d * 1e9 / bytes_per_sig if h2d > 0 else None
+    rate = world * n * reps / dt_max
+    return {"value": rate, "unit": "verifies/s", "per_gpu": rate / world, "n_gpus": world,
+            "signatures_per_pass": n, "passes": reps, "batch_sigs": batch, "slots_in_flight": slots,
+            "h2d_bytes_per_signature": bytes_per_sig, "achieved_h2d_GBps_per_gpu": rate / world * bytes_per_sig / 1e9,
+            "pinned_copy_h2d_GBps": h2d, "pcie_bound_verifies_per_s_per_gpu": bound,
+            "frac_of_pcie_bound": (rate / world / bound) if bound else None,
+            "direct_batches": st["direct_batches"], "staged_batches": st["staged_batches"],
+            "register_seconds": reg_s, "verdicts_match_labels": ok_all,
+            "path": "host SoA (page-locked) -> per-batch H2D (messages as one DMA of their span) -> verify -> "
+                    "D2H codes; fd_ed25519_hip_pool_verify, one feeder thread pinned to the GPU's NUMA node"}
+
+
 def pmc_traffic(n):
     """HBM bytes per dsm launch from the committed PMC summary (rocprofv3
     FETCH_SIZE + WRITE_SIZE passes, tools/pmc_summary.py), scaled to n.
@@ -218,8 +316,15 @@ def main():
     ap.add_argument("--latency-batch", type=int, default=256)
     ap.add_argument("--latency-slots", type=int, default=4)
     ap.add_argument("--latency-txns", type=int, default=100000, help="0 disables the latency mode")
+    ap.add_argument("--host-reps", type=int, default=4, help="host-fed passes (0 disables)")
+    ap.add_argument("--host-batch", type=int, default=131072)
+    ap.add_argument("--host-slots", type=int, default=4)
+    ap.add_argument("--allow-shared-device", action="store_true",
+                    help="let ranks share a GPU (one-GPU rehearsal of --gpus N; n_gpus then counts devices)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus)
     rank, local, world = dist_setup(args.gpus)
     from firedancer_amd import ed25519, workload
 
@@ -228,10 +333,20 @@ def main():
     strong = bool(cfg.get("total"))
     if strong:  # cfg n is the whole stream: this rank verifies its contiguous share
         n = (n + world - 1) // world
-    ndev = max(ed25519.device_count(), 1)
-    eng = ed25519.Engine(device=local % ndev, max_chunk=min(n, 1 << 20), half=args.half)
+    ndev = ed25519.device_count()
+    if local >= ndev and not args.allow_shared_device:
+        log(f"[rank {rank}] local rank {local} but only {ndev} visible GPU(s)")
+        return 2
+    device = local % max(ndev, 1)
+    eng = ed25519.Engine(device=device, max_chunk=min(n, 1 << 20), half=args.half)
     info = eng.info()
     log(f"[rank {rank}] engine {info}")
+    pci = f"{info['pci_domain']:04x}:{info['pci_bus']:02x}:{info['pci_device']:02x}"
+    devices = all_gather(pci, world)
+    n_dev = len(set(devices))
+    if n_dev != world and not args.allow_shared_device:
+        log(f"[rank {rank}] ranks share devices: {devices}")
+        return 2
 
     t = time.perf_counter()
     wl = ed25519.DeviceWorkload(eng, n, cfg["lo"], cfg["hi"], cfg["ppm"], seed=args.seed, index_base=rank * n)
@@ -295,9 +410,15 @@ def main():
             c1 = config_c1(eng, args)
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"cpu baseline failed: {ex!r}")
+    hf = None
+    if args.host_reps > 0:
+        try:
+            hf = host_fed(wl, device, world, args.host_reps, args.host_batch, args.host_slots)
+        except Exception as ex:  # reported, never fatal for the device-resident number
+            log(f"[rank {rank}] host-fed leg failed: {ex!r}")
     lat = None
-    if rank == 0 and args.latency_txns > 0:
-        lat = latency_mode(eng, args, local % ndev)
+    if rank == 0 and world == 1 and args.latency_txns > 0:
+        lat = latency_mode(eng, args, device)
     traffic, traffic_src = pmc_traffic(min(n, info["max_chunk"]))
     # executed (not algorithmic) instruction rate of the dsm kernel: the
     # half-size formulation executes fewer operations than the reference's
@@ -311,7 +432,7 @@ def main():
             "metric": METRIC,
             "value": value,
             "unit": "verifies/s",
-            "n_gpus": world,
+            "n_gpus": n_dev,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_step,
@@ -325,6 +446,7 @@ def main():
                                    + (f" ({world * n} in the stream)" if strong else "")
                                    + f", message size uniform [{cfg['lo']},{cfg['hi']}] B, {cfg['ppm'] / 1e4:.1f}% invalid",
                        "signatures_per_gpu": n, "parallelism": f"shard x{world} (independent batches, no collective)",
+                       "devices": devices,
                        "codes": "reference AVX-512 backend"},
             "roofline": {"bound": "valu-int32", "kernel": "fd_ed25519_dsm_kernel",
                          "achieved": achieved, "peak": peak, "unit": "TOPS",
@@ -345,6 +467,7 @@ def main():
                              "stream beside its hash + scalar (dsm alone either way)",
             "cpu_baseline": cpu,
             "gpu_over_cpu": (value / cpu["value"]) if cpu else None,
+            "host_fed": hf,
             "latency_mode": lat,
             "config_c1": c1,
             "verdicts_match_reference_labels": mism_all == 0,

@@ -62,7 +62,7 @@ extern "C" {
      pflag    [2][cap]   u8   A, R: bit0 decode failure, bit1 small order
      pts      [2][20][cap] i32 A, R: x (10 limbs), y (10 limbs), radix 2^25.5
      hs       [19][cap]  u32  half-size scalars: c, |d|, s_lo (5 words), s_hi (4)
-     hflag    [cap]      u8   bit0 d < 0, bit1 no half-size pair (full-length form)
+     hflag    [cap]      u8   bit0 d < 0, bit1 no verified half-size pair (full-length form)
      perm     [cap]      u32  hash order (length-sorted)
      fix_list [cap]      u32  signatures for the full-length form (scalar -> dsm)
    FD_ED25519_WORK_BYTES_PER_SIG bytes per signature of capacity. */
@@ -87,9 +87,7 @@ typedef struct {
   uint8_t *        hflag;
   uint32_t *       fix_list;
   uint32_t *       fix_cnt;  /* 1 word: entries of fix_list                   */
-  uint32_t *       work_ctr; /* 1 word: dsm items handed out (fix_cnt + 1); the
-                                next word counts the long-|d| items queued at the
-                                back of fix_list                                 */
+  uint32_t *       work_ctr; /* 1 word: dsm items handed out (fix_cnt + 1)      */
   uint32_t *       perm;     /* [cap] hash order (length-sorted), NULL: identity */
   uint32_t *       hist;     /* [2*SORT_BUCKETS] counting-sort scratch          */
   uint64_t         cap;
@@ -103,20 +101,11 @@ typedef struct {
   int              small;          /* small chunk: fused prep kernel, no sort, dsm4 (1: a
                                       quad of lanes per signature) or dsm8 (2: two quads),
                                       full-length items by a scan of hflag          */
-  int              fused;          /* large chunk: hash + scalar and decode in the
-                                      wave-specialised prep kernel                   */
-  uint64_t         tail;           /* large chunk: the dsm kernel leaves the last `tail`
-                                      half-size items to a dsm4 launch that fills its
-                                      drain (0: none)                                 */
-  uint64_t         qbase;          /* dsm4: first item (0, or n - tail for the drain) */
 } fd_ed25519_verify_params_t;
 
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a
    hipError_t value (0 on success). */
 int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
-/* dsm4 over items [p->qbase, p->n) of a large chunk (the drain of the dsm
-   kernel when p->tail > 0; p->atab: the drain's own quad tables) */
-int fd_ed25519_hip_launch_dsm4( fd_ed25519_verify_params_t const * p, void * stream );
 int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, int base_doublings, void * stream );
 /* [0..2^20)[2^base_doublings]B into d_tab; d_scratch holds
    FD_ED25519_BTAB20_ENTRIES*10 + 40 int32 */

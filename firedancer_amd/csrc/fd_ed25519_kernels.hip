@@ -52,9 +52,7 @@
 #define FD_PF_FAIL  1u
 #define FD_PF_SMALL 2u
 #define FD_HF_DNEG  1u   /* hflag: d < 0                        */
-#define FD_HF_FULL  2u   /* hflag: no half-size pair, full form */
-#define FD_HF_LONG  4u   /* hflag: |d| >= 2^131 (more than 33 windows), queued
-                            at the back of fix_list (large chunks)  */
+#define FD_HF_FULL  2u   /* hflag: no (verified) half-size pair, full form */
 
 /* ------------------------------------------------------------------------
    Length sort for the hash phase.  A wave runs as many SHA-512 blocks as
@@ -78,10 +76,6 @@ __global__ void __launch_bounds__(256) fd_ed25519_sort_hist_kernel(fd_ed25519_ve
   __syncthreads();
   if (threadIdx.x < FD_ED25519_SORT_BUCKETS && h[threadIdx.x]) atomicAdd(&p.hist[threadIdx.x], h[threadIdx.x]);
 }
-
-#ifndef FD_ED25519_LONG_LIST
-#define FD_ED25519_LONG_LIST 0   /* A/B: no measurable difference (profiles/r1_long_list_ab.txt) */
-#endif
 
 #ifndef FD_ED25519_SORT_DESC
 #define FD_ED25519_SORT_DESC 1   /* longest hashes first: hash 1.05 -> 1.01 ms per 1M */
@@ -246,6 +240,98 @@ FD_DEV void btab_add(ge_p1p1& Rt, const ge_p3& P, ge_precomp& b, int f) {
 }
 
 /* ------------------------------------------------------------------------
+   The invariant the half-size verdict rests on, re-checked with integer
+   arithmetic only.  fd_half_scalars (fd25519_half.h) finds (c, d) with a
+   Euclid whose quotients come from exact-integer double-precision steps; a
+   wrong quotient there, or a compiler change to that sequence, must never
+   reach the group equation.  So every pair is checked before use:
+
+       d odd,  0 <= c < 2^131,  |d| < 2^dbits,  c == d k (mod 8L)
+
+   the congruence as X = |d| k + (d < 0 ? c : 8L - c) == 0 (mod 8L), i.e.
+   X == 0 (mod 8) and X / 8 == 0 (mod L) (sc_reduce512: X < 2^406).  A pair
+   that fails goes to the full-length form, whose verdict is the
+   reference's equation itself (fd_ed25519_user.c:209-226). */
+
+FD_DEV bool half_pair_ok(const uint32_t (&k)[8], const uint32_t (&c)[FD_HALF_TW], const uint32_t (&dm)[FD_HALF_TW],
+                         int dneg, int dbits) {
+  uint32_t x[16];
+#pragma unroll
+  for (int w = 0; w < 16; w++) x[w] = 0u;
+#pragma unroll
+  for (int a = 0; a < FD_HALF_TW; a++) {   /* |d| k: 160 x 256 bits */
+    uint64_t carry = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const uint64_t t = (uint64_t)dm[a] * k[b] + x[a + b] + carry;
+      x[a + b] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    x[a + 8] = (uint32_t)carry;
+  }
+  const uint32_t n8l[8] = FD_HALF_N8L;
+  uint32_t add[8];
+  {
+    uint64_t br = 0;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+      const uint32_t cv = w < FD_HALF_TW ? c[w] : 0u;
+      const uint64_t t = (uint64_t)n8l[w] - cv - br;   /* 8L - c: c < 2^160 < 8L */
+      br = (t >> 63) & 1u;
+      add[w] = dneg ? cv : (uint32_t)t;
+    }
+  }
+  {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < 15; w++) {
+      const uint64_t t = (uint64_t)x[w] + (w < 8 ? add[w] : 0u) + carry;
+      x[w] = (uint32_t)t;
+      carry = t >> 32;
+    }
+  }
+  const uint32_t low = x[0] & 7u;
+#pragma unroll
+  for (int w = 0; w < 15; w++) x[w] = __builtin_amdgcn_alignbit(x[w + 1], x[w], 3);
+  x[15] >>= 3;
+  uint32_t r[8];
+  sc_reduce512(r, x);
+  uint32_t nz = low;
+#pragma unroll
+  for (int w = 0; w < 8; w++) nz |= r[w];
+  return nz == 0u && (dm[0] & 1u) && fd_half_bitlen<FD_HALF_TW>(c) <= FD_HALF_BITS &&
+         fd_half_bitlen<FD_HALF_TW>(dm) <= dbits;
+}
+
+/* Compile-time fault injection (-DFD_ED25519_HALF_FAULT=1, a test build
+   only: libfd_ed25519_hip_faultinj.so): a bit of c flipped for 1/8 of the
+   items and a bit of |d| above bit 0 for another 1/8, after the search and
+   before the check, so that the check -- not luck -- keeps the verdicts
+   bit-exact (tests/test_gpu_halfcheck.py). */
+#ifndef FD_ED25519_HALF_FAULT
+#define FD_ED25519_HALF_FAULT 0
+#endif
+
+FD_DEV int half_scalars_checked(const uint32_t (&k)[8], uint32_t (&c)[FD_HALF_TW], uint32_t (&dm)[FD_HALF_TW],
+                                int* dneg, int dbits, uint64_t tag) {
+  const int found = fd_half_scalars(k, c, dm, dneg, dbits);
+#if FD_ED25519_HALF_FAULT
+  {
+    const uint32_t h = (uint32_t)(tag * 0x9E3779B97F4A7C15ull >> 32);
+    const uint32_t sel = h >> 29, w = (h >> 8) & 3u, b = h & 31u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (sel == 1u && i == (int)w) c[i] ^= 1u << b;
+      if (sel == 2u && i == (int)w) dm[i] ^= (i == 0 && b == 0) ? 2u : (1u << b);
+    }
+  }
+#else
+  (void)tag;
+#endif
+  return found && half_pair_ok(k, c, dm, *dneg, dbits);
+}
+
+/* ------------------------------------------------------------------------
    scalar: the half-size scalars (fd25519_half.h) of every signature, one
    lane per signature, before the points are decoded:
 
@@ -269,7 +355,7 @@ FD_DEV void scalar_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
   }
   uint32_t cw[FD_HALF_TW], dm[FD_HALF_TW];
   int dneg = 0;
-  int ok = fd_half_scalars(k, cw, dm, &dneg, p.half_dbits);
+  int ok = half_scalars_checked(k, cw, dm, &dneg, p.half_dbits, j);
   if (!p.sflag[j]) ok = 1;   /* S >= L: decided without the equation, any scalars do */
 
   /* s' = d S mod L */
@@ -315,18 +401,10 @@ FD_DEV void scalar_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
 #pragma unroll
   for (int w = 0; w < 4; w++)
     hs[(uint64_t)(15 + w) * c] = __builtin_amdgcn_alignbit(sp[w + 5], sp[w + 4], 4);  /* bits 132..   */
-  /* large chunks: the ~0.16% with |d| >= 2^131 are gathered into waves of
-     their own (else ~10% of the dsm waves would run extra windows for one
-     lane each) */
-  const bool lng = ok && !p.small && FD_ED25519_LONG_LIST && fd_half_bitlen<FD_HALF_TW>(dm) > 131;
-  p.hflag[j] = (uint8_t)((dneg ? FD_HF_DNEG : 0u) | (ok ? 0u : FD_HF_FULL) | (lng ? FD_HF_LONG : 0u));
+  p.hflag[j] = (uint8_t)((dneg ? FD_HF_DNEG : 0u) | (ok ? 0u : FD_HF_FULL));
   if (!ok && !p.small) {   /* small chunks: the dsm scan finds them by hflag */
     const uint32_t slot = atomicAdd(p.fix_cnt, 1u);
     p.fix_list[slot] = (uint32_t)j;
-  }
-  if (lng) {
-    const uint32_t slot = atomicAdd(p.work_ctr + 1, 1u);
-    p.fix_list[p.cap - 1u - slot] = (uint32_t)j;
   }
 }
 
@@ -609,10 +687,8 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
     return;
   }
   const uint64_t nfix = *p.fix_cnt;
-  const uint64_t nfix64 = (nfix + 63u) & ~(uint64_t)63u;
-  const uint64_t nlong = p.work_ctr[1];
-  const uint64_t head = nfix64 + ((nlong + 63u) & ~(uint64_t)63u);
-  const uint64_t total = head + p.n - p.tail;   /* the last `tail` items: the dsm4 drain */
+  const uint64_t head = (nfix + 63u) & ~(uint64_t)63u;
+  const uint64_t total = head + p.n;
   for (;;) {
     uint32_t b = 0u;
     if (lane == 0u) b = atomicAdd(p.work_ctr, 64u);
@@ -622,12 +698,9 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
     if (t < nfix) {
       const uint64_t j = p.fix_list[t];
       p.out[p.base + j] = (int8_t)dsm_full_one(p, j, tabA);
-    } else if (t >= nfix64 && t < nfix64 + nlong) {
-      const uint64_t j = p.fix_list[p.cap - 1u - (t - nfix64)];
-      p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
     } else if (t >= head && t < total) {
       const uint64_t j = t - head;
-      if (!(p.hflag[j] & (FD_HF_FULL | FD_HF_LONG))) p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
+      if (!(p.hflag[j] & FD_HF_FULL)) p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
     }
   }
 }
@@ -699,10 +772,10 @@ FD_DEV void table4_build(int4* tab, const fe& x, const fe& y, bool negate, const
 
 __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_params_t p) {
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t j = (gid >> 2) + p.qbase;   /* a quad per signature: all four lanes take the same branches */
+  const uint64_t j = gid >> 2;   /* a quad per signature: all four lanes take the same branches */
   if (j >= p.n) return;
   const uint32_t hf = p.hflag[j];
-  if (hf & (FD_HF_FULL | FD_HF_LONG)) return;   /* the dsm kernel's (large-chunk drain) */
+  if (hf & FD_HF_FULL) return;   /* the dsm kernel's (full-length form) */
   const qmask_t m = quad_masks();
   int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + gid * FD_ED25519_QUAD_LANE_BYTES);
   int4* tabR = tabA + 27;
@@ -790,7 +863,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
   const uint64_t j = gid >> 3;                 /* 8 lanes per signature, the same branches */
   if (j >= p.n) return;
   const uint32_t hf = p.hflag[j];
-  if (hf & (FD_HF_FULL | FD_HF_LONG)) return;   /* the dsm kernel's (large-chunk drain) */
+  if (hf & FD_HF_FULL) return;   /* the dsm kernel's (full-length form) */
   const int half = (int)((threadIdx.x >> 2) & 1u);   /* 0: -A and B, 1: -+R and B' */
   const qmask_t m = quad_masks();
   int4* tab = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + gid * (FD_ED25519_QUAD_LANE_BYTES / 2));
@@ -1033,7 +1106,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_diag_half_kernel(const uint32_
   uint32_t k[8], c[FD_HALF_TW], d[FD_HALF_TW];
   for (int w = 0; w < 8; w++) k[w] = kin[8 * i + w];
   int neg = 0;
-  const int ok = fd_half_scalars(k, c, d, &neg, dbits);
+  const int ok = half_scalars_checked(k, c, d, &neg, dbits, i);
   uint32_t* o = out + 12 * i;
   o[0] = (uint32_t)ok;
   o[1] = (uint32_t)neg;
@@ -1070,19 +1143,6 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
       break;
     }
     const dim3 g((uint32_t)((p->n + blk - 1) / blk));
-    if (p->fused) {
-      if (p->perm) {
-        const hipError_t e = hipMemsetAsync(p->hist, 0, 2 * FD_ED25519_SORT_BUCKETS * sizeof(uint32_t), st);
-        if (e != hipSuccess) return (int)e;
-        hipLaunchKernelGGL(fd_ed25519_sort_hist_kernel, g, dim3(blk), 0, st, *p);
-        hipLaunchKernelGGL(fd_ed25519_sort_scan_kernel, dim3(1), dim3(64), 0, st, *p);
-        hipLaunchKernelGGL(fd_ed25519_sort_scatter_kernel, g, dim3(blk), 0, st, *p);
-      }
-      const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 3 * sizeof(uint32_t), st);
-      if (e != hipSuccess) return (int)e;
-      hipLaunchKernelGGL(fd_ed25519_prep_kernel, dim3((uint32_t)((p->n + 63) / 64)), dim3(192), 0, st, *p);
-      break;
-    }
     if (p->perm) {
       const hipError_t e = hipMemsetAsync(p->hist, 0, 2 * FD_ED25519_SORT_BUCKETS * sizeof(uint32_t), st);
       if (e != hipSuccess) return (int)e;
@@ -1093,14 +1153,14 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
     hipLaunchKernelGGL(fd_ed25519_hash_kernel, g, dim3(blk), 0, st, *p);
   } break;
   case FD_ED25519_PHASE_SCALAR: {
-    if (p->small || p->fused) break;   /* in the prep kernel */
-    /* fix_cnt, the dsm work counter and the long-|d| count, adjacent words */
-    const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 3 * sizeof(uint32_t), st);
+    if (p->small) break;   /* in the prep kernel */
+    /* fix_cnt and the dsm work counter, adjacent words */
+    const hipError_t e = hipMemsetAsync(p->fix_cnt, 0, 2 * sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(fd_ed25519_scalar_kernel, dim3((uint32_t)((p->n + blk - 1) / blk)), dim3(blk), 0, st, *p);
   } break;
   case FD_ED25519_PHASE_DECODE:
-    if (p->small || p->fused) break;   /* in the prep kernel */
+    if (p->small) break;   /* in the prep kernel */
     hipLaunchKernelGGL(fd_ed25519_decode_kernel, dim3((uint32_t)((2 * p->n + blk - 1) / blk)), dim3(blk), 0, st,
                        *p);
     break;
@@ -1126,13 +1186,6 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
   default:
     return (int)hipErrorInvalidValue;
   }
-  return (int)hipGetLastError();
-}
-
-extern "C" int fd_ed25519_hip_launch_dsm4(const fd_ed25519_verify_params_t* p, void* stream) {
-  if (p->qbase >= p->n) return 0;
-  hipLaunchKernelGGL(fd_ed25519_dsm4_kernel, dim3((uint32_t)((4 * (p->n - p->qbase) + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, *p);
   return (int)hipGetLastError();
 }
 

@@ -40,18 +40,15 @@ struct fd_ed25519_hip_engine {
   uint32_t     dsm_grid;
   uint64_t     quad_max;   /* chunks of at most this many signatures run dsm4 */
   uint64_t     oct_max;    /* ... and of at most this many, dsm8            */
-  int          fused;      /* large chunks: the fused prep kernel too       */
   uint64_t     max_chunk;
   uint64_t     device_bytes;
   char         arch[ 64 ];
+  int          pci[ 3 ];   /* domain, bus, device */
 
   int32_t *    d_btab;
   int32_t *    d_btab16;     /* [0..2^15]B, the verify kernels' wide B table  */
   int32_t *    btab20[2];    /* shared per device: [0..2^20)B, [0..2^20)[2^132]B */
-  /* work sets: the per-chunk scratch of one chunk in flight.  Set 1 and
-     stream2 exist only with `dual`: a large batch then runs as two chunks,
-     one per (stream, work set), whose kernels overlap on the device (one
-     chunk's phase tails fill with the other's work). */
+  /* the per-chunk scratch of the chunk in flight */
   struct {
     void *     d_atab;       /* dsm lane tables (and the dsm4 quad tables)  */
     uint8_t *  d_work;       /* one allocation carved into the work arrays */
@@ -64,22 +61,12 @@ struct fd_ed25519_hip_engine {
     uint8_t *  d_hflag;
     uint32_t * d_perm;       /* hash order (length-sorted) */
     uint32_t * d_hist;       /* counting-sort scratch      */
-  } ws[2];
-  int          dual;
-  int          dual_skew;  /* chunk 1 starts after this many phases of chunk 0 */
-  hipStream_t  stream2;
-  hipEvent_t   ev_fork, ev_join;
+  } ws;
   /* overlap: a large chunk's decode (A and R need neither the hash nor the
      scalars) runs on a side stream beside hash + scalar, dsm after both */
   int          overlap;
   hipStream_t  side;
-  hipEvent_t   ev_dfork, ev_djoin, ev_sjoin;
-  /* drain: with the overlap, the last `tail` items of a large chunk go to a
-     dsm4 launch on the (low-priority) side stream, whose blocks take the
-     slots the persistent dsm kernel's waves free as its work runs out */
-  uint64_t     tail;
-  void *       d_qtab;     /* the drain's quad tables, tail x 4 lanes */
-  int          sort;         /* sort the hash phase by SHA-512 block count */
+  hipEvent_t   ev_dfork, ev_djoin;
 
   /* host-API staging (pinned host + device mirrors), grown on demand */
   uint64_t     st_sig_cap;   /* signatures */
@@ -198,11 +185,12 @@ static void
 engine_free( fd_ed25519_hip_engine_t * e ) {
   if( !e ) return;
   hipSetDevice( e->device );
+  /* all work of the engine's streams has drained before any buffer goes:
+     a failed verify_dev may have left decode queued on the side stream */
   if( e->stream ) hipStreamSynchronize( e->stream );
-  if( e->stream2 ) hipStreamSynchronize( e->stream2 );
+  if( e->side   ) hipStreamSynchronize( e->side );
   hipFree( e->d_btab ); hipFree( e->d_btab16 );
-  for( int i=0; i<2; i++ ) { hipFree( e->ws[i].d_atab ); hipFree( e->ws[i].d_work ); }
-  hipFree( e->d_qtab );
+  hipFree( e->ws.d_atab ); hipFree( e->ws.d_work );
   if( e->btab20[0] ) btab20_release( e->device );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
@@ -212,13 +200,8 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   if( e->tm_ev_init )
     for( int i=0; i<FD_ED25519_HIP_TIMING_MAX; i++ )
       for( int j=0; j<=FD_ED25519_PHASE_CNT; j++ ) hipEventDestroy( e->tm_ev[i][j] );
-  if( e->stream2 ) {
-    hipEventDestroy( e->ev_fork ); hipEventDestroy( e->ev_join );
-    hipStreamDestroy( e->stream2 );
-  }
   if( e->side ) {
-    hipStreamSynchronize( e->side );
-    hipEventDestroy( e->ev_dfork ); hipEventDestroy( e->ev_djoin ); hipEventDestroy( e->ev_sjoin );
+    hipEventDestroy( e->ev_dfork ); hipEventDestroy( e->ev_djoin );
     hipStreamDestroy( e->side );
   }
   if( e->stream ) hipStreamDestroy( e->stream );
@@ -240,6 +223,7 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   HIPCHK( hipGetDeviceProperties( &prop, device ), "hipGetDeviceProperties" );
   e->cu_cnt = prop.multiProcessorCount;
   snprintf( e->arch, sizeof(e->arch), "%.63s", prop.gcnArchName );
+  e->pci[0] = prop.pciDomainID; e->pci[1] = prop.pciBusID; e->pci[2] = prop.pciDeviceID;
   if( strncmp( prop.gcnArchName, "gfx950", 6 ) ) {
     snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf),
               "device %d is %.63s; libfd_ed25519_hip is built for gfx950 only", device, prop.gcnArchName );
@@ -259,53 +243,30 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   size_t work_sz = (size_t)e->max_chunk * FD_ED25519_WORK_BYTES_PER_SIG + 1024;
   HIPCHK( hipMalloc( (void **)&e->d_btab, btab_sz ), "hipMalloc(btab)" );
   HIPCHK( hipMalloc( (void **)&e->d_btab16, btab16_sz ), "hipMalloc(btab16)" );
-  char const * ds = getenv( "FD_ED25519_HIP_DUAL" );
-  e->dual = ds ? ds[0]=='1' : FD_ED25519_HIP_DUAL_DEFAULT;
-  if( flags & FD_ED25519_HIP_FLAG_SINGLE ) e->dual = 0;
-  char const * sks = getenv( "FD_ED25519_HIP_DUAL_SKEW" );
-  e->dual_skew = sks ? atoi( sks ) : 0;
-  if( e->dual_skew<0 || e->dual_skew>=FD_ED25519_PHASE_CNT ) e->dual_skew = 0;
-  int nws = e->dual ? 2 : 1;
-  e->device_bytes = btab_sz + btab16_sz + (size_t)nws * (atab_sz + work_sz);   /* + 2 x 128 MB shared per device */
-  for( int i=0; i<nws; i++ ) {
-    HIPCHK( hipMalloc( &e->ws[i].d_atab, atab_sz ), "hipMalloc(atab)" );
-    HIPCHK( hipMalloc( (void **)&e->ws[i].d_work, work_sz ), "hipMalloc(work)" );
+  e->device_bytes = btab_sz + btab16_sz + atab_sz + work_sz;   /* + 2 x 128 MB shared per device */
+  HIPCHK( hipMalloc( &e->ws.d_atab, atab_sz ), "hipMalloc(atab)" );
+  HIPCHK( hipMalloc( (void **)&e->ws.d_work, work_sz ), "hipMalloc(work)" );
+  {
     uint64_t c = e->max_chunk;
-    uint8_t * w = e->ws[i].d_work;
-    e->ws[i].d_k     = (uint32_t *)w; w += 8UL*4UL*c;
-    e->ws[i].d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
-    e->ws[i].d_hs    = (uint32_t *)w; w += 19UL*4UL*c;
-    e->ws[i].d_perm  = (uint32_t *)w; w += 4UL*c;
-    e->ws[i].d_fix   = (uint32_t *)w; w += 4UL*c;
-    e->ws[i].d_sflag = w;             w += c;
-    e->ws[i].d_pflag = w;             w += 2UL*c;
-    e->ws[i].d_hflag = w;             w += c;
+    uint8_t * w = e->ws.d_work;
+    e->ws.d_k     = (uint32_t *)w; w += 8UL*4UL*c;
+    e->ws.d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
+    e->ws.d_hs    = (uint32_t *)w; w += 19UL*4UL*c;
+    e->ws.d_perm  = (uint32_t *)w; w += 4UL*c;
+    e->ws.d_fix   = (uint32_t *)w; w += 4UL*c;
+    e->ws.d_sflag = w;             w += c;
+    e->ws.d_pflag = w;             w += 2UL*c;
+    e->ws.d_hflag = w;             w += c;
     w = (uint8_t *)(((uintptr_t)w + 255UL) & ~(uintptr_t)255UL);
-    e->ws[i].d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words + fix count inside the 1024-byte slack */
-  }
-  if( e->dual ) {
-    HIPCHK( hipStreamCreateWithFlags( &e->stream2, hipStreamNonBlocking ), "hipStreamCreate" );
-    HIPCHK( hipEventCreateWithFlags( &e->ev_fork, hipEventDisableTiming ), "hipEventCreate" );
-    HIPCHK( hipEventCreateWithFlags( &e->ev_join, hipEventDisableTiming ), "hipEventCreate" );
+    e->ws.d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words + fix count inside the 1024-byte slack */
   }
   char const * ovs = getenv( "FD_ED25519_HIP_OVERLAP" );
   e->overlap = ovs ? ovs[0]=='1' : FD_ED25519_HIP_OVERLAP_DEFAULT;
-  char const * tls = getenv( "FD_ED25519_HIP_TAIL" );
-  e->tail = tls ? strtoul( tls, NULL, 0 ) : FD_ED25519_HIP_TAIL_DEFAULT;
-  if( !e->overlap ) e->tail = 0UL;
-  if( e->tail ) {
-    HIPCHK( hipMalloc( &e->d_qtab, e->tail * 4UL * FD_ED25519_QUAD_LANE_BYTES ), "hipMalloc(qtab)" );
-    e->device_bytes += e->tail * 4UL * FD_ED25519_QUAD_LANE_BYTES;
-  }
-  char const * ns = getenv( "FD_ED25519_HIP_NOSORT" );
-  e->sort = !(ns && ns[0]=='1');
   /* dsm4 (a quad of lanes per signature) below the size where one lane
      per signature fills the chip; its lane tables live in the atab scratch */
   uint64_t quad_cap = atab_sz / (4UL * FD_ED25519_QUAD_LANE_BYTES);
   char const * qs = getenv( "FD_ED25519_HIP_QUAD_MAX" );
   e->quad_max = qs ? strtoul( qs, NULL, 0 ) : FD_ED25519_HIP_QUAD_MAX_DEFAULT;
-  char const * fs = getenv( "FD_ED25519_HIP_FUSED" );
-  e->fused = fs ? fs[0]=='1' : 0;
   char const * os = getenv( "FD_ED25519_HIP_OCT_MAX" );
   e->oct_max = os ? strtoul( os, NULL, 0 ) : FD_ED25519_HIP_OCT_MAX_DEFAULT;
   if( flags & FD_ED25519_HIP_FLAG_DSM_QUAD ) { e->quad_max = ~0UL; e->oct_max = 0UL; }
@@ -346,6 +307,9 @@ fd_ed25519_hip_engine_info( fd_ed25519_hip_engine_t const * e, fd_ed25519_hip_in
   info->device_bytes      = e->device_bytes;
   info->flags             = e->flags;
   memcpy( info->arch, e->arch, sizeof(info->arch) );
+  info->pci_domain        = e->pci[0];
+  info->pci_bus           = e->pci[1];
+  info->pci_device        = e->pci[2];
   return FD_ED25519_HIP_OK;
 }
 
@@ -408,102 +372,53 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab20 = e->btab20[0]; p.btab20b = e->btab20[1];
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   p.half_dbits     = engine_half_dbits( e );
-  /* dual: chunks alternate between (st, set 0) and (stream2, set 1); at
-     least two chunks, each above the small-chunk size */
   uint64_t chunk = e->max_chunk;
-  int dual = 0;
-  if( e->dual && !e->timing && (n+1UL)/2UL > e->quad_max ) {
-    dual = 1;
-    if( (n+1UL)/2UL < chunk ) chunk = (n+1UL)/2UL;
-  }
-  if( dual && !e->dual_skew ) {
-    HIPCHK( hipEventRecord( e->ev_fork, st ), "hipEventRecord" );
-    HIPCHK( hipStreamWaitEvent( e->stream2, e->ev_fork, 0 ), "hipStreamWaitEvent" );
-  }
-  uint64_t ci = 0UL;
-  for( uint64_t base=0UL; base<n; base+=chunk, ci++ ) {
-    int          wi = dual ? (int)(ci & 1UL) : 0;
-    hipStream_t  cs = wi ? e->stream2 : st;
-    p.k = e->ws[wi].d_k; p.sflag = e->ws[wi].d_sflag; p.pflag = e->ws[wi].d_pflag; p.pts = e->ws[wi].d_pts;
-    p.fix_list = e->ws[wi].d_fix; p.fix_cnt = e->ws[wi].d_hist + 2*FD_ED25519_SORT_BUCKETS;
-    p.work_ctr = p.fix_cnt + 1; p.hs = e->ws[wi].d_hs; p.hflag = e->ws[wi].d_hflag;
-    p.hist = e->ws[wi].d_hist; p.atab = e->ws[wi].d_atab;
-    p.base = base;
-    p.n    = (n-base) < chunk ? (n-base) : chunk;
+  p.k = e->ws.d_k; p.sflag = e->ws.d_sflag; p.pflag = e->ws.d_pflag; p.pts = e->ws.d_pts;
+  p.fix_list = e->ws.d_fix; p.fix_cnt = e->ws.d_hist + 2*FD_ED25519_SORT_BUCKETS;
+  p.work_ctr = p.fix_cnt + 1; p.hs = e->ws.d_hs; p.hflag = e->ws.d_hflag;
+  p.hist = e->ws.d_hist; p.atab = e->ws.d_atab;
+  for( uint64_t base=0UL; base<n; base+=chunk ) {
+    p.base  = base;
+    p.n     = (n-base) < chunk ? (n-base) : chunk;
     p.small = p.n > e->quad_max ? 0 : (p.n <= e->oct_max ? 2 : 1);
-    p.fused = e->fused;
-    p.perm  = (e->sort && !p.small) ? e->ws[wi].d_perm : NULL;
+    p.perm  = p.small ? NULL : e->ws.d_perm;
     if( e->timing && e->tm_cnt<FD_ED25519_HIP_TIMING_MAX ) {
       /* events bracket each phase kernel on the stream it runs on */
       hipEvent_t * ev = e->tm_ev[ e->tm_cnt++ ];
-      HIPCHK( hipEventRecord( ev[0], cs ), "hipEventRecord" );
+      HIPCHK( hipEventRecord( ev[0], st ), "hipEventRecord" );
       for( int ph=0; ph<FD_ED25519_PHASE_CNT; ph++ ) {
-        int err = fd_ed25519_hip_launch_phase( &p, ph, e->dsm_grid, cs );
+        int err = fd_ed25519_hip_launch_phase( &p, ph, e->dsm_grid, st );
         if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-        HIPCHK( hipEventRecord( ev[ph+1], cs ), "hipEventRecord" );
+        HIPCHK( hipEventRecord( ev[ph+1], st ), "hipEventRecord" );
       }
-    } else if( dual && e->dual_skew && ci==0UL ) {
-      /* skewed start: the second chunk's phases trail the first's */
-      for( int ph=0; ph<FD_ED25519_PHASE_CNT; ph++ ) {
-        if( ph==e->dual_skew ) {
-          HIPCHK( hipEventRecord( e->ev_fork, cs ), "hipEventRecord" );
-          HIPCHK( hipStreamWaitEvent( e->stream2, e->ev_fork, 0 ), "hipStreamWaitEvent" );
-        }
-        int err = fd_ed25519_hip_launch_phase( &p, ph, e->dsm_grid, cs );
-        if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-      }
-    } else if( e->overlap && !dual && !p.small && !p.fused ) {
+    } else if( e->overlap && !p.small ) {
       if( !e->side ) {
         /* created on the first large chunk only: an engine that only sees
            small batches (a tile slot) keeps to one stream, since the
            device's few hardware queues are shared by every stream of the
            process and extra streams serialise the slots */
-        int least = 0, greatest = 0;
-        HIPCHK( hipDeviceGetStreamPriorityRange( &least, &greatest ), "hipDeviceGetStreamPriorityRange" );
-        int prio = e->tail ? least : 0;
-        char const * ps = getenv( "FD_ED25519_HIP_SIDE_PRIO" );   /* A/B: "high" | "low" */
-        if( ps && !strcmp( ps, "high" ) ) prio = greatest;
-        if( ps && !strcmp( ps, "low"  ) ) prio = least;
-        HIPCHK( hipStreamCreateWithPriority( &e->side, hipStreamNonBlocking, prio ), "hipStreamCreate" );
+        HIPCHK( hipStreamCreateWithFlags( &e->side, hipStreamNonBlocking ), "hipStreamCreate" );
         HIPCHK( hipEventCreateWithFlags( &e->ev_dfork, hipEventDisableTiming ), "hipEventCreate" );
         HIPCHK( hipEventCreateWithFlags( &e->ev_djoin, hipEventDisableTiming ), "hipEventCreate" );
-        HIPCHK( hipEventCreateWithFlags( &e->ev_sjoin, hipEventDisableTiming ), "hipEventCreate" );
       }
-      uint64_t tail = (e->tail && p.n > 4UL*e->tail) ? e->tail : 0UL;
-      HIPCHK( hipEventRecord( e->ev_dfork, cs ), "hipEventRecord" );
+      HIPCHK( hipEventRecord( e->ev_dfork, st ), "hipEventRecord" );
       HIPCHK( hipStreamWaitEvent( e->side, e->ev_dfork, 0 ), "hipStreamWaitEvent" );
       int err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DECODE, e->dsm_grid, e->side );
       if( err ) return hip_fail( (hipError_t)err, "verify launch" );
       HIPCHK( hipEventRecord( e->ev_djoin, e->side ), "hipEventRecord" );
-      err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_HASH, e->dsm_grid, cs );
-      if( !err ) err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_SCALAR, e->dsm_grid, cs );
+      err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_HASH, e->dsm_grid, st );
+      if( !err ) err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_SCALAR, e->dsm_grid, st );
+      /* dsm (and the next chunk, which reuses the work arrays) after decode,
+         even when a launch above failed */
+      hipError_t we = hipStreamWaitEvent( st, e->ev_djoin, 0 );
       if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-      HIPCHK( hipStreamWaitEvent( cs, e->ev_djoin, 0 ), "hipStreamWaitEvent" );
-      if( tail ) {
-        HIPCHK( hipEventRecord( e->ev_sjoin, cs ), "hipEventRecord" );
-        HIPCHK( hipStreamWaitEvent( e->side, e->ev_sjoin, 0 ), "hipStreamWaitEvent" );
-      }
-      p.tail = tail;
-      err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, cs );
+      HIPCHK( we, "hipStreamWaitEvent" );
+      err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, st );
       if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-      if( tail ) {
-        fd_ed25519_verify_params_t q = p;
-        q.atab  = e->d_qtab;
-        q.qbase = p.n - tail;
-        err = fd_ed25519_hip_launch_dsm4( &q, e->side );
-        if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-        HIPCHK( hipEventRecord( e->ev_djoin, e->side ), "hipEventRecord" );
-        HIPCHK( hipStreamWaitEvent( cs, e->ev_djoin, 0 ), "hipStreamWaitEvent" );
-      }
-      p.tail = 0UL;
     } else {
-      int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, cs );
+      int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, st );
       if( err ) return hip_fail( (hipError_t)err, "verify launch" );
     }
-  }
-  if( dual ) {
-    HIPCHK( hipEventRecord( e->ev_join, e->stream2 ), "hipEventRecord" );
-    HIPCHK( hipStreamWaitEvent( st, e->ev_join, 0 ), "hipStreamWaitEvent" );
   }
   return FD_ED25519_HIP_OK;
 }
@@ -848,8 +763,8 @@ fd_ed25519_verify( unsigned char const msg[], unsigned long msg_sz, unsigned cha
 
 int
 fd_ed25519_verify_batch_single_msg( unsigned char const msg[], unsigned long const msg_sz,
-                                    unsigned char const signatures[], unsigned char const pubkeys[],
-                                    fd_sha512_t * shas[], unsigned char const batch_sz ) {
+                                    unsigned char const signatures[ 64 ], unsigned char const pubkeys[ 32 ],
+                                    fd_sha512_t * shas[ 1 ], unsigned char const batch_sz ) {
   (void)shas;
   if( batch_sz==0 || batch_sz>16 ) return FD_ED25519_ERR_SIG;
   fd_ed25519_hip_engine_t * e = default_get();

@@ -14,6 +14,13 @@
    runs more than depth frags ahead (the reference's fctl / fseq pair,
    reduced to one counter).
 
+   The two sides need not trust each other (the tile may be compromised):
+   the geometry (depth, chunk count, MTU) is validated once at create /
+   join and kept in the process-local handle; later writes to the shared
+   header are never read again, and every frag a consumer takes is bounds
+   checked against the local geometry before its payload is copied (the
+   reference tile's own check, src/app/fdctl/run/tiles/fd_verify.c:67).
+
    No HIP: this file is also linked into the standalone sandboxed producer
    (tools/shlink_producer.c). */
 #define _GNU_SOURCE
@@ -62,7 +69,16 @@ struct fd_ed25519_hip_shlink {
      (consumer), and the producer's next dcache chunk */
   uint64_t        seq;
   uint64_t        chunk;
+  /* process-local geometry, validated at create / join */
+  uint64_t        depth;
+  uint64_t        chunk_cnt;
+  uint64_t        mtu;
 };
+
+static uint64_t
+shlink_mtu_chunks( void ) {
+  return (FD_ED25519_HIP_TXN_MTU + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
+}
 
 static size_t
 shlink_footprint( uint64_t depth, uint64_t chunk_cnt ) {
@@ -86,8 +102,7 @@ shlink_map( char const * name, int fd, size_t sz ) {
 fd_ed25519_hip_shlink_t *
 fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
   if( !name || !depth || (depth & (depth-1UL)) || strlen( name )>=120 ) return NULL;
-  uint64_t mtu_chunks = (FD_ED25519_HIP_TXN_MTU + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
-  uint64_t chunk_cnt  = (depth + 2UL) * mtu_chunks;
+  uint64_t chunk_cnt  = (depth + 2UL) * shlink_mtu_chunks();
   size_t   sz         = shlink_footprint( depth, chunk_cnt );
   int fd = shm_open( name, O_RDWR | O_CREAT | O_EXCL, 0600 );
   if( fd<0 ) return NULL;
@@ -98,9 +113,9 @@ fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
   for( uint64_t k=0UL; k<depth; k++ ) {
     atomic_store_explicit( &l->mcache[ k ].seq, k - depth, memory_order_relaxed );
   }
-  l->hdr->depth     = depth;
-  l->hdr->chunk_cnt = chunk_cnt;
-  l->hdr->mtu       = FD_ED25519_HIP_TXN_MTU;
+  l->hdr->depth     = l->depth     = depth;
+  l->hdr->chunk_cnt = l->chunk_cnt = chunk_cnt;
+  l->hdr->mtu       = l->mtu       = FD_ED25519_HIP_TXN_MTU;
   atomic_store_explicit( &l->hdr->consumed, 0UL, memory_order_relaxed );
   atomic_thread_fence( memory_order_release );
   l->hdr->magic = SHLINK_MAGIC;
@@ -116,11 +131,19 @@ fd_ed25519_hip_shlink_join( char const * name ) {
   if( fstat( fd, &st ) || (size_t)st.st_size<sizeof(shlink_hdr_t) ) { close( fd ); return NULL; }
   fd_ed25519_hip_shlink_t * l = shlink_map( name, fd, (size_t)st.st_size );
   if( !l ) return NULL;
-  if( l->hdr->magic!=SHLINK_MAGIC ||
-      shlink_footprint( l->hdr->depth, l->hdr->chunk_cnt )!=l->map_sz ) {
+  /* one snapshot of the geometry, checked against what create makes */
+  uint64_t magic     = l->hdr->magic;
+  atomic_thread_fence( memory_order_acquire );
+  uint64_t depth     = l->hdr->depth;
+  uint64_t chunk_cnt = l->hdr->chunk_cnt;
+  uint64_t mtu       = l->hdr->mtu;
+  if( magic!=SHLINK_MAGIC || !depth || (depth & (depth-1UL)) || depth>(1UL<<30) ||
+      mtu!=FD_ED25519_HIP_TXN_MTU || chunk_cnt!=(depth + 2UL) * shlink_mtu_chunks() ||
+      shlink_footprint( depth, chunk_cnt )!=l->map_sz ) {
     munmap( l->hdr, l->map_sz ); free( l ); return NULL;
   }
-  l->dcache = (unsigned char *)l->mcache + l->hdr->depth * sizeof(shlink_meta_t);
+  l->depth = depth; l->chunk_cnt = chunk_cnt; l->mtu = mtu;
+  l->dcache = (unsigned char *)l->mcache + depth * sizeof(shlink_meta_t);
   return l;
 }
 
@@ -134,19 +157,21 @@ fd_ed25519_hip_shlink_leave( fd_ed25519_hip_shlink_t * l, int unlink ) {
 
 unsigned long
 fd_ed25519_hip_shlink_depth( fd_ed25519_hip_shlink_t const * l ) {
-  return l ? l->hdr->depth : 0UL;
+  return l ? l->depth : 0UL;
 }
 
 int
 fd_ed25519_hip_shlink_publish( fd_ed25519_hip_shlink_t * l, unsigned char const * payload, unsigned long sz,
                                unsigned long sig, unsigned int ctl ) {
   shlink_hdr_t * h = l->hdr;
-  if( sz>h->mtu ) return FD_ED25519_HIP_ERR_INVAL;
+  if( sz>l->mtu ) return FD_ED25519_HIP_ERR_INVAL;
   uint64_t seq = l->seq;
-  if( seq - atomic_load_explicit( &h->consumed, memory_order_acquire )>=h->depth ) return 1;   /* no credit */
-  uint64_t mtu_chunks = (h->mtu + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
-  if( l->chunk + mtu_chunks>h->chunk_cnt ) l->chunk = 0UL;   /* compact wrap */
-  shlink_meta_t * m = &l->mcache[ seq & (h->depth-1UL) ];
+  /* a bogus credit count from the consumer only lets the producer overrun
+     that consumer: every write below stays inside the local geometry */
+  if( seq - atomic_load_explicit( &h->consumed, memory_order_acquire )>=l->depth ) return 1;   /* no credit */
+  uint64_t mtu_chunks = (l->mtu + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
+  if( l->chunk + mtu_chunks>l->chunk_cnt ) l->chunk = 0UL;   /* compact wrap */
+  shlink_meta_t * m = &l->mcache[ seq & (l->depth-1UL) ];
   atomic_store_explicit( &m->seq, seq-1UL, memory_order_relaxed );
   atomic_thread_fence( memory_order_release );
   if( sz ) memcpy( l->dcache + l->chunk*SHLINK_CHUNK, payload, sz );
@@ -167,15 +192,18 @@ fd_ed25519_hip_shlink_consume( fd_ed25519_hip_shlink_t * l, unsigned char * payl
                                unsigned long * sig, unsigned int * ctl ) {
   shlink_hdr_t * h = l->hdr;
   uint64_t seq = l->seq;
-  shlink_meta_t * m = &l->mcache[ seq & (h->depth-1UL) ];
+  shlink_meta_t * m = &l->mcache[ seq & (l->depth-1UL) ];
   uint64_t s0 = atomic_load_explicit( &m->seq, memory_order_acquire );
   if( (int64_t)(s0 - seq)<0 ) return 1;                      /* not yet published */
   if( s0!=seq ) return -1;                                    /* overrun */
-  unsigned long n = m->sz;
-  unsigned long sg = m->sig;
-  unsigned int  c  = m->ctl;
-  if( n>h->mtu ) return -1;
-  if( n ) memcpy( payload, l->dcache + (unsigned long)m->chunk*SHLINK_CHUNK, n );
+  unsigned long n     = m->sz;
+  unsigned long sg    = m->sig;
+  unsigned int  c     = m->ctl;
+  unsigned long chunk = m->chunk;
+  /* the frag must lie inside this side's dcache and fit the caller's
+     FD_ED25519_HIP_TXN_MTU-byte buffer (fd_verify.c:67) */
+  if( n>l->mtu || chunk>=l->chunk_cnt || chunk*SHLINK_CHUNK + n>l->chunk_cnt*SHLINK_CHUNK ) return -1;
+  if( n ) memcpy( payload, l->dcache + chunk*SHLINK_CHUNK, n );
   atomic_thread_fence( memory_order_acquire );
   if( atomic_load_explicit( &m->seq, memory_order_relaxed )!=s0 ) return -1;   /* overrun during the copy */
   *sz = n; *sig = sg; *ctl = c;

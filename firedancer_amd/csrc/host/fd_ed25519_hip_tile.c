@@ -922,7 +922,36 @@ done:
 }
 
 /* ======================================================================
-   pool: one feeder thread + pipe per device, batches dealt round-robin. */
+   pool: one feeder thread per device, batches dealt round-robin (batch b
+   to device b % N, the analogue of seq % verify_tile_count,
+   src/app/fdctl/run/tiles/fd_verify.c:46).
+
+   A batch reaches the device without its bytes being touched on the host
+   when the caller's arrays are page-locked (fd_ed25519_hip_host_register,
+   or hipHostMalloc'd): its messages go as one DMA of the byte range they
+   span (the kernels index that range with the caller's own offsets, the
+   device base pointer shifted by the range's start), msg_off / msg_sz /
+   sigs / pubs as one DMA each, and the codes come back by DMA straight
+   into out.  Pageable arrays, or messages scattered so widely that their
+   span is far larger than their bytes, are packed into the slot's pinned
+   staging block first.  Each slot has its own engine (stream and work
+   arrays), so one batch's copies overlap another's kernels; the feeder
+   thread runs on the CPUs of its GPU's NUMA node. */
+
+typedef struct {
+  fd_ed25519_hip_engine_t * eng;
+  hipEvent_t                ev;
+  unsigned char *           d_msgs;
+  unsigned long *           d_off;
+  unsigned int *            d_sz;
+  unsigned char *           d_sigs;
+  unsigned char *           d_pubs;
+  signed char *             d_out;
+  unsigned char *           h_stage;   /* pinned: [sigs | pubs | off | sz | msgs], staged batches only */
+  signed char *             h_out;     /* pinned codes, when out is pageable                            */
+  unsigned long             b, i0, i1;
+  int                       busy;
+} pool_slot_t;
 
 typedef struct {
   int                   device;
@@ -935,47 +964,206 @@ typedef struct {
   unsigned char const * sigs;
   unsigned char const * pubs;
   signed char *         out;
+  int                   direct_in, direct_out;   /* caller arrays page-locked */
   int                   err;
+  fd_ed25519_hip_pool_stats_t st;
 } pool_job_t;
+
+static int
+host_locked( void const * p ) {
+  if( !p ) return 0;
+  hipPointerAttribute_t a;
+  memset( &a, 0, sizeof(a) );
+  if( hipPointerGetAttributes( &a, p )!=hipSuccess ) { (void)hipGetLastError(); return 0; }
+  return a.type==hipMemoryTypeHost;
+}
+
+int
+fd_ed25519_hip_host_register( void * ptr, unsigned long sz ) {
+  if( !ptr || !sz ) return FD_ED25519_HIP_ERR_INVAL;
+  TCHK( hipHostRegister( ptr, sz, hipHostRegisterPortable | hipHostRegisterMapped ), "hipHostRegister" );
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_host_unregister( void * ptr ) {
+  if( !ptr ) return FD_ED25519_HIP_ERR_INVAL;
+  TCHK( hipHostUnregister( ptr ), "hipHostUnregister" );
+  return FD_ED25519_HIP_OK;
+}
+
+/* the calling thread onto the CPUs of the device's NUMA node (within its
+   current affinity); no change when that cannot be read */
+static void
+pin_near_device( int device ) {
+  char bdf[ 64 ];
+  if( hipDeviceGetPCIBusId( bdf, (int)sizeof(bdf), device )!=hipSuccess ) return;
+  for( char * c=bdf; *c; c++ ) if( *c>='A' && *c<='F' ) *c = (char)(*c - 'A' + 'a');
+  char path[ 160 ];
+  snprintf( path, sizeof(path), "/sys/bus/pci/devices/%s/local_cpulist", bdf );
+  FILE * f = fopen( path, "r" );
+  if( !f ) return;
+  char list[ 1024 ];
+  size_t len = fread( list, 1, sizeof(list)-1UL, f );
+  fclose( f );
+  list[ len ] = 0;
+  cpu_set_t cur, want;
+  if( pthread_getaffinity_np( pthread_self(), sizeof(cur), &cur ) ) return;
+  CPU_ZERO( &want );
+  for( char * t=list; *t; ) {
+    char * e;
+    long lo = strtol( t, &e, 10 ), hi = lo;
+    if( e==t ) break;
+    if( *e=='-' ) { t = e+1; hi = strtol( t, &e, 10 ); }
+    for( long c=lo; c<=hi && c<CPU_SETSIZE; c++ ) if( c>=0 && CPU_ISSET( (int)c, &cur ) ) CPU_SET( (int)c, &want );
+    t = *e==',' ? e+1 : e;
+    if( *e!=',' ) break;
+  }
+  if( CPU_COUNT( &want ) ) pthread_setaffinity_np( pthread_self(), sizeof(want), &want );
+}
+
+/* a batch's message span [lo, hi) and its bytes */
+static void
+batch_span( pool_job_t const * j, unsigned long i0, unsigned long i1, unsigned long * lo, unsigned long * hi,
+            unsigned long * bytes ) {
+  unsigned long l = ~0UL, h = 0UL, b = 0UL;
+  for( unsigned long i=i0; i<i1; i++ ) {
+    unsigned long o = j->msg_off[i], e = o + j->msg_sz[i];
+    l = o<l ? o : l;
+    h = e>h ? e : h;
+    b += j->msg_sz[i];
+  }
+  if( l>h ) l = h = 0UL;
+  *lo = l; *hi = h; *bytes = b;
+}
+
+/* the span goes as it is when it is not much larger than the bytes in it */
+#define POOL_SPAN_SLACK(bytes) (2UL*(bytes) + 65536UL)
+
+static int
+pool_slot_init( pool_slot_t * s, int device, unsigned long batch_sigs, unsigned long msg_cap, int stage, int stage_out ) {
+  s->eng = fd_ed25519_hip_engine_new( device, batch_sigs, 0 );
+  if( !s->eng ) return FD_ED25519_HIP_ERR_INVAL;
+  unsigned long dsz = 112UL*batch_sigs + msg_cap + 64UL + 1024UL;
+  unsigned char * d = NULL;
+  TCHK( hipMalloc( (void **)&d, dsz ), "hipMalloc(pool slot)" );
+  s->d_sigs = d;                                     d += 64UL*batch_sigs;
+  s->d_pubs = d;                                     d += 32UL*batch_sigs;
+  s->d_off  = (unsigned long *)d;                    d += 8UL*batch_sigs;
+  s->d_sz   = (unsigned int *)d;                     d += 4UL*batch_sigs;
+  s->d_out  = (signed char *)d;                      d += (batch_sigs + 255UL) & ~255UL;
+  s->d_msgs = d;
+  if( stage ) TCHK( hipHostMalloc( (void **)&s->h_stage, 108UL*batch_sigs + msg_cap + 64UL, hipHostMallocDefault ),
+                    "hipHostMalloc(pool stage)" );
+  if( stage_out ) TCHK( hipHostMalloc( (void **)&s->h_out, batch_sigs, hipHostMallocDefault ), "hipHostMalloc(pool out)" );
+  TCHK( hipEventCreateWithFlags( &s->ev, hipEventDisableTiming ), "hipEventCreate" );
+  return FD_ED25519_HIP_OK;
+}
+
+static void
+pool_slot_fini( pool_slot_t * s ) {
+  if( s->eng ) fd_ed25519_hip_engine_sync( s->eng );
+  hipFree( s->d_sigs );
+  hipHostFree( s->h_stage ); hipHostFree( s->h_out );
+  if( s->ev ) hipEventDestroy( s->ev );
+  if( s->eng ) fd_ed25519_hip_engine_delete( s->eng );
+}
+
+static int
+pool_submit( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
+  unsigned long i0 = b*j->batch_sigs, i1 = i0+j->batch_sigs < j->n ? i0+j->batch_sigs : j->n, cnt = i1-i0;
+  hipStream_t st = (hipStream_t)fd_ed25519_hip_engine_stream( s->eng );
+  unsigned long lo, hi, bytes;
+  batch_span( j, i0, i1, &lo, &hi, &bytes );
+  unsigned char const * dmsgs;
+  if( j->direct_in && hi-lo<=POOL_SPAN_SLACK( bytes ) ) {
+    if( hi>lo ) TCHK( hipMemcpyAsync( s->d_msgs, j->msgs + lo, hi-lo, hipMemcpyHostToDevice, st ), "H2D msgs" );
+    TCHK( hipMemcpyAsync( s->d_off,  j->msg_off + i0, 8UL*cnt,  hipMemcpyHostToDevice, st ), "H2D off"  );
+    TCHK( hipMemcpyAsync( s->d_sz,   j->msg_sz  + i0, 4UL*cnt,  hipMemcpyHostToDevice, st ), "H2D sz"   );
+    TCHK( hipMemcpyAsync( s->d_sigs, j->sigs + 64UL*i0, 64UL*cnt, hipMemcpyHostToDevice, st ), "H2D sigs" );
+    TCHK( hipMemcpyAsync( s->d_pubs, j->pubs + 32UL*i0, 32UL*cnt, hipMemcpyHostToDevice, st ), "H2D pubs" );
+    j->st.direct_batches++;
+    j->st.h2d_bytes += (hi-lo) + 108UL*cnt;
+    dmsgs = s->d_msgs - lo;   /* msg_off[i] indexes the span from its start */
+  } else {
+    /* pack into pinned staging: [sigs | pubs | off | sz | msgs], one DMA */
+    unsigned char * h = s->h_stage;
+    if( !h ) return FD_ED25519_HIP_ERR_INVAL;
+    memcpy( h,               j->sigs + 64UL*i0, 64UL*cnt );
+    memcpy( h + 64UL*cnt,    j->pubs + 32UL*i0, 32UL*cnt );
+    unsigned long * off = (unsigned long *)(h + 96UL*cnt);
+    unsigned int *  sz  = (unsigned int  *)(h + 104UL*cnt);
+    unsigned char * m   = h + 108UL*cnt;
+    unsigned long pos = 0UL;
+    for( unsigned long i=i0; i<i1; i++ ) {
+      unsigned long k = i-i0;
+      if( j->msg_sz[i] ) memcpy( m + pos, j->msgs + j->msg_off[i], j->msg_sz[i] );
+      off[k] = pos; sz[k] = j->msg_sz[i];
+      pos += j->msg_sz[i];
+    }
+    /* the device block has the same order at batch_sigs strides: copy the
+       four arrays and the messages separately */
+    TCHK( hipMemcpyAsync( s->d_sigs, h,               64UL*cnt, hipMemcpyHostToDevice, st ), "H2D sigs" );
+    TCHK( hipMemcpyAsync( s->d_pubs, h + 64UL*cnt,    32UL*cnt, hipMemcpyHostToDevice, st ), "H2D pubs" );
+    TCHK( hipMemcpyAsync( s->d_off,  off,             8UL*cnt,  hipMemcpyHostToDevice, st ), "H2D off"  );
+    TCHK( hipMemcpyAsync( s->d_sz,   sz,              4UL*cnt,  hipMemcpyHostToDevice, st ), "H2D sz"   );
+    if( pos ) TCHK( hipMemcpyAsync( s->d_msgs, m, pos, hipMemcpyHostToDevice, st ), "H2D msgs" );
+    j->st.staged_batches++;
+    j->st.h2d_bytes += pos + 108UL*cnt;
+    dmsgs = s->d_msgs;
+  }
+  int err = fd_ed25519_hip_verify_dev( s->eng, cnt, dmsgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
+  if( err ) return err;
+  signed char * dst = j->direct_out ? j->out + i0 : s->h_out;
+  TCHK( hipMemcpyAsync( dst, s->d_out, cnt, hipMemcpyDeviceToHost, st ), "D2H codes" );
+  TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
+  s->b = b; s->i0 = i0; s->i1 = i1; s->busy = 1;
+  return FD_ED25519_HIP_OK;
+}
 
 static void *
 pool_main( void * arg ) {
   pool_job_t * j = (pool_job_t *)arg;
+  pin_near_device( j->device );
+  if( hipSetDevice( j->device )!=hipSuccess ) { j->err = tile_fail( "hipSetDevice", hipErrorInvalidDevice ); return NULL; }
   unsigned long nb = (j->n + j->batch_sigs - 1UL) / j->batch_sigs;
+  /* device message capacity: the largest span (direct) or packed size */
   unsigned long msg_cap = 1UL;
+  int stage = !j->direct_in;
   for( unsigned long b=j->rank; b<nb; b+=j->ranks ) {
-    unsigned long i0 = b*j->batch_sigs, i1 = i0+j->batch_sigs < j->n ? i0+j->batch_sigs : j->n, bytes = 0UL;
-    for( unsigned long i=i0; i<i1; i++ ) bytes += j->msg_sz[i];
-    if( bytes>msg_cap ) msg_cap = bytes;
+    unsigned long i0 = b*j->batch_sigs, i1 = i0+j->batch_sigs < j->n ? i0+j->batch_sigs : j->n;
+    unsigned long lo, hi, bytes;
+    batch_span( j, i0, i1, &lo, &hi, &bytes );
+    unsigned long need = bytes;
+    if( j->direct_in && hi-lo<=POOL_SPAN_SLACK( bytes ) ) need = hi-lo;
+    else stage = 1;
+    if( need>msg_cap ) msg_cap = need;
   }
-  fd_ed25519_hip_pipe_t * pipe = fd_ed25519_hip_pipe_new( j->device, j->slot_cnt, j->batch_sigs, msg_cap, 0UL, 0 );
-  if( !pipe ) { j->err = FD_ED25519_HIP_ERR_INVAL; return NULL; }
+  pool_slot_t slot[ 8 ];
+  memset( slot, 0, sizeof(slot) );
+  unsigned sc = j->slot_cnt<1U ? 1U : (j->slot_cnt>8U ? 8U : j->slot_cnt);
+  for( unsigned k=0U; k<sc && !j->err; k++ )
+    j->err = pool_slot_init( &slot[k], j->device, j->batch_sigs, msg_cap, stage, !j->direct_out );
   unsigned long b_sub = j->rank, b_done = j->rank;
-  while( b_done<nb ) {
-    fd_ed25519_hip_slot_t * s = b_sub<nb ? fd_ed25519_hip_pipe_acquire( pipe ) : NULL;
-    if( s ) {
-      unsigned long i0 = b_sub*j->batch_sigs, i1 = i0+j->batch_sigs < j->n ? i0+j->batch_sigs : j->n, pos = 0UL;
-      for( unsigned long i=i0; i<i1; i++ ) {
-        unsigned long k = i-i0;
-        memcpy( s->msgs + pos, j->msgs + j->msg_off[i], j->msg_sz[i] );
-        s->msg_off[k] = pos; s->msg_sz[k] = j->msg_sz[i];
-        pos += j->msg_sz[i];
-      }
-      memcpy( s->sigs, j->sigs + 64UL*i0, 64UL*(i1-i0) );
-      memcpy( s->pubs, j->pubs + 32UL*i0, 32UL*(i1-i0) );
-      s->user = b_sub;
-      int err = fd_ed25519_hip_pipe_submit( pipe, s, i1-i0, pos, 0UL );
+  unsigned next = 0U, oldest = 0U;
+  while( !j->err && b_done<nb ) {
+    pool_slot_t * s = &slot[ next ];
+    if( b_sub<nb && !s->busy ) {
+      int err = pool_submit( j, s, b_sub );
       if( err ) { j->err = err; break; }
       b_sub += j->ranks;
+      next = (next+1U) % sc;
       continue;
     }
-    fd_ed25519_hip_slot_t * d = fd_ed25519_hip_pipe_poll( pipe, 1 );
-    if( !d ) break;
-    memcpy( j->out + d->user*j->batch_sigs, d->sig_out, d->sig_cnt );
-    fd_ed25519_hip_pipe_release( pipe, d );
+    pool_slot_t * d = &slot[ oldest ];
+    hipError_t e = hipEventSynchronize( d->ev );
+    if( e!=hipSuccess ) { j->err = tile_fail( "pool batch", e ); break; }
+    if( !j->direct_out ) memcpy( j->out + d->i0, d->h_out, d->i1 - d->i0 );
+    d->busy = 0;
+    oldest = (oldest+1U) % sc;
     b_done += j->ranks;
   }
-  fd_ed25519_hip_pipe_delete( pipe );
+  for( unsigned k=0U; k<sc; k++ ) pool_slot_fini( &slot[k] );
   return NULL;
 }
 
@@ -984,22 +1172,67 @@ fd_ed25519_hip_pool_verify( int const * devices, unsigned device_cnt, unsigned s
                             unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
                             unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
                             signed char * out, double * seconds ) {
+  return fd_ed25519_hip_pool_verify_ex( devices, device_cnt, slot_cnt, batch_sigs, n, msgs, msg_off, msg_sz, sigs,
+                                        pubs, out, seconds, NULL );
+}
+
+int
+fd_ed25519_hip_pool_verify_ex( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
+                               unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
+                               unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
+                               signed char * out, double * seconds, fd_ed25519_hip_pool_stats_t * stats ) {
   if( !devices || !device_cnt || device_cnt>64U || !batch_sigs || !out ) return FD_ED25519_HIP_ERR_INVAL;
+  if( n && (!msg_off || !msg_sz || !sigs || !pubs || !msgs) ) return FD_ED25519_HIP_ERR_INVAL;
   pool_job_t job[ 64 ];
   pthread_t  th[ 64 ];
+  int direct_in  = n && host_locked( msgs ) && host_locked( msg_off ) && host_locked( msg_sz ) &&
+                   host_locked( sigs ) && host_locked( pubs );
+  int direct_out = n && host_locked( out );
   double t0 = now_s();
   for( unsigned r=0U; r<device_cnt; r++ ) {
-    job[r] = (pool_job_t){ devices[r], slot_cnt, r, device_cnt, batch_sigs, n, msgs, msg_off, msg_sz, sigs, pubs, out, 0 };
+    memset( &job[r], 0, sizeof(job[r]) );
+    job[r].device = devices[r]; job[r].slot_cnt = slot_cnt; job[r].rank = r; job[r].ranks = device_cnt;
+    job[r].batch_sigs = batch_sigs; job[r].n = n; job[r].msgs = msgs; job[r].msg_off = msg_off;
+    job[r].msg_sz = msg_sz; job[r].sigs = sigs; job[r].pubs = pubs; job[r].out = out;
+    job[r].direct_in = direct_in; job[r].direct_out = direct_out;
     if( pthread_create( &th[r], NULL, pool_main, &job[r] ) ) {
       for( unsigned q=0U; q<r; q++ ) pthread_join( th[q], NULL );
       return FD_ED25519_HIP_ERR_NOMEM;
     }
   }
   int err = 0;
+  if( stats ) memset( stats, 0, sizeof(*stats) );
   for( unsigned r=0U; r<device_cnt; r++ ) {
     pthread_join( th[r], NULL );
     if( job[r].err && !err ) err = job[r].err;
+    if( stats ) {
+      stats->direct_batches += job[r].st.direct_batches;
+      stats->staged_batches += job[r].st.staged_batches;
+      stats->h2d_bytes      += job[r].st.h2d_bytes;
+    }
   }
   if( seconds ) *seconds = now_s() - t0;
   return err;
+}
+
+double
+fd_ed25519_hip_h2d_gbps( int device, unsigned long bytes, unsigned reps ) {
+  if( !bytes || !reps || hipSetDevice( device )!=hipSuccess ) return 0.0;
+  void * h = NULL, * d = NULL;
+  hipStream_t st = NULL;
+  double r = 0.0;
+  if( hipHostMalloc( &h, bytes, hipHostMallocDefault )==hipSuccess && hipMalloc( &d, bytes )==hipSuccess &&
+      hipStreamCreateWithFlags( &st, hipStreamNonBlocking )==hipSuccess ) {
+    memset( h, 0x5a, bytes );
+    int ok = hipMemcpyAsync( d, h, bytes, hipMemcpyHostToDevice, st )==hipSuccess &&
+             hipStreamSynchronize( st )==hipSuccess;   /* warm-up */
+    double t0 = now_s();
+    for( unsigned i=0U; ok && i<reps; i++ ) ok = hipMemcpyAsync( d, h, bytes, hipMemcpyHostToDevice, st )==hipSuccess;
+    ok = ok && hipStreamSynchronize( st )==hipSuccess;
+    double dt = now_s() - t0;
+    if( ok && dt>0.0 ) r = (double)bytes * reps / dt * 1e-9;
+  }
+  if( st ) hipStreamDestroy( st );
+  hipFree( d ); hipHostFree( h );
+  return r;
 }

@@ -81,7 +81,8 @@ _lib.fd_ed25519_hip_last_error.restype = ctypes.c_char_p
 class _Info(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("cu_cnt", ctypes.c_int), ("dsm_blocks_per_cu", ctypes.c_int),
                 ("dsm_grid", ctypes.c_uint), ("max_chunk", ctypes.c_ulong), ("device_bytes", ctypes.c_ulong),
-                ("flags", ctypes.c_int), ("arch", ctypes.c_char * 64)]
+                ("flags", ctypes.c_int), ("arch", ctypes.c_char * 64), ("pci_domain", ctypes.c_int),
+                ("pci_bus", ctypes.c_int), ("pci_device", ctypes.c_int)]
 
 
 _lib.fd_ed25519_hip_engine_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Info)]

@@ -70,6 +70,19 @@ _lib.fd_ed25519_hip_pool_verify.argtypes = [_v, ctypes.c_uint, ctypes.c_uint, ct
                                             _v, _v, _v, _v, ctypes.POINTER(ctypes.c_double)]
 
 
+class PoolStats(ctypes.Structure):
+    _fields_ = [("direct_batches", ctypes.c_ulong), ("staged_batches", ctypes.c_ulong), ("h2d_bytes", ctypes.c_ulong)]
+
+
+_lib.fd_ed25519_hip_pool_verify_ex.argtypes = [_v, ctypes.c_uint, ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, _v,
+                                               _v, _v, _v, _v, _v, ctypes.POINTER(ctypes.c_double),
+                                               ctypes.POINTER(PoolStats)]
+_lib.fd_ed25519_hip_host_register.argtypes = [_v, ctypes.c_ulong]
+_lib.fd_ed25519_hip_host_unregister.argtypes = [_v]
+_lib.fd_ed25519_hip_h2d_gbps.argtypes = [ctypes.c_int, ctypes.c_ulong, ctypes.c_uint]
+_lib.fd_ed25519_hip_h2d_gbps.restype = ctypes.c_double
+
+
 def txn_parse(payload):
     """fd_txn_parse: the parsed fields as a dict, or None if rejected."""
     t = Txn()
@@ -188,19 +201,53 @@ def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=25
     return lat, verdict, {f: getattr(res, f) for f, _ in LatencyResult._fields_}
 
 
-def pool_verify(devices, msgs, msg_off, msg_sz, sigs, pubs, batch_sigs=65536, slot_cnt=3):
-    """Signatures dealt round-robin in batches over `devices` (one host thread
-    and pipe per entry) -> (codes, seconds)."""
+def pool_verify(devices, msgs, msg_off, msg_sz, sigs, pubs, batch_sigs=65536, slot_cnt=3, out=None, stats=False):
+    """Signatures dealt round-robin in batches over `devices` (one host
+    feeder thread per entry, fd_ed25519_hip_pool_verify) -> (codes,
+    seconds[, stats]).  Arrays registered with HostRegistration (or numpy
+    views of pinned memory) are DMA'd in place; others are staged."""
     devs = np.ascontiguousarray(devices, np.int32)
     n = len(msg_sz)
-    out = np.zeros(max(n, 1), np.int8)
-    msgs = _c(msgs, np.uint8) if len(msgs) else np.zeros(1, np.uint8)
+    if out is None:
+        out = np.zeros(max(n, 1), np.int8)
+    msgs = msgs if len(msgs) else np.zeros(1, np.uint8)
+    arrs = [_c(msgs, np.uint8), _c(msg_off, np.uint64), _c(msg_sz, np.uint32), _c(sigs, np.uint8).reshape(-1),
+            _c(pubs, np.uint8).reshape(-1)]
     sec = ctypes.c_double(0.0)
-    _check(_lib.fd_ed25519_hip_pool_verify(_ptr(devs), len(devs), int(slot_cnt), int(batch_sigs), n, _ptr(msgs),
-                                           _ptr(_c(msg_off, np.uint64)), _ptr(_c(msg_sz, np.uint32)),
-                                           _ptr(_c(sigs, np.uint8).reshape(-1)), _ptr(_c(pubs, np.uint8).reshape(-1)),
-                                           _ptr(out), ctypes.byref(sec)))
+    st = PoolStats()
+    _check(_lib.fd_ed25519_hip_pool_verify_ex(_ptr(devs), len(devs), int(slot_cnt), int(batch_sigs), n,
+                                              *[_ptr(a) for a in arrs], _ptr(out), ctypes.byref(sec),
+                                              ctypes.byref(st)))
+    if stats:
+        return out[:n], sec.value, {f: getattr(st, f) for f, _ in PoolStats._fields_}
     return out[:n], sec.value
+
+
+class HostRegistration:
+    """Page-locks numpy arrays for direct DMA (fd_ed25519_hip_host_register)
+    for the life of the context."""
+
+    def __init__(self, *arrays):
+        self.arrays = [a for a in arrays if a is not None and a.nbytes]
+        self.done = []
+
+    def __enter__(self):
+        for a in self.arrays:
+            assert a.flags["C_CONTIGUOUS"]
+            _check(_lib.fd_ed25519_hip_host_register(a.ctypes.data, a.nbytes))
+            self.done.append(a)
+        return self
+
+    def __exit__(self, *exc):
+        for a in self.done:
+            _lib.fd_ed25519_hip_host_unregister(a.ctypes.data)
+        self.done = []
+        return False
+
+
+def h2d_gbps(device=0, nbytes=256 << 20, reps=8):
+    """Host -> device copy bandwidth from pinned memory, GB/s."""
+    return _lib.fd_ed25519_hip_h2d_gbps(int(device), int(nbytes), int(reps))
 
 
 # ---- shlink + verify service (the GPU process behind a sandboxed tile) ----

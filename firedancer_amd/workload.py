@@ -162,3 +162,37 @@ def ops_per_verify(msg_sz):
     sqrt_ = 253 * 85 + 21 * 130
     dsm = total - hash_ - 2 * sqrt_
     return dict(total=total, hash=hash_, scalar=np.zeros_like(total), decode=np.full_like(total, 2 * sqrt_), dsm=dsm)
+
+
+def host_cores():
+    """CPU cores this process may use: the cgroup CPU quota (cpu.max, v2; or
+    cpu.cfs_quota_us / cfs_period_us, v1) when one is set, else the
+    scheduler's share the environment states ($OMP_NUM_THREADS, which the
+    GPU box sets to the lease's CPU share), within the affinity mask.  On
+    the GPU box the affinity shows the whole machine (256 CPUs)."""
+    try:
+        n_aff = len(__import__("os").sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n_aff = __import__("os").cpu_count() or 1
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    env = __import__("os").environ.get("OMP_NUM_THREADS", "")
+    share = int(env) if env.isdigit() and int(env) > 0 else None
+    if quota is not None:
+        n, src = min(n_aff, max(1, int(quota))), "cgroup cpu quota"
+    elif share is not None:
+        n, src = min(n_aff, share), "OMP_NUM_THREADS (lease share)"
+    else:
+        n, src = n_aff, "affinity mask"
+    return max(1, n), {"affinity": n_aff, "cgroup_quota": quota, "omp_num_threads": share, "source": src}

@@ -55,7 +55,9 @@ fd_ed25519_verify( unsigned char const   msg[],
                    fd_sha512_t *         sha );
 
 /* Replaces fd_ed25519_verify_batch_single_msg (src/ballet/ed25519/fd_ed25519.h:124-130,
-   implementation src/ballet/ed25519/fd_ed25519_user.c:231-309): batch_sz
+   implementation src/ballet/ed25519/fd_ed25519_user.c:231-309), with the
+   reference's parameter spellings (array bounds included, so the two
+   headers compile together: tests/test_abi.py): batch_sz
    signatures (64 B each, contiguous) by batch_sz public keys (32 B each,
    contiguous) over one message.  batch_sz==0 or >16 -> FD_ED25519_ERR_SIG.
    Otherwise the first phase-1 error (bad S, undecodable or small-order key
@@ -64,9 +66,9 @@ fd_ed25519_verify( unsigned char const   msg[],
 int
 fd_ed25519_verify_batch_single_msg( unsigned char const   msg[],
                                     unsigned long const   msg_sz,
-                                    unsigned char const   signatures[],
-                                    unsigned char const   pubkeys[],
-                                    fd_sha512_t *         shas[],
+                                    unsigned char const   signatures[ 64 ], /* 64 * batch_sz */
+                                    unsigned char const   pubkeys[ 32 ],    /* 32 * batch_sz */
+                                    fd_sha512_t *         shas[ 1 ],        /* batch_sz      */
                                     unsigned char const   batch_sz );
 
 /* Replaces fd_ed25519_strerror (src/ballet/ed25519/fd_ed25519_user.c:311-321). */
@@ -100,22 +102,11 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
 #define FD_ED25519_HIP_FLAG_DSM_OCT        (16)
 #define FD_ED25519_HIP_QUAD_MAX_DEFAULT    (32768UL)
 #define FD_ED25519_HIP_OCT_MAX_DEFAULT     (8192UL)
-/* Dual: a batch larger than 2 x FD_ED25519_HIP_QUAD_MAX_DEFAULT runs as two
-   chunks on two streams with their own scratch, so the kernels of one fill
-   the other's phase tails ($FD_ED25519_HIP_DUAL=0/1 overrides the default).
-   Per-phase timing (fd_ed25519_hip_engine_timing) runs the single-stream
-   sequence.  FLAG_SINGLE never allocates the second set. */
-#define FD_ED25519_HIP_FLAG_SINGLE         (32)
-#define FD_ED25519_HIP_DUAL_DEFAULT        (0)
 /* Overlap: a large chunk's decode phase (A and R need neither the hash nor
    the scalars) runs on a side stream beside its hash and scalar phases, dsm
    after both: +1% at 1M, measured.  Per-phase timing runs the phases in
    sequence.  ($FD_ED25519_HIP_OVERLAP=0/1 overrides.) */
 #define FD_ED25519_HIP_OVERLAP_DEFAULT     (1)
-/* Drain (with the overlap): the last $FD_ED25519_HIP_TAIL signatures of a
-   large chunk are verified a quad of lanes per signature on the side stream,
-   in the slots the one-lane dsm kernel frees as its work runs out. */
-#define FD_ED25519_HIP_TAIL_DEFAULT        (0UL)
 
 /* Creates an engine on HIP device `device`.  max_chunk is the number of
    signatures processed per kernel sequence (0 = default 1<<20); larger
@@ -136,6 +127,9 @@ typedef struct {
   unsigned long device_bytes;   /* device memory held by the engine */
   int           flags;
   char          arch[ 64 ];
+  int           pci_domain;     /* the device's PCI address (tells ranks' devices apart) */
+  int           pci_bus;
+  int           pci_device;
 } fd_ed25519_hip_info_t;
 
 int
@@ -149,7 +143,10 @@ fd_ed25519_hip_engine_stream( fd_ed25519_hip_engine_t * engine );
    is sigs[64 i .. 64 i + 64) = R || S over message msgs[msg_off[i] ..
    msg_off[i] + msg_sz[i]) by public key pubs[32 i .. 32 i + 32); out[i]
    receives its code.  sigs and pubs must be 16-byte aligned; messages may
-   start at any byte.  Enqueued on `stream` (NULL = the engine's stream) and
+   start at any byte, and the message buffer must stay readable at least 16
+   bytes past the end of the last message (the SHA-512 loader reads aligned
+   16-byte granules, up to 15 bytes beyond a message's last byte; the same
+   holds for fd_ed25519_hip_sign_dev / _gen_dev).  Enqueued on `stream` (NULL = the engine's stream) and
    returns immediately; the engine's work arrays are reused by the next
    call, so calls on one engine must be ordered on one stream. */
 int

@@ -309,15 +309,50 @@ fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_
 
 /* Verifies n signatures (host SoA as in fd_ed25519_hip_verify_host) on
    device_cnt GPUs: batches of batch_sigs signatures are dealt round-robin,
-   batch b to device devices[b % device_cnt]; one host thread per device
-   packs its batches into its pipe (slot_cnt in flight) and writes the
-   codes into out.  Returns 0 or an engine status; *seconds (optional) is
-   the wall time of the whole call. */
+   batch b to device devices[b % device_cnt] (the reference's
+   seq % verify_tile_count, src/app/fdctl/run/tiles/fd_verify.c:46); one
+   host thread per device, on the CPUs of that GPU's NUMA node, keeps
+   slot_cnt (1..8) batches in flight and writes the codes into out.
+
+   When msgs, msg_off, msg_sz, sigs and pubs are page-locked
+   (fd_ed25519_hip_host_register or hipHostMalloc), a batch is DMA'd from
+   them as it is (its messages as the one byte range they span) and the
+   host never copies a byte; when out is page-locked too, the codes are
+   DMA'd into it.  Otherwise batches are packed into pinned staging first.
+   Returns 0 or an engine status; *seconds (optional) is the wall time of
+   the whole call. */
 int
 fd_ed25519_hip_pool_verify( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
                             unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
                             unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
                             signed char * out, double * seconds );
+
+typedef struct {
+  unsigned long direct_batches;   /* DMA'd from the caller's page-locked arrays */
+  unsigned long staged_batches;   /* packed into pinned staging first          */
+  unsigned long h2d_bytes;        /* bytes moved host -> device                */
+} fd_ed25519_hip_pool_stats_t;
+
+/* The same, with transfer statistics (stats may be NULL). */
+int
+fd_ed25519_hip_pool_verify_ex( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
+                               unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
+                               unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
+                               signed char * out, double * seconds, fd_ed25519_hip_pool_stats_t * stats );
+
+/* Page-locks [ptr, ptr+sz) of the caller's memory for every device
+   (hipHostRegister, portable + mapped) so the pool and the pipe DMA
+   directly from it; unregister with the same ptr. */
+int
+fd_ed25519_hip_host_register( void * ptr, unsigned long sz );
+
+int
+fd_ed25519_hip_host_unregister( void * ptr );
+
+/* Host -> device copy bandwidth of `device` in GB/s: reps copies of bytes
+   from a pinned buffer (the PCIe bound of a host-fed batch). */
+double
+fd_ed25519_hip_h2d_gbps( int device, unsigned long bytes, unsigned reps );
 
 #ifdef __cplusplus
 }

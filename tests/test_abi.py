@@ -70,3 +70,44 @@ def test_python_mirror_imports_without_gpu():
     from firedancer_amd import ed25519
     assert ed25519.strerror(-2) == "bad public key"
     assert ed25519.SUCCESS == 0 and ed25519.ERR_MSG == -3
+
+
+REF_SRC = "/root/reference/src"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference sources not present (GPU box)")
+def test_headers_compile_with_the_reference_header(tmp_path):
+    """The drop-in prototypes are the reference's own: a translation unit
+    that includes src/ballet/ed25519/fd_ed25519.h and include/*.h together
+    compiles warning-free (-Werror, array-parameter bounds included), and
+    the drop-ins convert to pointers of the reference's exact types."""
+    import subprocess
+    src = tmp_path / "both.c"
+    src.write_text("""
+#include "ballet/ed25519/fd_ed25519.h"
+#include "fd_ed25519_hip.h"
+#include "fd_ed25519_hip_tile.h"
+static int (*p1)( uchar const *, ulong, uchar const *, uchar const *, fd_sha512_t * ) = fd_ed25519_verify;
+static int (*p2)( uchar const *, ulong const, uchar const *, uchar const *, fd_sha512_t **, uchar const ) =
+  fd_ed25519_verify_batch_single_msg;
+static char const * (*p3)( int ) = fd_ed25519_strerror;
+int main( void ) { return (p1!=0) + (p2!=0) + (p3!=0) - 3; }
+""")
+    defs = ["-DFD_HAS_INT128=1", "-DFD_HAS_DOUBLE=1", "-DFD_HAS_ALLOCA=1", "-DFD_HAS_X86=1", "-DFD_IS_X86_64=1",
+            "-DFD_HAS_SSE=1", "-DFD_HAS_AVX=1", "-DFD_HAS_THREADS=1", "-DFD_HAS_ATOMIC=1"]
+    r = subprocess.run(["gcc", "-std=c17", "-march=haswell", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", *defs,
+                        "-I" + REF_SRC, "-I" + os.path.join(REPO, "include"), str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_headers_compile_as_c_and_cxx(tmp_path):
+    """include/*.h alone, as C11 and as C++17 (extern "C"), warning-free."""
+    import subprocess
+    src = tmp_path / "h.c"
+    src.write_text('#include "fd_ed25519_hip.h"\n#include "fd_ed25519_hip_tile.h"\nint main(void){return 0;}\n')
+    for cc, std in (("gcc", "-std=c11"), ("g++", "-std=c++17")):
+        args = [cc, std, "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-I" + os.path.join(REPO, "include")]
+        if cc == "g++":
+            args += ["-x", "c++"]
+        r = subprocess.run(args + [str(src)], capture_output=True, text=True)
+        assert r.returncode == 0, (cc, r.stderr)

@@ -171,30 +171,15 @@ def test_dsm_form_by_size(fd, oracle, monkeypatch):
     e.close()
 
 
-def test_fused_prep_large_chunks(fd, oracle, monkeypatch):
-    """$FD_ED25519_HIP_FUSED=1 (A/B path): the wave-specialised prep kernel
-    with the length sort for one-lane-per-signature chunks."""
-    monkeypatch.setenv("FD_ED25519_HIP_FUSED", "1")
-    e = fd.Engine(0, max_chunk=1 << 12, dsm="wide")
-    d = _random_set(oracle, 1500, seed=18)
-    _check(_run(e, d), oracle_many(oracle, d, 0))
-    e.close()
-
-
 @pytest.mark.parametrize("env", [
     {"FD_ED25519_HIP_OVERLAP": "0"},
-    {"FD_ED25519_HIP_DUAL": "1"},
-    {"FD_ED25519_HIP_DUAL": "1", "FD_ED25519_HIP_DUAL_SKEW": "1"},
-    {"FD_ED25519_HIP_DUAL": "1", "FD_ED25519_HIP_DUAL_SKEW": "3"},
-    {"FD_ED25519_HIP_TAIL": "200"},
-], ids=["sequential", "dual", "dual-skew1", "dual-skew3", "drain"])
+    {"FD_ED25519_HIP_OVERLAP": "1"},
+], ids=["sequential", "overlap"])
 def test_launch_options_large_chunks(fd, oracle, monkeypatch, env):
-    """The engine's launch options for one-lane-per-signature chunks (the
-    small-chunk threshold lowered so the batches stay small): phases in
-    sequence on one stream, two chunks on two streams with their own
-    scratch (optionally the second started behind the first), and the dsm4
-    drain of a chunk's last items on the side stream -- each against the
-    oracle, over a batch of two chunks."""
+    """The engine's two launch sequences for one-lane-per-signature chunks
+    (the small-chunk threshold lowered so the batches stay small): phases in
+    sequence on one stream, and decode on the side stream beside hash +
+    scalar -- each against the oracle, over a batch of two chunks."""
     monkeypatch.setenv("FD_ED25519_HIP_QUAD_MAX", "300")
     monkeypatch.setenv("FD_ED25519_HIP_OCT_MAX", "100")
     for k, v in env.items():

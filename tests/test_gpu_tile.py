@@ -82,11 +82,9 @@ def test_latency_run_unpaced(tile, ref, frags):
     assert np.array_equal(got, want)
 
 
-def test_pool_matches_engine(tile, oracle):
-    from firedancer_amd import ed25519
-    rng = random.Random(9)
-    signer = Signer(oracle, 9)
-    n = 3000
+def _pool_set(oracle, n, seed):
+    rng = random.Random(seed)
+    signer = Signer(oracle, seed)
     msgs, off, sz, sigs, pubs = bytearray(), [], [], bytearray(), bytearray()
     for i in range(n):
         priv, pub = signer.key() if i % 50 == 0 else signer.keys[-1]
@@ -95,17 +93,57 @@ def test_pool_matches_engine(tile, oracle):
         if i % 9 == 4:
             s[rng.randrange(64)] ^= 1
         off.append(len(msgs)); sz.append(len(m)); msgs += m; sigs += s; pubs += pub
-    msgs = np.frombuffer(bytes(msgs), np.uint8)
-    off, sz = np.array(off, np.uint64), np.array(sz, np.uint32)
-    sigs, pubs = np.frombuffer(bytes(sigs), np.uint8), np.frombuffer(bytes(pubs), np.uint8)
-    eng = ed25519.Engine(0, max_chunk=1 << 12)
-    want = eng.verify_host(msgs, off, sz, sigs, pubs)
-    eng.close()
-    for devices, batch in [([0], 1000), ([0, 0], 256), ([0, 0, 0], 7)]:
-        got, sec = tile.pool_verify(devices, msgs, off, sz, sigs, pubs, batch_sigs=batch, slot_cnt=2)
-        assert np.array_equal(got, want), devices
-        assert sec > 0
+    return (np.frombuffer(bytes(msgs), np.uint8).copy(), np.array(off, np.uint64), np.array(sz, np.uint32),
+            np.frombuffer(bytes(sigs), np.uint8).copy(), np.frombuffer(bytes(pubs), np.uint8).copy())
+
+
+@pytest.mark.parametrize("mode", ["staged", "direct", "scattered"])
+def test_pool_vs_oracle(tile, oracle, mode):
+    """The multi-device pool (round-robin batches, one feeder thread per
+    entry; device 0 repeated on a one-GPU box) against the oracle: staged
+    from pageable arrays, DMA'd in place from registered ones, and with the
+    messages scattered in reverse order (their span too wide to DMA as one
+    range: packed)."""
+    from conftest import oracle_many
+    msgs, off, sz, sigs, pubs = _pool_set(oracle, 3000, 9)
+    if mode == "scattered":
+        # messages stored back to front, with 4 KB gaps: each batch's span
+        # is many times its bytes
+        order = np.arange(len(sz))[::-1]
+        parts, noff, pos = [], np.zeros(len(sz), np.uint64), 0
+        for i in order:
+            parts.append(np.zeros(4096, np.uint8))
+            pos += 4096
+            parts.append(msgs[off[i]:off[i] + sz[i]])
+            noff[i] = pos
+            pos += int(sz[i])
+        msgs, off = np.concatenate(parts), noff
+    want = oracle_many(oracle, dict(msgs=msgs, msg_off=off, msg_sz=sz, sigs=sigs.reshape(-1, 64),
+                                    pubs=pubs.reshape(-1, 32)), 0)
     assert (want != 0).sum() > 0
+    out = np.zeros(len(sz), np.int8)
+    for devices, batch in [([0], 1000), ([0, 0], 256), ([0, 0, 0], 7)]:
+        out[:] = 99
+        if mode == "staged":
+            got, sec, st = tile.pool_verify(devices, msgs, off, sz, sigs, pubs, batch_sigs=batch, slot_cnt=2,
+                                            out=out, stats=True)
+            assert st["direct_batches"] == 0 and st["staged_batches"] > 0
+        else:
+            with tile.HostRegistration(msgs, off, sz, sigs, pubs, out):
+                got, sec, st = tile.pool_verify(devices, msgs, off, sz, sigs, pubs, batch_sigs=batch, slot_cnt=3,
+                                                out=out, stats=True)
+            if mode == "direct":
+                assert st["staged_batches"] == 0 and st["direct_batches"] == -(-len(sz) // batch)
+            else:
+                assert st["staged_batches"] > 0
+        bad = np.nonzero(got != want)[0]
+        assert len(bad) == 0, (mode, devices, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]])
+        assert sec > 0
+
+
+def test_h2d_bandwidth_probe(tile):
+    gbps = tile.h2d_gbps(0, 64 << 20, 4)
+    assert gbps > 1.0
 
 
 def test_txn_payload_generator(tile, ref):

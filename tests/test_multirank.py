@@ -85,3 +85,27 @@ def test_gloo_world2_coordination():
     assert all(x[2] == 2 for x in res)
     assert all(x[3] == 2.0 for x in res)      # max over ranks of (1 + rank)
     assert all(x[4] == 3.0 for x in res)      # sum over ranks of 3 * rank
+
+
+def test_bench_spawns_its_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts two ranks itself
+    (child processes, rank r on device r) which rendezvous over gloo and
+    then refuse to run here: there is no GPU, so local rank 0 already has
+    no device of its own -- the check that keeps two ranks from silently
+    sharing one device (--gpus N was ignored)."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "[rank 0] local rank 0 but only 0 visible GPU(s)" in r.stderr
+    assert "[rank 1] local rank 1 but only 0 visible GPU(s)" in r.stderr
+    assert r.stdout == ""
+
+
+def test_bench_rejects_a_launcher_world_that_differs_from_gpus():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 2 and "--gpus 2 but the launcher started 1 ranks" in r.stderr

@@ -114,3 +114,82 @@ def test_join_missing_fails():
     with pytest.raises(Exception):
         tile.ShLink(f"/fdt_missing_{uuid.uuid4().hex[:12]}")
     assert os.path.exists(tile.PRODUCER_BIN)
+
+
+# shared layout (host/fd_ed25519_hip_shlink.c): a 128-byte header
+# (magic, depth, chunk_cnt, mtu, pad, consumed, pad) then 32-byte mcache
+# lines (seq, sig, chunk u32, sz u16, ctl u16, tsorig, tspub)
+_HDR, _LINE = 128, 32
+
+
+def _shm(name):
+    return open("/dev/shm" + name, "r+b", buffering=0)
+
+
+def _poke(f, off, fmt, *vals):
+    import struct
+    f.seek(off)
+    f.write(struct.pack(fmt, *vals))
+
+
+def test_hostile_header_is_ignored_after_join():
+    """A compromised peer rewrites depth / chunk_cnt / mtu in the shared
+    header after both sides joined: both sides keep the geometry they
+    validated at join, so publish and consume stay inside the mapping and
+    the MTU-sized buffer (the service must not trust the tile)."""
+    name = f"/fdt_hh_{uuid.uuid4().hex[:12]}"
+    a = tile.ShLink(name, 8, create=True)
+    b = tile.ShLink(name)
+    try:
+        with _shm(name) as f:
+            _poke(f, 8, "<QQQ", 1 << 40, 1 << 40, 65535)
+        # a frag above the MTU is refused by the producer's local MTU
+        with pytest.raises(Exception):
+            a.publish(b"\0" * (tile.TXN_MTU + 1), 0)
+        for i in range(8):
+            assert a.publish(bytes([i]) * 100, i)
+        assert not a.publish(b"x", 99)   # credits still counted against depth 8
+        for i in range(8):
+            assert b.consume() == (bytes([i]) * 100, i, 0)
+    finally:
+        b.close()
+        a.close()
+
+
+@pytest.mark.parametrize("field", ["chunk", "sz"])
+def test_hostile_frag_is_refused(field):
+    """A published line whose chunk points past the dcache or whose size is
+    above the MTU: consume refuses it (-1, an overrun for the caller)
+    instead of copying out of bounds (the reference tile's own check,
+    src/app/fdctl/run/tiles/fd_verify.c:67)."""
+    name = f"/fdt_hf_{uuid.uuid4().hex[:12]}"
+    a = tile.ShLink(name, 8, create=True)
+    b = tile.ShLink(name)
+    try:
+        assert a.publish(b"hello", 7)
+        with _shm(name) as f:
+            line = _HDR + 0 * _LINE
+            if field == "chunk":
+                _poke(f, line + 16, "<I", 0xFFFFFFF0)
+            else:
+                _poke(f, line + 20, "<H", 65535)
+        with pytest.raises(Exception):
+            b.consume()
+    finally:
+        b.close()
+        a.close()
+
+
+def test_join_rejects_bad_geometry():
+    """A header whose geometry differs from what create makes (MTU, depth
+    not a power of two) is refused at join."""
+    for off, fmt, val in ((24, "<Q", 65535), (8, "<Q", 6)):
+        name = f"/fdt_bg_{uuid.uuid4().hex[:12]}"
+        a = tile.ShLink(name, 8, create=True)
+        try:
+            with _shm(name) as f:
+                _poke(f, off, fmt, val)
+            with pytest.raises(Exception):
+                tile.ShLink(name)
+        finally:
+            a.close()

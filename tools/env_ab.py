@@ -5,7 +5,7 @@ defaults) a fresh engine verifies the same signatures; whole-step wall time
 over K steps (no per-phase events), verdicts checked; specs interleaved.
 
     python tools/env_ab.py N STEPS REPS SPEC...
-    e.g. python tools/env_ab.py 1048576 20 3 - FD_ED25519_HIP_DUAL=1,FD_ED25519_HIP_DUAL_SKEW=1
+    e.g. python tools/env_ab.py 1048576 20 3 - FD_ED25519_HIP_OVERLAP=0
 """
 import os
 import sys
@@ -16,7 +16,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from firedancer_amd import ed25519, workload  # noqa: E402
 
-VARS = ("FD_ED25519_HIP_DUAL", "FD_ED25519_HIP_DUAL_SKEW", "FD_ED25519_HIP_OVERLAP", "FD_ED25519_HIP_TAIL", "FD_ED25519_HIP_SIDE_PRIO")
+VARS = ("FD_ED25519_HIP_OVERLAP", "FD_ED25519_HIP_QUAD_MAX", "FD_ED25519_HIP_OCT_MAX")
 
 
 def run(spec, n, steps, cfg):
