@@ -153,6 +153,7 @@ typedef struct {
   uint64_t *       msg_off;    /* [slots] out: into payloads                */
   uint32_t *       msg_sz;     /* [slots] out                               */
   uint8_t *        parse_ok;   /* [ntxn] out                                */
+  uint8_t *        trailer;    /* [ntxn][64] out (optional): fd_txn_t bytes  */
 } fd_ed25519_txn_stage_params_t;
 
 int fd_ed25519_hip_launch_txn_stage( fd_ed25519_txn_stage_params_t const * p, void * stream );

@@ -7,7 +7,8 @@
    reserve its signature slots.  On the device, one lane per transaction:
 
      stage   fd_txn_parse (fd_txn_parse_core.h, the same source the host
-             library compiles) and, if accepted, the gather of its
+             library compiles), with the first 64 bytes of its fd_txn_t
+             (the trailer the tile publishes) and, if accepted, the gather of its
              signatures and signer keys into the aligned SoA the verify
              phases read, with every signature's message pointing at the
              payload's message bytes in place (message_off .. end,
@@ -45,7 +46,7 @@ fd_ed25519_txn_stage_kernel(fd_ed25519_txn_stage_params_t p) {
   const uint8_t* pay = p.payloads + p.pay_off[t];
   const uint32_t sz = p.pay_sz[t];
   fd_ed25519_hip_txn_t tx;
-  const int good = fd_txn_core_parse(pay, sz, &tx);
+  const int good = fd_txn_core_parse(pay, sz, &tx, p.trailer ? p.trailer + 64 * t : nullptr, 64) != 0;
   p.parse_ok[t] = (uint8_t)good;
   const uint32_t cnt = p.txn_cnt[t];
   const uint32_t slots = (cnt >= 1u && cnt <= 16u) ? cnt : 0u;  /* the host reserved these */

@@ -9,7 +9,15 @@
    the compact-u16 rules of src/ballet/txn/fd_compact_u16.h.  Each rule
    below is the reference's CHECK at the cited line; a payload is accepted
    iff every rule holds.  Offsets are read only after the bytes are known
-   to be present. */
+   to be present.
+
+   Besides the summary fields (fd_ed25519_hip_txn_t), the parser can write
+   the reference's fd_txn_t itself, byte for byte (src/ballet/txn/fd_txn.h:
+   the 20-byte header, instr[instr_cnt] of 10 bytes, then the address
+   table lookups of 8 bytes, fd_txn_get_address_tables; little-endian,
+   padding bytes zero as fd_txn_parse writes them), into `full` when its
+   footprint fits full_cap bytes: the trailer the verify tile publishes
+   behind the payload (src/app/fdctl/run/tiles/fd_verify.c:102-133). */
 #ifndef FD_TXN_PARSE_CORE_H
 #define FD_TXN_PARSE_CORE_H
 
@@ -22,6 +30,16 @@
 #define FD_TXN_CORE_ACCT_MAX   128UL
 #define FD_TXN_CORE_INSTR_MAX   64UL
 #define FD_TXN_CORE_LUT_MAX    127UL
+#define FD_TXN_CORE_MAX_SZ     852UL   /* FD_TXN_MAX_SZ, fd_txn.h */
+
+/* fd_txn_footprint (src/ballet/txn/fd_txn.h): header, instructions, LUTs */
+#define FD_TXN_CORE_FOOTPRINT( instr_cnt, lut_cnt ) (20UL + 10UL*(unsigned long)(instr_cnt) + 8UL*(unsigned long)(lut_cnt))
+
+FD_TXN_FN void
+fd_txn_core_st16( unsigned char * d, unsigned long v ) {
+  d[0] = (unsigned char)v;
+  d[1] = (unsigned char)(v >> 8);
+}
 
 /* compact-u16: 1-3 bytes, 7 bits per byte little-endian, minimal encoding
    required; returns the encoded size (0: malformed / truncated) */
@@ -41,8 +59,12 @@ fd_txn_core_cu16( unsigned char const * b, unsigned long avail, unsigned * val )
   return 0UL;
 }
 
-FD_TXN_FN int
-fd_txn_core_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn_t * out ) {
+/* Returns fd_txn_t's footprint (0: rejected).  out (optional): the summary
+   fields; full (optional): fd_txn_t bytes, written only when the footprint
+   is at most full_cap. */
+FD_TXN_FN unsigned long
+fd_txn_core_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn_t * out, unsigned char * full,
+                   unsigned long full_cap ) {
   unsigned long i = 0UL, n;
   unsigned v;
 #define HAVE( k ) ( (unsigned long)(k) <= sz - i )
@@ -89,12 +111,20 @@ fd_txn_core_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn
     unsigned prog = p[ i++ ];
     unsigned ia; CU16( ia );
     if( !HAVE( ia ) ) return 0;
+    unsigned long ia_off = i;
     for( unsigned k=0U; k<ia; k++ ) if( p[ i+k ]>max_acct ) max_acct = p[ i+k ];
     i += ia;
     unsigned dsz; CU16( dsz );
     if( !HAVE( dsz ) ) return 0;
+    unsigned long d_off = i;
     i += dsz;
     if( !(0U<prog && prog<acct_cnt) ) return 0;                                          /* :175 */
+    if( full && 20UL + 10UL*(j+1UL)<=full_cap ) {                                        /* :177-186 */
+      unsigned char * e = full + 20UL + 10UL*j;
+      e[0] = (unsigned char)prog; e[1] = 0;
+      fd_txn_core_st16( e+2, ia ); fd_txn_core_st16( e+4, dsz );
+      fd_txn_core_st16( e+6, ia_off ); fd_txn_core_st16( e+8, d_off );
+    }
   }
   unsigned lut_cnt = 0U;
   unsigned long adtl = 0UL, adtl_w = 0UL;
@@ -104,13 +134,19 @@ fd_txn_core_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn
     if( !HAVE( 34UL*lut_cnt ) ) return 0;
     for( unsigned j=0U; j<lut_cnt; j++ ) {
       if( !HAVE( 32 ) ) return 0;
+      unsigned long a_off = i;
       i += 32UL;
       unsigned w, r;
-      CU16( w );  if( !HAVE( w ) ) return 0;  i += w;
-      CU16( r );  if( !HAVE( r ) ) return 0;  i += r;
+      CU16( w );  if( !HAVE( w ) ) return 0;  unsigned long w_off = i;  i += w;
+      CU16( r );  if( !HAVE( r ) ) return 0;  unsigned long r_off = i;  i += r;
       if( w > FD_TXN_CORE_ACCT_MAX - acct_cnt ) return 0;                                /* :212 */
       if( r > FD_TXN_CORE_ACCT_MAX - acct_cnt ) return 0;
       if( w + r < 1U ) return 0;
+      if( full && FD_TXN_CORE_FOOTPRINT( instr_cnt, j+1U )<=full_cap ) {                 /* :216-222 */
+        unsigned char * e = full + FD_TXN_CORE_FOOTPRINT( instr_cnt, j );
+        fd_txn_core_st16( e, a_off ); e[2] = (unsigned char)w; e[3] = (unsigned char)r;
+        fd_txn_core_st16( e+4, w_off ); fd_txn_core_st16( e+6, r_off );
+      }
       adtl_w += w;
       adtl   += (unsigned long)w + r;
     }
@@ -135,7 +171,18 @@ fd_txn_core_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn
     out->addr_table_adtl_writable_cnt = (unsigned char)adtl_w;
     out->addr_table_adtl_cnt          = (unsigned char)adtl;
   }
-  return 1;
+  unsigned long foot = FD_TXN_CORE_FOOTPRINT( instr_cnt, lut_cnt );
+  if( full && foot<=full_cap ) {                                                         /* :145-157, :238-243 */
+    full[0] = ver;                              full[1] = (unsigned char)sig_cnt;
+    fd_txn_core_st16( full+2,  sig_off );       fd_txn_core_st16( full+4,  msg_off );
+    full[6] = (unsigned char)ro_signed;         full[7] = (unsigned char)ro_unsigned;
+    fd_txn_core_st16( full+8,  acct_cnt );      fd_txn_core_st16( full+10, acct_off );
+    fd_txn_core_st16( full+12, bh_off );
+    full[14] = (unsigned char)lut_cnt;          full[15] = (unsigned char)adtl_w;
+    full[16] = (unsigned char)adtl;             full[17] = 0;
+    fd_txn_core_st16( full+18, instr_cnt );
+  }
+  return foot;
 }
 
 #endif

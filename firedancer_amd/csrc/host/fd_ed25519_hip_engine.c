@@ -262,6 +262,7 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   }
   char const * ovs = getenv( "FD_ED25519_HIP_OVERLAP" );
   e->overlap = ovs ? ovs[0]=='1' : FD_ED25519_HIP_OVERLAP_DEFAULT;
+  if( flags & FD_ED25519_HIP_FLAG_ONE_STREAM ) e->overlap = 0;
   /* dsm4 (a quad of lanes per signature) below the size where one lane
      per signature fills the chip; its lane tables live in the atab scratch */
   uint64_t quad_cap = atab_sz / (4UL * FD_ED25519_QUAD_LANE_BYTES);

@@ -77,7 +77,7 @@ struct fd_ed25519_hip_shlink {
 
 static uint64_t
 shlink_mtu_chunks( void ) {
-  return (FD_ED25519_HIP_TXN_MTU + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
+  return (FD_ED25519_HIP_SHLINK_MTU + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
 }
 
 static size_t
@@ -115,7 +115,7 @@ fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
   }
   l->hdr->depth     = l->depth     = depth;
   l->hdr->chunk_cnt = l->chunk_cnt = chunk_cnt;
-  l->hdr->mtu       = l->mtu       = FD_ED25519_HIP_TXN_MTU;
+  l->hdr->mtu       = l->mtu       = FD_ED25519_HIP_SHLINK_MTU;
   atomic_store_explicit( &l->hdr->consumed, 0UL, memory_order_relaxed );
   atomic_thread_fence( memory_order_release );
   l->hdr->magic = SHLINK_MAGIC;
@@ -138,7 +138,7 @@ fd_ed25519_hip_shlink_join( char const * name ) {
   uint64_t chunk_cnt = l->hdr->chunk_cnt;
   uint64_t mtu       = l->hdr->mtu;
   if( magic!=SHLINK_MAGIC || !depth || (depth & (depth-1UL)) || depth>(1UL<<30) ||
-      mtu!=FD_ED25519_HIP_TXN_MTU || chunk_cnt!=(depth + 2UL) * shlink_mtu_chunks() ||
+      mtu!=FD_ED25519_HIP_SHLINK_MTU || chunk_cnt!=(depth + 2UL) * shlink_mtu_chunks() ||
       shlink_footprint( depth, chunk_cnt )!=l->map_sz ) {
     munmap( l->hdr, l->map_sz ); free( l ); return NULL;
   }
@@ -201,7 +201,7 @@ fd_ed25519_hip_shlink_consume( fd_ed25519_hip_shlink_t * l, unsigned char * payl
   unsigned int  c     = m->ctl;
   unsigned long chunk = m->chunk;
   /* the frag must lie inside this side's dcache and fit the caller's
-     FD_ED25519_HIP_TXN_MTU-byte buffer (fd_verify.c:67) */
+     FD_ED25519_HIP_SHLINK_MTU-byte buffer (fd_verify.c:67) */
   if( n>l->mtu || chunk>=l->chunk_cnt || chunk*SHLINK_CHUNK + n>l->chunk_cnt*SHLINK_CHUNK ) return -1;
   if( n ) memcpy( payload, l->dcache + chunk*SHLINK_CHUNK, n );
   atomic_thread_fence( memory_order_acquire );

@@ -65,6 +65,7 @@ typedef struct {
   unsigned char *           h_in;
   unsigned char *           d_in;
   unsigned long             in_msgs;    /* offset of msgs in both blocks */
+  unsigned long             out_trl;    /* offset of the trailers in both output blocks */
   signed char *             h_outb;
   signed char *             d_outb;
   unsigned char *           d_msgs;
@@ -76,6 +77,7 @@ typedef struct {
   unsigned int *            d_tfirst;
   unsigned int *            d_tcnt;
   signed char *             d_tout;
+  unsigned char *           d_trailer; /* raw mode: 64 bytes of fd_txn_t per transaction       */
   unsigned long *           d_soff;    /* raw mode: per-signature message offset (device-made) */
   unsigned int *            d_ssz;     /* raw mode: per-signature message size             */
   unsigned char *           d_pok;     /* raw mode: fd_txn_parse accepted                  */
@@ -114,7 +116,7 @@ fd_ed25519_hip_pipe_delete( fd_ed25519_hip_pipe_t * pipe ) {
 static int
 pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned long msg_cap, unsigned long txn_cap,
                 int flags ) {
-  s->eng = fd_ed25519_hip_engine_new( device, sig_cap, flags );
+  s->eng = fd_ed25519_hip_engine_new( device, sig_cap, flags | FD_ED25519_HIP_FLAG_ONE_STREAM );
   if( !s->eng ) return FD_ED25519_HIP_ERR_INVAL;
   fd_ed25519_hip_slot_t * p = &s->pub;
   p->sig_cap = sig_cap; p->msg_cap = msg_cap; p->txn_cap = txn_cap;
@@ -131,10 +133,13 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   unsigned long o_msgs = (o_tc  + 4UL*tc + 255UL) & ~255UL;
   unsigned long in_sz  = o_msgs + msg_cap + 64UL;
   s->in_msgs = o_msgs;
-  TCHK( hipHostMalloc( (void **)&s->h_in,   in_sz,               hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&s->h_outb, sig_cap + tc,        hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipMalloc(     (void **)&s->d_in,   in_sz                                     ), "hipMalloc" );
-  TCHK( hipMalloc(     (void **)&s->d_outb, sig_cap + tc                              ), "hipMalloc" );
+  /* codes out: [sig_out | txn_out | trailers (64 B per transaction)] */
+  s->out_trl = (sig_cap + tc + 63UL) & ~63UL;
+  unsigned long out_sz = s->out_trl + 64UL*tc;
+  TCHK( hipHostMalloc( (void **)&s->h_in,   in_sz,  hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&s->h_outb, out_sz, hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipMalloc(     (void **)&s->d_in,   in_sz                        ), "hipMalloc" );
+  TCHK( hipMalloc(     (void **)&s->d_outb, out_sz                       ), "hipMalloc" );
   p->sigs        = s->h_in + o_sigs;                   s->d_sigs   = s->d_in + o_sigs;
   p->pubs        = s->h_in + o_pubs;                   s->d_pubs   = s->d_in + o_pubs;
   p->msg_off     = (unsigned long *)(s->h_in + o_off); s->d_off    = (unsigned long *)(s->d_in + o_off);
@@ -144,6 +149,7 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   p->msgs        = s->h_in + o_msgs;                   s->d_msgs   = s->d_in + o_msgs;
   p->sig_out     = s->h_outb;                          s->d_out    = s->d_outb;
   p->txn_out     = s->h_outb + sig_cap;                s->d_tout   = s->d_outb + sig_cap;
+  p->txn_trailer = (unsigned char *)s->h_outb + s->out_trl;  s->d_trailer = (unsigned char *)s->d_outb + s->out_trl;
   TCHK( hipMalloc( (void **)&s->d_soff, 8UL*sig_cap ), "hipMalloc" );
   TCHK( hipMalloc( (void **)&s->d_ssz,  4UL*sig_cap ), "hipMalloc" );
   TCHK( hipMalloc( (void **)&s->d_pok,  tc          ), "hipMalloc" );
@@ -206,10 +212,11 @@ slot_h2d( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long 
 }
 
 /* D2H of the codes: [sig_out | txn_out] in one copy when transactions are
-   combined (txn_out sits after sig_cap signature codes), else sig_out */
+   combined (txn_out sits after sig_cap signature codes), else sig_out;
+   with the device-parsed trailers too (raw mode) */
 static int
-slot_d2h( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt ) {
-  unsigned long n = txn_cnt ? s->pub.sig_cap + txn_cnt : sig_cnt;
+slot_d2h( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt, int trailers ) {
+  unsigned long n = trailers ? s->out_trl + 64UL*txn_cnt : (txn_cnt ? s->pub.sig_cap + txn_cnt : sig_cnt);
   if( n ) TCHK( hipMemcpyAsync( s->h_outb, s->d_outb, n, hipMemcpyDeviceToHost, st ), "D2H codes" );
   return FD_ED25519_HIP_OK;
 }
@@ -245,7 +252,7 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
     err = fd_ed25519_hip_txn_combine_dev( s->eng, txn_cnt, s->d_out, s->d_tfirst, s->d_tcnt, s->d_tout, st );
     if( err ) return err;
   }
-  err = slot_d2h( s, st, sig_cnt, txn_cnt );
+  err = slot_d2h( s, st, sig_cnt, txn_cnt, 0 );
   if( err ) return err;
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
   s->state = SLOT_BUSY;
@@ -283,7 +290,7 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
     fd_ed25519_txn_stage_params_t sp;
     sp.payloads = s->d_msgs; sp.pay_off = s->d_off; sp.pay_sz = s->d_sz; sp.txn_first = s->d_tfirst;
     sp.txn_cnt = s->d_tcnt; sp.ntxn = txn_cnt; sp.sigs = s->d_sigs; sp.pubs = s->d_pubs; sp.msg_off = s->d_soff;
-    sp.msg_sz = s->d_ssz; sp.parse_ok = s->d_pok;
+    sp.msg_sz = s->d_ssz; sp.parse_ok = s->d_pok; sp.trailer = s->d_trailer;
     err = fd_ed25519_hip_launch_txn_stage( &sp, st );
     if( err ) return tile_fail( "txn_stage launch", (hipError_t)err );
     if( slots ) {
@@ -293,7 +300,7 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
     }
     err = fd_ed25519_hip_launch_txn_finish( s->d_out, s->d_tfirst, s->d_tcnt, s->d_pok, s->d_tout, txn_cnt, st );
     if( err ) return tile_fail( "txn_finish launch", (hipError_t)err );
-    err = slot_d2h( s, st, slots, txn_cnt );
+    err = slot_d2h( s, st, slots, txn_cnt, 1 );
     if( err ) return err;
   }
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
@@ -340,7 +347,32 @@ fd_ed25519_hip_pipe_in_flight( fd_ed25519_hip_pipe_t const * pipe ) {
 
 int
 fd_ed25519_hip_txn_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn_t * out ) {
-  return fd_txn_core_parse( p, sz, out );
+  return fd_txn_core_parse( p, sz, out, NULL, 0UL ) ? 1 : 0;
+}
+
+unsigned long
+fd_ed25519_hip_txn_parse_full( unsigned char const * p, unsigned long sz, void * out_txn ) {
+  return fd_txn_core_parse( p, sz, NULL, (unsigned char *)out_txn, FD_ED25519_HIP_TXN_MAX_SZ );
+}
+
+/* [payload | pad to 2 | fd_txn_t | u16 payload_sz] (fd_verify.c:102-133) */
+static unsigned long
+txn_frag_core( unsigned char const * p, unsigned long sz, unsigned char * out, fd_ed25519_hip_txn_t * t ) {
+  if( sz>FD_ED25519_HIP_TXN_MTU ) return 0UL;
+  unsigned long toff = (sz + 1UL) & ~1UL;
+  unsigned long foot = fd_txn_core_parse( p, sz, t, out + toff, FD_ED25519_HIP_TXN_MAX_SZ );
+  if( !foot ) return 0UL;
+  memcpy( out, p, sz );
+  if( toff>sz ) out[ sz ] = 0;
+  out[ toff + foot     ] = (unsigned char)sz;
+  out[ toff + foot + 1 ] = (unsigned char)(sz >> 8);
+  return toff + foot + 2UL;
+}
+
+unsigned long
+fd_ed25519_hip_txn_frag( unsigned char const * p, unsigned long sz, unsigned char * out ) {
+  fd_ed25519_hip_txn_t t;
+  return txn_frag_core( p, sz, out, &t );
 }
 
 /* ======================================================================
@@ -441,13 +473,25 @@ fd_ed25519_hip_tcache_insert( fd_ed25519_hip_tcache_t * tc, unsigned long tag ) 
    SUCCESS -> FAILED; else tcache insert -> DEDUP if it was a duplicate, else
    SUCCESS.  Because batches complete in submission order and no frag's
    outcome is decided before the ones ahead of it, the verdict stream is the
-   one the reference tile produces on the same frags. */
+   one the reference tile produces on the same frags.
+
+   Each SUCCESS transaction also yields the frag the reference tile
+   publishes (after_frag, fd_verify.c:102-133: payload, pad, fd_txn_t,
+   payload_sz), built in an output arena: at frag time from the host
+   parse, or -- GPU-parse mode -- at resolve time from the slot's payload
+   copy and the trailer the device parser wrote (a host parse only for the
+   rare fd_txn_t longer than the device's 64-byte trailer slot).  Arena
+   bytes are handed out by vtile_poll_frags in frag order and reclaimed as
+   records are polled. */
 
 typedef struct {
   unsigned long cookie;
   unsigned long tag;
   unsigned long slot_seq;   /* submission seq of its batch (pending)  */
+  unsigned long arena_off;  /* its frag in the output arena            */
+  unsigned      arena_len;  /* bytes reserved there (0: none)          */
   unsigned      txn_idx;    /* index in its batch                      */
+  unsigned short frag_sz;   /* the frag's size (new_sz), 0: none       */
   signed char   verdict;
   unsigned char resolved;
 } vrec_t;
@@ -462,6 +506,8 @@ struct fd_ed25519_hip_vtile {
   vrec_t *                  q;          /* circular FIFO of records */
   unsigned long             q_cap, q_head, q_cnt;
   unsigned long             resolved_head;  /* records [q_head, q_head+resolved_head) are resolved */
+  unsigned char *           oa;         /* output arena: frags, live bytes [oa_head, oa_tail) */
+  unsigned long             oa_cap, oa_head, oa_tail;
 };
 
 fd_ed25519_hip_vtile_t *
@@ -476,7 +522,9 @@ fd_ed25519_hip_vtile_new( int device, unsigned slot_cnt, unsigned long batch_sig
   vt->tc   = fd_ed25519_hip_tcache_new( tcache_depth, tcache_map_cnt );
   vt->q_cap = 1024UL;
   vt->q = (vrec_t *)malloc( vt->q_cap*sizeof(vrec_t) );
-  if( !vt->pipe || !vt->tc || !vt->q ) {
+  vt->oa_cap = 1UL<<20;
+  vt->oa = (unsigned char *)malloc( vt->oa_cap );
+  if( !vt->pipe || !vt->tc || !vt->q || !vt->oa ) {
     if( !vt->tc ) fd_ed25519_hip_private_set_error( "vtile_new: bad tcache geometry" );
     fd_ed25519_hip_vtile_delete( vt );
     return NULL;
@@ -490,6 +538,7 @@ fd_ed25519_hip_vtile_delete( fd_ed25519_hip_vtile_t * vt ) {
   fd_ed25519_hip_pipe_delete( vt->pipe );
   fd_ed25519_hip_tcache_delete( vt->tc );
   free( vt->q );
+  free( vt->oa );
   free( vt );
 }
 
@@ -512,6 +561,39 @@ vq_push( fd_ed25519_hip_vtile_t * vt ) {
   vt->q_cnt++;
   memset( r, 0, sizeof(*r) );
   return r;
+}
+
+/* `need` bytes at the arena's tail (64-byte aligned offset): the live
+   region moves to the front, or the arena grows, when the tail is short */
+static unsigned long
+oa_reserve( fd_ed25519_hip_vtile_t * vt, unsigned long need ) {
+  if( vt->oa_tail + need > vt->oa_cap ) {
+    if( vt->oa_head ) {   /* compact: rebase the live records' offsets */
+      unsigned long h = vt->oa_head;
+      memmove( vt->oa, vt->oa + h, vt->oa_tail - h );
+      for( unsigned long k=0UL; k<vt->q_cnt; k++ ) {
+        vrec_t * r = vq_at( vt, k );
+        if( r->arena_len ) r->arena_off -= h;
+      }
+      vt->oa_tail -= h;
+      vt->oa_head  = 0UL;
+    }
+    if( vt->oa_tail + need > vt->oa_cap ) {
+      unsigned long ncap = vt->oa_cap;
+      while( vt->oa_tail + need > ncap ) ncap *= 2UL;
+      unsigned char * n = (unsigned char *)realloc( vt->oa, ncap );
+      if( !n ) { fprintf( stderr, "libfd_ed25519_hip: FATAL: vtile arena allocation failed\n" ); abort(); }
+      vt->oa = n; vt->oa_cap = ncap;
+    }
+  }
+  return vt->oa_tail;
+}
+
+static unsigned
+oa_commit( fd_ed25519_hip_vtile_t * vt, unsigned long off, unsigned long used ) {
+  unsigned long len = (used + 63UL) & ~63UL;
+  vt->oa_tail = off + len;
+  return (unsigned)len;
 }
 
 /* advance resolved_head over the resolved prefix of the FIFO */
@@ -538,6 +620,33 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
     else                                                      v = FD_ED25519_HIP_TXN_VERIFY_SUCCESS;
     r->verdict  = (signed char)v;
     r->resolved = 1;
+    if( v!=FD_ED25519_HIP_TXN_VERIFY_SUCCESS ) { r->frag_sz = 0; continue; }   /* filtered: not published */
+    if( vt->gpu_parse ) {
+      /* the published frag from the payload in the slot and the device's
+         fd_txn_t trailer (host parse when it exceeds the 64-byte slot) */
+      unsigned char const * pay = s->msgs + s->msg_off[ r->txn_idx ];
+      unsigned long         psz = s->msg_sz[ r->txn_idx ];
+      unsigned char const * tr  = s->txn_trailer + 64UL*r->txn_idx;
+      unsigned long foot = FD_ED25519_HIP_TXN_FOOTPRINT( (unsigned long)tr[18] | ((unsigned long)tr[19]<<8),
+                                                         (unsigned long)tr[14] );
+      unsigned long toff = (psz + 1UL) & ~1UL;
+      unsigned long aoff = oa_reserve( vt, toff + FD_ED25519_HIP_TXN_MAX_SZ + 2UL );
+      unsigned char * o = vt->oa + aoff;
+      unsigned long fsz;
+      if( foot<=64UL ) {
+        memcpy( o, pay, psz );
+        if( toff>psz ) o[ psz ] = 0;
+        memcpy( o + toff, tr, foot );
+        o[ toff + foot ] = (unsigned char)psz; o[ toff + foot + 1 ] = (unsigned char)(psz >> 8);
+        fsz = toff + foot + 2UL;
+      } else {
+        fd_ed25519_hip_txn_t t;
+        fsz = txn_frag_core( pay, psz, o, &t );
+      }
+      r->arena_off = aoff;
+      r->arena_len = oa_commit( vt, aoff, fsz );
+      r->frag_sz   = (unsigned short)fsz;
+    }
   }
   vt_advance( vt );
 }
@@ -616,13 +725,18 @@ int
 fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
                            unsigned long cookie ) {
   if( vt->gpu_parse ) return vt_frag_raw( vt, payload, payload_sz, cookie );
+  /* during_frag + after_frag: the payload and its fd_txn_t trailer go
+     into the output arena as the frag the tile publishes on SUCCESS */
   fd_ed25519_hip_txn_t t;
-  if( !fd_ed25519_hip_txn_parse( payload, payload_sz, &t ) ) {
+  unsigned long aoff = oa_reserve( vt, ((payload_sz + 1UL) & ~1UL) + FD_ED25519_HIP_TXN_MAX_SZ + 2UL );
+  unsigned long fsz  = txn_frag_core( payload, payload_sz, vt->oa + aoff, &t );
+  if( !fsz ) {
     vrec_t * r = vq_push( vt );
     r->cookie = cookie; r->verdict = FD_ED25519_HIP_TXN_PARSE_FAILED; r->resolved = 1;
     vt_advance( vt );
     return 0;
   }
+  unsigned alen = oa_commit( vt, aoff, fsz );
   unsigned long nsig   = (t.signature_cnt>=1U && t.signature_cnt<=16U) ? t.signature_cnt : 0UL;
   unsigned long msg_sz = payload_sz - t.message_off;
   vt_open( vt );
@@ -648,7 +762,10 @@ fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * pa
   s->txn_first  [ ti ] = (unsigned int)first;
   s->txn_sig_cnt[ ti ] = t.signature_cnt;   /* 17..127 -> ERR_SIG, no signatures staged */
   vrec_t * r = vq_push( vt );
-  r->cookie   = cookie;
+  r->cookie    = cookie;
+  r->arena_off = aoff;
+  r->arena_len = alen;
+  r->frag_sz   = (unsigned short)fsz;
   memcpy( &r->tag, payload + t.signature_off, 8UL );  /* ha_dedup_tag, fd_verify.h:65 */
   r->slot_seq = vt->open_seq;
   r->txn_idx  = (unsigned)ti;
@@ -663,22 +780,39 @@ fd_ed25519_hip_vtile_flush( fd_ed25519_hip_vtile_t * vt, int wait ) {
 }
 
 unsigned long
-fd_ed25519_hip_vtile_poll( fd_ed25519_hip_vtile_t * vt, int wait, unsigned long max, unsigned long * cookie,
-                           signed char * verdict, unsigned long * tag ) {
+fd_ed25519_hip_vtile_poll_frags( fd_ed25519_hip_vtile_t * vt, int wait, unsigned long max, unsigned long * cookie,
+                                 signed char * verdict, unsigned long * tag, unsigned long * frag_off,
+                                 unsigned long * frag_sz, unsigned char * frag_buf, unsigned long frag_buf_sz ) {
   while( vt_drain_one( vt, 0 ) ) {}
   if( wait && !vt->resolved_head && vt->q_cnt && fd_ed25519_hip_pipe_in_flight( vt->pipe ) ) vt_drain_one( vt, 1 );
-  unsigned long n = 0UL;
+  unsigned long n = 0UL, bo = 0UL;
   while( n<max && vt->resolved_head ) {
     vrec_t * r = vq_at( vt, 0UL );
+    unsigned long fsz = r->verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ? r->frag_sz : 0UL;
+    if( frag_buf && fsz ) {
+      if( bo + fsz > frag_buf_sz ) break;   /* the caller's buffer is full */
+      memcpy( frag_buf + bo, vt->oa + r->arena_off, fsz );
+    }
+    if( frag_off ) frag_off[ n ] = bo;
+    if( frag_sz  ) frag_sz [ n ] = fsz;
+    if( frag_buf && fsz ) bo += (fsz + 63UL) & ~63UL;
     if( cookie  ) cookie [ n ] = r->cookie;
     if( verdict ) verdict[ n ] = r->verdict;
     if( tag     ) tag    [ n ] = r->tag;
+    if( r->arena_len ) vt->oa_head = r->arena_off + r->arena_len;   /* arena bytes come free in record order */
     n++;
     vt->q_head = (vt->q_head+1UL) % vt->q_cap;
     vt->q_cnt--;
     vt->resolved_head--;
   }
+  if( !vt->q_cnt ) vt->oa_head = vt->oa_tail = 0UL;
   return n;
+}
+
+unsigned long
+fd_ed25519_hip_vtile_poll( fd_ed25519_hip_vtile_t * vt, int wait, unsigned long max, unsigned long * cookie,
+                           signed char * verdict, unsigned long * tag ) {
+  return fd_ed25519_hip_vtile_poll_frags( vt, wait, max, cookie, verdict, tag, NULL, NULL, NULL, 0UL );
 }
 
 unsigned long
@@ -867,28 +1001,34 @@ fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_
   fd_ed25519_hip_vtile_t * vt = fd_ed25519_hip_vtile_new( device, slot_cnt, batch_sigs, 16UL, 64UL, flags );
   if( !vt ) return FD_ED25519_HIP_ERR_INVAL;
   enum { QMAX = 4096 };
+  unsigned long   fbsz = QMAX * ((FD_ED25519_HIP_TPU_DCACHE_MTU + 63UL) & ~63UL);
   unsigned long * ck  = (unsigned long *)malloc( QMAX*sizeof(unsigned long) );
+  unsigned long * fo  = (unsigned long *)malloc( QMAX*sizeof(unsigned long) );
+  unsigned long * fs  = (unsigned long *)malloc( QMAX*sizeof(unsigned long) );
   signed char *   vd  = (signed char *)malloc( QMAX );
-  unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_TXN_MTU );
-  if( !ck || !vd || !buf ) {
-    free( ck ); free( vd ); free( buf ); fd_ed25519_hip_vtile_delete( vt );
+  unsigned char * fb  = (unsigned char *)malloc( fbsz );
+  unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
+  if( !ck || !fo || !fs || !vd || !fb || !buf ) {
+    free( ck ); free( fo ); free( fs ); free( vd ); free( fb ); free( buf ); fd_ed25519_hip_vtile_delete( vt );
     return FD_ED25519_HIP_ERR_NOMEM;
   }
   double t0 = now_s();
   unsigned long txns = 0UL, qn = 0UL, qi = 0UL;
   int eos = 0, rc = FD_ED25519_HIP_OK;
   for(;;) {
-    /* verdicts already collected go out first, as far as credits allow */
+    /* verdicts already collected go out first, as far as credits allow:
+       the verdict byte, then (SUCCESS) the frag the tile publishes */
     while( qi<qn ) {
-      unsigned char v = (unsigned char)vd[ qi ];
-      int r = fd_ed25519_hip_shlink_publish( out, &v, 1UL, ck[ qi ], 0U );
+      buf[ 0 ] = (unsigned char)vd[ qi ];
+      if( fs[ qi ] ) memcpy( buf + 1, fb + fo[ qi ], fs[ qi ] );
+      int r = fd_ed25519_hip_shlink_publish( out, buf, 1UL + fs[ qi ], ck[ qi ], 0U );
       if( r==1 ) break;
       if( r ) { rc = r; goto done; }
       qi++;
     }
     if( qi==qn ) {
       qi = qn = 0UL;
-      qn = fd_ed25519_hip_vtile_poll( vt, 0, QMAX, ck, vd, NULL );
+      qn = fd_ed25519_hip_vtile_poll_frags( vt, 0, QMAX, ck, vd, NULL, fo, fs, fb, fbsz );
     }
     if( eos && !qn && !fd_ed25519_hip_vtile_pending( vt ) ) break;
     /* after_frag for every frag that is ready */
@@ -916,7 +1056,7 @@ done:
     stats->batches = vt->pipe->seq;
     stats->seconds = now_s() - t0;
   }
-  free( ck ); free( vd ); free( buf );
+  free( ck ); free( fo ); free( fs ); free( vd ); free( fb ); free( buf );
   fd_ed25519_hip_vtile_delete( vt );
   return rc;
 }
@@ -947,25 +1087,34 @@ typedef struct {
   unsigned char *           d_sigs;
   unsigned char *           d_pubs;
   signed char *             d_out;
-  unsigned char *           h_stage;   /* pinned: [sigs | pubs | off | sz | msgs], staged batches only */
-  signed char *             h_out;     /* pinned codes, when out is pageable                            */
-  unsigned long             b, i0, i1;
+  unsigned char *           h_stage;   /* pinned: [sigs | pubs | off | sz | msgs], staged batches only (lazy) */
+  signed char *             h_out;     /* pinned codes, when out is pageable (lazy)                           */
+  unsigned long             i0, i1;
   int                       busy;
 } pool_slot_t;
 
+#define POOL_DEV_MAX  64U
+#define POOL_SLOT_MAX 8U
+
+struct fd_ed25519_hip_pool {
+  unsigned      device_cnt, slot_cnt;
+  unsigned long batch_sigs, msg_cap;
+  int           device[ POOL_DEV_MAX ];
+  pool_slot_t   slot[ POOL_DEV_MAX ][ POOL_SLOT_MAX ];
+};
+
 typedef struct {
-  int                   device;
-  unsigned              slot_cnt;
-  unsigned              rank, ranks;
-  unsigned long         batch_sigs, n;
-  unsigned char const * msgs;
-  unsigned long const * msg_off;
-  unsigned int const *  msg_sz;
-  unsigned char const * sigs;
-  unsigned char const * pubs;
-  signed char *         out;
-  int                   direct_in, direct_out;   /* caller arrays page-locked */
-  int                   err;
+  fd_ed25519_hip_pool_t * pool;
+  unsigned                rank;
+  unsigned long           n;
+  unsigned char const *   msgs;
+  unsigned long const *   msg_off;
+  unsigned int const *    msg_sz;
+  unsigned char const *   sigs;
+  unsigned char const *   pubs;
+  signed char *           out;
+  int                     direct_in, direct_out;   /* caller arrays page-locked */
+  int                     err;
   fd_ed25519_hip_pool_stats_t st;
 } pool_job_t;
 
@@ -1016,8 +1165,8 @@ pin_near_device( int device ) {
     if( e==t ) break;
     if( *e=='-' ) { t = e+1; hi = strtol( t, &e, 10 ); }
     for( long c=lo; c<=hi && c<CPU_SETSIZE; c++ ) if( c>=0 && CPU_ISSET( (int)c, &cur ) ) CPU_SET( (int)c, &want );
-    t = *e==',' ? e+1 : e;
     if( *e!=',' ) break;
+    t = e+1;
   }
   if( CPU_COUNT( &want ) ) pthread_setaffinity_np( pthread_self(), sizeof(want), &want );
 }
@@ -1037,12 +1186,18 @@ batch_span( pool_job_t const * j, unsigned long i0, unsigned long i1, unsigned l
   *lo = l; *hi = h; *bytes = b;
 }
 
-/* the span goes as it is when it is not much larger than the bytes in it */
-#define POOL_SPAN_SLACK(bytes) (2UL*(bytes) + 65536UL)
+/* the span goes as it is when it fits and is not much larger than the
+   bytes in it */
+static int
+span_direct( fd_ed25519_hip_pool_t const * pl, unsigned long span, unsigned long bytes ) {
+  return span<=pl->msg_cap && span<=2UL*bytes + 65536UL;
+}
 
 static int
-pool_slot_init( pool_slot_t * s, int device, unsigned long batch_sigs, unsigned long msg_cap, int stage, int stage_out ) {
-  s->eng = fd_ed25519_hip_engine_new( device, batch_sigs, 0 );
+pool_slot_init( pool_slot_t * s, int device, unsigned long batch_sigs, unsigned long msg_cap ) {
+  /* one stream per slot: the slots in flight overlap one another, a side
+     stream per slot would only crowd the device's hardware queues */
+  s->eng = fd_ed25519_hip_engine_new( device, batch_sigs, FD_ED25519_HIP_FLAG_ONE_STREAM );
   if( !s->eng ) return FD_ED25519_HIP_ERR_INVAL;
   unsigned long dsz = 112UL*batch_sigs + msg_cap + 64UL + 1024UL;
   unsigned char * d = NULL;
@@ -1053,9 +1208,6 @@ pool_slot_init( pool_slot_t * s, int device, unsigned long batch_sigs, unsigned 
   s->d_sz   = (unsigned int *)d;                     d += 4UL*batch_sigs;
   s->d_out  = (signed char *)d;                      d += (batch_sigs + 255UL) & ~255UL;
   s->d_msgs = d;
-  if( stage ) TCHK( hipHostMalloc( (void **)&s->h_stage, 108UL*batch_sigs + msg_cap + 64UL, hipHostMallocDefault ),
-                    "hipHostMalloc(pool stage)" );
-  if( stage_out ) TCHK( hipHostMalloc( (void **)&s->h_out, batch_sigs, hipHostMallocDefault ), "hipHostMalloc(pool out)" );
   TCHK( hipEventCreateWithFlags( &s->ev, hipEventDisableTiming ), "hipEventCreate" );
   return FD_ED25519_HIP_OK;
 }
@@ -1067,16 +1219,51 @@ pool_slot_fini( pool_slot_t * s ) {
   hipHostFree( s->h_stage ); hipHostFree( s->h_out );
   if( s->ev ) hipEventDestroy( s->ev );
   if( s->eng ) fd_ed25519_hip_engine_delete( s->eng );
+  memset( s, 0, sizeof(*s) );
+}
+
+void
+fd_ed25519_hip_pool_delete( fd_ed25519_hip_pool_t * pl ) {
+  if( !pl ) return;
+  for( unsigned r=0U; r<pl->device_cnt; r++ ) {
+    hipSetDevice( pl->device[r] );
+    for( unsigned k=0U; k<pl->slot_cnt; k++ ) pool_slot_fini( &pl->slot[r][k] );
+  }
+  free( pl );
+}
+
+fd_ed25519_hip_pool_t *
+fd_ed25519_hip_pool_new( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
+                         unsigned long msg_cap ) {
+  if( !devices || !device_cnt || device_cnt>POOL_DEV_MAX || slot_cnt<1U || slot_cnt>POOL_SLOT_MAX || !batch_sigs ) {
+    fd_ed25519_hip_private_set_error( "pool_new: 1..64 devices, 1..8 slots, batch_sigs > 0" );
+    return NULL;
+  }
+  fd_ed25519_hip_pool_t * pl = (fd_ed25519_hip_pool_t *)calloc( 1, sizeof(*pl) );
+  if( !pl ) return NULL;
+  pl->device_cnt = device_cnt; pl->slot_cnt = slot_cnt; pl->batch_sigs = batch_sigs;
+  pl->msg_cap = msg_cap ? msg_cap : 1UL;
+  for( unsigned r=0U; r<device_cnt; r++ ) {
+    pl->device[r] = devices[r];
+    if( hipSetDevice( devices[r] )!=hipSuccess ) { tile_fail( "hipSetDevice", hipErrorInvalidDevice ); goto fail; }
+    for( unsigned k=0U; k<slot_cnt; k++ )
+      if( pool_slot_init( &pl->slot[r][k], devices[r], batch_sigs, pl->msg_cap ) ) goto fail;
+  }
+  return pl;
+fail:
+  fd_ed25519_hip_pool_delete( pl );
+  return NULL;
 }
 
 static int
 pool_submit( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
-  unsigned long i0 = b*j->batch_sigs, i1 = i0+j->batch_sigs < j->n ? i0+j->batch_sigs : j->n, cnt = i1-i0;
+  fd_ed25519_hip_pool_t * pl = j->pool;
+  unsigned long i0 = b*pl->batch_sigs, i1 = i0+pl->batch_sigs < j->n ? i0+pl->batch_sigs : j->n, cnt = i1-i0;
   hipStream_t st = (hipStream_t)fd_ed25519_hip_engine_stream( s->eng );
   unsigned long lo, hi, bytes;
   batch_span( j, i0, i1, &lo, &hi, &bytes );
   unsigned char const * dmsgs;
-  if( j->direct_in && hi-lo<=POOL_SPAN_SLACK( bytes ) ) {
+  if( j->direct_in && span_direct( pl, hi-lo, bytes ) ) {
     if( hi>lo ) TCHK( hipMemcpyAsync( s->d_msgs, j->msgs + lo, hi-lo, hipMemcpyHostToDevice, st ), "H2D msgs" );
     TCHK( hipMemcpyAsync( s->d_off,  j->msg_off + i0, 8UL*cnt,  hipMemcpyHostToDevice, st ), "H2D off"  );
     TCHK( hipMemcpyAsync( s->d_sz,   j->msg_sz  + i0, 4UL*cnt,  hipMemcpyHostToDevice, st ), "H2D sz"   );
@@ -1086,9 +1273,15 @@ pool_submit( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
     j->st.h2d_bytes += (hi-lo) + 108UL*cnt;
     dmsgs = s->d_msgs - lo;   /* msg_off[i] indexes the span from its start */
   } else {
-    /* pack into pinned staging: [sigs | pubs | off | sz | msgs], one DMA */
+    /* pack into pinned staging: [sigs | pubs | off | sz | msgs] */
+    if( bytes>pl->msg_cap ) {
+      fd_ed25519_hip_private_set_error( "pool: a batch's messages exceed the pool's msg_cap" );
+      return FD_ED25519_HIP_ERR_INVAL;
+    }
+    if( !s->h_stage )
+      TCHK( hipHostMalloc( (void **)&s->h_stage, 108UL*pl->batch_sigs + pl->msg_cap + 64UL, hipHostMallocDefault ),
+            "hipHostMalloc(pool stage)" );
     unsigned char * h = s->h_stage;
-    if( !h ) return FD_ED25519_HIP_ERR_INVAL;
     memcpy( h,               j->sigs + 64UL*i0, 64UL*cnt );
     memcpy( h + 64UL*cnt,    j->pubs + 32UL*i0, 32UL*cnt );
     unsigned long * off = (unsigned long *)(h + 96UL*cnt);
@@ -1101,12 +1294,10 @@ pool_submit( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
       off[k] = pos; sz[k] = j->msg_sz[i];
       pos += j->msg_sz[i];
     }
-    /* the device block has the same order at batch_sigs strides: copy the
-       four arrays and the messages separately */
-    TCHK( hipMemcpyAsync( s->d_sigs, h,               64UL*cnt, hipMemcpyHostToDevice, st ), "H2D sigs" );
-    TCHK( hipMemcpyAsync( s->d_pubs, h + 64UL*cnt,    32UL*cnt, hipMemcpyHostToDevice, st ), "H2D pubs" );
-    TCHK( hipMemcpyAsync( s->d_off,  off,             8UL*cnt,  hipMemcpyHostToDevice, st ), "H2D off"  );
-    TCHK( hipMemcpyAsync( s->d_sz,   sz,              4UL*cnt,  hipMemcpyHostToDevice, st ), "H2D sz"   );
+    TCHK( hipMemcpyAsync( s->d_sigs, h,            64UL*cnt, hipMemcpyHostToDevice, st ), "H2D sigs" );
+    TCHK( hipMemcpyAsync( s->d_pubs, h + 64UL*cnt, 32UL*cnt, hipMemcpyHostToDevice, st ), "H2D pubs" );
+    TCHK( hipMemcpyAsync( s->d_off,  off,          8UL*cnt,  hipMemcpyHostToDevice, st ), "H2D off"  );
+    TCHK( hipMemcpyAsync( s->d_sz,   sz,           4UL*cnt,  hipMemcpyHostToDevice, st ), "H2D sz"   );
     if( pos ) TCHK( hipMemcpyAsync( s->d_msgs, m, pos, hipMemcpyHostToDevice, st ), "H2D msgs" );
     j->st.staged_batches++;
     j->st.h2d_bytes += pos + 108UL*cnt;
@@ -1114,95 +1305,73 @@ pool_submit( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
   }
   int err = fd_ed25519_hip_verify_dev( s->eng, cnt, dmsgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
   if( err ) return err;
+  if( !j->direct_out && !s->h_out )
+    TCHK( hipHostMalloc( (void **)&s->h_out, pl->batch_sigs, hipHostMallocDefault ), "hipHostMalloc(pool out)" );
   signed char * dst = j->direct_out ? j->out + i0 : s->h_out;
   TCHK( hipMemcpyAsync( dst, s->d_out, cnt, hipMemcpyDeviceToHost, st ), "D2H codes" );
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
-  s->b = b; s->i0 = i0; s->i1 = i1; s->busy = 1;
+  s->i0 = i0; s->i1 = i1; s->busy = 1;
   return FD_ED25519_HIP_OK;
 }
 
 static void *
 pool_main( void * arg ) {
   pool_job_t * j = (pool_job_t *)arg;
-  pin_near_device( j->device );
-  if( hipSetDevice( j->device )!=hipSuccess ) { j->err = tile_fail( "hipSetDevice", hipErrorInvalidDevice ); return NULL; }
-  unsigned long nb = (j->n + j->batch_sigs - 1UL) / j->batch_sigs;
-  /* device message capacity: the largest span (direct) or packed size */
-  unsigned long msg_cap = 1UL;
-  int stage = !j->direct_in;
-  for( unsigned long b=j->rank; b<nb; b+=j->ranks ) {
-    unsigned long i0 = b*j->batch_sigs, i1 = i0+j->batch_sigs < j->n ? i0+j->batch_sigs : j->n;
-    unsigned long lo, hi, bytes;
-    batch_span( j, i0, i1, &lo, &hi, &bytes );
-    unsigned long need = bytes;
-    if( j->direct_in && hi-lo<=POOL_SPAN_SLACK( bytes ) ) need = hi-lo;
-    else stage = 1;
-    if( need>msg_cap ) msg_cap = need;
-  }
-  pool_slot_t slot[ 8 ];
-  memset( slot, 0, sizeof(slot) );
-  unsigned sc = j->slot_cnt<1U ? 1U : (j->slot_cnt>8U ? 8U : j->slot_cnt);
-  for( unsigned k=0U; k<sc && !j->err; k++ )
-    j->err = pool_slot_init( &slot[k], j->device, j->batch_sigs, msg_cap, stage, !j->direct_out );
+  fd_ed25519_hip_pool_t * pl = j->pool;
+  int dev = pl->device[ j->rank ];
+  pin_near_device( dev );
+  if( hipSetDevice( dev )!=hipSuccess ) { j->err = tile_fail( "hipSetDevice", hipErrorInvalidDevice ); return NULL; }
+  pool_slot_t * slot = pl->slot[ j->rank ];
+  unsigned sc = pl->slot_cnt, ranks = pl->device_cnt;
+  unsigned long nb = (j->n + pl->batch_sigs - 1UL) / pl->batch_sigs;
   unsigned long b_sub = j->rank, b_done = j->rank;
   unsigned next = 0U, oldest = 0U;
-  while( !j->err && b_done<nb ) {
+  while( b_done<nb ) {
     pool_slot_t * s = &slot[ next ];
-    if( b_sub<nb && !s->busy ) {
+    if( !j->err && b_sub<nb && !s->busy ) {
       int err = pool_submit( j, s, b_sub );
-      if( err ) { j->err = err; break; }
-      b_sub += j->ranks;
+      if( err ) { j->err = err; continue; }   /* drain what is in flight */
+      b_sub += ranks;
       next = (next+1U) % sc;
       continue;
     }
     pool_slot_t * d = &slot[ oldest ];
+    if( !d->busy ) break;   /* an error stopped submission and everything drained */
     hipError_t e = hipEventSynchronize( d->ev );
-    if( e!=hipSuccess ) { j->err = tile_fail( "pool batch", e ); break; }
-    if( !j->direct_out ) memcpy( j->out + d->i0, d->h_out, d->i1 - d->i0 );
+    if( e!=hipSuccess && !j->err ) j->err = tile_fail( "pool batch", e );
+    if( !j->direct_out && e==hipSuccess ) memcpy( j->out + d->i0, d->h_out, d->i1 - d->i0 );
     d->busy = 0;
     oldest = (oldest+1U) % sc;
-    b_done += j->ranks;
+    b_done += ranks;
   }
-  for( unsigned k=0U; k<sc; k++ ) pool_slot_fini( &slot[k] );
   return NULL;
 }
 
 int
-fd_ed25519_hip_pool_verify( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
-                            unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
-                            unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
-                            signed char * out, double * seconds ) {
-  return fd_ed25519_hip_pool_verify_ex( devices, device_cnt, slot_cnt, batch_sigs, n, msgs, msg_off, msg_sz, sigs,
-                                        pubs, out, seconds, NULL );
-}
-
-int
-fd_ed25519_hip_pool_verify_ex( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
-                               unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
-                               unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
-                               signed char * out, double * seconds, fd_ed25519_hip_pool_stats_t * stats ) {
-  if( !devices || !device_cnt || device_cnt>64U || !batch_sigs || !out ) return FD_ED25519_HIP_ERR_INVAL;
+fd_ed25519_hip_pool_run( fd_ed25519_hip_pool_t * pl, unsigned long n, unsigned char const * msgs,
+                         unsigned long const * msg_off, unsigned int const * msg_sz, unsigned char const * sigs,
+                         unsigned char const * pubs, signed char * out, double * seconds,
+                         fd_ed25519_hip_pool_stats_t * stats ) {
+  if( !pl || !out ) return FD_ED25519_HIP_ERR_INVAL;
   if( n && (!msg_off || !msg_sz || !sigs || !pubs || !msgs) ) return FD_ED25519_HIP_ERR_INVAL;
-  pool_job_t job[ 64 ];
-  pthread_t  th[ 64 ];
+  pool_job_t job[ POOL_DEV_MAX ];
+  pthread_t  th[ POOL_DEV_MAX ];
   int direct_in  = n && host_locked( msgs ) && host_locked( msg_off ) && host_locked( msg_sz ) &&
                    host_locked( sigs ) && host_locked( pubs );
   int direct_out = n && host_locked( out );
   double t0 = now_s();
-  for( unsigned r=0U; r<device_cnt; r++ ) {
+  unsigned started = 0U;
+  int err = 0;
+  for( unsigned r=0U; r<pl->device_cnt; r++ ) {
     memset( &job[r], 0, sizeof(job[r]) );
-    job[r].device = devices[r]; job[r].slot_cnt = slot_cnt; job[r].rank = r; job[r].ranks = device_cnt;
-    job[r].batch_sigs = batch_sigs; job[r].n = n; job[r].msgs = msgs; job[r].msg_off = msg_off;
+    job[r].pool = pl; job[r].rank = r; job[r].n = n; job[r].msgs = msgs; job[r].msg_off = msg_off;
     job[r].msg_sz = msg_sz; job[r].sigs = sigs; job[r].pubs = pubs; job[r].out = out;
     job[r].direct_in = direct_in; job[r].direct_out = direct_out;
-    if( pthread_create( &th[r], NULL, pool_main, &job[r] ) ) {
-      for( unsigned q=0U; q<r; q++ ) pthread_join( th[q], NULL );
-      return FD_ED25519_HIP_ERR_NOMEM;
-    }
+    if( pthread_create( &th[r], NULL, pool_main, &job[r] ) ) { err = FD_ED25519_HIP_ERR_NOMEM; break; }
+    started++;
   }
-  int err = 0;
   if( stats ) memset( stats, 0, sizeof(*stats) );
-  for( unsigned r=0U; r<device_cnt; r++ ) {
+  for( unsigned r=0U; r<started; r++ ) {
     pthread_join( th[r], NULL );
     if( job[r].err && !err ) err = job[r].err;
     if( stats ) {
@@ -1211,6 +1380,32 @@ fd_ed25519_hip_pool_verify_ex( int const * devices, unsigned device_cnt, unsigne
       stats->h2d_bytes      += job[r].st.h2d_bytes;
     }
   }
+  if( seconds ) *seconds = now_s() - t0;
+  return err;
+}
+
+int
+fd_ed25519_hip_pool_verify( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
+                            unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
+                            unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
+                            signed char * out, double * seconds ) {
+  if( !batch_sigs ) return FD_ED25519_HIP_ERR_INVAL;
+  /* capacity: the largest span of a batch */
+  unsigned long cap = 1UL;
+  pool_job_t tmp;
+  memset( &tmp, 0, sizeof(tmp) );
+  tmp.msg_off = msg_off; tmp.msg_sz = msg_sz;
+  for( unsigned long i0=0UL; n && msg_off && msg_sz && i0<n; i0+=batch_sigs ) {
+    unsigned long lo, hi, bytes;
+    batch_span( &tmp, i0, i0+batch_sigs<n ? i0+batch_sigs : n, &lo, &hi, &bytes );
+    unsigned long need = hi-lo<=2UL*bytes + 65536UL ? hi-lo : bytes;
+    if( need>cap ) cap = need;
+  }
+  fd_ed25519_hip_pool_t * pl = fd_ed25519_hip_pool_new( devices, device_cnt, slot_cnt, batch_sigs, cap );
+  if( !pl ) return FD_ED25519_HIP_ERR_INVAL;
+  double t0 = now_s();
+  int err = fd_ed25519_hip_pool_run( pl, n, msgs, msg_off, msg_sz, sigs, pubs, out, NULL, NULL );
+  fd_ed25519_hip_pool_delete( pl );
   if( seconds ) *seconds = now_s() - t0;
   return err;
 }

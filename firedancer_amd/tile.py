@@ -20,6 +20,9 @@ TXN_VERIFY_DEDUP = -2
 TXN_PARSE_FAILED = -3
 
 TXN_MTU = 1232
+TXN_MAX_SZ = 852                          # FD_TXN_MAX_SZ: the largest fd_txn_t
+TPU_DCACHE_MTU = TXN_MTU + TXN_MAX_SZ + 2   # a published frag: payload, pad, fd_txn_t, payload_sz
+SHLINK_MTU = 1 + TPU_DCACHE_MTU            # a verdict frag: verdict byte + published frag
 VTILE_GPU_PARSE = 2   # FD_ED25519_HIP_VTILE_GPU_PARSE: fd_txn_parse on the device
 
 
@@ -48,6 +51,14 @@ class LatencyResult(ctypes.Structure):
 _v = ctypes.c_void_p
 _lib.fd_ed25519_hip_txn_parse.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.POINTER(Txn)]
 _lib.fd_ed25519_hip_txn_parse.restype = ctypes.c_int
+_lib.fd_ed25519_hip_txn_parse_full.argtypes = [ctypes.c_char_p, ctypes.c_ulong, _v]
+_lib.fd_ed25519_hip_txn_parse_full.restype = ctypes.c_ulong
+_lib.fd_ed25519_hip_txn_frag.argtypes = [ctypes.c_char_p, ctypes.c_ulong, _v]
+_lib.fd_ed25519_hip_txn_frag.restype = ctypes.c_ulong
+_lib.fd_ed25519_hip_txn_parse_full.argtypes = [ctypes.c_char_p, ctypes.c_ulong, _v]
+_lib.fd_ed25519_hip_txn_parse_full.restype = ctypes.c_ulong
+_lib.fd_ed25519_hip_txn_frag.argtypes = [ctypes.c_char_p, ctypes.c_ulong, _v]
+_lib.fd_ed25519_hip_txn_frag.restype = ctypes.c_ulong
 _lib.fd_ed25519_hip_tcache_new.argtypes = [ctypes.c_ulong, ctypes.c_ulong]
 _lib.fd_ed25519_hip_tcache_new.restype = _v
 _lib.fd_ed25519_hip_tcache_delete.argtypes = [_v]
@@ -61,6 +72,9 @@ _lib.fd_ed25519_hip_vtile_frag.argtypes = [_v, ctypes.c_char_p, ctypes.c_ulong, 
 _lib.fd_ed25519_hip_vtile_flush.argtypes = [_v, ctypes.c_int]
 _lib.fd_ed25519_hip_vtile_poll.argtypes = [_v, ctypes.c_int, ctypes.c_ulong, _v, _v, _v]
 _lib.fd_ed25519_hip_vtile_poll.restype = ctypes.c_ulong
+_lib.fd_ed25519_hip_vtile_poll_frags.argtypes = [_v, ctypes.c_int, ctypes.c_ulong, _v, _v, _v, _v, _v, _v,
+                                                 ctypes.c_ulong]
+_lib.fd_ed25519_hip_vtile_poll_frags.restype = ctypes.c_ulong
 _lib.fd_ed25519_hip_vtile_pending.argtypes = [_v]
 _lib.fd_ed25519_hip_vtile_pending.restype = ctypes.c_ulong
 _lib.fd_ed25519_hip_latency_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, _v, _v, _v, ctypes.c_ulong,
@@ -74,9 +88,11 @@ class PoolStats(ctypes.Structure):
     _fields_ = [("direct_batches", ctypes.c_ulong), ("staged_batches", ctypes.c_ulong), ("h2d_bytes", ctypes.c_ulong)]
 
 
-_lib.fd_ed25519_hip_pool_verify_ex.argtypes = [_v, ctypes.c_uint, ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, _v,
-                                               _v, _v, _v, _v, _v, ctypes.POINTER(ctypes.c_double),
-                                               ctypes.POINTER(PoolStats)]
+_lib.fd_ed25519_hip_pool_new.argtypes = [_v, ctypes.c_uint, ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong]
+_lib.fd_ed25519_hip_pool_new.restype = _v
+_lib.fd_ed25519_hip_pool_run.argtypes = [_v, ctypes.c_ulong, _v, _v, _v, _v, _v, _v, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(PoolStats)]
+_lib.fd_ed25519_hip_pool_delete.argtypes = [_v]
 _lib.fd_ed25519_hip_host_register.argtypes = [_v, ctypes.c_ulong]
 _lib.fd_ed25519_hip_host_unregister.argtypes = [_v]
 _lib.fd_ed25519_hip_h2d_gbps.argtypes = [ctypes.c_int, ctypes.c_ulong, ctypes.c_uint]
@@ -90,6 +106,23 @@ def txn_parse(payload):
     if not _lib.fd_ed25519_hip_txn_parse(payload, len(payload), ctypes.byref(t)):
         return None
     return {f: getattr(t, f) for f in Txn.FIELDS}
+
+
+def txn_parse_full(payload):
+    """fd_txn_parse: the fd_txn_t bytes (its footprint), or None."""
+    payload = bytes(payload)
+    buf = ctypes.create_string_buffer(TXN_MAX_SZ)
+    r = _lib.fd_ed25519_hip_txn_parse_full(payload, len(payload), buf)
+    return buf.raw[:r] if r else None
+
+
+def txn_frag(payload):
+    """after_frag's output frag (payload, pad, fd_txn_t, payload_sz), or
+    None when the parse filter drops the payload."""
+    payload = bytes(payload)
+    buf = ctypes.create_string_buffer(TPU_DCACHE_MTU)
+    r = _lib.fd_ed25519_hip_txn_frag(payload, len(payload), buf)
+    return buf.raw[:r] if r else None
 
 
 class TCache:
@@ -136,25 +169,47 @@ class VerifyTile:
         n = _lib.fd_ed25519_hip_vtile_poll(self._h, 1 if wait else 0, max_n, _ptr(ck), _ptr(vd), _ptr(tg))
         return ck[:n], vd[:n], tg[:n]
 
+    def poll_frags(self, wait=False, max_n=4096):
+        """As poll, plus the frag published for each SUCCESS (bytes) or None."""
+        ck = np.zeros(max_n, np.uint64)
+        vd = np.zeros(max_n, np.int8)
+        tg = np.zeros(max_n, np.uint64)
+        fo = np.zeros(max_n, np.uint64)
+        fs = np.zeros(max_n, np.uint64)
+        cap = max_n * ((TPU_DCACHE_MTU + 63) & ~63)
+        fb = np.zeros(cap, np.uint8)
+        n = _lib.fd_ed25519_hip_vtile_poll_frags(self._h, 1 if wait else 0, max_n, _ptr(ck), _ptr(vd), _ptr(tg),
+                                                 _ptr(fo), _ptr(fs), _ptr(fb), cap)
+        frags = [fb[int(fo[k]):int(fo[k]) + int(fs[k])].tobytes() if fs[k] else None for k in range(n)]
+        return ck[:n], vd[:n], tg[:n], frags
+
     def pending(self):
         return _lib.fd_ed25519_hip_vtile_pending(self._h)
 
-    def run(self, payloads):
-        """Every payload through the tile in order -> (verdicts, tags) by index."""
+    def run(self, payloads, frags=False):
+        """Every payload through the tile in order -> (verdicts, tags[,
+        published frags]) by index."""
         n = len(payloads)
         verdict = np.full(n, 99, np.int8)
         tags = np.zeros(n, np.uint64)
+        out = [None] * n
+
+        def take(r):
+            ck, vd, tg = r[:3]
+            verdict[ck] = vd
+            tags[ck] = tg
+            if frags:
+                for c, f in zip(ck, r[3]):
+                    out[int(c)] = f
+
+        poll = self.poll_frags if frags else self.poll
         for i, p in enumerate(payloads):
             self.frag(p, i)
-            ck, vd, tg = self.poll(False)
-            verdict[ck] = vd
-            tags[ck] = tg
+            take(poll(False))
         self.flush()
         while self.pending():
-            ck, vd, tg = self.poll(True)
-            verdict[ck] = vd
-            tags[ck] = tg
-        return verdict, tags
+            take(poll(True))
+        return (verdict, tags, out) if frags else (verdict, tags)
 
     def close(self):
         if self._h:
@@ -201,26 +256,68 @@ def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=25
     return lat, verdict, {f: getattr(res, f) for f, _ in LatencyResult._fields_}
 
 
+class Pool:
+    """fd_ed25519_hip_pool: one feeder thread per entry of `devices`,
+    slot_cnt batches of batch_sigs signatures in flight on each, msg_cap
+    message bytes per batch; set up once, run many times."""
+
+    def __init__(self, devices, batch_sigs=65536, slot_cnt=3, msg_cap=None):
+        devs = np.ascontiguousarray(devices, np.int32)
+        cap = int(msg_cap if msg_cap is not None else batch_sigs * TXN_MTU)
+        self._h = _lib.fd_ed25519_hip_pool_new(_ptr(devs), len(devs), int(slot_cnt), int(batch_sigs), cap)
+        if not self._h:
+            raise HipError(f"pool_new failed: {_lib.fd_ed25519_hip_last_error().decode()}")
+
+    def run(self, msgs, msg_off, msg_sz, sigs, pubs, out=None):
+        """-> (codes, seconds, transfer stats).  Arrays registered with
+        HostRegistration are DMA'd in place; others are staged."""
+        n = len(msg_sz)
+        if out is None:
+            out = np.zeros(max(n, 1), np.int8)
+        msgs = msgs if len(msgs) else np.zeros(1, np.uint8)
+        arrs = [_c(msgs, np.uint8), _c(msg_off, np.uint64), _c(msg_sz, np.uint32), _c(sigs, np.uint8).reshape(-1),
+                _c(pubs, np.uint8).reshape(-1)]
+        sec = ctypes.c_double(0.0)
+        st = PoolStats()
+        _check(_lib.fd_ed25519_hip_pool_run(self._h, n, *[_ptr(a) for a in arrs], _ptr(out), ctypes.byref(sec),
+                                            ctypes.byref(st)))
+        return out[:n], sec.value, {f: getattr(st, f) for f, _ in PoolStats._fields_}
+
+    def close(self):
+        if self._h:
+            _lib.fd_ed25519_hip_pool_delete(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def max_span(msg_off, msg_sz, batch_sigs):
+    """The message capacity a pool needs for these batches: the largest
+    span (or packed size) of a batch."""
+    off = np.asarray(msg_off, np.uint64)
+    end = off + np.asarray(msg_sz, np.uint64)
+    cap = 1
+    for i0 in range(0, len(off), batch_sigs):
+        lo, hi = int(off[i0:i0 + batch_sigs].min()), int(end[i0:i0 + batch_sigs].max())
+        byt = int(np.asarray(msg_sz[i0:i0 + batch_sigs], np.uint64).sum())
+        cap = max(cap, hi - lo if hi - lo <= 2 * byt + 65536 else byt)
+    return cap
+
+
 def pool_verify(devices, msgs, msg_off, msg_sz, sigs, pubs, batch_sigs=65536, slot_cnt=3, out=None, stats=False):
     """Signatures dealt round-robin in batches over `devices` (one host
-    feeder thread per entry, fd_ed25519_hip_pool_verify) -> (codes,
-    seconds[, stats]).  Arrays registered with HostRegistration (or numpy
-    views of pinned memory) are DMA'd in place; others are staged."""
-    devs = np.ascontiguousarray(devices, np.int32)
-    n = len(msg_sz)
-    if out is None:
-        out = np.zeros(max(n, 1), np.int8)
-    msgs = msgs if len(msgs) else np.zeros(1, np.uint8)
-    arrs = [_c(msgs, np.uint8), _c(msg_off, np.uint64), _c(msg_sz, np.uint32), _c(sigs, np.uint8).reshape(-1),
-            _c(pubs, np.uint8).reshape(-1)]
-    sec = ctypes.c_double(0.0)
-    st = PoolStats()
-    _check(_lib.fd_ed25519_hip_pool_verify_ex(_ptr(devs), len(devs), int(slot_cnt), int(batch_sigs), n,
-                                              *[_ptr(a) for a in arrs], _ptr(out), ctypes.byref(sec),
-                                              ctypes.byref(st)))
-    if stats:
-        return out[:n], sec.value, {f: getattr(st, f) for f, _ in PoolStats._fields_}
-    return out[:n], sec.value
+    feeder thread per entry) -> (codes, seconds[, stats]); a pool set up for
+    this one call."""
+    pool = Pool(devices, batch_sigs, slot_cnt, max_span(msg_off, msg_sz, batch_sigs) if len(msg_sz) else 1)
+    try:
+        codes, sec, st = pool.run(msgs, msg_off, msg_sz, sigs, pubs, out)
+    finally:
+        pool.close()
+    return (codes, sec, st) if stats else (codes, sec)
 
 
 class HostRegistration:
@@ -288,7 +385,7 @@ class ShLink:
         if not h:
             raise HipError(-1, f"shlink {'create' if create else 'join'} {name} failed")
         self._h, self._owner = h, create
-        self._buf = ctypes.create_string_buffer(TXN_MTU)
+        self._buf = ctypes.create_string_buffer(SHLINK_MTU)
 
     @property
     def depth(self):
@@ -333,6 +430,16 @@ def vservice_run(in_link, out_link, device=0, slot_cnt=3, batch_sigs=4096, gpu_p
     _check(_lib.fd_ed25519_hip_vservice_run(int(device), int(slot_cnt), int(batch_sigs), flags, in_link._h,
                                             out_link._h, ctypes.byref(st)))
     return {f: getattr(st, f) for f, _ in VServiceStats._fields_}
+
+
+def parse_producer_frags(blob):
+    """The producer tool's frag records (u32 size, bytes) -> list of bytes."""
+    out, i = [], 0
+    while i < len(blob):
+        k = int.from_bytes(blob[i:i + 4], "little")
+        out.append(bytes(blob[i + 4:i + 4 + k]))
+        i += 4 + k
+    return out
 
 
 def write_payload_file(path, payloads):

@@ -100,6 +100,11 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
 #define FD_ED25519_HIP_FLAG_DSM_QUAD       (4)
 #define FD_ED25519_HIP_FLAG_DSM_WIDE       (8)
 #define FD_ED25519_HIP_FLAG_DSM_OCT        (16)
+/* The engine keeps to its one stream (no side stream for the decode
+   overlap): for engines whose batches overlap one another already (the
+   pool's and the pipe's slots), where extra streams only crowd the
+   device's few hardware queues. */
+#define FD_ED25519_HIP_FLAG_ONE_STREAM     (32)
 #define FD_ED25519_HIP_QUAD_MAX_DEFAULT    (32768UL)
 #define FD_ED25519_HIP_OCT_MAX_DEFAULT     (8192UL)
 /* Overlap: a large chunk's decode phase (A and R need neither the hash nor

@@ -46,7 +46,10 @@ typedef struct fd_ed25519_hip_pipe fd_ed25519_hip_pipe_t;
    transaction t owns [txn_first[t], txn_first[t] + txn_sig_cnt[t]) and
    gets fd_ed25519_verify_batch_single_msg's code in txn_out[t] (a count of
    0 or > 16 gives ERR_SIG, such transactions stage no signatures).  After
-   poll returns the slot, sig_out / txn_out hold the codes. */
+   poll returns the slot, sig_out / txn_out hold the codes, and after a
+   raw-transaction submit txn_trailer[64 t ..] the first 64 bytes of
+   transaction t's fd_txn_t as the device parsed it (complete when its
+   footprint, FD_ED25519_HIP_TXN_FOOTPRINT, is at most 64 bytes). */
 typedef struct {
   unsigned char *  msgs;
   unsigned long *  msg_off;
@@ -57,6 +60,7 @@ typedef struct {
   unsigned int *   txn_sig_cnt;
   signed char *    sig_out;
   signed char *    txn_out;
+  unsigned char *  txn_trailer;
   unsigned long    sig_cap;
   unsigned long    msg_cap;
   unsigned long    txn_cap;
@@ -138,12 +142,34 @@ typedef struct {
 } fd_ed25519_hip_txn_t;
 
 #define FD_ED25519_HIP_TXN_MTU (1232UL)
+#define FD_ED25519_HIP_TXN_MAX_SZ (852UL)                 /* FD_TXN_MAX_SZ, src/ballet/txn/fd_txn.h */
+/* the verify tile's output frag: payload, pad, fd_txn_t, payload_sz
+   (FD_TPU_DCACHE_MTU, src/disco/fd_disco_base.h:41) */
+#define FD_ED25519_HIP_TPU_DCACHE_MTU (FD_ED25519_HIP_TXN_MTU + FD_ED25519_HIP_TXN_MAX_SZ + 2UL)
+/* fd_txn_footprint: 20-byte header, 10 bytes per instruction, 8 per
+   address table lookup */
+#define FD_ED25519_HIP_TXN_FOOTPRINT( instr_cnt, lut_cnt ) (20UL + 10UL*(instr_cnt) + 8UL*(lut_cnt))
 
 /* Accepts exactly the payloads fd_txn_parse(payload, sz, out, NULL)
    accepts (fd_txn_parse_core with allow_zero_signatures=0 and no trailing
    bytes), returning 1 and the fields, else 0. */
 int
 fd_ed25519_hip_txn_parse( unsigned char const * payload, unsigned long payload_sz, fd_ed25519_hip_txn_t * out );
+
+/* fd_txn_parse itself: writes the reference's fd_txn_t (src/ballet/txn/
+   fd_txn.h: header, instr[], address table lookups) byte for byte into
+   out_txn (FD_ED25519_HIP_TXN_MAX_SZ bytes) and returns its footprint,
+   or 0 if the payload is rejected. */
+unsigned long
+fd_ed25519_hip_txn_parse_full( unsigned char const * payload, unsigned long payload_sz, void * out_txn );
+
+/* after_frag's transformation of a frag (src/app/fdctl/run/tiles/
+   fd_verify.c:102-133): out (FD_ED25519_HIP_TPU_DCACHE_MTU bytes) receives
+   the payload, a zero pad byte to 2-byte alignment, the fd_txn_t and the
+   payload size as a little-endian u16; returns that frag's size (new_sz),
+   or 0 if fd_txn_parse rejects the payload (after_frag's filter). */
+unsigned long
+fd_ed25519_hip_txn_frag( unsigned char const * payload, unsigned long payload_sz, unsigned char * out );
 
 /* tcache: the verify tile's HA dedup cache of the last `depth` tags
    (map_cnt a power of two >= depth+2; the tile uses 16 / 64). */
@@ -211,6 +237,18 @@ unsigned long
 fd_ed25519_hip_vtile_poll( fd_ed25519_hip_vtile_t * vt, int wait, unsigned long max, unsigned long * cookie,
                            signed char * verdict, unsigned long * tag );
 
+/* The same, with the frags the tile publishes: for each verdict also
+   frag_off[k] / frag_sz[k], the frag after_frag publishes for a SUCCESS
+   transaction (fd_ed25519_hip_txn_frag's layout: payload, pad, fd_txn_t,
+   payload_sz; publish sig = tag) copied into frag_buf at frag_off[k]
+   (64-byte aligned, like the reference's compact dcache chunks), and
+   frag_sz[k] = 0 for filtered transactions.  Stops early, before a frag
+   that would not fit in frag_buf_sz bytes. */
+unsigned long
+fd_ed25519_hip_vtile_poll_frags( fd_ed25519_hip_vtile_t * vt, int wait, unsigned long max, unsigned long * cookie,
+                                 signed char * verdict, unsigned long * tag, unsigned long * frag_off,
+                                 unsigned long * frag_sz, unsigned char * frag_buf, unsigned long frag_buf_sz );
+
 /* Transactions staged or in flight whose verdicts have not been polled. */
 unsigned long
 fd_ed25519_hip_vtile_pending( fd_ed25519_hip_vtile_t const * vt );
@@ -248,12 +286,15 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
 /* A single-producer single-consumer tango-style link in a POSIX shm object
    `name` (e.g. "/fd_verify_in"): an mcache of depth (power of 2)
    fd_frag_meta_t-shaped lines and a dcache of 64-byte chunks for payloads
-   of up to FD_ED25519_HIP_TXN_MTU bytes, with credit-based flow control.
+   of up to FD_ED25519_HIP_SHLINK_MTU bytes, with credit-based flow control.
    create makes the object (it must not exist), join maps an existing one;
    each process keeps its own cursor, so one handle per side.  After the
    mapping, publish / consume are memory operations only (they may run
    under seccomp strict mode). */
 typedef struct fd_ed25519_hip_shlink fd_ed25519_hip_shlink_t;
+
+/* a verdict frag: 1 verdict byte, then the published frag */
+#define FD_ED25519_HIP_SHLINK_MTU (1UL + FD_ED25519_HIP_TPU_DCACHE_MTU)
 
 fd_ed25519_hip_shlink_t *
 fd_ed25519_hip_shlink_create( char const * name, unsigned long depth );
@@ -275,7 +316,7 @@ int
 fd_ed25519_hip_shlink_publish( fd_ed25519_hip_shlink_t * link, unsigned char const * payload, unsigned long sz,
                                unsigned long sig, unsigned int ctl );
 
-/* Consumer: takes the next frag into payload (FD_ED25519_HIP_TXN_MTU
+/* Consumer: takes the next frag into payload (FD_ED25519_HIP_SHLINK_MTU
    bytes of room).  Returns 0, 1 if none is published yet, -1 if the
    producer overran the consumer. */
 int
@@ -295,8 +336,9 @@ typedef struct {
    frags from `in` (sig = the tile's cookie), runs them through a vtile
    (slot_cnt, batch_sigs, flags as for fd_ed25519_hip_vtile_new) and
    publishes one frag per transaction to `out` in frag order: sig = cookie,
-   a 1-byte payload with the verdict (FD_ED25519_HIP_TXN_VERIFY_* /
-   FD_ED25519_HIP_TXN_PARSE_FAILED).  A frag with ctl EOS ends the stream:
+   the verdict (FD_ED25519_HIP_TXN_VERIFY_* / FD_ED25519_HIP_TXN_PARSE_FAILED)
+   as byte 0, and for SUCCESS the frag the verify tile publishes to dedup
+   after it (fd_ed25519_hip_txn_frag's layout, new_sz bytes).  A frag with ctl EOS ends the stream:
    the service answers everything before it, publishes an EOS frag and
    returns.  A batch is submitted when full, or when `in` is drained and a
    slot is free. */
@@ -333,12 +375,27 @@ typedef struct {
   unsigned long h2d_bytes;        /* bytes moved host -> device                */
 } fd_ed25519_hip_pool_stats_t;
 
-/* The same, with transfer statistics (stats may be NULL). */
+/* The same pool as a long-lived object (a deployment's feeder: engines,
+   streams and device buffers are set up once): slot_cnt (1..8) batches of
+   batch_sigs signatures in flight per device, msg_cap bytes of messages
+   per batch (the span a batch's messages cover when DMA'd in place, or
+   their bytes when packed).  pool_run verifies one SoA set as
+   fd_ed25519_hip_pool_verify does; stats (optional) reports the
+   transfers. */
+typedef struct fd_ed25519_hip_pool fd_ed25519_hip_pool_t;
+
+fd_ed25519_hip_pool_t *
+fd_ed25519_hip_pool_new( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
+                         unsigned long msg_cap );
+
 int
-fd_ed25519_hip_pool_verify_ex( int const * devices, unsigned device_cnt, unsigned slot_cnt, unsigned long batch_sigs,
-                               unsigned long n, unsigned char const * msgs, unsigned long const * msg_off,
-                               unsigned int const * msg_sz, unsigned char const * sigs, unsigned char const * pubs,
-                               signed char * out, double * seconds, fd_ed25519_hip_pool_stats_t * stats );
+fd_ed25519_hip_pool_run( fd_ed25519_hip_pool_t * pool, unsigned long n, unsigned char const * msgs,
+                         unsigned long const * msg_off, unsigned int const * msg_sz, unsigned char const * sigs,
+                         unsigned char const * pubs, signed char * out, double * seconds,
+                         fd_ed25519_hip_pool_stats_t * stats );
+
+void
+fd_ed25519_hip_pool_delete( fd_ed25519_hip_pool_t * pool );
 
 /* Page-locks [ptr, ptr+sz) of the caller's memory for every device
    (hipHostRegister, portable + mapped) so the pool and the pipe DMA

@@ -141,3 +141,43 @@ fdref_vtile_seq( ulong n, uchar const * payloads, ulong const * off, uint const 
   }
   free( ring ); free( map );
 }
+
+/* fd_txn_parse's output itself: the fd_txn_t bytes (FD_TXN_MAX_SZ buffer,
+   zeroed first); returns the footprint, 0 = rejected. */
+ulong
+fdref_txn_parse_raw( uchar const * payload, ulong sz, uchar * out ) {
+  fd_memset( out, 0, FD_TXN_MAX_SZ );
+  return fd_txn_parse( payload, sz, out, NULL );
+}
+
+/* after_frag's trailer (src/app/fdctl/run/tiles/fd_verify.c:102-133),
+   restated step by step on a zeroed FD_TPU_DCACHE_MTU buffer: the payload
+   as during_frag copied it, fd_txn_t at the payload size aligned up to 2,
+   then the payload size as a ushort.  Returns new_sz, 0 if the parse
+   filter drops the frag. */
+#define REF_TPU_DCACHE_MTU (1232UL + FD_TXN_MAX_SZ + 2UL)
+ulong
+fdref_after_frag( uchar const * payload, ulong payload_sz, uchar * out ) {
+  fd_memset( out, 0, REF_TPU_DCACHE_MTU );
+  fd_memcpy( out, payload, payload_sz );
+  ulong txnt_off = fd_ulong_align_up( payload_sz, 2UL );
+  fd_txn_t * txn_t = (fd_txn_t *)( out + txnt_off );
+  ulong txn_t_sz = fd_txn_parse( out, payload_sz, txn_t, NULL );
+  if( !txn_t_sz ) return 0UL;
+  ushort * payload_sz_p = (ushort *)( (ulong)txn_t + txn_t_sz );
+  *payload_sz_p = (ushort)payload_sz;
+  return ( (ulong)payload_sz_p + sizeof(ushort) ) - (ulong)out;
+}
+
+/* fdref_vtile_seq plus the frag each SUCCESS transaction publishes:
+   frags[i*REF_TPU_DCACHE_MTU ..] and frag_sz[i] (0 when filtered). */
+void
+fdref_vtile_seq_frags( ulong n, uchar const * payloads, ulong const * off, uint const * sz, ulong depth, ulong map_cnt,
+                       schar * verdict, ulong * tag_out, uchar * frags, ulong * frag_sz ) {
+  fdref_vtile_seq( n, payloads, off, sz, depth, map_cnt, verdict, tag_out );
+  for( ulong i=0UL; i<n; i++ ) {
+    frag_sz[i] = 0UL;
+    if( verdict[i]!=0 ) continue;
+    frag_sz[i] = fdref_after_frag( payloads + off[i], sz[i], frags + i*REF_TPU_DCACHE_MTU );
+  }
+}

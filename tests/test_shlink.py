@@ -20,6 +20,11 @@ def fake_verdict(payload):
     return (len(payload) % 7) - 3
 
 
+def fake_frag(payload):
+    """A SUCCESS verdict frag carries the published frag: here a stand-in."""
+    return payload[::-1] + b"\x5a"
+
+
 def serve_fake(txl, vdl, proc, deadline_s=60.0):
     """Consume txn frags, answer each with fake_verdict, until EOS."""
     t0 = time.time()
@@ -28,8 +33,8 @@ def serve_fake(txl, vdl, proc, deadline_s=60.0):
     n = 0
     while True:
         while pending:
-            sig, v = pending[0]
-            if not vdl.publish(bytes([v & 0xff]), sig):
+            sig, v, fr = pending[0]
+            if not vdl.publish(bytes([v & 0xff]) + fr, sig):
                 break
             pending.pop(0)
         if eos and not pending:
@@ -48,7 +53,8 @@ def serve_fake(txl, vdl, proc, deadline_s=60.0):
             eos = True
             continue
         assert sig == n
-        pending.append((sig, fake_verdict(payload)))
+        v = fake_verdict(payload)
+        pending.append((sig, v, fake_frag(payload) if v == 0 else b""))
         n += 1
 
 
@@ -77,9 +83,10 @@ def test_sandboxed_producer_round_trip(tmp_path, sandbox, n, depth):
         pytest.skip(f"seccomp strict mode unavailable: {err.decode()}")
     assert proc.returncode == 0, err.decode()
     assert served == n
-    got = np.frombuffer(out, np.int8)
+    got = np.frombuffer(out[:n], np.int8)
     want = np.array([fake_verdict(p) for p in payloads], np.int8)
     assert np.array_equal(got, want)
+    assert tile.parse_producer_frags(out[n:]) == [fake_frag(p) for p in payloads if fake_verdict(p) == 0]
 
 
 def test_link_credits_and_overrun_free():
@@ -145,7 +152,7 @@ def test_hostile_header_is_ignored_after_join():
             _poke(f, 8, "<QQQ", 1 << 40, 1 << 40, 65535)
         # a frag above the MTU is refused by the producer's local MTU
         with pytest.raises(Exception):
-            a.publish(b"\0" * (tile.TXN_MTU + 1), 0)
+            a.publish(b"\0" * (tile.SHLINK_MTU + 1), 0)
         for i in range(8):
             assert a.publish(bytes([i]) * 100, i)
         assert not a.publish(b"x", 99)   # credits still counted against depth 8

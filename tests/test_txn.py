@@ -12,7 +12,8 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN
-from txn_util import message, mutate, random_txn, ref_lib, ref_parse, ref_vtile, tile_workload, txn, Signer
+from txn_util import (message, mutate, random_txn, ref_after_frag, ref_lib, ref_parse, ref_parse_raw, ref_vtile,
+                      tile_workload, txn, Signer)
 
 
 @pytest.fixture(scope="module")
@@ -101,6 +102,46 @@ def test_edge_encodings(tile, ref):
     big = txn([sig], message(1, accts, instrs=[(2, [0], b"\0" * 1200)]))
     assert len(big) > 1232
     _same(tile, ref, big)
+
+
+def _same_full(tile, ref, p):
+    """fd_txn_t byte for byte (instr[], address table lookups, padding) and
+    the frag after_frag publishes (payload, pad, fd_txn_t, payload_sz)."""
+    assert tile.txn_parse_full(p) == ref_parse_raw(ref, p), p.hex()
+    assert tile.txn_frag(p) == ref_after_frag(ref, p), p.hex()
+
+
+def test_full_txn_and_frag_on_fixtures_and_mutations(tile, ref):
+    rng = random.Random(17)
+    n_ok = 0
+    for p in fixtures():
+        _same_full(tile, ref, p)
+        for _ in range(1500):
+            q = p
+            for _ in range(rng.randrange(1, 4)):
+                q = mutate(rng, q)
+            _same_full(tile, ref, q)
+            n_ok += tile.txn_parse_full(q) is not None
+    assert n_ok > 500
+
+
+def test_full_txn_and_frag_synthesized(tile, ref, oracle):
+    """Legacy and v0, 1..9 instructions, 0..4 lookup tables (fd_txn_t from
+    20 to ~150 bytes), odd and even payload sizes (the pad byte)."""
+    rng = random.Random(19)
+    signer = Signer(oracle, 19)
+    sizes = set()
+    for _ in range(400):
+        v0 = rng.random() < 0.5
+        p = random_txn(signer, rng, rng.choice([1, 2, 5, 12]), v0=v0, msg_pad=rng.randrange(300),
+                       instr_n=rng.randrange(1, 10), lut_n=rng.randrange(0, 5))
+        _same_full(tile, ref, p)
+        t = tile.txn_parse_full(p)
+        if t is not None:
+            sizes.add((len(t), len(p) & 1))
+        for _ in range(5):
+            _same_full(tile, ref, mutate(rng, p))
+    assert len({s for s, _ in sizes}) > 10 and {o for _, o in sizes} == {0, 1}
 
 
 class PyTCache:

@@ -70,10 +70,10 @@ class Signer:
         return s.raw
 
 
-def random_txn(signer, rng, nsig, v0=False, bad_sig=False, msg_pad=0):
+def random_txn(signer, rng, nsig, v0=False, bad_sig=False, msg_pad=0, instr_n=1, lut_n=1):
     """A parseable transaction with nsig signers (pubkeys = first nsig
-    account addresses), one instruction; bad_sig flips a bit of a random
-    signature after signing."""
+    account addresses), instr_n instructions (and, v0, lut_n address table
+    lookups); bad_sig flips a bit of a random signature after signing."""
     keys = [signer.key() for _ in range(nsig)] if nsig <= 16 else [signer.key() for _ in range(2)] * ((nsig + 1) // 2)
     keys = keys[:nsig]
     extra = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(1 + rng.randrange(3))]
@@ -81,7 +81,11 @@ def random_txn(signer, rng, nsig, v0=False, bad_sig=False, msg_pad=0):
     prog = len(accts) - 1
     data = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 40) + msg_pad))
     instrs = [(prog, [0, min(1, len(accts) - 1)], data)]
-    luts = [(bytes(32), [0], [1])] if v0 else ()
+    for _ in range(instr_n - 1):
+        instrs.append((prog, [rng.randrange(len(accts)) for _ in range(rng.randrange(4))],
+                       bytes(rng.getrandbits(8) for _ in range(rng.randrange(12)))))
+    luts = [(bytes(rng.getrandbits(8) for _ in range(32)), [0] * (1 + rng.randrange(2)), [1] * rng.randrange(3))
+            for _ in range(lut_n)] if v0 else ()
     m = message(nsig, accts, ro_signed=0, ro_unsigned=1, instrs=instrs, version=0 if v0 else None, luts=luts)
     sigs = [signer.sign(m, priv, pub) for priv, pub in keys]
     if bad_sig:
@@ -136,7 +140,47 @@ def ref_lib(flavour="portable"):
     lib.fdref_txn_parse.restype = ctypes.c_ulong
     lib.fdref_vtile_seq.argtypes = [ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
                                     ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p]
+    lib.fdref_txn_parse_raw.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_void_p]
+    lib.fdref_txn_parse_raw.restype = ctypes.c_ulong
+    lib.fdref_after_frag.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_void_p]
+    lib.fdref_after_frag.restype = ctypes.c_ulong
+    lib.fdref_vtile_seq_frags.argtypes = [ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_ulong, ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p]
     return lib
+
+
+TXN_MAX_SZ = 852                      # FD_TXN_MAX_SZ
+TPU_DCACHE_MTU = 1232 + TXN_MAX_SZ + 2  # FD_TPU_DCACHE_MTU
+
+
+def ref_parse_raw(lib, payload):
+    """fd_txn_parse's fd_txn_t bytes (footprint long), or None."""
+    buf = ctypes.create_string_buffer(TXN_MAX_SZ)
+    r = lib.fdref_txn_parse_raw(payload, len(payload), buf)
+    return buf.raw[:r] if r else None
+
+
+def ref_after_frag(lib, payload):
+    """The frag the reference verify tile's after_frag publishes, or None."""
+    buf = ctypes.create_string_buffer(TPU_DCACHE_MTU)
+    r = lib.fdref_after_frag(payload, len(payload), buf)
+    return buf.raw[:r] if r else None
+
+
+def ref_vtile_frags(lib, payloads, depth=16, map_cnt=64):
+    """The sequential reference tile: verdicts, tags, and the published
+    frag of every SUCCESS transaction (None otherwise)."""
+    from firedancer_amd.tile import pack_payloads
+    buf, off, sz = pack_payloads(payloads)
+    n = len(payloads)
+    v = np.zeros(n, np.int8)
+    tags = np.zeros(n, np.uint64)
+    fr = np.zeros((n, TPU_DCACHE_MTU), np.uint8)
+    fsz = np.zeros(n, np.uint64)
+    lib.fdref_vtile_seq_frags(n, buf.ctypes.data, off.ctypes.data, sz.ctypes.data, depth, map_cnt, v.ctypes.data,
+                              tags.ctypes.data, fr.ctypes.data, fsz.ctypes.data)
+    return v, tags, [fr[i, :int(fsz[i])].tobytes() if fsz[i] else None for i in range(n)]
 
 
 def ref_parse(lib, payload):
@@ -175,6 +219,9 @@ def tile_workload(oracle, seed, n, p_bad=0.1, p_dup=0.1, p_junk=0.05, p_many=0.0
             out.append(random_txn(signer, rng, 17 + rng.randrange(3)))
         else:
             nsig = rng.choice([1, 1, 1, 2, 2, 3, 4, 8, 12])
+            # some with fd_txn_t trailers longer than the device's 64-byte slot
+            many = rng.random() < 0.1
             out.append(random_txn(signer, rng, nsig, v0=rng.random() < 0.3, bad_sig=rng.random() < p_bad,
-                                  msg_pad=rng.randrange(0, 600)))
+                                  msg_pad=rng.randrange(0, 600), instr_n=rng.randrange(5, 9) if many else 1,
+                                  lut_n=rng.randrange(2, 5) if many else 1))
     return out

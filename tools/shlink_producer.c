@@ -10,9 +10,11 @@
    PAYLOAD_FILE: u64 n, n x u32 sizes, the payloads back to back.  Frag i
    carries sig = i; after the last one an EOS frag.  Verdict frags are
    consumed whenever a publish finds no credit, and after the EOS until
-   the service's EOS.  Output on stdout: n verdict bytes in frag order
-   (checked against the sig of every verdict frag), via write(2); exit
-   status 0, or 2 on a protocol error, 3 if strict mode is unavailable. */
+   the service's EOS.  Output on stdout, via write(2): n verdict bytes in
+   frag order (checked against the sig of every verdict frag), then for
+   each SUCCESS verdict the frag the service returned with it (the frag
+   the verify tile publishes: u32 size, then the bytes); exit status 0, or
+   2 on a protocol error, 3 if strict mode is unavailable. */
 #define _GNU_SOURCE
 #include "../include/fd_ed25519_hip_tile.h"
 
@@ -30,9 +32,14 @@ leave( int status ) {   /* exit(2) itself: exit_group is not allowed in strict m
   for(;;) {}
 }
 
+typedef struct {
+  unsigned char * mem;   /* preallocated: no allocation after seccomp */
+  unsigned long   cap, used;
+} frags_t;
+
 static int
 take_verdicts( fd_ed25519_hip_shlink_t * in, unsigned char * buf, signed char * verdict, unsigned long n,
-               unsigned long * next, int * eos ) {
+               unsigned long * next, int * eos, frags_t * fr ) {
   for(;;) {
     unsigned long sz = 0UL, sig = 0UL;
     unsigned int ctl = 0U;
@@ -40,8 +47,17 @@ take_verdicts( fd_ed25519_hip_shlink_t * in, unsigned char * buf, signed char * 
     if( r==1 ) return 0;
     if( r ) return -1;
     if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { *eos = 1; return 0; }
-    if( sz!=1UL || sig!=*next || *next>=n ) return -1;
-    verdict[ (*next)++ ] = (signed char)buf[ 0 ];
+    if( sz<1UL || sig!=*next || *next>=n ) return -1;
+    signed char v = (signed char)buf[ 0 ];
+    if( (v==FD_ED25519_HIP_TXN_VERIFY_SUCCESS) != (sz>1UL) ) return -1;   /* a frag with every SUCCESS, only then */
+    if( sz>1UL ) {
+      unsigned int fsz = (unsigned int)(sz - 1UL);
+      if( fr->used + 4UL + fsz > fr->cap ) return -1;
+      memcpy( fr->mem + fr->used, &fsz, 4UL );
+      memcpy( fr->mem + fr->used + 4UL, buf + 1, fsz );
+      fr->used += 4UL + fsz;
+    }
+    verdict[ (*next)++ ] = v;
   }
 }
 
@@ -62,7 +78,12 @@ main( int argc, char ** argv ) {
   if( !pay || fread( pay, 1, total, f )!=total ) return 1;
   fclose( f );
   signed char * verdict = (signed char *)malloc( n + 1UL );
-  unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_TXN_MTU );
+  unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
+  frags_t fr;
+  fr.cap = total + n*(FD_ED25519_HIP_TXN_MAX_SZ + 8UL) + 64UL;   /* every payload + its trailer, size word */
+  fr.used = 0UL;
+  fr.mem = (unsigned char *)malloc( fr.cap );
+  if( !fr.mem ) return 1;
   fd_ed25519_hip_shlink_t * txl = fd_ed25519_hip_shlink_join( argv[1] );
   fd_ed25519_hip_shlink_t * vdl = fd_ed25519_hip_shlink_join( argv[2] );
   if( !verdict || !buf || !txl || !vdl ) { fprintf( stderr, "cannot join the links\n" ); return 1; }
@@ -77,18 +98,24 @@ main( int argc, char ** argv ) {
     int r = fd_ed25519_hip_shlink_publish( txl, pay + off[ i ], sz[ i ], i, 0U );
     if( r==0 ) { i++; continue; }
     if( r!=1 ) leave( 2 );
-    if( take_verdicts( vdl, buf, verdict, n, &got, &eos ) || eos ) leave( 2 );
+    if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) || eos ) leave( 2 );
   }
   while( fd_ed25519_hip_shlink_publish( txl, NULL, 0UL, n, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
-    if( take_verdicts( vdl, buf, verdict, n, &got, &eos ) || eos ) leave( 2 );
+    if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) || eos ) leave( 2 );
   }
   while( !eos ) {
-    if( take_verdicts( vdl, buf, verdict, n, &got, &eos ) ) leave( 2 );
+    if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) ) leave( 2 );
   }
   if( got!=n ) leave( 2 );
   unsigned long w = 0UL;
   while( w<n ) {
     long k = write( 1, verdict + w, n - w );
+    if( k<=0 ) leave( 2 );
+    w += (unsigned long)k;
+  }
+  w = 0UL;
+  while( w<fr.used ) {
+    long k = write( 1, fr.mem + w, fr.used - w );
     if( k<=0 ) leave( 2 );
     w += (unsigned long)k;
   }
