@@ -225,7 +225,7 @@ def latency_mode(eng, args, device):
     return out
 
 
-def host_fed(wl, device, world, reps, batch, slots, copies):
+def host_fed(wl, device, info, world, reps, batch, slots, copies):
     """The host-fed path: the C2 signatures from host memory (page-locked,
     as a deployment registers its dcache once) through the pool's feeder
     thread (fd_ed25519_hip_pool_run, one thread on the GPU's NUMA node):
@@ -244,11 +244,14 @@ def host_fed(wl, device, world, reps, batch, slots, copies):
     sigs1 = wl.sigs.download(np.uint8, 64 * n)
     pubs1 = wl.pubs.download(np.uint8, 32 * n)
     expect1 = wl.expect.download(np.int8, n)
-    msgs = np.concatenate([msgs1] * copies + [np.zeros(16, np.uint8)])
-    off = np.concatenate([off1 + np.uint64(c * mb) for c in range(copies)])
-    sz = np.tile(wl.sizes.astype(np.uint32), copies)
-    sigs, pubs = np.tile(sigs1, copies), np.tile(pubs1, copies)
-    out = np.zeros(copies * n, np.int8)
+    # the stream's host buffers are first touched on the GPU's NUMA node
+    near = tile.NearDevice(info)
+    with near:
+        msgs = np.concatenate([msgs1] * copies + [np.zeros(16, np.uint8)])
+        off = np.concatenate([off1 + np.uint64(c * mb) for c in range(copies)])
+        sz = np.tile(wl.sizes.astype(np.uint32), copies)
+        sigs, pubs = np.tile(sigs1, copies), np.tile(pubs1, copies)
+        out = np.ones(copies * n, np.int8)
     pool = tile.Pool([device], batch, slots, tile.max_span(off, sz, batch))
     t = time.perf_counter()
     with tile.HostRegistration(msgs, off, sz, sigs, pubs, out):
@@ -282,6 +285,7 @@ def host_fed(wl, device, world, reps, batch, slots, copies):
             "frac_of_pcie_bound": (rate / world / bound) if bound else None,
             "direct_batches": st["direct_batches"], "staged_batches": st["staged_batches"],
             "register_seconds": reg_s, "verdicts_match_labels": ok_all,
+            "host_buffers_numa_cpus": f"{len(near.cpus)} CPUs of the GPU's NUMA node" if near.cpus else "unknown",
             "path": "host SoA (page-locked) -> per-batch H2D (messages as one DMA of their span) -> verify -> "
                     "D2H codes; fd_ed25519_hip_pool_run, one feeder thread pinned to the GPU's NUMA node"}
 
@@ -427,7 +431,8 @@ def main():
     hf = None
     if args.host_reps > 0:
         try:
-            hf = host_fed(wl, device, world, args.host_reps, args.host_batch, args.host_slots, args.host_copies)
+            hf = host_fed(wl, device, info, world, args.host_reps, args.host_batch, args.host_slots,
+                          args.host_copies)
         except Exception as ex:  # reported, never fatal for the device-resident number
             log(f"[rank {rank}] host-fed leg failed: {ex!r}")
     lat = None

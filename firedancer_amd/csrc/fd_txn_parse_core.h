@@ -15,9 +15,11 @@
    the reference's fd_txn_t itself, byte for byte (src/ballet/txn/fd_txn.h:
    the 20-byte header, instr[instr_cnt] of 10 bytes, then the address
    table lookups of 8 bytes, fd_txn_get_address_tables; little-endian,
-   padding bytes zero as fd_txn_parse writes them), into `full` when its
-   footprint fits full_cap bytes: the trailer the verify tile publishes
-   behind the payload (src/app/fdctl/run/tiles/fd_verify.c:102-133). */
+   padding bytes zero as fd_txn_parse writes them), into `full`: the
+   trailer the verify tile publishes behind the payload
+   (src/app/fdctl/run/tiles/fd_verify.c:102-133).  Entries past full_cap
+   bytes are not written (the header always is, so a reader of a short
+   buffer sees the footprint). */
 #ifndef FD_TXN_PARSE_CORE_H
 #define FD_TXN_PARSE_CORE_H
 
@@ -60,8 +62,8 @@ fd_txn_core_cu16( unsigned char const * b, unsigned long avail, unsigned * val )
 }
 
 /* Returns fd_txn_t's footprint (0: rejected).  out (optional): the summary
-   fields; full (optional): fd_txn_t bytes, written only when the footprint
-   is at most full_cap. */
+   fields; full (optional, full_cap >= 20): fd_txn_t bytes, the entries
+   that fit in full_cap bytes and always the header. */
 FD_TXN_FN unsigned long
 fd_txn_core_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn_t * out, unsigned char * full,
                    unsigned long full_cap ) {
@@ -172,7 +174,9 @@ fd_txn_core_parse( unsigned char const * p, unsigned long sz, fd_ed25519_hip_txn
     out->addr_table_adtl_cnt          = (unsigned char)adtl;
   }
   unsigned long foot = FD_TXN_CORE_FOOTPRINT( instr_cnt, lut_cnt );
-  if( full && foot<=full_cap ) {                                                         /* :145-157, :238-243 */
+  /* the header always (it tells a reader of a short buffer the footprint:
+     instr_cnt at 18, addr_table_lookup_cnt at 14) */
+  if( full && full_cap>=20UL ) {                                                         /* :145-157, :238-243 */
     full[0] = ver;                              full[1] = (unsigned char)sig_cnt;
     fd_txn_core_st16( full+2,  sig_off );       fd_txn_core_st16( full+4,  msg_off );
     full[6] = (unsigned char)ro_signed;         full[7] = (unsigned char)ro_unsigned;

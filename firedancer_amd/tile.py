@@ -342,6 +342,49 @@ class HostRegistration:
         return False
 
 
+def device_cpus(info):
+    """The host CPUs on the NUMA node of an engine's device (from its PCI
+    address, /sys/bus/pci/devices/<bdf>/local_cpulist), within this
+    process's affinity; empty if unknown."""
+    bdf = f"{info['pci_domain']:04x}:{info['pci_bus']:02x}:{info['pci_device']:02x}.0"
+    try:
+        text = open(f"/sys/bus/pci/devices/{bdf}/local_cpulist").read().strip()
+    except OSError:
+        return set()
+    cpus = set()
+    for part in text.split(","):
+        if "-" in part:
+            lo, hi = part.split("-")
+            cpus.update(range(int(lo), int(hi) + 1))
+        elif part:
+            cpus.add(int(part))
+    import os
+    return cpus & os.sched_getaffinity(0)
+
+
+class NearDevice:
+    """Runs the enclosed block on the CPUs of the device's NUMA node, so
+    that host buffers first touched there (numpy allocations) sit next to
+    the GPU's PCIe link: DMA from the far socket crosses the inter-socket
+    fabric."""
+
+    def __init__(self, info):
+        import os
+        self.cpus = device_cpus(info)
+        self.saved = os.sched_getaffinity(0)
+
+    def __enter__(self):
+        import os
+        if self.cpus:
+            os.sched_setaffinity(0, self.cpus)
+        return self
+
+    def __exit__(self, *exc):
+        import os
+        os.sched_setaffinity(0, self.saved)
+        return False
+
+
 def h2d_gbps(device=0, nbytes=256 << 20, reps=8):
     """Host -> device copy bandwidth from pinned memory, GB/s."""
     return _lib.fd_ed25519_hip_h2d_gbps(int(device), int(nbytes), int(reps))

@@ -22,11 +22,15 @@ def main():
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--out", default="gpurun_out/host_fed_probe.json")
     ap.add_argument("--stream-copies", type=int, default=4)
+    ap.add_argument("--near", type=int, default=1, help="allocate host buffers on the GPU's NUMA node")
     args = ap.parse_args()
     cfg = workload.CONFIGS["C2"]
     eng = ed25519.Engine(0, max_chunk=1 << 20)
     wl = ed25519.DeviceWorkload(eng, cfg["n"], cfg["lo"], cfg["hi"], cfg["ppm"], seed=0x5EED)
     n = wl.n
+    if args.near:
+        near = tile.NearDevice(eng.info())
+        near.__enter__()
     msgs = wl.msgs.download(np.uint8, wl.msg_bytes + 16)
     off = wl.off.download(np.uint64, n)
     sz = wl.sizes.astype(np.uint32)
