@@ -256,12 +256,14 @@ def host_fed(wl, device, info, world, reps, batch, slots, copies):
     t = time.perf_counter()
     with tile.HostRegistration(msgs, off, sz, sigs, pubs, out):
         reg_s = time.perf_counter() - t
-        pool.run(msgs[:mb + 16], off[:n], sz[:n], sigs[:64 * n], pubs[:32 * n], out[:n])  # warm-up
+        pool.run(msgs, off, sz, sigs, pubs, out)  # warm-up: a whole stream (clocks, DMA engines, page tables)
         barrier(world)
         t0 = time.perf_counter()
         st = None
+        runs = []
         for _ in range(reps):
-            _, _, st = pool.run(msgs, off, sz, sigs, pubs, out)
+            _, sec, st = pool.run(msgs, off, sz, sigs, pubs, out)
+            runs.append(sec)
         dt = time.perf_counter() - t0
         barrier(world)
         ok = bool(np.array_equal(out, np.tile(expect1, copies)))
@@ -279,6 +281,7 @@ def host_fed(wl, device, info, world, reps, batch, slots, copies):
     return {"value": rate, "unit": "verifies/s", "per_gpu": rate / world, "n_gpus": world,
             "stream": f"the {n}-signature C2 set {copies} times back to back ({copies * n} signatures) x {reps}",
             "single_pass_verifies_per_s_per_gpu": n * reps / dt1,
+            "stream_run_seconds": runs,
             "batch_sigs": batch, "slots_in_flight": slots,
             "h2d_bytes_per_signature": bytes_per_sig, "achieved_h2d_GBps_per_gpu": rate / world * bytes_per_sig / 1e9,
             "pinned_copy_h2d_GBps": h2d, "pcie_bound_verifies_per_s_per_gpu": bound,
@@ -333,10 +336,11 @@ def main():
     ap.add_argument("--latency-batch", type=int, default=256)
     ap.add_argument("--latency-slots", type=int, default=4)
     ap.add_argument("--latency-txns", type=int, default=100000, help="0 disables the latency mode")
-    ap.add_argument("--host-reps", type=int, default=2, help="host-fed stream passes (0 disables)")
+    ap.add_argument("--host-reps", type=int, default=3, help="host-fed stream passes (0 disables)")
     ap.add_argument("--host-copies", type=int, default=4, help="host-fed stream: the set this many times")
     ap.add_argument("--host-batch", type=int, default=131072)
     ap.add_argument("--host-slots", type=int, default=4)
+    ap.add_argument("--host-first", action="store_true", help="run the host-fed leg first (A/B)")
     ap.add_argument("--allow-shared-device", action="store_true",
                     help="let ranks share a GPU (one-GPU rehearsal of --gpus N; n_gpus then counts devices)")
     args = ap.parse_args()
@@ -371,6 +375,10 @@ def main():
     gen_s = time.perf_counter() - t
     log(f"[rank {rank}] generated {n} signatures ({wl.msg_bytes / 1e6:.1f} MB of messages) in {gen_s:.2f} s")
 
+    hf_first = None
+    if args.host_first and args.host_reps > 0:   # A/B: the host-fed leg before the engine's timed passes
+        hf_first = host_fed(wl, device, info, world, args.host_reps, args.host_batch, args.host_slots,
+                            args.host_copies)
     for _ in range(args.warmup):
         wl.verify()
     eng.sync()
@@ -428,8 +436,8 @@ def main():
             c1 = config_c1(eng, args)
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"cpu baseline failed: {ex!r}")
-    hf = None
-    if args.host_reps > 0:
+    hf = hf_first
+    if args.host_reps > 0 and hf is None:
         try:
             hf = host_fed(wl, device, info, world, args.host_reps, args.host_batch, args.host_slots,
                           args.host_copies)

@@ -1141,6 +1141,19 @@ fd_ed25519_hip_host_unregister( void * ptr ) {
   return FD_ED25519_HIP_OK;
 }
 
+void *
+fd_ed25519_hip_host_alloc( unsigned long sz ) {
+  void * p = NULL;
+  hipError_t e = hipHostMalloc( &p, sz ? sz : 1UL, hipHostMallocPortable );
+  if( e!=hipSuccess ) { tile_fail( "hipHostMalloc", e ); return NULL; }
+  return p;
+}
+
+void
+fd_ed25519_hip_host_free( void * ptr ) {
+  if( ptr ) hipHostFree( ptr );
+}
+
 /* the calling thread onto the CPUs of the device's NUMA node (within its
    current affinity); no change when that cannot be read */
 static void

@@ -385,6 +385,47 @@ class NearDevice:
         return False
 
 
+_lib.fd_ed25519_hip_host_alloc.argtypes = [ctypes.c_ulong]
+_lib.fd_ed25519_hip_host_alloc.restype = _v
+_lib.fd_ed25519_hip_host_free.argtypes = [_v]
+
+
+class _HostMem:
+    def __init__(self, nbytes):
+        self.ptr = _lib.fd_ed25519_hip_host_alloc(max(int(nbytes), 1))
+        if not self.ptr:
+            raise HipError(f"host_alloc({nbytes}) failed: {_lib.fd_ed25519_hip_last_error().decode()}")
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            _lib.fd_ed25519_hip_host_free(self.ptr)
+            self.ptr = None
+
+
+def host_array(shape, dtype, kind="thp"):
+    """A host array for a host-fed stream: "numpy" (default allocation),
+    "thp" (anonymous mmap with MADV_HUGEPAGE: 2 MB pages when the kernel
+    grants them, fewer DMA translations), or "hostmalloc" (page-locked by
+    the HIP driver, fd_ed25519_hip_host_alloc; needs no registration)."""
+    dtype = np.dtype(dtype)
+    nbytes = int(np.prod(shape)) * dtype.itemsize
+    if kind == "numpy":
+        return np.zeros(shape, dtype)
+    if kind == "hostmalloc":
+        mem = _HostMem(nbytes)
+        buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(mem.ptr)
+        buf._mem = mem   # the array's base keeps the allocation alive
+        return np.frombuffer(buf, np.uint8, count=nbytes).view(dtype).reshape(shape)
+    import mmap
+    m = mmap.mmap(-1, max(nbytes, 1), flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    if hasattr(mmap, "MADV_HUGEPAGE"):
+        try:
+            m.madvise(mmap.MADV_HUGEPAGE)
+        except OSError:
+            pass
+    return np.frombuffer(m, np.uint8, count=nbytes).view(dtype).reshape(shape)
+
+
 def h2d_gbps(device=0, nbytes=256 << 20, reps=8):
     """Host -> device copy bandwidth from pinned memory, GB/s."""
     return _lib.fd_ed25519_hip_h2d_gbps(int(device), int(nbytes), int(reps))

@@ -406,6 +406,14 @@ fd_ed25519_hip_host_register( void * ptr, unsigned long sz );
 int
 fd_ed25519_hip_host_unregister( void * ptr );
 
+/* Page-locked host memory from the HIP driver (hipHostMalloc, portable),
+   for host-fed streams that need no registration; NULL on failure. */
+void *
+fd_ed25519_hip_host_alloc( unsigned long sz );
+
+void
+fd_ed25519_hip_host_free( void * ptr );
+
 /* Host -> device copy bandwidth of `device` in GB/s: reps copies of bytes
    from a pinned buffer (the PCIe bound of a host-fed batch). */
 double

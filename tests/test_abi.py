@@ -111,3 +111,21 @@ def test_headers_compile_as_c_and_cxx(tmp_path):
             args += ["-x", "c++"]
         r = subprocess.run(args + [str(src)], capture_output=True, text=True)
         assert r.returncode == 0, (cc, r.stderr)
+
+
+DROPIN = os.path.join(REPO, "oracle", "_ref", "dropin")
+
+
+@pytest.mark.skipif(not os.path.isdir(DROPIN), reason="oracle/_ref/dropin not built (make -C oracle ref-dropin)")
+@pytest.mark.parametrize("prog", ["test_ed25519_dropin", "test_verify_dropin"])
+def test_reference_tests_bind_to_the_dropin(prog, tmp_path):
+    """The reference's own verify tests, compiled from its sources, call
+    into libfd_ed25519_hip: here, without a GPU, its first verify call
+    fails loudly in the product library's engine creation -- never a
+    silent CPU verify (the reference's definitions are local to their
+    object).  tests/test_gpu_dropin.py runs them to 'pass' on the GPU."""
+    import subprocess
+    r = subprocess.run([os.path.join(DROPIN, prog)], capture_output=True, text=True, timeout=120, cwd=tmp_path,
+                       env=dict(os.environ, TMPDIR=str(tmp_path), HIP_VISIBLE_DEVICES="-1"))
+    assert r.returncode != 0
+    assert "libfd_ed25519_hip: FATAL: cannot create the GPU engine" in r.stderr, r.stderr[-2000:]

@@ -85,6 +85,37 @@ def main():
                          "ok": bool(np.array_equal(out4, np.tile(expect, k)))}
                     res["runs"].append(r)
                     print(json.dumps(r), flush=True)
+        # host memory kinds for the same 4M stream: numpy (default pages),
+        # mmap + MADV_HUGEPAGE, hipHostMalloc (driver pinned)
+        if k > 1:
+            try:
+                res["thp"] = open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip()
+            except OSError:
+                res["thp"] = None
+            for kind in ("numpy", "thp", "hostmalloc"):
+                bufs = {}
+                for name, arr in (("msgs", msgs4), ("off", off4), ("sz", sz4), ("sigs", sigs4), ("pubs", pubs4),
+                                  ("out", out4)):
+                    bufs[name] = tile.host_array(arr.shape, arr.dtype, kind)
+                    bufs[name][...] = arr
+                reg = tile.HostRegistration(*[b for b in bufs.values()]) if kind != "hostmalloc" else None
+                if reg:
+                    reg.__enter__()
+                pool = tile.Pool([0], 131072, 4, tile.max_span(off4, sz4, 131072))
+                pool.run(bufs["msgs"], bufs["off"], bufs["sz"], bufs["sigs"], bufs["pubs"], bufs["out"])
+                t = time.perf_counter()
+                for _ in range(3):
+                    _, _, st = pool.run(bufs["msgs"], bufs["off"], bufs["sz"], bufs["sigs"], bufs["pubs"], bufs["out"])
+                dt = time.perf_counter() - t
+                pool.close()
+                if reg:
+                    reg.__exit__(None, None, None)
+                r = {"memory": kind, "stream": k * n, "verifies_per_s": 3 * k * n / dt,
+                     "h2d_GBps": 3 * st["h2d_bytes"] / dt / 1e9, "direct": st["direct_batches"],
+                     "ok": bool(np.array_equal(bufs["out"], np.tile(expect, k)))}
+                res["runs"].append(r)
+                print(json.dumps(r), flush=True)
+                del bufs
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
     wl.free()
