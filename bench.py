@@ -339,7 +339,8 @@ def main():
     ap.add_argument("--host-reps", type=int, default=3, help="host-fed stream passes (0 disables)")
     ap.add_argument("--host-copies", type=int, default=4, help="host-fed stream: the set this many times")
     ap.add_argument("--host-batch", type=int, default=131072)
-    ap.add_argument("--host-slots", type=int, default=4)
+    ap.add_argument("--host-slots", type=int, default=3,
+                    help="3: each slot stream on its own hardware queue (4 measured 35% slower, tools/pool_first_probe.py)")
     ap.add_argument("--host-first", action="store_true", help="run the host-fed leg first (A/B)")
     ap.add_argument("--allow-shared-device", action="store_true",
                     help="let ranks share a GPU (one-GPU rehearsal of --gpus N; n_gpus then counts devices)")

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--out", default="gpurun_out/host_fed_probe.json")
     ap.add_argument("--stream-copies", type=int, default=4)
     ap.add_argument("--near", type=int, default=1, help="allocate host buffers on the GPU's NUMA node")
+    ap.add_argument("--bench-leg", type=int, default=1, help="also run bench.py's host-fed leg")
+    ap.add_argument("--only-bench-leg", type=int, default=0)
     args = ap.parse_args()
     cfg = workload.CONFIGS["C2"]
     eng = ed25519.Engine(0, max_chunk=1 << 20)
@@ -50,7 +52,7 @@ def main():
     res = {"device_resident": dev_rate, "h2d_GBps": tile.h2d_gbps(0, 256 << 20, 8), "runs": []}
     print(json.dumps(res), flush=True)
     with tile.HostRegistration(msgs, off, sz, sigs, pubs, out):
-        for feeders, batch, slots in [(1, 131072, 4), (1, 65536, 4), (1, 262144, 3), (1, 131072, 2), (2, 131072, 3),
+        for feeders, batch, slots in [] if args.only_bench_leg else [(1, 131072, 4), (1, 65536, 4), (1, 262144, 3), (1, 131072, 2), (2, 131072, 3),
                                       (2, 65536, 4), (4, 65536, 2)]:
             pool = tile.Pool([0] * feeders, batch, slots, tile.max_span(off, sz, batch))
             pool.run(msgs, off, sz, sigs, pubs, out)
@@ -66,7 +68,7 @@ def main():
             print(json.dumps(r), flush=True)
         # a longer stream: the same set 4 times back to back in one run
         # (pipeline fill and drain once per 4M instead of once per 1M)
-        k = args.stream_copies
+        k = args.stream_copies if not args.only_bench_leg else 1
         if k > 1:
             msgs4 = np.concatenate([msgs[:wl.msg_bytes]] * k + [np.zeros(16, np.uint8)])
             off4 = np.concatenate([off + np.uint64(c * wl.msg_bytes) for c in range(k)])
@@ -116,6 +118,14 @@ def main():
                 res["runs"].append(r)
                 print(json.dumps(r), flush=True)
                 del bufs
+    if args.bench_leg:
+        # bench.py's own host-fed leg in this process (A/B against the runs above)
+        import bench
+        for rep in range(args.bench_leg):
+            hf = bench.host_fed(wl, 0, eng.info(), 1, 3, 131072, 4, 4)
+            r = {"bench_leg": rep, "verifies_per_s": hf["value"], "runs": hf["stream_run_seconds"]}
+            res["runs"].append(r)
+            print(json.dumps(r), flush=True)
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
     wl.free()
