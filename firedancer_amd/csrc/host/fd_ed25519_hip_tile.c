@@ -506,8 +506,8 @@ struct fd_ed25519_hip_vtile {
   vrec_t *                  q;          /* circular FIFO of records */
   unsigned long             q_cap, q_head, q_cnt;
   unsigned long             resolved_head;  /* records [q_head, q_head+resolved_head) are resolved */
-  unsigned char *           oa;         /* output arena: frags, live bytes [oa_head, oa_tail) */
-  unsigned long             oa_cap, oa_head, oa_tail;
+  unsigned char *           oa;         /* output arena: a ring of frags, [oa_head, oa_tail) cyclically */
+  unsigned long             oa_cap, oa_head, oa_tail, oa_live;
 };
 
 fd_ed25519_hip_vtile_t *
@@ -563,36 +563,46 @@ vq_push( fd_ed25519_hip_vtile_t * vt ) {
   return r;
 }
 
-/* `need` bytes at the arena's tail (64-byte aligned offset): the live
-   region moves to the front, or the arena grows, when the tail is short */
+/* The output arena is a ring of frags in record order: live bytes run
+   from oa_head to oa_tail, cyclically (oa_live tells a full ring from an
+   empty one); a frag never straddles the end (the tail wraps to 0 when the
+   end is short, the skipped bytes come free with the record before).  It
+   grows -- frags copied in order to a new ring, offsets rebased -- only
+   when full.  `need` bytes at a 64-byte aligned offset: */
 static unsigned long
 oa_reserve( fd_ed25519_hip_vtile_t * vt, unsigned long need ) {
-  if( vt->oa_tail + need > vt->oa_cap ) {
-    if( vt->oa_head ) {   /* compact: rebase the live records' offsets */
-      unsigned long h = vt->oa_head;
-      memmove( vt->oa, vt->oa + h, vt->oa_tail - h );
-      for( unsigned long k=0UL; k<vt->q_cnt; k++ ) {
-        vrec_t * r = vq_at( vt, k );
-        if( r->arena_len ) r->arena_off -= h;
-      }
-      vt->oa_tail -= h;
-      vt->oa_head  = 0UL;
-    }
-    if( vt->oa_tail + need > vt->oa_cap ) {
-      unsigned long ncap = vt->oa_cap;
-      while( vt->oa_tail + need > ncap ) ncap *= 2UL;
-      unsigned char * n = (unsigned char *)realloc( vt->oa, ncap );
-      if( !n ) { fprintf( stderr, "libfd_ed25519_hip: FATAL: vtile arena allocation failed\n" ); abort(); }
-      vt->oa = n; vt->oa_cap = ncap;
-    }
+  need = (need + 63UL) & ~63UL;   /* oa_commit's aligned length never exceeds it */
+  if( !vt->oa_live ) vt->oa_head = vt->oa_tail = 0UL;
+  if( vt->oa_tail>=vt->oa_head ) {                        /* free: [tail, cap) and [0, head) */
+    if( vt->oa_cap - vt->oa_tail>=need ) return vt->oa_tail;
+    if( vt->oa_head>need ) return 0UL;                    /* wrap */
+  } else if( vt->oa_head - vt->oa_tail>need ) {           /* free: [tail, head) */
+    return vt->oa_tail;
   }
-  return vt->oa_tail;
+  /* full: a ring twice as large (or more), the live frags copied over in
+     record order */
+  unsigned long ncap = 2UL*vt->oa_cap;
+  while( ncap < 2UL*need ) ncap *= 2UL;
+  unsigned char * n = (unsigned char *)malloc( ncap );
+  if( !n ) { fprintf( stderr, "libfd_ed25519_hip: FATAL: vtile arena allocation failed\n" ); abort(); }
+  unsigned long pos = 0UL;
+  for( unsigned long k=0UL; k<vt->q_cnt; k++ ) {
+    vrec_t * r = vq_at( vt, k );
+    if( !r->arena_len ) continue;
+    memcpy( n + pos, vt->oa + r->arena_off, r->arena_len );
+    r->arena_off = pos;
+    pos += r->arena_len;
+  }
+  free( vt->oa );
+  vt->oa = n; vt->oa_cap = ncap; vt->oa_head = 0UL; vt->oa_tail = pos;
+  return pos;
 }
 
 static unsigned
 oa_commit( fd_ed25519_hip_vtile_t * vt, unsigned long off, unsigned long used ) {
   unsigned long len = (used + 63UL) & ~63UL;
   vt->oa_tail = off + len;
+  vt->oa_live++;
   return (unsigned)len;
 }
 
@@ -799,13 +809,15 @@ fd_ed25519_hip_vtile_poll_frags( fd_ed25519_hip_vtile_t * vt, int wait, unsigned
     if( cookie  ) cookie [ n ] = r->cookie;
     if( verdict ) verdict[ n ] = r->verdict;
     if( tag     ) tag    [ n ] = r->tag;
-    if( r->arena_len ) vt->oa_head = r->arena_off + r->arena_len;   /* arena bytes come free in record order */
+    if( r->arena_len ) {   /* arena bytes come free in record order */
+      vt->oa_head = r->arena_off + r->arena_len;
+      vt->oa_live--;
+    }
     n++;
     vt->q_head = (vt->q_head+1UL) % vt->q_cap;
     vt->q_cnt--;
     vt->resolved_head--;
   }
-  if( !vt->q_cnt ) vt->oa_head = vt->oa_tail = 0UL;
   return n;
 }
 
@@ -987,6 +999,90 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
   free( rg.mcache ); free( rg.dcache ); free( t_pub ); free( ck ); free( vd ); free( buf );
   fd_ed25519_hip_vtile_delete( vt );
   return FD_ED25519_HIP_OK;
+}
+
+/* ======================================================================
+   several verify tiles: one thread per tile, each a whole latency_run on
+   its round-robin share of the transactions */
+
+typedef struct {
+  int                   device;
+  unsigned              slot_cnt;
+  unsigned long         batch_sigs, ring_depth, n;
+  unsigned char const * payloads;
+  unsigned long *       off;
+  unsigned int *        sz;
+  double                rate;
+  int                   flags;
+  double *              lat;
+  signed char *         verdict;
+  fd_ed25519_hip_latency_result_t res;
+  int                   err;
+} tile_job_t;
+
+static void *
+tile_main( void * arg ) {
+  tile_job_t * j = (tile_job_t *)arg;
+  j->err = fd_ed25519_hip_latency_run( j->device, j->slot_cnt, j->batch_sigs, j->payloads, j->off, j->sz, j->n, j->rate,
+                                       j->ring_depth, j->flags, j->lat, j->verdict, &j->res );
+  return NULL;
+}
+
+int
+fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_cnt, unsigned long batch_sigs,
+                                  unsigned char const * payloads, unsigned long const * payload_off,
+                                  unsigned int const * payload_sz, unsigned long txn_cnt, double offered_txn_per_s,
+                                  unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
+                                  fd_ed25519_hip_latency_result_t * res ) {
+  if( !tile_cnt || tile_cnt>64U || txn_cnt<tile_cnt || !lat_s || !verdict || !res ) return FD_ED25519_HIP_ERR_INVAL;
+  tile_job_t job[ 64 ];
+  pthread_t  th[ 64 ];
+  memset( job, 0, sizeof(job) );
+  int err = 0;
+  for( unsigned k=0U; k<tile_cnt; k++ ) {
+    tile_job_t * j = &job[k];
+    j->n = (txn_cnt - k + tile_cnt - 1UL) / tile_cnt;   /* transactions k, k+K, k+2K, ... */
+    j->off = (unsigned long *)malloc( j->n*sizeof(unsigned long) );
+    j->sz  = (unsigned int  *)malloc( j->n*sizeof(unsigned int) );
+    j->lat = (double *)malloc( j->n*sizeof(double) );
+    j->verdict = (signed char *)malloc( j->n );
+    if( !j->off || !j->sz || !j->lat || !j->verdict ) { err = FD_ED25519_HIP_ERR_NOMEM; break; }
+    for( unsigned long i=0UL; i<j->n; i++ ) {
+      j->off[i] = payload_off[ k + i*tile_cnt ];
+      j->sz [i] = payload_sz [ k + i*tile_cnt ];
+    }
+    j->device = device; j->slot_cnt = slot_cnt; j->batch_sigs = batch_sigs; j->ring_depth = ring_depth;
+    j->payloads = payloads; j->rate = offered_txn_per_s / (double)tile_cnt; j->flags = flags;
+  }
+  unsigned started = 0U;
+  for( unsigned k=0U; !err && k<tile_cnt; k++ ) {
+    if( pthread_create( &th[k], NULL, tile_main, &job[k] ) ) { err = FD_ED25519_HIP_ERR_NOMEM; break; }
+    started++;
+  }
+  for( unsigned k=0U; k<started; k++ ) pthread_join( th[k], NULL );
+  memset( res, 0, sizeof(*res) );
+  res->offered_txn_per_s = offered_txn_per_s;
+  for( unsigned k=0U; k<tile_cnt; k++ ) {
+    tile_job_t * j = &job[k];
+    if( !err && j->err ) err = j->err;
+    if( !err ) {
+      for( unsigned long i=0UL; i<j->n; i++ ) {
+        lat_s  [ k + i*tile_cnt ] = j->lat[i];
+        verdict[ k + i*tile_cnt ] = j->verdict[i];
+      }
+      if( j->res.seconds>res->seconds ) res->seconds = j->res.seconds;
+      res->txn_cnt       += j->res.txn_cnt;
+      res->sig_cnt       += j->res.sig_cnt;
+      res->batches       += j->res.batches;
+      res->ring_overruns += j->res.ring_overruns;
+    }
+    free( j->off ); free( j->sz ); free( j->lat ); free( j->verdict );
+  }
+  if( !err && res->seconds>0.0 ) {
+    res->achieved_txn_per_s = (double)res->txn_cnt / res->seconds;
+    res->achieved_sig_per_s = (double)res->sig_cnt / res->seconds;
+  }
+  return err;
 }
 
 /* ======================================================================

@@ -80,6 +80,9 @@ _lib.fd_ed25519_hip_vtile_pending.restype = ctypes.c_ulong
 _lib.fd_ed25519_hip_latency_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, _v, _v, _v, ctypes.c_ulong,
                                             ctypes.c_double, ctypes.c_ulong, ctypes.c_int, _v, _v,
                                             ctypes.POINTER(LatencyResult)]
+_lib.fd_ed25519_hip_latency_run_tiles.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_ulong, _v, _v, _v,
+                                                  ctypes.c_ulong, ctypes.c_double, ctypes.c_ulong, ctypes.c_int, _v,
+                                                  _v, ctypes.POINTER(LatencyResult)]
 _lib.fd_ed25519_hip_pool_verify.argtypes = [_v, ctypes.c_uint, ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, _v, _v,
                                             _v, _v, _v, _v, ctypes.POINTER(ctypes.c_double)]
 
@@ -232,7 +235,8 @@ def pack_payloads(payloads):
     return buf, off, sz
 
 
-def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=256, ring_depth=4096, gpu_parse=False):
+def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=256, ring_depth=4096, gpu_parse=False,
+                tiles=1):
     """Latency mode (C5): a producer thread publishes the payloads into a
     tango-style ring at the offered rate; the verify tile consumes them.
     payloads: a list of byte strings, or a uint8 array [n][size] of
@@ -249,10 +253,16 @@ def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=25
     lat = np.zeros(n, np.float64)
     verdict = np.zeros(n, np.int8)
     res = LatencyResult()
-    _check(_lib.fd_ed25519_hip_latency_run(int(device), int(slot_cnt), int(batch_sigs), _ptr(buf), _ptr(off), _ptr(sz),
-                                           n, float(offered_txn_per_s), int(ring_depth),
-                                           VTILE_GPU_PARSE if gpu_parse else 0, _ptr(lat), _ptr(verdict),
-                                           ctypes.byref(res)))
+    if tiles > 1:   # several verify tiles, transaction i to tile i % tiles
+        _check(_lib.fd_ed25519_hip_latency_run_tiles(int(device), int(tiles), int(slot_cnt), int(batch_sigs), _ptr(buf),
+                                                     _ptr(off), _ptr(sz), n, float(offered_txn_per_s), int(ring_depth),
+                                                     VTILE_GPU_PARSE if gpu_parse else 0, _ptr(lat), _ptr(verdict),
+                                                     ctypes.byref(res)))
+    else:
+        _check(_lib.fd_ed25519_hip_latency_run(int(device), int(slot_cnt), int(batch_sigs), _ptr(buf), _ptr(off),
+                                               _ptr(sz), n, float(offered_txn_per_s), int(ring_depth),
+                                               VTILE_GPU_PARSE if gpu_parse else 0, _ptr(lat), _ptr(verdict),
+                                               ctypes.byref(res)))
     return lat, verdict, {f: getattr(res, f) for f, _ in LatencyResult._fields_}
 
 

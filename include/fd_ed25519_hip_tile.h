@@ -281,6 +281,20 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
                             unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
                             fd_ed25519_hip_latency_result_t * res );
 
+/* Several verify tiles on one GPU (the reference runs
+   verify_tile_count of them, src/app/fdctl/config/default.toml:535, frag
+   seq going to tile seq % count, src/app/fdctl/run/tiles/fd_verify.c:46):
+   tile_cnt threads, each with its own ring, producer, tcache and pipe
+   (slot_cnt batches in flight), transaction i to tile i % tile_cnt, all at
+   the offered rate in total.  lat_s / verdict are by transaction index;
+   res sums the tiles (seconds: the longest tile). */
+int
+fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_cnt, unsigned long batch_sigs,
+                                  unsigned char const * payloads, unsigned long const * payload_off,
+                                  unsigned int const * payload_sz, unsigned long txn_cnt, double offered_txn_per_s,
+                                  unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
+                                  fd_ed25519_hip_latency_result_t * res );
+
 /* ---- shlink + verify service (GPU process outside the sandbox) -------- */
 
 /* A single-producer single-consumer tango-style link in a POSIX shm object

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--batches", default="256,4096,16384,65536")
     ap.add_argument("--slots", default="3")
     ap.add_argument("--modes", default="host,gpu", help="parse on the host, the GPU, or both")
+    ap.add_argument("--tiles", default="1", help="verify tiles (threads) on the GPU, comma list")
     args = ap.parse_args()
     from firedancer_amd import ed25519, tile, workload
     eng = ed25519.Engine(0, max_chunk=1 << 16)
@@ -39,12 +40,14 @@ def main():
            "python_parse_call_us": parse_us_py, "runs": []}
     tile.latency_run(pay[:20000], 0.0, slot_cnt=2, batch_sigs=4096)   # warm-up: code objects, pinned pools
     for mode in args.modes.split(","):
+     for tiles in [int(x) for x in args.tiles.split(",")]:
       for slots in [int(s) for s in args.slots.split(",")]:
         for b in [int(x) for x in args.batches.split(",")]:
             lat, v, res = tile.latency_run(pay, 0.0, slot_cnt=slots, batch_sigs=b, ring_depth=1 << 14,
-                                           gpu_parse=(mode == "gpu"))
+                                           gpu_parse=(mode == "gpu"), tiles=tiles)
             ms = lat * 1e3
-            out["runs"].append({"parse": mode, "batch_sigs": b, "slots": slots, "txn_per_s": res["achieved_txn_per_s"],
+            out["runs"].append({"parse": mode, "tiles": tiles, "batch_sigs": b, "slots": slots,
+                                "txn_per_s": res["achieved_txn_per_s"],
                                 "p50_ms": float(np.percentile(ms, 50)), "p99_ms": float(np.percentile(ms, 99)),
                                 "batches": res["batches"], "overruns": res["ring_overruns"],
                                 "all_success": bool((v == 0).all())})
