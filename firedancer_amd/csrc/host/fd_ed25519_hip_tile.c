@@ -477,12 +477,12 @@ fd_ed25519_hip_tcache_insert( fd_ed25519_hip_tcache_t * tc, unsigned long tag ) 
 
    Each SUCCESS transaction also yields the frag the reference tile
    publishes (after_frag, fd_verify.c:102-133: payload, pad, fd_txn_t,
-   payload_sz), built in an output arena: at frag time from the host
-   parse, or -- GPU-parse mode -- at resolve time from the slot's payload
-   copy and the trailer the device parser wrote (a host parse only for the
-   rare fd_txn_t longer than the device's 64-byte trailer slot).  Arena
-   bytes are handed out by vtile_poll_frags in frag order and reclaimed as
-   records are polled. */
+   payload_sz), built in an output arena at resolve time from the
+   payload copy in the batch and the fd_txn_t trailer its parse left there
+   (64 bytes per transaction, written by the host parse or -- GPU-parse
+   mode -- the device's; a host parse only for the rare fd_txn_t longer
+   than that).  Arena bytes are handed out by vtile_poll_frags in frag
+   order and reclaimed as records are polled. */
 
 typedef struct {
   unsigned long cookie;
@@ -630,13 +630,22 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
     else                                                      v = FD_ED25519_HIP_TXN_VERIFY_SUCCESS;
     r->verdict  = (signed char)v;
     r->resolved = 1;
-    if( v!=FD_ED25519_HIP_TXN_VERIFY_SUCCESS ) { r->frag_sz = 0; continue; }   /* filtered: not published */
-    if( vt->gpu_parse ) {
-      /* the published frag from the payload in the slot and the device's
-         fd_txn_t trailer (host parse when it exceeds the 64-byte slot) */
-      unsigned char const * pay = s->msgs + s->msg_off[ r->txn_idx ];
-      unsigned long         psz = s->msg_sz[ r->txn_idx ];
-      unsigned char const * tr  = s->txn_trailer + 64UL*r->txn_idx;
+    if( v!=FD_ED25519_HIP_TXN_VERIFY_SUCCESS ) continue;   /* filtered: not published */
+    {
+      /* the published frag from the payload in the slot and the fd_txn_t
+         trailer its parse left in the slot (the device's in GPU-parse
+         mode; a host parse when it exceeds the 64-byte trailer slot) */
+      unsigned long ti = r->txn_idx, poff, psz;
+      if( vt->gpu_parse ) {
+        poff = s->msg_off[ ti ];
+        psz  = s->msg_sz [ ti ];
+      } else {   /* the signatures' message pointer, back over the signatures (signature_off is 1) */
+        unsigned long k = s->txn_first[ ti ], mo = 1UL + 64UL*s->txn_sig_cnt[ ti ];
+        poff = s->msg_off[ k ] - mo;
+        psz  = s->msg_sz [ k ] + mo;
+      }
+      unsigned char const * pay = s->msgs + poff;
+      unsigned char const * tr  = s->txn_trailer + 64UL*ti;
       unsigned long foot = FD_ED25519_HIP_TXN_FOOTPRINT( (unsigned long)tr[18] | ((unsigned long)tr[19]<<8),
                                                          (unsigned long)tr[14] );
       unsigned long toff = (psz + 1UL) & ~1UL;
@@ -735,30 +744,32 @@ int
 fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
                            unsigned long cookie ) {
   if( vt->gpu_parse ) return vt_frag_raw( vt, payload, payload_sz, cookie );
-  /* during_frag + after_frag: the payload and its fd_txn_t trailer go
-     into the output arena as the frag the tile publishes on SUCCESS */
+  /* during_frag + after_frag: the payload goes into the open batch whole
+     (the published frag is built from it if the transaction succeeds) and
+     the parse writes fd_txn_t's first 64 bytes into the batch's trailer
+     slot */
   fd_ed25519_hip_txn_t t;
-  unsigned long aoff = oa_reserve( vt, ((payload_sz + 1UL) & ~1UL) + FD_ED25519_HIP_TXN_MAX_SZ + 2UL );
-  unsigned long fsz  = txn_frag_core( payload, payload_sz, vt->oa + aoff, &t );
-  if( !fsz ) {
+  vt_open( vt );
+  fd_ed25519_hip_slot_t * s = vt->open;
+  unsigned long foot = fd_txn_core_parse( payload, payload_sz, &t, s->txn_trailer + 64UL*s->txn_cnt, 64UL );
+  if( !foot ) {
     vrec_t * r = vq_push( vt );
     r->cookie = cookie; r->verdict = FD_ED25519_HIP_TXN_PARSE_FAILED; r->resolved = 1;
     vt_advance( vt );
     return 0;
   }
-  unsigned alen = oa_commit( vt, aoff, fsz );
-  unsigned long nsig   = (t.signature_cnt>=1U && t.signature_cnt<=16U) ? t.signature_cnt : 0UL;
-  unsigned long msg_sz = payload_sz - t.message_off;
-  vt_open( vt );
-  fd_ed25519_hip_slot_t * s = vt->open;
-  if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap || s->msg_bytes+msg_sz>s->msg_cap ) ) {
+  unsigned long nsig = (t.signature_cnt>=1U && t.signature_cnt<=16U) ? t.signature_cnt : 0UL;
+  if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap || s->msg_bytes+payload_sz>s->msg_cap ) ) {
     vt_submit_open( vt );
     vt_open( vt );
     s = vt->open;
+    fd_txn_core_parse( payload, payload_sz, &t, s->txn_trailer + 64UL*s->txn_cnt, 64UL );
   }
-  unsigned long moff = s->msg_bytes;
-  memcpy( s->msgs + moff, payload + t.message_off, msg_sz );
-  s->msg_bytes += msg_sz;
+  unsigned long poff   = s->msg_bytes;
+  unsigned long moff   = poff + t.message_off;
+  unsigned long msg_sz = payload_sz - t.message_off;
+  memcpy( s->msgs + poff, payload, payload_sz );
+  s->msg_bytes += payload_sz;
   unsigned long first = s->sig_cnt;
   for( unsigned long j=0UL; j<nsig; j++ ) {
     unsigned long k = first + j;
@@ -773,9 +784,6 @@ fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * pa
   s->txn_sig_cnt[ ti ] = t.signature_cnt;   /* 17..127 -> ERR_SIG, no signatures staged */
   vrec_t * r = vq_push( vt );
   r->cookie    = cookie;
-  r->arena_off = aoff;
-  r->arena_len = alen;
-  r->frag_sz   = (unsigned short)fsz;
   memcpy( &r->tag, payload + t.signature_off, 8UL );  /* ha_dedup_tag, fd_verify.h:65 */
   r->slot_seq = vt->open_seq;
   r->txn_idx  = (unsigned)ti;
