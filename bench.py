@@ -309,6 +309,20 @@ def pmc_traffic(n):
         return None, None
 
 
+def pmc_issue_rate(cu_cnt):
+    """The dsm kernel's VALU issue rate from the committed PMC summary:
+    wave-instructions (SQ_INSTS_VALU) per SIMD over the kernel's active
+    cycles (GRBM_GUI_ACTIVE, summed over the 8 XCDs), i.e. cycles per
+    VALU wave-instruction per SIMD (the measured issue
+    costs are 2.5 for 32-bit VOP2 ops, 4.2-4.4 for VOP3, 5.2 for the
+    32x32->64 multiply-add)."""
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", "pmc_latest.json")))["fd_ed25519_dsm_kernel"]["per_dispatch"]
+        return d["GRBM_GUI_ACTIVE"] / 8.0 / (d["SQ_INSTS_VALU"] / (cu_cnt * 4))
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
+
+
 def pmc_valu_per_sig():
     """Executed INT32+INT64 VALU instructions per signature (= per lane:
     one signature per lane) of the dsm kernel (rocprofv3
@@ -485,7 +499,11 @@ def main():
                          "ops_per_launch": dsm_ops, "launch_ms": per_launch["dsm"],
                          "executed": {"achieved": executed, "frac": (executed / peak) if executed else None,
                                       "unit": "TOPS (INT32+INT64 VALU lane-instructions / s)",
-                                      "valu_per_signature": valu, "source": traffic_src},
+                                      "valu_per_signature": valu, "source": traffic_src,
+                                      "cycles_per_valu_instruction_per_simd": pmc_issue_rate(info["cu_cnt"]),
+                                      "issue_note": "the peak assumes a wave64 instruction every 2 cycles per SIMD; "
+                                                    "measured issue costs are 2.5 (VOP2), 4.2-4.4 (VOP3), 5.2 "
+                                                    "(32x32->64 mad, 68% of dsm's instructions): DESIGN.md 2.4"},
                          "path": {"achieved": path_achieved, "frac": (path_achieved / peak) if path_achieved else None,
                                   "ops_per_verify_mean": path_ops * chunks / n, "ms_per_launch": path_ms},
                          "signatures_per_launch": min(n, info["max_chunk"])},
