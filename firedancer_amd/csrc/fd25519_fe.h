@@ -206,6 +206,125 @@ FD_DEV void fe_sq2(fe& h, const fe& f) {
   fe_carry_wide(h, a);
 }
 
+/* ------------------------------------------------------------------------
+   Unsigned-limb forms (suffix _u): the same products, reduced with floor
+   carries, so the output limbs are the plain digits, in [0, 2^w) (limbs 1
+   and 6 within 2^10 of that range): <= 2.0x in the units above, i.e.
+   "tight" only in magnitude, not centered.
+
+   Without a rounding bias no column needs a constant, so each column's
+   accumulation starts from the previous column's carry -- the carry is the
+   addend of the column's first multiply-add -- and the 64-bit add of every
+   carry step disappears (9 v_lshl_add_u64 per product), as do the ten
+   bias subtractions.  The columns run in two chains (0..4 and 5..9) so two
+   multiply-add streams are in flight; the chains are joined by two short
+   steps: column 4's carry into limb 5 (re-split into limb 6) and 19 times
+   column 9's carry into limb 0 (re-split into limb 1).
+
+   Inputs as for fe_mul / fe_sq (the 19-side <= 3.3x).  The callers keep
+   every sum fed to a product within that bound (fd25519_ge.h). */
+FD_DEV void fe_join_u(int32_t (&u)[10], int64_t c4, int64_t c9) {
+  {
+    const int64_t t = c4 + (int64_t)(uint32_t)u[5];
+    u[5] = (int32_t)t & ((1 << 25) - 1);
+    u[6] += (int32_t)(t >> 25);
+  }
+  {
+    const int64_t t = c9 * 19 + (int64_t)(uint32_t)u[0];
+    u[0] = (int32_t)t & ((1 << 26) - 1);
+    u[1] += (int32_t)(t >> 26);
+  }
+}
+
+/* The digits are known non-negative to the compiler, which then splits a
+   later signed product into an unsigned multiply-add plus a correction of
+   the high word (two instructions and moves instead of one
+   v_mad_i64_i32); hiding the range keeps every product one instruction. */
+FD_DEV void fe_launder_u(fe& h, int32_t (&u)[10]) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    asm("" : "+v"(u[i]));
+    h.v[i] = u[i];
+  }
+}
+
+FD_DEV void fe_mul19_u(fe& h, const fe& f, const fe& g, const fe& g19) {
+  int32_t u[10];
+  int64_t cA = 0, cB = 0;
+#pragma unroll
+  for (int s = 0; s < 5; s++) {
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      const int k = s + 5 * half;
+      int64_t acc = half ? cB : cA;
+#pragma unroll
+      for (int n = 0; n < 10; n++) {
+        const int i = n, j = (k - i + 10) % 10;
+        const int32_t x = ((i & 1) && (j & 1)) ? 2 * f.v[i] : f.v[i];
+        const int32_t y = (i + j >= 10) ? g19.v[j] : g.v[j];
+        if (s == 0 && n == 0) acc = (int64_t)x * y;
+        else acc += (int64_t)x * y;
+#if FE_ASM_MAD
+        asm("" : "+v"(acc));
+#endif
+      }
+      const int w = (k & 1) ? 25 : 26;
+      u[k] = (int32_t)acc & ((1 << w) - 1);
+      if (half) cB = acc >> w;
+      else cA = acc >> w;
+    }
+  }
+  fe_join_u(u, cA, cB);
+  fe_launder_u(h, u);
+}
+
+FD_DEV void fe_mul_u(fe& h, const fe& f, const fe& g) {
+  fe g19;
+  fe_19(g19, g);
+  fe_mul19_u(h, f, g, g19);
+}
+
+/* h = S f^2, S = 1 or 2 */
+template <int S>
+FD_DEV void fe_sqs_u(fe& h, const fe& f) {
+  int32_t u[10];
+  int64_t cA = 0, cB = 0;
+#pragma unroll
+  for (int s = 0; s < 5; s++) {
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      const int k = s + 5 * half;
+      int64_t acc = half ? cB : cA;
+      bool first = (s == 0);
+#pragma unroll
+      for (int i = 0; i < 10; i++) {
+#pragma unroll
+        for (int j = i; j < 10; j++) {
+          if ((i + j) % 10 != k) continue;
+          const int m = (((i & 1) && (j & 1)) ? 2 : 1) * ((i + j >= 10) ? 19 : 1);
+          const int32_t x = (i == j) ? S * f.v[i] : 2 * S * f.v[i];
+          const int32_t y = m * f.v[j];
+          if (first) acc = (int64_t)x * y;
+          else acc += (int64_t)x * y;
+          first = false;
+#if FE_ASM_MAD
+          asm("" : "+v"(acc));
+#endif
+        }
+      }
+      const int w = (k & 1) ? 25 : 26;
+      u[k] = (int32_t)acc & ((1 << w) - 1);
+      if (half) cB = acc >> w;
+      else cA = acc >> w;
+    }
+  }
+  fe_join_u(u, cA, cB);
+  fe_launder_u(h, u);
+}
+
+FD_DEV void fe_sq_u(fe& h, const fe& f) { fe_sqs_u<1>(h, f); }
+FD_DEV void fe_sq2_u(fe& h, const fe& f) { fe_sqs_u<2>(h, f); }
+
 /* Re-tighten a 32-bit-limb element (e.g. the result of adds/subs). */
 FD_DEV void fe_carry(fe& h, const fe& f) {
   int64_t a[10];
