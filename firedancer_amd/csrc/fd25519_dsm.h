@@ -146,7 +146,7 @@ FD_DEV void atab_store(int4* lane_tab, int e, const ge_cached& c) {
   for (int i = 0; i < 10; i++) {
     v[i] = c.YplusX.v[i];
     v[10 + i] = c.YminusX.v[i];
-    v[20 + i] = c.Z.v[i];
+    v[20 + i] = c.Z2.v[i];
     v[30 + i] = c.T2d.v[i];
   }
 #pragma unroll
@@ -165,7 +165,7 @@ FD_DEV void atab_load(ge_cached& c, const int4* lane_tab, int e) {
   for (int i = 0; i < 10; i++) {
     c.YplusX.v[i] = v[i];
     c.YminusX.v[i] = v[10 + i];
-    c.Z.v[i] = v[20 + i];
+    c.Z2.v[i] = v[20 + i];
     c.T2d.v[i] = v[30 + i];
   }
 }

@@ -403,37 +403,39 @@ FD_DEV int fe_isodd(const fe& f) {
 }
 
 /* z^(2^252-3) -- same addition chain as fd_f25519_pow22523
-   (src/ballet/ed25519/fd_f25519.c:11-59): 250 squarings, 11 products. */
+   (src/ballet/ed25519/fd_f25519.c:11-59): 250 squarings, 11 products, all
+   in the unsigned-limb forms (a chain of products only: every input is a
+   previous output, <= 2x; the result is unsigned, <= 2x). */
 FD_DEV void fe_sqn(fe& h, const fe& f, int n) {
-  fe_sq(h, f);
+  fe_sq_u(h, f);
 #pragma clang loop unroll(disable)
-  for (int i = 1; i < n; i++) fe_sq(h, h);
+  for (int i = 1; i < n; i++) fe_sq_u(h, h);
 }
 
 FD_DEV void fe_pow22523(fe& out, const fe& z) {
   fe t0, t1, t2;
-  fe_sq(t0, z);
+  fe_sq_u(t0, z);
   fe_sqn(t1, t0, 2);
-  fe_mul(t1, z, t1);
-  fe_mul(t0, t0, t1);
-  fe_sq(t0, t0);
-  fe_mul(t0, t1, t0);
+  fe_mul_u(t1, z, t1);
+  fe_mul_u(t0, t0, t1);
+  fe_sq_u(t0, t0);
+  fe_mul_u(t0, t1, t0);
   fe_sqn(t1, t0, 5);
-  fe_mul(t0, t1, t0);
+  fe_mul_u(t0, t1, t0);
   fe_sqn(t1, t0, 10);
-  fe_mul(t1, t1, t0);
+  fe_mul_u(t1, t1, t0);
   fe_sqn(t2, t1, 20);
-  fe_mul(t1, t2, t1);
+  fe_mul_u(t1, t2, t1);
   fe_sqn(t1, t1, 10);
-  fe_mul(t0, t1, t0);
+  fe_mul_u(t0, t1, t0);
   fe_sqn(t1, t0, 50);
-  fe_mul(t1, t1, t0);
+  fe_mul_u(t1, t1, t0);
   fe_sqn(t2, t1, 100);
-  fe_mul(t1, t2, t1);
+  fe_mul_u(t1, t2, t1);
   fe_sqn(t1, t1, 50);
-  fe_mul(t0, t1, t0);
+  fe_mul_u(t0, t1, t0);
   fe_sqn(t0, t0, 2);
-  fe_mul(out, t0, z);
+  fe_mul_u(out, t0, z);
 }
 
 /* 1/z = z^(p-2) = (z^(2^252-3))^8 * z^3 */

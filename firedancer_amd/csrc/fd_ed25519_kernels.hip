@@ -199,7 +199,14 @@ FD_DEV int precheck(const fd_ed25519_verify_params_t& p, uint64_t j) {
 }
 
 /* [0..8](sign P) in cached form for the affine point (x, y), into a lane's
-   9-entry table */
+   9-entry table; NT: the entries hold -2dT (ge_add<true>) */
+template <bool NT>
+FD_DEV void table_store(int4* tab, int e, ge_cached c) {
+  if (NT) fe_neg(c.T2d, c.T2d);
+  atab_store(tab, e, c);
+}
+
+template <bool NT>
 FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
   ge_p3 P0;
   fe xn;
@@ -209,10 +216,10 @@ FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
   fe_1(P0.Z);
   fe_mul(P0.T, P0.X, y);
   ge_cached c1, c;
-  c.YplusX = P0.Z; c.YminusX = P0.Z; c.Z = P0.Z; fe_0(c.T2d);  /* identity */
+  c.YplusX = P0.Z; c.YminusX = P0.Z; fe_add(c.Z2, P0.Z, P0.Z); fe_0(c.T2d);  /* identity */
   atab_store(tab, 0, c);
   ge_p3_to_cached(c1, P0);
-  atab_store(tab, 1, c1);
+  table_store<NT>(tab, 1, c1);
   /* P0 is affine: the multiples by mixed additions (3 multiplications) */
   ge_precomp pre;
   pre.yplusx = c1.YplusX; pre.yminusx = c1.YminusX; pre.xy2d = c1.T2d;
@@ -223,7 +230,7 @@ FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
     ge_madd(sum, cur, pre);
     ge_p1p1_to_p3(cur, sum);
     ge_p3_to_cached(c, cur);
-    atab_store(tab, e, c);
+    table_store<NT>(tab, e, c);
   }
 }
 
@@ -527,9 +534,9 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
   {
     fe x, y;
     load_pt(x, y, p, 0, j);
-    table_build(tabA, x, y, true);
+    table_build<true>(tabA, x, y, true);
     load_pt(x, y, p, 1, j);
-    table_build(tabR, x, y, !(hf & FD_HF_DNEG));
+    table_build<false>(tabR, x, y, !(hf & FD_HF_DNEG));
   }
   /* digits, most significant first, top-aligned in 160 bits: c, |d| in
      radix 16 (W signed digits, the top one in [0,8]), s_lo, s_hi in
@@ -571,12 +578,12 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
         ge_p2_dbl(Rt, Q);
         if (dbl < 3) ge_p1p1_to_p2(Q, Rt);
       }
-      ge_p1p1_to_p3(P, Rt);
+      ge_p1p1_to_p3_u(P, Rt);
     }
     atab_load(cr, tabR, er < 0 ? -er : er);
     ge_cached_cneg(ca, ea < 0);
-    ge_add(Rt, P, ca);
-    ge_p1p1_to_p3(P, Rt);
+    ge_add<true>(Rt, P, ca);
+    ge_p1p1_to_p3_u(P, Rt);
     if (badd) {
       f = pop160u<20>(ld);
       g = pop160u<20>(hd);
@@ -586,9 +593,9 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     ge_cached_cneg(cr, er < 0);
     ge_add(Rt, P, cr);
     if (badd) {
-      ge_p1p1_to_p3(P, Rt);
+      ge_p1p1_to_p3_uxyt(P, Rt);
       ge_madd(Rt, P, b1);
-      ge_p1p1_to_p3(P, Rt);
+      ge_p1p1_to_p3_uxyt(P, Rt);
       ge_madd(Rt, P, b2);
     }
     ge_p1p1_to_p2(Q, Rt);
@@ -612,7 +619,7 @@ FD_DEV int dsm_full_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
   {
     fe x, y;
     load_pt(x, y, p, 0, j);
-    table_build(tabA, x, y, true);
+    table_build<false>(tabA, x, y, true);
   }
   uint32_t kd[8], sd[8];
   {
@@ -645,11 +652,11 @@ FD_DEV int dsm_full_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
         ge_p2_dbl(Rt, Q);
         if (dbl < 3) ge_p1p1_to_p2(Q, Rt);
       }
-      ge_p1p1_to_p3(P, Rt);
+      ge_p1p1_to_p3_u(P, Rt);
     }
     table_add(Rt, P, tabA, pop_digit<4>(kd));
     if (badd) {
-      ge_p1p1_to_p3(P, Rt);
+      ge_p1p1_to_p3_uxyt(P, Rt);
       btab_add(Rt, P, b, f);
     }
     ge_p1p1_to_p2(Q, Rt);

@@ -4,7 +4,8 @@
 // previous column's carry).  Squaring chains of 1 (a decompression's
 // exponentiation: one serial chain per lane) and 4 (a doubling's four
 // independent squarings) per lane, and 3 interleaved products, at 2 waves
-// per SIMD like the decode and dsm kernels.  The _u results are checked
+// per SIMD like the decode and dsm kernels (latency exposed: the interleave
+// of the other wave is all that hides it) and at 8 (issue-bound).  The _u results are checked
 // against the centered ones on the device (canonical bytes) first.
 //
 //   hipcc --offload-arch=gfx950 -O3 -I firedancer_amd/csrc -o fe_carry_ubench tools/ubench/fe_carry_ubench.hip
@@ -87,19 +88,18 @@ int main() {
   hipDeviceProp_t prop;
   CHECK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
-  const int block = 256, grid = cus * 2 * 4;
-  const int lanes = grid * block;
+  const int block = 256, max_lanes = cus * 8 * block;
   int32_t *in, *out;
   int* bad;
-  CHECK(hipMalloc(&in, sizeof(int32_t) * lanes * 32));
-  CHECK(hipMalloc(&out, sizeof(int32_t) * lanes));
+  CHECK(hipMalloc(&in, sizeof(int32_t) * max_lanes * 32));
+  CHECK(hipMalloc(&out, sizeof(int32_t) * max_lanes));
   CHECK(hipMalloc(&bad, sizeof(int)));
-  int32_t* h = (int32_t*)malloc(sizeof(int32_t) * lanes * 32);
+  int32_t* h = (int32_t*)malloc(sizeof(int32_t) * max_lanes * 32);
   uint64_t x = 88172645463325252ull;
-  for (long i = 0; i < (long)lanes * 32; i++) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; h[i] = (int32_t)x; }
+  for (long i = 0; i < (long)max_lanes * 32; i++) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; h[i] = (int32_t)x; }
   /* a few lanes at the top of the range (limbs near 2^w - 1) */
   for (int t = 0; t < 64; t++) for (int i = 0; i < 32; i++) h[t * 32 + i] = -1;
-  CHECK(hipMemcpy(in, h, sizeof(int32_t) * lanes * 32, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(in, h, sizeof(int32_t) * max_lanes * 32, hipMemcpyHostToDevice));
   CHECK(hipMemset(bad, 0, sizeof(int)));
   hipLaunchKernelGGL(k_check, dim3(cus * 2), dim3(block), 0, 0, in, bad, 256);
   int hbad = -1;
@@ -108,12 +108,15 @@ int main() {
   if (hbad) return 1;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
-  const int iters = 200;
+  const int iters = 400;
   struct { const char* name; void (*f)(const int32_t*, int32_t*, int); double ops_per_iter; } ks[] = {
     {"fe_sq   x1 (centered)", k_sq<0, 1>, 1}, {"fe_sq_u x1 (unsigned)", k_sq<1, 1>, 1},
     {"fe_sq   x4 (centered)", k_sq<0, 4>, 4}, {"fe_sq_u x4 (unsigned)", k_sq<1, 4>, 4},
     {"fe_mul  x3 (centered)", k_mul<0>, 3},   {"fe_mul_u x3 (unsigned)", k_mul<1>, 3},
   };
+  for (int wps : {2, 8}) {   /* resident waves per SIMD: grid of wps blocks of 4 waves per CU */
+  const int grid = cus * wps, lanes = grid * block;
+  printf("-- %d waves per SIMD\n", wps);
   for (auto& k : ks) {
     hipLaunchKernelGGL(k.f, dim3(grid), dim3(block), 0, 0, in, out, iters);
     CHECK(hipDeviceSynchronize());
@@ -129,6 +132,7 @@ int main() {
     const double ops = (double)lanes * iters * k.ops_per_iter;
     printf("%-24s %8.3f ms  %7.2f G field ops/s  %6.1f SIMD-cycles per op per wave at 2.4 GHz\n", k.name, best,
            ops / (best * 1e-3) / 1e9, best * 1e-3 * 2.4e9 * cus * 4 / (ops / 64));
+  }
   }
   return 0;
 }
