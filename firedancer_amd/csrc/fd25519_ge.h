@@ -36,7 +36,7 @@ FD_DEV void ge_p3_0(ge_p3& h) {
    19-side operand must stay <= 3.3x, its other operand may be larger.
    Every completed point these formulas produce has X, Z, T within 3x and
    Y within [-1x, 4x], so the conversions below take X, Z (and T) as
-   19-sides and Y only as the other operand.
+   19-sides and Y (and T: ge_add<true>) only as the other operand.
 
    The conversions share each 19-side between two products, so its
    19-multiples (the wrapped terms) are computed once.  Swapping the
@@ -45,11 +45,12 @@ FD_DEV void ge_p3_0(ge_p3& h) {
 
 /* -> projective, unsigned (the doublings' input) */
 FD_DEV void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
-  fe t19;
-  fe_19(t19, p.T);
-  fe_mul19_u(r.X, p.X, p.T, t19);
-  fe_mul19_u(r.Z, p.Z, p.T, t19);
-  fe_mul_u(r.Y, p.Y, p.Z);
+  fe x19, z19;
+  fe_19(x19, p.X);
+  fe_19(z19, p.Z);
+  fe_mul19_u(r.X, p.T, p.X, x19);
+  fe_mul19_u(r.Y, p.Y, p.Z, z19);
+  fe_mul19_u(r.Z, p.T, p.Z, z19);
 }
 
 /* -> extended.  UXYT: X, Y, T unsigned (an addition's input: they only
@@ -106,13 +107,25 @@ FD_DEV void ge_p3_dbl(ge_p1p1& r, const ge_p3& p) {
   ge_p2_dbl(r, q);
 }
 
-/* p centered (|X|, |Y|, |Z| <= 1x): the entry's sums are 19-sides */
+/* |X|, |Y| <= 1x (centered) or in [0, 2x] (unsigned), |Z| <= 1x: the
+   entry's Y+X, Y-X and 2Z are 19-sides of the addition, so Y+X of two
+   unsigned coordinates ([0, 4x]) is moved by p (limbs ~2x each, value 0)
+   into [-2x, 2x] */
+#define FE_P_LIMBS {(1 << 26) - 19, (1 << 25) - 1, (1 << 26) - 1, (1 << 25) - 1, (1 << 26) - 1, \
+                    (1 << 25) - 1, (1 << 26) - 1, (1 << 25) - 1, (1 << 26) - 1, (1 << 25) - 1}
+template <bool UXY = false>
 FD_DEV void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
   const fe d2 = {FE_D2};
-  fe_add(r.YplusX, p.Y, p.X);
+  if (UXY) {
+    const fe pl = {FE_P_LIMBS};
+#pragma unroll
+    for (int i = 0; i < 10; i++) r.YplusX.v[i] = p.Y.v[i] + p.X.v[i] - pl.v[i];
+  } else {
+    fe_add(r.YplusX, p.Y, p.X);
+  }
   fe_sub(r.YminusX, p.Y, p.X);
   fe_add(r.Z2, p.Z, p.Z);
-  fe_mul(r.T2d, p.T, d2);
+  fe_mul_u(r.T2d, p.T, d2);
 }
 
 /* r = p + q (add-2008-hwcd-3, k = 2d, with 2 Z1 Z2 formed by the product
@@ -123,8 +136,8 @@ FD_DEV void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
      r.Z = 2Z1Z2 + c, r.T = 2Z1Z2 - c in [-1x, 3x];
    NT = true: the table holds -2dT, c' = -2dT1T2 unsigned too,
      r.Z = 2Z1Z2 - c' in [-2x, 2x], r.T = 2Z1Z2 + c' in [0, 4x] --
-   T then enters only the 19-free side of the next product (the
-   ge_p1p1_to_p3 forms; not ge_p1p1_to_p2, which takes T as a 19-side). */
+   T then enters only the 19-free side of the next product (every
+   conversion below takes X and Z as its 19-sides). */
 template <bool NT = false>
 FD_DEV void ge_add(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
   fe a, b, c, zz2;

@@ -51,7 +51,7 @@ extern "C" {
 #define FD_ED25519_SCALAR_WAVES_PER_SIMD 4
 #endif
 #ifndef FD_ED25519_DECODE_WAVES_PER_SIMD
-#define FD_ED25519_DECODE_WAVES_PER_SIMD 2
+#define FD_ED25519_DECODE_WAVES_PER_SIMD 4  /* 128 VGPR: spills 292 B/lane outside the squaring loops; 1.87 -> 1.85 ms (profiles/r2_ab_decode_waves.txt) */
 #endif
 #define FD_ED25519_SORT_BUCKETS 64
 

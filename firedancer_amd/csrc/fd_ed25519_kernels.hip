@@ -228,8 +228,8 @@ FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
 #pragma clang loop unroll(disable)
   for (int e = 2; e <= 8; e++) {
     ge_madd(sum, cur, pre);
-    ge_p1p1_to_p3(cur, sum);
-    ge_p3_to_cached(c, cur);
+    ge_p1p1_to_p3_uxyt(cur, sum);   /* Z centered: the next mixed addition doubles it */
+    ge_p3_to_cached<true>(c, cur);
     table_store<NT>(tab, e, c);
   }
 }
@@ -536,7 +536,7 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     load_pt(x, y, p, 0, j);
     table_build<true>(tabA, x, y, true);
     load_pt(x, y, p, 1, j);
-    table_build<false>(tabR, x, y, !(hf & FD_HF_DNEG));
+    table_build<true>(tabR, x, y, !(hf & FD_HF_DNEG));
   }
   /* digits, most significant first, top-aligned in 160 bits: c, |d| in
      radix 16 (W signed digits, the top one in [0,8]), s_lo, s_hi in
@@ -591,7 +591,7 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
       btab16_load(b2, g_btab2, (int)g);
     }
     ge_cached_cneg(cr, er < 0);
-    ge_add(Rt, P, cr);
+    ge_add<true>(Rt, P, cr);
     if (badd) {
       ge_p1p1_to_p3_uxyt(P, Rt);
       ge_madd(Rt, P, b1);
