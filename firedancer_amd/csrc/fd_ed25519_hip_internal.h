@@ -21,13 +21,17 @@ extern "C" {
    (y+x, y-x, 2dxy, pad), read from HBM / L2 / MALL with each entry loaded
    ahead of its use:
      btab16   [0..2^15]B, signed radix-2^16 digits of S (full-length form), 4.2 MB
-     btab20   [0..2^20)B, unsigned radix-2^20 digits of s_lo (half-size form), 128 MB
-     btab20b  [0..2^20)[2^132]B, digits of s_hi, 128 MB
-   The two 128 MB tables are shared by all engines of a device. */
+     btab_lo  [0..2^24)B, unsigned radix-2^24 digits of s_lo (half-size form), 2 GiB
+     btab_hi  [0..2^24)[2^144]B, digits of s_hi, 2 GiB
+   The two wide tables are shared by all engines of a device (4 GiB of the
+   288 GB: s' = s_lo + 2^144 s_hi costs 6 + 5 mixed additions, against
+   7 + 7 at radix 2^20 with 2 x 128 MB; the random 128-byte reads, 11 per
+   signature, are prefetched a window ahead). */
 #define FD_ED25519_BTAB16_ENTRIES ((1 << 15) + 1)
 #define FD_ED25519_BTAB16_STRIDE  32
-#define FD_ED25519_BTAB20_ENTRIES (1 << 20)
-#define FD_ED25519_BTAB20B_SHIFT  132
+#define FD_ED25519_BTABW_BITS     24
+#define FD_ED25519_BTABW_ENTRIES  (1 << FD_ED25519_BTABW_BITS)
+#define FD_ED25519_BTABW_SHIFT    144   /* s_lo: 6 digits (bits 0..143), s_hi: 5 digits (109 bits) */
 
 /* Per-lane tables [0..8](-A) and [0..8](-+R) in cached form, in HBM: 2 x 9
    entries x 40 int32 per lane, laid out [wave][lane][entry][quad] (int4
@@ -93,8 +97,8 @@ typedef struct {
   uint64_t         cap;
   int32_t const *  btab;     /* device base-point table (FD_ED25519_BTAB_INTS) */
   int32_t const *  btab16;   /* [0..2^15]B,          [FD_ED25519_BTAB16_ENTRIES][32] */
-  int32_t const *  btab20;   /* [0..2^20)B,          [FD_ED25519_BTAB20_ENTRIES][32] */
-  int32_t const *  btab20b;  /* [0..2^20)[2^132]B,   same layout                     */
+  int32_t const *  btab_lo;  /* [0..2^24)B,          [FD_ED25519_BTABW_ENTRIES][32] */
+  int32_t const *  btab_hi;  /* [0..2^24)[2^144]B,   same layout                     */
   void *           atab;     /* device scratch, waves * ATAB_BYTES_PER_WAVE    */
   int              codes_portable; /* 0: AVX-512 backend codes, 1: portable  */
   int              half_dbits;     /* longest |d| of the half-size form (fd25519_half.h) */
@@ -107,9 +111,9 @@ typedef struct {
    hipError_t value (0 on success). */
 int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
 int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, int base_doublings, void * stream );
-/* [0..2^20)[2^base_doublings]B into d_tab; d_scratch holds
-   FD_ED25519_BTAB20_ENTRIES*10 + 40 int32 */
-int fd_ed25519_hip_launch_gen_btab20( int32_t * d_tab, int base_doublings, int32_t * d_scratch, void * stream );
+/* [0..2^24)[2^base_doublings]B into d_tab; d_scratch holds
+   FD_ED25519_BTABW_ENTRIES*10 + 40 int32 */
+int fd_ed25519_hip_launch_gen_btabw( int32_t * d_tab, int base_doublings, int32_t * d_scratch, void * stream );
 /* Enqueues hash, decode and dsm for one chunk; `grid` caps the persistent
    dsm grid (its atab scratch must hold grid*VERIFY_BLOCK/64 waves). */
 int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t grid, void * stream );

@@ -343,7 +343,7 @@ FD_DEV int half_scalars_checked(const uint32_t (&k)[8], uint32_t (&c)[FD_HALF_TW
    lane per signature, before the points are decoded:
 
        c == d k (mod 8L), d odd, 0 <= c < 2^131, |d| < 2^half_dbits,
-       s' = d S mod L = s_lo + 2^132 s_hi
+       s' = d S mod L = s_lo + 2^144 s_hi
 
    written to hs[19][cap] (c, |d|, s_lo: 5 words each, s_hi: 4) with d's
    sign in hflag.  Signatures whose k has no such pair (~1e-6 of random k
@@ -399,15 +399,16 @@ FD_DEV void scalar_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
   }
   uint32_t* hs = p.hs + j;
   const uint64_t c = p.cap;
+  static_assert(FD_ED25519_BTABW_SHIFT == 144, "s_lo is words 0..3 and the low half of word 4");
 #pragma unroll
   for (int w = 0; w < 5; w++) {
     hs[(uint64_t)w * c] = cw[w];
     hs[(uint64_t)(5 + w) * c] = dm[w];
-    hs[(uint64_t)(10 + w) * c] = w < 4 ? sp[w] : (sp[4] & 0xfu);               /* bits 0..131   */
+    hs[(uint64_t)(10 + w) * c] = w < 4 ? sp[w] : (sp[4] & 0xffffu);            /* bits 0..143   */
   }
 #pragma unroll
-  for (int w = 0; w < 4; w++)
-    hs[(uint64_t)(15 + w) * c] = __builtin_amdgcn_alignbit(sp[w + 5], sp[w + 4], 4);  /* bits 132..   */
+  for (int w = 0; w < 4; w++)                                                  /* bits 144..252 */
+    hs[(uint64_t)(15 + w) * c] = __builtin_amdgcn_alignbit(w + 5 < 8 ? sp[w + 5] : 0u, sp[w + 4], 16);
   p.hflag[j] = (uint8_t)((dneg ? FD_HF_DNEG : 0u) | (ok ? 0u : FD_HF_FULL));
   if (!ok && !p.small) {   /* small chunks: the dsm scan finds them by hflag */
     const uint32_t slot = atomicAdd(p.fix_cnt, 1u);
@@ -505,12 +506,25 @@ FD_DEV void load_hs(uint32_t (&x)[5], const fd_ed25519_verify_params_t& p, int r
   for (int w = 0; w < 5; w++) x[w] = w < words ? p.hs[(uint64_t)(row + w) * p.cap + j] : 0u;
 }
 
+/* base digits: s_lo's 6 and s_hi's 5 radix-2^24 digits sit at bits 24m,
+   i.e. windows 6m (s_lo: 30, 24, .., 0; s_hi: 24, .., 0), top-aligned in
+   160 bits for pop160u */
+#define FD_BW_STEP   (FD_ED25519_BTABW_BITS / 4)
+#define FD_BW_LO_N   6
+#define FD_BW_HI_N   5
+#define FD_BW_LO_SHL (160 - FD_BW_LO_N * FD_ED25519_BTABW_BITS)
+#define FD_BW_HI_SHL (160 - FD_BW_HI_N * FD_ED25519_BTABW_BITS)
+#define FD_BW_LO_AT(it) ((it) <= FD_BW_STEP * (FD_BW_LO_N - 1) && (it) % FD_BW_STEP == 0)
+#define FD_BW_HI_AT(it) ((it) <= FD_BW_STEP * (FD_BW_HI_N - 1) && (it) % FD_BW_STEP == 0)
+static_assert(FD_BW_LO_N * FD_ED25519_BTABW_BITS == FD_ED25519_BTABW_SHIFT, "s_lo digits cover bits 0..SHIFT-1");
+static_assert(FD_BW_HI_N * FD_ED25519_BTABW_BITS >= 253 - FD_ED25519_BTABW_SHIFT, "s_hi digits cover s' >> SHIFT");
+
 /* ------------------------------------------------------------------------
    dsm: the group equation with half-size scalars.
 
    E = [S]B - R - [k]A == 0 is tested as [d]E == 0, i.e.
 
-       [c](-A) + [|d|](-sign(d) R) + [s_lo]B + [s_hi]B' == 0,   B' = [2^132]B
+       [c](-A) + [|d|](-sign(d) R) + [s_lo]B + [s_hi]B' == 0,   B' = [2^144]B
 
    exactly equivalent (fd25519_half.h: the group has order 8L and [d] is
    invertible on it).  A four-scalar Straus loop over W signed 4-bit
@@ -519,9 +533,9 @@ FD_DEV void load_hs(uint32_t (&x)[5], const fd_ed25519_verify_params_t& p, int r
    lanes' top digits being 0): 4(W-1) = 128 doublings (against 252 for the
    reference's double-scalar form), W additions from each lane's
    [0..8](-A) and [0..8](-+R) tables
-   (HBM, lane-contiguous 160-byte entries) and 7 + 7 mixed additions from
-   the two unsigned radix-2^20 base tables [0..2^20)B and [0..2^20)B'
-   (128 MB each, HBM/MALL).  Every table entry is loaded
+   (HBM, lane-contiguous 160-byte entries) and 6 + 5 mixed additions from
+   the two unsigned radix-2^24 base tables [0..2^24)B and [0..2^24)B'
+   (2 GiB each, HBM).  Every table entry is loaded
    one step ahead of its use: the -A entry before the window's doublings,
    the R entry before the -A addition, the base entries before the R
    addition.  The result is compared with the identity (X == 0, Y == Z). */
@@ -540,7 +554,7 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
   }
   /* digits, most significant first, top-aligned in 160 bits: c, |d| in
      radix 16 (W signed digits, the top one in [0,8]), s_lo, s_hi in
-     radix 2^20 (7 unsigned digits: no recoding, no negation) */
+     radix 2^24 (6 and 5 unsigned digits: no recoding, no negation) */
   uint32_t cd[5], dd[5], ld[5], hd[5];
   int W = 33;
   {
@@ -553,11 +567,11 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     const int sh = 160 - 4 * W;
     shl160v(t, x, sh); recode160<4>(dd, t);
     load_hs(x, p, 0, 5, j);  shl160v(t, x, sh); recode160<4>(cd, t);
-    load_hs(x, p, 10, 5, j); shl160<20>(ld, x);
-    load_hs(x, p, 15, 4, j); shl160<20>(hd, x);
+    load_hs(x, p, 10, 5, j); shl160<FD_BW_LO_SHL>(ld, x);
+    load_hs(x, p, 15, 4, j); shl160<FD_BW_HI_SHL>(hd, x);
   }
-  const int4* g_btab = reinterpret_cast<const int4*>(p.btab20);
-  const int4* g_btab2 = reinterpret_cast<const int4*>(p.btab20b);
+  const int4* g_btab = reinterpret_cast<const int4*>(p.btab_lo);
+  const int4* g_btab2 = reinterpret_cast<const int4*>(p.btab_hi);
 
   ge_p3 P;
   ge_p3_0(P);
@@ -568,8 +582,7 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     int ea = pop160<4>(cd), er = pop160<4>(dd);
     if (it == W - 1) { ea &= 15; er &= 15; }   /* top digits in [0,8] */
     ge_cached ca, cr;
-    const bool badd = it <= 30 && it % 5 == 0;   /* base digits at bits 20m: windows 30, 25, .., 0 */
-    uint32_t f = 0, g = 0;
+    const bool blo = FD_BW_LO_AT(it), bhi = FD_BW_HI_AT(it);
     ge_precomp b1, b2;
     atab_load(ca, tabA, ea < 0 ? -ea : ea);
     if (it != W - 1) {
@@ -584,17 +597,15 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     ge_cached_cneg(ca, ea < 0);
     ge_add<true>(Rt, P, ca);
     ge_p1p1_to_p3_u(P, Rt);
-    if (badd) {
-      f = pop160u<20>(ld);
-      g = pop160u<20>(hd);
-      btab16_load(b1, g_btab, (int)f);
-      btab16_load(b2, g_btab2, (int)g);
-    }
+    if (blo) btab16_load(b1, g_btab, (int)pop160u<FD_ED25519_BTABW_BITS>(ld));
+    if (bhi) btab16_load(b2, g_btab2, (int)pop160u<FD_ED25519_BTABW_BITS>(hd));
     ge_cached_cneg(cr, er < 0);
     ge_add<true>(Rt, P, cr);
-    if (badd) {
+    if (blo) {
       ge_p1p1_to_p3_uxyt(P, Rt);
       ge_madd(Rt, P, b1);
+    }
+    if (bhi) {
       ge_p1p1_to_p3_uxyt(P, Rt);
       ge_madd(Rt, P, b2);
     }
@@ -805,8 +816,8 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
     const int sh = 160 - 4 * W;
     shl160v(t, x, sh); recode160<4>(dd, t);
     load_hs(x, p, 0, 5, j);  shl160v(t, x, sh); recode160<4>(cd, t);
-    load_hs(x, p, 10, 5, j); shl160<20>(ld, x);
-    load_hs(x, p, 15, 4, j); shl160<20>(hd, x);
+    load_hs(x, p, 10, 5, j); shl160<FD_BW_LO_SHL>(ld, x);
+    load_hs(x, p, 15, 4, j); shl160<FD_BW_HI_SHL>(hd, x);
   }
   fe P, Rt;
 #pragma unroll
@@ -815,7 +826,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
   for (int it = W - 1; it >= 0; it--) {
     int ea = pop160<4>(cd), er = pop160<4>(dd);
     if (it == W - 1) { ea &= 15; er &= 15; }
-    const bool badd = it <= 30 && it % 5 == 0;
+    const bool blo = FD_BW_LO_AT(it), bhi = FD_BW_HI_AT(it);
     fe ca, cr, b1, b2;
     tab4_load(ca, tabA, ea < 0 ? -ea : ea);
     if (it != W - 1) {
@@ -830,17 +841,17 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
     ge4_add(Rt, P, ca, m);
     ge4_cneg(Rt, m.l0, ea < 0);
     ge4_to_p3(P, Rt);
-    if (badd) {
-      btab4_load(b1, p.btab20, (int)pop160u<20>(ld), m);
-      btab4_load(b2, p.btab20b, (int)pop160u<20>(hd), m);
-    }
+    if (blo) btab4_load(b1, p.btab_lo, (int)pop160u<FD_ED25519_BTABW_BITS>(ld), m);
+    if (bhi) btab4_load(b2, p.btab_hi, (int)pop160u<FD_ED25519_BTABW_BITS>(hd), m);
     ge4_cneg(P, m.l03, er < 0);
     ge4_add(Rt, P, cr, m);
     ge4_cneg(Rt, m.l0, er < 0);
     ge4_to_p3(P, Rt);
-    if (badd) {
+    if (blo) {
       ge4_add(Rt, P, b1, m);
       ge4_to_p3(P, Rt);
+    }
+    if (bhi) {
       ge4_add(Rt, P, b2, m);
       ge4_to_p3(P, Rt);
     }
@@ -861,7 +872,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
        quad 0: [c](-A) + [s_lo]B        quad 1: [|d|](-+R) + [s_hi]B',
 
    each quad building only its own [0..8] table and doing one table
-   addition (plus one base addition every 5th window) per 4 doublings;
+   addition (plus one base addition every 6th window) per 4 doublings;
    quad 1 then hands its point to quad 0 (DPP row shift) for one last
    addition and the identity test.  ~22% less latency than dsm4 for ~57%
    more lane work. */
@@ -890,11 +901,15 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
     for (int w = 34; w <= (FD_HALF_DBITS_MAX + 4) / 4; w++) W += __ballot(wl >= w) != 0ull;
     if (!half) load_hs(x, p, 0, 5, j);
     shl160v(t, x, 160 - 4 * W); recode160<4>(sd, t);
-    if (half) load_hs(x, p, 15, 4, j);
-    else load_hs(x, p, 10, 5, j);
-    shl160<20>(bd, x);
+    if (half) {
+      load_hs(x, p, 15, 4, j);
+      shl160<FD_BW_HI_SHL>(bd, x);
+    } else {
+      load_hs(x, p, 10, 5, j);
+      shl160<FD_BW_LO_SHL>(bd, x);
+    }
   }
-  const int32_t* btab = half ? p.btab20b : p.btab20;
+  const int32_t* btab = half ? p.btab_hi : p.btab_lo;
   fe P, Rt;
 #pragma unroll
   for (int i = 0; i < 10; i++) P.v[i] = (i == 0 && (m.l1 | m.l2)) ? 1 : 0;   /* identity (0, 1, 1, 0) */
@@ -902,7 +917,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
   for (int it = W - 1; it >= 0; it--) {
     int e = pop160<4>(sd);
     if (it == W - 1) e &= 15;
-    const bool badd = it <= 30 && it % 5 == 0;
+    const bool badd = half ? FD_BW_HI_AT(it) : FD_BW_LO_AT(it);
     fe ce, b;
     tab4_load(ce, tab, e < 0 ? -e : e);
     if (it != W - 1) {
@@ -912,7 +927,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
         ge4_to_p3(P, Rt);
       }
     }
-    if (badd) btab4_load(b, btab, (int)pop160u<20>(bd), m);
+    if (badd) btab4_load(b, btab, (int)pop160u<FD_ED25519_BTABW_BITS>(bd), m);
     ge4_cneg(P, m.l03, e < 0);
     ge4_add(Rt, P, ce, m);
     ge4_cneg(Rt, m.l0, e < 0);
@@ -983,7 +998,7 @@ __global__ void fd_ed25519_gen_btab_kernel(int32_t* btab, int entries, int strid
   for (int i = 30; i < stride; i++) o[i] = 0;
 }
 
-/* Wide unsigned-digit tables [0..2^20)[2^base_dbl]B.  The base is computed
+/* Wide unsigned-digit tables [0..2^24)[2^base_dbl]B.  The base is computed
    once (gen_base), then each thread produces a run of consecutive entries
    by additions and puts them in affine form with one inversion per run
    (Montgomery's trick: prefix products of Z in `scratch`). */
@@ -1023,7 +1038,7 @@ fd_ed25519_gen_btab_run_kernel(int32_t* tab, int entries, const int32_t* base, i
   ge_p3_to_cached(cb, B);
   ge_p3_0(P);
   ge_p1p1 r;
-  for (int bit = 20; bit >= 0; bit--) {   /* P = [e0] base */
+  for (int bit = FD_ED25519_BTABW_BITS - 1; bit >= 0; bit--) {   /* P = [e0] base */
     ge_p3_dbl(r, P);
     ge_p1p1_to_p3(P, r);
     if ((e0 >> bit) & 1) {
@@ -1128,8 +1143,8 @@ extern "C" int fd_ed25519_hip_launch_diag_half(const uint32_t* d_k, uint32_t* d_
   return (int)hipGetLastError();
 }
 
-extern "C" int fd_ed25519_hip_launch_gen_btab20(int32_t* d_tab, int base_dbl, int32_t* d_scratch, void* stream) {
-  const int entries = FD_ED25519_BTAB20_ENTRIES;
+extern "C" int fd_ed25519_hip_launch_gen_btabw(int32_t* d_tab, int base_dbl, int32_t* d_scratch, void* stream) {
+  const int entries = FD_ED25519_BTABW_ENTRIES;
   int32_t* base = d_scratch + (size_t)entries * 10;   /* 40 ints after the prefix products */
   hipLaunchKernelGGL(fd_ed25519_gen_base_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, base, base_dbl);
   const int threads = (entries + FD_BTAB_RUN - 1) / FD_BTAB_RUN;

@@ -11,7 +11,7 @@
    allocation on the device-resident path):
      btab   129 x 36 int32            base-point table [0..128]B (LDS image, signing)
      btab16 32769 x 32 int32          base-point table [0..2^15]B (full-length verify, 4.2 MB)
-     btab20 2 x 2^20 x 32 int32       [0..2^20)B, [0..2^20)[2^132]B (half-size verify, 2 x 128 MB,
+     btabw  2 x 2^24 x 32 int32       [0..2^24)B, [0..2^24)[2^144]B (half-size verify, 2 x 2 GiB,
                                       shared by the engines of a device)
      atab   dsm waves x 184320 B      per-lane [0..8](-A), [0..8](-+R) tables
      work   max_chunk x 280 B         k, flags, half-size scalars, decoded A and R, lists per signature
@@ -47,7 +47,7 @@ struct fd_ed25519_hip_engine {
 
   int32_t *    d_btab;
   int32_t *    d_btab16;     /* [0..2^15]B, the verify kernels' wide B table  */
-  int32_t *    btab20[2];    /* shared per device: [0..2^20)B, [0..2^20)[2^132]B */
+  int32_t *    btabw[2];    /* shared per device: [0..2^24)B, [0..2^24)[2^144]B */
   /* the per-chunk scratch of the chunk in flight */
   struct {
     void *     d_atab;       /* dsm lane tables (and the dsm4 quad tables)  */
@@ -123,62 +123,63 @@ fd_ed25519_hip_strerror( int status ) {
   return "unknown";
 }
 
-/* The half-size form's base tables, [0..2^20)B and [0..2^20)[2^132]B
-   (128 MB each), are shared by every engine of a device: generated by the
-   first engine, freed with the last. */
+/* The half-size form's base tables, [0..2^24)B and [0..2^24)[2^144]B
+   (2 GiB each), are shared by every engine of a device: generated by the
+   first engine (with a 640 MiB scratch freed right after), freed with the
+   last. */
 #define FD_ED25519_HIP_MAX_DEV 64
-static pthread_mutex_t btab20_lock = PTHREAD_MUTEX_INITIALIZER;
-static struct { int refs; int32_t * tab[2]; } btab20[ FD_ED25519_HIP_MAX_DEV ];
+static pthread_mutex_t btabw_lock = PTHREAD_MUTEX_INITIALIZER;
+static struct { int refs; int32_t * tab[2]; } btabw[ FD_ED25519_HIP_MAX_DEV ];
 
 static size_t
-btab20_bytes( void ) {
-  return sizeof(int32_t) * (size_t)FD_ED25519_BTAB20_ENTRIES * FD_ED25519_BTAB16_STRIDE;
+btabw_bytes( void ) {
+  return sizeof(int32_t) * (size_t)FD_ED25519_BTABW_ENTRIES * FD_ED25519_BTAB16_STRIDE;
 }
 
 static int
-btab20_acquire( int device, hipStream_t stream, int32_t * tab[2] ) {
+btabw_acquire( int device, hipStream_t stream, int32_t * tab[2] ) {
   if( device<0 || device>=FD_ED25519_HIP_MAX_DEV ) {
     snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "device %d out of range", device );
     return FD_ED25519_HIP_ERR_INVAL;
   }
-  pthread_mutex_lock( &btab20_lock );
+  pthread_mutex_lock( &btabw_lock );
   int rc = FD_ED25519_HIP_OK;
-  if( !btab20[device].refs ) {
+  if( !btabw[device].refs ) {
     int32_t * t[2] = { NULL, NULL };
     int32_t * scratch = NULL;
-    hipError_t he = hipMalloc( (void **)&t[0], btab20_bytes() );
-    if( he==hipSuccess ) he = hipMalloc( (void **)&t[1], btab20_bytes() );
-    if( he==hipSuccess ) he = hipMalloc( (void **)&scratch, sizeof(int32_t) * ((size_t)FD_ED25519_BTAB20_ENTRIES * 10 + 64) );
-    if( he==hipSuccess ) he = (hipError_t)fd_ed25519_hip_launch_gen_btab20( t[0], 0, scratch, stream );
-    if( he==hipSuccess ) he = (hipError_t)fd_ed25519_hip_launch_gen_btab20( t[1], FD_ED25519_BTAB20B_SHIFT, scratch, stream );
+    hipError_t he = hipMalloc( (void **)&t[0], btabw_bytes() );
+    if( he==hipSuccess ) he = hipMalloc( (void **)&t[1], btabw_bytes() );
+    if( he==hipSuccess ) he = hipMalloc( (void **)&scratch, sizeof(int32_t) * ((size_t)FD_ED25519_BTABW_ENTRIES * 10 + 64) );
+    if( he==hipSuccess ) he = (hipError_t)fd_ed25519_hip_launch_gen_btabw( t[0], 0, scratch, stream );
+    if( he==hipSuccess ) he = (hipError_t)fd_ed25519_hip_launch_gen_btabw( t[1], FD_ED25519_BTABW_SHIFT, scratch, stream );
     if( he==hipSuccess ) he = hipStreamSynchronize( stream );
     hipFree( scratch );
     if( he!=hipSuccess ) {
       hipFree( t[0] ); hipFree( t[1] );
-      rc = hip_fail( he, "base tables (btab20)" );
+      rc = hip_fail( he, "base tables (btabw)" );
     } else {
-      btab20[device].tab[0] = t[0];
-      btab20[device].tab[1] = t[1];
+      btabw[device].tab[0] = t[0];
+      btabw[device].tab[1] = t[1];
     }
   }
   if( rc==FD_ED25519_HIP_OK ) {
-    btab20[device].refs++;
-    tab[0] = btab20[device].tab[0];
-    tab[1] = btab20[device].tab[1];
+    btabw[device].refs++;
+    tab[0] = btabw[device].tab[0];
+    tab[1] = btabw[device].tab[1];
   }
-  pthread_mutex_unlock( &btab20_lock );
+  pthread_mutex_unlock( &btabw_lock );
   return rc;
 }
 
 static void
-btab20_release( int device ) {
-  pthread_mutex_lock( &btab20_lock );
-  if( btab20[device].refs>0 && !--btab20[device].refs ) {
-    hipFree( btab20[device].tab[0] );
-    hipFree( btab20[device].tab[1] );
-    btab20[device].tab[0] = btab20[device].tab[1] = NULL;
+btabw_release( int device ) {
+  pthread_mutex_lock( &btabw_lock );
+  if( btabw[device].refs>0 && !--btabw[device].refs ) {
+    hipFree( btabw[device].tab[0] );
+    hipFree( btabw[device].tab[1] );
+    btabw[device].tab[0] = btabw[device].tab[1] = NULL;
   }
-  pthread_mutex_unlock( &btab20_lock );
+  pthread_mutex_unlock( &btabw_lock );
 }
 
 static void
@@ -191,7 +192,7 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   if( e->side   ) hipStreamSynchronize( e->side );
   hipFree( e->d_btab ); hipFree( e->d_btab16 );
   hipFree( e->ws.d_atab ); hipFree( e->ws.d_work );
-  if( e->btab20[0] ) btab20_release( e->device );
+  if( e->btabw[0] ) btabw_release( e->device );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
   hipHostFree( e->h_msgs ); hipHostFree( e->h_off ); hipHostFree( e->h_sz ); hipHostFree( e->h_sigs );
@@ -280,11 +281,11 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   err = fd_ed25519_hip_launch_gen_btab16( e->d_btab16, 0, e->stream );
   if( err ) return hip_fail( (hipError_t)err, "gen_btab16 launch" );
   HIPCHK( hipStreamSynchronize( e->stream ), "gen_btab" );
-  int32_t * t20[2] = { NULL, NULL };
-  err = btab20_acquire( e->device, e->stream, t20 );
+  int32_t * tw[2] = { NULL, NULL };
+  err = btabw_acquire( e->device, e->stream, tw );
   if( err ) return err;
-  e->btab20[0] = t20[0];
-  e->btab20[1] = t20[1];
+  e->btabw[0] = tw[0];
+  e->btabw[1] = tw[1];
   return FD_ED25519_HIP_OK;
 }
 
@@ -370,7 +371,7 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz;
   p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
   p.cap = e->max_chunk;
-  p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab20 = e->btab20[0]; p.btab20b = e->btab20[1];
+  p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab_lo = e->btabw[0]; p.btab_hi = e->btabw[1];
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   p.half_dbits     = engine_half_dbits( e );
   uint64_t chunk = e->max_chunk;

@@ -305,7 +305,7 @@ def test_halfsize_fallback_scattered(fd, eng, eng_strict, halfsize, adversarial,
 
 
 def test_engines_share_base_tables(fd, adversarial):
-    """The 2 x 128 MB base tables are shared by the engines of a device and
+    """The 2 x 2 GiB base tables are shared by the engines of a device and
     freed with the last one: engines created and destroyed in overlapping
     order all verify correctly, including after a full release."""
     want = adversarial["codes_avx512"]
