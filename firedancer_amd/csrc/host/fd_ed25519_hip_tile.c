@@ -515,7 +515,9 @@ fd_ed25519_hip_vtile_new( int device, unsigned slot_cnt, unsigned long batch_sig
                           unsigned long tcache_map_cnt, int flags ) {
   fd_ed25519_hip_vtile_t * vt = (fd_ed25519_hip_vtile_t *)calloc( 1, sizeof(*vt) );
   if( !vt ) return NULL;
-  vt->batch_sigs = batch_sigs ? batch_sigs : 4096UL;
+  /* a transaction stages up to 16 signatures into one batch: a smaller
+     batch could not hold it (its signatures would run past the slot) */
+  vt->batch_sigs = !batch_sigs ? 4096UL : batch_sigs<16UL ? 16UL : batch_sigs;
   vt->gpu_parse  = !!(flags & FD_ED25519_HIP_VTILE_GPU_PARSE);
   vt->pipe = fd_ed25519_hip_pipe_new( device, slot_cnt, vt->batch_sigs, vt->batch_sigs*FD_ED25519_HIP_TXN_MTU,
                                       vt->batch_sigs, flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE );

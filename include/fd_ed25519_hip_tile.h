@@ -202,7 +202,8 @@ fd_ed25519_hip_tcache_insert( fd_ed25519_hip_tcache_t * tc, unsigned long tag );
 typedef struct fd_ed25519_hip_vtile fd_ed25519_hip_vtile_t;
 
 /* A verify tile's batched core on `device`: batches of up to batch_sigs
-   signatures, slot_cnt in flight, tcache of tcache_depth / tcache_map_cnt
+   signatures (at least 16, the most a transaction stages: smaller values
+   are raised to 16; 0 = 4096), slot_cnt in flight, tcache of tcache_depth / tcache_map_cnt
    (the reference: 16 / 64, fd_verify.h:6-7).  flags: the engine flags
    (FD_ED25519_HIP_FLAG_CODES_PORTABLE) and FD_ED25519_HIP_VTILE_GPU_PARSE:
    payloads go to the device as they are and fd_txn_parse runs there

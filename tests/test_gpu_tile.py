@@ -33,7 +33,7 @@ def frags(oracle):
 
 
 @pytest.mark.parametrize("gpu_parse", [False, True])
-@pytest.mark.parametrize("batch_sigs,slot_cnt", [(64, 3), (1000, 2), (16, 1), (4096, 4)])
+@pytest.mark.parametrize("batch_sigs,slot_cnt", [(64, 3), (1000, 2), (16, 1), (4096, 4), (1, 2)])  # 1: raised to 16
 def test_vtile_matches_reference_tile(tile, ref, frags, batch_sigs, slot_cnt, gpu_parse):
     """Verdicts, dedup tags and the published frags (payload, pad, fd_txn_t,
     payload_sz: after_frag, src/app/fdctl/run/tiles/fd_verify.c:102-133)
