@@ -231,12 +231,37 @@ fd_ed25519_hip_pipe_acquire( fd_ed25519_hip_pipe_t * pipe ) {
   return &s->pub;
 }
 
+/* The kernels read what the staged offsets point at, with no bounds of
+   their own: a message range past the staged bytes, or a transaction's
+   signature range past the staged signatures, would be an out-of-bounds
+   device read.  Checked on the host before anything is copied (a few ns
+   per signature). */
+static int
+slot_check( fd_ed25519_hip_slot_t const * slot, unsigned long sig_cnt, unsigned long msg_bytes,
+            unsigned long txn_cnt ) {
+  for( unsigned long i=0UL; i<sig_cnt; i++ ) {
+    if( slot->msg_off[ i ]>msg_bytes || slot->msg_sz[ i ]>msg_bytes - slot->msg_off[ i ] ) {
+      fd_ed25519_hip_private_set_error( "pipe_submit: a signature's message lies outside the staged bytes" );
+      return FD_ED25519_HIP_ERR_INVAL;
+    }
+  }
+  for( unsigned long t=0UL; t<txn_cnt; t++ ) {
+    unsigned long c = slot->txn_sig_cnt[ t ];
+    if( c>=1UL && c<=16UL && ( slot->txn_first[ t ]>sig_cnt || c>sig_cnt - slot->txn_first[ t ] ) ) {
+      fd_ed25519_hip_private_set_error( "pipe_submit: a transaction's signatures lie outside the staged ones" );
+      return FD_ED25519_HIP_ERR_INVAL;
+    }
+  }
+  return FD_ED25519_HIP_OK;
+}
+
 int
 fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot,
                             unsigned long sig_cnt, unsigned long msg_bytes, unsigned long txn_cnt ) {
   pipe_slot_t * s = (pipe_slot_t *)slot;
   if( s->state!=SLOT_FILL || sig_cnt>slot->sig_cap || msg_bytes>slot->msg_cap || txn_cnt>slot->txn_cap )
     return FD_ED25519_HIP_ERR_INVAL;
+  if( slot_check( slot, sig_cnt, msg_bytes, txn_cnt ) ) return FD_ED25519_HIP_ERR_INVAL;
   TCHK( hipSetDevice( pipe->device ), "hipSetDevice" );
   hipStream_t st = (hipStream_t)fd_ed25519_hip_engine_stream( s->eng );
   slot->sig_cnt = sig_cnt; slot->msg_bytes = msg_bytes; slot->txn_cnt = txn_cnt;
@@ -270,6 +295,10 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
      fd_txn_parse accepts it; 0 or > 16 reserve none) */
   unsigned long slots = 0UL;
   for( unsigned long t=0UL; t<txn_cnt; t++ ) {
+    if( slot->msg_off[ t ]>payload_bytes || slot->msg_sz[ t ]>payload_bytes - slot->msg_off[ t ] ) {
+      fd_ed25519_hip_private_set_error( "pipe_submit_txns: a payload lies outside the staged bytes" );
+      return FD_ED25519_HIP_ERR_INVAL;
+    }
     unsigned int c = slot->msg_sz[ t ] ? slot->msgs[ slot->msg_off[ t ] ] : 0U;
     slot->txn_first  [ t ] = (unsigned int)slots;
     slot->txn_sig_cnt[ t ] = c;

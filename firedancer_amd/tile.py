@@ -55,10 +55,6 @@ _lib.fd_ed25519_hip_txn_parse_full.argtypes = [ctypes.c_char_p, ctypes.c_ulong, 
 _lib.fd_ed25519_hip_txn_parse_full.restype = ctypes.c_ulong
 _lib.fd_ed25519_hip_txn_frag.argtypes = [ctypes.c_char_p, ctypes.c_ulong, _v]
 _lib.fd_ed25519_hip_txn_frag.restype = ctypes.c_ulong
-_lib.fd_ed25519_hip_txn_parse_full.argtypes = [ctypes.c_char_p, ctypes.c_ulong, _v]
-_lib.fd_ed25519_hip_txn_parse_full.restype = ctypes.c_ulong
-_lib.fd_ed25519_hip_txn_frag.argtypes = [ctypes.c_char_p, ctypes.c_ulong, _v]
-_lib.fd_ed25519_hip_txn_frag.restype = ctypes.c_ulong
 _lib.fd_ed25519_hip_tcache_new.argtypes = [ctypes.c_ulong, ctypes.c_ulong]
 _lib.fd_ed25519_hip_tcache_new.restype = _v
 _lib.fd_ed25519_hip_tcache_delete.argtypes = [_v]
@@ -85,6 +81,87 @@ _lib.fd_ed25519_hip_latency_run_tiles.argtypes = [ctypes.c_int, ctypes.c_uint, c
                                                   _v, ctypes.POINTER(LatencyResult)]
 _lib.fd_ed25519_hip_pool_verify.argtypes = [_v, ctypes.c_uint, ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, _v, _v,
                                             _v, _v, _v, _v, ctypes.POINTER(ctypes.c_double)]
+
+
+class Slot(ctypes.Structure):
+    """fd_ed25519_hip_slot_t: one batch of a pipe (pinned host arrays)."""
+    _fields_ = [("msgs", ctypes.POINTER(ctypes.c_ubyte)), ("msg_off", ctypes.POINTER(ctypes.c_ulong)),
+                ("msg_sz", ctypes.POINTER(ctypes.c_uint)), ("sigs", ctypes.POINTER(ctypes.c_ubyte)),
+                ("pubs", ctypes.POINTER(ctypes.c_ubyte)), ("txn_first", ctypes.POINTER(ctypes.c_uint)),
+                ("txn_sig_cnt", ctypes.POINTER(ctypes.c_uint)), ("sig_out", ctypes.POINTER(ctypes.c_byte)),
+                ("txn_out", ctypes.POINTER(ctypes.c_byte)), ("txn_trailer", ctypes.POINTER(ctypes.c_ubyte)),
+                ("sig_cap", ctypes.c_ulong), ("msg_cap", ctypes.c_ulong), ("txn_cap", ctypes.c_ulong),
+                ("sig_cnt", ctypes.c_ulong), ("msg_bytes", ctypes.c_ulong), ("txn_cnt", ctypes.c_ulong),
+                ("seq", ctypes.c_ulong), ("t_submit", ctypes.c_double), ("t_done", ctypes.c_double),
+                ("user", ctypes.c_ulong)]
+
+
+_lib.fd_ed25519_hip_pipe_new.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong,
+                                         ctypes.c_int]
+_lib.fd_ed25519_hip_pipe_new.restype = _v
+_lib.fd_ed25519_hip_pipe_delete.argtypes = [_v]
+_lib.fd_ed25519_hip_pipe_acquire.argtypes = [_v]
+_lib.fd_ed25519_hip_pipe_acquire.restype = ctypes.POINTER(Slot)
+_lib.fd_ed25519_hip_pipe_submit.argtypes = [_v, ctypes.POINTER(Slot), ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong]
+_lib.fd_ed25519_hip_pipe_submit_txns.argtypes = [_v, ctypes.POINTER(Slot), ctypes.c_ulong, ctypes.c_ulong]
+_lib.fd_ed25519_hip_pipe_poll.argtypes = [_v, ctypes.c_int]
+_lib.fd_ed25519_hip_pipe_poll.restype = ctypes.POINTER(Slot)
+_lib.fd_ed25519_hip_pipe_release.argtypes = [_v, ctypes.POINTER(Slot)]
+
+
+class Pipe:
+    """fd_ed25519_hip_pipe_*: slot_cnt batches in flight on one device, the
+    caller staging each batch in place in its slot's pinned arrays."""
+
+    def __init__(self, device=0, slot_cnt=2, sig_cap=4096, msg_cap=None, txn_cap=None, flags=0):
+        msg_cap = sig_cap * TXN_MTU if msg_cap is None else msg_cap
+        txn_cap = sig_cap if txn_cap is None else txn_cap
+        self._p = _lib.fd_ed25519_hip_pipe_new(device, slot_cnt, sig_cap, msg_cap, txn_cap, flags)
+        if not self._p:
+            raise HipError("pipe_new failed")
+
+    def acquire(self):
+        s = _lib.fd_ed25519_hip_pipe_acquire(self._p)
+        return s if s else None
+
+    @staticmethod
+    def arrays(slot):
+        """numpy views of a slot's staging and output arrays"""
+        c = slot.contents
+        return {"msgs": np.ctypeslib.as_array(c.msgs, (c.msg_cap,)),
+                "msg_off": np.ctypeslib.as_array(c.msg_off, (max(c.sig_cap, c.txn_cap),)),
+                "msg_sz": np.ctypeslib.as_array(c.msg_sz, (max(c.sig_cap, c.txn_cap),)),
+                "sigs": np.ctypeslib.as_array(c.sigs, (c.sig_cap * 64,)),
+                "pubs": np.ctypeslib.as_array(c.pubs, (c.sig_cap * 32,)),
+                "txn_first": np.ctypeslib.as_array(c.txn_first, (max(c.txn_cap, 1),)),
+                "txn_sig_cnt": np.ctypeslib.as_array(c.txn_sig_cnt, (max(c.txn_cap, 1),)),
+                "sig_out": np.ctypeslib.as_array(c.sig_out, (c.sig_cap,)),
+                "txn_out": np.ctypeslib.as_array(c.txn_out, (max(c.txn_cap, 1),))}
+
+    def submit(self, slot, sig_cnt, msg_bytes, txn_cnt=0):
+        """the library's status code (0, or FD_ED25519_HIP_ERR_* with nothing enqueued)"""
+        return _lib.fd_ed25519_hip_pipe_submit(self._p, slot, sig_cnt, msg_bytes, txn_cnt)
+
+    def submit_txns(self, slot, txn_cnt, payload_bytes):
+        return _lib.fd_ed25519_hip_pipe_submit_txns(self._p, slot, txn_cnt, payload_bytes)
+
+    def poll(self, wait=True):
+        s = _lib.fd_ed25519_hip_pipe_poll(self._p, 1 if wait else 0)
+        return s if s else None
+
+    def release(self, slot):
+        _lib.fd_ed25519_hip_pipe_release(self._p, slot)
+
+    def close(self):
+        if self._p:
+            _lib.fd_ed25519_hip_pipe_delete(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class PoolStats(ctypes.Structure):

@@ -90,7 +90,12 @@ fd_ed25519_hip_slot_t *
 fd_ed25519_hip_pipe_acquire( fd_ed25519_hip_pipe_t * pipe );
 
 /* Enqueues H2D, verification (and the per-transaction combine if
-   txn_cnt>0) and D2H of an acquired slot; returns immediately. */
+   txn_cnt>0) and D2H of an acquired slot; returns immediately.
+   FD_ED25519_HIP_ERR_INVAL, with nothing enqueued, if a count exceeds its
+   capacity, a signature's message range [msg_off, msg_off+msg_sz) is not
+   within the msg_bytes staged, or a transaction's signature range
+   [txn_first, txn_first+txn_sig_cnt) (counts 1..16) is not within the
+   sig_cnt staged (the kernels would read out of bounds). */
 int
 fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot,
                             unsigned long sig_cnt, unsigned long msg_bytes, unsigned long txn_cnt );
@@ -103,7 +108,9 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
    code, or FD_ED25519_HIP_TXN_CODE_PARSE_FAILED.  txn_first / txn_sig_cnt
    are filled by the pipe (from payload byte 0, the signature count).  The
    signature slots (counts of 1..16) must fit sig_cap, payloads msg_cap
-   (the buffer is readable 64 bytes past the end, as the kernels need). */
+   (the buffer is readable 64 bytes past the end, as the kernels need);
+   a payload range outside the payload_bytes staged is
+   FD_ED25519_HIP_ERR_INVAL, nothing enqueued. */
 #define FD_ED25519_HIP_TXN_CODE_PARSE_FAILED (-4)
 
 int

@@ -247,3 +247,72 @@ def test_sandboxed_tile_with_gpu_service(tile, ref, frags, tmp_path, gpu_parse):
     # the frags the sandboxed tile receives for its SUCCESS transactions are
     # the reference tile's published frags
     assert tile.parse_producer_frags(out[len(frags):]) == [f for f in want_frags if f is not None]
+
+
+def test_pipe_stages_in_place_and_rejects_out_of_range(tile, adversarial):
+    """The raw pipe API (fd_ed25519_hip_pipe_*): a batch staged in a slot's
+    pinned arrays verifies to the reference's codes, several batches in
+    flight; a message or transaction range outside what was staged is
+    refused on the host (ERR_INVAL, nothing enqueued) -- the kernels would
+    read out of bounds -- and the pipe keeps working after it."""
+    d = adversarial
+    want = d["codes_avx512"]
+    n = len(want)
+    cap = 512
+    p = tile.Pipe(0, slot_cnt=2, sig_cap=cap, msg_cap=cap * 1300, txn_cap=cap)
+
+    def stage(slot, i0, i1):
+        a = tile.Pipe.arrays(slot)
+        pos = 0
+        for k, i in enumerate(range(i0, i1)):
+            o, z = int(d["msg_off"][i]), int(d["msg_sz"][i])
+            a["msgs"][pos:pos + z] = d["msgs"][o:o + z]
+            a["msg_off"][k], a["msg_sz"][k] = pos, z
+            a["sigs"][64 * k:64 * k + 64] = d["sigs"][i]
+            a["pubs"][32 * k:32 * k + 32] = d["pubs"][i]
+            pos += z
+        return a, pos
+
+    got = np.zeros(n, np.int8)
+    spans, inflight = [(i, min(i + cap, n)) for i in range(0, n, cap)], []
+    for i0, i1 in spans:
+        s = p.acquire()
+        while s is None:
+            done = p.poll(True)
+            j0, j1 = done.contents.user, done.contents.user + done.contents.sig_cnt
+            got[j0:j1] = tile.Pipe.arrays(done)["sig_out"][:j1 - j0]
+            p.release(done)
+            s = p.acquire()
+        a, pos = stage(s, i0, i1)
+        s.contents.user = i0
+        assert p.submit(s, i1 - i0, pos) == 0
+    while True:
+        done = p.poll(True)
+        if done is None:
+            break
+        j0, j1 = done.contents.user, done.contents.user + done.contents.sig_cnt
+        got[j0:j1] = tile.Pipe.arrays(done)["sig_out"][:j1 - j0]
+        p.release(done)
+    assert np.array_equal(got, want)
+
+    # out-of-range stagings are refused before any device work
+    s = p.acquire()
+    a, pos = stage(s, 0, 8)
+    a["msg_off"][3] = pos                      # message starts at the end, size > 0
+    assert p.submit(s, 8, pos) != 0
+    a["msg_off"][3], a["msg_sz"][3] = 0, pos + 1   # runs one byte past the staged bytes
+    assert p.submit(s, 8, pos) != 0
+    a, pos = stage(s, 0, 8)
+    a["txn_first"][0], a["txn_sig_cnt"][0] = 6, 3  # signatures 6..8 of 8 staged
+    assert p.submit(s, 8, pos, txn_cnt=1) != 0
+    a["txn_first"][0], a["txn_sig_cnt"][0] = 5, 3
+    assert p.submit(s, 8, pos, txn_cnt=1) == 0
+    done = p.poll(True)
+    assert np.array_equal(tile.Pipe.arrays(done)["sig_out"][:8], want[:8])
+    p.release(done)
+    s = p.acquire()
+    a = tile.Pipe.arrays(s)
+    a["msgs"][:64] = 1
+    a["msg_off"][0], a["msg_sz"][0] = 10, 100      # raw mode: payload past the 64 bytes staged
+    assert p.submit_txns(s, 1, 64) != 0
+    p.close()
