@@ -44,9 +44,18 @@ __constant__ uint64_t fd_sha512_dev_k[80] = {
    shifts), xor3 / maj / ch one v_bitop3_b32 each (gfx950's 3-input LUT op,
    truth-table index = a<<2 | b<<1 | c).  Left to itself LLVM builds the
    rotations from 64-bit shifts and ors. */
+#ifndef FD_SHA_OPAQUE_PAIR
+#define FD_SHA_OPAQUE_PAIR 1
+#endif
 FD_DEV uint32_t sha_lo(uint64_t x) { return (uint32_t)x; }
 FD_DEV uint32_t sha_hi(uint64_t x) { return (uint32_t)(x >> 32); }
-FD_DEV uint64_t sha_pair(uint32_t hi, uint32_t lo) { return ((uint64_t)hi << 32) | lo; }
+FD_DEV uint64_t sha_pair(uint32_t hi, uint32_t lo) {
+  uint64_t x = ((uint64_t)hi << 32) | lo;
+#if FD_SHA_OPAQUE_PAIR
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
 
 FD_DEV uint64_t sha_ror(uint64_t x, int n) {
   const uint32_t lo = sha_lo(x), hi = sha_hi(x);

@@ -38,7 +38,7 @@ def main():
     if show_blocks:
         for b, c in blocks:
             n = sum(c.values())
-            if n > 200:
+            if n > int(__import__("os").environ.get("ISA_MIN", "200")):
                 vv = sum(v for k, v in c.items() if k.startswith("v_"))
                 print(f"{b[:70]:70s} {n:6d} instr, {vv} valu; top: " +
                       ", ".join(f"{k}:{v}" for k, v in c.most_common(8)))
