@@ -82,26 +82,38 @@ FD_DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 /* One compression: h <- h + F(h, w).  The schedule is kept as a rolling
    16-word window; rounds are unrolled 16 at a time with the round constants
    read through the scalar cache. */
-FD_DEV void sha512_block(uint64_t (&h)[8], uint64_t (&w)[16]) {
-  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-  for (int r0 = 0; r0 < 80; r0 += 16) {
+template <bool SCHED>
+FD_DEV void sha512_rounds16(uint64_t (&v)[8], uint64_t (&w)[16], int r0) {
+  uint64_t a = v[0], b = v[1], c = v[2], d = v[3], e = v[4], f = v[5], g = v[6], hh = v[7];
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-      if (r0 > 0) {
-        const uint64_t w15 = w[(r + 1) & 15], w2 = w[(r + 14) & 15];
-        const uint64_t s0 = sha_bitop3<SHA_XOR3>(sha_ror(w15, 1), sha_ror(w15, 8), sha_shr(w15, 7));
-        const uint64_t s1 = sha_bitop3<SHA_XOR3>(sha_ror(w2, 19), sha_ror(w2, 61), sha_shr(w2, 6));
-        w[r] += s0 + w[(r + 9) & 15] + s1;
-      }
-      const uint64_t S1 = sha_bitop3<SHA_XOR3>(sha_ror(e, 14), sha_ror(e, 18), sha_ror(e, 41));
-      const uint64_t ch = sha_bitop3<SHA_CH>(e, f, g);
-      const uint64_t t1 = hh + S1 + ch + fd_sha512_dev_k[r0 + r] + w[r];
-      const uint64_t S0 = sha_bitop3<SHA_XOR3>(sha_ror(a, 28), sha_ror(a, 34), sha_ror(a, 39));
-      const uint64_t mj = sha_bitop3<SHA_MAJ>(a, b, c);
-      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+  for (int r = 0; r < 16; r++) {
+    if (SCHED) {
+      const uint64_t w15 = w[(r + 1) & 15], w2 = w[(r + 14) & 15];
+      const uint64_t s0 = sha_bitop3<SHA_XOR3>(sha_ror(w15, 1), sha_ror(w15, 8), sha_shr(w15, 7));
+      const uint64_t s1 = sha_bitop3<SHA_XOR3>(sha_ror(w2, 19), sha_ror(w2, 61), sha_shr(w2, 6));
+      w[r] += s0 + w[(r + 9) & 15] + s1;
     }
+    const uint64_t S1 = sha_bitop3<SHA_XOR3>(sha_ror(e, 14), sha_ror(e, 18), sha_ror(e, 41));
+    const uint64_t ch = sha_bitop3<SHA_CH>(e, f, g);
+    const uint64_t t1 = hh + S1 + ch + fd_sha512_dev_k[r0 + r] + w[r];
+    const uint64_t S0 = sha_bitop3<SHA_XOR3>(sha_ror(a, 28), sha_ror(a, 34), sha_ror(a, 39));
+    const uint64_t mj = sha_bitop3<SHA_MAJ>(a, b, c);
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }
-  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  v[0] = a; v[1] = b; v[2] = c; v[3] = d; v[4] = e; v[5] = f; v[6] = g; v[7] = hh;
+}
+
+/* rounds 0..15 on the block's words, then 4 x 16 with the schedule (a
+   loop with no per-round test) */
+FD_DEV void sha512_block(uint64_t (&h)[8], uint64_t (&w)[16]) {
+  uint64_t v[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = h[i];
+  sha512_rounds16<false>(v, w, 0);
+#pragma clang loop unroll(disable)
+  for (int r0 = 16; r0 < 80; r0 += 16) sha512_rounds16<true>(v, w, r0);
+#pragma unroll
+  for (int i = 0; i < 8; i++) h[i] += v[i];
 }
 
 /* A lane's message: base is the aligned dword holding message byte 0,
