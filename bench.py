@@ -237,41 +237,78 @@ def host_fed(wl, device, info, world, reps, batch, slots, copies):
     (never as it), with the PCIe bound it is up against: the H2D rate of a
     plain pinned copy over the bytes a signature moves."""
     from firedancer_amd import tile
+    import contextlib
     n = wl.n
     mb = wl.msg_bytes
-    msgs1 = wl.msgs.download(np.uint8, mb)
-    off1 = wl.off.download(np.uint64, n)
-    sigs1 = wl.sigs.download(np.uint8, 64 * n)
-    pubs1 = wl.pubs.download(np.uint8, 32 * n)
-    expect1 = wl.expect.download(np.int8, n)
-    # the stream's host buffers are first touched on the GPU's NUMA node
+    # Every rank reaches every collective below whatever happens to its own
+    # leg (a rank that raised before a barrier would hang the others): each
+    # stage runs under a guard and the ranks agree on the outcome first.
+    err = [None]
+
+    def guarded(fn):
+        if err[0] is None:
+            try:
+                return fn()
+            except Exception as ex:  # reported below, on every rank
+                err[0] = ex
+        return None
+
+    def agree(what):
+        if allreduce_sum(0 if err[0] is None else 1, world) != 0:
+            raise RuntimeError(f"host-fed leg failed on a rank ({what}): {err[0]!r}")
+
     near = tile.NearDevice(info)
-    with near:
-        msgs = np.concatenate([msgs1] * copies + [np.zeros(16, np.uint8)])
-        off = np.concatenate([off1 + np.uint64(c * mb) for c in range(copies)])
-        sz = np.tile(wl.sizes.astype(np.uint32), copies)
-        sigs, pubs = np.tile(sigs1, copies), np.tile(pubs1, copies)
-        out = np.ones(copies * n, np.int8)
-    pool = tile.Pool([device], batch, slots, tile.max_span(off, sz, batch))
-    t = time.perf_counter()
-    with tile.HostRegistration(msgs, off, sz, sigs, pubs, out):
-        reg_s = time.perf_counter() - t
-        pool.run(msgs, off, sz, sigs, pubs, out)  # warm-up: a whole stream (clocks, DMA engines, page tables)
+    res = {}
+    with contextlib.ExitStack() as stack:
+        def prepare():
+            msgs1 = wl.msgs.download(np.uint8, mb)
+            off1 = wl.off.download(np.uint64, n)
+            sigs1 = wl.sigs.download(np.uint8, 64 * n)
+            pubs1 = wl.pubs.download(np.uint8, 32 * n)
+            res["expect1"] = wl.expect.download(np.int8, n)
+            # the stream's host buffers are first touched on the GPU's NUMA node
+            with near:
+                res["msgs"] = np.concatenate([msgs1] * copies + [np.zeros(16, np.uint8)])
+                res["off"] = np.concatenate([off1 + np.uint64(c * mb) for c in range(copies)])
+                res["sz"] = np.tile(wl.sizes.astype(np.uint32), copies)
+                res["sigs"], res["pubs"] = np.tile(sigs1, copies), np.tile(pubs1, copies)
+                res["out"] = np.ones(copies * n, np.int8)
+            pool = tile.Pool([device], batch, slots, tile.max_span(res["off"], res["sz"], batch))
+            stack.callback(pool.close)
+            res["pool"] = pool
+            t = time.perf_counter()
+            stack.enter_context(tile.HostRegistration(res["msgs"], res["off"], res["sz"], res["sigs"], res["pubs"],
+                                                      res["out"]))
+            res["reg_s"] = time.perf_counter() - t
+            # warm-up: a whole stream (clocks, DMA engines, page tables)
+            pool.run(res["msgs"], res["off"], res["sz"], res["sigs"], res["pubs"], res["out"])
+
+        guarded(prepare)
+        agree("setup")
         barrier(world)
         t0 = time.perf_counter()
-        st = None
-        runs = []
-        for _ in range(reps):
-            _, sec, st = pool.run(msgs, off, sz, sigs, pubs, out)
-            runs.append(sec)
+
+        def stream():
+            runs, st = [], None
+            for _ in range(reps):
+                _, sec, st = res["pool"].run(res["msgs"], res["off"], res["sz"], res["sigs"], res["pubs"], res["out"])
+                runs.append(sec)
+            res["runs"], res["st"] = runs, st
+        guarded(stream)
         dt = time.perf_counter() - t0
         barrier(world)
-        ok = bool(np.array_equal(out, np.tile(expect1, copies)))
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            pool.run(msgs[:mb + 16], off[:n], sz[:n], sigs[:64 * n], pubs[:32 * n], out[:n])
-        dt1 = time.perf_counter() - t1
-    pool.close()
+        agree("stream")
+        ok = bool(np.array_equal(res["out"], np.tile(res["expect1"], copies)))
+
+        def single():
+            t1 = time.perf_counter()
+            for _ in range(reps):
+                res["pool"].run(res["msgs"][:mb + 16], res["off"][:n], res["sz"][:n], res["sigs"][:64 * n],
+                                res["pubs"][:32 * n], res["out"][:n])
+            res["dt1"] = time.perf_counter() - t1
+        guarded(single)
+    agree("single pass")
+    st, runs, dt1, reg_s = res["st"], res["runs"], res["dt1"], res["reg_s"]
     dt_max = allreduce_max(dt, world)
     ok_all = allreduce_sum(0 if ok else 1, world) == 0
     h2d = tile.h2d_gbps(device, 256 << 20, 8)
@@ -392,8 +429,11 @@ def main():
 
     hf_first = None
     if args.host_first and args.host_reps > 0:   # A/B: the host-fed leg before the engine's timed passes
-        hf_first = host_fed(wl, device, info, world, args.host_reps, args.host_batch, args.host_slots,
-                            args.host_copies)
+        try:
+            hf_first = host_fed(wl, device, info, world, args.host_reps, args.host_batch, args.host_slots,
+                                args.host_copies)
+        except Exception as ex:  # the same on every rank (host_fed agrees first); never fatal
+            log(f"[rank {rank}] host-fed leg failed: {ex!r}")
     for _ in range(args.warmup):
         wl.verify()
     eng.sync()
@@ -460,7 +500,11 @@ def main():
             log(f"[rank {rank}] host-fed leg failed: {ex!r}")
     lat = None
     if rank == 0 and world == 1 and args.latency_txns > 0:
-        lat = latency_mode(eng, args, device)
+        try:
+            lat = latency_mode(eng, args, device)
+        except Exception as ex:  # reported, never fatal for the device-resident number
+            log(f"latency mode failed: {ex!r}")
+            lat = {"error": repr(ex)}
     traffic, traffic_src = pmc_traffic(min(n, info["max_chunk"]))
     # executed (not algorithmic) instruction rate of the dsm kernel: the
     # half-size formulation executes fewer operations than the reference's

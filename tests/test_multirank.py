@@ -109,3 +109,93 @@ def test_bench_rejects_a_launcher_world_that_differs_from_gpus():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], capture_output=True, text=True,
                        timeout=300, env=env)
     assert r.returncode == 2 and "--gpus 2 but the launcher started 1 ranks" in r.stderr
+
+
+class _Buf:
+    def __init__(self, a):
+        self.a = a
+
+    def download(self, dtype, n):
+        return self.a[:n].astype(dtype)
+
+
+class _Workload:
+    def __init__(self, n=64):
+        self.n, self.msg_bytes = n, 16 * n
+        self.msgs = _Buf(np.zeros(16 * n, np.uint8))
+        self.off = _Buf(np.arange(n, dtype=np.uint64) * 16)
+        self.sigs, self.pubs = _Buf(np.zeros(64 * n, np.uint8)), _Buf(np.zeros(32 * n, np.uint8))
+        self.expect = _Buf(np.zeros(n, np.int8))
+        self.sizes = np.full(n, 16, np.uint32)
+
+
+def _host_fed_worker(rank, world, port, q, fail_rank):
+    """bench.host_fed with the tile layer replaced by fakes: one rank's
+    setup raises, the other's succeeds"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import contextlib
+    import bench
+    from firedancer_amd import tile
+
+    class Pool:
+        def __init__(self, *a):
+            if rank == fail_rank:
+                raise OSError("pinned allocation failed (injected)")
+
+        def run(self, msgs, off, sz, sigs, pubs, out):
+            out[:] = 0
+            return out, 0.01, {"h2d_bytes": 100 * len(out), "direct_batches": 1, "staged_batches": 0}
+
+        def close(self):
+            pass
+
+    class Near:
+        cpus = [0]
+
+        def __init__(self, info):
+            pass
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+    tile.Pool, tile.NearDevice = Pool, Near
+    tile.HostRegistration = lambda *a: contextlib.nullcontext()
+    tile.max_span = lambda *a: 1 << 20
+    tile.h2d_gbps = lambda *a: 50.0
+    r, _, w = bench.dist_setup(world)
+    try:
+        bench.host_fed(_Workload(), 0, {}, w, 2, 32, 2, 2)
+        outcome = "ok"
+    except RuntimeError as ex:
+        outcome = "raised: " + str(ex)[:60]
+    bench.barrier(w)   # both ranks got here: nobody was left waiting in a collective
+    import torch.distributed as dist
+    dist.destroy_process_group()
+    q.put((r, outcome))
+
+
+@pytest.mark.parametrize("fail_rank", [0, 1, -1])
+def test_host_fed_failure_is_agreed_by_every_rank(fail_rank):
+    """A host-fed leg that fails on one rank fails on every rank, with no
+    rank left blocked in a barrier (the leg's collectives are reached by all
+    ranks whatever happens to their own setup); with no failure both
+    succeed."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_fed_worker, args=(r, 2, port, q, fail_rank)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if fail_rank < 0:
+        assert [o for _, o in res] == ["ok", "ok"]
+    else:
+        assert all(o.startswith("raised: host-fed leg failed on a rank (setup)") for _, o in res), res
