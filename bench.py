@@ -195,6 +195,45 @@ def config_c1(eng, args):
             "cpu_reference": cpu}
 
 
+def config_c3(eng, args):
+    """C3 (BASELINE.json configs[2]): multi-signer transactions with
+    fd_ed25519_verify_batch_single_msg's semantics -- 1..12 signatures
+    (uniform) over one shared 200-byte message each, all valid -- as a
+    device-resident batch of 65,536 transactions: the per-signature verify,
+    then the per-transaction combine (fd_ed25519_hip_txn_combine_dev).
+    Parity of this path is in tests/test_gpu_c3.py."""
+    rng = np.random.default_rng(args.seed + 3)
+    ntxn, msz = 65536, 200
+    cnt = rng.integers(1, 13, ntxn).astype(np.uint32)
+    first = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint32)
+    nsig = int(cnt.sum())
+    off = np.repeat(np.arange(ntxn, dtype=np.uint64) * msz, cnt)
+    sz = np.full(nsig, msz, np.uint32)
+    bufs = [eng.alloc(ntxn * msz + 16), eng.alloc(8 * nsig).upload(off), eng.alloc(4 * nsig).upload(sz),
+            eng.alloc(64 * nsig), eng.alloc(32 * nsig), eng.alloc(nsig), eng.alloc(4 * ntxn).upload(first),
+            eng.alloc(4 * ntxn).upload(cnt), eng.alloc(ntxn)]
+    msgs, d_off, d_sz, sigs, pubs, out, d_first, d_cnt, tout = bufs
+    eng.gen_dev(nsig, args.seed + 3, 0, msgs.ptr, ntxn * msz, d_off.ptr, d_sz.ptr, sigs.ptr, pubs.ptr)
+
+    def run():
+        eng.verify_dev(nsig, msgs.ptr, d_off.ptr, d_sz.ptr, sigs.ptr, pubs.ptr, out.ptr)
+        eng.txn_combine_dev(ntxn, out.ptr, d_first.ptr, d_cnt.ptr, tout.ptr)
+    for _ in range(2):
+        run()
+    eng.sync()
+    t = time.perf_counter()
+    for _ in range(10):
+        run()
+    eng.sync()
+    dt = time.perf_counter() - t
+    codes = tout.download(np.int8, ntxn)
+    for b in bufs:
+        b.free()
+    return {"txns": ntxn, "signatures": nsig, "sigs_per_txn": "1..12 uniform, one shared 200-byte message",
+            "gpu_txn_per_s": 10 * ntxn / dt, "gpu_verifies_per_s": 10 * nsig / dt,
+            "gpu_ms_per_batch": dt * 1e3 / 10, "all_success": bool((codes == 0).all())}
+
+
 def latency_mode(eng, args, device):
     """C5: the verify tile's latency mode.  Signed single-signer Solana
     transactions (~200-byte messages, GPU-signed) are published into a
@@ -484,13 +523,18 @@ def main():
     path_ops = float(ops["total"].sum()) / chunks
     path_achieved = path_ops / (path_ms * 1e-3) / 1e12 if path_ms > 0 else None
 
-    cpu = c1 = None
+    cpu = c1 = c3 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(wl, out, args.cpu_sample, args.cpu_reps)
             c1 = config_c1(eng, args)
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"cpu baseline failed: {ex!r}")
+        try:
+            c3 = config_c3(eng, args)
+        except Exception as ex:  # reported, never fatal for the GPU number
+            log(f"C3 leg failed: {ex!r}")
+            c3 = {"error": repr(ex)}
     hf = hf_first
     if args.host_reps > 0 and hf is None:
         try:
@@ -560,6 +604,7 @@ def main():
             "host_fed": hf,
             "latency_mode": lat,
             "config_c1": c1,
+            "config_c3": c3,
             "verdicts_match_reference_labels": mism_all == 0,
             "verdict_mismatches": mism_all,
             "invalid_fraction": float((expect != 0).mean()),
