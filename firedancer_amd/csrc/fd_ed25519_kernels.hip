@@ -1082,6 +1082,61 @@ fd_ed25519_gen_btab_run_kernel(int32_t* tab, int entries, const int32_t* base, i
   }
 }
 
+/* Self-check of a wide base table: entry e + 1 == entry e + entry 1 for
+   every e (entry 0 the identity), one lane per e; mismatches counted with a
+   vector atomic.  With entry 1 (and a few others) compared against an
+   independent [s]B on the host, this proves every entry
+   (fd_ed25519_hip_engine_check_base_tables, tests/test_gpu_parity.py). */
+FD_DEV void btab_entry_p3(ge_p3& P, const int32_t* o) {
+  const fe dinv = {FE_DINV};
+  fe ypx, ymx, xy2d;
+  fe_ld(ypx, o); fe_ld(ymx, o + 10); fe_ld(xy2d, o + 20);
+  fe_sub(P.X, ypx, ymx);          /* 2x */
+  fe_add(P.Y, ypx, ymx);          /* 2y */
+  fe_0(P.Z); P.Z.v[0] = 2;        /* 2  */
+  fe_mul(P.T, xy2d, dinv);        /* 2xy = X Y / Z */
+}
+
+__global__ void __launch_bounds__(256)
+fd_ed25519_check_btabw_kernel(const int32_t* tab, int entries, uint32_t* bad) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e + 1 >= entries) return;
+  const int32_t* o = tab + (int64_t)e * FD_ED25519_BTAB16_STRIDE;
+  const int32_t* n = o + FD_ED25519_BTAB16_STRIDE;
+  const int32_t* b = tab + FD_ED25519_BTAB16_STRIDE;
+  ge_p3 P;
+  btab_entry_p3(P, o);
+  ge_precomp q;
+  fe_ld(q.yplusx, b); fe_ld(q.yminusx, b + 10); fe_ld(q.xy2d, b + 20);
+  ge_p1p1 r;
+  ge_madd(r, P, q);                /* x = r.X / r.Z, y = r.Y / r.T */
+  fe ypx, ymx, d, t, u;
+  fe_ld(ypx, n); fe_ld(ymx, n + 10);
+  fe_sub(d, ypx, ymx);             /* 2x' */
+  fe_mul(t, d, r.Z);
+  fe_add(u, r.X, r.X);
+  fe_sub(t, t, u);
+  bool ok = fe_iszero(t);
+  fe_add(d, ypx, ymx);             /* 2y' */
+  fe_mul(t, d, r.T);
+  fe_add(u, r.Y, r.Y);
+  fe_sub(t, t, u);
+  ok = ok && fe_iszero(t);
+  if (e == 0) {                    /* entry 0: the identity (1, 1, 0) */
+    bool id = o[0] == 1 && o[10] == 1 && o[20] == 0;
+    for (int i = 1; i < 10; i++) id = id && o[i] == 0 && o[10 + i] == 0 && o[20 + i] == 0;
+    ok = ok && id;
+  }
+  if (!ok) atomicAdd(bad, 1u);
+}
+
+extern "C" int fd_ed25519_hip_launch_check_btabw(const int32_t* d_tab, uint32_t* d_bad, void* stream) {
+  const int entries = FD_ED25519_BTABW_ENTRIES;
+  hipLaunchKernelGGL(fd_ed25519_check_btabw_kernel, dim3((entries + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     d_tab, entries, d_bad);
+  return (int)hipGetLastError();
+}
+
 /* ------------------------------------------------------------------------
    Per-transaction combine (fd_ed25519_verify_batch_single_msg priority). */
 

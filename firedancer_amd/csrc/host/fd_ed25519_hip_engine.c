@@ -458,6 +458,41 @@ fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * e, double * phase_m
   return FD_ED25519_HIP_OK;
 }
 
+/* ---- base-table self-check ------------------------------------------ */
+
+#if FD_ED25519_BTABW_BITS != FD_ED25519_HIP_BASE_TABLE_BITS || FD_ED25519_BTABW_SHIFT != FD_ED25519_HIP_BASE_TABLE_SHIFT
+#error "base table geometry differs from the public header's"
+#endif
+
+int
+fd_ed25519_hip_engine_check_base_tables( fd_ed25519_hip_engine_t * e, unsigned long bad[2] ) {
+  if( !e || !bad || !e->btabw[0] || !e->btabw[1] ) return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  uint32_t * d_bad = NULL;
+  HIPCHK( hipMalloc( (void **)&d_bad, 2*sizeof(uint32_t) ), "hipMalloc" );
+  uint32_t h_bad[2] = { 0U, 0U };
+  hipError_t he = hipMemsetAsync( d_bad, 0, 2*sizeof(uint32_t), e->stream );
+  for( int t=0; t<2 && he==hipSuccess; t++ )
+    he = (hipError_t)fd_ed25519_hip_launch_check_btabw( e->btabw[t], d_bad + t, e->stream );
+  if( he==hipSuccess ) he = hipMemcpyAsync( h_bad, d_bad, sizeof(h_bad), hipMemcpyDeviceToHost, e->stream );
+  if( he==hipSuccess ) he = hipStreamSynchronize( e->stream );
+  hipFree( d_bad );
+  if( he!=hipSuccess ) return hip_fail( he, "check_base_tables" );
+  bad[0] = h_bad[0]; bad[1] = h_bad[1];
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_engine_base_entry( fd_ed25519_hip_engine_t * e, int which, unsigned long index, int out[30] ) {
+  if( !e || !out || which<0 || which>1 || index>=(unsigned long)FD_ED25519_BTABW_ENTRIES || !e->btabw[which] )
+    return FD_ED25519_HIP_ERR_INVAL;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  HIPCHK( hipMemcpyAsync( out, e->btabw[which] + index*FD_ED25519_BTAB16_STRIDE, 30*sizeof(int32_t),
+                          hipMemcpyDeviceToHost, e->stream ), "hipMemcpy" );
+  HIPCHK( hipStreamSynchronize( e->stream ), "hipStreamSynchronize" );
+  return FD_ED25519_HIP_OK;
+}
+
 /* ---- device memory helpers (the engine's HIP runtime) ---------------- */
 
 void *

@@ -66,6 +66,11 @@ _lib.fd_ed25519_hip_corrupt_dev.argtypes = [ctypes.c_void_p, ctypes.c_ulong, cty
 _lib.fd_ed25519_hip_engine_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
 _lib.fd_ed25519_hip_engine_timing_read.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                                    ctypes.POINTER(ctypes.c_ulong)]
+_lib.fd_ed25519_hip_engine_check_base_tables.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulong)]
+_lib.fd_ed25519_hip_engine_base_entry.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_ulong,
+                                                  ctypes.POINTER(ctypes.c_int)]
+BASE_TABLE_BITS = 24     # FD_ED25519_HIP_BASE_TABLE_BITS
+BASE_TABLE_SHIFT = 144   # FD_ED25519_HIP_BASE_TABLE_SHIFT
 _lib.fd_ed25519_hip_dev_alloc.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
 _lib.fd_ed25519_hip_dev_alloc.restype = ctypes.c_void_p
 _lib.fd_ed25519_hip_dev_free.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
@@ -226,6 +231,20 @@ class Engine:
         cnt = ctypes.c_ulong(0)
         _check(_lib.fd_ed25519_hip_engine_timing_read(self._h, ms, ctypes.byref(cnt)))
         return {name: ms[i] for i, name in enumerate(PHASES)}, cnt.value
+
+    def check_base_tables(self):
+        """per wide base table, the count of entries e with entry e+1 !=
+        entry e + entry 1 (0, 0 for correct tables)"""
+        bad = (ctypes.c_ulong * 2)()
+        _check(_lib.fd_ed25519_hip_engine_check_base_tables(self._h, bad))
+        return bad[0], bad[1]
+
+    def base_entry(self, which, index):
+        """entry `index` of wide base table `which` (0: [e]B, 1: [e][2^144]B):
+        int32 [30] = (y+x, y-x, 2dxy) in radix-2^25.5 limbs"""
+        out = (ctypes.c_int * 30)()
+        _check(_lib.fd_ed25519_hip_engine_base_entry(self._h, which, index, out))
+        return np.array(out[:], dtype=np.int64)
 
     def diag_half_scalars(self, k_words):
         """Diagnostic: the device's half-size scalar search for k given as

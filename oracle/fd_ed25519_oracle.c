@@ -582,6 +582,16 @@ ge_scalarmult_base( ge * r, uint8_t const s[32] ) {
 /* ------------------------------------------------------------------------
    Public API (restating fd_ed25519_user.c) */
 
+/* encoding of [s]B, s < L (test infrastructure: anchors the GPU's base
+   tables, tests/test_gpu_parity.py) */
+void
+oracle_base_mul_encode( uint8_t out[32], uint8_t const s[32] ) {
+  ensure_init();
+  ge r;
+  ge_scalarmult_base( &r, s );
+  ge_tobytes( out, &r );
+}
+
 int
 oracle_ed25519_verify( uint8_t const * msg, uint64_t msg_sz, uint8_t const sig[64],
                        uint8_t const pub[32], int codes ) {

@@ -27,6 +27,7 @@ def _oracle():
     lib.oracle_ed25519_strerror.restype = ctypes.c_char_p
     lib.oracle_sha512.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]
     lib.oracle_scalar_reduce.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    lib.oracle_base_mul_encode.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     lib.oracle_verify_many.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     return lib

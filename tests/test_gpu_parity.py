@@ -321,3 +321,35 @@ def test_engines_share_base_tables(fd, adversarial):
     d = fd.Engine(0, max_chunk=1 << 12)   # the module's engines may still hold them; either way correct
     _check(_run(d, adversarial), want)
     d.close()
+
+
+def test_base_tables_are_exact(fd, oracle):
+    """The half-size form's 2 x 2^24-entry base tables: on the device every
+    entry e+1 equals entry e + entry 1 (entry 0 the identity), and entries
+    1, 2, the run boundaries of the generator (runs of 32), the middle and
+    the last, plus random ones, equal the oracle's [e 2^shift]B -- anchors
+    that, with the chain, pin every entry; 2dxy checked too."""
+    eng = fd.Engine(0, max_chunk=1 << 12)
+    assert eng.check_base_tables() == (0, 0)
+    P = 2**255 - 19
+    L = 2**252 + 27742317777372353535851937790883648493
+    d = (-121665 * pow(121666, P - 2, P)) % P
+    off = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+
+    def val(limbs):
+        return sum(int(l) << o for l, o in zip(limbs, off)) % P
+
+    rng = np.random.default_rng(7)
+    idx = [1, 2, 3, 31, 32, 33, 63, 64, 1 << 23, (1 << 24) - 33, (1 << 24) - 32, (1 << 24) - 2, (1 << 24) - 1]
+    idx += [int(x) for x in rng.integers(1, 1 << 24, 8)]
+    for which, shift in ((0, 0), (1, fd.BASE_TABLE_SHIFT)):
+        for e in idx:
+            ent = eng.base_entry(which, e)
+            ypx, ymx, xy2d = val(ent[0:10]), val(ent[10:20]), val(ent[20:30])
+            inv2 = (P + 1) // 2
+            y, x = (ypx + ymx) * inv2 % P, (ypx - ymx) * inv2 % P
+            assert xy2d == 2 * d * x * y % P, (which, e)
+            want = ctypes.create_string_buffer(32)
+            oracle.oracle_base_mul_encode(want, ((e << shift) % L).to_bytes(32, "little"))
+            assert (y | ((x & 1) << 255)).to_bytes(32, "little") == want.raw, (which, e)
+    eng.close()
