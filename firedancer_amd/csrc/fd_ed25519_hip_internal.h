@@ -114,9 +114,9 @@ int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, int base_doublings, vo
 /* [0..2^24)[2^base_doublings]B into d_tab; d_scratch holds
    FD_ED25519_BTABW_ENTRIES*10 + 40 int32 */
 int fd_ed25519_hip_launch_gen_btabw( int32_t * d_tab, int base_doublings, int32_t * d_scratch, void * stream );
-/* counts into *d_bad the entries e of a wide table with entry e+1 !=
-   entry e + entry 1 (and entry 0 not the identity) */
-int fd_ed25519_hip_launch_check_btabw( int32_t const * d_tab, uint32_t * d_bad, void * stream );
+/* counts into *d_bad the entries e < entries-1 of a 32-int-stride base
+   table with entry e+1 != entry e + entry 1 (and entry 0 not the identity) */
+int fd_ed25519_hip_launch_check_btabw( int32_t const * d_tab, int entries, uint32_t * d_bad, void * stream );
 /* Enqueues hash, decode and dsm for one chunk; `grid` caps the persistent
    dsm grid (its atab scratch must hold grid*VERIFY_BLOCK/64 waves). */
 int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t grid, void * stream );

@@ -1130,8 +1130,7 @@ fd_ed25519_check_btabw_kernel(const int32_t* tab, int entries, uint32_t* bad) {
   if (!ok) atomicAdd(bad, 1u);
 }
 
-extern "C" int fd_ed25519_hip_launch_check_btabw(const int32_t* d_tab, uint32_t* d_bad, void* stream) {
-  const int entries = FD_ED25519_BTABW_ENTRIES;
+extern "C" int fd_ed25519_hip_launch_check_btabw(const int32_t* d_tab, int entries, uint32_t* d_bad, void* stream) {
   hipLaunchKernelGGL(fd_ed25519_check_btabw_kernel, dim3((entries + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      d_tab, entries, d_bad);
   return (int)hipGetLastError();

@@ -465,20 +465,22 @@ fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * e, double * phase_m
 #endif
 
 int
-fd_ed25519_hip_engine_check_base_tables( fd_ed25519_hip_engine_t * e, unsigned long bad[2] ) {
-  if( !e || !bad || !e->btabw[0] || !e->btabw[1] ) return FD_ED25519_HIP_ERR_INVAL;
+fd_ed25519_hip_engine_check_base_tables( fd_ed25519_hip_engine_t * e, unsigned long bad[3] ) {
+  if( !e || !bad || !e->btabw[0] || !e->btabw[1] || !e->d_btab16 ) return FD_ED25519_HIP_ERR_INVAL;
   HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
   uint32_t * d_bad = NULL;
-  HIPCHK( hipMalloc( (void **)&d_bad, 2*sizeof(uint32_t) ), "hipMalloc" );
-  uint32_t h_bad[2] = { 0U, 0U };
-  hipError_t he = hipMemsetAsync( d_bad, 0, 2*sizeof(uint32_t), e->stream );
-  for( int t=0; t<2 && he==hipSuccess; t++ )
-    he = (hipError_t)fd_ed25519_hip_launch_check_btabw( e->btabw[t], d_bad + t, e->stream );
+  HIPCHK( hipMalloc( (void **)&d_bad, 3*sizeof(uint32_t) ), "hipMalloc" );
+  uint32_t h_bad[3] = { 0U, 0U, 0U };
+  int32_t const * tab[3] = { e->btabw[0], e->btabw[1], e->d_btab16 };
+  int             cnt[3] = { FD_ED25519_BTABW_ENTRIES, FD_ED25519_BTABW_ENTRIES, FD_ED25519_BTAB16_ENTRIES };
+  hipError_t he = hipMemsetAsync( d_bad, 0, 3*sizeof(uint32_t), e->stream );
+  for( int t=0; t<3 && he==hipSuccess; t++ )
+    he = (hipError_t)fd_ed25519_hip_launch_check_btabw( tab[t], cnt[t], d_bad + t, e->stream );
   if( he==hipSuccess ) he = hipMemcpyAsync( h_bad, d_bad, sizeof(h_bad), hipMemcpyDeviceToHost, e->stream );
   if( he==hipSuccess ) he = hipStreamSynchronize( e->stream );
   hipFree( d_bad );
   if( he!=hipSuccess ) return hip_fail( he, "check_base_tables" );
-  bad[0] = h_bad[0]; bad[1] = h_bad[1];
+  for( int t=0; t<3; t++ ) bad[t] = h_bad[t];
   return FD_ED25519_HIP_OK;
 }
 

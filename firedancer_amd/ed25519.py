@@ -233,11 +233,12 @@ class Engine:
         return {name: ms[i] for i, name in enumerate(PHASES)}, cnt.value
 
     def check_base_tables(self):
-        """per wide base table, the count of entries e with entry e+1 !=
-        entry e + entry 1 (0, 0 for correct tables)"""
-        bad = (ctypes.c_ulong * 2)()
+        """per base table ([e]B, [e][2^144]B, and the full-length form's
+        [0..2^15]B), the count of entries e with entry e+1 != entry e +
+        entry 1 ((0, 0, 0) for correct tables)"""
+        bad = (ctypes.c_ulong * 3)()
         _check(_lib.fd_ed25519_hip_engine_check_base_tables(self._h, bad))
-        return bad[0], bad[1]
+        return bad[0], bad[1], bad[2]
 
     def base_entry(self, which, index):
         """entry `index` of wide base table `which` (0: [e]B, 1: [e][2^144]B):

@@ -283,8 +283,9 @@ fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * engine,
 /* The half-size form's base tables (generated on the device, shared by the
    engines of a device): table 0 holds [e]B, table 1 [e][2^SHIFT]B, for
    0 <= e < 2^BITS, as (y+x, y-x, 2dxy) in ten radix-2^25.5 limbs each.
-   check_base_tables counts, per table, the entries e with entry e+1 !=
-   entry e + entry 1 (or entry 0 not the identity); together with a few
+   check_base_tables counts, per table (bad[2]: the full-length form's
+   [0..2^15]B table), the entries e with entry e+1 != entry e + entry 1 (or
+   entry 0 not the identity); together with a few
    entries compared against an independent [s]B (base_entry), a zero count
    proves the whole table.  base_entry copies entry `index` of table
    `which` (30 int32) to the host. */
@@ -292,7 +293,7 @@ fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * engine,
 #define FD_ED25519_HIP_BASE_TABLE_SHIFT 144
 
 int
-fd_ed25519_hip_engine_check_base_tables( fd_ed25519_hip_engine_t * engine, unsigned long bad[2] );
+fd_ed25519_hip_engine_check_base_tables( fd_ed25519_hip_engine_t * engine, unsigned long bad[3] );
 
 int
 fd_ed25519_hip_engine_base_entry( fd_ed25519_hip_engine_t * engine, int which, unsigned long index, int out[30] );

@@ -324,13 +324,14 @@ def test_engines_share_base_tables(fd, adversarial):
 
 
 def test_base_tables_are_exact(fd, oracle):
-    """The half-size form's 2 x 2^24-entry base tables: on the device every
+    """The half-size form's 2 x 2^24-entry base tables (and the full-length
+    form's 2^15 + 1): on the device every
     entry e+1 equals entry e + entry 1 (entry 0 the identity), and entries
     1, 2, the run boundaries of the generator (runs of 32), the middle and
     the last, plus random ones, equal the oracle's [e 2^shift]B -- anchors
     that, with the chain, pin every entry; 2dxy checked too."""
     eng = fd.Engine(0, max_chunk=1 << 12)
-    assert eng.check_base_tables() == (0, 0)
+    assert eng.check_base_tables() == (0, 0, 0)
     P = 2**255 - 19
     L = 2**252 + 27742317777372353535851937790883648493
     d = (-121665 * pow(121666, P - 2, P)) % P
