@@ -432,6 +432,8 @@ def main():
     ap.add_argument("--host-slots", type=int, default=3,
                     help="3: each slot stream on its own hardware queue (4 measured 35% slower, tools/pool_first_probe.py)")
     ap.add_argument("--host-first", action="store_true", help="run the host-fed leg first (A/B)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight on the GPU (steps alternate between this many engines)")
     ap.add_argument("--allow-shared-device", action="store_true",
                     help="let ranks share a GPU (one-GPU rehearsal of --gpus N; n_gpus then counts devices)")
     args = ap.parse_args()
@@ -473,19 +475,42 @@ def main():
                                 args.host_copies)
         except Exception as ex:  # the same on every rank (host_fed agrees first); never fatal
             log(f"[rank {rank}] host-fed leg failed: {ex!r}")
-    for _ in range(args.warmup):
-        wl.verify()
-    eng.sync()
+    # batches in flight: consecutive steps alternate between `inflight`
+    # engines (each its own streams, work arrays and lane tables; the base
+    # tables are shared), so a step's hash/scalar/decode run beside the
+    # previous step's dsm and fill its tail -- the last waves of a
+    # persistent kernel whose items last ~1 ms -- as the pool's and the
+    # verify tile's slots do.  Every step still verifies all n signatures.
+    engines = [eng] + [ed25519.Engine(device=device, max_chunk=min(n, 1 << 20), half=args.half)
+                       for _ in range(args.inflight - 1)]
+    outs = [wl.out] + [e.alloc(n) for e in engines[1:]]
+
+    def step(s):
+        e, o = engines[s % len(engines)], outs[s % len(engines)]
+        e.verify_dev(n, wl.msgs.ptr, wl.off.ptr, wl.sz.ptr, wl.sigs.ptr, wl.pubs.ptr, o.ptr, e.stream)
+
+    def sync_all():
+        for e in engines:
+            e.sync()
+    for s in range(args.warmup):
+        step(s)
+    sync_all()
 
     barrier(world)
-    eng.sync()
+    sync_all()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        wl.verify()
-    eng.sync()
+    for s in range(args.steps):
+        step(s)
+    sync_all()
     t1 = time.perf_counter()
     barrier(world)
     elapsed = allreduce_max(t1 - t0, world)
+    mism_inflight = 0
+    for o in outs[1:]:
+        mism_inflight += int((o.download(np.int8, n) != wl.expect.download(np.int8, n)).sum())
+        o.free()
+    for e in engines[1:]:
+        e.close()
     # per-kernel durations: a separate pass of the same steps with HIP events
     # around each phase on the engine stream (the phases then run in sequence;
     # in the timed region above a chunk's decode overlaps its hash + scalar,
@@ -500,7 +525,7 @@ def main():
     # full-size verdict check: every code equals the class label's reference code
     out = wl.out.download(np.int8, n)
     expect = wl.expect.download(np.int8, n)
-    mism = int((out != expect).sum())
+    mism = int((out != expect).sum()) + mism_inflight
     mism_all = int(allreduce_sum(mism, world))
     if mism:
         log(f"[rank {rank}] VERDICT MISMATCH on {mism} of {n} signatures")
@@ -577,6 +602,7 @@ def main():
                                    + f", message size uniform [{cfg['lo']},{cfg['hi']}] B, {cfg['ppm'] / 1e4:.1f}% invalid",
                        "signatures_per_gpu": n, "parallelism": f"shard x{world} (independent batches, no collective)",
                        "devices": devices,
+                       "batches_in_flight": args.inflight,
                        "codes": "reference AVX-512 backend"},
             "roofline": {"bound": "valu-int32", "kernel": "fd_ed25519_dsm_kernel",
                          "achieved": achieved, "peak": peak, "unit": "TOPS",
@@ -597,8 +623,10 @@ def main():
                          "signatures_per_launch": min(n, info["max_chunk"])},
             "kernel_ms_per_launch": per_launch,
             "kernel_timing": "HIP events around each phase on the engine stream, in a separate pass of the same "
-                             "steps (phases in sequence); in the timed region a chunk's decode runs on a side "
-                             "stream beside its hash + scalar (dsm alone either way)",
+                             "steps on one engine (phases in sequence); in the timed region a chunk's decode "
+                             "runs on a side stream beside its hash + scalar, and consecutive steps alternate "
+                             "between config.batches_in_flight engines so a step's phases run beside the "
+                             "previous step's dsm",
             "cpu_baseline": cpu,
             "gpu_over_cpu": (value / cpu["value"]) if cpu else None,
             "host_fed": hf,
