@@ -48,25 +48,34 @@ struct fd_ed25519_hip_engine {
   int32_t *    d_btab;
   int32_t *    d_btab16;     /* [0..2^15]B, the verify kernels' wide B table  */
   int32_t *    btabw[2];    /* shared per device: [0..2^24)B, [0..2^24)[2^144]B */
-  /* the per-chunk scratch of the chunk in flight */
+  /* Pipeline lanes: the per-chunk scratch of a chunk in flight, and the
+     streams its phases run on.  Lane 0 runs on the caller's stream (or the
+     engine's); the chunks of a multi-chunk call alternate between lane 0
+     and lane 1 (its own streams and scratch, made on the first such call),
+     so one chunk's hash / scalar / decode run beside the previous chunk's
+     dsm and fill the tail of that persistent kernel (its work items last
+     ~1 ms, so its last ~0.46 ms per launch leaves SIMDs idle). */
   struct {
-    void *     d_atab;       /* dsm lane tables (and the dsm4 quad tables)  */
-    uint8_t *  d_work;       /* one allocation carved into the work arrays */
-    uint32_t * d_k;
-    uint8_t *  d_sflag;
-    uint8_t *  d_pflag;
-    int32_t *  d_pts;
-    uint32_t * d_fix;        /* scalar -> dsm full-length list */
-    uint32_t * d_hs;         /* half-size scalars             */
-    uint8_t *  d_hflag;
-    uint32_t * d_perm;       /* hash order (length-sorted) */
-    uint32_t * d_hist;       /* counting-sort scratch      */
-  } ws;
-  /* overlap: a large chunk's decode (A and R need neither the hash nor the
-     scalars) runs on a side stream beside hash + scalar, dsm after both */
+    void *      d_atab;      /* dsm lane tables (and the dsm4 quad tables)  */
+    uint8_t *   d_work;      /* one allocation carved into the work arrays */
+    uint32_t *  d_k;
+    uint8_t *   d_sflag;
+    uint8_t *   d_pflag;
+    int32_t *   d_pts;
+    uint32_t *  d_fix;       /* scalar -> dsm full-length list */
+    uint32_t *  d_hs;        /* half-size scalars             */
+    uint8_t *   d_hflag;
+    uint32_t *  d_perm;      /* hash order (length-sorted) */
+    uint32_t *  d_hist;      /* counting-sort scratch      */
+    hipStream_t stream;      /* lane 1 only (lane 0: the call's stream)       */
+    /* overlap: a large chunk's decode (A and R need neither the hash nor
+       the scalars) runs on a side stream beside hash + scalar, dsm after */
+    hipStream_t side;
+    hipEvent_t  ev_dfork, ev_djoin;
+  } lane[ 2 ];
   int          overlap;
-  hipStream_t  side;
-  hipEvent_t   ev_dfork, ev_djoin;
+  int          pipeline;     /* multi-chunk calls alternate lanes */
+  hipEvent_t   ev_start, ev_end;   /* lane 1 after the call's prior work; the call's stream after lane 1 */
 
   /* host-API staging (pinned host + device mirrors), grown on demand */
   uint64_t     st_sig_cap;   /* signatures */
@@ -189,9 +198,12 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   /* all work of the engine's streams has drained before any buffer goes:
      a failed verify_dev may have left decode queued on the side stream */
   if( e->stream ) hipStreamSynchronize( e->stream );
-  if( e->side   ) hipStreamSynchronize( e->side );
+  for( int l=0; l<2; l++ ) {
+    if( e->lane[l].stream ) hipStreamSynchronize( e->lane[l].stream );
+    if( e->lane[l].side   ) hipStreamSynchronize( e->lane[l].side );
+  }
   hipFree( e->d_btab ); hipFree( e->d_btab16 );
-  hipFree( e->ws.d_atab ); hipFree( e->ws.d_work );
+  for( int l=0; l<2; l++ ) { hipFree( e->lane[l].d_atab ); hipFree( e->lane[l].d_work ); }
   if( e->btabw[0] ) btabw_release( e->device );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
@@ -201,10 +213,14 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   if( e->tm_ev_init )
     for( int i=0; i<FD_ED25519_HIP_TIMING_MAX; i++ )
       for( int j=0; j<=FD_ED25519_PHASE_CNT; j++ ) hipEventDestroy( e->tm_ev[i][j] );
-  if( e->side ) {
-    hipEventDestroy( e->ev_dfork ); hipEventDestroy( e->ev_djoin );
-    hipStreamDestroy( e->side );
+  for( int l=0; l<2; l++ ) {
+    if( e->lane[l].side ) {
+      hipEventDestroy( e->lane[l].ev_dfork ); hipEventDestroy( e->lane[l].ev_djoin );
+      hipStreamDestroy( e->lane[l].side );
+    }
+    if( e->lane[l].stream ) hipStreamDestroy( e->lane[l].stream );
   }
+  if( e->lane[1].d_work ) { hipEventDestroy( e->ev_start ); hipEventDestroy( e->ev_end ); }
   if( e->stream ) hipStreamDestroy( e->stream );
   free( e );
 }
@@ -212,6 +228,40 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
 void
 fd_ed25519_hip_engine_delete( fd_ed25519_hip_engine_t * engine ) {
   engine_free( engine );
+}
+
+static size_t
+lane_atab_bytes( fd_ed25519_hip_engine_t const * e ) {
+  return (size_t)e->dsm_grid * (FD_ED25519_VERIFY_BLOCK / 64) * FD_ED25519_ATAB_BYTES_PER_WAVE;
+}
+
+/* a lane's scratch (dsm lane tables + work arrays for max_chunk
+   signatures); lane 1 also gets its streams and the join events */
+static int
+lane_alloc( fd_ed25519_hip_engine_t * e, int l ) {
+  size_t atab_sz = lane_atab_bytes( e );
+  size_t work_sz = (size_t)e->max_chunk * FD_ED25519_WORK_BYTES_PER_SIG + 1024;
+  HIPCHK( hipMalloc( &e->lane[l].d_atab, atab_sz ), "hipMalloc(atab)" );
+  HIPCHK( hipMalloc( (void **)&e->lane[l].d_work, work_sz ), "hipMalloc(work)" );
+  e->device_bytes += atab_sz + work_sz;
+  uint64_t c = e->max_chunk;
+  uint8_t * w = e->lane[l].d_work;
+  e->lane[l].d_k     = (uint32_t *)w; w += 8UL*4UL*c;
+  e->lane[l].d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
+  e->lane[l].d_hs    = (uint32_t *)w; w += 19UL*4UL*c;
+  e->lane[l].d_perm  = (uint32_t *)w; w += 4UL*c;
+  e->lane[l].d_fix   = (uint32_t *)w; w += 4UL*c;
+  e->lane[l].d_sflag = w;             w += c;
+  e->lane[l].d_pflag = w;             w += 2UL*c;
+  e->lane[l].d_hflag = w;             w += c;
+  w = (uint8_t *)(((uintptr_t)w + 255UL) & ~(uintptr_t)255UL);
+  e->lane[l].d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words + fix count inside the 1024-byte slack */
+  if( l ) {
+    HIPCHK( hipStreamCreateWithFlags( &e->lane[l].stream, hipStreamNonBlocking ), "hipStreamCreate" );
+    HIPCHK( hipEventCreateWithFlags( &e->ev_start, hipEventDisableTiming ), "hipEventCreate" );
+    HIPCHK( hipEventCreateWithFlags( &e->ev_end,   hipEventDisableTiming ), "hipEventCreate" );
+  }
+  return FD_ED25519_HIP_OK;
 }
 
 static int
@@ -240,30 +290,17 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
 
   size_t btab_sz = sizeof(int32_t) * FD_ED25519_BTAB_INTS;
   size_t btab16_sz = sizeof(int32_t) * (size_t)FD_ED25519_BTAB16_ENTRIES * FD_ED25519_BTAB16_STRIDE;
-  size_t atab_sz = (size_t)e->dsm_grid * (FD_ED25519_VERIFY_BLOCK / 64) * FD_ED25519_ATAB_BYTES_PER_WAVE;
-  size_t work_sz = (size_t)e->max_chunk * FD_ED25519_WORK_BYTES_PER_SIG + 1024;
+  size_t atab_sz = lane_atab_bytes( e );
   HIPCHK( hipMalloc( (void **)&e->d_btab, btab_sz ), "hipMalloc(btab)" );
   HIPCHK( hipMalloc( (void **)&e->d_btab16, btab16_sz ), "hipMalloc(btab16)" );
-  e->device_bytes = btab_sz + btab16_sz + atab_sz + work_sz;   /* + 2 x 128 MB shared per device */
-  HIPCHK( hipMalloc( &e->ws.d_atab, atab_sz ), "hipMalloc(atab)" );
-  HIPCHK( hipMalloc( (void **)&e->ws.d_work, work_sz ), "hipMalloc(work)" );
-  {
-    uint64_t c = e->max_chunk;
-    uint8_t * w = e->ws.d_work;
-    e->ws.d_k     = (uint32_t *)w; w += 8UL*4UL*c;
-    e->ws.d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
-    e->ws.d_hs    = (uint32_t *)w; w += 19UL*4UL*c;
-    e->ws.d_perm  = (uint32_t *)w; w += 4UL*c;
-    e->ws.d_fix   = (uint32_t *)w; w += 4UL*c;
-    e->ws.d_sflag = w;             w += c;
-    e->ws.d_pflag = w;             w += 2UL*c;
-    e->ws.d_hflag = w;             w += c;
-    w = (uint8_t *)(((uintptr_t)w + 255UL) & ~(uintptr_t)255UL);
-    e->ws.d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words + fix count inside the 1024-byte slack */
-  }
+  e->device_bytes = btab_sz + btab16_sz;   /* + each lane's scratch; + the base tables shared per device */
+  int lerr = lane_alloc( e, 0 );
+  if( lerr ) return lerr;
   char const * ovs = getenv( "FD_ED25519_HIP_OVERLAP" );
   e->overlap = ovs ? ovs[0]=='1' : FD_ED25519_HIP_OVERLAP_DEFAULT;
-  if( flags & FD_ED25519_HIP_FLAG_ONE_STREAM ) e->overlap = 0;
+  char const * pls = getenv( "FD_ED25519_HIP_PIPELINE" );
+  e->pipeline = pls ? pls[0]=='1' : 1;
+  if( flags & FD_ED25519_HIP_FLAG_ONE_STREAM ) e->overlap = e->pipeline = 0;
   /* dsm4 (a quad of lanes per signature) below the size where one lane
      per signature fills the chip; its lane tables live in the atab scratch */
   uint64_t quad_cap = atab_sz / (4UL * FD_ED25519_QUAD_LANE_BYTES);
@@ -351,6 +388,59 @@ fd_ed25519_hip_engine_sync( fd_ed25519_hip_engine_t * e ) {
   return FD_ED25519_HIP_OK;
 }
 
+/* one chunk [base,base+cnt) through the phases on lane l's scratch, on
+   stream st (the call's stream for lane 0, lane 1's own stream otherwise) */
+static int
+verify_chunk( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p, int l,
+              uint64_t base, uint64_t cnt, hipStream_t st ) {
+  p->k = e->lane[l].d_k; p->sflag = e->lane[l].d_sflag; p->pflag = e->lane[l].d_pflag; p->pts = e->lane[l].d_pts;
+  p->fix_list = e->lane[l].d_fix; p->fix_cnt = e->lane[l].d_hist + 2*FD_ED25519_SORT_BUCKETS;
+  p->work_ctr = p->fix_cnt + 1; p->hs = e->lane[l].d_hs; p->hflag = e->lane[l].d_hflag;
+  p->hist = e->lane[l].d_hist; p->atab = e->lane[l].d_atab;
+  p->base  = base;
+  p->n     = cnt;
+  p->small = p->n > e->quad_max ? 0 : (p->n <= e->oct_max ? 2 : 1);
+  p->perm  = p->small ? NULL : e->lane[l].d_perm;
+  if( e->timing && e->tm_cnt<FD_ED25519_HIP_TIMING_MAX ) {
+    /* events bracket each phase kernel on the stream it runs on */
+    hipEvent_t * ev = e->tm_ev[ e->tm_cnt++ ];
+    HIPCHK( hipEventRecord( ev[0], st ), "hipEventRecord" );
+    for( int ph=0; ph<FD_ED25519_PHASE_CNT; ph++ ) {
+      int err = fd_ed25519_hip_launch_phase( p, ph, e->dsm_grid, st );
+      if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+      HIPCHK( hipEventRecord( ev[ph+1], st ), "hipEventRecord" );
+    }
+  } else if( e->overlap && !p->small ) {
+    if( !e->lane[l].side ) {
+      /* created on the first large chunk only: an engine that only sees
+         small batches (a tile slot) keeps to one stream, since the
+         device's few hardware queues are shared by every stream of the
+         process and extra streams serialise the slots */
+      HIPCHK( hipStreamCreateWithFlags( &e->lane[l].side, hipStreamNonBlocking ), "hipStreamCreate" );
+      HIPCHK( hipEventCreateWithFlags( &e->lane[l].ev_dfork, hipEventDisableTiming ), "hipEventCreate" );
+      HIPCHK( hipEventCreateWithFlags( &e->lane[l].ev_djoin, hipEventDisableTiming ), "hipEventCreate" );
+    }
+    HIPCHK( hipEventRecord( e->lane[l].ev_dfork, st ), "hipEventRecord" );
+    HIPCHK( hipStreamWaitEvent( e->lane[l].side, e->lane[l].ev_dfork, 0 ), "hipStreamWaitEvent" );
+    int err = fd_ed25519_hip_launch_phase( p, FD_ED25519_PHASE_DECODE, e->dsm_grid, e->lane[l].side );
+    if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+    HIPCHK( hipEventRecord( e->lane[l].ev_djoin, e->lane[l].side ), "hipEventRecord" );
+    err = fd_ed25519_hip_launch_phase( p, FD_ED25519_PHASE_HASH, e->dsm_grid, st );
+    if( !err ) err = fd_ed25519_hip_launch_phase( p, FD_ED25519_PHASE_SCALAR, e->dsm_grid, st );
+    /* dsm (and the lane's next chunk, which reuses the work arrays) after
+       decode, even when a launch above failed */
+    hipError_t we = hipStreamWaitEvent( st, e->lane[l].ev_djoin, 0 );
+    if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+    HIPCHK( we, "hipStreamWaitEvent" );
+    err = fd_ed25519_hip_launch_phase( p, FD_ED25519_PHASE_DSM, e->dsm_grid, st );
+    if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+  } else {
+    int err = fd_ed25519_hip_launch_verify( p, e->dsm_grid, st );
+    if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+  }
+  return FD_ED25519_HIP_OK;
+}
+
 int
 fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
                            unsigned long n,
@@ -375,54 +465,36 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   p.half_dbits     = engine_half_dbits( e );
   uint64_t chunk = e->max_chunk;
-  p.k = e->ws.d_k; p.sflag = e->ws.d_sflag; p.pflag = e->ws.d_pflag; p.pts = e->ws.d_pts;
-  p.fix_list = e->ws.d_fix; p.fix_cnt = e->ws.d_hist + 2*FD_ED25519_SORT_BUCKETS;
-  p.work_ctr = p.fix_cnt + 1; p.hs = e->ws.d_hs; p.hflag = e->ws.d_hflag;
-  p.hist = e->ws.d_hist; p.atab = e->ws.d_atab;
-  for( uint64_t base=0UL; base<n; base+=chunk ) {
-    p.base  = base;
-    p.n     = (n-base) < chunk ? (n-base) : chunk;
-    p.small = p.n > e->quad_max ? 0 : (p.n <= e->oct_max ? 2 : 1);
-    p.perm  = p.small ? NULL : e->ws.d_perm;
-    if( e->timing && e->tm_cnt<FD_ED25519_HIP_TIMING_MAX ) {
-      /* events bracket each phase kernel on the stream it runs on */
-      hipEvent_t * ev = e->tm_ev[ e->tm_cnt++ ];
-      HIPCHK( hipEventRecord( ev[0], st ), "hipEventRecord" );
-      for( int ph=0; ph<FD_ED25519_PHASE_CNT; ph++ ) {
-        int err = fd_ed25519_hip_launch_phase( &p, ph, e->dsm_grid, st );
-        if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-        HIPCHK( hipEventRecord( ev[ph+1], st ), "hipEventRecord" );
-      }
-    } else if( e->overlap && !p.small ) {
-      if( !e->side ) {
-        /* created on the first large chunk only: an engine that only sees
-           small batches (a tile slot) keeps to one stream, since the
-           device's few hardware queues are shared by every stream of the
-           process and extra streams serialise the slots */
-        HIPCHK( hipStreamCreateWithFlags( &e->side, hipStreamNonBlocking ), "hipStreamCreate" );
-        HIPCHK( hipEventCreateWithFlags( &e->ev_dfork, hipEventDisableTiming ), "hipEventCreate" );
-        HIPCHK( hipEventCreateWithFlags( &e->ev_djoin, hipEventDisableTiming ), "hipEventCreate" );
-      }
-      HIPCHK( hipEventRecord( e->ev_dfork, st ), "hipEventRecord" );
-      HIPCHK( hipStreamWaitEvent( e->side, e->ev_dfork, 0 ), "hipStreamWaitEvent" );
-      int err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DECODE, e->dsm_grid, e->side );
-      if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-      HIPCHK( hipEventRecord( e->ev_djoin, e->side ), "hipEventRecord" );
-      err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_HASH, e->dsm_grid, st );
-      if( !err ) err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_SCALAR, e->dsm_grid, st );
-      /* dsm (and the next chunk, which reuses the work arrays) after decode,
-         even when a launch above failed */
-      hipError_t we = hipStreamWaitEvent( st, e->ev_djoin, 0 );
-      if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-      HIPCHK( we, "hipStreamWaitEvent" );
-      err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, st );
-      if( err ) return hip_fail( (hipError_t)err, "verify launch" );
-    } else {
-      int err = fd_ed25519_hip_launch_verify( &p, e->dsm_grid, st );
-      if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+  /* a multi-chunk call alternates its chunks between the two lanes; lane 1
+     starts after the work already queued on the call's stream and the
+     call's stream waits for lane 1 before it returns, so the call stays
+     one ordered unit of work on the caller's stream */
+  int two = e->pipeline && !e->timing && n > chunk;
+  if( two && !e->lane[1].d_work ) {
+    int err = lane_alloc( e, 1 );
+    if( err ) return err;
+  }
+  if( two ) {
+    HIPCHK( hipEventRecord( e->ev_start, st ), "hipEventRecord" );
+    HIPCHK( hipStreamWaitEvent( e->lane[1].stream, e->ev_start, 0 ), "hipStreamWaitEvent" );
+  }
+  int err = FD_ED25519_HIP_OK;
+  uint64_t c = 0UL;
+  for( uint64_t base=0UL; base<n && !err; base+=chunk, c++ ) {
+    int l = two ? (int)(c & 1UL) : 0;
+    err = verify_chunk( e, &p, l, base, (n-base) < chunk ? (n-base) : chunk, l ? e->lane[1].stream : st );
+  }
+  if( two ) {
+    /* joined even when a launch failed, so the caller's stream never runs
+       ahead of work still queued on lane 1 */
+    hipError_t re = hipEventRecord( e->ev_end, e->lane[1].stream );
+    if( re==hipSuccess ) re = hipStreamWaitEvent( st, e->ev_end, 0 );
+    if( re!=hipSuccess ) {
+      hipStreamSynchronize( e->lane[1].stream );
+      if( !err ) return hip_fail( re, "lane join" );
     }
   }
-  return FD_ED25519_HIP_OK;
+  return err;
 }
 
 int

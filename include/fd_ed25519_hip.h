@@ -153,7 +153,13 @@ fd_ed25519_hip_engine_stream( fd_ed25519_hip_engine_t * engine );
    16-byte granules, up to 15 bytes beyond a message's last byte; the same
    holds for fd_ed25519_hip_sign_dev / _gen_dev).  Enqueued on `stream` (NULL = the engine's stream) and
    returns immediately; the engine's work arrays are reused by the next
-   call, so calls on one engine must be ordered on one stream. */
+   call, so calls on one engine must be ordered on one stream.  A call of
+   more than max_chunk signatures alternates its chunks between two sets of
+   work arrays on two streams (the second set, max_chunk x 280 B plus the
+   dsm lane tables, allocated on the first such call), so a chunk's hash,
+   scalar and decode phases fill the tail of the previous chunk's dsm; the
+   call still completes in order on `stream` ($FD_ED25519_HIP_PIPELINE=0 or
+   FD_ED25519_HIP_FLAG_ONE_STREAM keeps one set, per-phase timing too). */
 int
 fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * engine,
                            unsigned long             n,

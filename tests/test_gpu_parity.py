@@ -172,21 +172,27 @@ def test_dsm_form_by_size(fd, oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("env", [
-    {"FD_ED25519_HIP_OVERLAP": "0"},
-    {"FD_ED25519_HIP_OVERLAP": "1"},
-], ids=["sequential", "overlap"])
+    {"FD_ED25519_HIP_OVERLAP": "0", "FD_ED25519_HIP_PIPELINE": "0"},
+    {"FD_ED25519_HIP_OVERLAP": "1", "FD_ED25519_HIP_PIPELINE": "0"},
+    {"FD_ED25519_HIP_OVERLAP": "0", "FD_ED25519_HIP_PIPELINE": "1"},
+    {"FD_ED25519_HIP_OVERLAP": "1", "FD_ED25519_HIP_PIPELINE": "1"},
+], ids=["sequential", "overlap", "pipelined", "overlap-pipelined"])
 def test_launch_options_large_chunks(fd, oracle, monkeypatch, env):
-    """The engine's two launch sequences for one-lane-per-signature chunks
-    (the small-chunk threshold lowered so the batches stay small): phases in
-    sequence on one stream, and decode on the side stream beside hash +
-    scalar -- each against the oracle, over a batch of two chunks."""
+    """The engine's launch sequences for one-lane-per-signature chunks (the
+    small-chunk threshold lowered so the batches stay small): phases in
+    sequence on one stream or decode on a side stream beside hash + scalar,
+    with the chunks of one call on one set of work arrays or alternating
+    between two (each set used twice, the last chunk a short one) -- each
+    against the oracle; then a second call on the same engine, which must
+    order after the first's lane-1 work."""
     monkeypatch.setenv("FD_ED25519_HIP_QUAD_MAX", "300")
     monkeypatch.setenv("FD_ED25519_HIP_OCT_MAX", "100")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     e = fd.Engine(0, max_chunk=1000)
-    d = _random_set(oracle, 1700, seed=19)
-    _check(_run(e, d), oracle_many(oracle, d, 0))
+    for n, seed in ((3700, 19), (2400, 20)):
+        d = _random_set(oracle, n, seed=seed)
+        _check(_run(e, d), oracle_many(oracle, d, 0))
     e.close()
 
 
