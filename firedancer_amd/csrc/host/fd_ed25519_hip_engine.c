@@ -236,16 +236,31 @@ lane_atab_bytes( fd_ed25519_hip_engine_t const * e ) {
 }
 
 /* a lane's scratch (dsm lane tables + work arrays for max_chunk
-   signatures); lane 1 also gets its streams and the join events */
+   signatures); lane 1 also gets its stream and the join events.  All or
+   nothing: the lane is usable once d_work is set, which happens last. */
 static int
 lane_alloc( fd_ed25519_hip_engine_t * e, int l ) {
   size_t atab_sz = lane_atab_bytes( e );
   size_t work_sz = (size_t)e->max_chunk * FD_ED25519_WORK_BYTES_PER_SIG + 1024;
-  HIPCHK( hipMalloc( &e->lane[l].d_atab, atab_sz ), "hipMalloc(atab)" );
-  HIPCHK( hipMalloc( (void **)&e->lane[l].d_work, work_sz ), "hipMalloc(work)" );
+  void * atab = NULL; uint8_t * work = NULL;
+  hipStream_t st = NULL; hipEvent_t ev0 = NULL, ev1 = NULL;
+  hipError_t he = hipMalloc( &atab, atab_sz );
+  if( he==hipSuccess ) he = hipMalloc( (void **)&work, work_sz );
+  if( l ) {
+    if( he==hipSuccess ) he = hipStreamCreateWithFlags( &st, hipStreamNonBlocking );
+    if( he==hipSuccess ) he = hipEventCreateWithFlags( &ev0, hipEventDisableTiming );
+    if( he==hipSuccess ) he = hipEventCreateWithFlags( &ev1, hipEventDisableTiming );
+  }
+  if( he!=hipSuccess ) {
+    if( ev1 ) hipEventDestroy( ev1 );
+    if( ev0 ) hipEventDestroy( ev0 );
+    if( st  ) hipStreamDestroy( st );
+    hipFree( work ); hipFree( atab );
+    return hip_fail( he, "lane scratch" );
+  }
   e->device_bytes += atab_sz + work_sz;
   uint64_t c = e->max_chunk;
-  uint8_t * w = e->lane[l].d_work;
+  uint8_t * w = work;
   e->lane[l].d_k     = (uint32_t *)w; w += 8UL*4UL*c;
   e->lane[l].d_pts   = (int32_t  *)w; w += 2UL*20UL*4UL*c;
   e->lane[l].d_hs    = (uint32_t *)w; w += 19UL*4UL*c;
@@ -256,11 +271,9 @@ lane_alloc( fd_ed25519_hip_engine_t * e, int l ) {
   e->lane[l].d_hflag = w;             w += c;
   w = (uint8_t *)(((uintptr_t)w + 255UL) & ~(uintptr_t)255UL);
   e->lane[l].d_hist  = (uint32_t *)w; /* 2*SORT_BUCKETS words + fix count inside the 1024-byte slack */
-  if( l ) {
-    HIPCHK( hipStreamCreateWithFlags( &e->lane[l].stream, hipStreamNonBlocking ), "hipStreamCreate" );
-    HIPCHK( hipEventCreateWithFlags( &e->ev_start, hipEventDisableTiming ), "hipEventCreate" );
-    HIPCHK( hipEventCreateWithFlags( &e->ev_end,   hipEventDisableTiming ), "hipEventCreate" );
-  }
+  e->lane[l].d_atab  = atab;
+  if( l ) { e->lane[l].stream = st; e->ev_start = ev0; e->ev_end = ev1; }
+  e->lane[l].d_work  = work;
   return FD_ED25519_HIP_OK;
 }
 
