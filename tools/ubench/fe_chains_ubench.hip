@@ -206,15 +206,14 @@ int main() {
   CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
   const int iters = 400;
   struct { const char* name; void (*f)(const int32_t*, int32_t*, int); double ops_per_iter; int wps; } ks[] = {
-    {"sq  2ch x1 w2", k_sq<2, 1, 2>, 1, 2}, {"sq  3ch x1 w2", k_sq<3, 1, 2>, 1, 2}, {"sq  4ch x1 w2", k_sq<4, 1, 2>, 1, 2},
-    {"sq  2ch x1 w4", k_sq<2, 1, 4>, 1, 4}, {"sq  3ch x1 w4", k_sq<3, 1, 4>, 1, 4}, {"sq  4ch x1 w4", k_sq<4, 1, 4>, 1, 4},
-    {"sq  2ch x2 w2", k_sq<2, 2, 2>, 2, 2}, {"sq  3ch x2 w2", k_sq<3, 2, 2>, 2, 2}, {"sq  4ch x2 w2", k_sq<4, 2, 2>, 2, 2},
-    {"sq  2ch x2 w3", k_sq<2, 2, 3>, 2, 3}, {"sq  3ch x2 w3", k_sq<3, 2, 3>, 2, 3},
-    {"sq  2ch x2 w4", k_sq<2, 2, 4>, 2, 4}, {"sq  3ch x2 w4", k_sq<3, 2, 4>, 2, 4}, {"sq  4ch x2 w4", k_sq<4, 2, 4>, 2, 4},
-    {"sq  2ch x4 w2", k_sq<2, 4, 2>, 4, 2}, {"sq  3ch x4 w2", k_sq<3, 4, 2>, 4, 2},
-    {"sq  2ch x1 w8", k_sq<2, 1, 8>, 1, 8}, {"sq  3ch x1 w8", k_sq<3, 1, 8>, 1, 8},
-    {"mul 2ch x3 w2", k_mul<2, 2>, 3, 2}, {"mul 3ch x3 w2", k_mul<3, 2>, 3, 2}, {"mul 4ch x3 w2", k_mul<4, 2>, 3, 2},
-    {"mul 2ch x3 w8", k_mul<2, 8>, 3, 8}, {"mul 3ch x3 w8", k_mul<3, 8>, 3, 8},
+    {"sq  2ch x1 w2", k_sq<2, 1, 2>, 1, 2}, {"sq  2ch x1 w3", k_sq<2, 1, 3>, 1, 3}, {"sq  2ch x1 w4", k_sq<2, 1, 4>, 1, 4},
+    {"sq  2ch x2 w2", k_sq<2, 2, 2>, 2, 2}, {"sq  2ch x2 w3", k_sq<2, 2, 3>, 2, 3}, {"sq  2ch x2 w4", k_sq<2, 2, 4>, 2, 4},
+    {"sq  2ch x4 w2", k_sq<2, 4, 2>, 4, 2}, {"sq  2ch x4 w3", k_sq<2, 4, 3>, 4, 3}, {"sq  2ch x4 w4", k_sq<2, 4, 4>, 4, 4},
+    {"sq  2ch x1 w8", k_sq<2, 1, 8>, 1, 8}, {"sq  2ch x4 w8", k_sq<2, 4, 8>, 4, 8},
+    {"mul 2ch x3 w2", k_mul<2, 2>, 3, 2}, {"mul 2ch x3 w3", k_mul<2, 3>, 3, 3}, {"mul 2ch x3 w4", k_mul<2, 4>, 3, 4},
+    {"mul 2ch x3 w8", k_mul<2, 8>, 3, 8},
+    {"sq  3ch x1 w2", k_sq<3, 1, 2>, 1, 2}, {"sq  3ch x1 w4", k_sq<3, 1, 4>, 1, 4},
+    {"mul 3ch x3 w2", k_mul<3, 2>, 3, 2}, {"mul 3ch x3 w3", k_mul<3, 3>, 3, 3},
   };
   for (auto& k : ks) {
     const int grid = cus * k.wps, lanes = grid * block;
