@@ -869,13 +869,27 @@ dropin_fatal( int err ) {
   abort();
 }
 
+/* The device path carries message sizes as 32-bit values.  The reference
+   takes any ulong size; a larger message must never be verified as its
+   truncated prefix (that would accept a signature over the prefix), so it
+   fails loudly like any other GPU failure. */
+static unsigned int
+dropin_msg_sz( unsigned long msg_sz ) {
+  if( msg_sz>(unsigned long)UINT32_MAX ) {
+    fprintf( stderr, "libfd_ed25519_hip: FATAL: message of %lu bytes exceeds the GPU path's %u-byte limit\n",
+             msg_sz, (unsigned)UINT32_MAX );
+    abort();
+  }
+  return (unsigned int)msg_sz;
+}
+
 int
 fd_ed25519_verify( unsigned char const msg[], unsigned long msg_sz, unsigned char const sig[ 64 ],
                    unsigned char const public_key[ 32 ], fd_sha512_t * sha ) {
   (void)sha;
+  unsigned int  sz  = dropin_msg_sz( msg_sz );
   fd_ed25519_hip_engine_t * e = default_get();
   unsigned long off = 0UL;
-  unsigned int  sz  = (unsigned int)msg_sz;
   signed char   out = 0;
   static unsigned char const empty[1] = {0};
   pthread_mutex_lock( &default_lock );
@@ -891,9 +905,9 @@ fd_ed25519_verify_batch_single_msg( unsigned char const msg[], unsigned long con
                                     fd_sha512_t * shas[ 1 ], unsigned char const batch_sz ) {
   (void)shas;
   if( batch_sz==0 || batch_sz>16 ) return FD_ED25519_ERR_SIG;
+  unsigned int  sz = dropin_msg_sz( msg_sz ), first = 0U, cnt = batch_sz;
   fd_ed25519_hip_engine_t * e = default_get();
   unsigned long off = 0UL;
-  unsigned int  sz = (unsigned int)msg_sz, first = 0U, cnt = batch_sz;
   signed char   out = 0;
   static unsigned char const empty[1] = {0};
   pthread_mutex_lock( &default_lock );

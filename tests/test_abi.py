@@ -60,6 +60,34 @@ def test_batch_size_guard_needs_no_gpu(lib):
     assert f(b"m", 1, b"\0" * 64 * 17, b"\0" * 32 * 17, None, 17) == -1
 
 
+@pytest.mark.parametrize("fn", ["fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg"])
+def test_dropin_refuses_messages_past_4gib(fn):
+    """The device path carries 32-bit message sizes; a larger msg_sz must
+    fail loudly (abort, before any device work) and never be verified as its
+    truncated prefix, which would accept a signature over the prefix."""
+    import subprocess
+    import sys
+    code = f"""
+import ctypes
+lib = ctypes.CDLL({LIB!r})
+buf = ctypes.create_string_buffer(64)
+sz = (1 << 32) + 5
+if {fn!r} == "fd_ed25519_verify":
+    f = lib.fd_ed25519_verify
+    f.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    f(buf, sz, buf, buf, None)
+else:
+    f = lib.fd_ed25519_verify_batch_single_msg
+    f.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ubyte]
+    f(buf, sz, buf, buf, None, 1)
+print("returned")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, HIP_VISIBLE_DEVICES=""))
+    assert r.returncode != 0 and "returned" not in r.stdout
+    assert "exceeds the GPU path's 4294967295-byte limit" in r.stderr, r.stderr
+
+
 def test_engine_status_strings(lib):
     lib.fd_ed25519_hip_strerror.restype = ctypes.c_char_p
     assert lib.fd_ed25519_hip_strerror(0) == b"ok"

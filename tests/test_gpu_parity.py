@@ -135,6 +135,21 @@ def test_every_message_size_vs_oracle(eng, oracle):
     _check(_run(eng, d), want)
 
 
+def test_long_messages_vs_oracle(eng, oracle):
+    """Messages past the Solana MTU (the drop-in takes any size): 1233 B ..
+    70 KB, the 2^16 boundary, and 1 MiB -- one lane hashes a whole message,
+    all of these in the sort's open-ended last bucket."""
+    big = [1233, 4096, 65535, 65536, 65537, 70000, 1 << 20]
+    d = _random_set(oracle, 64, seed=15, mutate=False,
+                    sizes=lambda i, rng: big[i] if i < len(big) else rng.randrange(1233, 70001))
+    sigs = d["sigs"].copy()
+    sigs[1::3, 5] ^= 1   # a third of them invalid (R corrupted)
+    d["sigs"] = sigs
+    want = oracle_many(oracle, d, 0)
+    assert (want == 0).sum() > 30 and (want != 0).sum() > 15
+    _check(_run(eng, d), want)
+
+
 def test_scalar_edges(eng, oracle):
     """S around L and all-ones; S+kL for small k."""
     d = _random_set(oracle, 64, seed=13, mutate=False)
