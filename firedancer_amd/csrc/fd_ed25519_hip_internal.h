@@ -39,7 +39,13 @@ extern "C" {
    reads 160 contiguous bytes of the lane's own table, so every fetched line
    is fully used (the [entry][quad][lane] layout fetched ~2.4x the table
    bytes from HBM because lanes pick different entries). */
-#define FD_ED25519_ATAB_BYTES_PER_WAVE (2UL * 9UL * 10UL * 64UL * 16UL)  /* -A and -+R tables */
+#ifndef FD_ED25519_SIGNED_TABS
+#define FD_ED25519_SIGNED_TABS 0
+#endif
+/* entries per lane table: [0..8], or [-8..8] (SIGNED_TABS: the negative
+   entries stored too, so a lookup needs no conditional negation) */
+#define FD_ED25519_ATAB_ENTRIES (FD_ED25519_SIGNED_TABS ? 17UL : 9UL)
+#define FD_ED25519_ATAB_BYTES_PER_WAVE (2UL * FD_ED25519_ATAB_ENTRIES * 10UL * 64UL * 16UL)  /* -A and -+R tables */
 
 #define FD_ED25519_VERIFY_BLOCK 256
 #define FD_ED25519_QUAD_LANE_BYTES 864UL   /* dsm4 lane tables: 2 x 9 entries x 48 B */
@@ -129,6 +135,9 @@ int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t
 #define FD_ED25519_PHASE_CNT    4
 int fd_ed25519_hip_launch_phase( fd_ed25519_verify_params_t const * p, int phase, uint32_t grid, void * stream );
 int fd_ed25519_hip_verify_occupancy( int * blocks_per_cu );
+/* lane-table bytes per dsm wave as compiled into the kernels (the host
+   sizes the atab scratch from this, never from its own copy of the macro) */
+unsigned long fd_ed25519_hip_atab_bytes_per_wave( void );
 
 /* Per-transaction combine with fd_ed25519_verify_batch_single_msg's
    priority (src/ballet/ed25519/fd_ed25519_user.c:231-309): the first

@@ -206,7 +206,18 @@ FD_DEV void table_store(int4* tab, int e, ge_cached c) {
   atab_store(tab, e, c);
 }
 
+/* the negated entry: Y+X and Y-X swapped, the T term negated */
 template <bool NT>
+FD_DEV void table_store2(int4* tab, int e, ge_cached c) {
+  if (NT) fe_neg(c.T2d, c.T2d);
+  atab_store(tab, 8 + e, c);
+  ge_cached n;
+  n.YplusX = c.YminusX; n.YminusX = c.YplusX; n.Z2 = c.Z2; fe_neg(n.T2d, c.T2d);
+  atab_store(tab, 8 - e, n);
+}
+
+/* SIGNED: [-8..8](sign P) at entries 0..16 (entry 8 the identity) */
+template <bool NT, bool SIGNED = false>
 FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
   ge_p3 P0;
   fe xn;
@@ -217,9 +228,10 @@ FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
   fe_mul(P0.T, P0.X, y);
   ge_cached c1, c;
   c.YplusX = P0.Z; c.YminusX = P0.Z; fe_add(c.Z2, P0.Z, P0.Z); fe_0(c.T2d);  /* identity */
-  atab_store(tab, 0, c);
+  atab_store(tab, SIGNED ? 8 : 0, c);
   ge_p3_to_cached(c1, P0);
-  table_store<NT>(tab, 1, c1);
+  if (SIGNED) table_store2<NT>(tab, 1, c1);
+  else table_store<NT>(tab, 1, c1);
   /* P0 is affine: the multiples by mixed additions (3 multiplications) */
   ge_precomp pre;
   pre.yplusx = c1.YplusX; pre.yminusx = c1.YminusX; pre.xy2d = c1.T2d;
@@ -230,7 +242,8 @@ FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
     ge_madd(sum, cur, pre);
     ge_p1p1_to_p3_uxyt(cur, sum);   /* Z centered: the next mixed addition doubles it */
     ge_p3_to_cached<true>(c, cur);
-    table_store<NT>(tab, e, c);
+    if (SIGNED) table_store2<NT>(tab, e, c);
+    else table_store<NT>(tab, e, c);
   }
 }
 
@@ -548,9 +561,9 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
   {
     fe x, y;
     load_pt(x, y, p, 0, j);
-    table_build<true>(tabA, x, y, true);
+    table_build<true, FD_ED25519_SIGNED_TABS>(tabA, x, y, true);
     load_pt(x, y, p, 1, j);
-    table_build<true>(tabR, x, y, !(hf & FD_HF_DNEG));
+    table_build<true, FD_ED25519_SIGNED_TABS>(tabR, x, y, !(hf & FD_HF_DNEG));
   }
   /* digits, most significant first, top-aligned in 160 bits: c, |d| in
      radix 16 (W signed digits, the top one in [0,8]), s_lo, s_hi in
@@ -584,7 +597,11 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     ge_cached ca, cr;
     const bool blo = FD_BW_LO_AT(it), bhi = FD_BW_HI_AT(it);
     ge_precomp b1, b2;
+#if FD_ED25519_SIGNED_TABS
+    atab_load(ca, tabA, ea + 8);
+#else
     atab_load(ca, tabA, ea < 0 ? -ea : ea);
+#endif
     if (it != W - 1) {
 #pragma clang loop unroll(disable)
       for (int dbl = 0; dbl < 4; dbl++) {
@@ -593,13 +610,19 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
       }
       ge_p1p1_to_p3_u(P, Rt);
     }
+#if FD_ED25519_SIGNED_TABS
+    atab_load(cr, tabR, er + 8);
+#else
     atab_load(cr, tabR, er < 0 ? -er : er);
     ge_cached_cneg(ca, ea < 0);
+#endif
     ge_add<true>(Rt, P, ca);
     ge_p1p1_to_p3_u(P, Rt);
     if (blo) btab16_load(b1, g_btab, (int)pop160u<FD_ED25519_BTABW_BITS>(ld));
     if (bhi) btab16_load(b2, g_btab2, (int)pop160u<FD_ED25519_BTABW_BITS>(hd));
+#if !FD_ED25519_SIGNED_TABS
     ge_cached_cneg(cr, er < 0);
+#endif
     ge_add<true>(Rt, P, cr);
     if (blo) {
       ge_p1p1_to_p3_uxyt(P, Rt);
@@ -694,8 +717,8 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + wave * FD_ED25519_ATAB_BYTES_PER_WAVE) +
-               lane * 180;
-  int4* tabR = tabA + 90;
+               lane * (2 * FD_ED25519_ATAB_ENTRIES * 10);
+  int4* tabR = tabA + FD_ED25519_ATAB_ENTRIES * 10;
   if (p.small) {
     /* after dsm4: the full-length items only, found by their flag (a
        static stride: the work counter is not reset for small chunks) */
@@ -1272,6 +1295,8 @@ extern "C" int fd_ed25519_hip_launch_verify(const fd_ed25519_verify_params_t* p,
   }
   return 0;
 }
+
+extern "C" unsigned long fd_ed25519_hip_atab_bytes_per_wave(void) { return FD_ED25519_ATAB_BYTES_PER_WAVE; }
 
 extern "C" int fd_ed25519_hip_verify_occupancy(int* blocks_per_cu) {
   return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fd_ed25519_dsm_kernel,

@@ -232,7 +232,7 @@ fd_ed25519_hip_engine_delete( fd_ed25519_hip_engine_t * engine ) {
 
 static size_t
 lane_atab_bytes( fd_ed25519_hip_engine_t const * e ) {
-  return (size_t)e->dsm_grid * (FD_ED25519_VERIFY_BLOCK / 64) * FD_ED25519_ATAB_BYTES_PER_WAVE;
+  return (size_t)e->dsm_grid * (FD_ED25519_VERIFY_BLOCK / 64) * fd_ed25519_hip_atab_bytes_per_wave();
 }
 
 /* a lane's scratch (dsm lane tables + work arrays for max_chunk
