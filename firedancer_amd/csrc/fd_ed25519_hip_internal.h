@@ -33,19 +33,18 @@ extern "C" {
 #define FD_ED25519_BTABW_ENTRIES  (1 << FD_ED25519_BTABW_BITS)
 #define FD_ED25519_BTABW_SHIFT    144   /* s_lo: 6 digits (bits 0..143), s_hi: 5 digits (109 bits) */
 
-/* Per-lane tables [0..8](-A) and [0..8](-+R) in cached form, in HBM: 2 x 9
+/* Per-lane tables [1..8](-A) and [1..8](-+R) in cached form, in HBM: 2 x 8
    entries x 40 int32 per lane, laid out [wave][lane][entry][quad] (int4
-   granules, lane stride 180 int4): a lookup
+   granules, lane stride 160 int4): a lookup
    reads 160 contiguous bytes of the lane's own table, so every fetched line
    is fully used (the [entry][quad][lane] layout fetched ~2.4x the table
-   bytes from HBM because lanes pick different entries). */
-#ifndef FD_ED25519_SIGNED_TABS
-#define FD_ED25519_SIGNED_TABS 0
-#endif
-/* entries per lane table: [0..8], or [-8..8] (SIGNED_TABS: the negative
-   entries stored too, so a lookup needs no conditional negation) */
-#define FD_ED25519_ATAB_ENTRIES (FD_ED25519_SIGNED_TABS ? 17UL : 9UL)
-#define FD_ED25519_ATAB_BYTES_PER_WAVE (2UL * FD_ED25519_ATAB_ENTRIES * 10UL * 64UL * 16UL)  /* -A and -+R tables */
+   bytes from HBM because lanes pick different entries).  A zero digit reads
+   one identity entry shared by all lanes (L2-resident) instead of a
+   per-lane copy: 1/9 less table written, dsm -1.2%
+   (profiles/r2_ab_atab_ident.txt).  The full-length form keeps [0..8] at
+   tabA, 9 entries, extending into the (then unused) tabR half. */
+#define FD_ED25519_ATAB_STRIDE 8UL
+#define FD_ED25519_ATAB_BYTES_PER_WAVE (2UL * FD_ED25519_ATAB_STRIDE * 10UL * 64UL * 16UL)  /* -A and -+R tables */
 
 #define FD_ED25519_VERIFY_BLOCK 256
 #define FD_ED25519_QUAD_LANE_BYTES 864UL   /* dsm4 lane tables: 2 x 9 entries x 48 B */

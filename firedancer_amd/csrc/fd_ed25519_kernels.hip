@@ -206,18 +206,23 @@ FD_DEV void table_store(int4* tab, int e, ge_cached c) {
   atab_store(tab, e, c);
 }
 
-/* the negated entry: Y+X and Y-X swapped, the T term negated */
-template <bool NT>
-FD_DEV void table_store2(int4* tab, int e, ge_cached c) {
-  if (NT) fe_neg(c.T2d, c.T2d);
-  atab_store(tab, 8 + e, c);
-  ge_cached n;
-  n.YplusX = c.YminusX; n.YminusX = c.YplusX; n.Z2 = c.Z2; fe_neg(n.T2d, c.T2d);
-  atab_store(tab, 8 - e, n);
+/* The cached identity (Y+X = Y-X = 1, 2Z = 2, T = 0) that a zero digit
+   reads from the half-size form's [1..8] lane tables: one 160-byte
+   entry shared by every lane, L2-resident. */
+__device__ const int4 fd_ident_cached[10] = {{1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 0}, {0, 0, 0, 0},
+                                             {2, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+
+/* the entry for digit e: [|e|] of the lane's table (IDENT: [1..8] at 0..7,
+   the shared identity for e == 0) */
+template <bool IDENT>
+FD_DEV const int4* tab_entry(const int4* tab, int e) {
+  const int a = e < 0 ? -e : e;
+  if (IDENT) return a == 0 ? fd_ident_cached : tab + (a - 1) * 10;
+  return tab + a * 10;
 }
 
-/* SIGNED: [-8..8](sign P) at entries 0..16 (entry 8 the identity) */
-template <bool NT, bool SIGNED = false>
+/* IDENT: [1..8] at entries 0..7, no identity entry */
+template <bool NT, bool IDENT = false>
 FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
   ge_p3 P0;
   fe xn;
@@ -227,11 +232,12 @@ FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
   fe_1(P0.Z);
   fe_mul(P0.T, P0.X, y);
   ge_cached c1, c;
-  c.YplusX = P0.Z; c.YminusX = P0.Z; fe_add(c.Z2, P0.Z, P0.Z); fe_0(c.T2d);  /* identity */
-  atab_store(tab, SIGNED ? 8 : 0, c);
+  if (!IDENT) {
+    c.YplusX = P0.Z; c.YminusX = P0.Z; fe_add(c.Z2, P0.Z, P0.Z); fe_0(c.T2d);  /* identity */
+    atab_store(tab, 0, c);
+  }
   ge_p3_to_cached(c1, P0);
-  if (SIGNED) table_store2<NT>(tab, 1, c1);
-  else table_store<NT>(tab, 1, c1);
+  table_store<NT>(tab, IDENT ? 0 : 1, c1);
   /* P0 is affine: the multiples by mixed additions (3 multiplications) */
   ge_precomp pre;
   pre.yplusx = c1.YplusX; pre.yminusx = c1.YminusX; pre.xy2d = c1.T2d;
@@ -242,8 +248,7 @@ FD_DEV void table_build(int4* tab, const fe& x, const fe& y, bool negate) {
     ge_madd(sum, cur, pre);
     ge_p1p1_to_p3_uxyt(cur, sum);   /* Z centered: the next mixed addition doubles it */
     ge_p3_to_cached<true>(c, cur);
-    if (SIGNED) table_store2<NT>(tab, e, c);
-    else table_store<NT>(tab, e, c);
+    table_store<NT>(tab, IDENT ? e - 1 : e, c);
   }
 }
 
@@ -545,7 +550,7 @@ static_assert(FD_BW_HI_N * FD_ED25519_BTABW_BITS >= 253 - FD_ED25519_BTABW_SHIFT
    signatures; then up to 38, the same W for the whole wave, the other
    lanes' top digits being 0): 4(W-1) = 128 doublings (against 252 for the
    reference's double-scalar form), W additions from each lane's
-   [0..8](-A) and [0..8](-+R) tables
+   [1..8](-A) and [1..8](-+R) tables (a zero digit adds the shared identity entry)
    (HBM, lane-contiguous 160-byte entries) and 6 + 5 mixed additions from
    the two unsigned radix-2^24 base tables [0..2^24)B and [0..2^24)B'
    (2 GiB each, HBM).  Every table entry is loaded
@@ -557,13 +562,13 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
   int code = precheck(p, j);
   const uint32_t hf = p.hflag[j];
 
-  /* lane tables: [0..8](-A) and [0..8](-sign(d) R) */
+  /* lane tables: [1..8](-A) and [1..8](-sign(d) R) */
   {
     fe x, y;
     load_pt(x, y, p, 0, j);
-    table_build<true, FD_ED25519_SIGNED_TABS>(tabA, x, y, true);
+    table_build<true, true>(tabA, x, y, true);
     load_pt(x, y, p, 1, j);
-    table_build<true, FD_ED25519_SIGNED_TABS>(tabR, x, y, !(hf & FD_HF_DNEG));
+    table_build<true, true>(tabR, x, y, !(hf & FD_HF_DNEG));
   }
   /* digits, most significant first, top-aligned in 160 bits: c, |d| in
      radix 16 (W signed digits, the top one in [0,8]), s_lo, s_hi in
@@ -597,11 +602,7 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     ge_cached ca, cr;
     const bool blo = FD_BW_LO_AT(it), bhi = FD_BW_HI_AT(it);
     ge_precomp b1, b2;
-#if FD_ED25519_SIGNED_TABS
-    atab_load(ca, tabA, ea + 8);
-#else
-    atab_load(ca, tabA, ea < 0 ? -ea : ea);
-#endif
+    atab_load(ca, tab_entry<true>(tabA, ea), 0);
     if (it != W - 1) {
 #pragma clang loop unroll(disable)
       for (int dbl = 0; dbl < 4; dbl++) {
@@ -610,19 +611,13 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
       }
       ge_p1p1_to_p3_u(P, Rt);
     }
-#if FD_ED25519_SIGNED_TABS
-    atab_load(cr, tabR, er + 8);
-#else
-    atab_load(cr, tabR, er < 0 ? -er : er);
+    atab_load(cr, tab_entry<true>(tabR, er), 0);
     ge_cached_cneg(ca, ea < 0);
-#endif
     ge_add<true>(Rt, P, ca);
     ge_p1p1_to_p3_u(P, Rt);
     if (blo) btab16_load(b1, g_btab, (int)pop160u<FD_ED25519_BTABW_BITS>(ld));
     if (bhi) btab16_load(b2, g_btab2, (int)pop160u<FD_ED25519_BTABW_BITS>(hd));
-#if !FD_ED25519_SIGNED_TABS
     ge_cached_cneg(cr, er < 0);
-#endif
     ge_add<true>(Rt, P, cr);
     if (blo) {
       ge_p1p1_to_p3_uxyt(P, Rt);
@@ -717,8 +712,8 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + wave * FD_ED25519_ATAB_BYTES_PER_WAVE) +
-               lane * (2 * FD_ED25519_ATAB_ENTRIES * 10);
-  int4* tabR = tabA + FD_ED25519_ATAB_ENTRIES * 10;
+               lane * (2 * FD_ED25519_ATAB_STRIDE * 10);
+  int4* tabR = tabA + FD_ED25519_ATAB_STRIDE * 10;   /* the full-length form uses tabA's 9 entries, into tabR's space */
   if (p.small) {
     /* after dsm4: the full-length items only, found by their flag (a
        static stride: the work counter is not reset for small chunks) */

@@ -13,7 +13,7 @@
      btab16 32769 x 32 int32          base-point table [0..2^15]B (full-length verify, 4.2 MB)
      btabw  2 x 2^24 x 32 int32       [0..2^24)B, [0..2^24)[2^144]B (half-size verify, 2 x 2 GiB,
                                       shared by the engines of a device)
-     atab   dsm waves x 184320 B      per-lane [0..8](-A), [0..8](-+R) tables
+     atab   dsm waves x 163840 B      per-lane [1..8](-A), [1..8](-+R) tables
      work   max_chunk x 280 B         k, flags, half-size scalars, decoded A and R, lists per signature
      in/out staging for the host API  grown on demand */
 
