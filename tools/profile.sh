@@ -11,7 +11,9 @@ TAG=${1:-prof}
 N=${2:-262144}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
-B="python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-txns 0 --host-reps 0"
+# one batch in flight: each kernel runs alone, so the trace durations are
+# comparable with the bench's per-phase HIP events
+B="python3 $R/bench.py --steps 3 --warmup 1 --inflight 1 --no-cpu-baseline --latency-txns 0 --host-reps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B \
   > $O/trace_bench.json 2> $O/trace.err || exit $?
 P="python3 $R/bench.py --n $N --steps 2 --warmup 0 --no-cpu-baseline --latency-txns 0 --host-reps 0"
