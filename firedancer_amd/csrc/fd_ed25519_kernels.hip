@@ -67,12 +67,46 @@ FD_DEV uint32_t nblk_bucket(uint32_t sz) {
   return b < (FD_ED25519_SORT_BUCKETS - 1) ? b : (FD_ED25519_SORT_BUCKETS - 1);
 }
 
+/* Each block sorts FD_SORT_PER_BLOCK signatures (FD_SORT_PER_THREAD per
+   lane), so a bucket's global counter takes one atomic per 4096 signatures
+   (one per 256 had the same-address atomics at the L2 serialize: ~49 us
+   per kernel at 1M).  Inside a wave, lanes of one bucket are counted
+   together (a ballot per distinct bucket, one LDS atomic by the first
+   such lane), and a lane's rank is its group's offset plus the lanes of
+   the group below it. */
+#define FD_SORT_PER_THREAD 16
+#define FD_SORT_PER_BLOCK (256 * FD_SORT_PER_THREAD)
+
+/* adds this lane's element (bucket b, if `valid`) to cnt[]; returns its rank
+   among the block's elements of that bucket */
+FD_DEV uint32_t sort_wave_count(uint32_t* cnt, uint32_t b, bool valid) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t active = __ballot(valid);
+  uint32_t r = 0;
+  while (active) {
+    const int lead = __ffsll((unsigned long long)active) - 1;
+    const uint32_t bl = (uint32_t)__shfl((int)b, lead);
+    const uint64_t grp = __ballot(valid && b == bl) & active;
+    uint32_t off = 0;
+    if ((int)lane == lead) off = atomicAdd(&cnt[bl], (uint32_t)__popcll(grp));
+    off = (uint32_t)__shfl((int)off, lead);
+    if ((grp >> lane) & 1ull) r = off + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
+    active &= ~grp;
+  }
+  return r;
+}
+
 __global__ void __launch_bounds__(256) fd_ed25519_sort_hist_kernel(fd_ed25519_verify_params_t p) {
   __shared__ uint32_t h[FD_ED25519_SORT_BUCKETS];
   if (threadIdx.x < FD_ED25519_SORT_BUCKETS) h[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < p.n) atomicAdd(&h[nblk_bucket(p.msg_sz[p.base + j])], 1u);
+  const uint64_t j0 = (uint64_t)blockIdx.x * FD_SORT_PER_BLOCK + threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < FD_SORT_PER_THREAD; e++) {
+    const uint64_t j = j0 + (uint64_t)e * 256u;
+    const bool v = j < p.n;
+    sort_wave_count(h, v ? nblk_bucket(p.msg_sz[p.base + j]) : 0u, v);
+  }
   __syncthreads();
   if (threadIdx.x < FD_ED25519_SORT_BUCKETS && h[threadIdx.x]) atomicAdd(&p.hist[threadIdx.x], h[threadIdx.x]);
 }
@@ -96,17 +130,24 @@ __global__ void __launch_bounds__(256) fd_ed25519_sort_scatter_kernel(fd_ed25519
   __shared__ uint32_t cnt[FD_ED25519_SORT_BUCKETS], base[FD_ED25519_SORT_BUCKETS];
   if (threadIdx.x < FD_ED25519_SORT_BUCKETS) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t b = 0, r = 0;
-  if (j < p.n) {
-    b = nblk_bucket(p.msg_sz[p.base + j]);
-    r = atomicAdd(&cnt[b], 1u);
+  const uint64_t j0 = (uint64_t)blockIdx.x * FD_SORT_PER_BLOCK + threadIdx.x;
+  uint32_t b[FD_SORT_PER_THREAD], r[FD_SORT_PER_THREAD];
+#pragma unroll
+  for (int e = 0; e < FD_SORT_PER_THREAD; e++) {
+    const uint64_t j = j0 + (uint64_t)e * 256u;
+    const bool v = j < p.n;
+    b[e] = v ? nblk_bucket(p.msg_sz[p.base + j]) : 0u;
+    r[e] = sort_wave_count(cnt, b[e], v);
   }
   __syncthreads();
   if (threadIdx.x < FD_ED25519_SORT_BUCKETS && cnt[threadIdx.x])
     base[threadIdx.x] = atomicAdd(&p.hist[FD_ED25519_SORT_BUCKETS + threadIdx.x], cnt[threadIdx.x]);
   __syncthreads();
-  if (j < p.n) p.perm[base[b] + r] = (uint32_t)j;
+#pragma unroll
+  for (int e = 0; e < FD_SORT_PER_THREAD; e++) {
+    const uint64_t j = j0 + (uint64_t)e * 256u;
+    if (j < p.n) p.perm[base[b[e]] + r[e]] = (uint32_t)j;
+  }
 }
 
 FD_DEV void hash_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
@@ -1240,9 +1281,10 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
     if (p->perm) {
       const hipError_t e = hipMemsetAsync(p->hist, 0, 2 * FD_ED25519_SORT_BUCKETS * sizeof(uint32_t), st);
       if (e != hipSuccess) return (int)e;
-      hipLaunchKernelGGL(fd_ed25519_sort_hist_kernel, g, dim3(blk), 0, st, *p);
+      const dim3 gs((uint32_t)((p->n + FD_SORT_PER_BLOCK - 1) / FD_SORT_PER_BLOCK));
+      hipLaunchKernelGGL(fd_ed25519_sort_hist_kernel, gs, dim3(blk), 0, st, *p);
       hipLaunchKernelGGL(fd_ed25519_sort_scan_kernel, dim3(1), dim3(64), 0, st, *p);
-      hipLaunchKernelGGL(fd_ed25519_sort_scatter_kernel, g, dim3(blk), 0, st, *p);
+      hipLaunchKernelGGL(fd_ed25519_sort_scatter_kernel, gs, dim3(blk), 0, st, *p);
     }
     hipLaunchKernelGGL(fd_ed25519_hash_kernel, g, dim3(blk), 0, st, *p);
   } break;
