@@ -166,7 +166,9 @@ FD_DEV uint32_t sha_chunk_dword(const uint4 (&c)[SHA_CHUNKS], int i) {
    previous block is compressed, so the load latency hides under 80 rounds. */
 /* Message schedule words of block b from its chunks (and, for the first
    block, the register prefix), with padding and the length in the last. */
-template <int NPRE, bool FIRST>
+/* FULL: every byte of the block is a message byte (blocks b + 2 < nblk), so
+   no padding masks and no length words. */
+template <int NPRE, bool FIRST, bool FULL = false>
 FD_DEV void sha_build_w(uint64_t (&w)[16], const uint4 (&c)[SHA_CHUNKS], const uint32_t (&pre)[NPRE],
                         const sha_msg_src& m, uint32_t b, uint32_t nblk, uint64_t bitlen) {
   constexpr int PB = 4 * NPRE;
@@ -178,13 +180,21 @@ FD_DEV void sha_build_w(uint64_t (&w)[16], const uint4 (&c)[SHA_CHUNKS], const u
     if (FIRST && t < PW) {
       d0 = pre[2 * t];
       d1 = pre[2 * t + 1];
+    } else if (FULL) {
+      /* realign and byte-swap in one v_perm_b32: byte k of the big-endian
+         word is byte shift + 3 - k of {hi, lo} */
+      const uint32_t sel = 0x00010203u + m.shift * 0x01010101u;
+      const uint32_t e0 = __builtin_amdgcn_perm(sha_chunk_dword(c, 2 * t + 1), sha_chunk_dword(c, 2 * t), sel);
+      const uint32_t e1 = __builtin_amdgcn_perm(sha_chunk_dword(c, 2 * t + 2), sha_chunk_dword(c, 2 * t + 1), sel);
+      w[t] = ((uint64_t)e0 << 32) | (uint64_t)e1;
+      continue;
     } else {
       const int p = p0 + 8 * t;
       d0 = sha_msg_dword(m, p, sha_chunk_dword(c, 2 * t), sha_chunk_dword(c, 2 * t + 1));
       d1 = sha_msg_dword(m, p + 4, sha_chunk_dword(c, 2 * t + 1), sha_chunk_dword(c, 2 * t + 2));
     }
     uint64_t word = ((uint64_t)bswap32(d0) << 32) | (uint64_t)bswap32(d1);
-    if (b + 1 == nblk) {
+    if (!FULL && b + 1 == nblk) {
       if (t == 14) word = 0;
       if (t == 15) word = bitlen;
     }
@@ -216,7 +226,8 @@ FD_DEV void sha512_pre(uint32_t (&out)[16], const uint32_t (&pre)[NPRE], const s
   if (nblk > 1) sha_load_block(cur, m, 32 - NPRE);
   sha512_block(h, w);
   for (uint32_t b = 1; b < nblk; b++) {
-    sha_build_w<NPRE, false>(w, cur, pre, m, b, nblk, bitlen);
+    if (b + 2 < nblk) sha_build_w<NPRE, false, true>(w, cur, pre, m, b, nblk, bitlen);
+    else sha_build_w<NPRE, false>(w, cur, pre, m, b, nblk, bitlen);
     if (b + 1 < nblk) sha_load_block(cur, m, 32 * (int)(b + 1) - NPRE);
     sha512_block(h, w);
   }
