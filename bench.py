@@ -432,8 +432,13 @@ def main():
     ap.add_argument("--host-slots", type=int, default=3,
                     help="3: each slot stream on its own hardware queue (4 measured 35% slower, tools/pool_first_probe.py)")
     ap.add_argument("--host-first", action="store_true", help="run the host-fed leg first (A/B)")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="batches in flight on the GPU (steps alternate between this many engines)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches in flight on the GPU (steps alternate between this many engines); "
+                         "0: 4 for C2-like configs, 2 for a strong-scaling stream (one call of many chunks, "
+                         "pipelined inside the engine)")
+    ap.add_argument("--one-stream", default="auto", choices=["auto", "0", "1"],
+                    help="engines of the timed steps keep to one stream (no decode side stream); "
+                         "auto: when 3 or more batches are in flight")
     ap.add_argument("--allow-shared-device", action="store_true",
                     help="let ranks share a GPU (one-GPU rehearsal of --gpus N; n_gpus then counts devices)")
     args = ap.parse_args()
@@ -481,9 +486,22 @@ def main():
     # previous step's dsm and fill its tail -- the last waves of a
     # persistent kernel whose items last ~1 ms -- as the pool's and the
     # verify tile's slots do.  Every step still verifies all n signatures.
-    engines = [eng] + [ed25519.Engine(device=device, max_chunk=min(n, 1 << 20), half=args.half)
-                       for _ in range(args.inflight - 1)]
-    outs = [wl.out] + [e.alloc(n) for e in engines[1:]]
+    # With 3+ in flight the batches overlap one another enough that each
+    # engine keeps to one stream (FD_ED25519_HIP_FLAG_ONE_STREAM, as the
+    # pool's slots do): 4 one-stream engines measured 107.7-108.7M/s against
+    # 104.9-105.5M/s for 2 engines with the decode side stream
+    # (profiles/r2_inflight_streams_ab.txt; extra streams share the process's
+    # 4 hardware queues).
+    inflight = args.inflight or (2 if strong else 4)
+    one_stream = inflight >= 3 if args.one_stream == "auto" else args.one_stream == "1"
+    if one_stream:
+        engines = [ed25519.Engine(device=device, max_chunk=min(n, 1 << 20), half=args.half, one_stream=True)
+                   for _ in range(inflight)]
+        outs = [e.alloc(n) for e in engines]
+    else:
+        engines = [eng] + [ed25519.Engine(device=device, max_chunk=min(n, 1 << 20), half=args.half)
+                           for _ in range(inflight - 1)]
+        outs = [wl.out] + [e.alloc(n) for e in engines[1:]]
 
     def step(s):
         e, o = engines[s % len(engines)], outs[s % len(engines)]
@@ -506,11 +524,14 @@ def main():
     barrier(world)
     elapsed = allreduce_max(t1 - t0, world)
     mism_inflight = 0
-    for o in outs[1:]:
+    for o in outs:
+        if o is wl.out:
+            continue
         mism_inflight += int((o.download(np.int8, n) != wl.expect.download(np.int8, n)).sum())
         o.free()
-    for e in engines[1:]:
-        e.close()
+    for e in engines:
+        if e is not eng:
+            e.close()
     # per-kernel durations: a separate pass of the same steps with HIP events
     # around each phase on the engine stream (the phases then run in sequence;
     # in the timed region above a chunk's decode overlaps its hash + scalar,
@@ -602,7 +623,8 @@ def main():
                                    + f", message size uniform [{cfg['lo']},{cfg['hi']}] B, {cfg['ppm'] / 1e4:.1f}% invalid",
                        "signatures_per_gpu": n, "parallelism": f"shard x{world} (independent batches, no collective)",
                        "devices": devices,
-                       "batches_in_flight": args.inflight,
+                       "batches_in_flight": inflight,
+                       "engine_streams": "one per engine" if one_stream else "two per engine (decode side stream)",
                        "codes": "reference AVX-512 backend"},
             "roofline": {"bound": "valu-int32", "kernel": "fd_ed25519_dsm_kernel",
                          "achieved": achieved, "peak": peak, "unit": "TOPS",
@@ -623,10 +645,9 @@ def main():
                          "signatures_per_launch": min(n, info["max_chunk"])},
             "kernel_ms_per_launch": per_launch,
             "kernel_timing": "HIP events around each phase on the engine stream, in a separate pass of the same "
-                             "steps on one engine (phases in sequence); in the timed region a chunk's decode "
-                             "runs on a side stream beside its hash + scalar, and consecutive steps alternate "
-                             "between config.batches_in_flight engines so a step's phases run beside the "
-                             "previous step's dsm",
+                             "steps on one engine (phases in sequence); in the timed region consecutive steps "
+                             "alternate between config.batches_in_flight engines (config.engine_streams), so "
+                             "a step's phases run beside the other steps' dsm",
             "cpu_baseline": cpu,
             "gpu_over_cpu": (value / cpu["value"]) if cpu else None,
             "host_fed": hf,

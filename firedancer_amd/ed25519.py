@@ -27,6 +27,7 @@ FLAG_HALF_STRICT = 2     # half-size |d| < 2^131 only (full-length form for the 
 FLAG_DSM_QUAD = 4        # dsm with a quad of lanes per signature at every chunk size
 FLAG_DSM_WIDE = 8        # dsm with one lane per signature at every chunk size
 FLAG_DSM_OCT = 16        # dsm with two quads of lanes per signature at every chunk size
+FLAG_ONE_STREAM = 32     # no decode side stream / second lane: for engines whose batches overlap one another
 
 # phases of a verify launch (FD_ED25519_HIP_PHASE_CNT, include/fd_ed25519_hip.h)
 PHASES = ("hash", "scalar", "decode", "dsm")
@@ -138,8 +139,9 @@ def _c(a, dtype):
 class Engine:
     """A libfd_ed25519_hip engine bound to one GPU."""
 
-    def __init__(self, device=0, max_chunk=0, codes="avx512", half="extended", dsm="auto"):
+    def __init__(self, device=0, max_chunk=0, codes="avx512", half="extended", dsm="auto", one_stream=False):
         flags = FLAG_CODES_PORTABLE if codes == "portable" else 0
+        flags |= FLAG_ONE_STREAM if one_stream else 0
         flags |= FLAG_HALF_STRICT if half == "strict" else 0
         flags |= {"auto": 0, "quad": FLAG_DSM_QUAD, "wide": FLAG_DSM_WIDE, "oct": FLAG_DSM_OCT}[dsm]
         self._h = _lib.fd_ed25519_hip_engine_new(int(device), int(max_chunk), flags)
