@@ -473,8 +473,22 @@ def main():
     gen_s = time.perf_counter() - t
     log(f"[rank {rank}] generated {n} signatures ({wl.msg_bytes / 1e6:.1f} MB of messages) in {gen_s:.2f} s")
 
+    inflight = args.inflight or (2 if strong else 4)
+    one_stream = inflight >= 3 if args.one_stream == "auto" else args.one_stream == "1"
     hf_first = None
-    if args.host_first and args.host_reps > 0:   # A/B: the host-fed leg before the engine's timed passes
+    if one_stream and args.host_reps > 0:
+        # The host-fed pool's 3 slot streams run at full rate only for some
+        # placements on the process's 4 hardware queues, which follow the
+        # streams created before it: after the main engine's two streams
+        # (the first large chunk creates its decode side stream) they do
+        # (69.8M/s, profiles/r2_pool_slots_queue_probe.txt), after the four
+        # one-stream engines of the timed steps they do not (47-57M/s,
+        # profiles/r2_host_fed_order_ab.txt).  So the leg runs first, after
+        # one warm verify on the main engine.
+        wl.verify()
+        eng.sync()
+        args.host_first = True
+    if args.host_first and args.host_reps > 0:   # the host-fed leg before the engine's timed passes
         try:
             hf_first = host_fed(wl, device, info, world, args.host_reps, args.host_batch, args.host_slots,
                                 args.host_copies)
@@ -492,8 +506,6 @@ def main():
     # 104.9-105.5M/s for 2 engines with the decode side stream
     # (profiles/r2_inflight_streams_ab.txt; extra streams share the process's
     # 4 hardware queues).
-    inflight = args.inflight or (2 if strong else 4)
-    one_stream = inflight >= 3 if args.one_stream == "auto" else args.one_stream == "1"
     if one_stream:
         engines = [ed25519.Engine(device=device, max_chunk=min(n, 1 << 20), half=args.half, one_stream=True)
                    for _ in range(inflight)]
