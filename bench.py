@@ -536,10 +536,12 @@ def main():
     barrier(world)
     elapsed = allreduce_max(t1 - t0, world)
     mism_inflight = 0
-    for o in outs:
+    used = {s % len(engines) for s in range(max(args.warmup, args.steps))}   # K or W below the depth: some idle
+    for i, o in enumerate(outs):
         if o is wl.out:
             continue
-        mism_inflight += int((o.download(np.int8, n) != wl.expect.download(np.int8, n)).sum())
+        if i in used:
+            mism_inflight += int((o.download(np.int8, n) != wl.expect.download(np.int8, n)).sum())
         o.free()
     for e in engines:
         if e is not eng:
