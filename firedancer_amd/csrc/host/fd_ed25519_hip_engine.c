@@ -180,6 +180,15 @@ btabw_acquire( int device, hipStream_t stream, int32_t * tab[2] ) {
   return rc;
 }
 
+unsigned long
+fd_ed25519_hip_shared_device_bytes( int device ) {
+  if( device<0 || device>=FD_ED25519_HIP_MAX_DEV ) return 0UL;
+  pthread_mutex_lock( &btabw_lock );
+  unsigned long b = btabw[device].refs ? 2UL*btabw_bytes() : 0UL;
+  pthread_mutex_unlock( &btabw_lock );
+  return b;
+}
+
 static void
 btabw_release( int device ) {
   pthread_mutex_lock( &btabw_lock );
@@ -230,9 +239,15 @@ fd_ed25519_hip_engine_delete( fd_ed25519_hip_engine_t * engine ) {
   engine_free( engine );
 }
 
+/* a lane's dsm scratch: the one-lane kernel's tables for every wave of
+   its grid, and room for the quad kernels' tables (4 x 864 B per
+   signature, dsm4 / dsm8) for every chunk size that takes them */
 static size_t
 lane_atab_bytes( fd_ed25519_hip_engine_t const * e ) {
-  return (size_t)e->dsm_grid * (FD_ED25519_VERIFY_BLOCK / 64) * fd_ed25519_hip_atab_bytes_per_wave();
+  size_t wide = (size_t)e->dsm_grid * (FD_ED25519_VERIFY_BLOCK / 64) * fd_ed25519_hip_atab_bytes_per_wave();
+  uint64_t qn = e->max_chunk < FD_ED25519_HIP_QUAD_MAX_DEFAULT ? e->max_chunk : FD_ED25519_HIP_QUAD_MAX_DEFAULT;
+  size_t quad = (size_t)qn * 4UL * FD_ED25519_QUAD_LANE_BYTES;
+  return wide > quad ? wide : quad;
 }
 
 /* a lane's scratch (dsm lane tables + work arrays for max_chunk
@@ -300,6 +315,12 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   if( bpc<1 ) bpc = 1;
   e->dsm_blocks_per_cu = bpc;
   e->dsm_grid = (uint32_t)(bpc * e->cu_cnt);
+  /* the dsm launch never uses more blocks than a chunk needs (one wave of
+     64 beyond it, fd_ed25519_hip_launch_phase): an engine of small chunks
+     (a tile's or a pipe's slot) sizes its grid, and so its lane tables, to
+     that -- ~14 MB instead of ~335 MB for a 4096-signature slot */
+  uint64_t need = (e->max_chunk + 64UL + FD_ED25519_VERIFY_BLOCK - 1UL) / FD_ED25519_VERIFY_BLOCK;
+  if( need < (uint64_t)e->dsm_grid ) e->dsm_grid = (uint32_t)need;
 
   size_t btab_sz = sizeof(int32_t) * FD_ED25519_BTAB_INTS;
   size_t btab16_sz = sizeof(int32_t) * (size_t)FD_ED25519_BTAB16_ENTRIES * FD_ED25519_BTAB16_STRIDE;
@@ -309,22 +330,24 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   e->device_bytes = btab_sz + btab16_sz;   /* + each lane's scratch; + the base tables shared per device */
   int lerr = lane_alloc( e, 0 );
   if( lerr ) return lerr;
-  char const * ovs = getenv( "FD_ED25519_HIP_OVERLAP" );
-  e->overlap = ovs ? ovs[0]=='1' : FD_ED25519_HIP_OVERLAP_DEFAULT;
-  char const * pls = getenv( "FD_ED25519_HIP_PIPELINE" );
-  e->pipeline = pls ? pls[0]=='1' : 1;
-  if( flags & FD_ED25519_HIP_FLAG_ONE_STREAM ) e->overlap = e->pipeline = 0;
+  /* launch forms come from the engine flags only, never the environment */
+  e->overlap  = !(flags & (FD_ED25519_HIP_FLAG_NO_OVERLAP  | FD_ED25519_HIP_FLAG_ONE_STREAM)) && FD_ED25519_HIP_OVERLAP_DEFAULT;
+  e->pipeline = !(flags & (FD_ED25519_HIP_FLAG_NO_PIPELINE | FD_ED25519_HIP_FLAG_ONE_STREAM));
   /* dsm4 (a quad of lanes per signature) below the size where one lane
      per signature fills the chip; its lane tables live in the atab scratch */
   uint64_t quad_cap = atab_sz / (4UL * FD_ED25519_QUAD_LANE_BYTES);
-  char const * qs = getenv( "FD_ED25519_HIP_QUAD_MAX" );
-  e->quad_max = qs ? strtoul( qs, NULL, 0 ) : FD_ED25519_HIP_QUAD_MAX_DEFAULT;
-  char const * os = getenv( "FD_ED25519_HIP_OCT_MAX" );
-  e->oct_max = os ? strtoul( os, NULL, 0 ) : FD_ED25519_HIP_OCT_MAX_DEFAULT;
+  e->quad_max = FD_ED25519_HIP_QUAD_MAX_DEFAULT;
+  e->oct_max  = FD_ED25519_HIP_OCT_MAX_DEFAULT;
   if( flags & FD_ED25519_HIP_FLAG_DSM_QUAD ) { e->quad_max = ~0UL; e->oct_max = 0UL; }
   if( flags & FD_ED25519_HIP_FLAG_DSM_OCT  ) { e->quad_max = ~0UL; e->oct_max = ~0UL; }
   if( flags & FD_ED25519_HIP_FLAG_DSM_WIDE ) e->quad_max = 0UL;
   if( e->quad_max > quad_cap ) e->quad_max = quad_cap;
+  /* a throughput engine pipelines its multi-chunk calls: the second lane
+     up front, so verify_dev never allocates (fd_ed25519_hip.h) */
+  if( e->pipeline && e->max_chunk > FD_ED25519_HIP_QUAD_MAX_DEFAULT ) {
+    lerr = lane_alloc( e, 1 );
+    if( lerr ) return lerr;
+  }
 
   int err = fd_ed25519_hip_launch_gen_btab( e->d_btab, e->stream );
   if( err ) return hip_fail( (hipError_t)err, "gen_btab launch" );
@@ -345,6 +368,18 @@ fd_ed25519_hip_engine_new( int device, unsigned long max_chunk, int flags ) {
   if( !e ) { snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "calloc failed" ); return NULL; }
   if( engine_init( e, device, max_chunk, flags ) ) { engine_free( e ); return NULL; }
   return e;
+}
+
+int
+fd_ed25519_hip_engine_set_forms( fd_ed25519_hip_engine_t * e, unsigned long quad_max, unsigned long oct_max ) {
+  if( !e || oct_max>quad_max ) return FD_ED25519_HIP_ERR_INVAL;
+  if( quad_max > lane_atab_bytes( e ) / (4UL * FD_ED25519_QUAD_LANE_BYTES) ) {
+    snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "set_forms: quad_max above the lane tables' room" );
+    return FD_ED25519_HIP_ERR_INVAL;
+  }
+  e->quad_max = quad_max;
+  e->oct_max  = oct_max;
+  return FD_ED25519_HIP_OK;
 }
 
 int

@@ -14,6 +14,18 @@
    runs more than depth frags ahead (the reference's fctl / fseq pair,
    reduced to one counter).
 
+   Liveness (fd_cnc's heartbeat / signal pair, src/tango/cnc/fd_cnc.h:63-65,
+   129-130, reduced to two words): each producer ticks a heartbeat word in
+   the header of the link it produces, and either side can mark the link
+   failed with a nonzero status.  A peer that sees the heartbeat stop
+   advancing for longer than its bound, or a failed status, knows the other
+   process is gone or gave up, instead of waiting on credits or frags that
+   will never come.
+
+   Zero-copy forms: prepare / commit let a producer write a payload straight
+   into the dcache (the verify tile's during_frag copies an incoming frag
+   there), peek / advance let a consumer read a frag in place.
+
    The two sides need not trust each other (the tile may be compromised):
    the geometry (depth, chunk count, MTU) is validated once at create /
    join and kept in the process-local handle; later writes to the shared
@@ -54,7 +66,9 @@ typedef struct {
   uint64_t         depth;       /* mcache lines, power of 2 */
   uint64_t         chunk_cnt;   /* dcache chunks */
   uint64_t         mtu;
-  uint64_t         pad0[4];
+  _Atomic uint64_t heartbeat;   /* producer's liveness tick (0: not started) */
+  _Atomic uint64_t status;      /* 0, or a failure code either side wrote     */
+  uint64_t         pad0[2];
   _Atomic uint64_t consumed;    /* consumer -> producer credits (own line) */
   uint64_t         pad1[7];
 } shlink_hdr_t;
@@ -69,6 +83,7 @@ struct fd_ed25519_hip_shlink {
      (consumer), and the producer's next dcache chunk */
   uint64_t        seq;
   uint64_t        chunk;
+  int             prepared;   /* producer: prepare() found a credit for seq */
   /* process-local geometry, validated at create / join */
   uint64_t        depth;
   uint64_t        chunk_cnt;
@@ -117,6 +132,8 @@ fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
   l->hdr->chunk_cnt = l->chunk_cnt = chunk_cnt;
   l->hdr->mtu       = l->mtu       = FD_ED25519_HIP_SHLINK_MTU;
   atomic_store_explicit( &l->hdr->consumed, 0UL, memory_order_relaxed );
+  atomic_store_explicit( &l->hdr->heartbeat, 0UL, memory_order_relaxed );
+  atomic_store_explicit( &l->hdr->status, 0UL, memory_order_relaxed );
   atomic_thread_fence( memory_order_release );
   l->hdr->magic = SHLINK_MAGIC;
   return l;
@@ -160,21 +177,30 @@ fd_ed25519_hip_shlink_depth( fd_ed25519_hip_shlink_t const * l ) {
   return l ? l->depth : 0UL;
 }
 
-int
-fd_ed25519_hip_shlink_publish( fd_ed25519_hip_shlink_t * l, unsigned char const * payload, unsigned long sz,
-                               unsigned long sig, unsigned int ctl ) {
-  shlink_hdr_t * h = l->hdr;
-  if( sz>l->mtu ) return FD_ED25519_HIP_ERR_INVAL;
-  uint64_t seq = l->seq;
+/* The payload room of the next frag if the consumer has returned a credit
+   for it, else NULL.  The room is MTU bytes inside this side's dcache; it
+   is reused for a later frag only after depth+1 more frags, so it is never
+   a region the consumer may still be reading. */
+unsigned char *
+fd_ed25519_hip_shlink_prepare( fd_ed25519_hip_shlink_t * l ) {
   /* a bogus credit count from the consumer only lets the producer overrun
-     that consumer: every write below stays inside the local geometry */
-  if( seq - atomic_load_explicit( &h->consumed, memory_order_acquire )>=l->depth ) return 1;   /* no credit */
+     that consumer: every write stays inside the local geometry */
+  if( l->seq - atomic_load_explicit( &l->hdr->consumed, memory_order_acquire )>=l->depth ) return NULL;
   uint64_t mtu_chunks = (l->mtu + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
   if( l->chunk + mtu_chunks>l->chunk_cnt ) l->chunk = 0UL;   /* compact wrap */
+  l->prepared = 1;
+  return l->dcache + l->chunk*SHLINK_CHUNK;
+}
+
+int
+fd_ed25519_hip_shlink_commit( fd_ed25519_hip_shlink_t * l, unsigned long sz, unsigned long sig, unsigned int ctl ) {
+  if( !l->prepared || sz>l->mtu ) return FD_ED25519_HIP_ERR_INVAL;
+  uint64_t seq = l->seq;
   shlink_meta_t * m = &l->mcache[ seq & (l->depth-1UL) ];
+  /* the payload is already in place: invalidate the line, then write the
+     metadata and publish seq (fd_mcache_publish's order) */
   atomic_store_explicit( &m->seq, seq-1UL, memory_order_relaxed );
   atomic_thread_fence( memory_order_release );
-  if( sz ) memcpy( l->dcache + l->chunk*SHLINK_CHUNK, payload, sz );
   m->sig    = sig;
   m->chunk  = (uint32_t)l->chunk;
   m->sz     = (uint16_t)sz;
@@ -182,32 +208,92 @@ fd_ed25519_hip_shlink_publish( fd_ed25519_hip_shlink_t * l, unsigned char const 
   m->tsorig = 0U;
   m->tspub  = 0U;
   atomic_store_explicit( &m->seq, seq, memory_order_release );
-  l->chunk += (sz + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
-  l->seq    = seq + 1UL;
+  l->chunk   += (sz + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
+  l->seq      = seq + 1UL;
+  l->prepared = 0;
   return 0;
+}
+
+int
+fd_ed25519_hip_shlink_publish( fd_ed25519_hip_shlink_t * l, unsigned char const * payload, unsigned long sz,
+                               unsigned long sig, unsigned int ctl ) {
+  if( sz>l->mtu ) return FD_ED25519_HIP_ERR_INVAL;
+  unsigned char * dst = fd_ed25519_hip_shlink_prepare( l );
+  if( !dst ) return 1;   /* no credit */
+  if( sz ) memcpy( dst, payload, sz );
+  return fd_ed25519_hip_shlink_commit( l, sz, sig, ctl );
+}
+
+/* The next frag in place: its payload address inside this side's dcache
+   (bounds checked against the local geometry, fd_verify.c:67), or NULL
+   with *err = 1 (none published yet) or -1 (overrun, or a line pointing
+   outside the dcache).  The bytes may be overwritten by a producer that
+   ignores credits; advance() tells whether they were. */
+unsigned char const *
+fd_ed25519_hip_shlink_peek( fd_ed25519_hip_shlink_t * l, unsigned long * sz, unsigned long * sig, unsigned int * ctl,
+                            int * err ) {
+  uint64_t seq = l->seq;
+  shlink_meta_t * m = &l->mcache[ seq & (l->depth-1UL) ];
+  uint64_t s0 = atomic_load_explicit( &m->seq, memory_order_acquire );
+  if( (int64_t)(s0 - seq)<0 ) { *err = 1; return NULL; }     /* not yet published */
+  if( s0!=seq ) { *err = -1; return NULL; }                   /* overrun */
+  unsigned long n     = m->sz;
+  unsigned long sg    = m->sig;
+  unsigned int  c     = m->ctl;
+  unsigned long chunk = m->chunk;
+  if( n>l->mtu || chunk>=l->chunk_cnt || chunk*SHLINK_CHUNK + n>l->chunk_cnt*SHLINK_CHUNK ) { *err = -1; return NULL; }
+  *sz = n; *sig = sg; *ctl = c; *err = 0;
+  return l->dcache + chunk*SHLINK_CHUNK;
+}
+
+/* Done with the peeked frag: 0 if it was intact while it was read, -1 if
+   the producer overran it meanwhile.  Either way the credit goes back. */
+int
+fd_ed25519_hip_shlink_advance( fd_ed25519_hip_shlink_t * l ) {
+  uint64_t seq = l->seq;
+  shlink_meta_t * m = &l->mcache[ seq & (l->depth-1UL) ];
+  atomic_thread_fence( memory_order_acquire );
+  int ok = atomic_load_explicit( &m->seq, memory_order_relaxed )==seq;
+  l->seq = seq + 1UL;
+  atomic_store_explicit( &l->hdr->consumed, l->seq, memory_order_release );
+  return ok ? 0 : -1;
 }
 
 int
 fd_ed25519_hip_shlink_consume( fd_ed25519_hip_shlink_t * l, unsigned char * payload, unsigned long * sz,
                                unsigned long * sig, unsigned int * ctl ) {
-  shlink_hdr_t * h = l->hdr;
-  uint64_t seq = l->seq;
-  shlink_meta_t * m = &l->mcache[ seq & (l->depth-1UL) ];
-  uint64_t s0 = atomic_load_explicit( &m->seq, memory_order_acquire );
-  if( (int64_t)(s0 - seq)<0 ) return 1;                      /* not yet published */
-  if( s0!=seq ) return -1;                                    /* overrun */
-  unsigned long n     = m->sz;
-  unsigned long sg    = m->sig;
-  unsigned int  c     = m->ctl;
-  unsigned long chunk = m->chunk;
-  /* the frag must lie inside this side's dcache and fit the caller's
-     FD_ED25519_HIP_SHLINK_MTU-byte buffer (fd_verify.c:67) */
-  if( n>l->mtu || chunk>=l->chunk_cnt || chunk*SHLINK_CHUNK + n>l->chunk_cnt*SHLINK_CHUNK ) return -1;
-  if( n ) memcpy( payload, l->dcache + chunk*SHLINK_CHUNK, n );
+  unsigned long n = 0UL, sg = 0UL;
+  unsigned int c = 0U;
+  int err;
+  unsigned char const * src = fd_ed25519_hip_shlink_peek( l, &n, &sg, &c, &err );
+  if( !src ) return err;
+  if( n ) memcpy( payload, src, n );
+  /* a frag overwritten during the copy is an overrun (never happens when
+     the producer honours credits) */
   atomic_thread_fence( memory_order_acquire );
-  if( atomic_load_explicit( &m->seq, memory_order_relaxed )!=s0 ) return -1;   /* overrun during the copy */
+  shlink_meta_t * m = &l->mcache[ l->seq & (l->depth-1UL) ];
+  if( atomic_load_explicit( &m->seq, memory_order_relaxed )!=l->seq ) return -1;
   *sz = n; *sig = sg; *ctl = c;
-  l->seq = seq + 1UL;
-  atomic_store_explicit( &h->consumed, l->seq, memory_order_release );
+  fd_ed25519_hip_shlink_advance( l );
   return 0;
+}
+
+void
+fd_ed25519_hip_shlink_heartbeat( fd_ed25519_hip_shlink_t * l, unsigned long now ) {
+  atomic_store_explicit( &l->hdr->heartbeat, now, memory_order_release );
+}
+
+unsigned long
+fd_ed25519_hip_shlink_heartbeat_query( fd_ed25519_hip_shlink_t const * l ) {
+  return atomic_load_explicit( &l->hdr->heartbeat, memory_order_acquire );
+}
+
+void
+fd_ed25519_hip_shlink_fail( fd_ed25519_hip_shlink_t * l, int code ) {
+  atomic_store_explicit( &l->hdr->status, (uint64_t)(int64_t)(code ? code : -1), memory_order_release );
+}
+
+int
+fd_ed25519_hip_shlink_status( fd_ed25519_hip_shlink_t const * l ) {
+  return (int)(int64_t)atomic_load_explicit( &l->hdr->status, memory_order_acquire );
 }

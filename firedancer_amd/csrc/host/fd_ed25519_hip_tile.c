@@ -81,6 +81,7 @@ typedef struct {
   unsigned long *           d_soff;    /* raw mode: per-signature message offset (device-made) */
   unsigned int *            d_ssz;     /* raw mode: per-signature message size             */
   unsigned char *           d_pok;     /* raw mode: fd_txn_parse accepted                  */
+  unsigned long             dev_bytes; /* the staging mirrors' device bytes                */
 } pipe_slot_t;
 
 struct fd_ed25519_hip_pipe {
@@ -90,6 +91,7 @@ struct fd_ed25519_hip_pipe {
   unsigned long next_poll;   /* ring index of the oldest submitted slot */
   unsigned long seq;
   unsigned      in_flight;
+  int           err;         /* sticky: a batch failed on the GPU (FD_ED25519_HIP_ERR_HIP - hipError_t) */
   pipe_slot_t   slot[ PIPE_SLOT_MAX ];
 };
 
@@ -153,6 +155,7 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   TCHK( hipMalloc( (void **)&s->d_soff, 8UL*sig_cap ), "hipMalloc" );
   TCHK( hipMalloc( (void **)&s->d_ssz,  4UL*sig_cap ), "hipMalloc" );
   TCHK( hipMalloc( (void **)&s->d_pok,  tc          ), "hipMalloc" );
+  s->dev_bytes = in_sz + out_sz + 12UL*sig_cap + tc;
   TCHK( hipEventCreateWithFlags( &s->ev, hipEventDisableTiming ), "hipEventCreate" );
   s->state = SLOT_FREE;
   return FD_ED25519_HIP_OK;
@@ -345,9 +348,13 @@ fd_ed25519_hip_pipe_poll( fd_ed25519_hip_pipe_t * pipe, int wait ) {
   hipError_t e = wait ? hipEventSynchronize( s->ev ) : hipEventQuery( s->ev );
   if( e==hipErrorNotReady ) return NULL;
   if( e!=hipSuccess ) {
-    /* a failed batch is unrecoverable for the pipe: report loudly */
-    fprintf( stderr, "libfd_ed25519_hip: FATAL: batch %lu failed on the GPU: %s\n", s->pub.seq, hipGetErrorString( e ) );
-    abort();
+    /* a failed batch is unrecoverable for the pipe: the error sticks (no
+       later batch is trusted either), the caller decides what to do
+       (the verify service marks its links failed and stops) */
+    char what[ 64 ];
+    snprintf( what, sizeof(what), "batch %lu failed on the GPU", s->pub.seq );
+    if( !pipe->err ) pipe->err = tile_fail( what, e );
+    return NULL;
   }
   s->pub.t_done = now_s();
   s->state = SLOT_DONE;
@@ -366,6 +373,22 @@ fd_ed25519_hip_pipe_release( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t
 unsigned
 fd_ed25519_hip_pipe_in_flight( fd_ed25519_hip_pipe_t const * pipe ) {
   return pipe->in_flight;
+}
+
+int
+fd_ed25519_hip_pipe_error( fd_ed25519_hip_pipe_t const * pipe ) {
+  return pipe->err;
+}
+
+unsigned long
+fd_ed25519_hip_pipe_device_bytes( fd_ed25519_hip_pipe_t const * pipe ) {
+  unsigned long b = 0UL;
+  for( unsigned i=0U; i<pipe->slot_cnt; i++ ) {
+    fd_ed25519_hip_info_t info;
+    if( !fd_ed25519_hip_engine_info( pipe->slot[i].eng, &info ) ) b += info.device_bytes;
+    b += pipe->slot[i].dev_bytes;
+  }
+  return b;
 }
 
 /* ======================================================================
@@ -532,6 +555,7 @@ struct fd_ed25519_hip_vtile {
   unsigned long             open_seq;   /* seq the open slot will get   */
   unsigned long             batch_sigs;
   int                       gpu_parse;  /* FD_ED25519_HIP_VTILE_GPU_PARSE: raw payloads to the device */
+  int                       err;        /* sticky failure: nothing more is staged or resolved */
   vrec_t *                  q;          /* circular FIFO of records */
   unsigned long             q_cap, q_head, q_cnt;
   unsigned long             resolved_head;  /* records [q_head, q_head+resolved_head) are resolved */
@@ -583,7 +607,11 @@ vq_push( fd_ed25519_hip_vtile_t * vt ) {
   if( vt->q_cnt==vt->q_cap ) {
     unsigned long ncap = 2UL*vt->q_cap;
     vrec_t * nq = (vrec_t *)malloc( ncap*sizeof(vrec_t) );
-    if( !nq ) { fprintf( stderr, "libfd_ed25519_hip: FATAL: vtile queue allocation failed\n" ); abort(); }
+    if( !nq ) {
+      fd_ed25519_hip_private_set_error( "vtile: queue allocation failed" );
+      vt->err = FD_ED25519_HIP_ERR_NOMEM;
+      return NULL;
+    }
     for( unsigned long k=0UL; k<vt->q_cnt; k++ ) nq[k] = *vq_at( vt, k );
     free( vt->q );
     vt->q = nq; vt->q_cap = ncap; vt->q_head = 0UL;
@@ -615,7 +643,11 @@ oa_reserve( fd_ed25519_hip_vtile_t * vt, unsigned long need ) {
   unsigned long ncap = 2UL*vt->oa_cap;
   while( ncap < 2UL*need ) ncap *= 2UL;
   unsigned char * n = (unsigned char *)malloc( ncap );
-  if( !n ) { fprintf( stderr, "libfd_ed25519_hip: FATAL: vtile arena allocation failed\n" ); abort(); }
+  if( !n ) {
+    fd_ed25519_hip_private_set_error( "vtile: arena allocation failed" );
+    vt->err = FD_ED25519_HIP_ERR_NOMEM;
+    return ~0UL;
+  }
   unsigned long pos = 0UL;
   for( unsigned long k=0UL; k<vt->q_cnt; k++ ) {
     vrec_t * r = vq_at( vt, k );
@@ -681,6 +713,7 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
                                                          (unsigned long)tr[14] );
       unsigned long toff = (psz + 1UL) & ~1UL;
       unsigned long aoff = oa_reserve( vt, toff + FD_ED25519_HIP_TXN_MAX_SZ + 2UL );
+      if( aoff==~0UL ) return;   /* vt->err is set: nothing more resolves */
       unsigned char * o = vt->oa + aoff;
       unsigned long fsz;
       if( foot<=64UL ) {
@@ -703,8 +736,12 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
 
 static int
 vt_drain_one( fd_ed25519_hip_vtile_t * vt, int wait ) {
+  if( vt->err ) return 0;
   fd_ed25519_hip_slot_t * s = fd_ed25519_hip_pipe_poll( vt->pipe, wait );
-  if( !s ) return 0;
+  if( !s ) {
+    if( fd_ed25519_hip_pipe_error( vt->pipe ) ) vt->err = fd_ed25519_hip_pipe_error( vt->pipe );
+    return 0;
+  }
   vt_resolve( vt, s );
   fd_ed25519_hip_pipe_release( vt->pipe, s );
   return 1;
@@ -716,24 +753,26 @@ vt_submit_open( fd_ed25519_hip_vtile_t * vt ) {
   if( !s || !s->txn_cnt ) return 0;
   int err = vt->gpu_parse ? fd_ed25519_hip_pipe_submit_txns( vt->pipe, s, s->txn_cnt, s->msg_bytes )
                           : fd_ed25519_hip_pipe_submit( vt->pipe, s, s->sig_cnt, s->msg_bytes, s->txn_cnt );
-  if( err ) {
-    fprintf( stderr, "libfd_ed25519_hip: FATAL: vtile submit failed: %s (%s)\n", fd_ed25519_hip_strerror( err ),
-             fd_ed25519_hip_last_error() );
-    abort();
+  if( err ) {   /* a launch failed: the batch's transactions have no verdicts, and the vtile stops */
+    vt->err = err;
+    return 0;
   }
   vt->open = NULL;
   return 1;
 }
 
-static void
+/* 0, or the vtile's sticky error (the open slot is then NULL) */
+static int
 vt_open( fd_ed25519_hip_vtile_t * vt ) {
-  if( vt->open ) return;
+  if( vt->err ) return vt->err;
+  if( vt->open ) return 0;
   for( ;; ) {
     vt->open = fd_ed25519_hip_pipe_acquire( vt->pipe );  /* counts start at 0 */
     if( vt->open ) break;
-    vt_drain_one( vt, 1 );  /* every slot in flight: wait for the oldest */
+    if( !vt_drain_one( vt, 1 ) && vt->err ) return vt->err;  /* every slot in flight: wait for the oldest */
   }
   vt->open_seq = vt->pipe->seq;
+  return 0;
 }
 
 /* GPU-parse mode: the payload goes to the device as is; the host reads
@@ -742,18 +781,20 @@ vt_open( fd_ed25519_hip_vtile_t * vt ) {
 static int
 vt_frag_raw( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
              unsigned long cookie ) {
+  if( vt->err ) return vt->err;
   if( !payload_sz || payload_sz>FD_ED25519_HIP_TXN_MTU ) {   /* fd_txn_parse rejects these before reading */
     vrec_t * r = vq_push( vt );
+    if( !r ) return vt->err;
     r->cookie = cookie; r->verdict = FD_ED25519_HIP_TXN_PARSE_FAILED; r->resolved = 1;
     vt_advance( vt );
     return 0;
   }
   unsigned long c = payload[0], nsig = (c>=1UL && c<=16UL) ? c : 0UL;
-  vt_open( vt );
+  if( vt_open( vt ) ) return vt->err;
   fd_ed25519_hip_slot_t * s = vt->open;
   if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap || s->msg_bytes+payload_sz>s->msg_cap ) ) {
     vt_submit_open( vt );
-    vt_open( vt );
+    if( vt_open( vt ) ) return vt->err;
     s = vt->open;
   }
   unsigned long ti = s->txn_cnt++;
@@ -763,6 +804,7 @@ vt_frag_raw( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigne
   s->msg_bytes += payload_sz;
   s->sig_cnt   += nsig;
   vrec_t * r = vq_push( vt );
+  if( !r ) return vt->err;
   r->cookie = cookie;
   if( payload_sz>=9UL ) memcpy( &r->tag, payload + 1, 8UL );
   r->slot_seq = vt->open_seq;
@@ -775,16 +817,18 @@ int
 fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
                            unsigned long cookie ) {
   if( vt->gpu_parse ) return vt_frag_raw( vt, payload, payload_sz, cookie );
+  if( vt->err ) return vt->err;
   /* during_frag + after_frag: the payload goes into the open batch whole
      (the published frag is built from it if the transaction succeeds) and
      the parse writes fd_txn_t's first 64 bytes into the batch's trailer
      slot */
   fd_ed25519_hip_txn_t t;
-  vt_open( vt );
+  if( vt_open( vt ) ) return vt->err;
   fd_ed25519_hip_slot_t * s = vt->open;
   unsigned long foot = fd_txn_core_parse( payload, payload_sz, &t, s->txn_trailer + 64UL*s->txn_cnt, 64UL );
   if( !foot ) {
     vrec_t * r = vq_push( vt );
+    if( !r ) return vt->err;
     r->cookie = cookie; r->verdict = FD_ED25519_HIP_TXN_PARSE_FAILED; r->resolved = 1;
     vt_advance( vt );
     return 0;
@@ -792,7 +836,7 @@ fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * pa
   unsigned long nsig = (t.signature_cnt>=1U && t.signature_cnt<=16U) ? t.signature_cnt : 0UL;
   if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap || s->msg_bytes+payload_sz>s->msg_cap ) ) {
     vt_submit_open( vt );
-    vt_open( vt );
+    if( vt_open( vt ) ) return vt->err;
     s = vt->open;
     fd_txn_core_parse( payload, payload_sz, &t, s->txn_trailer + 64UL*s->txn_cnt, 64UL );
   }
@@ -814,6 +858,7 @@ fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * pa
   s->txn_first  [ ti ] = (unsigned int)first;
   s->txn_sig_cnt[ ti ] = t.signature_cnt;   /* 17..127 -> ERR_SIG, no signatures staged */
   vrec_t * r = vq_push( vt );
+  if( !r ) return vt->err;
   r->cookie    = cookie;
   memcpy( &r->tag, payload + t.signature_off, 8UL );  /* ha_dedup_tag, fd_verify.h:65 */
   r->slot_seq = vt->open_seq;
@@ -871,6 +916,16 @@ fd_ed25519_hip_vtile_pending( fd_ed25519_hip_vtile_t const * vt ) {
   return vt->q_cnt;
 }
 
+int
+fd_ed25519_hip_vtile_error( fd_ed25519_hip_vtile_t const * vt ) {
+  return vt->err;
+}
+
+unsigned long
+fd_ed25519_hip_vtile_device_bytes( fd_ed25519_hip_vtile_t const * vt ) {
+  return fd_ed25519_hip_pipe_device_bytes( vt->pipe );
+}
+
 /* ======================================================================
    ring: a single-producer single-consumer tango-style mcache / dcache.
    The frag metadata is fd_frag_meta_t's layout (src/tango/fd_tango_base.h:
@@ -909,6 +964,7 @@ typedef struct {
   double                rate;
   double *              t_pub;
   _Atomic int           go;
+  _Atomic int           stop;       /* the consumer gave up (its vtile failed) */
   _Atomic uint64_t      consumed;   /* frags the consumer has taken (credits) */
   double                t0;
 } producer_t;
@@ -931,7 +987,9 @@ producer_main( void * arg ) {
     } else {
       due = now_s();
     }
-    while( i - atomic_load_explicit( &pr->consumed, memory_order_acquire ) >= rg->depth ) {}
+    while( i - atomic_load_explicit( &pr->consumed, memory_order_acquire ) >= rg->depth ) {
+      if( atomic_load_explicit( &pr->stop, memory_order_relaxed ) ) return NULL;
+    }
     unsigned long sz = pr->sz[ i ];
     unsigned long nch = (sz + RING_CHUNK - 1UL) / RING_CHUNK;
     if( chunk + RING_MTU_CHUNKS > rg->chunk_cnt ) chunk = 0UL;   /* compact wrap */
@@ -990,7 +1048,12 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
 
   unsigned long next = 0UL, done = 0UL, sigs = 0UL;
   unsigned long batches0 = 0UL;
+  int err = 0;
   while( done<txn_cnt ) {
+    if( (err = fd_ed25519_hip_vtile_error( vt )) ) {   /* the GPU failed: stop the producer, report */
+      atomic_store_explicit( &pr.stop, 1, memory_order_release );
+      break;
+    }
     /* pull every frag that is ready (after_frag) */
     int pulled = 0;
     while( next<txn_cnt ) {
@@ -1028,6 +1091,11 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
   }
   double t_end = now_s();
   pthread_join( th, NULL );
+  if( err ) {
+    free( rg.mcache ); free( rg.dcache ); free( t_pub ); free( ck ); free( vd ); free( buf );
+    fd_ed25519_hip_vtile_delete( vt );
+    return err;
+  }
   res->offered_txn_per_s  = offered_txn_per_s;
   res->seconds            = t_end - pr.t0;
   res->txn_cnt            = txn_cnt;
@@ -1126,15 +1194,28 @@ fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_c
 
 /* ======================================================================
    vservice: the GPU process behind a sandboxed verify tile (shlink in,
-   shlink out). */
+   shlink out).
 
-int
-fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
-                             fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
-                             fd_ed25519_hip_vservice_stats_t * stats ) {
+   Liveness and failure policy (the GPU side of fd_cnc's heartbeat,
+   src/tango/cnc/fd_cnc.h:63-65,129-130): every pass of the loop ticks the
+   heartbeat of `out` (the tile watches it and stops waiting when it goes
+   stale, integration/fd_verify_hip.c).  On a failure -- a batch the GPU did
+   not complete, a launch or allocation that failed, a tile that broke the
+   frag protocol or marked a link failed, a stop request from a sibling
+   link of the same service -- the service publishes nothing more, marks
+   both links failed with the code (fd_ed25519_hip_shlink_status) and
+   returns it; it never aborts the process mid-batch. */
+
+static int
+vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+               fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
+               fd_ed25519_hip_vservice_stats_t * stats, _Atomic int * stop ) {
   if( !in || !out ) return FD_ED25519_HIP_ERR_INVAL;
   fd_ed25519_hip_vtile_t * vt = fd_ed25519_hip_vtile_new( device, slot_cnt, batch_sigs, 16UL, 64UL, flags );
-  if( !vt ) return FD_ED25519_HIP_ERR_INVAL;
+  if( !vt ) {
+    fd_ed25519_hip_shlink_fail( in, FD_ED25519_HIP_ERR_INVAL ); fd_ed25519_hip_shlink_fail( out, FD_ED25519_HIP_ERR_INVAL );
+    return FD_ED25519_HIP_ERR_INVAL;
+  }
   enum { QMAX = 4096 };
   unsigned long   fbsz = QMAX * ((FD_ED25519_HIP_TPU_DCACHE_MTU + 63UL) & ~63UL);
   unsigned long * ck  = (unsigned long *)malloc( QMAX*sizeof(unsigned long) );
@@ -1143,39 +1224,44 @@ fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_
   signed char *   vd  = (signed char *)malloc( QMAX );
   unsigned char * fb  = (unsigned char *)malloc( fbsz );
   unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
-  if( !ck || !fo || !fs || !vd || !fb || !buf ) {
-    free( ck ); free( fo ); free( fs ); free( vd ); free( fb ); free( buf ); fd_ed25519_hip_vtile_delete( vt );
-    return FD_ED25519_HIP_ERR_NOMEM;
-  }
   double t0 = now_s();
-  unsigned long txns = 0UL, qn = 0UL, qi = 0UL;
+  unsigned long txns = 0UL, qn = 0UL, qi = 0UL, beat = 1UL;
   int eos = 0, rc = FD_ED25519_HIP_OK;
+  if( !ck || !fo || !fs || !vd || !fb || !buf ) { rc = FD_ED25519_HIP_ERR_NOMEM; goto fail; }
   for(;;) {
+    fd_ed25519_hip_shlink_heartbeat( out, beat++ );
+    if( stop && atomic_load_explicit( stop, memory_order_acquire ) ) { rc = FD_ED25519_HIP_SHLINK_FAIL_STOPPED; goto fail; }
+    int ts = fd_ed25519_hip_shlink_status( in );
+    if( !ts ) ts = fd_ed25519_hip_shlink_status( out );
+    if( ts ) { rc = ts; goto fail; }   /* the tile gave up on the link */
     /* verdicts already collected go out first, as far as credits allow:
        the verdict byte, then (SUCCESS) the frag the tile publishes */
     while( qi<qn ) {
-      buf[ 0 ] = (unsigned char)vd[ qi ];
-      if( fs[ qi ] ) memcpy( buf + 1, fb + fo[ qi ], fs[ qi ] );
-      int r = fd_ed25519_hip_shlink_publish( out, buf, 1UL + fs[ qi ], ck[ qi ], 0U );
-      if( r==1 ) break;
-      if( r ) { rc = r; goto done; }
+      unsigned char * dst = fd_ed25519_hip_shlink_prepare( out );
+      if( !dst ) break;
+      dst[ 0 ] = (unsigned char)vd[ qi ];
+      if( fs[ qi ] ) memcpy( dst + 1, fb + fo[ qi ], fs[ qi ] );
+      if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + fs[ qi ], ck[ qi ], 0U )) ) goto fail;
       qi++;
     }
     if( qi==qn ) {
       qi = qn = 0UL;
       qn = fd_ed25519_hip_vtile_poll_frags( vt, 0, QMAX, ck, vd, NULL, fo, fs, fb, fbsz );
     }
+    if( (rc = fd_ed25519_hip_vtile_error( vt )) ) goto fail;
     if( eos && !qn && !fd_ed25519_hip_vtile_pending( vt ) ) break;
-    /* after_frag for every frag that is ready */
+    /* after_frag for every frag that is ready (copied out of the shared
+       dcache first: the tile is not trusted not to change it meanwhile) */
     int pulled = 0;
     while( !eos ) {
       unsigned long sz = 0UL, sig = 0UL;
       unsigned int ctl = 0U;
       int r = fd_ed25519_hip_shlink_consume( in, buf, &sz, &sig, &ctl );
       if( r==1 ) break;
-      if( r ) { rc = FD_ED25519_HIP_ERR_INVAL; goto done; }   /* overrun: cannot happen with credits */
+      if( r ) { rc = FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL; goto fail; }   /* overrun: the tile ignored credits */
       if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { eos = 1; break; }
-      fd_ed25519_hip_vtile_frag( vt, buf, sz, sig );
+      r = fd_ed25519_hip_vtile_frag( vt, buf, sz, sig );
+      if( r<0 ) { rc = r; goto fail; }
       txns++;
       pulled = 1;
     }
@@ -1184,15 +1270,84 @@ fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_
         ( eos || slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<slot_cnt ) )
       fd_ed25519_hip_vtile_flush( vt, eos );
   }
-  while( fd_ed25519_hip_shlink_publish( out, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {}
+  while( fd_ed25519_hip_shlink_publish( out, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
+    fd_ed25519_hip_shlink_heartbeat( out, beat++ );
+    if( fd_ed25519_hip_shlink_status( in ) || fd_ed25519_hip_shlink_status( out ) ) break;
+  }
+  goto done;
+fail:
+  fd_ed25519_hip_shlink_fail( in, rc );
+  fd_ed25519_hip_shlink_fail( out, rc );
+  if( stop ) atomic_store_explicit( stop, 1, memory_order_release );
 done:
   if( stats ) {
-    stats->txn_cnt = txns;
-    stats->batches = vt->pipe->seq;
-    stats->seconds = now_s() - t0;
+    stats->txn_cnt      = txns;
+    stats->batches      = vt->pipe->seq;
+    stats->seconds      = now_s() - t0;
+    stats->device_bytes = fd_ed25519_hip_vtile_device_bytes( vt );
+    stats->shared_device_bytes = fd_ed25519_hip_shared_device_bytes( device );
   }
   free( ck ); free( fo ); free( fs ); free( vd ); free( fb ); free( buf );
   fd_ed25519_hip_vtile_delete( vt );
+  return rc;
+}
+
+int
+fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+                             fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
+                             fd_ed25519_hip_vservice_stats_t * stats ) {
+  return vservice_loop( device, slot_cnt, batch_sigs, flags, in, out, stats, NULL );
+}
+
+typedef struct {
+  int                              device, flags, rc;
+  unsigned                         slot_cnt;
+  unsigned long                    batch_sigs;
+  fd_ed25519_hip_shlink_t *        in;
+  fd_ed25519_hip_shlink_t *        out;
+  fd_ed25519_hip_vservice_stats_t  st;
+  _Atomic int *                    stop;
+} vservice_job_t;
+
+static void *
+vservice_main( void * arg ) {
+  vservice_job_t * j = (vservice_job_t *)arg;
+  j->rc = vservice_loop( j->device, j->slot_cnt, j->batch_sigs, j->flags, j->in, j->out, &j->st, j->stop );
+  return NULL;
+}
+
+int
+fd_ed25519_hip_vservice_run_links( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+                                   fd_ed25519_hip_shlink_t * const * in, fd_ed25519_hip_shlink_t * const * out,
+                                   unsigned link_cnt, fd_ed25519_hip_vservice_stats_t * stats ) {
+  if( !link_cnt || link_cnt>FD_ED25519_HIP_VSERVICE_LINK_MAX || !in || !out ) return FD_ED25519_HIP_ERR_INVAL;
+  vservice_job_t * job = (vservice_job_t *)calloc( link_cnt, sizeof(vservice_job_t) );
+  pthread_t *      th  = (pthread_t *)calloc( link_cnt, sizeof(pthread_t) );
+  if( !job || !th ) { free( job ); free( th ); return FD_ED25519_HIP_ERR_NOMEM; }
+  _Atomic int stop = 0;
+  unsigned started = 0U;
+  int rc = FD_ED25519_HIP_OK;
+  for( unsigned k=0U; k<link_cnt; k++ ) {
+    vservice_job_t * j = &job[ k ];
+    j->device = device; j->flags = flags; j->slot_cnt = slot_cnt; j->batch_sigs = batch_sigs;
+    j->in = in[ k ]; j->out = out[ k ]; j->stop = &stop;
+    if( pthread_create( &th[ k ], NULL, vservice_main, j ) ) {
+      rc = FD_ED25519_HIP_ERR_NOMEM;
+      atomic_store_explicit( &stop, 1, memory_order_release );
+      for( unsigned m=k; m<link_cnt; m++ ) {
+        fd_ed25519_hip_shlink_fail( in[ m ], rc ); fd_ed25519_hip_shlink_fail( out[ m ], rc );
+      }
+      break;
+    }
+    started++;
+  }
+  for( unsigned k=0U; k<started; k++ ) {
+    pthread_join( th[ k ], NULL );
+    /* the first real failure, not the siblings' stop that it caused */
+    if( job[ k ].rc && ( !rc || rc==FD_ED25519_HIP_SHLINK_FAIL_STOPPED ) ) rc = job[ k ].rc;
+    if( stats ) stats[ k ] = job[ k ].st;
+  }
+  free( job ); free( th );
   return rc;
 }
 

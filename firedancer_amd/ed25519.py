@@ -28,6 +28,8 @@ FLAG_DSM_QUAD = 4        # dsm with a quad of lanes per signature at every chunk
 FLAG_DSM_WIDE = 8        # dsm with one lane per signature at every chunk size
 FLAG_DSM_OCT = 16        # dsm with two quads of lanes per signature at every chunk size
 FLAG_ONE_STREAM = 32     # no decode side stream / second lane: for engines whose batches overlap one another
+FLAG_NO_OVERLAP = 64     # a large chunk's phases in sequence (no decode side stream): tests / A-B
+FLAG_NO_PIPELINE = 128   # a multi-chunk call on one set of work arrays (no second lane): tests / A-B
 
 # phases of a verify launch (FD_ED25519_HIP_PHASE_CNT, include/fd_ed25519_hip.h)
 PHASES = ("hash", "scalar", "decode", "dsm")
@@ -52,6 +54,7 @@ _lib.fd_ed25519_strerror.restype = ctypes.c_char_p
 _lib.fd_ed25519_hip_engine_new.argtypes = [ctypes.c_int, ctypes.c_ulong, ctypes.c_int]
 _lib.fd_ed25519_hip_engine_new.restype = ctypes.c_void_p
 _lib.fd_ed25519_hip_engine_delete.argtypes = [ctypes.c_void_p]
+_lib.fd_ed25519_hip_engine_set_forms.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_ulong]
 _lib.fd_ed25519_hip_engine_stream.argtypes = [ctypes.c_void_p]
 _lib.fd_ed25519_hip_engine_stream.restype = ctypes.c_void_p
 _lib.fd_ed25519_hip_engine_sync.argtypes = [ctypes.c_void_p]
@@ -139,15 +142,20 @@ def _c(a, dtype):
 class Engine:
     """A libfd_ed25519_hip engine bound to one GPU."""
 
-    def __init__(self, device=0, max_chunk=0, codes="avx512", half="extended", dsm="auto", one_stream=False):
+    def __init__(self, device=0, max_chunk=0, codes="avx512", half="extended", dsm="auto", one_stream=False,
+                 overlap=True, pipeline=True, forms=None):
         flags = FLAG_CODES_PORTABLE if codes == "portable" else 0
         flags |= FLAG_ONE_STREAM if one_stream else 0
+        flags |= 0 if overlap else FLAG_NO_OVERLAP
+        flags |= 0 if pipeline else FLAG_NO_PIPELINE
         flags |= FLAG_HALF_STRICT if half == "strict" else 0
         flags |= {"auto": 0, "quad": FLAG_DSM_QUAD, "wide": FLAG_DSM_WIDE, "oct": FLAG_DSM_OCT}[dsm]
         self._h = _lib.fd_ed25519_hip_engine_new(int(device), int(max_chunk), flags)
         if not self._h:
             raise HipError(f"engine_new failed: {_lib.fd_ed25519_hip_last_error().decode()}")
         self.codes = codes
+        if forms is not None:   # (quad_max, oct_max): fd_ed25519_hip_engine_set_forms
+            _check(_lib.fd_ed25519_hip_engine_set_forms(self._h, int(forms[0]), int(forms[1])))
 
     def close(self):
         if self._h:

@@ -526,7 +526,8 @@ PRODUCER_BIN = __import__("os").path.join(__import__("os").path.dirname(__import
 
 
 class VServiceStats(ctypes.Structure):
-    _fields_ = [("txn_cnt", ctypes.c_ulong), ("batches", ctypes.c_ulong), ("seconds", ctypes.c_double)]
+    _fields_ = [("txn_cnt", ctypes.c_ulong), ("batches", ctypes.c_ulong), ("seconds", ctypes.c_double),
+                ("device_bytes", ctypes.c_ulong), ("shared_device_bytes", ctypes.c_ulong)]
 
 
 _lib.fd_ed25519_hip_shlink_create.argtypes = [ctypes.c_char_p, ctypes.c_ulong]
@@ -543,6 +544,14 @@ _lib.fd_ed25519_hip_shlink_consume.argtypes = [_v, _v, ctypes.POINTER(ctypes.c_u
 _lib.fd_ed25519_hip_shlink_consume.restype = ctypes.c_int
 _lib.fd_ed25519_hip_vservice_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, ctypes.c_int, _v, _v,
                                              ctypes.POINTER(VServiceStats)]
+_lib.fd_ed25519_hip_shlink_heartbeat.argtypes = [_v, ctypes.c_ulong]
+_lib.fd_ed25519_hip_shlink_heartbeat_query.argtypes = [_v]
+_lib.fd_ed25519_hip_shlink_heartbeat_query.restype = ctypes.c_ulong
+_lib.fd_ed25519_hip_shlink_fail.argtypes = [_v, ctypes.c_int]
+_lib.fd_ed25519_hip_shlink_status.argtypes = [_v]
+_lib.fd_ed25519_hip_shlink_status.restype = ctypes.c_int
+SHLINK_FAIL_PROTOCOL = -100
+SHLINK_FAIL_STOPPED = -101
 
 
 class ShLink:
@@ -579,6 +588,19 @@ class ShLink:
         if r:
             raise HipError(r, "shlink overrun")
         return self._buf.raw[:sz.value], sig.value, ctl.value
+
+    def heartbeat(self, value):
+        """The producer's liveness tick (fd_ed25519_hip_shlink_heartbeat)."""
+        _lib.fd_ed25519_hip_shlink_heartbeat(self._h, int(value))
+
+    def heartbeat_query(self):
+        return _lib.fd_ed25519_hip_shlink_heartbeat_query(self._h)
+
+    def fail(self, code):
+        _lib.fd_ed25519_hip_shlink_fail(self._h, int(code))
+
+    def status(self):
+        return _lib.fd_ed25519_hip_shlink_status(self._h)
 
     def close(self, unlink=None):
         if self._h:

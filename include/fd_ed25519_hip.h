@@ -92,11 +92,12 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    ~1e-6 of random k.  Same verdicts either way; for tests and A/B. */
 #define FD_ED25519_HIP_FLAG_HALF_STRICT    (2)
 /* The dsm phase runs one signature per lane (throughput) or, for chunks of
-   at most FD_ED25519_HIP_QUAD_MAX_DEFAULT signatures ($FD_ED25519_HIP_QUAD_MAX),
+   at most FD_ED25519_HIP_QUAD_MAX_DEFAULT signatures,
    one per quad of lanes (latency: each group operation in one
    multiplication's time), and for at most FD_ED25519_HIP_OCT_MAX_DEFAULT
-   ($FD_ED25519_HIP_OCT_MAX) one per two quads (the two halves of the
-   multi-scalar sum in parallel).  These force one form (tests / A-B). */
+   one per two quads (the two halves of the multi-scalar sum in parallel)
+   (fd_ed25519_hip_engine_set_forms moves both thresholds).  These force
+   one form (tests / A-B). */
 #define FD_ED25519_HIP_FLAG_DSM_QUAD       (4)
 #define FD_ED25519_HIP_FLAG_DSM_WIDE       (8)
 #define FD_ED25519_HIP_FLAG_DSM_OCT        (16)
@@ -105,12 +106,19 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    pool's and the pipe's slots), where extra streams only crowd the
    device's few hardware queues. */
 #define FD_ED25519_HIP_FLAG_ONE_STREAM     (32)
+/* A large chunk's phases in sequence on the call's stream (no decode side
+   stream, below), and a call of several chunks on one set of work arrays
+   (no second lane, fd_ed25519_hip_verify_dev): same verdicts; A/B and
+   tests.  FLAG_ONE_STREAM implies both.  The library reads no environment
+   variable for its launch forms. */
+#define FD_ED25519_HIP_FLAG_NO_OVERLAP     (64)
+#define FD_ED25519_HIP_FLAG_NO_PIPELINE    (128)
 #define FD_ED25519_HIP_QUAD_MAX_DEFAULT    (32768UL)
 #define FD_ED25519_HIP_OCT_MAX_DEFAULT     (8192UL)
 /* Overlap: a large chunk's decode phase (A and R need neither the hash nor
    the scalars) runs on a side stream beside its hash and scalar phases, dsm
    after both: +1% at 1M, measured.  Per-phase timing runs the phases in
-   sequence.  ($FD_ED25519_HIP_OVERLAP=0/1 overrides.) */
+   sequence.  (FD_ED25519_HIP_FLAG_NO_OVERLAP turns it off.) */
 #define FD_ED25519_HIP_OVERLAP_DEFAULT     (1)
 
 /* Creates an engine on HIP device `device`.  max_chunk is the number of
@@ -122,6 +130,21 @@ fd_ed25519_hip_engine_new( int device, unsigned long max_chunk, int flags );
 
 void
 fd_ed25519_hip_engine_delete( fd_ed25519_hip_engine_t * engine );
+
+/* Moves the chunk sizes at which the engine switches from one quad of lanes
+   per signature (chunks of at most quad_max) and two quads (at most
+   oct_max) to one lane per signature.  FD_ED25519_HIP_ERR_INVAL if
+   oct_max > quad_max or quad_max exceeds what the engine's lane tables
+   hold.  For tests and tuning; the defaults are the measured crossovers. */
+/* Device memory this process shares between all its engines on `device`:
+   the half-size form's two base tables (2 x 2 GiB) while any engine holds
+   them, else 0.  An engine's own memory is fd_ed25519_hip_engine_info's
+   device_bytes. */
+unsigned long
+fd_ed25519_hip_shared_device_bytes( int device );
+
+int
+fd_ed25519_hip_engine_set_forms( fd_ed25519_hip_engine_t * engine, unsigned long quad_max, unsigned long oct_max );
 
 typedef struct {
   int           device;
@@ -158,8 +181,13 @@ fd_ed25519_hip_engine_stream( fd_ed25519_hip_engine_t * engine );
    work arrays on two streams (the second set, max_chunk x 280 B plus the
    dsm lane tables, allocated on the first such call), so a chunk's hash,
    scalar and decode phases fill the tail of the previous chunk's dsm; the
-   call still completes in order on `stream` ($FD_ED25519_HIP_PIPELINE=0 or
-   FD_ED25519_HIP_FLAG_ONE_STREAM keeps one set, per-phase timing too). */
+   call still completes in order on `stream` (FD_ED25519_HIP_FLAG_NO_PIPELINE
+   or FD_ED25519_HIP_FLAG_ONE_STREAM keeps one set, per-phase timing too).
+   An engine whose max_chunk exceeds FD_ED25519_HIP_QUAD_MAX_DEFAULT and that
+   may pipeline allocates the second set with the first, in engine_new, so
+   no call allocates device memory or fails for lack of it; a smaller
+   engine allocates it on its first multi-chunk call (one hipMalloc, which
+   may synchronise the device once). */
 int
 fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * engine,
                            unsigned long             n,

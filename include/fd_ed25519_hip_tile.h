@@ -129,6 +129,18 @@ fd_ed25519_hip_pipe_release( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t
 unsigned
 fd_ed25519_hip_pipe_in_flight( fd_ed25519_hip_pipe_t const * pipe );
 
+/* 0, or the sticky error of a batch that failed on the GPU
+   (FD_ED25519_HIP_ERR_HIP - hipError_t): poll then returns NULL for that
+   batch and every later one, and the pipe must be deleted. */
+int
+fd_ed25519_hip_pipe_error( fd_ed25519_hip_pipe_t const * pipe );
+
+/* Device memory the pipe holds: its slots' engines (lane tables sized to
+   the batch, work arrays, the full-length table) and staging mirrors; the
+   base tables shared by the process are fd_ed25519_hip_shared_device_bytes. */
+unsigned long
+fd_ed25519_hip_pipe_device_bytes( fd_ed25519_hip_pipe_t const * pipe );
+
 /* ---- txn -------------------------------------------------------------- */
 
 /* The fields of fd_txn_t (src/ballet/txn/fd_txn.h) the verify tile reads. */
@@ -227,7 +239,8 @@ fd_ed25519_hip_vtile_delete( fd_ed25519_hip_vtile_t * vt );
 /* after_frag for one transaction payload: parse and stage it (copying the
    payload into the open batch).  `cookie` comes back with its verdict.
    Returns 1 if staged, 0 if it was answered immediately (parse failure:
-   the verdict is queued for the next vtile_poll in order).  May submit the
+   the verdict is queued for the next vtile_poll in order), or the vtile's
+   sticky error (negative, see vtile_error; nothing staged).  May submit the
    open batch when it is full; blocks only if every slot is in flight. */
 int
 fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
@@ -260,6 +273,19 @@ fd_ed25519_hip_vtile_poll_frags( fd_ed25519_hip_vtile_t * vt, int wait, unsigned
 /* Transactions staged or in flight whose verdicts have not been polled. */
 unsigned long
 fd_ed25519_hip_vtile_pending( fd_ed25519_hip_vtile_t const * vt );
+
+/* 0, or the vtile's sticky failure: a batch failed on the GPU or could not
+   be launched (FD_ED25519_HIP_ERR_HIP - hipError_t, or an engine status),
+   or a host allocation failed (FD_ED25519_HIP_ERR_NOMEM).  The library never
+   aborts the process for these: the transactions in flight have no
+   verdicts, vtile_frag refuses new ones, and the caller stops (the verify
+   service marks its links failed, fd_ed25519_hip_vservice_run). */
+int
+fd_ed25519_hip_vtile_error( fd_ed25519_hip_vtile_t const * vt );
+
+/* Device memory the vtile holds (its pipe's, above). */
+unsigned long
+fd_ed25519_hip_vtile_device_bytes( fd_ed25519_hip_vtile_t const * vt );
 
 /* ---- ring + latency mode ------------------------------------------- */
 
@@ -345,6 +371,53 @@ int
 fd_ed25519_hip_shlink_consume( fd_ed25519_hip_shlink_t * link, unsigned char * payload, unsigned long * sz,
                                unsigned long * sig, unsigned int * ctl );
 
+/* Zero-copy producer: prepare returns the room (MTU bytes, inside the
+   dcache) for the next frag's payload if the consumer has returned a
+   credit for it, else NULL; the caller writes the payload there and
+   commit publishes it (FD_ED25519_HIP_ERR_INVAL without a successful
+   prepare, or sz above the MTU).  prepare may be repeated before commit
+   (it returns the same room). */
+unsigned char *
+fd_ed25519_hip_shlink_prepare( fd_ed25519_hip_shlink_t * link );
+
+int
+fd_ed25519_hip_shlink_commit( fd_ed25519_hip_shlink_t * link, unsigned long sz, unsigned long sig, unsigned int ctl );
+
+/* Zero-copy consumer: peek returns the next frag's payload in place
+   (bounds checked against this side's geometry) and its size, sig and ctl,
+   or NULL with *err = 1 (nothing published yet) or -1 (overrun / a line
+   pointing outside the dcache); advance then returns its credit and
+   reports 0 if the bytes were intact while they were read, -1 if the
+   producer overran them meanwhile. */
+unsigned char const *
+fd_ed25519_hip_shlink_peek( fd_ed25519_hip_shlink_t * link, unsigned long * sz, unsigned long * sig,
+                            unsigned int * ctl, int * err );
+
+int
+fd_ed25519_hip_shlink_advance( fd_ed25519_hip_shlink_t * link );
+
+/* Liveness (fd_cnc's heartbeat and signal, src/tango/cnc/fd_cnc.h:63-65,
+   129-130): the producer of a link ticks its heartbeat word (any value that
+   changes while it is alive; 0 means not started), either side may mark
+   the link failed with a nonzero code (FD_ED25519_HIP_ERR_* or
+   FD_ED25519_HIP_SHLINK_FAIL_*), status returns it (0: healthy).  A
+   consumer that sees the heartbeat unchanged for longer than its bound, or
+   a nonzero status, stops waiting on the link. */
+#define FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL (-100)   /* the peer broke the frag protocol */
+#define FD_ED25519_HIP_SHLINK_FAIL_STOPPED  (-101)   /* the service was told to stop      */
+
+void
+fd_ed25519_hip_shlink_heartbeat( fd_ed25519_hip_shlink_t * link, unsigned long now );
+
+unsigned long
+fd_ed25519_hip_shlink_heartbeat_query( fd_ed25519_hip_shlink_t const * link );
+
+void
+fd_ed25519_hip_shlink_fail( fd_ed25519_hip_shlink_t * link, int code );
+
+int
+fd_ed25519_hip_shlink_status( fd_ed25519_hip_shlink_t const * link );
+
 /* ctl bit of the last frag of a stream, both directions */
 #define FD_ED25519_HIP_SHLINK_CTL_EOS (1U)
 
@@ -352,6 +425,8 @@ typedef struct {
   unsigned long txn_cnt;
   unsigned long batches;
   double        seconds;
+  unsigned long device_bytes;   /* the link pair's own device memory (its vtile's) */
+  unsigned long shared_device_bytes;   /* the process's base tables on the device, shared by every pair */
 } fd_ed25519_hip_vservice_stats_t;
 
 /* The GPU side of a sandboxed verify tile: consumes transaction payload
@@ -368,6 +443,28 @@ int
 fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
                              fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
                              fd_ed25519_hip_vservice_stats_t * stats );
+
+/* One service process for several verify tiles of a GPU (the reference
+   runs verify_tile_count tiles, src/app/fdctl/config/default.toml:535):
+   link_cnt (1..FD_ED25519_HIP_VSERVICE_LINK_MAX) link pairs, each served as
+   by vservice_run on a thread of its own with its own vtile (engines,
+   streams, tcache), all sharing the device's base tables -- one copy of the
+   4 GiB per GPU instead of one per tile process.  Returns when every link
+   pair has ended (EOS), or on the first failure, which stops the others
+   (their links marked FD_ED25519_HIP_SHLINK_FAIL_STOPPED); stats[k] per
+   pair (optional).
+
+   Liveness and failure policy, both entry points: the service ticks the
+   heartbeat of each `out` link on every pass of its loop; on a GPU or
+   launch failure, an allocation failure, a tile that overran its own link
+   or marked a link failed, it stops publishing, marks both links failed
+   with the code and returns it (it never aborts the process). */
+#define FD_ED25519_HIP_VSERVICE_LINK_MAX (64U)
+
+int
+fd_ed25519_hip_vservice_run_links( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+                                   fd_ed25519_hip_shlink_t * const * in, fd_ed25519_hip_shlink_t * const * out,
+                                   unsigned link_cnt, fd_ed25519_hip_vservice_stats_t * stats );
 
 /* ---- pool ------------------------------------------------------------- */
 

@@ -1,0 +1,376 @@
+/* mux_harness.c -- TEST INFRASTRUCTURE ONLY (oracle/Makefile ref-mux).
+
+   Runs one verify tile -- the reference's own fd_tile_verify
+   (src/app/fdctl/run/tiles/fd_verify.c:230-244, compiled from its sources,
+   CPU verify) or the accelerated fd_tile_verify_hip
+   (integration/fd_verify_hip.c, GPU service behind shared-memory links) --
+   inside the reference's tile runtime, the way fd_topo_run_tile starts a
+   tile (src/disco/topo/fd_topo_run.c:56-180):
+
+     privileged_init -> the tile's own seccomp filter
+     (populate_allowed_seccomp) installed on the tile's thread ->
+     fd_metrics_register -> unprivileged_init -> fd_mux_tile (the
+     reference's run loop, src/disco/mux/fd_mux.c:90-710) with the tile's
+     mux_flags, burst and callbacks,
+
+   over a topology with the quic -> verify link (mcache + compact dcache of
+   FD_TPU_MTU frags, reliable, fseq flow control) and the verify -> dedup
+   link (FD_TPU_DCACHE_MTU frags).  round_robin_cnt verify tiles exist in
+   the topology; the one of kind id round_robin_idx runs.  A producer thread
+   publishes the payloads of a file into the in link with the reference's
+   fd_mcache_publish (sig = seq, at an optional rate); a consumer thread is
+   the dedup tile's side: it reads every published frag (sig, sz, bytes)
+   and returns credits through its fseq.
+
+     mux_harness verify|verify_hip PAYLOADS OUT [--app NAME] [--depth D]
+                 [--rr-cnt N] [--rr-idx I] [--no-sandbox] [--rate TXN_PER_S]
+                 [--timeout S]
+
+   PAYLOADS: u64 n, n x u32 sizes, the payloads.  OUT: every published frag
+   in order as u64 sig, u32 sz, sz bytes.  stdout: one JSON line of
+   counts.  The run ends when the tile has consumed every frag and has
+   nothing pending (fd_verify_hip_pending for the accelerated tile), the
+   consumer has drained the out link, and the tile has halted on its cnc;
+   the accelerated tile's txn link then carries the end-of-stream frag, so
+   the GPU service exits.  A tile that stops (FD_LOG_ERR inside the
+   sandbox) ends the process; exit status 3 on the harness's own timeout. */
+
+#define _GNU_SOURCE
+#include "disco/tiles.h"
+#include "disco/metrics/fd_metrics.h"
+#include "fd_ed25519_hip_tile.h"
+
+#include <linux/filter.h>
+#include <linux/seccomp.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/prctl.h>
+#include <time.h>
+#include <unistd.h>
+
+extern fd_topo_run_tile_t fd_tile_verify;
+extern fd_topo_run_tile_t fd_tile_verify_hip;
+ulong fd_verify_hip_pending( void const * ctx );
+fd_ed25519_hip_shlink_t * fd_verify_hip_txn_link( void * ctx );
+
+#define OUT_BURST (16UL)
+
+static double
+now_s( void ) {
+  struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (double)ts.tv_sec + 1e-9*(double)ts.tv_nsec;
+}
+
+/* bump allocator over the one region that serves as the workspace: the
+   tiles translate chunks relative to its base (fd_chunk_to_laddr) */
+static uchar * g_mem;
+static ulong   g_used, g_cap;
+
+static void *
+walloc( ulong align, ulong sz ) {
+  if( align<4096UL ) align = 4096UL;
+  ulong off = fd_ulong_align_up( g_used, align );
+  FD_TEST( off + sz<=g_cap );
+  g_used = off + sz;
+  return g_mem + off;
+}
+
+static ulong
+woff( void const * p ) {
+  return (ulong)((uchar const *)p - g_mem);
+}
+
+typedef struct {
+  /* input */
+  ulong            n;
+  uchar const *    pay;
+  ulong const *    off;
+  uint const *     sz;
+  double           rate;
+  /* links */
+  fd_frag_meta_t * in_mcache;   ulong in_depth;  uchar * in_dcache;  ulong * in_fseq;
+  fd_frag_meta_t * out_mcache;  ulong out_depth; uchar * out_dcache; ulong * out_fseq;
+  /* tile */
+  fd_topo_t *          topo;
+  fd_topo_tile_t *     tile;
+  fd_topo_run_tile_t * run;
+  void *               scratch;
+  void *               mux_scratch;
+  fd_cnc_t *           cnc;
+  int                  sandbox;
+  void *               ctx;
+  volatile int         tile_booted;
+  volatile int         tile_halted;
+  /* consumer output */
+  uchar *          res;
+  ulong            res_used, res_cap;
+  volatile ulong   res_cnt;
+  volatile ulong   out_seq;      /* next out seq the consumer expects */
+  volatile int     producer_done;
+  volatile int     stop;
+  volatile int     consumer_err;
+} harness_t;
+
+static void *
+producer_main( void * arg ) {
+  harness_t * h = (harness_t *)arg;
+  ulong chunk0 = fd_dcache_compact_chunk0( g_mem, h->in_dcache );
+  ulong wmark  = fd_dcache_compact_wmark ( g_mem, h->in_dcache, FD_TPU_MTU );
+  ulong chunk  = chunk0;
+  double t0 = now_s();
+  for( ulong seq=0UL; seq<h->n && !h->stop; seq++ ) {
+    if( h->rate>0.0 ) while( now_s() < t0 + (double)seq/h->rate ) FD_SPIN_PAUSE();
+    /* credits: never more than depth frags ahead of the tile's fseq */
+    while( fd_seq_diff( seq, fd_fseq_query( h->in_fseq ) )>=(long)h->in_depth ) { if( h->stop ) return NULL; FD_SPIN_PAUSE(); }
+    ulong sz = h->sz[ seq ];
+    fd_memcpy( fd_chunk_to_laddr( g_mem, chunk ), h->pay + h->off[ seq ], sz );
+    ulong ts = (ulong)fd_frag_meta_ts_comp( fd_tickcount() );
+    fd_mcache_publish( h->in_mcache, h->in_depth, seq, seq, chunk, sz, fd_frag_meta_ctl( 0UL, 1, 1, 0 ), ts, ts );
+    chunk = fd_dcache_compact_next( chunk, sz, chunk0, wmark );
+  }
+  h->producer_done = 1;
+  return NULL;
+}
+
+/* the dedup tile's side of the out link: every frag, in order */
+static void *
+consumer_main( void * arg ) {
+  harness_t * h = (harness_t *)arg;
+  ulong seq = 0UL;
+  while( !h->stop ) {
+    fd_frag_meta_t const * m = h->out_mcache + fd_mcache_line_idx( seq, h->out_depth );
+    ulong s0 = FD_VOLATILE_CONST( m->seq );
+    long d = fd_seq_diff( s0, seq );
+    if( d<0L ) { FD_SPIN_PAUSE(); continue; }
+    if( d>0L ) { h->consumer_err = 1; return NULL; }       /* overrun: the tile ignored our credits */
+    FD_COMPILER_MFENCE();
+    ulong sig = m->sig, chunk = m->chunk, sz = m->sz;
+    FD_COMPILER_MFENCE();
+    if( sz>FD_TPU_DCACHE_MTU || h->res_used + 12UL + sz>h->res_cap ) { h->consumer_err = 2; return NULL; }
+    uchar * r = h->res + h->res_used;
+    fd_memcpy( r, &sig, 8UL ); uint usz = (uint)sz; fd_memcpy( r+8, &usz, 4UL );
+    fd_memcpy( r+12, fd_chunk_to_laddr_const( g_mem, chunk ), sz );
+    FD_COMPILER_MFENCE();
+    if( FD_VOLATILE_CONST( m->seq )!=s0 ) { h->consumer_err = 3; return NULL; }
+    h->res_used += 12UL + sz;
+    h->res_cnt++;
+    seq++;
+    h->out_seq = seq;
+    fd_fseq_update( h->out_fseq, seq );
+  }
+  return NULL;
+}
+
+/* fd_topo_run_tile's sequence on this thread (src/disco/topo/fd_topo_run.c) */
+static void *
+tile_main( void * arg ) {
+  harness_t * h = (harness_t *)arg;
+  fd_log_cpu_set( NULL );
+  fd_log_thread_set( h->run==&fd_tile_verify ? "verify:ref" : "verify:hip" );
+  FD_LOG_NOTICE(( "booting tile" ));   /* as fd_topo_run_tile does: warms the logger (thread state, time zone) before the sandbox */
+
+  if( h->sandbox && h->run->populate_allowed_seccomp ) {
+    struct sock_filter filter[ 128 ];
+    ulong cnt = h->run->populate_allowed_seccomp( h->scratch, 128UL, filter );
+    struct sock_fprog prog = { .len = (ushort)cnt, .filter = filter };
+    /* this thread only (no TSYNC): the harness's other threads stay free to
+       write the result; the tile itself runs under exactly its policy */
+    if( prctl( PR_SET_NO_NEW_PRIVS, 1, 0, 0, 0 ) || prctl( PR_SET_SECCOMP, SECCOMP_MODE_FILTER, &prog ) )
+      FD_LOG_ERR(( "seccomp filter install failed" ));
+  }
+
+  fd_metrics_register( (ulong *)h->tile->metrics );
+  if( h->run->unprivileged_init ) h->run->unprivileged_init( h->topo, h->tile, h->scratch );
+
+  fd_mux_callbacks_t callbacks = {
+    .during_housekeeping = h->run->mux_during_housekeeping,
+    .before_credit       = h->run->mux_before_credit,
+    .after_credit        = h->run->mux_after_credit,
+    .before_frag         = h->run->mux_before_frag,
+    .during_frag         = h->run->mux_during_frag,
+    .after_frag          = h->run->mux_after_frag,
+    .metrics_write       = h->run->mux_metrics_write,
+  };
+  h->ctx = h->run->mux_ctx ? h->run->mux_ctx( h->scratch ) : NULL;
+  fd_frag_meta_t const * in_mcache[1] = { h->in_mcache };
+  ulong *                in_fseq[1]   = { h->in_fseq };
+  ulong *                out_fseq[1]  = { h->out_fseq };
+  fd_rng_t rng[1];
+  h->tile_booted = 1;
+  int ret = fd_mux_tile( h->cnc, h->run->mux_flags, 1UL, in_mcache, in_fseq, h->out_mcache, 1UL, out_fseq,
+                         h->run->burst, 0UL, 0L, fd_rng_join( fd_rng_new( rng, 0U, 0UL ) ), h->mux_scratch, h->ctx,
+                         &callbacks );
+  h->tile_halted = ret ? -1 : 1;
+  /* a sandboxed thread may not even exit: park until the process ends */
+  for(;;) FD_SPIN_PAUSE();
+  return NULL;
+}
+
+static void
+calibrate_ticks( void ) {
+  /* fd_tempo_tick_per_ns, measured before the sandbox (it sleeps) */
+  long t0 = fd_log_wallclock(); long k0 = fd_tickcount();
+  struct timespec ts = { 0, 50L*1000L*1000L }; nanosleep( &ts, NULL );
+  long t1 = fd_log_wallclock(); long k1 = fd_tickcount();
+  fd_tempo_set_tick_per_ns( (double)(k1-k0)/(double)(t1-t0), 0.0 );
+}
+
+int
+main( int argc, char ** argv ) {
+  fd_log_private_boot( &argc, &argv );
+  if( argc<4 ) FD_LOG_ERR(( "usage: %s verify|verify_hip PAYLOADS OUT [--app NAME] [--depth D] [--rr-cnt N] [--rr-idx I] "
+                            "[--no-sandbox] [--rate TXN_PER_S] [--timeout S]", argv[0] ));
+  harness_t * h = (harness_t *)calloc( 1, sizeof(harness_t) );
+  char const * kind = argv[1];
+  if(      !strcmp( kind, "verify"     ) ) h->run = &fd_tile_verify;
+  else if( !strcmp( kind, "verify_hip" ) ) h->run = &fd_tile_verify_hip;
+  else FD_LOG_ERR(( "unknown tile %s", kind ));
+  char const * app = "harness";
+  ulong depth = 4096UL, rr_cnt = 1UL, rr_idx = 0UL;
+  double timeout = 120.0;
+  h->sandbox = 1;
+  for( int i=4; i<argc; i++ ) {
+    char const * a = argv[i]; char const * v = i+1<argc ? argv[i+1] : NULL;
+    if(      !strcmp( a, "--app"     ) && v ) { app = v; i++; }
+    else if( !strcmp( a, "--depth"   ) && v ) { depth = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--rr-cnt"  ) && v ) { rr_cnt = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--rr-idx"  ) && v ) { rr_idx = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--rate"    ) && v ) { h->rate = strtod( v, NULL ); i++; }
+    else if( !strcmp( a, "--timeout" ) && v ) { timeout = strtod( v, NULL ); i++; }
+    else if( !strcmp( a, "--no-sandbox" ) ) h->sandbox = 0;
+    else FD_LOG_ERR(( "bad argument %s", a ));
+  }
+  FD_TEST( rr_cnt>=1UL && rr_idx<rr_cnt && rr_cnt<=16UL && fd_ulong_is_pow2( depth ) );
+
+  /* payloads */
+  FILE * f = fopen( argv[2], "rb" );
+  if( !f ) FD_LOG_ERR(( "cannot open %s", argv[2] ));
+  FD_TEST( fread( &h->n, 8UL, 1UL, f )==1UL );
+  uint *  sz  = (uint  *)malloc( 4UL*(h->n+1UL) );
+  ulong * off = (ulong *)malloc( 8UL*(h->n+1UL) );
+  FD_TEST( fread( sz, 4UL, h->n, f )==h->n );
+  ulong total = 0UL;
+  for( ulong i=0UL; i<h->n; i++ ) { off[i] = total; total += sz[i]; FD_TEST( sz[i]<=FD_TPU_MTU ); }
+  uchar * pay = (uchar *)malloc( total+1UL );
+  FD_TEST( fread( pay, 1UL, total, f )==total );
+  fclose( f );
+  h->pay = pay; h->off = off; h->sz = sz;
+
+  calibrate_ticks();
+
+  /* the workspace region and the objects in it */
+  ulong out_depth = depth;
+  ulong in_data  = fd_dcache_req_data_sz( FD_TPU_MTU,        depth,     1UL,       1 );
+  ulong out_data = fd_dcache_req_data_sz( FD_TPU_DCACHE_MTU, out_depth, OUT_BURST, 1 );
+  g_cap = 64UL*1024UL*1024UL + fd_dcache_footprint( in_data, 0UL ) + fd_dcache_footprint( out_data, 0UL ) +
+          fd_mcache_footprint( depth, 0UL ) + fd_mcache_footprint( out_depth, 0UL ) +
+          h->run->scratch_footprint( NULL ) + FD_MUX_TILE_SCRATCH_FOOTPRINT( 1UL, 1UL );
+  FD_TEST( !posix_memalign( (void **)&g_mem, 4096UL, g_cap ) );
+  fd_memset( g_mem, 0, g_cap );
+
+  h->in_depth   = depth;
+  h->in_mcache  = fd_mcache_join( fd_mcache_new( walloc( fd_mcache_align(), fd_mcache_footprint( depth, 0UL ) ), depth, 0UL, 0UL ) );
+  h->in_dcache  = fd_dcache_join( fd_dcache_new( walloc( fd_dcache_align(), fd_dcache_footprint( in_data, 0UL ) ), in_data, 0UL ) );
+  h->in_fseq    = fd_fseq_join( fd_fseq_new( walloc( fd_fseq_align(), fd_fseq_footprint() ), 0UL ) );
+  h->out_depth  = out_depth;
+  h->out_mcache = fd_mcache_join( fd_mcache_new( walloc( fd_mcache_align(), fd_mcache_footprint( out_depth, 0UL ) ), out_depth, 0UL, 0UL ) );
+  h->out_dcache = fd_dcache_join( fd_dcache_new( walloc( fd_dcache_align(), fd_dcache_footprint( out_data, 0UL ) ), out_data, 0UL ) );
+  h->out_fseq   = fd_fseq_join( fd_fseq_new( walloc( fd_fseq_align(), fd_fseq_footprint() ), 0UL ) );
+  h->cnc        = fd_cnc_join( fd_cnc_new( walloc( fd_cnc_align(), fd_cnc_footprint( 64UL ) ), 64UL, 0UL, fd_tickcount() ) );
+  ulong * metrics = fd_metrics_new( walloc( FD_METRICS_ALIGN, FD_METRICS_FOOTPRINT( 1UL, 1UL ) ), 1UL, 1UL );
+  h->scratch     = walloc( h->run->scratch_align(), h->run->scratch_footprint( NULL ) );
+  h->mux_scratch = walloc( FD_MUX_TILE_SCRATCH_ALIGN, FD_MUX_TILE_SCRATCH_FOOTPRINT( 1UL, 1UL ) );
+  FD_TEST( h->in_mcache && h->in_dcache && h->in_fseq && h->out_mcache && h->out_dcache && h->out_fseq && h->cnc );
+
+  /* the topology the tile's init reads */
+  fd_topo_t * topo = (fd_topo_t *)calloc( 1, sizeof(fd_topo_t) );
+  h->topo = topo;
+  FD_TEST( fd_cstr_printf_check( topo->app_name, sizeof(topo->app_name), NULL, "%s", app ) );
+  topo->wksp_cnt = 1UL;
+  topo->workspaces[0].id = 0UL;
+  strcpy( topo->workspaces[0].name, "harness" );
+  topo->workspaces[0].wksp = (fd_wksp_t *)g_mem;
+  void * objs[4] = { h->in_mcache, h->in_dcache, h->out_mcache, h->out_dcache };
+  for( ulong o=0UL; o<4UL; o++ ) {
+    topo->objs[o].id = o; topo->objs[o].wksp_id = 0UL; topo->objs[o].offset = woff( objs[o] );
+  }
+  topo->obj_cnt  = 4UL;
+  topo->link_cnt = 2UL;
+  fd_topo_link_t * lin = &topo->links[0];
+  lin->id = 0UL; strcpy( lin->name, "quic_verify" ); lin->depth = depth; lin->mtu = FD_TPU_MTU; lin->burst = 1UL;
+  lin->mcache_obj_id = 0UL; lin->dcache_obj_id = 1UL; lin->mcache = h->in_mcache; lin->dcache = h->in_dcache;
+  fd_topo_link_t * lout = &topo->links[1];
+  lout->id = 1UL; strcpy( lout->name, "verify_dedup" ); lout->depth = out_depth; lout->mtu = FD_TPU_DCACHE_MTU;
+  lout->burst = OUT_BURST; lout->mcache_obj_id = 2UL; lout->dcache_obj_id = 3UL;
+  lout->mcache = h->out_mcache; lout->dcache = h->out_dcache;
+  topo->tile_cnt = rr_cnt;
+  for( ulong k=0UL; k<rr_cnt; k++ ) {
+    fd_topo_tile_t * t = &topo->tiles[k];
+    t->id = k; strcpy( t->name, "verify" ); t->kind_id = k;
+    t->in_cnt = 1UL; t->in_link_id[0] = 0UL; t->in_link_reliable[0] = 1; t->in_link_poll[0] = 1;
+    t->out_link_id_primary = 1UL;
+    t->in_link_fseq[0] = h->in_fseq;
+    t->cnc = h->cnc; t->metrics = metrics;
+  }
+  h->tile = &topo->tiles[ rr_idx ];
+
+  h->res_cap = 64UL + h->n*(12UL + FD_TPU_DCACHE_MTU);
+  h->res     = (uchar *)malloc( h->res_cap );
+
+  /* privileged_init (maps the accelerated tile's links), then the threads */
+  if( h->run->privileged_init ) h->run->privileged_init( topo, h->tile, h->scratch );
+  double t_start = now_s();
+  pthread_t tt, tp, tc;
+  FD_TEST( !pthread_create( &tc, NULL, consumer_main, h ) );
+  FD_TEST( !pthread_create( &tt, NULL, tile_main, h ) );
+  while( fd_cnc_signal_query( h->cnc )!=FD_CNC_SIGNAL_RUN ) {
+    if( now_s() - t_start > timeout ) { printf( "{\"error\": \"tile did not boot\"}\n" ); fflush( stdout ); _exit( 3 ); }
+    FD_SPIN_PAUSE();
+  }
+  double t0 = now_s();
+  FD_TEST( !pthread_create( &tp, NULL, producer_main, h ) );
+
+  /* quiescence: every frag consumed by the tile, nothing pending inside it,
+     the consumer caught up with what was published */
+  int hip = h->run==&fd_tile_verify_hip;
+  for(;;) {
+    if( now_s() - t_start > timeout ) { printf( "{\"error\": \"timeout\", \"published\": %lu}\n", h->res_cnt ); fflush( stdout ); _exit( 3 ); }
+    if( h->consumer_err ) { printf( "{\"error\": \"consumer %d\"}\n", h->consumer_err ); fflush( stdout ); _exit( 4 ); }
+    if( !h->producer_done || fd_fseq_query( h->in_fseq )<h->n ) { FD_SPIN_PAUSE(); continue; }
+    if( hip && fd_verify_hip_pending( h->ctx ) ) { FD_SPIN_PAUSE(); continue; }
+    /* all of the tile's publishes happened before what was just read;
+       the consumer has them once the next line is still unpublished */
+    FD_COMPILER_MFENCE();
+    ulong seq = h->out_seq;
+    fd_frag_meta_t const * m = h->out_mcache + fd_mcache_line_idx( seq, h->out_depth );
+    if( fd_seq_diff( FD_VOLATILE_CONST( m->seq ), seq )>=0L ) { FD_SPIN_PAUSE(); continue; }
+    break;
+  }
+  double t1 = now_s();
+  fd_cnc_signal( h->cnc, FD_CNC_SIGNAL_HALT );
+  while( !h->tile_halted ) {
+    if( now_s() - t_start > timeout ) { printf( "{\"error\": \"halt timeout\"}\n" ); fflush( stdout ); _exit( 3 ); }
+    FD_SPIN_PAUSE();
+  }
+  h->stop = 1;
+  pthread_join( tc, NULL );
+  pthread_join( tp, NULL );
+  if( hip ) {   /* end the service's stream */
+    fd_ed25519_hip_shlink_t * txl = fd_verify_hip_txn_link( h->ctx );
+    while( fd_ed25519_hip_shlink_publish( txl, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
+      if( now_s() - t_start > timeout ) break;
+      FD_SPIN_PAUSE();
+    }
+  }
+
+  FILE * o = fopen( argv[3], "wb" );
+  FD_TEST( o && fwrite( h->res, 1UL, h->res_used, o )==h->res_used );
+  fclose( o );
+  printf( "{\"tile\": \"%s\", \"frags\": %lu, \"published\": %lu, \"seconds\": %.6f, \"txn_per_s\": %.1f, "
+          "\"rr_cnt\": %lu, \"rr_idx\": %lu, \"sandbox\": %d}\n",
+          kind, h->n, h->res_cnt, t1-t0, (double)h->n/(t1-t0), rr_cnt, rr_idx, h->sandbox );
+  fflush( stdout );
+  _exit( h->tile_halted==1 ? 0 : 5 );
+}

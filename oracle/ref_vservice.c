@@ -1,0 +1,182 @@
+/* ref_vservice.c -- TEST INFRASTRUCTURE ONLY (oracle/Makefile ref-mux).
+
+   A CPU stand-in for fd_verify_hip_service: the same links, names, frag
+   protocol, heartbeat and failure marking, but every verdict comes from
+   the reference's own code, compiled from its sources -- after_frag's
+   fd_txn_parse and trailer (src/app/fdctl/run/tiles/fd_verify.c:102-133)
+   and fd_txn_verify (src/app/fdctl/run/tiles/fd_verify.h:43-88: tcache
+   query, fd_ed25519_verify_batch_single_msg, tcache insert) with the
+   verify tile's tcache geometry.  It lets the accelerated tile's mux
+   integration (integration/fd_verify_hip.c) run in a container without a
+   GPU, and it plays the service that dies or fails for the liveness tests.
+
+     ref_vservice --prefix NAME --tiles K [--depth D]
+                  [--die-after N]    stop ticking and hang (SIGKILL-like) after N verdicts
+                  [--fail-after N]   mark every link failed after N verdicts and exit 2
+                  [--hold N]         answer in batches of N (verdicts held until N arrive or input idles)
+
+   Like the GPU service it keeps taking frags from the txn link whatever
+   the state of the verdict link (the protocol's one rule for a service:
+   the tile may wait for room in the txn link, so a service must never wait
+   on the tile before consuming); verdicts it cannot publish yet queue.
+
+   Prints "ready K" once the links exist; exits 0 after every tile's EOS. */
+
+#define _GNU_SOURCE
+#include "app/fdctl/run/tiles/fd_verify.h"
+#include "disco/quic/fd_tpu.h"
+#include "fd_ed25519_hip_tile.h"
+
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#define LINK_MAX (16UL)
+
+typedef struct {
+  fd_ed25519_hip_shlink_t * in;
+  fd_ed25519_hip_shlink_t * out;
+  fd_verify_ctx_t           vctx;   /* the reference tile's context: tcache + sha */
+  uchar *                   tcache_mem;
+  uchar                     sha_mem[ FD_TXN_ACTUAL_SIG_MAX ][ FD_SHA512_FOOTPRINT ] __attribute__((aligned(FD_SHA512_ALIGN)));
+  int                       eos, eos_sent;
+  /* verdict frags not yet published: [q_head, q_cnt); a batch of them is
+     released once `hold` are pending (--hold), input idles, or at the end */
+  uchar *                   q;
+  ulong *                   q_sz;
+  ulong *                   q_sig;
+  ulong                     q_cnt, q_head, q_cap, q_rel;
+} svc_link_t;
+
+/* after_frag + fd_txn_verify of one payload into out (verdict byte, then
+   the published frag for SUCCESS); returns the verdict frag's size */
+static ulong
+answer( svc_link_t * L, uchar const * payload, ulong payload_sz, uchar * out ) {
+  uchar * frag = out + 1;
+  if( payload_sz>FD_TPU_MTU ) { out[0] = (uchar)(schar)-3; return 1UL; }
+  fd_memset( frag, 0, FD_TPU_DCACHE_MTU );
+  fd_memcpy( frag, payload, payload_sz );
+  ulong txnt_off = fd_ulong_align_up( payload_sz, 2UL );
+  fd_txn_t * txn_t = (fd_txn_t *)( frag + txnt_off );
+  ulong txn_t_sz = fd_txn_parse( frag, payload_sz, txn_t, NULL );
+  if( !txn_t_sz ) { out[0] = (uchar)(schar)-3; return 1UL; }            /* fd_verify.c:118-121 */
+  ushort * payload_sz_p = (ushort *)( (ulong)txn_t + txn_t_sz );
+  *payload_sz_p = (ushort)payload_sz;
+  ulong new_sz = ( (ulong)payload_sz_p + sizeof(ushort) ) - (ulong)frag;
+  ulong txn_sig;
+  int res = fd_txn_verify( &L->vctx, frag, (ushort)payload_sz, txn_t, &txn_sig );
+  if( res!=FD_TXN_VERIFY_SUCCESS ) { out[0] = (uchar)(schar)res; return 1UL; }
+  out[0] = 0;
+  return 1UL + new_sz;
+}
+
+int
+main( int argc, char ** argv ) {
+  fd_log_private_boot( &argc, &argv );
+  char const * prefix = NULL;
+  ulong tiles = 0UL, depth = 16384UL, die_after = ~0UL, fail_after = ~0UL, hold = 1UL;
+  for( int i=1; i<argc; i++ ) {
+    char const * a = argv[i]; char const * v = i+1<argc ? argv[i+1] : NULL;
+    if(      !strcmp( a, "--prefix"     ) && v ) { prefix = v; i++; }
+    else if( !strcmp( a, "--tiles"      ) && v ) { tiles = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--depth"      ) && v ) { depth = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--die-after"  ) && v ) { die_after = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--fail-after" ) && v ) { fail_after = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--hold"       ) && v ) { hold = strtoul( v, NULL, 0 ); i++; }
+    else FD_LOG_ERR(( "bad argument %s", a ));
+  }
+  FD_TEST( prefix && tiles>=1UL && tiles<=LINK_MAX && hold>=1UL );
+
+  svc_link_t * L = (svc_link_t *)aligned_alloc( 128UL, LINK_MAX*sizeof(svc_link_t) );
+  fd_memset( L, 0, LINK_MAX*sizeof(svc_link_t) );
+  ulong frag_max = 1UL + FD_TPU_DCACHE_MTU;
+  for( ulong k=0UL; k<tiles; k++ ) {
+    char name[ 160 ];
+    snprintf( name, sizeof(name), "%s%lu_txn", prefix, k );
+    L[k].in = fd_ed25519_hip_shlink_create( name, depth );
+    snprintf( name, sizeof(name), "%s%lu_vd", prefix, k );
+    L[k].out = fd_ed25519_hip_shlink_create( name, depth );
+    if( !L[k].in || !L[k].out ) FD_LOG_ERR(( "cannot create the links of tile %lu (%s*)", k, prefix ));
+    /* the reference tile's dedup state, as unprivileged_init builds it (fd_verify.c:161-179) */
+    L[k].tcache_mem = aligned_alloc( FD_TCACHE_ALIGN, FD_TCACHE_FOOTPRINT( VERIFY_TCACHE_DEPTH, VERIFY_TCACHE_MAP_CNT ) );
+    fd_tcache_t * tcache = fd_tcache_join( fd_tcache_new( L[k].tcache_mem, VERIFY_TCACHE_DEPTH, VERIFY_TCACHE_MAP_CNT ) );
+    FD_TEST( tcache );
+    for( ulong i=0UL; i<FD_TXN_ACTUAL_SIG_MAX; i++ ) L[k].vctx.sha[i] = fd_sha512_join( fd_sha512_new( L[k].sha_mem[i] ) );
+    L[k].vctx.tcache_depth   = fd_tcache_depth       ( tcache );
+    L[k].vctx.tcache_map_cnt = fd_tcache_map_cnt     ( tcache );
+    L[k].vctx.tcache_sync    = fd_tcache_oldest_laddr( tcache );
+    L[k].vctx.tcache_ring    = fd_tcache_ring_laddr  ( tcache );
+    L[k].vctx.tcache_map     = fd_tcache_map_laddr   ( tcache );
+    L[k].q_cap = 1024UL;
+    L[k].q     = (uchar *)malloc( L[k].q_cap*frag_max );
+    L[k].q_sz  = (ulong *)malloc( L[k].q_cap*sizeof(ulong) );
+    L[k].q_sig = (ulong *)malloc( L[k].q_cap*sizeof(ulong) );
+  }
+  printf( "ready %lu\n", tiles );
+  fflush( stdout );
+
+  uchar * buf = (uchar *)malloc( FD_ED25519_HIP_SHLINK_MTU );
+  ulong answered = 0UL, beat = 1UL, idle = 0UL;
+  for(;;) {
+    ulong done = 0UL;
+    int progress = 0;
+    for( ulong k=0UL; k<tiles; k++ ) {
+      svc_link_t * S = &L[k];
+      fd_ed25519_hip_shlink_heartbeat( S->out, beat );
+      if( fd_ed25519_hip_shlink_status( S->in ) ) FD_LOG_ERR(( "tile %lu marked its link failed", k ));
+      if( S->eos_sent ) { done++; continue; }
+      /* release the held verdicts when `hold` are pending, at the end, or when input idles */
+      if( S->q_cnt - S->q_rel>=hold || S->eos || idle>64UL ) S->q_rel = S->q_cnt;
+      while( S->q_head<S->q_rel ) {
+        if( fd_ed25519_hip_shlink_publish( S->out, S->q + S->q_head*frag_max, S->q_sz[ S->q_head ], S->q_sig[ S->q_head ], 0U ) ) break;
+        S->q_head++;
+        answered++;
+        progress = 1;
+        if( answered==fail_after ) {
+          for( ulong m=0UL; m<tiles; m++ ) { fd_ed25519_hip_shlink_fail( L[m].in, FD_ED25519_HIP_ERR_HIP - 700 ); fd_ed25519_hip_shlink_fail( L[m].out, FD_ED25519_HIP_ERR_HIP - 700 ); }
+          FD_LOG_WARNING(( "stand-in: marked every link failed after %lu verdicts", answered ));
+          for( ulong m=0UL; m<tiles; m++ ) { fd_ed25519_hip_shlink_leave( L[m].in, 1 ); fd_ed25519_hip_shlink_leave( L[m].out, 1 ); }
+          return 2;
+        }
+        if( answered==die_after ) {
+          FD_LOG_WARNING(( "stand-in: stopping dead after %lu verdicts", answered ));
+          raise( SIGKILL );
+        }
+      }
+      if( S->q_head==S->q_cnt ) S->q_head = S->q_cnt = S->q_rel = 0UL;
+      if( S->eos && !S->q_cnt ) {
+        if( !fd_ed25519_hip_shlink_publish( S->out, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS ) ) S->eos_sent = 1;
+        continue;
+      }
+      while( !S->eos ) {
+        ulong sz = 0UL, sig = 0UL; uint ctl = 0U;
+        int r = fd_ed25519_hip_shlink_consume( S->in, buf, &sz, &sig, &ctl );
+        if( r==1 ) break;
+        if( r ) {
+          fd_ed25519_hip_shlink_fail( S->in, FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL );
+          fd_ed25519_hip_shlink_fail( S->out, FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL );
+          FD_LOG_ERR(( "tile %lu overran its txn link", k ));
+        }
+        if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { S->eos = 1; break; }
+        if( S->q_cnt==S->q_cap ) {   /* grow the queue: never wait on the tile */
+          S->q_cap *= 2UL;
+          S->q     = (uchar *)realloc( S->q, S->q_cap*frag_max );
+          S->q_sz  = (ulong *)realloc( S->q_sz, S->q_cap*sizeof(ulong) );
+          S->q_sig = (ulong *)realloc( S->q_sig, S->q_cap*sizeof(ulong) );
+          FD_TEST( S->q && S->q_sz && S->q_sig );
+        }
+        S->q_sz [ S->q_cnt ] = answer( S, buf, sz, S->q + S->q_cnt*frag_max );
+        S->q_sig[ S->q_cnt ] = sig;
+        S->q_cnt++;
+        progress = 1;
+      }
+    }
+    beat++;
+    idle = progress ? 0UL : idle+1UL;
+    if( done==tiles ) break;
+  }
+  for( ulong k=0UL; k<tiles; k++ ) { fd_ed25519_hip_shlink_leave( L[k].in, 1 ); fd_ed25519_hip_shlink_leave( L[k].out, 1 ); }
+  return 0;
+}

@@ -1,0 +1,140 @@
+"""The accelerated verify tile under the reference's fd_mux_tile with the
+real GPU verify service behind it (firedancer_amd/_lib/fd_verify_hip_service):
+its published frags against the reference's fd_tile_verify on the same
+stream, one tile and three tiles on one service process (the device's base
+tables held once for all of them), and the service's failure policy.  The
+CPU version with a stand-in service is test_mux_tile.py."""
+import json
+import os
+import subprocess
+import time
+import uuid
+
+import pytest
+
+from firedancer_amd import tile
+from test_mux_tile import HARNESS, MTU, assert_same_frags, cleanup, parse_out, run_harness
+from txn_util import tile_workload
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SERVICE = os.path.join(REPO, "firedancer_amd", "_lib", "fd_verify_hip_service")
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not (os.path.exists(HARNESS) and os.path.exists(SERVICE)),
+                                 reason="oracle/_ref/mux or the service binary not built")]
+
+
+def start_service(app, tiles, *extra):
+    env = dict(os.environ)
+    env.setdefault("GPU_MAX_HW_QUEUES", "16")   # K tiles x 3 slots of one stream each
+    svc = subprocess.Popen([SERVICE, "--prefix", f"/fd_vhip_{app}_", "--tiles", str(tiles), *extra],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    line = svc.stdout.readline()
+    assert line.startswith("ready"), (line, svc.stderr.read() if svc.poll() is not None else "")
+    return svc
+
+
+def finish_service(svc):
+    so, se = svc.communicate(timeout=60)
+    return svc.returncode, json.loads(so.strip().splitlines()[-1]), se
+
+
+@pytest.fixture(scope="module")
+def stream(oracle, tmp_path_factory):
+    frags = [p for p in tile_workload(oracle, 12, 2600) if len(p) <= MTU]
+    path = str(tmp_path_factory.mktemp("gmux") / "payloads.bin")
+    tile.write_payload_file(path, frags)
+    return path, frags
+
+
+@pytest.fixture(scope="module")
+def reference_runs(stream, tmp_path_factory):
+    path, _ = stream
+    d = tmp_path_factory.mktemp("gmuxref")
+    runs = {}
+    for rr in ((1, 0), (3, 0), (3, 1), (3, 2)):
+        out = str(d / f"ref_{rr[0]}_{rr[1]}.bin")
+        p = run_harness("verify", path, out, rr=rr)
+        so, se = p.communicate(timeout=120)
+        assert p.returncode == 0, se[-2000:]
+        runs[rr] = parse_out(out)
+    return runs
+
+
+@pytest.mark.parametrize("gpu_parse", [False, True], ids=["host-parse", "gpu-parse"])
+def test_gpu_service_tile_matches_reference_tile(stream, reference_runs, tmp_path, gpu_parse):
+    """The sandboxed tile under fd_mux_tile, the GPU service verifying in
+    batches of 256 signatures with 3 in flight: the reference tile's frags,
+    byte for byte and in order."""
+    path, frags = stream
+    app = uuid.uuid4().hex[:10]
+    svc = start_service(app, 1, "--batch", "256", *(["--gpu-parse"] if gpu_parse else []))
+    try:
+        out = str(tmp_path / "hip.bin")
+        p = run_harness("verify_hip", path, out, app=app, timeout=100)
+        so, se = p.communicate(timeout=120)
+        assert p.returncode == 0, se[-2000:]
+        rc, res, se2 = finish_service(svc)
+        assert rc == 0, se2[-2000:]
+    finally:
+        if svc.poll() is None:
+            svc.kill()
+        cleanup(app)
+    assert res["txns"] == [len(frags)]
+    assert_same_frags(reference_runs[(1, 0)], parse_out(out))
+
+
+def test_gpu_service_three_tiles_one_process(stream, reference_runs, tmp_path):
+    """Three verify tiles (seq % 3) on one service process: each publishes
+    what the reference tile at its position does; the device's base tables
+    (2 x 2 GiB) exist once in that process, and each further tile costs its
+    own pipe only (batch-sized lane tables: well under 1 GiB)."""
+    path, _ = stream
+    app = uuid.uuid4().hex[:10]
+    svc = start_service(app, 3, "--batch", "512")
+    try:
+        procs = [(k, run_harness("verify_hip", path, str(tmp_path / f"hip{k}.bin"), app=app, rr=(3, k), timeout=100))
+                 for k in range(3)]
+        for k, p in procs:
+            so, se = p.communicate(timeout=120)
+            assert p.returncode == 0, (k, se[-2000:])
+        rc, res, se2 = finish_service(svc)
+        assert rc == 0, se2[-2000:]
+    finally:
+        if svc.poll() is None:
+            svc.kill()
+        cleanup(app)
+    for k in range(3):
+        assert_same_frags(reference_runs[(3, k)], parse_out(str(tmp_path / f"hip{k}.bin")))
+    assert res["shared_device_bytes"] == 2 * (1 << 24) * 128
+    assert all(0 < b < (1 << 30) for b in res["tile_device_bytes"]), res
+
+
+def test_gpu_service_stops_on_tile_failure(tmp_path):
+    """The service's failure policy, driven from the tile side: a tile that
+    marks its txn link failed stops the service, which marks every link
+    failed (the other tile's too) and exits with status 2 instead of
+    serving on."""
+    app = uuid.uuid4().hex[:10]
+    svc = start_service(app, 2)
+    try:
+        txl = tile.ShLink(f"/fd_vhip_{app}_0_txn")
+        vdl = tile.ShLink(f"/fd_vhip_{app}_0_vd")
+        other = tile.ShLink(f"/fd_vhip_{app}_1_vd")
+        t0 = time.time()
+        while vdl.heartbeat_query() == 0 and time.time() - t0 < 60:   # the service's first tick
+            time.sleep(0.01)
+        assert vdl.heartbeat_query() != 0
+        txl.fail(tile.SHLINK_FAIL_PROTOCOL)
+        rc, res, se = finish_service(svc)
+        status_vd, status_other = vdl.status(), other.status()
+        for link in (txl, vdl, other):
+            link.close(unlink=False)
+    finally:
+        if svc.poll() is None:
+            svc.kill()
+        cleanup(app)
+    assert rc == 2, se[-2000:]
+    assert res["rc"] == tile.SHLINK_FAIL_PROTOCOL
+    assert status_vd == tile.SHLINK_FAIL_PROTOCOL
+    assert status_other != 0

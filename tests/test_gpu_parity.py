@@ -173,26 +173,21 @@ def test_chunking(fd, oracle):
     e.close()
 
 
-def test_dsm_form_by_size(fd, oracle, monkeypatch):
-    """The automatic choice by chunk size (thresholds lowered through the
-    environment so the test stays small): a batch of two chunks (1000 wide,
-    600 quad), one of 600 (quad) and one of 300 (oct), against the oracle."""
-    monkeypatch.setenv("FD_ED25519_HIP_QUAD_MAX", "600")
-    monkeypatch.setenv("FD_ED25519_HIP_OCT_MAX", "300")
-    e = fd.Engine(0, max_chunk=1000)
+def test_dsm_form_by_size(fd, oracle):
+    """The automatic choice by chunk size (thresholds lowered with
+    fd_ed25519_hip_engine_set_forms so the test stays small): a batch of two
+    chunks (1000 wide, 600 quad), one of 600 (quad) and one of 300 (oct),
+    against the oracle."""
+    e = fd.Engine(0, max_chunk=1000, forms=(600, 300))
     for n, seed in ((1600, 15), (600, 16), (300, 17)):
         d = _random_set(oracle, n, seed=seed)
         _check(_run(e, d), oracle_many(oracle, d, 0))
     e.close()
 
 
-@pytest.mark.parametrize("env", [
-    {"FD_ED25519_HIP_OVERLAP": "0", "FD_ED25519_HIP_PIPELINE": "0"},
-    {"FD_ED25519_HIP_OVERLAP": "1", "FD_ED25519_HIP_PIPELINE": "0"},
-    {"FD_ED25519_HIP_OVERLAP": "0", "FD_ED25519_HIP_PIPELINE": "1"},
-    {"FD_ED25519_HIP_OVERLAP": "1", "FD_ED25519_HIP_PIPELINE": "1"},
-], ids=["sequential", "overlap", "pipelined", "overlap-pipelined"])
-def test_launch_options_large_chunks(fd, oracle, monkeypatch, env):
+@pytest.mark.parametrize("overlap,pipeline", [(False, False), (True, False), (False, True), (True, True)],
+                         ids=["sequential", "overlap", "pipelined", "overlap-pipelined"])
+def test_launch_options_large_chunks(fd, oracle, overlap, pipeline):
     """The engine's launch sequences for one-lane-per-signature chunks (the
     small-chunk threshold lowered so the batches stay small): phases in
     sequence on one stream or decode on a side stream beside hash + scalar,
@@ -200,11 +195,7 @@ def test_launch_options_large_chunks(fd, oracle, monkeypatch, env):
     between two (each set used twice, the last chunk a short one) -- each
     against the oracle; then a second call on the same engine, which must
     order after the first's lane-1 work."""
-    monkeypatch.setenv("FD_ED25519_HIP_QUAD_MAX", "300")
-    monkeypatch.setenv("FD_ED25519_HIP_OCT_MAX", "100")
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    e = fd.Engine(0, max_chunk=1000)
+    e = fd.Engine(0, max_chunk=1000, overlap=overlap, pipeline=pipeline, forms=(300, 100))
     for n, seed in ((3700, 19), (2400, 20)):
         d = _random_set(oracle, n, seed=seed)
         _check(_run(e, d), oracle_many(oracle, d, 0))

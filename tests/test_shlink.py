@@ -25,18 +25,34 @@ def fake_frag(payload):
     return payload[::-1] + b"\x5a"
 
 
-def serve_fake(txl, vdl, proc, deadline_s=60.0):
-    """Consume txn frags, answer each with fake_verdict, until EOS."""
+def serve_fake(txl, vdl, proc, deadline_s=60.0, stop_after=None, fail_after=None):
+    """Consume txn frags, answer each with fake_verdict, until EOS; tick the
+    heartbeat of the verdict link as the GPU service does.  stop_after:
+    go silent (no heartbeat, no verdicts) after that many verdicts, as a
+    killed service would; fail_after: mark both links failed instead."""
     t0 = time.time()
     pending = []
     eos = False
     n = 0
+    sent = 0
+    beat = 0
     while True:
+        if stop_after is not None and sent >= stop_after:
+            return n
+        if fail_after is not None and sent >= fail_after:
+            txl.fail(-1000 - 700)
+            vdl.fail(-1000 - 700)
+            return n
+        beat += 1
+        vdl.heartbeat(beat)
         while pending:
             sig, v, fr = pending[0]
             if not vdl.publish(bytes([v & 0xff]) + fr, sig):
                 break
             pending.pop(0)
+            sent += 1
+            if stop_after is not None and sent >= stop_after:
+                break
         if eos and not pending:
             while not vdl.publish(b"", 0, tile.SHLINK_CTL_EOS):
                 pass
@@ -87,6 +103,44 @@ def test_sandboxed_producer_round_trip(tmp_path, sandbox, n, depth):
     want = np.array([fake_verdict(p) for p in payloads], np.int8)
     assert np.array_equal(got, want)
     assert tile.parse_producer_frags(out[n:]) == [fake_frag(p) for p in payloads if fake_verdict(p) == 0]
+
+
+@pytest.mark.parametrize("how", ["killed", "failed"])
+def test_producer_stops_when_service_dies(tmp_path, how):
+    """Liveness across the sandbox split: the stand-in service stops
+    mid-stream -- silent (no heartbeat, no verdicts: a killed or hung
+    process) or marking both links failed (its failure policy) -- while the
+    producer is under seccomp strict mode; the producer notices with the
+    time-stamp counter alone and exits with status 4 within its bound
+    instead of waiting on credits forever."""
+    rng = random.Random(5)
+    n = 4000
+    payloads = [bytes(rng.getrandbits(8) for _ in range(rng.choice([1, 64, 200]))) for _ in range(n)]
+    path = str(tmp_path / "payloads.bin")
+    tile.write_payload_file(path, payloads)
+    tag = uuid.uuid4().hex[:12]
+    txl = tile.ShLink(f"/fdt_tx_{tag}", 64, create=True)
+    vdl = tile.ShLink(f"/fdt_vd_{tag}", 64, create=True)
+    proc = subprocess.Popen([tile.PRODUCER_BIN, txl.name, vdl.name, path, "--stale-ms", "300"],
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    try:
+        if how == "killed":
+            serve_fake(txl, vdl, proc, stop_after=500)
+        else:
+            serve_fake(txl, vdl, proc, fail_after=500)
+        t0 = time.time()
+        out, err = proc.communicate(timeout=30)
+        dt = time.time() - t0
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+        txl.close()
+        vdl.close()
+    if proc.returncode == 3:
+        pytest.skip(f"seccomp strict mode unavailable: {err.decode()}")
+    assert proc.returncode == 4, (proc.returncode, err.decode())
+    assert (b"stale" if how == "killed" else b"marked a link failed") in err
+    assert dt < 5.0
 
 
 def test_link_credits_and_overrun_free():

@@ -21,8 +21,7 @@ from firedancer_amd import ed25519  # noqa: E402
 
 
 def engine(pipeline, chunk):
-    os.environ["FD_ED25519_HIP_PIPELINE"] = "1" if pipeline else "0"
-    return ed25519.Engine(0, max_chunk=chunk)
+    return ed25519.Engine(0, max_chunk=chunk, pipeline=pipeline)
 
 
 def main():

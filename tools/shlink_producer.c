@@ -5,7 +5,7 @@
    src/app/fdctl/run/tiles/verify.seccomppolicy) and runs the whole stream
    with memory operations only.  Any other system call would kill it.
 
-     shlink_producer IN_LINK OUT_LINK PAYLOAD_FILE [--no-sandbox]
+     shlink_producer IN_LINK OUT_LINK PAYLOAD_FILE [--no-sandbox] [--stale-ms MS]
 
    PAYLOAD_FILE: u64 n, n x u32 sizes, the payloads back to back.  Frag i
    carries sig = i; after the last one an EOS frag.  Verdict frags are
@@ -14,7 +14,14 @@
    frag order (checked against the sig of every verdict frag), then for
    each SUCCESS verdict the frag the service returned with it (the frag
    the verify tile publishes: u32 size, then the bytes); exit status 0, or
-   2 on a protocol error, 3 if strict mode is unavailable. */
+   2 on a protocol error, 3 if strict mode is unavailable, 4 if the service
+   stopped: its heartbeat on OUT_LINK unchanged for MS milliseconds
+   (default 1000; 60 s before its first tick) or a link marked failed
+   (fd_cnc's heartbeat check, src/tango/cnc/fd_cnc.h:63-65,129-130).  Strict
+   mode leaves no clock -- not even the time-stamp counter, which the kernel
+   disables for it -- so time is counted in pause instructions, their rate
+   measured before the sandbox (the waits only run longer than that, so the
+   bound is a lower bound on the time waited). */
 #define _GNU_SOURCE
 #include "../include/fd_ed25519_hip_tile.h"
 
@@ -24,12 +31,53 @@
 #include <string.h>
 #include <sys/prctl.h>
 #include <sys/syscall.h>
+#include <time.h>
 #include <unistd.h>
+#include <x86intrin.h>
 
 static void
 leave( int status ) {   /* exit(2) itself: exit_group is not allowed in strict mode */
   syscall( SYS_exit, status );
   for(;;) {}
+}
+
+/* the service's liveness, checked while waiting on it */
+typedef struct {
+  fd_ed25519_hip_shlink_t * txl;
+  fd_ed25519_hip_shlink_t * vdl;
+  unsigned long hb_last;
+  unsigned long since;       /* pauses since hb_last changed */
+  unsigned long stale, boot; /* bounds in pauses */
+  unsigned long spin;
+} watch_t;
+
+static void
+say( char const * msg ) {
+  long k = write( 2, msg, strlen( msg ) );
+  (void)k;
+}
+
+static void
+watch( watch_t * w ) {
+  _mm_pause();
+  w->since++;
+  if( (++w->spin & 255UL) ) return;
+  if( fd_ed25519_hip_shlink_status( w->vdl ) || fd_ed25519_hip_shlink_status( w->txl ) ) {
+    say( "shlink_producer: the verify service marked a link failed\n" );
+    leave( 4 );
+  }
+  unsigned long hb = fd_ed25519_hip_shlink_heartbeat_query( w->vdl );
+  if( hb!=w->hb_last ) { w->hb_last = hb; w->since = 0UL; return; }
+  if( w->since > (hb ? w->stale : w->boot) ) {
+    say( "shlink_producer: the verify service's heartbeat is stale\n" );
+    leave( 4 );
+  }
+}
+
+static double
+now_ns( void ) {
+  struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return 1e9*(double)ts.tv_sec + (double)ts.tv_nsec;
 }
 
 typedef struct {
@@ -63,8 +111,14 @@ take_verdicts( fd_ed25519_hip_shlink_t * in, unsigned char * buf, signed char * 
 
 int
 main( int argc, char ** argv ) {
-  if( argc<4 ) { fprintf( stderr, "usage: %s IN_LINK OUT_LINK PAYLOAD_FILE [--no-sandbox]\n", argv[0] ); return 1; }
-  int sandbox = !(argc>4 && !strcmp( argv[4], "--no-sandbox" ));
+  if( argc<4 ) { fprintf( stderr, "usage: %s IN_LINK OUT_LINK PAYLOAD_FILE [--no-sandbox] [--stale-ms MS]\n", argv[0] ); return 1; }
+  int sandbox = 1;
+  double stale_ms = 1000.0;
+  for( int a=4; a<argc; a++ ) {
+    if(      !strcmp( argv[a], "--no-sandbox" ) ) sandbox = 0;
+    else if( !strcmp( argv[a], "--stale-ms" ) && a+1<argc ) stale_ms = strtod( argv[++a], NULL );
+    else { fprintf( stderr, "bad argument %s\n", argv[a] ); return 1; }
+  }
   FILE * f = fopen( argv[3], "rb" );
   if( !f ) { perror( "payload file" ); return 1; }
   unsigned long n = 0UL;
@@ -87,6 +141,12 @@ main( int argc, char ** argv ) {
   fd_ed25519_hip_shlink_t * txl = fd_ed25519_hip_shlink_join( argv[1] );
   fd_ed25519_hip_shlink_t * vdl = fd_ed25519_hip_shlink_join( argv[2] );
   if( !verdict || !buf || !txl || !vdl ) { fprintf( stderr, "cannot join the links\n" ); return 1; }
+  /* pauses per ns, measured before the sandbox */
+  double n0 = now_ns();
+  for( unsigned long k=0UL; k<(1UL<<20); k++ ) _mm_pause();
+  double pause_per_ns = (double)(1UL<<20) / (now_ns() - n0);
+  watch_t wt = { txl, vdl, fd_ed25519_hip_shlink_heartbeat_query( vdl ), 0UL,
+                 (unsigned long)(pause_per_ns * stale_ms * 1e6), (unsigned long)(pause_per_ns * 60e9), 0UL };
   fflush( stdout ); fflush( stderr );
 
   if( sandbox && prctl( PR_SET_SECCOMP, SECCOMP_MODE_STRICT ) ) { perror( "seccomp strict" ); return 3; }
@@ -99,12 +159,15 @@ main( int argc, char ** argv ) {
     if( r==0 ) { i++; continue; }
     if( r!=1 ) leave( 2 );
     if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) || eos ) leave( 2 );
+    watch( &wt );
   }
   while( fd_ed25519_hip_shlink_publish( txl, NULL, 0UL, n, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
     if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) || eos ) leave( 2 );
+    watch( &wt );
   }
   while( !eos ) {
     if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) ) leave( 2 );
+    watch( &wt );
   }
   if( got!=n ) leave( 2 );
   unsigned long w = 0UL;
