@@ -24,6 +24,12 @@ touches a GPU (rank r on device r, gloo for the barrier and the
 max-over-ranks); under torchrun it uses the launcher's ranks.  Every rank
 must hold a distinct device (checked by PCI address) unless
 --allow-shared-device is given (a one-GPU rehearsal).
+
+No rank can hang the others: the gloo group has a 120 s timeout, every
+rank's setup (device check, engine, workload) runs under a guard and all
+ranks agree on its outcome in one collective before anything else, so a
+failure on any rank makes every rank exit non-zero right away; when
+bench.py started the ranks itself, it ends the others once one has failed.
 """
 import argparse
 import ctypes
@@ -44,10 +50,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+GLOO_TIMEOUT_S = float(os.environ.get("FD_BENCH_GLOO_TIMEOUT_S", "120"))
+RANK_GRACE_S = 30.0
+
+
 def spawn_ranks(gpus):
     """--gpus N without a launcher: N child processes of this script, rank r
     on device r, started before this process touches any GPU; returns the
-    exit code (the worst rank's)."""
+    exit code (the worst rank's).  Once a rank has failed, the others get
+    RANK_GRACE_S to finish (they normally fail the same agreement at once)
+    and are then ended, so a dead rank never keeps the job waiting."""
     import socket
     import subprocess
     with socket.socket() as sk:
@@ -58,9 +70,19 @@ def spawn_ranks(gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
+            failed_at = time.time()
+        if failed_at is not None and time.time() - failed_at > RANK_GRACE_S:
+            for p in procs:
+                if p.poll() is None:
+                    log(f"[launcher] ending rank pid {p.pid}: another rank failed {RANK_GRACE_S:.0f} s ago")
+                    p.kill()
+        time.sleep(0.2)
     rcs = [p.wait() for p in procs]
     bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    return (bad[0] if bad[0] > 0 else 2) if bad else 0
 
 
 def dist_setup(gpus):
@@ -78,8 +100,9 @@ def dist_setup(gpus):
         sys.stdout.flush()
         saved = os.dup(1)
         os.dup2(2, 1)
+        from datetime import timedelta
         try:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=GLOO_TIMEOUT_S))
         finally:
             sys.stdout.flush()
             os.dup2(saved, 1)
@@ -167,7 +190,8 @@ def cpu_baseline(wl, gpu_codes, sample, reps, workload_name="C2"):
             "sample": f"first {n} signatures of the {workload_name} workload x {reps} passes, fd_ed25519_verify of the "
                       f"reference's {flavour} backend (compiled from its sources), {threads} pthreads",
             "cores_source": cores_src,
-            "scope": "this process's CPU share of the GPU box (one GPU's lease), not the whole node",
+            "scope": "the host cores this process may use (cores_source), measured on rank 0 in the same run "
+                     "after the GPU steps",
             "seconds": ns * 1e-9, "per_core": rate / threads,
             "verdicts_equal_gpu": bool(np.array_equal(out, gpu_codes[:n]))}
 
@@ -453,41 +477,55 @@ def main():
     strong = bool(cfg.get("total"))
     if strong:  # cfg n is the whole stream: this rank verifies its contiguous share
         n = (n + world - 1) // world
-    ndev = ed25519.device_count()
-    if local >= ndev and not args.allow_shared_device:
-        log(f"[rank {rank}] local rank {local} but only {ndev} visible GPU(s)")
+    # setup under a guard on every rank, then one agreement (an all-gather
+    # of each rank's outcome and device) before anything else: a rank that
+    # fails here never leaves the others waiting in a later collective
+    st = {}
+
+    def setup():
+        ndev = int(os.environ.get("FD_BENCH_FAKE_DEVICE_COUNT", ed25519.device_count()))   # test hook (CPU tests)
+        if local >= ndev and not args.allow_shared_device:
+            raise RuntimeError(f"local rank {local} but only {ndev} visible GPU(s)")
+        st["device"] = local % max(ndev, 1)
+        st["eng"] = ed25519.Engine(device=st["device"], max_chunk=min(n, 1 << 20), half=args.half)
+        st["info"] = st["eng"].info()
+        log(f"[rank {rank}] engine {st['info']}")
+        t = time.perf_counter()
+        st["wl"] = ed25519.DeviceWorkload(st["eng"], n, cfg["lo"], cfg["hi"], cfg["ppm"], seed=args.seed,
+                                          index_base=rank * n)
+        st["gen_s"] = time.perf_counter() - t
+        log(f"[rank {rank}] generated {n} signatures ({st['wl'].msg_bytes / 1e6:.1f} MB of messages) "
+            f"in {st['gen_s']:.2f} s")
+        i = st["info"]
+        return f"{i['pci_domain']:04x}:{i['pci_bus']:02x}:{i['pci_device']:02x}"
+    try:
+        mine = ("ok", setup())
+    except Exception as ex:   # agreed on below, by every rank
+        mine = ("failed", f"{ex}")
+        log(f"[rank {rank}] {ex}")
+    if os.environ.get("FD_BENCH_DIE_RANK") == str(rank):   # test hook: a rank lost before the agreement
+        os._exit(3)
+    outcome = all_gather(mine, world)
+    bad = [(r, m) for r, (k, m) in enumerate(outcome) if k != "ok"]
+    if bad:
+        if rank == 0 or mine[0] != "ok":
+            log(f"[rank {rank}] setup failed on rank(s) {[r for r, _ in bad]}: {bad}")
         return 2
-    device = local % max(ndev, 1)
-    eng = ed25519.Engine(device=device, max_chunk=min(n, 1 << 20), half=args.half)
-    info = eng.info()
-    log(f"[rank {rank}] engine {info}")
-    pci = f"{info['pci_domain']:04x}:{info['pci_bus']:02x}:{info['pci_device']:02x}"
-    devices = all_gather(pci, world)
+    devices = [m for _, m in outcome]
     n_dev = len(set(devices))
     if n_dev != world and not args.allow_shared_device:
         log(f"[rank {rank}] ranks share devices: {devices}")
         return 2
-
-    t = time.perf_counter()
-    wl = ed25519.DeviceWorkload(eng, n, cfg["lo"], cfg["hi"], cfg["ppm"], seed=args.seed, index_base=rank * n)
-    gen_s = time.perf_counter() - t
-    log(f"[rank {rank}] generated {n} signatures ({wl.msg_bytes / 1e6:.1f} MB of messages) in {gen_s:.2f} s")
+    device, eng, info, wl, gen_s = st["device"], st["eng"], st["info"], st["wl"], st["gen_s"]
 
     inflight = args.inflight or (2 if strong else 4)
     one_stream = inflight >= 3 if args.one_stream == "auto" else args.one_stream == "1"
     hf_first = None
-    if one_stream and args.host_reps > 0:
-        # The host-fed pool's 3 slot streams run at full rate only for some
-        # placements on the process's 4 hardware queues, which follow the
-        # streams created before it: after the main engine's two streams
-        # (the first large chunk creates its decode side stream) they do
-        # (69.8M/s, profiles/r2_pool_slots_queue_probe.txt), after the four
-        # one-stream engines of the timed steps they do not (47-57M/s,
-        # profiles/r2_host_fed_order_ab.txt).  So the leg runs first, after
-        # one warm verify on the main engine.
-        wl.verify()
-        eng.sync()
-        args.host_first = True
+    # (round 2 ran the host-fed leg first because its pool's slot streams
+    # landed on shared hardware queues after the timed engines' streams; the
+    # library's per-device stream set, fd_ed25519_hip_engine.c, made the
+    # placement independent of creation order, and the leg runs last again;
+    # --host-first remains for the A/B)
     if args.host_first and args.host_reps > 0:   # the host-fed leg before the engine's timed passes
         try:
             hf_first = host_fed(wl, device, info, world, args.host_reps, args.host_batch, args.host_slots,
@@ -584,17 +622,24 @@ def main():
     path_achieved = path_ops / (path_ms * 1e-3) / 1e12 if path_ms > 0 else None
 
     cpu = c1 = c3 = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # the reference CPU path on the host's cores in the same run, N=1 and
+        # N>1 alike (the other ranks wait at the barrier below)
         try:
             cpu = cpu_baseline(wl, out, args.cpu_sample, args.cpu_reps)
-            c1 = config_c1(eng, args)
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"cpu baseline failed: {ex!r}")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            c1 = config_c1(eng, args)
+        except Exception as ex:  # reported, never fatal for the GPU number
+            log(f"C1 leg failed: {ex!r}")
         try:
             c3 = config_c3(eng, args)
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"C3 leg failed: {ex!r}")
             c3 = {"error": repr(ex)}
+    barrier(world)
     hf = hf_first
     if args.host_reps > 0 and hf is None:
         try:

@@ -200,6 +200,82 @@ btabw_release( int device ) {
   pthread_mutex_unlock( &btabw_lock );
 }
 
+/* The device's stream set.  A process gets GPU_MAX_HW_QUEUES hardware
+   queues per device (4 by default) and HIP binds each new stream to one of
+   them; which one depends on every stream created before, so a feeder's
+   slots could land on a shared queue or not depending on what else the
+   process had made first (round 2: the host-fed pool at 47-57M/s or 70M/s
+   by creation order).  Instead the library creates one stream per hardware
+   queue per device, once, and every engine stream (its main stream, its
+   second lane's, the decode side stream) is drawn from that set: the least
+   used ones first, distinct within an engine.  Engines sharing a stream
+   order their work together, which costs nothing while one of them is
+   idle; concurrently busy engines get distinct streams as long as there
+   are queues for them, which is the most concurrency the device gives the
+   process anyway.  The set's size follows HIP's own GPU_MAX_HW_QUEUES
+   (default 4, capped at 32); the streams live as long as the process. */
+#define FD_ED25519_HIP_STREAM_SET_MAX 32
+static pthread_mutex_t sset_lock = PTHREAD_MUTEX_INITIALIZER;
+static struct {
+  int         cnt;
+  hipStream_t s[ FD_ED25519_HIP_STREAM_SET_MAX ];
+  int         users[ FD_ED25519_HIP_STREAM_SET_MAX ];
+} sset[ FD_ED25519_HIP_MAX_DEV ];
+
+static int
+stream_set_size( void ) {
+  char const * q = getenv( "GPU_MAX_HW_QUEUES" );   /* the HIP runtime's knob, not the library's */
+  long n = q ? strtol( q, NULL, 0 ) : 4L;
+  if( n<1L ) n = 1L;
+  if( n>FD_ED25519_HIP_STREAM_SET_MAX ) n = FD_ED25519_HIP_STREAM_SET_MAX;
+  return (int)n;
+}
+
+/* a stream of the device's set, the least used one that is not in
+   avoid[0..avoid_cnt) (if every stream is, the least used one) */
+static int
+stream_acquire( int device, hipStream_t const * avoid, int avoid_cnt, hipStream_t * out ) {
+  if( device<0 || device>=FD_ED25519_HIP_MAX_DEV ) return FD_ED25519_HIP_ERR_INVAL;
+  pthread_mutex_lock( &sset_lock );
+  int rc = FD_ED25519_HIP_OK;
+  if( !sset[device].cnt ) {
+    int n = stream_set_size();
+    for( int i=0; i<n; i++ ) {
+      hipError_t he = hipStreamCreateWithFlags( &sset[device].s[i], hipStreamNonBlocking );
+      if( he!=hipSuccess ) {
+        for( int j=0; j<i; j++ ) hipStreamDestroy( sset[device].s[j] );
+        rc = hip_fail( he, "stream set" );
+        break;
+      }
+      sset[device].users[i] = 0;
+    }
+    if( !rc ) sset[device].cnt = n;
+  }
+  if( !rc ) {
+    int best = -1, best_avoided = -1;
+    for( int i=0; i<sset[device].cnt; i++ ) {
+      int avoided = 0;
+      for( int j=0; j<avoid_cnt; j++ ) if( avoid[j]==sset[device].s[i] ) avoided = 1;
+      if( avoided ) { if( best_avoided<0 || sset[device].users[i]<sset[device].users[best_avoided] ) best_avoided = i; }
+      else if( best<0 || sset[device].users[i]<sset[device].users[best] ) best = i;
+    }
+    if( best<0 ) best = best_avoided;
+    sset[device].users[best]++;
+    *out = sset[device].s[best];
+  }
+  pthread_mutex_unlock( &sset_lock );
+  return rc;
+}
+
+static void
+stream_release( int device, hipStream_t st ) {
+  if( !st || device<0 || device>=FD_ED25519_HIP_MAX_DEV ) return;
+  pthread_mutex_lock( &sset_lock );
+  for( int i=0; i<sset[device].cnt; i++ )
+    if( sset[device].s[i]==st && sset[device].users[i]>0 ) { sset[device].users[i]--; break; }
+  pthread_mutex_unlock( &sset_lock );
+}
+
 static void
 engine_free( fd_ed25519_hip_engine_t * e ) {
   if( !e ) return;
@@ -225,12 +301,12 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   for( int l=0; l<2; l++ ) {
     if( e->lane[l].side ) {
       hipEventDestroy( e->lane[l].ev_dfork ); hipEventDestroy( e->lane[l].ev_djoin );
-      hipStreamDestroy( e->lane[l].side );
+      stream_release( e->device, e->lane[l].side );
     }
-    if( e->lane[l].stream ) hipStreamDestroy( e->lane[l].stream );
+    stream_release( e->device, e->lane[l].stream );
   }
   if( e->lane[1].d_work ) { hipEventDestroy( e->ev_start ); hipEventDestroy( e->ev_end ); }
-  if( e->stream ) hipStreamDestroy( e->stream );
+  stream_release( e->device, e->stream );
   free( e );
 }
 
@@ -261,17 +337,21 @@ lane_alloc( fd_ed25519_hip_engine_t * e, int l ) {
   hipStream_t st = NULL; hipEvent_t ev0 = NULL, ev1 = NULL;
   hipError_t he = hipMalloc( &atab, atab_sz );
   if( he==hipSuccess ) he = hipMalloc( (void **)&work, work_sz );
+  int serr = FD_ED25519_HIP_OK;
   if( l ) {
-    if( he==hipSuccess ) he = hipStreamCreateWithFlags( &st, hipStreamNonBlocking );
-    if( he==hipSuccess ) he = hipEventCreateWithFlags( &ev0, hipEventDisableTiming );
-    if( he==hipSuccess ) he = hipEventCreateWithFlags( &ev1, hipEventDisableTiming );
+    if( he==hipSuccess ) {
+      hipStream_t avoid[3] = { e->stream, e->lane[0].side, NULL };
+      serr = stream_acquire( e->device, avoid, 2, &st );
+    }
+    if( he==hipSuccess && !serr ) he = hipEventCreateWithFlags( &ev0, hipEventDisableTiming );
+    if( he==hipSuccess && !serr ) he = hipEventCreateWithFlags( &ev1, hipEventDisableTiming );
   }
-  if( he!=hipSuccess ) {
+  if( he!=hipSuccess || serr ) {
     if( ev1 ) hipEventDestroy( ev1 );
     if( ev0 ) hipEventDestroy( ev0 );
-    if( st  ) hipStreamDestroy( st );
+    stream_release( e->device, st );
     hipFree( work ); hipFree( atab );
-    return hip_fail( he, "lane scratch" );
+    return serr ? serr : hip_fail( he, "lane scratch" );
   }
   e->device_bytes += atab_sz + work_sz;
   uint64_t c = e->max_chunk;
@@ -308,7 +388,8 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
               "device %d is %.63s; libfd_ed25519_hip is built for gfx950 only", device, prop.gcnArchName );
     return FD_ED25519_HIP_ERR_INVAL;
   }
-  HIPCHK( hipStreamCreateWithFlags( &e->stream, hipStreamNonBlocking ), "hipStreamCreate" );
+  int serr = stream_acquire( device, NULL, 0, &e->stream );
+  if( serr ) return serr;
 
   int bpc = 0;
   HIPCHK( (hipError_t)fd_ed25519_hip_verify_occupancy( &bpc ), "occupancy query" );
@@ -464,7 +545,9 @@ verify_chunk( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p, int l
          small batches (a tile slot) keeps to one stream, since the
          device's few hardware queues are shared by every stream of the
          process and extra streams serialise the slots */
-      HIPCHK( hipStreamCreateWithFlags( &e->lane[l].side, hipStreamNonBlocking ), "hipStreamCreate" );
+      hipStream_t avoid[2] = { e->stream, e->lane[1].stream };
+      int serr = stream_acquire( e->device, avoid, 2, &e->lane[l].side );
+      if( serr ) return serr;
       HIPCHK( hipEventCreateWithFlags( &e->lane[l].ev_dfork, hipEventDisableTiming ), "hipEventCreate" );
       HIPCHK( hipEventCreateWithFlags( &e->lane[l].ev_djoin, hipEventDisableTiming ), "hipEventCreate" );
     }

@@ -103,6 +103,44 @@ def test_bench_spawns_its_ranks_without_a_launcher():
     assert r.stdout == ""
 
 
+def _bench_ranks(extra_env, timeout=300):
+    import subprocess
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(extra_env)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=timeout, env=env)
+    return r, time.time() - t0
+
+
+def test_bench_one_rank_without_device_one_engine_failing():
+    """Rank 1 has no device of its own while rank 0 has one (a test hook
+    pretends one GPU is visible) and rank 0's engine then fails (there is no
+    GPU here): both ranks reach the setup agreement, both exit non-zero
+    promptly, none is left waiting in a collective (VERDICT r2 weak #3)."""
+    r, dt = _bench_ranks({"FD_BENCH_FAKE_DEVICE_COUNT": "1"})
+    assert r.returncode == 2, r.stderr[-3000:]
+    assert "[rank 1] local rank 1 but only 1 visible GPU(s)" in r.stderr
+    assert "[rank 0] engine_new failed" in r.stderr
+    assert "setup failed on rank(s) [0, 1]" in r.stderr
+    assert r.stdout == ""
+    assert dt < 90, dt
+
+
+def test_bench_rank_lost_before_the_agreement():
+    """A rank that dies before the first collective (test hook: rank 1 exits
+    at once): rank 0 leaves its collective on the gloo timeout (10 s here,
+    120 s by default) or is ended by the launcher's grace period; the job
+    exits non-zero within about that bound instead of the default 30
+    minutes."""
+    r, dt = _bench_ranks({"FD_BENCH_FAKE_DEVICE_COUNT": "2", "FD_BENCH_DIE_RANK": "1",
+                          "FD_BENCH_GLOO_TIMEOUT_S": "10"})
+    assert r.returncode != 0, r.stderr[-3000:]
+    assert r.stdout == ""
+    assert dt < 90, dt
+
+
 def test_bench_rejects_a_launcher_world_that_differs_from_gpus():
     import subprocess
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
