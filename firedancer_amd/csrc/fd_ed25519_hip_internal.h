@@ -32,6 +32,12 @@ extern "C" {
 #define FD_ED25519_BTABW_BITS     24
 #define FD_ED25519_BTABW_ENTRIES  (1 << FD_ED25519_BTABW_BITS)
 #define FD_ED25519_BTABW_SHIFT    144   /* s_lo: 6 digits (bits 0..143), s_hi: 5 digits (109 bits) */
+/* The compact tables (FD_ED25519_HIP_FLAG_COMPACT_TABLES): the same two
+   tables at radix 2^16, [0..2^16)B and [0..2^16)[2^144]B, 8 MiB each,
+   9 + 7 mixed additions per signature -- for processes that verify little
+   (the drop-in's engines) and should not hold 4 GiB. */
+#define FD_ED25519_BTABC_BITS     16
+#define FD_ED25519_BTABC_ENTRIES  (1 << FD_ED25519_BTABC_BITS)
 
 /* Per-lane tables [1..8](-A) and [1..8](-+R) in cached form, in HBM: 2 x 8
    entries x 40 int32 per lane, laid out [wave][lane][entry][quad] (int4
@@ -110,15 +116,17 @@ typedef struct {
   int              small;          /* small chunk: fused prep kernel, no sort, dsm4 (1: a
                                       quad of lanes per signature) or dsm8 (2: two quads),
                                       full-length items by a scan of hflag          */
+  int              bw_bits;        /* radix of btab_lo / btab_hi: FD_ED25519_BTABW_BITS or
+                                      FD_ED25519_BTABC_BITS (compact)                 */
 } fd_ed25519_verify_params_t;
 
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a
    hipError_t value (0 on success). */
 int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
 int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, int base_doublings, void * stream );
-/* [0..2^24)[2^base_doublings]B into d_tab; d_scratch holds
-   FD_ED25519_BTABW_ENTRIES*10 + 40 int32 */
-int fd_ed25519_hip_launch_gen_btabw( int32_t * d_tab, int base_doublings, int32_t * d_scratch, void * stream );
+/* [0..2^bits)[2^base_doublings]B into d_tab (bits FD_ED25519_BTABW_BITS or
+   FD_ED25519_BTABC_BITS); d_scratch holds 2^bits*10 + 40 int32 */
+int fd_ed25519_hip_launch_gen_btabw( int32_t * d_tab, int base_doublings, int bits, int32_t * d_scratch, void * stream );
 /* counts into *d_bad the entries e < entries-1 of a 32-int-stride base
    table with entry e+1 != entry e + entry 1 (and entry 0 not the identity) */
 int fd_ed25519_hip_launch_check_btabw( int32_t const * d_tab, int entries, uint32_t * d_bad, void * stream );

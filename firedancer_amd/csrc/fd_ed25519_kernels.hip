@@ -565,18 +565,25 @@ FD_DEV void load_hs(uint32_t (&x)[5], const fd_ed25519_verify_params_t& p, int r
   for (int w = 0; w < 5; w++) x[w] = w < words ? p.hs[(uint64_t)(row + w) * p.cap + j] : 0u;
 }
 
-/* base digits: s_lo's 6 and s_hi's 5 radix-2^24 digits sit at bits 24m,
-   i.e. windows 6m (s_lo: 30, 24, .., 0; s_hi: 24, .., 0), top-aligned in
-   160 bits for pop160u */
-#define FD_BW_STEP   (FD_ED25519_BTABW_BITS / 4)
-#define FD_BW_LO_N   6
-#define FD_BW_HI_N   5
-#define FD_BW_LO_SHL (160 - FD_BW_LO_N * FD_ED25519_BTABW_BITS)
-#define FD_BW_HI_SHL (160 - FD_BW_HI_N * FD_ED25519_BTABW_BITS)
-#define FD_BW_LO_AT(it) ((it) <= FD_BW_STEP * (FD_BW_LO_N - 1) && (it) % FD_BW_STEP == 0)
-#define FD_BW_HI_AT(it) ((it) <= FD_BW_STEP * (FD_BW_HI_N - 1) && (it) % FD_BW_STEP == 0)
-static_assert(FD_BW_LO_N * FD_ED25519_BTABW_BITS == FD_ED25519_BTABW_SHIFT, "s_lo digits cover bits 0..SHIFT-1");
-static_assert(FD_BW_HI_N * FD_ED25519_BTABW_BITS >= 253 - FD_ED25519_BTABW_SHIFT, "s_hi digits cover s' >> SHIFT");
+/* base digits of s_lo and s_hi in radix 2^BW: digit m sits at bits BW m,
+   i.e. window (BW/4) m, top-aligned in 160 bits for pop160u.  BW = 24 (the
+   wide tables: s_lo's 6 and s_hi's 5 digits at windows 30, 24, .., 0 and
+   24, .., 0) or 16 (the compact tables, FD_ED25519_HIP_FLAG_COMPACT_TABLES:
+   9 and 7 digits at windows 32, 28, .., 0 and 24, .., 0). */
+template <int BW>
+struct fd_bw {
+  static constexpr int STEP   = BW / 4;
+  static constexpr int LO_N   = FD_ED25519_BTABW_SHIFT / BW;
+  static constexpr int HI_N   = (253 - FD_ED25519_BTABW_SHIFT + BW - 1) / BW;
+  static constexpr int LO_SHL = 160 - LO_N * BW;
+  static constexpr int HI_SHL = 160 - HI_N * BW;
+  static_assert(BW % 4 == 0, "base digits start at window boundaries");
+  static_assert(LO_N * BW == FD_ED25519_BTABW_SHIFT, "s_lo digits cover bits 0..SHIFT-1");
+  static_assert(HI_N * BW >= 253 - FD_ED25519_BTABW_SHIFT, "s_hi digits cover s' >> SHIFT");
+  static_assert(STEP * (LO_N - 1) <= 32, "every base digit falls within the 33 windows");
+  FD_DEV static bool lo_at(int it) { return it <= STEP * (LO_N - 1) && it % STEP == 0; }
+  FD_DEV static bool hi_at(int it) { return it <= STEP * (HI_N - 1) && it % STEP == 0; }
+};
 
 /* ------------------------------------------------------------------------
    dsm: the group equation with half-size scalars.
@@ -594,11 +601,13 @@ static_assert(FD_BW_HI_N * FD_ED25519_BTABW_BITS >= 253 - FD_ED25519_BTABW_SHIFT
    [1..8](-A) and [1..8](-+R) tables (a zero digit adds the shared identity entry)
    (HBM, lane-contiguous 160-byte entries) and 6 + 5 mixed additions from
    the two unsigned radix-2^24 base tables [0..2^24)B and [0..2^24)B'
-   (2 GiB each, HBM).  Every table entry is loaded
+   (2 GiB each, HBM) -- or, with BW = 16, 9 + 7 from the compact
+   [0..2^16) tables (8 MiB each).  Every table entry is loaded
    one step ahead of its use: the -A entry before the window's doublings,
    the R entry before the -A addition, the base entries before the R
    addition.  The result is compared with the identity (X == 0, Y == Z). */
 
+template <int BW>
 FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* tabA, int4* tabR) {
   int code = precheck(p, j);
   const uint32_t hf = p.hflag[j];
@@ -626,8 +635,8 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     const int sh = 160 - 4 * W;
     shl160v(t, x, sh); recode160<4>(dd, t);
     load_hs(x, p, 0, 5, j);  shl160v(t, x, sh); recode160<4>(cd, t);
-    load_hs(x, p, 10, 5, j); shl160<FD_BW_LO_SHL>(ld, x);
-    load_hs(x, p, 15, 4, j); shl160<FD_BW_HI_SHL>(hd, x);
+    load_hs(x, p, 10, 5, j); shl160<fd_bw<BW>::LO_SHL>(ld, x);
+    load_hs(x, p, 15, 4, j); shl160<fd_bw<BW>::HI_SHL>(hd, x);
   }
   const int4* g_btab = reinterpret_cast<const int4*>(p.btab_lo);
   const int4* g_btab2 = reinterpret_cast<const int4*>(p.btab_hi);
@@ -641,7 +650,7 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     int ea = pop160<4>(cd), er = pop160<4>(dd);
     if (it == W - 1) { ea &= 15; er &= 15; }   /* top digits in [0,8] */
     ge_cached ca, cr;
-    const bool blo = FD_BW_LO_AT(it), bhi = FD_BW_HI_AT(it);
+    const bool blo = fd_bw<BW>::lo_at(it), bhi = fd_bw<BW>::hi_at(it);
     ge_precomp b1, b2;
     atab_load(ca, tab_entry<true>(tabA, ea), 0);
     if (it != W - 1) {
@@ -656,8 +665,8 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     ge_cached_cneg(ca, ea < 0);
     ge_add<true>(Rt, P, ca);
     ge_p1p1_to_p3_u(P, Rt);
-    if (blo) btab16_load(b1, g_btab, (int)pop160u<FD_ED25519_BTABW_BITS>(ld));
-    if (bhi) btab16_load(b2, g_btab2, (int)pop160u<FD_ED25519_BTABW_BITS>(hd));
+    if (blo) btab16_load(b1, g_btab, (int)pop160u<BW>(ld));
+    if (bhi) btab16_load(b2, g_btab2, (int)pop160u<BW>(hd));
     ge_cached_cneg(cr, er < 0);
     ge_add<true>(Rt, P, cr);
     if (blo) {
@@ -748,6 +757,7 @@ FD_DEV int dsm_full_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
    chunk's signatures (those queued as full-length skipped), so the ~2x
    longer full-length work is spread over the grid instead of forming a
    tail. */
+template <int BW>
 __global__ void __launch_bounds__(FD_ED25519_VERIFY_BLOCK, FD_ED25519_DSM_WAVES_PER_SIMD)
 fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -777,7 +787,7 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
       p.out[p.base + j] = (int8_t)dsm_full_one(p, j, tabA);
     } else if (t >= head && t < total) {
       const uint64_t j = t - head;
-      if (!(p.hflag[j] & FD_HF_FULL)) p.out[p.base + j] = (int8_t)dsm_half_one(p, j, tabA, tabR);
+      if (!(p.hflag[j] & FD_HF_FULL)) p.out[p.base + j] = (int8_t)dsm_half_one<BW>(p, j, tabA, tabR);
     }
   }
 }
@@ -847,6 +857,7 @@ FD_DEV void table4_build(int4* tab, const fe& x, const fe& y, bool negate, const
   }
 }
 
+template <int BW>
 __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_params_t p) {
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t j = gid >> 2;   /* a quad per signature: all four lanes take the same branches */
@@ -875,8 +886,8 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
     const int sh = 160 - 4 * W;
     shl160v(t, x, sh); recode160<4>(dd, t);
     load_hs(x, p, 0, 5, j);  shl160v(t, x, sh); recode160<4>(cd, t);
-    load_hs(x, p, 10, 5, j); shl160<FD_BW_LO_SHL>(ld, x);
-    load_hs(x, p, 15, 4, j); shl160<FD_BW_HI_SHL>(hd, x);
+    load_hs(x, p, 10, 5, j); shl160<fd_bw<BW>::LO_SHL>(ld, x);
+    load_hs(x, p, 15, 4, j); shl160<fd_bw<BW>::HI_SHL>(hd, x);
   }
   fe P, Rt;
 #pragma unroll
@@ -885,7 +896,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
   for (int it = W - 1; it >= 0; it--) {
     int ea = pop160<4>(cd), er = pop160<4>(dd);
     if (it == W - 1) { ea &= 15; er &= 15; }
-    const bool blo = FD_BW_LO_AT(it), bhi = FD_BW_HI_AT(it);
+    const bool blo = fd_bw<BW>::lo_at(it), bhi = fd_bw<BW>::hi_at(it);
     fe ca, cr, b1, b2;
     tab4_load(ca, tabA, ea < 0 ? -ea : ea);
     if (it != W - 1) {
@@ -900,8 +911,8 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
     ge4_add(Rt, P, ca, m);
     ge4_cneg(Rt, m.l0, ea < 0);
     ge4_to_p3(P, Rt);
-    if (blo) btab4_load(b1, p.btab_lo, (int)pop160u<FD_ED25519_BTABW_BITS>(ld), m);
-    if (bhi) btab4_load(b2, p.btab_hi, (int)pop160u<FD_ED25519_BTABW_BITS>(hd), m);
+    if (blo) btab4_load(b1, p.btab_lo, (int)pop160u<BW>(ld), m);
+    if (bhi) btab4_load(b2, p.btab_hi, (int)pop160u<BW>(hd), m);
     ge4_cneg(P, m.l03, er < 0);
     ge4_add(Rt, P, cr, m);
     ge4_cneg(Rt, m.l0, er < 0);
@@ -935,6 +946,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm4_kernel(fd_ed25519_verify_
    quad 1 then hands its point to quad 0 (DPP row shift) for one last
    addition and the identity test.  ~22% less latency than dsm4 for ~57%
    more lane work. */
+template <int BW>
 __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_params_t p) {
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t j = gid >> 3;                 /* 8 lanes per signature, the same branches */
@@ -962,10 +974,10 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
     shl160v(t, x, 160 - 4 * W); recode160<4>(sd, t);
     if (half) {
       load_hs(x, p, 15, 4, j);
-      shl160<FD_BW_HI_SHL>(bd, x);
+      shl160<fd_bw<BW>::HI_SHL>(bd, x);
     } else {
       load_hs(x, p, 10, 5, j);
-      shl160<FD_BW_LO_SHL>(bd, x);
+      shl160<fd_bw<BW>::LO_SHL>(bd, x);
     }
   }
   const int32_t* btab = half ? p.btab_hi : p.btab_lo;
@@ -976,7 +988,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
   for (int it = W - 1; it >= 0; it--) {
     int e = pop160<4>(sd);
     if (it == W - 1) e &= 15;
-    const bool badd = half ? FD_BW_HI_AT(it) : FD_BW_LO_AT(it);
+    const bool badd = half ? fd_bw<BW>::hi_at(it) : fd_bw<BW>::lo_at(it);
     fe ce, b;
     tab4_load(ce, tab, e < 0 ? -e : e);
     if (it != W - 1) {
@@ -986,7 +998,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
         ge4_to_p3(P, Rt);
       }
     }
-    if (badd) btab4_load(b, btab, (int)pop160u<FD_ED25519_BTABW_BITS>(bd), m);
+    if (badd) btab4_load(b, btab, (int)pop160u<BW>(bd), m);
     ge4_cneg(P, m.l03, e < 0);
     ge4_add(Rt, P, ce, m);
     ge4_cneg(Rt, m.l0, e < 0);
@@ -1057,7 +1069,8 @@ __global__ void fd_ed25519_gen_btab_kernel(int32_t* btab, int entries, int strid
   for (int i = 30; i < stride; i++) o[i] = 0;
 }
 
-/* Wide unsigned-digit tables [0..2^24)[2^base_dbl]B.  The base is computed
+/* Wide unsigned-digit tables [0..2^bits)[2^base_dbl]B (bits 24, or 16 for
+   the compact tables).  The base is computed
    once (gen_base), then each thread produces a run of consecutive entries
    by additions and puts them in affine form with one inversion per run
    (Montgomery's trick: prefix products of Z in `scratch`). */
@@ -1086,7 +1099,7 @@ FD_DEV void fe_ld(fe& a, const int32_t* o) {
 }
 
 __global__ void __launch_bounds__(256)
-fd_ed25519_gen_btab_run_kernel(int32_t* tab, int entries, const int32_t* base, int32_t* scratch) {
+fd_ed25519_gen_btab_run_kernel(int32_t* tab, int entries, int bits, const int32_t* base, int32_t* scratch) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int e0 = t * FD_BTAB_RUN;
   if (e0 >= entries) return;
@@ -1097,7 +1110,7 @@ fd_ed25519_gen_btab_run_kernel(int32_t* tab, int entries, const int32_t* base, i
   ge_p3_to_cached(cb, B);
   ge_p3_0(P);
   ge_p1p1 r;
-  for (int bit = FD_ED25519_BTABW_BITS - 1; bit >= 0; bit--) {   /* P = [e0] base */
+  for (int bit = bits - 1; bit >= 0; bit--) {   /* P = [e0] base */
     ge_p3_dbl(r, P);
     ge_p1p1_to_p3(P, r);
     if ((e0 >> bit) & 1) {
@@ -1256,13 +1269,15 @@ extern "C" int fd_ed25519_hip_launch_diag_half(const uint32_t* d_k, uint32_t* d_
   return (int)hipGetLastError();
 }
 
-extern "C" int fd_ed25519_hip_launch_gen_btabw(int32_t* d_tab, int base_dbl, int32_t* d_scratch, void* stream) {
-  const int entries = FD_ED25519_BTABW_ENTRIES;
+extern "C" int fd_ed25519_hip_launch_gen_btabw(int32_t* d_tab, int base_dbl, int bits, int32_t* d_scratch,
+                                               void* stream) {
+  if (bits != FD_ED25519_BTABW_BITS && bits != FD_ED25519_BTABC_BITS) return (int)hipErrorInvalidValue;
+  const int entries = 1 << bits;
   int32_t* base = d_scratch + (size_t)entries * 10;   /* 40 ints after the prefix products */
   hipLaunchKernelGGL(fd_ed25519_gen_base_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, base, base_dbl);
   const int threads = (entries + FD_BTAB_RUN - 1) / FD_BTAB_RUN;
   hipLaunchKernelGGL(fd_ed25519_gen_btab_run_kernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     d_tab, entries, (const int32_t*)base, d_scratch);
+                     d_tab, entries, bits, (const int32_t*)base, d_scratch);
   return (int)hipGetLastError();
 }
 
@@ -1304,20 +1319,29 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
     if (p->small) {
       /* a quad per signature, then the (rare) full-length items, found by
          a scan of the flags */
-      if (p->small == 2)
-        hipLaunchKernelGGL(fd_ed25519_dsm8_kernel, dim3((uint32_t)((8 * p->n + 255) / 256)), dim3(256), 0, st, *p);
-      else
-        hipLaunchKernelGGL(fd_ed25519_dsm4_kernel, dim3((uint32_t)((4 * p->n + 255) / 256)), dim3(256), 0, st, *p);
+      const bool compact = p->bw_bits == FD_ED25519_BTABC_BITS;
+      const dim3 g8((uint32_t)((8 * p->n + 255) / 256)), g4((uint32_t)((4 * p->n + 255) / 256));
+      if (p->small == 2) {
+        if (compact) hipLaunchKernelGGL(fd_ed25519_dsm8_kernel<FD_ED25519_BTABC_BITS>, g8, dim3(256), 0, st, *p);
+        else         hipLaunchKernelGGL(fd_ed25519_dsm8_kernel<FD_ED25519_BTABW_BITS>, g8, dim3(256), 0, st, *p);
+      } else {
+        if (compact) hipLaunchKernelGGL(fd_ed25519_dsm4_kernel<FD_ED25519_BTABC_BITS>, g4, dim3(256), 0, st, *p);
+        else         hipLaunchKernelGGL(fd_ed25519_dsm4_kernel<FD_ED25519_BTABW_BITS>, g4, dim3(256), 0, st, *p);
+      }
       const uint64_t need = (p->n + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
       const uint32_t g = (uint32_t)(need < grid ? need : grid);
-      hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
+      if (compact) hipLaunchKernelGGL(fd_ed25519_dsm_kernel<FD_ED25519_BTABC_BITS>, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
+      else         hipLaunchKernelGGL(fd_ed25519_dsm_kernel<FD_ED25519_BTABW_BITS>, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
       break;
     }
     /* one wave more than the chunk needs: the full-length items (counted on
        the device) run in waves of their own, in parallel with the rest */
     const uint64_t need = (p->n + 64 + FD_ED25519_VERIFY_BLOCK - 1) / FD_ED25519_VERIFY_BLOCK;
     const uint32_t g = (uint32_t)(need < grid ? need : grid);
-    hipLaunchKernelGGL(fd_ed25519_dsm_kernel, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
+    if (p->bw_bits == FD_ED25519_BTABC_BITS)
+      hipLaunchKernelGGL(fd_ed25519_dsm_kernel<FD_ED25519_BTABC_BITS>, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
+    else
+      hipLaunchKernelGGL(fd_ed25519_dsm_kernel<FD_ED25519_BTABW_BITS>, dim3(g), dim3(FD_ED25519_VERIFY_BLOCK), 0, st, *p);
   } break;
   default:
     return (int)hipErrorInvalidValue;
@@ -1336,7 +1360,7 @@ extern "C" int fd_ed25519_hip_launch_verify(const fd_ed25519_verify_params_t* p,
 extern "C" unsigned long fd_ed25519_hip_atab_bytes_per_wave(void) { return FD_ED25519_ATAB_BYTES_PER_WAVE; }
 
 extern "C" int fd_ed25519_hip_verify_occupancy(int* blocks_per_cu) {
-  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fd_ed25519_dsm_kernel,
+  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fd_ed25519_dsm_kernel<FD_ED25519_BTABW_BITS>,
                                                            FD_ED25519_VERIFY_BLOCK, 0);
 }
 

@@ -135,46 +135,54 @@ fd_ed25519_hip_strerror( int status ) {
 /* The half-size form's base tables, [0..2^24)B and [0..2^24)[2^144]B
    (2 GiB each), are shared by every engine of a device: generated by the
    first engine (with a 640 MiB scratch freed right after), freed with the
-   last. */
+   last.  The compact pair at radix 2^16 (8 MiB each,
+   FD_ED25519_HIP_FLAG_COMPACT_TABLES) is shared the same way; kind 0 is
+   the wide pair, kind 1 the compact one. */
 #define FD_ED25519_HIP_MAX_DEV 64
 static pthread_mutex_t btabw_lock = PTHREAD_MUTEX_INITIALIZER;
-static struct { int refs; int32_t * tab[2]; } btabw[ FD_ED25519_HIP_MAX_DEV ];
+static struct { int refs; int32_t * tab[2]; } btabw[ 2 ][ FD_ED25519_HIP_MAX_DEV ];
+
+static int
+btab_kind_bits( int kind ) {
+  return kind ? FD_ED25519_BTABC_BITS : FD_ED25519_BTABW_BITS;
+}
 
 static size_t
-btabw_bytes( void ) {
-  return sizeof(int32_t) * (size_t)FD_ED25519_BTABW_ENTRIES * FD_ED25519_BTAB16_STRIDE;
+btabw_bytes( int kind ) {
+  return sizeof(int32_t) * ((size_t)1 << btab_kind_bits( kind )) * FD_ED25519_BTAB16_STRIDE;
 }
 
 static int
-btabw_acquire( int device, hipStream_t stream, int32_t * tab[2] ) {
+btabw_acquire( int device, int kind, hipStream_t stream, int32_t * tab[2] ) {
   if( device<0 || device>=FD_ED25519_HIP_MAX_DEV ) {
     snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "device %d out of range", device );
     return FD_ED25519_HIP_ERR_INVAL;
   }
   pthread_mutex_lock( &btabw_lock );
   int rc = FD_ED25519_HIP_OK;
-  if( !btabw[device].refs ) {
+  int bits = btab_kind_bits( kind );
+  if( !btabw[kind][device].refs ) {
     int32_t * t[2] = { NULL, NULL };
     int32_t * scratch = NULL;
-    hipError_t he = hipMalloc( (void **)&t[0], btabw_bytes() );
-    if( he==hipSuccess ) he = hipMalloc( (void **)&t[1], btabw_bytes() );
-    if( he==hipSuccess ) he = hipMalloc( (void **)&scratch, sizeof(int32_t) * ((size_t)FD_ED25519_BTABW_ENTRIES * 10 + 64) );
-    if( he==hipSuccess ) he = (hipError_t)fd_ed25519_hip_launch_gen_btabw( t[0], 0, scratch, stream );
-    if( he==hipSuccess ) he = (hipError_t)fd_ed25519_hip_launch_gen_btabw( t[1], FD_ED25519_BTABW_SHIFT, scratch, stream );
+    hipError_t he = hipMalloc( (void **)&t[0], btabw_bytes( kind ) );
+    if( he==hipSuccess ) he = hipMalloc( (void **)&t[1], btabw_bytes( kind ) );
+    if( he==hipSuccess ) he = hipMalloc( (void **)&scratch, sizeof(int32_t) * (((size_t)1 << bits) * 10 + 64) );
+    if( he==hipSuccess ) he = (hipError_t)fd_ed25519_hip_launch_gen_btabw( t[0], 0, bits, scratch, stream );
+    if( he==hipSuccess ) he = (hipError_t)fd_ed25519_hip_launch_gen_btabw( t[1], FD_ED25519_BTABW_SHIFT, bits, scratch, stream );
     if( he==hipSuccess ) he = hipStreamSynchronize( stream );
     hipFree( scratch );
     if( he!=hipSuccess ) {
       hipFree( t[0] ); hipFree( t[1] );
       rc = hip_fail( he, "base tables (btabw)" );
     } else {
-      btabw[device].tab[0] = t[0];
-      btabw[device].tab[1] = t[1];
+      btabw[kind][device].tab[0] = t[0];
+      btabw[kind][device].tab[1] = t[1];
     }
   }
   if( rc==FD_ED25519_HIP_OK ) {
-    btabw[device].refs++;
-    tab[0] = btabw[device].tab[0];
-    tab[1] = btabw[device].tab[1];
+    btabw[kind][device].refs++;
+    tab[0] = btabw[kind][device].tab[0];
+    tab[1] = btabw[kind][device].tab[1];
   }
   pthread_mutex_unlock( &btabw_lock );
   return rc;
@@ -184,20 +192,26 @@ unsigned long
 fd_ed25519_hip_shared_device_bytes( int device ) {
   if( device<0 || device>=FD_ED25519_HIP_MAX_DEV ) return 0UL;
   pthread_mutex_lock( &btabw_lock );
-  unsigned long b = btabw[device].refs ? 2UL*btabw_bytes() : 0UL;
+  unsigned long b = 0UL;
+  for( int kind=0; kind<2; kind++ ) if( btabw[kind][device].refs ) b += 2UL*btabw_bytes( kind );
   pthread_mutex_unlock( &btabw_lock );
   return b;
 }
 
 static void
-btabw_release( int device ) {
+btabw_release( int device, int kind ) {
   pthread_mutex_lock( &btabw_lock );
-  if( btabw[device].refs>0 && !--btabw[device].refs ) {
-    hipFree( btabw[device].tab[0] );
-    hipFree( btabw[device].tab[1] );
-    btabw[device].tab[0] = btabw[device].tab[1] = NULL;
+  if( btabw[kind][device].refs>0 && !--btabw[kind][device].refs ) {
+    hipFree( btabw[kind][device].tab[0] );
+    hipFree( btabw[kind][device].tab[1] );
+    btabw[kind][device].tab[0] = btabw[kind][device].tab[1] = NULL;
   }
   pthread_mutex_unlock( &btabw_lock );
+}
+
+static int
+engine_btab_kind( fd_ed25519_hip_engine_t const * e ) {
+  return (e->flags & FD_ED25519_HIP_FLAG_COMPACT_TABLES) ? 1 : 0;
 }
 
 /* The device's stream set.  A process gets GPU_MAX_HW_QUEUES hardware
@@ -289,7 +303,7 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   }
   hipFree( e->d_btab ); hipFree( e->d_btab16 );
   for( int l=0; l<2; l++ ) { hipFree( e->lane[l].d_atab ); hipFree( e->lane[l].d_work ); }
-  if( e->btabw[0] ) btabw_release( e->device );
+  if( e->btabw[0] ) btabw_release( e->device, engine_btab_kind( e ) );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
   hipHostFree( e->h_msgs ); hipHostFree( e->h_off ); hipHostFree( e->h_sz ); hipHostFree( e->h_sigs );
@@ -436,7 +450,7 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   if( err ) return hip_fail( (hipError_t)err, "gen_btab16 launch" );
   HIPCHK( hipStreamSynchronize( e->stream ), "gen_btab" );
   int32_t * tw[2] = { NULL, NULL };
-  err = btabw_acquire( e->device, e->stream, tw );
+  err = btabw_acquire( e->device, engine_btab_kind( e ), e->stream, tw );
   if( err ) return err;
   e->btabw[0] = tw[0];
   e->btabw[1] = tw[1];
@@ -593,6 +607,7 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
   p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
   p.cap = e->max_chunk;
   p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab_lo = e->btabw[0]; p.btab_hi = e->btabw[1];
+  p.bw_bits = engine_btab_kind( e ) ? FD_ED25519_BTABC_BITS : FD_ED25519_BTABW_BITS;
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   p.half_dbits     = engine_half_dbits( e );
   uint64_t chunk = e->max_chunk;
@@ -675,7 +690,8 @@ fd_ed25519_hip_engine_check_base_tables( fd_ed25519_hip_engine_t * e, unsigned l
   HIPCHK( hipMalloc( (void **)&d_bad, 3*sizeof(uint32_t) ), "hipMalloc" );
   uint32_t h_bad[3] = { 0U, 0U, 0U };
   int32_t const * tab[3] = { e->btabw[0], e->btabw[1], e->d_btab16 };
-  int             cnt[3] = { FD_ED25519_BTABW_ENTRIES, FD_ED25519_BTABW_ENTRIES, FD_ED25519_BTAB16_ENTRIES };
+  int             ent    = 1 << btab_kind_bits( engine_btab_kind( e ) );
+  int             cnt[3] = { ent, ent, FD_ED25519_BTAB16_ENTRIES };
   hipError_t he = hipMemsetAsync( d_bad, 0, 3*sizeof(uint32_t), e->stream );
   for( int t=0; t<3 && he==hipSuccess; t++ )
     he = (hipError_t)fd_ed25519_hip_launch_check_btabw( tab[t], cnt[t], d_bad + t, e->stream );
@@ -689,7 +705,7 @@ fd_ed25519_hip_engine_check_base_tables( fd_ed25519_hip_engine_t * e, unsigned l
 
 int
 fd_ed25519_hip_engine_base_entry( fd_ed25519_hip_engine_t * e, int which, unsigned long index, int out[30] ) {
-  if( !e || !out || which<0 || which>1 || index>=(unsigned long)FD_ED25519_BTABW_ENTRIES || !e->btabw[which] )
+  if( !e || !out || which<0 || which>1 || index>=(1UL << btab_kind_bits( engine_btab_kind( e ) )) || !e->btabw[which] )
     return FD_ED25519_HIP_ERR_INVAL;
   HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
   HIPCHK( hipMemcpyAsync( out, e->btabw[which] + index*FD_ED25519_BTAB16_STRIDE, 30*sizeof(int32_t),
@@ -955,29 +971,66 @@ fd_ed25519_hip_verify_txns_host( fd_ed25519_hip_engine_t * e, unsigned long ntxn
   return FD_ED25519_HIP_OK;
 }
 
-/* ---- drop-in API ------------------------------------------------------- */
+/* ---- drop-in API -------------------------------------------------------
 
-static pthread_once_t           default_once = PTHREAD_ONCE_INIT;
-static pthread_mutex_t          default_lock = PTHREAD_MUTEX_INITIALIZER;
-static fd_ed25519_hip_engine_t * default_engine;
+   fd_ed25519_verify / fd_ed25519_verify_batch_single_msg for any number of
+   calling threads (the reference's are reentrant and keep no global state,
+   src/ballet/ed25519/fd_ed25519.h:86-94).  Concurrent calls are coalesced
+   by flat combining: each call queues a request; a caller that finds one
+   of the process's DROPIN_ENGINES drop-in engines idle takes every queued
+   request (its own and the others', up to DROPIN_BATCH_MAX) into one
+   launch -- each request one transaction of 1..16 signatures over its
+   message, with batch_single_msg's combine -- and hands every caller its
+   code; the others wait on a condition variable.  One caller alone pays
+   one GPU round trip as before; N concurrent callers share a round trip,
+   and two engines keep a second batch filling while one is on the GPU, so
+   calls per second grow with the caller count instead of serialising on
+   one lock.  The engines use the compact base tables
+   (FD_ED25519_HIP_FLAG_COMPACT_TABLES: 2 x 8 MiB instead of 2 x 2 GiB) and
+   small chunks, so a process that only uses the drop-ins holds well under
+   600 MB of device memory. */
+
+#define DROPIN_ENGINES   2
+#define DROPIN_BATCH_MAX 4096UL
+#define DROPIN_CHUNK     16384UL
+
+typedef struct dropin_req {
+  unsigned char const * msg;
+  unsigned int          msg_sz;
+  unsigned char const * sigs;
+  unsigned char const * pubs;
+  unsigned int          cnt;      /* signatures, 1..16                     */
+  int                   single;   /* fd_ed25519_verify: the signature's code */
+  int                   result;
+  int                   done;
+  struct dropin_req *   next;
+} dropin_req_t;
+
+static pthread_once_t  dropin_once = PTHREAD_ONCE_INIT;
+static pthread_mutex_t dropin_lock = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t  dropin_cv   = PTHREAD_COND_INITIALIZER;
+static struct {
+  fd_ed25519_hip_engine_t * eng[ DROPIN_ENGINES ];
+  int                       busy[ DROPIN_ENGINES ];
+  dropin_req_t *            head;
+  dropin_req_t *            tail;
+  unsigned long             launches, requests;   /* for fd_ed25519_hip_dropin_stats */
+} dq;
 
 static void
-default_init( void ) {
+dropin_init( void ) {
   char const * dev_s   = getenv( "FD_ED25519_HIP_DEVICE" );
   char const * codes_s = getenv( "FD_ED25519_HIP_CODES" );
   int dev   = dev_s ? atoi( dev_s ) : 0;
-  int flags = (codes_s && !strcmp( codes_s, "portable" )) ? FD_ED25519_HIP_FLAG_CODES_PORTABLE : 0;
-  default_engine = fd_ed25519_hip_engine_new( dev, 1UL<<16, flags );
-}
-
-static fd_ed25519_hip_engine_t *
-default_get( void ) {
-  pthread_once( &default_once, default_init );
-  if( !default_engine ) {
-    fprintf( stderr, "libfd_ed25519_hip: FATAL: cannot create the GPU engine: %s\n", fd_ed25519_hip_last_error() );
-    abort();
+  int flags = FD_ED25519_HIP_FLAG_COMPACT_TABLES | FD_ED25519_HIP_FLAG_ONE_STREAM |
+              ((codes_s && !strcmp( codes_s, "portable" )) ? FD_ED25519_HIP_FLAG_CODES_PORTABLE : 0);
+  for( int k=0; k<DROPIN_ENGINES; k++ ) {
+    dq.eng[k] = fd_ed25519_hip_engine_new( dev, DROPIN_CHUNK, flags );
+    if( !dq.eng[k] ) {
+      fprintf( stderr, "libfd_ed25519_hip: FATAL: cannot create the GPU engine: %s\n", fd_ed25519_hip_last_error() );
+      abort();
+    }
   }
-  return default_engine;
 }
 
 static void
@@ -987,10 +1040,94 @@ dropin_fatal( int err ) {
   abort();
 }
 
+/* one combined launch of the requests in list (n of them) on engine e:
+   packed into the engine's pinned staging as transactions, verified, the
+   per-transaction combine, codes back */
+static int
+dropin_run( fd_ed25519_hip_engine_t * e, dropin_req_t * list, unsigned long n ) {
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  uint64_t nsig = 0UL, bytes = 0UL;
+  for( dropin_req_t * r=list; r; r=r->next ) { nsig += r->cnt; bytes += r->msg_sz; }
+  int err;
+  if( (err = stage_sigs( e, nsig )) ) return err;
+  if( (err = stage_msgs( e, bytes )) ) return err;
+  if( (err = stage_txns( e, n )) ) return err;
+  uint64_t pos = 0UL, k = 0UL, t = 0UL;
+  for( dropin_req_t * r=list; r; r=r->next, t++ ) {
+    if( r->msg_sz ) memcpy( e->h_msgs + pos, r->msg, r->msg_sz );
+    e->h_tfirst[t] = (uint32_t)k;
+    e->h_tcnt  [t] = r->cnt;
+    memcpy( e->h_sigs + 64UL*k, r->sigs, 64UL*r->cnt );
+    memcpy( e->h_pubs + 32UL*k, r->pubs, 32UL*r->cnt );
+    for( uint32_t j=0U; j<r->cnt; j++, k++ ) { e->h_off[k] = pos; e->h_sz[k] = r->msg_sz; }
+    pos += r->msg_sz;
+  }
+  if( (err = upload_and_verify( e, nsig, bytes )) ) return err;
+  HIPCHK( hipMemcpyAsync( e->d_tfirst, e->h_tfirst, 4UL*n, hipMemcpyHostToDevice, e->stream ), "H2D tfirst" );
+  HIPCHK( hipMemcpyAsync( e->d_tcnt,   e->h_tcnt,   4UL*n, hipMemcpyHostToDevice, e->stream ), "H2D tcnt" );
+  if( (err = fd_ed25519_hip_txn_combine_dev( e, n, (signed char const *)e->d_out, e->d_tfirst, e->d_tcnt,
+                                             (signed char *)e->d_tout, e->stream )) ) return err;
+  HIPCHK( hipMemcpyAsync( e->h_tout, e->d_tout, n, hipMemcpyDeviceToHost, e->stream ), "D2H tout" );
+  HIPCHK( hipMemcpyAsync( e->h_out, e->d_out, nsig, hipMemcpyDeviceToHost, e->stream ), "D2H out" );
+  HIPCHK( hipStreamSynchronize( e->stream ), "drop-in verify" );
+  t = 0UL;
+  for( dropin_req_t * r=list; r; r=r->next, t++ )
+    r->result = r->single ? (int)e->h_out[ e->h_tfirst[t] ] : (int)e->h_tout[t];
+  return FD_ED25519_HIP_OK;
+}
+
+static int
+dropin_submit( dropin_req_t * r ) {
+  pthread_once( &dropin_once, dropin_init );
+  r->done = 0; r->next = NULL;
+  pthread_mutex_lock( &dropin_lock );
+  if( dq.tail ) dq.tail->next = r; else dq.head = r;
+  dq.tail = r;
+  while( !r->done ) {
+    int k = -1;
+    for( int i=0; i<DROPIN_ENGINES; i++ ) if( !dq.busy[i] ) { k = i; break; }
+    if( k<0 || !dq.head ) { pthread_cond_wait( &dropin_cv, &dropin_lock ); continue; }
+    /* combine: take up to DROPIN_BATCH_MAX queued requests onto engine k */
+    dropin_req_t * list = dq.head, * last = dq.head;
+    unsigned long n = 1UL;
+    while( last->next && n<DROPIN_BATCH_MAX ) { last = last->next; n++; }
+    dq.head = last->next;
+    if( !dq.head ) dq.tail = NULL;
+    last->next = NULL;
+    dq.busy[k] = 1;
+    dq.launches++; dq.requests += n;
+    pthread_mutex_unlock( &dropin_lock );
+    int err = dropin_run( dq.eng[k], list, n );
+    if( err ) dropin_fatal( err );
+    pthread_mutex_lock( &dropin_lock );
+    for( dropin_req_t * q=list; q; ) { dropin_req_t * nx = q->next; q->done = 1; q = nx; }
+    dq.busy[k] = 0;
+    pthread_cond_broadcast( &dropin_cv );
+  }
+  pthread_mutex_unlock( &dropin_lock );
+  return r->result;
+}
+
+void
+fd_ed25519_hip_dropin_stats( unsigned long * launches, unsigned long * requests ) {
+  pthread_mutex_lock( &dropin_lock );
+  if( launches ) *launches = dq.launches;
+  if( requests ) *requests = dq.requests;
+  pthread_mutex_unlock( &dropin_lock );
+}
+
+unsigned long
+fd_ed25519_hip_dropin_device_bytes( void ) {
+  pthread_once( &dropin_once, dropin_init );
+  unsigned long b = 0UL;
+  for( int k=0; k<DROPIN_ENGINES; k++ ) b += dq.eng[k]->device_bytes;
+  return b + fd_ed25519_hip_shared_device_bytes( dq.eng[0]->device );
+}
+
 /* The device path carries message sizes as 32-bit values.  The reference
    takes any ulong size; a larger message must never be verified as its
    truncated prefix (that would accept a signature over the prefix), so it
-   fails loudly like any other GPU failure. */
+   fails loudly like any other GPU failure (INTEGRATION.md section 1). */
 static unsigned int
 dropin_msg_sz( unsigned long msg_sz ) {
   if( msg_sz>(unsigned long)UINT32_MAX ) {
@@ -1005,16 +1142,9 @@ int
 fd_ed25519_verify( unsigned char const msg[], unsigned long msg_sz, unsigned char const sig[ 64 ],
                    unsigned char const public_key[ 32 ], fd_sha512_t * sha ) {
   (void)sha;
-  unsigned int  sz  = dropin_msg_sz( msg_sz );
-  fd_ed25519_hip_engine_t * e = default_get();
-  unsigned long off = 0UL;
-  signed char   out = 0;
-  static unsigned char const empty[1] = {0};
-  pthread_mutex_lock( &default_lock );
-  int err = fd_ed25519_hip_verify_host( e, 1UL, msg ? msg : empty, &off, &sz, sig, public_key, &out );
-  pthread_mutex_unlock( &default_lock );
-  if( err ) dropin_fatal( err );
-  return (int)out;
+  dropin_req_t r;
+  r.msg = msg; r.msg_sz = dropin_msg_sz( msg_sz ); r.sigs = sig; r.pubs = public_key; r.cnt = 1U; r.single = 1;
+  return dropin_submit( &r );
 }
 
 int
@@ -1023,17 +1153,10 @@ fd_ed25519_verify_batch_single_msg( unsigned char const msg[], unsigned long con
                                     fd_sha512_t * shas[ 1 ], unsigned char const batch_sz ) {
   (void)shas;
   if( batch_sz==0 || batch_sz>16 ) return FD_ED25519_ERR_SIG;
-  unsigned int  sz = dropin_msg_sz( msg_sz ), first = 0U, cnt = batch_sz;
-  fd_ed25519_hip_engine_t * e = default_get();
-  unsigned long off = 0UL;
-  signed char   out = 0;
-  static unsigned char const empty[1] = {0};
-  pthread_mutex_lock( &default_lock );
-  int err = fd_ed25519_hip_verify_txns_host( e, 1UL, msg ? msg : empty, &off, &sz, &first, &cnt, signatures,
-                                             pubkeys, &out, NULL );
-  pthread_mutex_unlock( &default_lock );
-  if( err ) dropin_fatal( err );
-  return (int)out;
+  dropin_req_t r;
+  r.msg = msg; r.msg_sz = dropin_msg_sz( msg_sz ); r.sigs = signatures; r.pubs = pubkeys; r.cnt = batch_sz;
+  r.single = 0;
+  return dropin_submit( &r );
 }
 
 char const *

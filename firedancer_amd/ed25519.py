@@ -30,6 +30,7 @@ FLAG_DSM_OCT = 16        # dsm with two quads of lanes per signature at every ch
 FLAG_ONE_STREAM = 32     # no decode side stream / second lane: for engines whose batches overlap one another
 FLAG_NO_OVERLAP = 64     # a large chunk's phases in sequence (no decode side stream): tests / A-B
 FLAG_NO_PIPELINE = 128   # a multi-chunk call on one set of work arrays (no second lane): tests / A-B
+FLAG_COMPACT_TABLES = 256  # radix-2^16 base tables (2 x 8 MiB, shared) instead of radix 2^24 (2 x 2 GiB)
 
 # phases of a verify launch (FD_ED25519_HIP_PHASE_CNT, include/fd_ed25519_hip.h)
 PHASES = ("hash", "scalar", "decode", "dsm")
@@ -143,11 +144,12 @@ class Engine:
     """A libfd_ed25519_hip engine bound to one GPU."""
 
     def __init__(self, device=0, max_chunk=0, codes="avx512", half="extended", dsm="auto", one_stream=False,
-                 overlap=True, pipeline=True, forms=None):
+                 overlap=True, pipeline=True, forms=None, compact=False):
         flags = FLAG_CODES_PORTABLE if codes == "portable" else 0
         flags |= FLAG_ONE_STREAM if one_stream else 0
         flags |= 0 if overlap else FLAG_NO_OVERLAP
         flags |= 0 if pipeline else FLAG_NO_PIPELINE
+        flags |= FLAG_COMPACT_TABLES if compact else 0
         flags |= FLAG_HALF_STRICT if half == "strict" else 0
         flags |= {"auto": 0, "quad": FLAG_DSM_QUAD, "wide": FLAG_DSM_WIDE, "oct": FLAG_DSM_OCT}[dsm]
         self._h = _lib.fd_ed25519_hip_engine_new(int(device), int(max_chunk), flags)
@@ -343,6 +345,28 @@ class DeviceWorkload:
 
 
 _lib.fd_ed25519_hip_device_count.restype = ctypes.c_int
+
+
+_lib.fd_ed25519_hip_dropin_stats.argtypes = [ctypes.POINTER(ctypes.c_ulong), ctypes.POINTER(ctypes.c_ulong)]
+_lib.fd_ed25519_hip_dropin_device_bytes.restype = ctypes.c_ulong
+_lib.fd_ed25519_hip_shared_device_bytes.argtypes = [ctypes.c_int]
+_lib.fd_ed25519_hip_shared_device_bytes.restype = ctypes.c_ulong
+
+
+def dropin_stats():
+    """(launches, calls): the drop-ins' combined launches and the calls they carried."""
+    a, b = ctypes.c_ulong(), ctypes.c_ulong()
+    _lib.fd_ed25519_hip_dropin_stats(ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def dropin_device_bytes():
+    """Device memory the drop-ins hold: their engines plus the process's shared base tables."""
+    return _lib.fd_ed25519_hip_dropin_device_bytes()
+
+
+def shared_device_bytes(device=0):
+    return _lib.fd_ed25519_hip_shared_device_bytes(int(device))
 
 
 def device_count():

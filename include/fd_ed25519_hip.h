@@ -75,6 +75,18 @@ fd_ed25519_verify_batch_single_msg( unsigned char const   msg[],
 char const *
 fd_ed25519_strerror( int err );
 
+/* The drop-ins above serve any number of calling threads: concurrent calls
+   are coalesced into shared launches on the process's two drop-in engines
+   (compact tables, 16K-signature chunks).  dropin_stats reports the
+   launches made and the calls they carried; dropin_device_bytes the device
+   memory the drop-ins hold (their engines plus the compact tables; it
+   creates them if no call has yet). */
+void
+fd_ed25519_hip_dropin_stats( unsigned long * launches, unsigned long * requests );
+
+unsigned long
+fd_ed25519_hip_dropin_device_bytes( void );
+
 /* ---- Part 2: batch engine -------------------------------------------- */
 
 typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
@@ -113,6 +125,12 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    variable for its launch forms. */
 #define FD_ED25519_HIP_FLAG_NO_OVERLAP     (64)
 #define FD_ED25519_HIP_FLAG_NO_PIPELINE    (128)
+/* The half-size form's two base tables at radix 2^16 ([0..2^16)B and
+   [0..2^16)[2^144]B, 8 MiB each, shared by the process's compact engines
+   of a device) instead of radix 2^24 (2 GiB each): 9 + 7 instead of 6 + 5
+   mixed additions per signature, same verdicts.  For processes that verify
+   little and should not hold 4 GiB of device memory; the drop-ins use it. */
+#define FD_ED25519_HIP_FLAG_COMPACT_TABLES (256)
 #define FD_ED25519_HIP_QUAD_MAX_DEFAULT    (32768UL)
 #define FD_ED25519_HIP_OCT_MAX_DEFAULT     (8192UL)
 /* Overlap: a large chunk's decode phase (A and R need neither the hash nor
@@ -322,8 +340,11 @@ fd_ed25519_hip_engine_timing_read( fd_ed25519_hip_engine_t * engine,
    entry 0 not the identity); together with a few
    entries compared against an independent [s]B (base_entry), a zero count
    proves the whole table.  base_entry copies entry `index` of table
-   `which` (30 int32) to the host. */
+   `which` (30 int32) to the host.  An engine with
+   FD_ED25519_HIP_FLAG_COMPACT_TABLES has the 2^FD_ED25519_HIP_COMPACT_TABLE_BITS-entry
+   pair instead. */
 #define FD_ED25519_HIP_BASE_TABLE_BITS  24
+#define FD_ED25519_HIP_COMPACT_TABLE_BITS 16
 #define FD_ED25519_HIP_BASE_TABLE_SHIFT 144
 
 int

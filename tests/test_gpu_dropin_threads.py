@@ -1,0 +1,128 @@
+"""The drop-in fd_ed25519_verify / fd_ed25519_verify_batch_single_msg under
+concurrent callers (the reference's are reentrant, src/ballet/ed25519/
+fd_ed25519.h:86-94): calls from many threads are coalesced into shared
+launches, every caller gets its own code, and a process that only uses the
+drop-ins holds its compact base tables, not the 4 GiB wide ones."""
+import json
+import os
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def fd():
+    from firedancer_amd import ed25519
+    return ed25519
+
+
+def _calls(vectors, idx):
+    out = []
+    for i in idx:
+        off, sz = int(vectors["msg_off"][i]), int(vectors["msg_sz"][i])
+        out.append((bytes(vectors["msgs"][off:off + sz]), vectors["sigs"][i].tobytes(), vectors["pubs"][i].tobytes(),
+                    int(vectors["codes_avx512"][i]), str(vectors["tags"][i])))
+    return out
+
+
+def test_dropin_threads_parity_and_coalescing(fd, vectors, batch):
+    """16 threads call fd_ed25519_verify (the reference's vector set, each
+    thread a slice, several passes) and 4 more call batch_single_msg at the
+    same time: every code is the reference's, and the launches carried
+    more than one call each on average (coalesced)."""
+    n = len(vectors["msg_sz"])
+    calls = _calls(vectors, range(n))
+    l0, r0 = fd.dropin_stats()
+    errors = []
+
+    def single(k):
+        for m, s, p, want, tag in calls[k::16] * 3:
+            got = fd.verify(m, s, p)
+            if got != want:
+                errors.append(("single", tag, got, want))
+
+    def multi(k):
+        for t in range(k, len(batch["txn_cnt"]), 4):
+            off, sz = int(batch["txn_msg_off"][t]), int(batch["txn_msg_sz"][t])
+            f, c = int(batch["txn_first"][t]), int(batch["txn_cnt"][t])
+            got = fd.verify_batch_single_msg(bytes(batch["msgs"][off:off + sz]), batch["sigs"][f:f + c].tobytes(),
+                                             batch["pubs"][f:f + c].tobytes(), c)
+            if got != int(batch["codes_avx512"][t]):
+                errors.append(("batch", t, got, int(batch["codes_avx512"][t])))
+
+    th = [threading.Thread(target=single, args=(k,)) for k in range(16)]
+    th += [threading.Thread(target=multi, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th)
+    assert not errors, errors[:10]
+    l1, r1 = fd.dropin_stats()
+    launches, reqs = l1 - l0, r1 - r0
+    assert reqs == 3 * n + len(range(0, len(batch["txn_cnt"])))
+    assert launches < reqs   # coalesced: fewer GPU round trips than calls
+
+
+def test_dropin_calls_scale_with_threads(fd):
+    """Calls per second with 1, 2, 4, 8 calling threads (200-byte messages):
+    more threads share launches, so the rate grows instead of serialising
+    on one lock; the single-thread latency is the one GPU round trip."""
+    from firedancer_amd import workload
+    eng = fd.Engine(0, max_chunk=1 << 12)
+    wl = fd.DeviceWorkload(eng, 256, 200, 200, 0, seed=99)
+    msgs = wl.msgs.download(np.uint8, 256 * 200)
+    sigs = wl.sigs.download(np.uint8, 64 * 256).reshape(256, 64)
+    pubs = wl.pubs.download(np.uint8, 32 * 256).reshape(256, 32)
+    wl.free()
+    eng.close()
+    calls = [(msgs[200 * i:200 * i + 200].tobytes(), sigs[i].tobytes(), pubs[i].tobytes()) for i in range(256)]
+    fd.verify(*calls[0])   # engines up
+    res = {}
+    for nth in (1, 2, 4, 8):
+        per = 400 // nth if nth > 1 else 200
+        lat = []
+        bad = []
+
+        def run(k):
+            for j in range(per):
+                m, s, p = calls[(k * 31 + j) % 256]
+                t = time.perf_counter()
+                if fd.verify(m, s, p) != 0:
+                    bad.append(j)
+                lat.append(time.perf_counter() - t)
+        th = [threading.Thread(target=run, args=(k,)) for k in range(nth)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        dt = time.perf_counter() - t0
+        assert not bad
+        res[nth] = {"calls_per_s": nth * per / dt, "p50_us": float(np.percentile(lat, 50) * 1e6),
+                    "p99_us": float(np.percentile(lat, 99) * 1e6)}
+    print(json.dumps({"dropin_thread_scaling": res}))
+    assert res[8]["calls_per_s"] > 3.0 * res[1]["calls_per_s"], res
+    assert res[1]["p50_us"] < 1000, res
+
+
+def test_dropin_only_process_device_bytes():
+    """A process that only calls the drop-ins: its device memory is the two
+    drop-in engines plus the compact base tables (2 x 8 MiB), well under
+    600 MB -- not the 2 x 2 GiB wide tables."""
+    code = ("import sys; sys.path.insert(0, %r); from firedancer_amd import ed25519 as e; "
+            "print(e.verify(b'', bytes(64), bytes(32)), e.dropin_device_bytes(), e.shared_device_bytes(0))" % REPO)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rc, dev, shared = (int(x) for x in r.stdout.split())
+    assert rc != 0   # an all-zero signature is refused
+    assert shared == 2 * (1 << 16) * 128
+    assert dev < 600 * 1000 * 1000, dev

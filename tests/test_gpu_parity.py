@@ -22,10 +22,13 @@ def fd():
 
 # Every engine test runs with each dsm form: two quads of lanes per
 # signature (chunks of up to FD_ED25519_HIP_OCT_MAX_DEFAULT signatures), a
-# quad (up to FD_ED25519_HIP_QUAD_MAX_DEFAULT) and one lane per signature.
-@pytest.fixture(scope="module", params=["oct", "quad", "wide"])
+# quad (up to FD_ED25519_HIP_QUAD_MAX_DEFAULT) and one lane per signature;
+# each with the wide radix-2^24 base tables and with the compact radix-2^16
+# ones (FD_ED25519_HIP_FLAG_COMPACT_TABLES, the drop-ins' engines).
+@pytest.fixture(scope="module", params=["oct", "quad", "wide", "oct-compact", "quad-compact", "wide-compact"])
 def eng(fd, request):
-    e = fd.Engine(0, max_chunk=1 << 16, dsm=request.param)
+    form, _, compact = request.param.partition("-")
+    e = fd.Engine(0, max_chunk=1 << 16, dsm=form, compact=bool(compact))
     yield e
     e.close()
 
@@ -150,8 +153,8 @@ def test_long_messages_vs_oracle(eng, oracle):
     _check(_run(eng, d), want)
 
 
-def test_scalar_edges(eng, oracle):
-    """S around L and all-ones; S+kL for small k."""
+def test_scalar_edges(eng, eng_portable, oracle):
+    """S around L and all-ones; S+kL for small k; both code flavours."""
     d = _random_set(oracle, 64, seed=13, mutate=False)
     sigs = d["sigs"].copy()
     for i in range(64):
@@ -159,10 +162,8 @@ def test_scalar_edges(eng, oracle):
         choice = [S, S + L, L - 1, L, L + 1, 2**256 - 1, 0, 2**253, S + 2 * L, 2**255 + S][i % 10]
         sigs[i, 32:] = np.frombuffer((choice % 2**256).to_bytes(32, "little"), np.uint8)
     d["sigs"] = sigs
-    for codes in (0, 1):
-        pass
-    want = oracle_many(oracle, d, 0)
-    _check(_run(eng, d), want)
+    _check(_run(eng, d), oracle_many(oracle, d, 0))
+    _check(_run(eng_portable, d), oracle_many(oracle, d, 1))
 
 
 def test_chunking(fd, oracle):
@@ -335,15 +336,17 @@ def test_engines_share_base_tables(fd, adversarial):
     d.close()
 
 
-def test_base_tables_are_exact(fd, oracle):
+@pytest.mark.parametrize("compact", [False, True], ids=["wide", "compact"])
+def test_base_tables_are_exact(fd, oracle, compact):
     """The half-size form's 2 x 2^24-entry base tables (and the full-length
     form's 2^15 + 1): on the device every
     entry e+1 equals entry e + entry 1 (entry 0 the identity), and entries
     1, 2, the run boundaries of the generator (runs of 32), the middle and
     the last, plus random ones, equal the oracle's [e 2^shift]B -- anchors
     that, with the chain, pin every entry; 2dxy checked too."""
-    eng = fd.Engine(0, max_chunk=1 << 12)
+    eng = fd.Engine(0, max_chunk=1 << 12, compact=compact)
     assert eng.check_base_tables() == (0, 0, 0)
+    bits = 16 if compact else 24
     P = 2**255 - 19
     L = 2**252 + 27742317777372353535851937790883648493
     d = (-121665 * pow(121666, P - 2, P)) % P
@@ -353,8 +356,9 @@ def test_base_tables_are_exact(fd, oracle):
         return sum(int(l) << o for l, o in zip(limbs, off)) % P
 
     rng = np.random.default_rng(7)
-    idx = [1, 2, 3, 31, 32, 33, 63, 64, 1 << 23, (1 << 24) - 33, (1 << 24) - 32, (1 << 24) - 2, (1 << 24) - 1]
-    idx += [int(x) for x in rng.integers(1, 1 << 24, 8)]
+    top = 1 << bits
+    idx = [1, 2, 3, 31, 32, 33, 63, 64, top >> 1, top - 33, top - 32, top - 2, top - 1]
+    idx += [int(x) for x in rng.integers(1, top, 8)]
     for which, shift in ((0, 0), (1, fd.BASE_TABLE_SHIFT)):
         for e in idx:
             ent = eng.base_entry(which, e)
