@@ -1,6 +1,7 @@
 /* fd25519_dsm.h -- device helpers shared by the verify and generator
    kernels: point decoding with the reference's acceptance rules, signed
-   fixed-window scalar recoding, and the -A (HBM) / B (LDS) table accessors. */
+   fixed-window scalar recoding, and the table accessors: per-lane -A / -+R
+   tables and the base tables in HBM (verify), [0..128]B in LDS (signing). */
 #pragma once
 #include "fd25519_ge.h"
 #include "fd_ed25519_hip_internal.h"

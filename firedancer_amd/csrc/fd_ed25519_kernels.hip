@@ -3,28 +3,34 @@
    Verification of a batch: every step of fd_ed25519_verify
    (src/ballet/ed25519/fd_ed25519_user.c:134-229) for every signature, with
    the verdict computed as data (no early exits, so a wave never diverges on
-   an invalid signature), in three phase kernels (see "Phase kernels"):
+   an invalid signature), in four phase kernels (see "Phase kernels"):
 
      1. S < L                          (fd_curve25519_scalar_validate)
      2. decode A and R, reject on no square root (and, in AVX-512 code mode,
         x == 0 with the sign bit set)  (fd_ed25519_point_frombytes_2x)
      3. small-order A, then R          (fd_ed25519_affine_is_small_order)
      4. k = SHA-512(R||A||M) mod L     (fd_sha512_*, fd_curve25519_scalar_reduce)
-     5. R' = [k](-A) + [S]B            (fd_ed25519_double_scalar_mul_base)
-     6. R' == R projectively           (fd_ed25519_point_eq_z1)
+     5. the group equation [S]B - R - [k]A == 0, cofactorless, as the
+        reference's R' = [k](-A) + [S]B == R (fd_ed25519_double_scalar_mul_base,
+        fd_ed25519_point_eq_z1)
 
-   Steps 2-3 for R and step 6 are done together, without decompressing R,
-   by comparing the encoding of R' with R's bytes (fin, below).
+   R is decoded (step 2, the decode kernel) and enters the equation as a
+   point.  Step 5 runs, for all but ~1e-6 of signatures, in the half-size
+   form: with c == d k (mod 8L), d odd (the scalar kernel, fd25519_half.h,
+   every pair re-checked with integers only), [c](-A) + [|d|](-+R) +
+   [s_lo]B + [s_hi][2^144]B == 0 in a four-scalar Straus loop of 33 signed
+   4-bit windows (dsm_half_one), exactly equivalent since [d] is invertible
+   on the group of order 8L; the rest in the full-length form
+   [k](-A) + [S]B == R (dsm_full_one).  Fixed windows instead of the
+   reference's sliding wNAF make every lane of a wave execute the same
+   additions; the group element is the same, so the verdict is
+   bit-identical.
 
-   Step 5 uses fixed signed windows instead of the reference's sliding
-   wNAF so that every lane of a wave executes the same additions: k in
-   radix 16 (64 digits in [-8,8], table [0..8](-A) per lane in HBM) and S in
-   radix 256 (32 digits in [-128,128], table [0..128]B shared in LDS).  The
-   group element computed is the same, so the verdict is bit-identical.
-
-   The dsm kernel is persistent: its grid is sized to the resident occupancy
-   and each lane strides over signatures, so the per-lane -A table lives in
-   a fixed HBM scratch of waves x 90 KiB. */
+   Tables: per-lane [1..8](-A) and [1..8](-+R) in an HBM scratch of the
+   persistent dsm grid (dynamically scheduled, 64 items per wave); the base
+   tables [0..2^24)B and [0..2^24)[2^144]B (or the compact radix-2^16 pair)
+   and [0..2^15]B (full-length form) in HBM, shared by the engines of a
+   device; [0..128]B in LDS for the signing kernels only. */
 #include <hip/hip_runtime.h>
 #include "fd25519_dsm.h"
 #include "fd25519_ge4.h"

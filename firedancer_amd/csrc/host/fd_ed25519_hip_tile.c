@@ -43,6 +43,27 @@ tile_fail( char const * what, hipError_t err ) {
     if( _e!=hipSuccess ) return tile_fail( what, _e ); \
   } while(0)
 
+unsigned
+fd_ed25519_hip_abi_version( void ) {
+  return FD_ED25519_HIP_ABI_VERSION;
+}
+
+int
+fd_ed25519_hip_abi_check( unsigned version, unsigned long slot_sz, unsigned long info_sz,
+                          unsigned long vservice_stats_sz ) {
+  if( version!=FD_ED25519_HIP_ABI_VERSION || slot_sz!=sizeof(fd_ed25519_hip_slot_t) ||
+      info_sz!=sizeof(fd_ed25519_hip_info_t) || vservice_stats_sz!=sizeof(fd_ed25519_hip_vservice_stats_t) ) {
+    char buf[ 200 ];
+    snprintf( buf, sizeof(buf), "ABI mismatch: caller v%u (%lu, %lu, %lu), library v%u (%lu, %lu, %lu)",
+              version, slot_sz, info_sz, vservice_stats_sz, FD_ED25519_HIP_ABI_VERSION,
+              (unsigned long)sizeof(fd_ed25519_hip_slot_t), (unsigned long)sizeof(fd_ed25519_hip_info_t),
+              (unsigned long)sizeof(fd_ed25519_hip_vservice_stats_t) );
+    fd_ed25519_hip_private_set_error( buf );
+    return FD_ED25519_HIP_ERR_INVAL;
+  }
+  return FD_ED25519_HIP_OK;
+}
+
 /* ======================================================================
    pipe */
 
@@ -1559,7 +1580,7 @@ fail:
 }
 
 static int
-pool_submit( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
+pool_enqueue( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
   fd_ed25519_hip_pool_t * pl = j->pool;
   unsigned long i0 = b*pl->batch_sigs, i1 = i0+pl->batch_sigs < j->n ? i0+pl->batch_sigs : j->n, cnt = i1-i0;
   hipStream_t st = (hipStream_t)fd_ed25519_hip_engine_stream( s->eng );
@@ -1615,6 +1636,17 @@ pool_submit( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
   s->i0 = i0; s->i1 = i1; s->busy = 1;
   return FD_ED25519_HIP_OK;
+}
+
+/* A batch whose enqueue failed part way may have left copies from or into
+   the caller's page-locked arrays on the slot's stream: they finish before
+   the error is reported, so pool_run never returns while DMA may still
+   touch memory the caller is free to release. */
+static int
+pool_submit( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
+  int err = pool_enqueue( j, s, b );
+  if( err ) hipStreamSynchronize( (hipStream_t)fd_ed25519_hip_engine_stream( s->eng ) );
+  return err;
 }
 
 static void *

@@ -544,6 +544,12 @@ _lib.fd_ed25519_hip_shlink_consume.argtypes = [_v, _v, ctypes.POINTER(ctypes.c_u
 _lib.fd_ed25519_hip_shlink_consume.restype = ctypes.c_int
 _lib.fd_ed25519_hip_vservice_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, ctypes.c_int, _v, _v,
                                              ctypes.POINTER(VServiceStats)]
+# the library and these ctypes mirrors must describe the same ABI
+_lib.fd_ed25519_hip_abi_check.argtypes = [ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong]
+ABI_VERSION = 3   # FD_ED25519_HIP_ABI_VERSION
+if _lib.fd_ed25519_hip_abi_check(ABI_VERSION, ctypes.sizeof(Slot), ctypes.sizeof(__import__(
+        "firedancer_amd.ed25519", fromlist=["_Info"])._Info), ctypes.sizeof(VServiceStats)) != 0:
+    raise ImportError("libfd_ed25519_hip ABI mismatch: " + _lib.fd_ed25519_hip_last_error().decode())
 _lib.fd_ed25519_hip_shlink_heartbeat.argtypes = [_v, ctypes.c_ulong]
 _lib.fd_ed25519_hip_shlink_heartbeat_query.argtypes = [_v]
 _lib.fd_ed25519_hip_shlink_heartbeat_query.restype = ctypes.c_ulong

@@ -91,6 +91,24 @@ fd_ed25519_hip_dropin_device_bytes( void );
 
 typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
 
+/* ABI version of the two headers (include/fd_ed25519_hip.h and
+   include/fd_ed25519_hip_tile.h): bumped whenever a flag's meaning, a
+   struct layout or a prototype changes (3: round 3 -- engine flags 64..256,
+   vservice stats' device bytes, shlink liveness words).  A consumer checks
+   the library it loaded against the header it was built with:
+   fd_ed25519_hip_abi_check( FD_ED25519_HIP_ABI_VERSION,
+   sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
+   sizeof(fd_ed25519_hip_vservice_stats_t) ) returns 0 when they agree,
+   FD_ED25519_HIP_ERR_INVAL (with fd_ed25519_hip_last_error) when not. */
+#define FD_ED25519_HIP_ABI_VERSION (3U)
+
+unsigned
+fd_ed25519_hip_abi_version( void );
+
+int
+fd_ed25519_hip_abi_check( unsigned version, unsigned long slot_sz, unsigned long info_sz,
+                          unsigned long vservice_stats_sz );
+
 /* Engine API status codes (not verdicts). */
 #define FD_ED25519_HIP_OK          (0)
 #define FD_ED25519_HIP_ERR_INVAL   (-22)   /* bad argument / misaligned device buffer */

@@ -8,11 +8,9 @@
    wycheproof / cctv tables, fd_log) is the reference's.  Exit 0 means the
    reference's tests passed against the GPU drop-ins.
 
-   test_ed25519.c's main runs the field / scalar unit tests and a verify
-   benchmark of ~300K synchronous single calls as well; this driver runs the
-   three verify suites (the ones that exercise the drop-in) and also
-   test_point_validate... no: fd_ed25519_point_validate is not part of the
-   drop-in; only the verify suites are called. */
+   test_ed25519.c's main also runs the field / scalar unit tests and a
+   verify benchmark of ~300K synchronous single calls; this driver runs only
+   the three verify suites, the ones that exercise the drop-ins. */
 #define main fdref_test_ed25519_unused_main
 #include "ballet/ed25519/test_ed25519.c"
 #undef main
