@@ -91,6 +91,27 @@ FD_DEV void fe_select(fe& h, const fe& f, const fe& g, bool c) {
 #define FE_ASM_MAD 1
 #endif
 
+/* How the unsigned-limb forms (below) pin their accumulation order.
+   FE_USE_BARRIER=0: asm("" : "+v"(acc)) after each multiply-add, like the
+   centered forms.  FE_USE_BARRIER=1: a use-only asm (acc is read, not
+   redefined).  Both keep every partial sum as its own value, so LLVM
+   cannot reassociate the column; but an asm that *defines* a VGPR counts
+   as a possible dst-forwarding producer for gfx950's hazard recognizer,
+   which then puts an s_nop before the next instruction that reads it (one
+   per multiply-add pair wherever the scheduler groups two barriers: 2353
+   in the dsm kernel, 821 in decode).  The use-only form leaves 141 and
+   122: dsm 7.82 -> 7.75 ms per 1M, decode unchanged (interleaved A/B x3,
+   profiles/r3_ab_use_barrier.txt).  The centered forms keep the defining
+   barrier: the use-only form there makes decode spill 3.4 KB per lane. */
+#ifndef FE_USE_BARRIER
+#define FE_USE_BARRIER 1
+#endif
+#if FE_USE_BARRIER
+#define FE_ACC_BARRIER_U(acc) asm volatile("" ::"v"(acc))
+#else
+#define FE_ACC_BARRIER_U(acc) asm("" : "+v"(acc))
+#endif
+
 FD_DEV void fe_mad(int64_t& acc, int32_t x, int32_t y) {
   acc += (int64_t)x * y;
 #if FE_ASM_MAD
@@ -265,7 +286,7 @@ FD_DEV void fe_mul19_u(fe& h, const fe& f, const fe& g, const fe& g19) {
         if (s == 0 && n == 0) acc = (int64_t)x * y;
         else acc += (int64_t)x * y;
 #if FE_ASM_MAD
-        asm("" : "+v"(acc));
+        FE_ACC_BARRIER_U(acc);
 #endif
       }
       const int w = (k & 1) ? 25 : 26;
@@ -308,7 +329,7 @@ FD_DEV void fe_sqs_u(fe& h, const fe& f) {
           else acc += (int64_t)x * y;
           first = false;
 #if FE_ASM_MAD
-          asm("" : "+v"(acc));
+          FE_ACC_BARRIER_U(acc);
 #endif
         }
       }

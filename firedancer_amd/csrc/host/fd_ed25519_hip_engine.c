@@ -250,6 +250,13 @@ stream_set_size( void ) {
 static int
 stream_acquire( int device, hipStream_t const * avoid, int avoid_cnt, hipStream_t * out ) {
   if( device<0 || device>=FD_ED25519_HIP_MAX_DEV ) return FD_ED25519_HIP_ERR_INVAL;
+#ifdef FD_ED25519_HIP_AB_FRESH_STREAMS
+  /* A/B build only (tools/build_variant.sh): a new stream per request, as
+     in round 2 */
+  (void)avoid; (void)avoid_cnt;
+  { hipError_t he = hipStreamCreateWithFlags( out, hipStreamNonBlocking );
+    return he==hipSuccess ? FD_ED25519_HIP_OK : hip_fail( he, "stream" ); }
+#endif
   pthread_mutex_lock( &sset_lock );
   int rc = FD_ED25519_HIP_OK;
   if( !sset[device].cnt ) {
@@ -284,6 +291,10 @@ stream_acquire( int device, hipStream_t const * avoid, int avoid_cnt, hipStream_
 static void
 stream_release( int device, hipStream_t st ) {
   if( !st || device<0 || device>=FD_ED25519_HIP_MAX_DEV ) return;
+#ifdef FD_ED25519_HIP_AB_FRESH_STREAMS
+  hipStreamDestroy( st );
+  return;
+#endif
   pthread_mutex_lock( &sset_lock );
   for( int i=0; i<sset[device].cnt; i++ )
     if( sset[device].s[i]==st && sset[device].users[i]>0 ) { sset[device].users[i]--; break; }

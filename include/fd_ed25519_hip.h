@@ -167,18 +167,18 @@ fd_ed25519_hip_engine_new( int device, unsigned long max_chunk, int flags );
 void
 fd_ed25519_hip_engine_delete( fd_ed25519_hip_engine_t * engine );
 
+/* Device memory this process shares between all its engines on `device`:
+   the half-size form's two base tables while any engine holds them (2 x 2
+   GiB; 2 x 8 MiB for FD_ED25519_HIP_FLAG_COMPACT_TABLES engines), else 0.  An engine's own memory is fd_ed25519_hip_engine_info's
+   device_bytes. */
+unsigned long
+fd_ed25519_hip_shared_device_bytes( int device );
+
 /* Moves the chunk sizes at which the engine switches from one quad of lanes
    per signature (chunks of at most quad_max) and two quads (at most
    oct_max) to one lane per signature.  FD_ED25519_HIP_ERR_INVAL if
    oct_max > quad_max or quad_max exceeds what the engine's lane tables
    hold.  For tests and tuning; the defaults are the measured crossovers. */
-/* Device memory this process shares between all its engines on `device`:
-   the half-size form's two base tables (2 x 2 GiB) while any engine holds
-   them, else 0.  An engine's own memory is fd_ed25519_hip_engine_info's
-   device_bytes. */
-unsigned long
-fd_ed25519_hip_shared_device_bytes( int device );
-
 int
 fd_ed25519_hip_engine_set_forms( fd_ed25519_hip_engine_t * engine, unsigned long quad_max, unsigned long oct_max );
 

@@ -68,7 +68,10 @@ def test_dropin_threads_parity_and_coalescing(fd, vectors, batch):
     assert not errors, errors[:10]
     l1, r1 = fd.dropin_stats()
     launches, reqs = l1 - l0, r1 - r0
-    assert reqs == 3 * n + len(range(0, len(batch["txn_cnt"])))
+    # a batch_single_msg call with n outside 1..16 returns ERR_SIG before
+    # queueing anything (the reference's check), so it is no request
+    valid = int(((batch["txn_cnt"] >= 1) & (batch["txn_cnt"] <= 16)).sum())
+    assert reqs == 3 * n + valid
     assert launches < reqs   # coalesced: fewer GPU round trips than calls
 
 
