@@ -261,6 +261,10 @@ stream_acquire( int device, hipStream_t const * avoid, int avoid_cnt, hipStream_
   int rc = FD_ED25519_HIP_OK;
   if( !sset[device].cnt ) {
     int n = stream_set_size();
+#ifdef FD_ED25519_HIP_AB_SET_SKIP
+    /* A/B build only: streams created (and never used) before the set */
+    for( int i=0; i<FD_ED25519_HIP_AB_SET_SKIP; i++ ) { hipStream_t t; (void)hipStreamCreateWithFlags( &t, hipStreamNonBlocking ); }
+#endif
     for( int i=0; i<n; i++ ) {
       hipError_t he = hipStreamCreateWithFlags( &sset[device].s[i], hipStreamNonBlocking );
       if( he!=hipSuccess ) {
