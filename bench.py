@@ -454,7 +454,8 @@ def main():
     ap.add_argument("--host-copies", type=int, default=4, help="host-fed stream: the set this many times")
     ap.add_argument("--host-batch", type=int, default=131072)
     ap.add_argument("--host-slots", type=int, default=3,
-                    help="3: each slot stream on its own hardware queue (4 measured 35% slower, tools/pool_first_probe.py)")
+                    help="batches in flight per GPU in the pool (70.1-70.5M/s at 3, 66-71M/s at 2 or 4: "
+                         "profiles/r3_pool_h2d_serialize_ab.txt)")
     ap.add_argument("--host-first", action="store_true", help="run the host-fed leg first (A/B)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight on the GPU (steps alternate between this many engines); "
@@ -521,11 +522,12 @@ def main():
     inflight = args.inflight or (2 if strong else 4)
     one_stream = inflight >= 3 if args.one_stream == "auto" else args.one_stream == "1"
     hf_first = None
-    # (round 2 ran the host-fed leg first because its pool's slot streams
-    # landed on shared hardware queues after the timed engines' streams; the
-    # library's per-device stream set, fd_ed25519_hip_engine.c, made the
-    # placement independent of creation order, and the leg runs last again;
-    # --host-first remains for the A/B)
+    # (round 2 ran the host-fed leg first: its rate depended on where the
+    # pool's slot streams landed on the hardware queues.  The cause was two
+    # batches crossing PCIe at once, which moves fewer bytes than one; the
+    # pool now lets one batch's H2D run at a time (its kernels overlap the
+    # next copy), at the same rate wherever the streams land, so the leg runs
+    # last again; --host-first remains for the A/B)
     if args.host_first and args.host_reps > 0:   # the host-fed leg before the engine's timed passes
         try:
             hf_first = host_fed(wl, device, info, world, args.host_reps, args.host_batch, args.host_slots,

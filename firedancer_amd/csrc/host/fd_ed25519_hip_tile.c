@@ -1392,6 +1392,7 @@ fd_ed25519_hip_vservice_run_links( int device, unsigned slot_cnt, unsigned long 
 typedef struct {
   fd_ed25519_hip_engine_t * eng;
   hipEvent_t                ev;
+  hipEvent_t                ev_h2d;    /* this slot's last batch has crossed the link */
   unsigned char *           d_msgs;
   unsigned long *           d_off;
   unsigned int *            d_sz;
@@ -1417,6 +1418,7 @@ struct fd_ed25519_hip_pool {
 typedef struct {
   fd_ed25519_hip_pool_t * pool;
   unsigned                rank;
+  hipEvent_t              h2d_tail;   /* ev_h2d of the batch submitted last on this device (or NULL) */
   unsigned long           n;
   unsigned char const *   msgs;
   unsigned long const *   msg_off;
@@ -1533,6 +1535,7 @@ pool_slot_init( pool_slot_t * s, int device, unsigned long batch_sigs, unsigned 
   s->d_out  = (signed char *)d;                      d += (batch_sigs + 255UL) & ~255UL;
   s->d_msgs = d;
   TCHK( hipEventCreateWithFlags( &s->ev, hipEventDisableTiming ), "hipEventCreate" );
+  TCHK( hipEventCreateWithFlags( &s->ev_h2d, hipEventDisableTiming ), "hipEventCreate" );
   return FD_ED25519_HIP_OK;
 }
 
@@ -1542,6 +1545,7 @@ pool_slot_fini( pool_slot_t * s ) {
   hipFree( s->d_sigs );
   hipHostFree( s->h_stage ); hipHostFree( s->h_out );
   if( s->ev ) hipEventDestroy( s->ev );
+  if( s->ev_h2d ) hipEventDestroy( s->ev_h2d );
   if( s->eng ) fd_ed25519_hip_engine_delete( s->eng );
   memset( s, 0, sizeof(*s) );
 }
@@ -1587,6 +1591,15 @@ pool_enqueue( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
   unsigned long lo, hi, bytes;
   batch_span( j, i0, i1, &lo, &hi, &bytes );
   unsigned char const * dmsgs;
+#ifndef FD_ED25519_HIP_AB_POOL_PARALLEL_H2D
+  /* One batch crosses the link at a time: this batch's copies start once
+     the previous batch's are done (its kernels still overlap them).  Two
+     batches copying at once split the link between two DMA streams and
+     move fewer bytes in total than one (the host-fed rate fell to ~46M/s
+     with 3 slots, 69M/s with 2, depending on where the slots' streams
+     land on the device's hardware queues). */
+  if( j->h2d_tail ) TCHK( hipStreamWaitEvent( st, j->h2d_tail, 0U ), "hipStreamWaitEvent(h2d)" );
+#endif
   if( j->direct_in && span_direct( pl, hi-lo, bytes ) ) {
     if( hi>lo ) TCHK( hipMemcpyAsync( s->d_msgs, j->msgs + lo, hi-lo, hipMemcpyHostToDevice, st ), "H2D msgs" );
     TCHK( hipMemcpyAsync( s->d_off,  j->msg_off + i0, 8UL*cnt,  hipMemcpyHostToDevice, st ), "H2D off"  );
@@ -1627,6 +1640,8 @@ pool_enqueue( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
     j->st.h2d_bytes += pos + 108UL*cnt;
     dmsgs = s->d_msgs;
   }
+  TCHK( hipEventRecord( s->ev_h2d, st ), "hipEventRecord(h2d)" );
+  j->h2d_tail = s->ev_h2d;
   int err = fd_ed25519_hip_verify_dev( s->eng, cnt, dmsgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
   if( err ) return err;
   if( !j->direct_out && !s->h_out )
