@@ -1027,6 +1027,9 @@ static pthread_cond_t  dropin_cv   = PTHREAD_COND_INITIALIZER;
 static struct {
   fd_ed25519_hip_engine_t * eng[ DROPIN_ENGINES ];
   int                       busy[ DROPIN_ENGINES ];
+  unsigned char *           h_blk[ DROPIN_ENGINES ];   /* pinned: one launch's inputs, then its codes */
+  unsigned char *           d_blk[ DROPIN_ENGINES ];
+  uint64_t                  blk_cap[ DROPIN_ENGINES ];
   dropin_req_t *            head;
   dropin_req_t *            tail;
   unsigned long             launches, requests;   /* for fd_ed25519_hip_dropin_stats */
@@ -1055,39 +1058,78 @@ dropin_fatal( int err ) {
   abort();
 }
 
-/* one combined launch of the requests in list (n of them) on engine e:
-   packed into the engine's pinned staging as transactions, verified, the
-   per-transaction combine, codes back */
+/* One combined launch of the requests in list (n of them) on drop-in
+   engine k.  A drop-in call is latency-bound (a handful of signatures per
+   GPU round trip), so the launch moves one pinned block each way instead
+   of an array per field: in, [off | sz | tfirst | tcnt | sigs | pubs |
+   msgs] (sigs and pubs 16-byte aligned, 16 readable bytes past the last
+   message for the SHA-512 loader); out, [codes | per-transaction codes].
+   The per-transaction combine (batch_single_msg's priority rule) runs only
+   when a request has more than one signature; a lone signature's code is
+   its request's result. */
+#define DROPIN_ALIGN16( x ) (((x) + 15UL) & ~15UL)
+
 static int
-dropin_run( fd_ed25519_hip_engine_t * e, dropin_req_t * list, unsigned long n ) {
+dropin_run( int k, dropin_req_t * list, unsigned long n ) {
+  fd_ed25519_hip_engine_t * e = dq.eng[k];
   HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
   uint64_t nsig = 0UL, bytes = 0UL;
-  for( dropin_req_t * r=list; r; r=r->next ) { nsig += r->cnt; bytes += r->msg_sz; }
-  int err;
-  if( (err = stage_sigs( e, nsig )) ) return err;
-  if( (err = stage_msgs( e, bytes )) ) return err;
-  if( (err = stage_txns( e, n )) ) return err;
-  uint64_t pos = 0UL, k = 0UL, t = 0UL;
+  int multi = 0;
+  for( dropin_req_t * r=list; r; r=r->next ) { nsig += r->cnt; bytes += r->msg_sz; multi |= r->cnt>1U; }
+  uint64_t o_off  = 0UL;
+  uint64_t o_sz   = DROPIN_ALIGN16( o_off  + 8UL*nsig );
+  uint64_t o_tf   = DROPIN_ALIGN16( o_sz   + 4UL*nsig );
+  uint64_t o_tc   = DROPIN_ALIGN16( o_tf   + 4UL*n );
+  uint64_t o_sig  = DROPIN_ALIGN16( o_tc   + 4UL*n );
+  uint64_t o_pub  = DROPIN_ALIGN16( o_sig  + 64UL*nsig );
+  uint64_t o_msg  = DROPIN_ALIGN16( o_pub  + 32UL*nsig );
+  uint64_t in_sz  = o_msg + bytes;
+  uint64_t o_out  = DROPIN_ALIGN16( in_sz + 16UL );
+  uint64_t o_tout = o_out + nsig;
+  uint64_t need   = o_tout + n + 16UL;
+  if( need>dq.blk_cap[k] ) {
+    uint64_t cap = dq.blk_cap[k] ? dq.blk_cap[k] : (1UL<<20);
+    while( cap<need ) cap *= 2UL;
+    hipHostFree( dq.h_blk[k] ); hipFree( dq.d_blk[k] );
+    dq.h_blk[k] = NULL; dq.d_blk[k] = NULL; dq.blk_cap[k] = 0UL;
+    HIPCHK( hipHostMalloc( (void **)&dq.h_blk[k], cap, hipHostMallocDefault ), "hipHostMalloc(drop-in)" );
+    HIPCHK( hipMalloc( (void **)&dq.d_blk[k], cap ), "hipMalloc(drop-in)" );
+    dq.blk_cap[k] = cap;
+  }
+  unsigned char * h = dq.h_blk[k];
+  unsigned char * d = dq.d_blk[k];
+  unsigned long * off = (unsigned long *)(h + o_off);
+  unsigned int *  sz  = (unsigned int  *)(h + o_sz);
+  uint32_t *      tf  = (uint32_t      *)(h + o_tf);
+  uint32_t *      tc  = (uint32_t      *)(h + o_tc);
+  uint64_t pos = 0UL, j = 0UL, t = 0UL;
   for( dropin_req_t * r=list; r; r=r->next, t++ ) {
-    if( r->msg_sz ) memcpy( e->h_msgs + pos, r->msg, r->msg_sz );
-    e->h_tfirst[t] = (uint32_t)k;
-    e->h_tcnt  [t] = r->cnt;
-    memcpy( e->h_sigs + 64UL*k, r->sigs, 64UL*r->cnt );
-    memcpy( e->h_pubs + 32UL*k, r->pubs, 32UL*r->cnt );
-    for( uint32_t j=0U; j<r->cnt; j++, k++ ) { e->h_off[k] = pos; e->h_sz[k] = r->msg_sz; }
+    if( r->msg_sz ) memcpy( h + o_msg + pos, r->msg, r->msg_sz );
+    tf[t] = (uint32_t)j;
+    tc[t] = r->cnt;
+    memcpy( h + o_sig + 64UL*j, r->sigs, 64UL*r->cnt );
+    memcpy( h + o_pub + 32UL*j, r->pubs, 32UL*r->cnt );
+    for( uint32_t i=0U; i<r->cnt; i++, j++ ) { off[j] = pos; sz[j] = r->msg_sz; }
     pos += r->msg_sz;
   }
-  if( (err = upload_and_verify( e, nsig, bytes )) ) return err;
-  HIPCHK( hipMemcpyAsync( e->d_tfirst, e->h_tfirst, 4UL*n, hipMemcpyHostToDevice, e->stream ), "H2D tfirst" );
-  HIPCHK( hipMemcpyAsync( e->d_tcnt,   e->h_tcnt,   4UL*n, hipMemcpyHostToDevice, e->stream ), "H2D tcnt" );
-  if( (err = fd_ed25519_hip_txn_combine_dev( e, n, (signed char const *)e->d_out, e->d_tfirst, e->d_tcnt,
-                                             (signed char *)e->d_tout, e->stream )) ) return err;
-  HIPCHK( hipMemcpyAsync( e->h_tout, e->d_tout, n, hipMemcpyDeviceToHost, e->stream ), "D2H tout" );
-  HIPCHK( hipMemcpyAsync( e->h_out, e->d_out, nsig, hipMemcpyDeviceToHost, e->stream ), "D2H out" );
-  HIPCHK( hipStreamSynchronize( e->stream ), "drop-in verify" );
+  hipStream_t st = e->stream;
+  HIPCHK( hipMemcpyAsync( d, h, in_sz ? in_sz : 1UL, hipMemcpyHostToDevice, st ), "H2D drop-in" );
+  int err = fd_ed25519_hip_verify_dev( e, nsig, d + o_msg, (unsigned long const *)(d + o_off),
+                                       (unsigned int const *)(d + o_sz), d + o_sig, d + o_pub,
+                                       (signed char *)(d + o_out), st );
+  if( err ) { hipStreamSynchronize( st ); return err; }
+  if( multi ) {
+    err = fd_ed25519_hip_txn_combine_dev( e, n, (signed char const *)(d + o_out), (uint32_t const *)(d + o_tf),
+                                          (uint32_t const *)(d + o_tc), (signed char *)(d + o_tout), st );
+    if( err ) { hipStreamSynchronize( st ); return err; }
+  }
+  HIPCHK( hipMemcpyAsync( h + o_out, d + o_out, multi ? nsig + n : nsig, hipMemcpyDeviceToHost, st ), "D2H drop-in" );
+  HIPCHK( hipStreamSynchronize( st ), "drop-in verify" );
+  signed char const * codes = (signed char const *)(h + o_out);
+  signed char const * tcode = (signed char const *)(h + o_tout);
   t = 0UL;
   for( dropin_req_t * r=list; r; r=r->next, t++ )
-    r->result = r->single ? (int)e->h_out[ e->h_tfirst[t] ] : (int)e->h_tout[t];
+    r->result = (r->single || !multi) ? (int)codes[ tf[t] ] : (int)tcode[t];
   return FD_ED25519_HIP_OK;
 }
 
@@ -1112,7 +1154,7 @@ dropin_submit( dropin_req_t * r ) {
     dq.busy[k] = 1;
     dq.launches++; dq.requests += n;
     pthread_mutex_unlock( &dropin_lock );
-    int err = dropin_run( dq.eng[k], list, n );
+    int err = dropin_run( k, list, n );
     if( err ) dropin_fatal( err );
     pthread_mutex_lock( &dropin_lock );
     for( dropin_req_t * q=list; q; ) { dropin_req_t * nx = q->next; q->done = 1; q = nx; }
@@ -1135,7 +1177,7 @@ unsigned long
 fd_ed25519_hip_dropin_device_bytes( void ) {
   pthread_once( &dropin_once, dropin_init );
   unsigned long b = 0UL;
-  for( int k=0; k<DROPIN_ENGINES; k++ ) b += dq.eng[k]->device_bytes;
+  for( int k=0; k<DROPIN_ENGINES; k++ ) b += dq.eng[k]->device_bytes + dq.blk_cap[k];
   return b + fd_ed25519_hip_shared_device_bytes( dq.eng[0]->device );
 }
 

@@ -78,6 +78,7 @@ typedef struct {
   fd_ed25519_hip_slot_t     pub;     /* first member: the public handle */
   fd_ed25519_hip_engine_t * eng;
   hipEvent_t                ev;
+  hipEvent_t                ev_h2d;    /* the slot's batch has crossed the link */
   int                       state;
   /* staging: the public host arrays live in one pinned block laid out as
      [sigs | pubs | msg_off | msg_sz | txn_first | txn_sig_cnt | msgs], its
@@ -112,6 +113,7 @@ struct fd_ed25519_hip_pipe {
   unsigned long next_poll;   /* ring index of the oldest submitted slot */
   unsigned long seq;
   unsigned      in_flight;
+  hipEvent_t    h2d_tail;    /* ev_h2d of the last batch submitted (one batch on the link at a time, as the pool) */
   int           err;         /* sticky: a batch failed on the GPU (FD_ED25519_HIP_ERR_HIP - hipError_t) */
   pipe_slot_t   slot[ PIPE_SLOT_MAX ];
 };
@@ -122,6 +124,7 @@ pipe_slot_free( pipe_slot_t * s ) {
   hipFree( s->d_in ); hipFree( s->d_outb );
   hipFree( s->d_soff ); hipFree( s->d_ssz ); hipFree( s->d_pok );
   if( s->ev ) hipEventDestroy( s->ev );
+  if( s->ev_h2d ) hipEventDestroy( s->ev_h2d );
   if( s->eng ) fd_ed25519_hip_engine_delete( s->eng );
 }
 
@@ -178,6 +181,7 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   TCHK( hipMalloc( (void **)&s->d_pok,  tc          ), "hipMalloc" );
   s->dev_bytes = in_sz + out_sz + 12UL*sig_cap + tc;
   TCHK( hipEventCreateWithFlags( &s->ev, hipEventDisableTiming ), "hipEventCreate" );
+  TCHK( hipEventCreateWithFlags( &s->ev_h2d, hipEventDisableTiming ), "hipEventCreate" );
   s->state = SLOT_FREE;
   return FD_ED25519_HIP_OK;
 }
@@ -209,8 +213,28 @@ fd_ed25519_hip_pipe_new( int device, unsigned slot_cnt, unsigned long sig_cap, u
    counts the signature arrays in use, oc_cnt the msg_off/msg_sz entries. */
 #define SLOT_ONE_COPY_SLACK (256UL << 10)
 
+static int slot_h2d_copies( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt,
+                            unsigned long msg_bytes );
+
+/* ... after the previous batch's copies (two batches on the link at once
+   move fewer bytes than one: DESIGN.md 3b); the batch's kernels still
+   overlap the next batch's copy */
 static int
-slot_h2d( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt, unsigned long msg_bytes ) {
+slot_h2d( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt,
+          unsigned long txn_cnt, unsigned long msg_bytes ) {
+#ifndef FD_ED25519_HIP_AB_POOL_PARALLEL_H2D
+  if( pipe->h2d_tail ) TCHK( hipStreamWaitEvent( st, pipe->h2d_tail, 0U ), "hipStreamWaitEvent(h2d)" );
+#endif
+  int err = slot_h2d_copies( s, st, sig_cnt, txn_cnt, msg_bytes );
+  if( err ) return err;
+  TCHK( hipEventRecord( s->ev_h2d, st ), "hipEventRecord(h2d)" );
+  pipe->h2d_tail = s->ev_h2d;
+  return FD_ED25519_HIP_OK;
+}
+
+static int
+slot_h2d_copies( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt,
+                 unsigned long msg_bytes ) {
   fd_ed25519_hip_slot_t * p = &s->pub;
   unsigned long oc_cnt = sig_cnt > txn_cnt ? sig_cnt : txn_cnt;
   unsigned long used = 96UL*sig_cnt + 12UL*oc_cnt + 8UL*txn_cnt + msg_bytes;
@@ -291,7 +315,7 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   slot->sig_cnt = sig_cnt; slot->msg_bytes = msg_bytes; slot->txn_cnt = txn_cnt;
   slot->seq = pipe->seq++;
   slot->t_submit = now_s();
-  int err = slot_h2d( s, st, sig_cnt, txn_cnt, msg_bytes );
+  int err = slot_h2d( pipe, s, st, sig_cnt, txn_cnt, msg_bytes );
   if( err ) return err;
   if( sig_cnt ) {
     err = fd_ed25519_hip_verify_dev( s->eng, sig_cnt, s->d_msgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
@@ -338,7 +362,7 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
     /* the per-transaction offsets / sizes travel in msg_off / msg_sz; the
        device writes the per-signature ones (and the signatures and keys)
        into arrays of its own */
-    int err = slot_h2d( s, st, 0UL, txn_cnt, payload_bytes );
+    int err = slot_h2d( pipe, s, st, 0UL, txn_cnt, payload_bytes );
     if( err ) return err;
     fd_ed25519_txn_stage_params_t sp;
     sp.payloads = s->d_msgs; sp.pay_off = s->d_off; sp.pay_sz = s->d_sz; sp.txn_first = s->d_tfirst;
