@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -29,7 +30,9 @@ def main():
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                k = r["Kernel_Name"].split("(")[0]
+                # "void fd_ed25519_dsm_kernel<24>(...)" -> fd_ed25519_dsm_kernel
+                # (the template argument is the base-table radix)
+                k = re.sub(r"<[^>]*>$", "", re.sub(r"^void ", "", r["Kernel_Name"].split("(")[0]))
                 c = r["Counter_Name"]
                 agg[k][c] += float(r["Counter_Value"])
                 disp[k][c].add((f, r["Dispatch_Id"]))
