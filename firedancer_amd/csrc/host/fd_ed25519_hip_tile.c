@@ -12,6 +12,9 @@
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 #include <stdatomic.h>
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+#include <x86intrin.h>
+#endif
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -644,7 +647,7 @@ fd_ed25519_hip_vtile_delete( fd_ed25519_hip_vtile_t * vt ) {
 
 static vrec_t *
 vq_at( fd_ed25519_hip_vtile_t * vt, unsigned long k ) {
-  return &vt->q[ (vt->q_head + k) % vt->q_cap ];
+  return &vt->q[ (vt->q_head + k) & (vt->q_cap - 1UL) ];   /* q_cap: a power of 2 */
 }
 
 static vrec_t *
@@ -661,7 +664,7 @@ vq_push( fd_ed25519_hip_vtile_t * vt ) {
     free( vt->q );
     vt->q = nq; vt->q_cap = ncap; vt->q_head = 0UL;
   }
-  vrec_t * r = &vt->q[ (vt->q_head + vt->q_cnt) % vt->q_cap ];
+  vrec_t * r = &vt->q[ (vt->q_head + vt->q_cnt) & (vt->q_cap - 1UL) ];
   vt->q_cnt++;
   memset( r, 0, sizeof(*r) );
   return r;
@@ -723,12 +726,31 @@ vt_advance( fd_ed25519_hip_vtile_t * vt ) {
 /* resolve the records of a completed batch, in frag order (records ahead
    of them are resolved already: earlier batches completed first, parse
    failures at once) */
+/* where record r's payload starts in its batch (the frag is built from it) */
+static inline unsigned char const *
+vt_payload( fd_ed25519_hip_vtile_t const * vt, fd_ed25519_hip_slot_t const * s, vrec_t const * r ) {
+  unsigned long ti = r->txn_idx;
+  if( vt->gpu_parse ) return s->msgs + s->msg_off[ ti ];
+  unsigned long k = s->txn_first[ ti ];
+  return s->msgs + s->msg_off[ k ] - ( 1UL + 64UL*s->txn_sig_cnt[ ti ] );
+}
+
 static void
 vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
   for( unsigned long k=vt->resolved_head; k<vt->q_cnt; k++ ) {
     vrec_t * r = vq_at( vt, k );
     if( r->resolved ) continue;
     if( r->slot_seq!=s->seq ) break;
+    /* the payload a few records ahead is read into the cache while this
+       one resolves (the batch's bytes were staged a few batches ago) */
+    if( k+4UL<vt->q_cnt ) {
+      vrec_t const * a = vq_at( vt, k+4UL );
+      if( !a->resolved && a->slot_seq==s->seq && s->txn_sig_cnt[ a->txn_idx ]-1U<16U ) {
+        unsigned char const * pp = vt_payload( vt, s, a );
+        for( unsigned long l=0UL; l<448UL; l+=64UL ) __builtin_prefetch( pp + l, 0, 3 );
+        __builtin_prefetch( s->txn_trailer + 64UL*a->txn_idx, 0, 3 );
+      }
+    }
     int code = s->txn_out[ r->txn_idx ];
     int v;
     if( code==FD_ED25519_HIP_TXN_CODE_PARSE_FAILED )          v = FD_ED25519_HIP_TXN_PARSE_FAILED;  /* device parse */
@@ -779,16 +801,30 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
   vt_advance( vt );
 }
 
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+static __thread unsigned long long vt_wait_cycles, vt_resolve_cycles, vt_blocks;   /* A/B build only */
+#endif
+
 static int
 vt_drain_one( fd_ed25519_hip_vtile_t * vt, int wait ) {
   if( vt->err ) return 0;
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  unsigned long long w0 = __rdtsc();
+#endif
   fd_ed25519_hip_slot_t * s = fd_ed25519_hip_pipe_poll( vt->pipe, wait );
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  unsigned long long w1 = __rdtsc();
+  if( wait ) { vt_wait_cycles += w1 - w0; vt_blocks++; }
+#endif
   if( !s ) {
     if( fd_ed25519_hip_pipe_error( vt->pipe ) ) vt->err = fd_ed25519_hip_pipe_error( vt->pipe );
     return 0;
   }
   vt_resolve( vt, s );
   fd_ed25519_hip_pipe_release( vt->pipe, s );
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  vt_resolve_cycles += __rdtsc() - w1;
+#endif
   return 1;
 }
 
@@ -943,11 +979,32 @@ fd_ed25519_hip_vtile_poll_frags( fd_ed25519_hip_vtile_t * vt, int wait, unsigned
       vt->oa_live--;
     }
     n++;
-    vt->q_head = (vt->q_head+1UL) % vt->q_cap;
+    vt->q_head = (vt->q_head+1UL) & (vt->q_cap - 1UL);
     vt->q_cnt--;
     vt->resolved_head--;
   }
   return n;
+}
+
+/* The service's path (vservice_loop): resolved records are published
+   straight from the output arena, without poll_frags' copy into a caller
+   buffer.  vt_head returns the oldest record once it is resolved (its frag,
+   for SUCCESS, at vt->oa + arena_off, frag_sz bytes), vt_pop retires it. */
+static vrec_t const *
+vt_head( fd_ed25519_hip_vtile_t * vt ) {
+  return vt->resolved_head ? vq_at( vt, 0UL ) : NULL;
+}
+
+static void
+vt_pop( fd_ed25519_hip_vtile_t * vt ) {
+  vrec_t const * r = vq_at( vt, 0UL );
+  if( r->arena_len ) {   /* arena bytes come free in record order */
+    vt->oa_head = r->arena_off + r->arena_len;
+    vt->oa_live--;
+  }
+  vt->q_head = (vt->q_head+1UL) & (vt->q_cap - 1UL);
+  vt->q_cnt--;
+  vt->resolved_head--;
 }
 
 unsigned long
@@ -1251,6 +1308,16 @@ fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_c
    both links failed with the code (fd_ed25519_hip_shlink_status) and
    returns it; it never aborts the process mid-batch. */
 
+/* an idle pass of a polling loop (FD_SPIN_PAUSE's role in the reference's
+   tiles): a pause hint, so a link thread with nothing to do yields its
+   core's pipeline to the sibling hyperthread */
+static inline void
+spin_pause( void ) {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#endif
+}
+
 static int
 vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
                fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
@@ -1261,60 +1328,94 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
     fd_ed25519_hip_shlink_fail( in, FD_ED25519_HIP_ERR_INVAL ); fd_ed25519_hip_shlink_fail( out, FD_ED25519_HIP_ERR_INVAL );
     return FD_ED25519_HIP_ERR_INVAL;
   }
-  enum { QMAX = 4096 };
-  unsigned long   fbsz = QMAX * ((FD_ED25519_HIP_TPU_DCACHE_MTU + 63UL) & ~63UL);
-  unsigned long * ck  = (unsigned long *)malloc( QMAX*sizeof(unsigned long) );
-  unsigned long * fo  = (unsigned long *)malloc( QMAX*sizeof(unsigned long) );
-  unsigned long * fs  = (unsigned long *)malloc( QMAX*sizeof(unsigned long) );
-  signed char *   vd  = (signed char *)malloc( QMAX );
-  unsigned char * fb  = (unsigned char *)malloc( fbsz );
   unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
-  double t0 = now_s();
-  unsigned long txns = 0UL, qn = 0UL, qi = 0UL, beat = 1UL;
+  double t0 = now_s(), t_first = 0.0;   /* the stream's time runs from its first frag */
+  unsigned long txns = 0UL, beat = 1UL;
   int eos = 0, rc = FD_ED25519_HIP_OK;
-  if( !ck || !fo || !fs || !vd || !fb || !buf ) { rc = FD_ED25519_HIP_ERR_NOMEM; goto fail; }
+  if( !buf ) { rc = FD_ED25519_HIP_ERR_NOMEM; goto fail; }
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  /* A/B build only: cycles per loop section (printed at the end) */
+  unsigned long long pf_t[ 5 ] = { 0ULL, 0ULL, 0ULL, 0ULL, 0ULL }, pf_idle = 0ULL, pf_pass = 0ULL, pf_c = __rdtsc(), pf_n;
+  unsigned long long pf_cons = 0ULL;
+  vt_wait_cycles = vt_resolve_cycles = vt_blocks = 0ULL;
+#define PF_MARK( i ) do { pf_n = __rdtsc(); pf_t[ i ] += pf_n - pf_c; pf_c = pf_n; } while(0)
+#else
+#define PF_MARK( i ) do {} while(0)
+#endif
   for(;;) {
     fd_ed25519_hip_shlink_heartbeat( out, beat++ );
     if( stop && atomic_load_explicit( stop, memory_order_acquire ) ) { rc = FD_ED25519_HIP_SHLINK_FAIL_STOPPED; goto fail; }
     int ts = fd_ed25519_hip_shlink_status( in );
     if( !ts ) ts = fd_ed25519_hip_shlink_status( out );
     if( ts ) { rc = ts; goto fail; }   /* the tile gave up on the link */
-    /* verdicts already collected go out first, as far as credits allow:
-       the verdict byte, then (SUCCESS) the frag the tile publishes */
-    while( qi<qn ) {
+    PF_MARK( 0 );
+    /* completed batches resolve (in frag order); their verdicts go out as
+       far as credits allow: the verdict byte, then (SUCCESS) the frag the
+       tile publishes, copied from the vtile's arena */
+    while( vt_drain_one( vt, 0 ) ) {}
+    PF_MARK( 2 );
+    int published = 0;
+    for( vrec_t const * r; (r = vt_head( vt )); ) {
       unsigned char * dst = fd_ed25519_hip_shlink_prepare( out );
       if( !dst ) break;
-      dst[ 0 ] = (unsigned char)vd[ qi ];
-      if( fs[ qi ] ) memcpy( dst + 1, fb + fo[ qi ], fs[ qi ] );
-      if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + fs[ qi ], ck[ qi ], 0U )) ) goto fail;
-      qi++;
+      unsigned long fsz = r->verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ? r->frag_sz : 0UL;
+      dst[ 0 ] = (unsigned char)r->verdict;
+      if( fsz ) memcpy( dst + 1, vt->oa + r->arena_off, fsz );
+      if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + fsz, r->cookie, 0U )) ) goto fail;
+      vt_pop( vt );
+      published = 1;
     }
-    if( qi==qn ) {
-      qi = qn = 0UL;
-      qn = fd_ed25519_hip_vtile_poll_frags( vt, 0, QMAX, ck, vd, NULL, fo, fs, fb, fbsz );
-    }
+    PF_MARK( 1 );
     if( (rc = fd_ed25519_hip_vtile_error( vt )) ) goto fail;
-    if( eos && !qn && !fd_ed25519_hip_vtile_pending( vt ) ) break;
+    if( eos && !fd_ed25519_hip_vtile_pending( vt ) ) break;
     /* after_frag for every frag that is ready (copied out of the shared
        dcache first: the tile is not trusted not to change it meanwhile) */
     int pulled = 0;
     while( !eos ) {
       unsigned long sz = 0UL, sig = 0UL;
       unsigned int ctl = 0U;
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+      unsigned long long c0 = __rdtsc();
+#endif
       int r = fd_ed25519_hip_shlink_consume( in, buf, &sz, &sig, &ctl );
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+      pf_cons += __rdtsc() - c0;
+#endif
       if( r==1 ) break;
       if( r ) { rc = FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL; goto fail; }   /* overrun: the tile ignored credits */
       if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { eos = 1; break; }
+      if( !txns ) t_first = now_s();
       r = fd_ed25519_hip_vtile_frag( vt, buf, sz, sig );
       if( r<0 ) { rc = r; goto fail; }
       txns++;
       pulled = 1;
     }
+    PF_MARK( 3 );
     /* `in` drained: send the open batch if a slot can take it (all of it at the end) */
     if( !pulled && vt->open && vt->open->txn_cnt &&
         ( eos || slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<slot_cnt ) )
       fd_ed25519_hip_vtile_flush( vt, eos );
+    else if( !pulled && !published ) {
+      spin_pause();
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+      pf_idle++;
+#endif
+    }
+    PF_MARK( 4 );
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+    pf_pass++;
+#endif
   }
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  fprintf( stderr, "vservice profile: %lu txns, %llu passes (%llu idle); cycles per txn: status %.0f publish %.0f "
+           "poll %.0f consume+frag %.0f (of which consume %.0f, waits on the GPU %.0f in %llu waits) flush+pause %.0f; "
+           "resolve (any section) %.0f\n",
+           txns, pf_pass, pf_idle,
+           (double)pf_t[0]/(double)(txns+1UL), (double)pf_t[1]/(double)(txns+1UL), (double)pf_t[2]/(double)(txns+1UL),
+           (double)pf_t[3]/(double)(txns+1UL), (double)pf_cons/(double)(txns+1UL),
+           (double)vt_wait_cycles/(double)(txns+1UL), vt_blocks, (double)pf_t[4]/(double)(txns+1UL),
+           (double)vt_resolve_cycles/(double)(txns+1UL) );
+#endif
   while( fd_ed25519_hip_shlink_publish( out, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
     fd_ed25519_hip_shlink_heartbeat( out, beat++ );
     if( fd_ed25519_hip_shlink_status( in ) || fd_ed25519_hip_shlink_status( out ) ) break;
@@ -1328,11 +1429,11 @@ done:
   if( stats ) {
     stats->txn_cnt      = txns;
     stats->batches      = vt->pipe->seq;
-    stats->seconds      = now_s() - t0;
+    stats->seconds      = now_s() - ( txns ? t_first : t0 );
     stats->device_bytes = fd_ed25519_hip_vtile_device_bytes( vt );
     stats->shared_device_bytes = fd_ed25519_hip_shared_device_bytes( device );
   }
-  free( ck ); free( fo ); free( fs ); free( vd ); free( fb ); free( buf );
+  free( buf );
   fd_ed25519_hip_vtile_delete( vt );
   return rc;
 }

@@ -424,7 +424,7 @@ fd_ed25519_hip_shlink_status( fd_ed25519_hip_shlink_t const * link );
 typedef struct {
   unsigned long txn_cnt;
   unsigned long batches;
-  double        seconds;
+  double        seconds;        /* from the first frag consumed to the end of the stream */
   unsigned long device_bytes;   /* the link pair's own device memory (its vtile's) */
   unsigned long shared_device_bytes;   /* the process's base tables on the device, shared by every pair */
 } fd_ed25519_hip_vservice_stats_t;

@@ -10,7 +10,8 @@
    PAYLOAD_FILE: u64 n, n x u32 sizes, the payloads back to back.  Frag i
    carries sig = i; after the last one an EOS frag.  Verdict frags are
    consumed whenever a publish finds no credit, and after the EOS until
-   the service's EOS.  Output on stdout, via write(2): n verdict bytes in
+   the service's EOS (and, as the tile's after_credit does, every 16
+   frags).  Output on stdout, via write(2): n verdict bytes in
    frag order (checked against the sig of every verdict frag), then for
    each SUCCESS verdict the frag the service returned with it (the frag
    the verify tile publishes: u32 size, then the bytes); exit status 0, or
@@ -138,9 +139,14 @@ main( int argc, char ** argv ) {
   fr.used = 0UL;
   fr.mem = (unsigned char *)malloc( fr.cap );
   if( !fr.mem ) return 1;
+  /* touched before the stream: page faults of the output buffers would
+     otherwise land inside it (a tile publishes into its out dcache, which
+     is mapped and warm) */
+  memset( fr.mem, 0, fr.cap );
   fd_ed25519_hip_shlink_t * txl = fd_ed25519_hip_shlink_join( argv[1] );
   fd_ed25519_hip_shlink_t * vdl = fd_ed25519_hip_shlink_join( argv[2] );
   if( !verdict || !buf || !txl || !vdl ) { fprintf( stderr, "cannot join the links\n" ); return 1; }
+  memset( verdict, 0x7f, n + 1UL );
   /* pauses per ns, measured before the sandbox */
   double n0 = now_ns();
   for( unsigned long k=0UL; k<(1UL<<20); k++ ) _mm_pause();
@@ -156,7 +162,13 @@ main( int argc, char ** argv ) {
   int eos = 0;
   while( i<n ) {
     int r = fd_ed25519_hip_shlink_publish( txl, pay + off[ i ], sz[ i ], i, 0U );
-    if( r==0 ) { i++; continue; }
+    if( r==0 ) {
+      /* as the tile's mux loop does (after_credit between frags): the
+         verdicts that are back are taken every 16 frags, not only when the
+         txn link runs out of credits */
+      if( !(++i & 15UL) && ( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) || eos ) ) leave( 2 );
+      continue;
+    }
     if( r!=1 ) leave( 2 );
     if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) || eos ) leave( 2 );
     watch( &wt );
