@@ -743,7 +743,7 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
     if( r->slot_seq!=s->seq ) break;
     /* the payload a few records ahead is read into the cache while this
        one resolves (the batch's bytes were staged a few batches ago) */
-    if( k+4UL<vt->q_cnt ) {
+    if( vt->gpu_parse && k+4UL<vt->q_cnt ) {
       vrec_t const * a = vq_at( vt, k+4UL );
       if( !a->resolved && a->slot_seq==s->seq && s->txn_sig_cnt[ a->txn_idx ]-1U<16U ) {
         unsigned char const * pp = vt_payload( vt, s, a );
@@ -761,6 +761,10 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
     r->verdict  = (signed char)v;
     r->resolved = 1;
     if( v!=FD_ED25519_HIP_TXN_VERIFY_SUCCESS ) continue;   /* filtered: not published */
+    if( !vt->gpu_parse ) continue;                         /* its frag was built with the frag (vtile_frag) */
+#ifdef FD_ED25519_HIP_AB_NO_FRAGS
+    continue;   /* A/B build only: verdicts without the published frags (cost probe) */
+#endif
     {
       /* the published frag from the payload in the slot and the fd_txn_t
          trailer its parse left in the slot (the device's in GPU-parse
@@ -899,15 +903,19 @@ fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * pa
                            unsigned long cookie ) {
   if( vt->gpu_parse ) return vt_frag_raw( vt, payload, payload_sz, cookie );
   if( vt->err ) return vt->err;
-  /* during_frag + after_frag: the payload goes into the open batch whole
-     (the published frag is built from it if the transaction succeeds) and
-     the parse writes fd_txn_t's first 64 bytes into the batch's trailer
-     slot */
-  fd_ed25519_hip_txn_t t;
+  /* during_frag + after_frag: the payload goes into the open batch whole,
+     and the frag the tile publishes if the transaction succeeds (payload,
+     pad, fd_txn_t, payload_sz) is built now, while the payload is in the
+     cache, into the output arena: the parse writes fd_txn_t there directly.
+     Resolving a batch then only decides verdicts (a frag whose transaction
+     fails stays unpublished and comes free in record order). */
   if( vt_open( vt ) ) return vt->err;
   fd_ed25519_hip_slot_t * s = vt->open;
-  unsigned long foot = fd_txn_core_parse( payload, payload_sz, &t, s->txn_trailer + 64UL*s->txn_cnt, 64UL );
-  if( !foot ) {
+  unsigned long aoff = oa_reserve( vt, ((payload_sz + 1UL) & ~1UL) + FD_ED25519_HIP_TXN_MAX_SZ + 2UL );
+  if( aoff==~0UL ) return vt->err;
+  fd_ed25519_hip_txn_t t;
+  unsigned long fsz = txn_frag_core( payload, payload_sz, vt->oa + aoff, &t );
+  if( !fsz ) {
     vrec_t * r = vq_push( vt );
     if( !r ) return vt->err;
     r->cookie = cookie; r->verdict = FD_ED25519_HIP_TXN_PARSE_FAILED; r->resolved = 1;
@@ -919,7 +927,6 @@ fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * pa
     vt_submit_open( vt );
     if( vt_open( vt ) ) return vt->err;
     s = vt->open;
-    fd_txn_core_parse( payload, payload_sz, &t, s->txn_trailer + 64UL*s->txn_cnt, 64UL );
   }
   unsigned long poff   = s->msg_bytes;
   unsigned long moff   = poff + t.message_off;
@@ -944,6 +951,9 @@ fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * pa
   memcpy( &r->tag, payload + t.signature_off, 8UL );  /* ha_dedup_tag, fd_verify.h:65 */
   r->slot_seq = vt->open_seq;
   r->txn_idx  = (unsigned)ti;
+  r->arena_off = aoff;
+  r->arena_len = oa_commit( vt, aoff, fsz );
+  r->frag_sz   = (unsigned short)fsz;
   if( s->sig_cnt>=s->sig_cap || s->txn_cnt>=s->txn_cap ) vt_submit_open( vt );
   return 1;
 }
@@ -1360,6 +1370,9 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
       if( !dst ) break;
       unsigned long fsz = r->verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ? r->frag_sz : 0UL;
       dst[ 0 ] = (unsigned char)r->verdict;
+#ifdef FD_ED25519_HIP_AB_NO_FRAGS
+      if( !fsz ) dst[ 0 ] = (unsigned char)FD_ED25519_HIP_TXN_VERIFY_FAILED;   /* A/B cost probe: no frag to send */
+#endif
       if( fsz ) memcpy( dst + 1, vt->oa + r->arena_off, fsz );
       if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + fsz, r->cookie, 0U )) ) goto fail;
       vt_pop( vt );

@@ -34,6 +34,7 @@ def gen(paths, txns, q):
     sys.path.insert(0, REPO)
     from firedancer_amd import ed25519, tile, workload
     eng = ed25519.Engine(0, max_chunk=1 << 16)
+    q.put(sorted(tile.device_cpus(eng.info())))
     for k, path in enumerate(paths):
         pay, _ = workload.txn_payloads(eng, txns, 7000 + k, msg_sz=200)
         tile.write_payload_file(path, pay)
@@ -50,6 +51,9 @@ def main():
     ap.add_argument("--gpu-parse", action="store_true")
     ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES of the service process")
     ap.add_argument("--service", default=SERVICE, help="service binary (an A/B build's)")
+    ap.add_argument("--pin", choices=["none", "node"], default="node",
+                    help="node: the service and the tile processes on the CPUs of the GPU's NUMA node, as fdctl "
+                         "pins its tiles (default); none: wherever the OS puts them")
     args = ap.parse_args()
     ks = [int(x) for x in args.tiles.split(",")]
     tmp = tempfile.mkdtemp(prefix="svcb")
@@ -58,8 +62,13 @@ def main():
     q = ctx.Queue()
     p = ctx.Process(target=gen, args=(paths, args.txns, q))
     p.start()
+    node_cpus = q.get(timeout=600)
     q.get(timeout=600)
     p.join(timeout=60)
+    pin = None
+    if args.pin == "node" and node_cpus:
+        def pin():
+            os.sched_setaffinity(0, node_cpus)
     out = []
     for k in ks:
         app = uuid.uuid4().hex[:10]
@@ -67,13 +76,13 @@ def main():
         env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.hw_queues))
         svc = subprocess.Popen([args.service, "--prefix", prefix, "--tiles", str(k), "--batch", str(args.batch),
                                 "--slots", str(args.slots), *(["--gpu-parse"] if args.gpu_parse else [])],
-                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, preexec_fn=pin)
         line = svc.stdout.readline()
         if not line.startswith("ready"):
             raise SystemExit(f"service did not start: {line!r} {svc.stderr.read()[-2000:]}")
         t0 = time.time()
         prods = [subprocess.Popen([PRODUCER, f"{prefix}{i}_txn", f"{prefix}{i}_vd", paths[i]],
-                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE) for i in range(k)]
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, preexec_fn=pin) for i in range(k)]
         ok = True
         for pr in prods:
             so, se = pr.communicate(timeout=300)
@@ -103,7 +112,7 @@ def main():
     for path in paths:
         os.unlink(path)
     print(json.dumps({"service_bench": out, "batch": args.batch, "slots": args.slots, "gpu_parse": args.gpu_parse,
-                      "hw_queues": args.hw_queues}))
+                      "hw_queues": args.hw_queues, "pin": args.pin, "node_cpus": len(node_cpus)}))
 
 
 if __name__ == "__main__":
