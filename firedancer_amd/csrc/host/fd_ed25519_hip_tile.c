@@ -1237,6 +1237,7 @@ typedef struct {
   signed char *         verdict;
   fd_ed25519_hip_latency_result_t res;
   int                   err;
+  char                  errmsg[ 256 ];   /* the worker's last_error (it is per thread) */
 } tile_job_t;
 
 static void *
@@ -1244,6 +1245,7 @@ tile_main( void * arg ) {
   tile_job_t * j = (tile_job_t *)arg;
   j->err = fd_ed25519_hip_latency_run( j->device, j->slot_cnt, j->batch_sigs, j->payloads, j->off, j->sz, j->n, j->rate,
                                        j->ring_depth, j->flags, j->lat, j->verdict, &j->res );
+  if( j->err ) snprintf( j->errmsg, sizeof(j->errmsg), "%s", fd_ed25519_hip_last_error() );
   return NULL;
 }
 
@@ -1283,7 +1285,7 @@ fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_c
   res->offered_txn_per_s = offered_txn_per_s;
   for( unsigned k=0U; k<tile_cnt; k++ ) {
     tile_job_t * j = &job[k];
-    if( !err && j->err ) err = j->err;
+    if( !err && j->err ) { err = j->err; fd_ed25519_hip_private_set_error( j->errmsg ); }
     if( !err ) {
       for( unsigned long i=0UL; i<j->n; i++ ) {
         lat_s  [ k + i*tile_cnt ] = j->lat[i];
@@ -1566,6 +1568,7 @@ typedef struct {
   signed char *           out;
   int                     direct_in, direct_out;   /* caller arrays page-locked */
   int                     err;
+  char                    errmsg[ 256 ];   /* the feeder's last_error for err (last_error is per thread) */
   fd_ed25519_hip_pool_stats_t st;
 } pool_job_t;
 
@@ -1780,6 +1783,14 @@ pool_enqueue( pool_job_t * j, pool_slot_t * s, unsigned long b ) {
   }
   TCHK( hipEventRecord( s->ev_h2d, st ), "hipEventRecord(h2d)" );
   j->h2d_tail = s->ev_h2d;
+#ifdef FD_ED25519_HIP_HOST_FAULT
+  /* test build only (tests/test_gpu_pool_fault.py): the second batch's
+     launch fails after its copies from the caller's arrays are enqueued */
+  if( b==1UL ) {
+    fd_ed25519_hip_private_set_error( "pool: injected launch failure (fault-injection build)" );
+    return FD_ED25519_HIP_ERR_HIP - (int)hipErrorLaunchFailure;
+  }
+#endif
   int err = fd_ed25519_hip_verify_dev( s->eng, cnt, dmsgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
   if( err ) return err;
   if( !j->direct_out && !s->h_out )
@@ -1808,7 +1819,11 @@ pool_main( void * arg ) {
   fd_ed25519_hip_pool_t * pl = j->pool;
   int dev = pl->device[ j->rank ];
   pin_near_device( dev );
-  if( hipSetDevice( dev )!=hipSuccess ) { j->err = tile_fail( "hipSetDevice", hipErrorInvalidDevice ); return NULL; }
+  if( hipSetDevice( dev )!=hipSuccess ) {
+    j->err = tile_fail( "hipSetDevice", hipErrorInvalidDevice );
+    snprintf( j->errmsg, sizeof(j->errmsg), "%s", fd_ed25519_hip_last_error() );
+    return NULL;
+  }
   pool_slot_t * slot = pl->slot[ j->rank ];
   unsigned sc = pl->slot_cnt, ranks = pl->device_cnt;
   unsigned long nb = (j->n + pl->batch_sigs - 1UL) / pl->batch_sigs;
@@ -1818,7 +1833,11 @@ pool_main( void * arg ) {
     pool_slot_t * s = &slot[ next ];
     if( !j->err && b_sub<nb && !s->busy ) {
       int err = pool_submit( j, s, b_sub );
-      if( err ) { j->err = err; continue; }   /* drain what is in flight */
+      if( err ) {   /* drain what is in flight */
+        j->err = err;
+        snprintf( j->errmsg, sizeof(j->errmsg), "%s", fd_ed25519_hip_last_error() );
+        continue;
+      }
       b_sub += ranks;
       next = (next+1U) % sc;
       continue;
@@ -1826,7 +1845,10 @@ pool_main( void * arg ) {
     pool_slot_t * d = &slot[ oldest ];
     if( !d->busy ) break;   /* an error stopped submission and everything drained */
     hipError_t e = hipEventSynchronize( d->ev );
-    if( e!=hipSuccess && !j->err ) j->err = tile_fail( "pool batch", e );
+    if( e!=hipSuccess && !j->err ) {
+      j->err = tile_fail( "pool batch", e );
+      snprintf( j->errmsg, sizeof(j->errmsg), "%s", fd_ed25519_hip_last_error() );
+    }
     if( !j->direct_out && e==hipSuccess ) memcpy( j->out + d->i0, d->h_out, d->i1 - d->i0 );
     d->busy = 0;
     oldest = (oldest+1U) % sc;
@@ -1861,7 +1883,7 @@ fd_ed25519_hip_pool_run( fd_ed25519_hip_pool_t * pl, unsigned long n, unsigned c
   if( stats ) memset( stats, 0, sizeof(*stats) );
   for( unsigned r=0U; r<started; r++ ) {
     pthread_join( th[r], NULL );
-    if( job[r].err && !err ) err = job[r].err;
+    if( job[r].err && !err ) { err = job[r].err; fd_ed25519_hip_private_set_error( job[r].errmsg ); }
     if( stats ) {
       stats->direct_batches += job[r].st.direct_batches;
       stats->staged_batches += job[r].st.staged_batches;
