@@ -603,6 +603,8 @@ struct fd_ed25519_hip_vtile {
   unsigned long             open_seq;   /* seq the open slot will get   */
   unsigned long             batch_sigs;
   int                       gpu_parse;  /* FD_ED25519_HIP_VTILE_GPU_PARSE: raw payloads to the device */
+  int                       trailer_only;   /* the arena holds each frag's trailer only (fd_txn_t, payload_sz):
+                                               the verify service, whose tile keeps the payload */
   int                       err;        /* sticky failure: nothing more is staged or resolved */
   vrec_t *                  q;          /* circular FIFO of records */
   unsigned long             q_cap, q_head, q_cnt;
@@ -782,12 +784,21 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
       unsigned char const * tr  = s->txn_trailer + 64UL*ti;
       unsigned long foot = FD_ED25519_HIP_TXN_FOOTPRINT( (unsigned long)tr[18] | ((unsigned long)tr[19]<<8),
                                                          (unsigned long)tr[14] );
-      unsigned long toff = (psz + 1UL) & ~1UL;
+      unsigned long toff = vt->trailer_only ? 0UL : (psz + 1UL) & ~1UL;
       unsigned long aoff = oa_reserve( vt, toff + FD_ED25519_HIP_TXN_MAX_SZ + 2UL );
       if( aoff==~0UL ) return;   /* vt->err is set: nothing more resolves */
       unsigned char * o = vt->oa + aoff;
       unsigned long fsz;
-      if( foot<=64UL ) {
+      if( vt->trailer_only ) {
+        if( foot>64UL ) {
+          fd_ed25519_hip_txn_t t;
+          foot = fd_txn_core_parse( pay, psz, &t, o, FD_ED25519_HIP_TXN_MAX_SZ );
+        } else {
+          memcpy( o, tr, foot );
+        }
+        o[ foot ] = (unsigned char)psz; o[ foot + 1 ] = (unsigned char)(psz >> 8);
+        fsz = foot + 2UL;
+      } else if( foot<=64UL ) {
         memcpy( o, pay, psz );
         if( toff>psz ) o[ psz ] = 0;
         memcpy( o + toff, tr, foot );
@@ -911,10 +922,20 @@ fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * pa
      fails stays unpublished and comes free in record order). */
   if( vt_open( vt ) ) return vt->err;
   fd_ed25519_hip_slot_t * s = vt->open;
-  unsigned long aoff = oa_reserve( vt, ((payload_sz + 1UL) & ~1UL) + FD_ED25519_HIP_TXN_MAX_SZ + 2UL );
+  unsigned long aoff = oa_reserve( vt, ( vt->trailer_only ? 0UL : (payload_sz + 1UL) & ~1UL ) +
+                                       FD_ED25519_HIP_TXN_MAX_SZ + 2UL );
   if( aoff==~0UL ) return vt->err;
   fd_ed25519_hip_txn_t t;
-  unsigned long fsz = txn_frag_core( payload, payload_sz, vt->oa + aoff, &t );
+  unsigned long fsz;
+  if( vt->trailer_only ) {   /* the trailer only: fd_txn_t, then payload_sz */
+    unsigned char * o = vt->oa + aoff;
+    unsigned long foot = payload_sz>FD_ED25519_HIP_TXN_MTU ? 0UL :
+                         fd_txn_core_parse( payload, payload_sz, &t, o, FD_ED25519_HIP_TXN_MAX_SZ );
+    if( foot ) { o[ foot ] = (unsigned char)payload_sz; o[ foot + 1 ] = (unsigned char)(payload_sz >> 8); }
+    fsz = foot ? foot + 2UL : 0UL;
+  } else {
+    fsz = txn_frag_core( payload, payload_sz, vt->oa + aoff, &t );
+  }
   if( !fsz ) {
     vrec_t * r = vq_push( vt );
     if( !r ) return vt->err;
@@ -1340,6 +1361,7 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
     fd_ed25519_hip_shlink_fail( in, FD_ED25519_HIP_ERR_INVAL ); fd_ed25519_hip_shlink_fail( out, FD_ED25519_HIP_ERR_INVAL );
     return FD_ED25519_HIP_ERR_INVAL;
   }
+  vt->trailer_only = 1;   /* the tile keeps its payloads: verdict frags carry the trailers */
   unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
   double t0 = now_s(), t_first = 0.0;   /* the stream's time runs from its first frag */
   unsigned long txns = 0UL, beat = 1UL;
@@ -1362,21 +1384,22 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
     if( ts ) { rc = ts; goto fail; }   /* the tile gave up on the link */
     PF_MARK( 0 );
     /* completed batches resolve (in frag order); their verdicts go out as
-       far as credits allow: the verdict byte, then (SUCCESS) the frag the
-       tile publishes, copied from the vtile's arena */
+       far as credits allow: the verdict byte, then (SUCCESS) the trailer
+       of the frag the tile publishes (its fd_txn_t and payload_sz, from
+       the frag in the vtile's arena: the tile has the payload) */
     while( vt_drain_one( vt, 0 ) ) {}
     PF_MARK( 2 );
     int published = 0;
     for( vrec_t const * r; (r = vt_head( vt )); ) {
       unsigned char * dst = fd_ed25519_hip_shlink_prepare( out );
       if( !dst ) break;
-      unsigned long fsz = r->verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ? r->frag_sz : 0UL;
+      unsigned long tsz = r->verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ? r->frag_sz : 0UL;
       dst[ 0 ] = (unsigned char)r->verdict;
 #ifdef FD_ED25519_HIP_AB_NO_FRAGS
-      if( !fsz ) dst[ 0 ] = (unsigned char)FD_ED25519_HIP_TXN_VERIFY_FAILED;   /* A/B cost probe: no frag to send */
+      if( !tsz ) dst[ 0 ] = (unsigned char)FD_ED25519_HIP_TXN_VERIFY_FAILED;   /* A/B cost probe: no frag to send */
 #endif
-      if( fsz ) memcpy( dst + 1, vt->oa + r->arena_off, fsz );
-      if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + fsz, r->cookie, 0U )) ) goto fail;
+      if( tsz ) memcpy( dst + 1, vt->oa + r->arena_off, tsz );
+      if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + tsz, r->cookie, 0U )) ) goto fail;
       vt_pop( vt );
       published = 1;
     }

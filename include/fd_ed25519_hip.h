@@ -94,13 +94,15 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
 /* ABI version of the two headers (include/fd_ed25519_hip.h and
    include/fd_ed25519_hip_tile.h): bumped whenever a flag's meaning, a
    struct layout or a prototype changes (3: round 3 -- engine flags 64..256,
-   vservice stats' device bytes, shlink liveness words).  A consumer checks
+   vservice stats' device bytes, shlink liveness words; 4: a SUCCESS verdict
+   frag carries the published frag's trailer only, the tile keeps the
+   payload).  A consumer checks
    the library it loaded against the header it was built with:
    fd_ed25519_hip_abi_check( FD_ED25519_HIP_ABI_VERSION,
    sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
    sizeof(fd_ed25519_hip_vservice_stats_t) ) returns 0 when they agree,
    FD_ED25519_HIP_ERR_INVAL (with fd_ed25519_hip_last_error) when not. */
-#define FD_ED25519_HIP_ABI_VERSION (3U)
+#define FD_ED25519_HIP_ABI_VERSION (4U)
 
 unsigned
 fd_ed25519_hip_abi_version( void );

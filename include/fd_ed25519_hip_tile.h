@@ -341,8 +341,35 @@ fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_c
    under seccomp strict mode). */
 typedef struct fd_ed25519_hip_shlink fd_ed25519_hip_shlink_t;
 
-/* a verdict frag: 1 verdict byte, then the published frag */
+/* the largest frag either direction carries (a verdict frag is smaller
+   than this: 1 verdict byte + at most FD_ED25519_HIP_TXN_MAX_SZ + 2) */
 #define FD_ED25519_HIP_SHLINK_MTU (1UL + FD_ED25519_HIP_TPU_DCACHE_MTU)
+
+/* The verdict frag protocol (service -> tile).  One frag per transaction,
+   in the tile's frag order, sig = the tile's cookie: byte 0 the verdict
+   (FD_ED25519_HIP_TXN_VERIFY_* / FD_ED25519_HIP_TXN_PARSE_FAILED), then,
+   for SUCCESS only, the published frag's trailer: the bytes that follow
+   the payload and its 2-byte alignment pad in the frag after_frag
+   publishes (src/app/fdctl/run/tiles/fd_verify.c:102-133), i.e. the
+   fd_txn_t and the u16 payload_sz.  The tile still holds the payload (it
+   wrote it into the txn link), so only the trailer crosses back and the
+   tile assembles payload | pad | trailer in its out dcache.
+   fd_ed25519_hip_frag_assemble does that into dst (room for
+   FD_ED25519_HIP_TPU_DCACHE_MTU bytes) and returns the frag's size, or 0
+   if the trailer does not belong to a payload of payload_sz bytes (too
+   short or too long, or its payload_sz differs): a protocol error.  The
+   pad byte is written as 0. */
+static inline unsigned long
+fd_ed25519_hip_frag_assemble( unsigned char * dst, unsigned char const * payload, unsigned long payload_sz,
+                              unsigned char const * trailer, unsigned long trailer_sz ) {
+  if( payload_sz>FD_ED25519_HIP_TXN_MTU || trailer_sz<2UL || trailer_sz>FD_ED25519_HIP_TXN_MAX_SZ + 2UL ) return 0UL;
+  if( ( (unsigned long)trailer[ trailer_sz-2UL ] | ( (unsigned long)trailer[ trailer_sz-1UL ]<<8 ) )!=payload_sz ) return 0UL;
+  unsigned long toff = ( payload_sz + 1UL ) & ~1UL;
+  __builtin_memcpy( dst, payload, payload_sz );
+  if( toff>payload_sz ) dst[ payload_sz ] = 0;
+  __builtin_memcpy( dst + toff, trailer, trailer_sz );
+  return toff + trailer_sz;
+}
 
 fd_ed25519_hip_shlink_t *
 fd_ed25519_hip_shlink_create( char const * name, unsigned long depth );
@@ -434,8 +461,9 @@ typedef struct {
    (slot_cnt, batch_sigs, flags as for fd_ed25519_hip_vtile_new) and
    publishes one frag per transaction to `out` in frag order: sig = cookie,
    the verdict (FD_ED25519_HIP_TXN_VERIFY_* / FD_ED25519_HIP_TXN_PARSE_FAILED)
-   as byte 0, and for SUCCESS the frag the verify tile publishes to dedup
-   after it (fd_ed25519_hip_txn_frag's layout, new_sz bytes).  A frag with ctl EOS ends the stream:
+   as byte 0, and for SUCCESS the trailer of the frag the verify tile
+   publishes to dedup after it (fd_ed25519_hip_frag_assemble above; the
+   frag as fd_ed25519_hip_txn_frag lays it out).  A frag with ctl EOS ends the stream:
    the service answers everything before it, publishes an EOS frag and
    returns.  A batch is submitted when full, or when `in` is drained and a
    slot is free. */

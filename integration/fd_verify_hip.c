@@ -28,18 +28,25 @@
      after_frag    ... and handed over (commit); sig = (frag count << 32) |
                    tsorig, which the service echoes with the verdict
      after_credit  up to `burst` verdict frags are taken back in frag order;
-                   each SUCCESS frag is copied into the out dcache and
-                   published with fd_mux_publish (the mux guarantees `burst`
-                   credits here, src/disco/mux/fd_mux.c:548-559), the others
-                   are filtered -- publishing moves from after_frag to
-                   after_credit, which FD_MUX_FLAG_COPY|MANUAL_PUBLISH allow
-                   (fd_verify.c:232)
+                   a SUCCESS verdict carries the published frag's trailer
+                   (fd_txn_t, payload_sz), which the tile appends to its own
+                   payload (still in the txn link's dcache) in the out dcache
+                   (fd_ed25519_hip_frag_assemble) and publishes with
+                   fd_mux_publish (the mux guarantees `burst` credits here,
+                   src/disco/mux/fd_mux.c:548-559); the others are filtered
+                   -- publishing moves from after_frag to after_credit, which
+                   FD_MUX_FLAG_COPY|MANUAL_PUBLISH allow (fd_verify.c:232)
 
-   Flow control: the tile waits (in during_frag) only for room in the txn
-   link, which the service frees without ever waiting on the tile (it keeps
-   verdicts it cannot publish yet); so the wait always ends while the
-   service lives, and the mux's own backpressure (no after_credit, no new
-   frags while dedup is behind) bounds what is in flight.
+   Flow control: at most `cap` (the txn link's depth, at most
+   FD_VERIFY_HIP_RING) frags are unanswered, so the payload of every one of
+   them is still intact in the txn link's dcache (a room is reused only
+   depth+1 frags later).  The mux runs after_credit before each frag it
+   processes, one frag per pass (fd_mux.c:548-559), so after_credit keeps
+   the count below cap: when it is at cap, it waits for the oldest verdict,
+   which the service produces without ever waiting on the tile (it keeps
+   verdicts it cannot publish yet).  The wait ends while the service lives;
+   during_frag then always finds room, and the mux's own backpressure (no
+   after_credit, no new frags while dedup is behind) bounds the rest.
 
    Liveness (fd_cnc's heartbeat, src/tango/cnc/fd_cnc.h:63-65,129-130):
    the service ticks the heartbeat of the verdict link; during housekeeping
@@ -64,6 +71,7 @@
 #include <linux/unistd.h>
 
 #define FD_VERIFY_HIP_BURST    (16UL)
+#define FD_VERIFY_HIP_RING     (16384UL)                  /* unanswered frags at most (power of 2) */
 #define FD_VERIFY_HIP_STALE_NS (1000L*1000L*1000L)        /* 1 s without a heartbeat: the service is gone */
 #define FD_VERIFY_HIP_BOOT_NS  (60L*1000L*1000L*1000L)    /* the service's first tick (tables, engines)   */
 
@@ -87,6 +95,7 @@ typedef struct {
   fd_ed25519_hip_shlink_t * txl;   /* tile -> service: payloads */
   fd_ed25519_hip_shlink_t * vdl;   /* service -> tile: verdict byte (+ the frag to publish) */
   uchar *                   room;  /* during_frag's copy in the txn link, committed by after_frag */
+  ulong                     cap;   /* unanswered frags at most: min( txn link depth, FD_VERIFY_HIP_RING ) */
 
   ulong sent;                      /* frags handed to the service */
   ulong answered;                  /* verdicts taken back */
@@ -97,6 +106,11 @@ typedef struct {
   long  stale_ticks;
   long  boot_ticks;
   ulong beat;                      /* this tile's own heartbeat on the txn link */
+
+  struct {                         /* the payload of unanswered frag k, in the txn link's dcache */
+    uchar const * p;
+    ulong         sz;
+  } pay[ FD_VERIFY_HIP_RING ];     /* at k & (FD_VERIFY_HIP_RING-1) */
 } fd_verify_hip_ctx_t;
 
 FD_FN_CONST static inline ulong
@@ -220,64 +234,84 @@ after_frag( void *             _ctx,
   ulong cookie = ( (ctx->sent & 0xffffffffUL)<<32 ) | ( *opt_tsorig & 0xffffffffUL );
   if( FD_UNLIKELY( !ctx->room || fd_ed25519_hip_shlink_commit( ctx->txl, *opt_sz, cookie, 0U ) ) )
     FD_LOG_CRIT(( "txn link commit failed (sz %lu)", *opt_sz ));
+  ctx->pay[ ctx->sent & (FD_VERIFY_HIP_RING-1UL) ].p  = ctx->room;
+  ctx->pay[ ctx->sent & (FD_VERIFY_HIP_RING-1UL) ].sz = *opt_sz;
   ctx->room = NULL;
   ctx->sent++;
   /* not filtered and not published here: its verdict comes back through
      after_credit, which publishes it (SUCCESS) or drops it */
 }
 
-/* Up to FD_VERIFY_HIP_BURST verdicts, in frag order.  A verdict frag is the
-   fd_txn_verify / after_frag outcome as one byte (FD_TXN_VERIFY_SUCCESS 0,
-   FAILED -1, DEDUP -2, fd_txn_parse failed -3), followed for SUCCESS by the
-   frag after_frag publishes.  The service is trusted for verdicts (it
-   computes them), not for memory safety: every size is checked before a
-   byte lands in the out dcache. */
+/* The next verdict frag, if the service has published it: 1 taken (and
+   published or filtered), 0 none yet.  A verdict frag is the fd_txn_verify
+   / after_frag outcome as one byte (FD_TXN_VERIFY_SUCCESS 0, FAILED -1,
+   DEDUP -2, fd_txn_parse failed -3), followed for SUCCESS by the published
+   frag's trailer.  The service is trusted for verdicts (it computes them),
+   not for memory safety: every size is checked before a byte lands in the
+   out dcache. */
+static int
+take_verdict( fd_verify_hip_ctx_t * ctx,
+              fd_mux_context_t *    mux ) {
+  ulong sz; ulong sig; uint ctl; int err;
+  uchar const * v = fd_ed25519_hip_shlink_peek( ctx->vdl, &sz, &sig, &ctl, &err );
+  if( FD_LIKELY( !v ) ) {
+    if( FD_UNLIKELY( err<0 ) ) protocol_error( ctx, "verdict link overrun or line out of bounds" );
+    return 0;
+  }
+  if( FD_UNLIKELY( (ctl & FD_ED25519_HIP_SHLINK_CTL_EOS) || ctx->answered==ctx->sent ) ) protocol_error( ctx, "unexpected frag" );
+  if( FD_UNLIKELY( (sig>>32)!=(ctx->answered & 0xffffffffUL) || !sz ) ) protocol_error( ctx, "verdict out of order" );
+  schar verdict = (schar)v[ 0 ];
+  ulong tsorig  = sig & 0xffffffffUL;
+
+  if( FD_LIKELY( verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ) ) {
+    ulong         k   = ctx->answered & (FD_VERIFY_HIP_RING-1UL);
+    uchar const * pay = ctx->pay[ k ].p;
+    ulong         psz = ctx->pay[ k ].sz;
+    uchar * dst = (uchar *)fd_chunk_to_laddr( ctx->out_mem, ctx->out_chunk );
+    ulong new_sz = fd_ed25519_hip_frag_assemble( dst, pay, psz, v+1, sz-1UL );
+    if( FD_UNLIKELY( !new_sz || new_sz>FD_TPU_DCACHE_MTU ) ) protocol_error( ctx, "published frag trailer" );
+    if( FD_UNLIKELY( fd_ed25519_hip_shlink_advance( ctx->vdl ) ) ) protocol_error( ctx, "verdict frag overwritten" );
+
+    /* the publish sig is fd_txn_verify's txn_sig, the HA dedup tag: the
+       first 8 bytes of the first signature (fd_verify.h:65), found
+       through the frag's own fd_txn_t (fd_verify.c:102-128 layout) */
+    ulong txnt_off = fd_ulong_align_up( psz, 2UL );
+    if( FD_UNLIKELY( txnt_off + sizeof(fd_txn_t) + 2UL>new_sz ) ) protocol_error( ctx, "published frag layout" );
+    fd_txn_t const * txn_t = (fd_txn_t const *)( dst + txnt_off );
+    ulong signature_off = (ulong)txn_t->signature_off;
+    if( FD_UNLIKELY( signature_off + 8UL>psz ) ) protocol_error( ctx, "published frag signature offset" );
+    ulong txn_sig = FD_LOAD( ulong, dst + signature_off );
+
+    ulong tspub = (ulong)fd_frag_meta_ts_comp( fd_tickcount() );
+    fd_mux_publish( mux, txn_sig, ctx->out_chunk, new_sz, 0UL, tsorig, tspub );
+    ctx->out_chunk = fd_dcache_compact_next( ctx->out_chunk, new_sz, ctx->out_chunk0, ctx->out_wmark );
+    ctx->published++;
+  } else {
+    if( FD_UNLIKELY( sz!=1UL || verdict<FD_ED25519_HIP_TXN_PARSE_FAILED || verdict>FD_ED25519_HIP_TXN_VERIFY_FAILED ) )
+      protocol_error( ctx, "verdict value" );
+    if( FD_UNLIKELY( fd_ed25519_hip_shlink_advance( ctx->vdl ) ) ) protocol_error( ctx, "verdict frag overwritten" );
+    /* filtered, as fd_verify.c:119 / :148 */
+  }
+  ctx->answered++;
+  return 1;
+}
+
+/* Up to FD_VERIFY_HIP_BURST verdicts, in frag order; then, if cap frags
+   are unanswered, wait for the oldest (the frag the mux processes next
+   needs room, and every unanswered payload must stay intact).  At most
+   one frag arrives between two calls, so the wait takes one verdict and
+   the burst is never exceeded. */
 static void
 after_credit( void *             _ctx,
               fd_mux_context_t * mux ) {
   fd_verify_hip_ctx_t * ctx = (fd_verify_hip_ctx_t *)_ctx;
 
-  for( ulong n=0UL; n<FD_VERIFY_HIP_BURST; n++ ) {
-    ulong sz; ulong sig; uint ctl; int err;
-    uchar const * v = fd_ed25519_hip_shlink_peek( ctx->vdl, &sz, &sig, &ctl, &err );
-    if( FD_LIKELY( !v ) ) {
-      if( FD_UNLIKELY( err<0 ) ) protocol_error( ctx, "verdict link overrun or line out of bounds" );
-      return;
-    }
-    if( FD_UNLIKELY( (ctl & FD_ED25519_HIP_SHLINK_CTL_EOS) || ctx->answered==ctx->sent ) ) protocol_error( ctx, "unexpected frag" );
-    if( FD_UNLIKELY( (sig>>32)!=(ctx->answered & 0xffffffffUL) || !sz ) ) protocol_error( ctx, "verdict out of order" );
-    schar verdict = (schar)v[ 0 ];
-    ulong tsorig  = sig & 0xffffffffUL;
-
-    if( FD_LIKELY( verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ) ) {
-      ulong new_sz = sz - 1UL;
-      if( FD_UNLIKELY( new_sz<2UL || new_sz>FD_TPU_DCACHE_MTU ) ) protocol_error( ctx, "published frag size" );
-      uchar * dst = (uchar *)fd_chunk_to_laddr( ctx->out_mem, ctx->out_chunk );
-      fd_memcpy( dst, v+1, new_sz );
-      if( FD_UNLIKELY( fd_ed25519_hip_shlink_advance( ctx->vdl ) ) ) protocol_error( ctx, "verdict frag overwritten" );
-
-      /* the publish sig is fd_txn_verify's txn_sig, the HA dedup tag: the
-         first 8 bytes of the first signature (fd_verify.h:65), found
-         through the frag's own fd_txn_t (fd_verify.c:102-128 layout) */
-      ulong payload_sz = (ulong)FD_LOAD( ushort, dst + new_sz - 2UL );
-      ulong txnt_off   = fd_ulong_align_up( payload_sz, 2UL );
-      if( FD_UNLIKELY( payload_sz>FD_TPU_MTU || txnt_off + sizeof(fd_txn_t) + 2UL>new_sz ) ) protocol_error( ctx, "published frag layout" );
-      fd_txn_t const * txn_t = (fd_txn_t const *)( dst + txnt_off );
-      ulong signature_off = (ulong)txn_t->signature_off;
-      if( FD_UNLIKELY( signature_off + 8UL>payload_sz ) ) protocol_error( ctx, "published frag signature offset" );
-      ulong txn_sig = FD_LOAD( ulong, dst + signature_off );
-
-      ulong tspub = (ulong)fd_frag_meta_ts_comp( fd_tickcount() );
-      fd_mux_publish( mux, txn_sig, ctx->out_chunk, new_sz, 0UL, tsorig, tspub );
-      ctx->out_chunk = fd_dcache_compact_next( ctx->out_chunk, new_sz, ctx->out_chunk0, ctx->out_wmark );
-      ctx->published++;
-    } else {
-      if( FD_UNLIKELY( sz!=1UL || verdict<FD_ED25519_HIP_TXN_PARSE_FAILED || verdict>FD_ED25519_HIP_TXN_VERIFY_FAILED ) )
-        protocol_error( ctx, "verdict value" );
-      if( FD_UNLIKELY( fd_ed25519_hip_shlink_advance( ctx->vdl ) ) ) protocol_error( ctx, "verdict frag overwritten" );
-      /* filtered, as fd_verify.c:119 / :148 */
-    }
-    ctx->answered++;
+  ulong n = 0UL;
+  while( n<FD_VERIFY_HIP_BURST && take_verdict( ctx, mux ) ) n++;
+  for( ulong spin=1UL; ctx->sent - ctx->answered>=ctx->cap; spin++ ) {
+    if( take_verdict( ctx, mux ) ) continue;
+    if( !(spin & 1023UL) ) check_service( ctx );
+    FD_SPIN_PAUSE();
   }
 }
 
@@ -308,6 +342,7 @@ privileged_init( fd_topo_t *      topo,
   link_name( name, sizeof(name), topo, tile, "vd" );
   ctx->vdl = fd_ed25519_hip_shlink_join( name );
   if( FD_UNLIKELY( !ctx->vdl ) ) FD_LOG_ERR(( "cannot join %s: is fd_verify_hip_service running for this GPU?", name ));
+  ctx->cap = fd_ulong_min( fd_ed25519_hip_shlink_depth( ctx->txl ), FD_VERIFY_HIP_RING );
 }
 
 static void

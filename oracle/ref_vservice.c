@@ -51,7 +51,9 @@ typedef struct {
 } svc_link_t;
 
 /* after_frag + fd_txn_verify of one payload into out (verdict byte, then
-   the published frag for SUCCESS); returns the verdict frag's size */
+   for SUCCESS the published frag's trailer: its bytes after the payload and
+   pad, the fd_txn_t and payload_sz -- the tile has the payload); returns
+   the verdict frag's size */
 static ulong
 answer( svc_link_t * L, uchar const * payload, ulong payload_sz, uchar * out ) {
   uchar * frag = out + 1;
@@ -69,7 +71,8 @@ answer( svc_link_t * L, uchar const * payload, ulong payload_sz, uchar * out ) {
   int res = fd_txn_verify( &L->vctx, frag, (ushort)payload_sz, txn_t, &txn_sig );
   if( res!=FD_TXN_VERIFY_SUCCESS ) { out[0] = (uchar)(schar)res; return 1UL; }
   out[0] = 0;
-  return 1UL + new_sz;
+  memmove( out + 1, frag + txnt_off, new_sz - txnt_off );
+  return 1UL + new_sz - txnt_off;
 }
 
 int

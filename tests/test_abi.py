@@ -20,6 +20,9 @@ def declared_symbols():
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^\s*(fd_[a-z0-9_]+)\s*\(", text, flags=re.M):
             syms.add(m.group(1))
+        # header-only helpers (static inline) are not library symbols
+        for m in re.finditer(r"^static inline [^\n]*\n\s*(fd_[a-z0-9_]+)\s*\(", text, flags=re.M):
+            syms.discard(m.group(1))
     return syms
 
 

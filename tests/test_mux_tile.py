@@ -201,10 +201,11 @@ def test_tile_stops_when_service_fails(stream, tmp_path):
     _expect_tile_stops(stream, tmp_path, ("--fail-after", "400"), "verify service failed (link status -1700)", 15.0)
 
 
-@pytest.mark.parametrize("bad", ["order", "size", "verdict"])
+@pytest.mark.parametrize("bad", ["order", "size", "trailer", "verdict"])
 def test_tile_refuses_protocol_violations(stream, tmp_path, bad):
     """A service that answers out of order, with a SUCCESS verdict that
-    carries no frag, or with a verdict that does not exist: the tile marks its txn
+    carries no trailer, with a trailer that belongs to a payload of another
+    size, or with a verdict that does not exist: the tile marks its txn
     link failed (so the service stops too) and ends; nothing malformed is
     published."""
     path, frags = stream
@@ -227,7 +228,9 @@ def test_tile_refuses_protocol_violations(stream, tmp_path, bad):
             elif bad == "order":
                 assert vdl.publish(bytes([0xFF]), sig + (1 << 32))
             elif bad == "size":
-                assert vdl.publish(b"\0", sig)   # SUCCESS without the frag to publish
+                assert vdl.publish(b"\0", sig)   # SUCCESS without the trailer
+            elif bad == "trailer":   # fd_txn_t-sized, but its payload_sz is not this payload's
+                assert vdl.publish(b"\0" + bytes(64) + (len(payload) + 1).to_bytes(2, "little"), sig)
             else:
                 assert vdl.publish(bytes([0x05]), sig)
             n += 1

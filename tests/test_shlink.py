@@ -20,9 +20,16 @@ def fake_verdict(payload):
     return (len(payload) % 7) - 3
 
 
-def fake_frag(payload):
-    """A SUCCESS verdict frag carries the published frag: here a stand-in."""
-    return payload[::-1] + b"\x5a"
+def fake_trailer(payload):
+    """A SUCCESS verdict frag carries the published frag's trailer (the
+    fd_txn_t, then the u16 payload_sz): here a stand-in of some length."""
+    return b"\x5a" * (len(payload) % 13) + len(payload).to_bytes(2, "little")
+
+
+def assembled(payload):
+    """what the tile publishes: payload, the alignment pad (0), the trailer
+    (fd_ed25519_hip_frag_assemble)"""
+    return payload + b"\0" * (len(payload) % 2) + fake_trailer(payload)
 
 
 def serve_fake(txl, vdl, proc, deadline_s=60.0, stop_after=None, fail_after=None):
@@ -70,7 +77,7 @@ def serve_fake(txl, vdl, proc, deadline_s=60.0, stop_after=None, fail_after=None
             continue
         assert sig == n
         v = fake_verdict(payload)
-        pending.append((sig, v, fake_frag(payload) if v == 0 else b""))
+        pending.append((sig, v, fake_trailer(payload) if v == 0 else b""))
         n += 1
 
 
@@ -102,7 +109,7 @@ def test_sandboxed_producer_round_trip(tmp_path, sandbox, n, depth):
     got = np.frombuffer(out[:n], np.int8)
     want = np.array([fake_verdict(p) for p in payloads], np.int8)
     assert np.array_equal(got, want)
-    assert tile.parse_producer_frags(out[n:]) == [fake_frag(p) for p in payloads if fake_verdict(p) == 0]
+    assert tile.parse_producer_frags(out[n:]) == [assembled(p) for p in payloads if fake_verdict(p) == 0]
 
 
 @pytest.mark.parametrize("how", ["killed", "failed"])

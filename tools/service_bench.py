@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--gpu-parse", action="store_true")
     ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES of the service process")
     ap.add_argument("--service", default=SERVICE, help="service binary (an A/B build's)")
+    ap.add_argument("--producer", default=PRODUCER, help="tile-side binary (the same A/B build's: the frag protocol)")
     ap.add_argument("--pin", choices=["none", "node"], default="node",
                     help="node: the service and the tile processes on the CPUs of the GPU's NUMA node, as fdctl "
                          "pins its tiles (default); none: wherever the OS puts them")
@@ -81,7 +82,7 @@ def main():
         if not line.startswith("ready"):
             raise SystemExit(f"service did not start: {line!r} {svc.stderr.read()[-2000:]}")
         t0 = time.time()
-        prods = [subprocess.Popen([PRODUCER, f"{prefix}{i}_txn", f"{prefix}{i}_vd", paths[i]],
+        prods = [subprocess.Popen([args.producer, f"{prefix}{i}_txn", f"{prefix}{i}_vd", paths[i]],
                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, preexec_fn=pin) for i in range(k)]
         ok = True
         for pr in prods:

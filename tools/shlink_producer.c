@@ -13,8 +13,9 @@
    the service's EOS (and, as the tile's after_credit does, every 16
    frags).  Output on stdout, via write(2): n verdict bytes in
    frag order (checked against the sig of every verdict frag), then for
-   each SUCCESS verdict the frag the service returned with it (the frag
-   the verify tile publishes: u32 size, then the bytes); exit status 0, or
+   each SUCCESS verdict the frag the verify tile publishes, assembled as the
+   tile does from its own payload and the trailer the service returned
+   (fd_ed25519_hip_frag_assemble: u32 size, then the bytes); exit status 0, or
    2 on a protocol error, 3 if strict mode is unavailable, 4 if the service
    stopped: its heartbeat on OUT_LINK unchanged for MS milliseconds
    (default 1000; 60 s before its first tick) or a link marked failed
@@ -86,9 +87,15 @@ typedef struct {
   unsigned long   cap, used;
 } frags_t;
 
+typedef struct {
+  unsigned char const * pay;
+  unsigned long const * off;
+  unsigned int const *  sz;
+} stream_t;
+
 static int
 take_verdicts( fd_ed25519_hip_shlink_t * in, unsigned char * buf, signed char * verdict, unsigned long n,
-               unsigned long * next, int * eos, frags_t * fr ) {
+               unsigned long * next, int * eos, frags_t * fr, stream_t const * st ) {
   for(;;) {
     unsigned long sz = 0UL, sig = 0UL;
     unsigned int ctl = 0U;
@@ -100,10 +107,12 @@ take_verdicts( fd_ed25519_hip_shlink_t * in, unsigned char * buf, signed char * 
     signed char v = (signed char)buf[ 0 ];
     if( (v==FD_ED25519_HIP_TXN_VERIFY_SUCCESS) != (sz>1UL) ) return -1;   /* a frag with every SUCCESS, only then */
     if( sz>1UL ) {
-      unsigned int fsz = (unsigned int)(sz - 1UL);
-      if( fr->used + 4UL + fsz > fr->cap ) return -1;
+      unsigned long k = *next;
+      if( fr->used + 4UL + FD_ED25519_HIP_TPU_DCACHE_MTU > fr->cap ) return -1;
+      unsigned int fsz = (unsigned int)fd_ed25519_hip_frag_assemble( fr->mem + fr->used + 4UL, st->pay + st->off[ k ],
+                                                                     st->sz[ k ], buf + 1, sz - 1UL );
+      if( !fsz ) return -1;
       memcpy( fr->mem + fr->used, &fsz, 4UL );
-      memcpy( fr->mem + fr->used + 4UL, buf + 1, fsz );
       fr->used += 4UL + fsz;
     }
     verdict[ (*next)++ ] = v;
@@ -135,7 +144,7 @@ main( int argc, char ** argv ) {
   signed char * verdict = (signed char *)malloc( n + 1UL );
   unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
   frags_t fr;
-  fr.cap = total + n*(FD_ED25519_HIP_TXN_MAX_SZ + 8UL) + 64UL;   /* every payload + its trailer, size word */
+  fr.cap = total + n*(FD_ED25519_HIP_TXN_MAX_SZ + 8UL) + FD_ED25519_HIP_TPU_DCACHE_MTU;   /* every payload + pad, trailer, size word; one frag's room */
   fr.used = 0UL;
   fr.mem = (unsigned char *)malloc( fr.cap );
   if( !fr.mem ) return 1;
@@ -160,25 +169,26 @@ main( int argc, char ** argv ) {
   /* from here on: memory operations, write(2) and _exit(2) only */
   unsigned long i = 0UL, got = 0UL;
   int eos = 0;
+  stream_t st = { pay, off, sz };
   while( i<n ) {
     int r = fd_ed25519_hip_shlink_publish( txl, pay + off[ i ], sz[ i ], i, 0U );
     if( r==0 ) {
       /* as the tile's mux loop does (after_credit between frags): the
          verdicts that are back are taken every 16 frags, not only when the
          txn link runs out of credits */
-      if( !(++i & 15UL) && ( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) || eos ) ) leave( 2 );
+      if( !(++i & 15UL) && ( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr, &st ) || eos ) ) leave( 2 );
       continue;
     }
     if( r!=1 ) leave( 2 );
-    if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) || eos ) leave( 2 );
+    if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr, &st ) || eos ) leave( 2 );
     watch( &wt );
   }
   while( fd_ed25519_hip_shlink_publish( txl, NULL, 0UL, n, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
-    if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) || eos ) leave( 2 );
+    if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr, &st ) || eos ) leave( 2 );
     watch( &wt );
   }
   while( !eos ) {
-    if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr ) ) leave( 2 );
+    if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr, &st ) ) leave( 2 );
     watch( &wt );
   }
   if( got!=n ) leave( 2 );
