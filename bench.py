@@ -219,7 +219,7 @@ def config_c1(eng, args):
             "cpu_reference": cpu}
 
 
-def config_c3(eng, args):
+def config_c3(eng, args, inflight):
     """C3 (BASELINE.json configs[2]): multi-signer transactions with
     fd_ed25519_verify_batch_single_msg's semantics -- 1..12 signatures
     (uniform) over one shared 200-byte message each, all valid -- as a
@@ -251,11 +251,41 @@ def config_c3(eng, args):
     eng.sync()
     dt = time.perf_counter() - t
     codes = tout.download(np.int8, ntxn)
+    # the same batches with `inflight` of them in flight on one-stream
+    # engines (as the C2 steps and the pool's slots run): a batch's phases
+    # fill the previous batch's dsm tail
+    from firedancer_amd import ed25519
+    engs = [ed25519.Engine(device=eng.info()["device"], max_chunk=nsig, half=args.half, one_stream=True)
+            for _ in range(max(inflight, 1))]
+    eouts = [(e.alloc(nsig), e.alloc(ntxn)) for e in engs]
+
+    def run_k(k):
+        e, (o, to) = engs[k % len(engs)], eouts[k % len(engs)]
+        e.verify_dev(nsig, msgs.ptr, d_off.ptr, d_sz.ptr, sigs.ptr, pubs.ptr, o.ptr, e.stream)
+        e.txn_combine_dev(ntxn, o.ptr, d_first.ptr, d_cnt.ptr, to.ptr, e.stream)
+    for k in range(len(engs)):
+        run_k(k)
+    for e in engs:
+        e.sync()
+    t = time.perf_counter()
+    for k in range(20):
+        run_k(k)
+    for e in engs:
+        e.sync()
+    dtp = time.perf_counter() - t
+    ok_p = all(bool((to.download(np.int8, ntxn) == 0).all()) for _, to in eouts)
+    for o, to in eouts:
+        o.free()
+        to.free()
+    for e in engs:
+        e.close()
     for b in bufs:
         b.free()
     return {"txns": ntxn, "signatures": nsig, "sigs_per_txn": "1..12 uniform, one shared 200-byte message",
             "gpu_txn_per_s": 10 * ntxn / dt, "gpu_verifies_per_s": 10 * nsig / dt,
-            "gpu_ms_per_batch": dt * 1e3 / 10, "all_success": bool((codes == 0).all())}
+            "gpu_ms_per_batch": dt * 1e3 / 10, "all_success": bool((codes == 0).all()),
+            "pipelined": {"batches_in_flight": len(engs), "gpu_txn_per_s": 20 * ntxn / dtp,
+                          "gpu_verifies_per_s": 20 * nsig / dtp, "all_success": ok_p}}
 
 
 def latency_mode(eng, args, device):
@@ -637,7 +667,7 @@ def main():
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"C1 leg failed: {ex!r}")
         try:
-            c3 = config_c3(eng, args)
+            c3 = config_c3(eng, args, inflight)
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"C3 leg failed: {ex!r}")
             c3 = {"error": repr(ex)}
