@@ -196,7 +196,7 @@ def cpu_baseline(wl, gpu_codes, sample, reps, workload_name="C2"):
             "verdicts_equal_gpu": bool(np.array_equal(out, gpu_codes[:n]))}
 
 
-def config_c1(eng, args):
+def config_c1(eng, args, inflight):
     """C1 (BASELINE.json configs[0]): 16,384 single-signer ~200-byte
     signatures, all valid -- the reference's own CPU case.  The reference's
     fd_ed25519_verify on this host's cores (20 passes) next to this engine
@@ -212,10 +212,35 @@ def config_c1(eng, args):
     eng.sync()
     gpu_s = time.perf_counter() - t
     out = wl.out.download(np.int8, wl.n)
+    # the same batch with `inflight` launches in flight on one-stream engines
+    engs = [ed25519.Engine(device=eng.info()["device"], max_chunk=wl.n, half=args.half, one_stream=True)
+            for _ in range(max(inflight, 1))]
+    eouts = [e.alloc(wl.n) for e in engs]
+
+    def run_k(k):
+        e, o = engs[k % len(engs)], eouts[k % len(engs)]
+        e.verify_dev(wl.n, wl.msgs.ptr, wl.off.ptr, wl.sz.ptr, wl.sigs.ptr, wl.pubs.ptr, o.ptr, e.stream)
+    for k in range(len(engs)):
+        run_k(k)
+    for e in engs:
+        e.sync()
+    t = time.perf_counter()
+    for k in range(80):
+        run_k(k)
+    for e in engs:
+        e.sync()
+    gpu_p = time.perf_counter() - t
+    ok_p = all(bool((o.download(np.int8, wl.n) == 0).all()) for o in eouts)
+    for o in eouts:
+        o.free()
+    for e in engs:
+        e.close()
     cpu = cpu_baseline(wl, out, wl.n, 20, workload_name="C1")
     wl.free()
     return {"signatures": 16384, "msg_sz": 200, "gpu_verifies_per_s": 20 * 16384 / gpu_s,
             "gpu_ms_per_batch": gpu_s * 1e3 / 20, "all_valid": bool((out == 0).all()),
+            "pipelined": {"batches_in_flight": len(engs), "gpu_verifies_per_s": 80 * 16384 / gpu_p,
+                          "all_valid": ok_p},
             "cpu_reference": cpu}
 
 
@@ -663,7 +688,7 @@ def main():
             log(f"cpu baseline failed: {ex!r}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            c1 = config_c1(eng, args)
+            c1 = config_c1(eng, args, inflight)
         except Exception as ex:  # reported, never fatal for the GPU number
             log(f"C1 leg failed: {ex!r}")
         try:
