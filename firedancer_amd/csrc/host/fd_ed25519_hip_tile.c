@@ -764,9 +764,6 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
     r->resolved = 1;
     if( v!=FD_ED25519_HIP_TXN_VERIFY_SUCCESS ) continue;   /* filtered: not published */
     if( !vt->gpu_parse ) continue;                         /* its frag was built with the frag (vtile_frag) */
-#ifdef FD_ED25519_HIP_AB_NO_FRAGS
-    continue;   /* A/B build only: verdicts without the published frags (cost probe) */
-#endif
     {
       /* the published frag from the payload in the slot and the fd_txn_t
          trailer its parse left in the slot (the device's in GPU-parse
@@ -1395,9 +1392,6 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
       if( !dst ) break;
       unsigned long tsz = r->verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ? r->frag_sz : 0UL;
       dst[ 0 ] = (unsigned char)r->verdict;
-#ifdef FD_ED25519_HIP_AB_NO_FRAGS
-      if( !tsz ) dst[ 0 ] = (unsigned char)FD_ED25519_HIP_TXN_VERIFY_FAILED;   /* A/B cost probe: no frag to send */
-#endif
       if( tsz ) memcpy( dst + 1, vt->oa + r->arena_off, tsz );
       if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + tsz, r->cookie, 0U )) ) goto fail;
       vt_pop( vt );
