@@ -634,6 +634,9 @@ fd_ed25519_hip_vtile_new( int device, unsigned slot_cnt, unsigned long batch_sig
     fd_ed25519_hip_vtile_delete( vt );
     return NULL;
   }
+  /* touched now, not on the first frags (first-touch faults in the stream) */
+  memset( vt->q, 0, vt->q_cap*sizeof(vrec_t) );
+  memset( vt->oa, 0, vt->oa_cap );
   return vt;
 }
 
@@ -1163,6 +1166,15 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
     return FD_ED25519_HIP_ERR_NOMEM;
   }
   for( unsigned long k=0UL; k<ring_depth; k++ ) atomic_store( &rg.mcache[k].seq, (uint64_t)(k - ring_depth) );
+  /* every page the timed run writes is touched now: a first-touch fault
+     (a huge page zeroed, or compaction on a freshly started host) inside
+     the run would stall the producer or the tile for milliseconds and show
+     up as latency */
+  memset( rg.dcache, 0, rg.chunk_cnt*RING_CHUNK );
+  memset( t_pub, 0, txn_cnt*sizeof(double) );
+  memset( ck, 0, 4096UL*sizeof(unsigned long) );
+  memset( vd, 0, 4096UL );
+  for( unsigned long i=0UL; i<txn_cnt; i++ ) { lat_s[ i ] = -1.0; verdict[ i ] = 0; }
 
   producer_t pr;
   memset( &pr, 0, sizeof(pr) );
