@@ -320,6 +320,14 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   slot->t_submit = now_s();
   int err = slot_h2d( pipe, s, st, sig_cnt, txn_cnt, msg_bytes );
   if( err ) return err;
+#ifdef FD_ED25519_HIP_HOST_FAULT
+  /* test build only (tests/test_gpu_service_fault.py): the third batch's
+     launch fails after its copies are enqueued */
+  if( slot->seq==2UL ) {
+    fd_ed25519_hip_private_set_error( "pipe: injected launch failure (fault-injection build)" );
+    return FD_ED25519_HIP_ERR_HIP - (int)hipErrorLaunchFailure;
+  }
+#endif
   if( sig_cnt ) {
     err = fd_ed25519_hip_verify_dev( s->eng, sig_cnt, s->d_msgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
     if( err ) return err;
