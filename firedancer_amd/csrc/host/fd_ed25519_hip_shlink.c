@@ -33,12 +33,22 @@
    checked against the local geometry before its payload is copied (the
    reference tile's own check, src/app/fdctl/run/tiles/fd_verify.c:67).
 
+   Versioning and restarts: the header carries the frag protocol both
+   sides speak (FD_ED25519_HIP_SHLINK_PROTO); join refuses a link of
+   another protocol (errno EPROTO), so a tile and a service built from
+   different revisions of the verdict protocol never exchange frags.  It
+   also records the creating process: create reclaims a same-name link
+   whose creator has exited (a service that was killed leaves its links
+   behind) instead of failing, and still refuses one whose creator lives.
+
    No HIP: this file is also linked into the standalone sandboxed producer
    (tools/shlink_producer.c). */
 #define _GNU_SOURCE
 #include "../../../include/fd_ed25519_hip_tile.h"
 
+#include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -48,7 +58,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
-#define SHLINK_MAGIC 0xfd25519517a4c0deUL
+#define SHLINK_MAGIC 0xfd25519517a4c0dfUL   /* ...c0de before the protocol word (ABI <= 4) */
 #define SHLINK_CHUNK 64UL
 
 typedef struct {
@@ -68,7 +78,8 @@ typedef struct {
   uint64_t         mtu;
   _Atomic uint64_t heartbeat;   /* producer's liveness tick (0: not started) */
   _Atomic uint64_t status;      /* 0, or a failure code either side wrote     */
-  uint64_t         pad0[2];
+  uint64_t         proto;       /* FD_ED25519_HIP_SHLINK_PROTO of the creator  */
+  uint64_t         creator;     /* pid of the creating process                 */
   _Atomic uint64_t consumed;    /* consumer -> producer credits (own line) */
   uint64_t         pad1[7];
 } shlink_hdr_t;
@@ -114,13 +125,43 @@ shlink_map( char const * name, int fd, size_t sz ) {
   return l;
 }
 
+/* 1 if the object `name` is a link of this layout whose creating process
+   has exited (kill(pid, 0) fails with ESRCH): left behind by a process that
+   was killed, safe to remove.  A link whose creator lives (or cannot be
+   told apart: no creator recorded, another layout, a pid of another user)
+   is not. */
+static int
+shlink_orphaned( char const * name ) {
+  int fd = shm_open( name, O_RDONLY, 0 );
+  if( fd<0 ) return 0;
+  struct stat st;
+  int orphan = 0;
+  if( !fstat( fd, &st ) && (size_t)st.st_size>=sizeof(shlink_hdr_t) ) {
+    void * m = mmap( NULL, sizeof(shlink_hdr_t), PROT_READ, MAP_SHARED, fd, 0 );
+    if( m!=MAP_FAILED ) {
+      shlink_hdr_t const * h = (shlink_hdr_t const *)m;
+      uint64_t pid = h->creator;
+      if( h->magic==SHLINK_MAGIC && pid && pid<(1UL<<31) && kill( (pid_t)pid, 0 ) && errno==ESRCH ) orphan = 1;
+      munmap( m, sizeof(shlink_hdr_t) );
+    }
+  }
+  close( fd );
+  return orphan;
+}
+
 fd_ed25519_hip_shlink_t *
 fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
-  if( !name || !depth || (depth & (depth-1UL)) || strlen( name )>=120 ) return NULL;
+  if( !name || !depth || (depth & (depth-1UL)) || strlen( name )>=120 ) { errno = EINVAL; return NULL; }
   uint64_t chunk_cnt  = (depth + 2UL) * shlink_mtu_chunks();
   size_t   sz         = shlink_footprint( depth, chunk_cnt );
   int fd = shm_open( name, O_RDWR | O_CREAT | O_EXCL, 0600 );
-  if( fd<0 ) return NULL;
+  if( fd<0 && errno==EEXIST && shlink_orphaned( name ) ) {
+    /* a previous creator's link: reclaimed (a peer that still maps it keeps
+       the old object, whose heartbeat has stopped) */
+    shm_unlink( name );
+    fd = shm_open( name, O_RDWR | O_CREAT | O_EXCL, 0600 );
+  }
+  if( fd<0 ) return NULL;   /* errno EEXIST: a live process's link of that name */
   if( ftruncate( fd, (off_t)sz ) ) { close( fd ); shm_unlink( name ); return NULL; }
   fd_ed25519_hip_shlink_t * l = shlink_map( name, fd, sz );
   if( !l ) { shm_unlink( name ); return NULL; }
@@ -131,6 +172,8 @@ fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
   l->hdr->depth     = l->depth     = depth;
   l->hdr->chunk_cnt = l->chunk_cnt = chunk_cnt;
   l->hdr->mtu       = l->mtu       = FD_ED25519_HIP_SHLINK_MTU;
+  l->hdr->proto     = FD_ED25519_HIP_SHLINK_PROTO;
+  l->hdr->creator   = (uint64_t)getpid();
   atomic_store_explicit( &l->hdr->consumed, 0UL, memory_order_relaxed );
   atomic_store_explicit( &l->hdr->heartbeat, 0UL, memory_order_relaxed );
   atomic_store_explicit( &l->hdr->status, 0UL, memory_order_relaxed );
@@ -141,11 +184,11 @@ fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
 
 fd_ed25519_hip_shlink_t *
 fd_ed25519_hip_shlink_join( char const * name ) {
-  if( !name ) return NULL;
+  if( !name ) { errno = EINVAL; return NULL; }
   int fd = shm_open( name, O_RDWR, 0600 );
-  if( fd<0 ) return NULL;
+  if( fd<0 ) return NULL;   /* errno ENOENT: no such link (no service) */
   struct stat st;
-  if( fstat( fd, &st ) || (size_t)st.st_size<sizeof(shlink_hdr_t) ) { close( fd ); return NULL; }
+  if( fstat( fd, &st ) || (size_t)st.st_size<sizeof(shlink_hdr_t) ) { close( fd ); errno = EINVAL; return NULL; }
   fd_ed25519_hip_shlink_t * l = shlink_map( name, fd, (size_t)st.st_size );
   if( !l ) return NULL;
   /* one snapshot of the geometry, checked against what create makes */
@@ -154,10 +197,15 @@ fd_ed25519_hip_shlink_join( char const * name ) {
   uint64_t depth     = l->hdr->depth;
   uint64_t chunk_cnt = l->hdr->chunk_cnt;
   uint64_t mtu       = l->hdr->mtu;
-  if( magic!=SHLINK_MAGIC || !depth || (depth & (depth-1UL)) || depth>(1UL<<30) ||
+  uint64_t proto     = l->hdr->proto;
+  if( magic!=SHLINK_MAGIC || proto!=FD_ED25519_HIP_SHLINK_PROTO ) {
+    /* another layout or frag protocol (an earlier magic is a link of ABI <= 4) */
+    munmap( l->hdr, l->map_sz ); free( l ); errno = EPROTO; return NULL;
+  }
+  if( !depth || (depth & (depth-1UL)) || depth>(1UL<<30) ||
       mtu!=FD_ED25519_HIP_SHLINK_MTU || chunk_cnt!=(depth + 2UL) * shlink_mtu_chunks() ||
       shlink_footprint( depth, chunk_cnt )!=l->map_sz ) {
-    munmap( l->hdr, l->map_sz ); free( l ); return NULL;
+    munmap( l->hdr, l->map_sz ); free( l ); errno = EINVAL; return NULL;
   }
   l->depth = depth; l->chunk_cnt = chunk_cnt; l->mtu = mtu;
   l->dcache = (unsigned char *)l->mcache + depth * sizeof(shlink_meta_t);
@@ -286,6 +334,15 @@ fd_ed25519_hip_shlink_heartbeat( fd_ed25519_hip_shlink_t * l, unsigned long now 
 unsigned long
 fd_ed25519_hip_shlink_heartbeat_query( fd_ed25519_hip_shlink_t const * l ) {
   return atomic_load_explicit( &l->hdr->heartbeat, memory_order_acquire );
+}
+
+int
+fd_ed25519_hip_shlink_watch( fd_ed25519_hip_shlink_watch_t * w, fd_ed25519_hip_shlink_t const * l, long now_ns,
+                             long stale_ns ) {
+  unsigned long hb = fd_ed25519_hip_shlink_heartbeat_query( l );
+  if( !w->seen || hb!=w->last ) { w->last = hb; w->t_ns = now_ns; w->seen = 1; }
+  if( !hb ) return 1;     /* the producer has not ticked yet */
+  return ( stale_ns>0L && now_ns - w->t_ns>stale_ns ) ? -1 : 0;
 }
 
 void

@@ -619,6 +619,14 @@ struct fd_ed25519_hip_vtile {
   unsigned long             resolved_head;  /* records [q_head, q_head+resolved_head) are resolved */
   unsigned char *           oa;         /* output arena: a ring of frags, [oa_head, oa_tail) cyclically */
   unsigned long             oa_cap, oa_head, oa_tail, oa_live;
+  /* the verify service's waits (internal): while every slot is in flight
+     the vtile polls the oldest batch instead of blocking in the runtime,
+     calling idle between polls (heartbeats, link watch: nonzero aborts the
+     wait with that code), and fails with FD_ED25519_HIP_ERR_TIMEOUT when
+     the batch has not completed after hang_s (a hung GPU) */
+  int                    (* idle)( void * );
+  void *                    idle_ctx;
+  double                    hang_s;
 };
 
 fd_ed25519_hip_vtile_t *
@@ -865,6 +873,35 @@ vt_submit_open( fd_ed25519_hip_vtile_t * vt ) {
   return 1;
 }
 
+static inline void spin_pause( void );
+
+/* every slot in flight: wait for the oldest batch (1: one completed and
+   resolved, 0: vt->err is set) -- blocking in the runtime, or, with an idle
+   hook (the verify service), polling it with the hook between polls and a
+   bound on how long a batch may take */
+static int
+vt_wait_oldest( fd_ed25519_hip_vtile_t * vt ) {
+  if( !vt->idle ) return vt_drain_one( vt, 1 );
+  double t0 = now_s();
+  for( unsigned long spin=1UL;; spin++ ) {
+    if( vt_drain_one( vt, 0 ) ) return 1;
+    if( vt->err ) return 0;
+    if( !(spin & 63UL) ) {
+      int r = vt->idle( vt->idle_ctx );
+      if( r ) { vt->err = r; return 0; }
+      if( vt->hang_s>0.0 && now_s() - t0>vt->hang_s ) {
+        char buf[ 128 ];
+        snprintf( buf, sizeof(buf), "vtile: batch %lu did not complete within %.1f s (GPU hang)",
+                  vt->pipe->seq - fd_ed25519_hip_pipe_in_flight( vt->pipe ), vt->hang_s );
+        fd_ed25519_hip_private_set_error( buf );
+        vt->err = FD_ED25519_HIP_ERR_TIMEOUT;
+        return 0;
+      }
+    }
+    spin_pause();
+  }
+}
+
 /* 0, or the vtile's sticky error (the open slot is then NULL) */
 static int
 vt_open( fd_ed25519_hip_vtile_t * vt ) {
@@ -873,7 +910,7 @@ vt_open( fd_ed25519_hip_vtile_t * vt ) {
   for( ;; ) {
     vt->open = fd_ed25519_hip_pipe_acquire( vt->pipe );  /* counts start at 0 */
     if( vt->open ) break;
-    if( !vt_drain_one( vt, 1 ) && vt->err ) return vt->err;  /* every slot in flight: wait for the oldest */
+    if( !vt_wait_oldest( vt ) && vt->err ) return vt->err;
   }
   vt->open_seq = vt->pipe->seq;
   return 0;
@@ -1349,14 +1386,20 @@ fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_c
    shlink out).
 
    Liveness and failure policy (the GPU side of fd_cnc's heartbeat,
-   src/tango/cnc/fd_cnc.h:63-65,129-130): every pass of the loop ticks the
-   heartbeat of `out` (the tile watches it and stops waiting when it goes
-   stale, integration/fd_verify_hip.c).  On a failure -- a batch the GPU did
-   not complete, a launch or allocation that failed, a tile that broke the
-   frag protocol or marked a link failed, a stop request from a sibling
-   link of the same service -- the service publishes nothing more, marks
-   both links failed with the code (fd_ed25519_hip_shlink_status) and
-   returns it; it never aborts the process mid-batch. */
+   src/tango/cnc/fd_cnc.h:63-65,129-130, and of fd_topo_run's supervision,
+   src/disco/topo/fd_topo_run.c:50-100): every pass of the loop, and every
+   few polls while it waits for the GPU, ticks the heartbeat of `out` (the
+   tile watches it and stops waiting when it goes stale,
+   integration/fd_verify_hip.c) and watches the tile's heartbeat on `in`.
+   What a tile causes -- it marked a link failed, overran its txn link, or
+   its heartbeat stopped -- ends that link pair: nothing more is published
+   on it, both links are marked failed with the code, its vtile (engines,
+   device memory) is freed, and the service's other links are served on.
+   What the device causes -- a batch the GPU failed or did not complete in
+   time, a launch or allocation that failed -- ends every link: the failing
+   link raises the service's stop flag and each sibling ends with
+   FD_ED25519_HIP_SHLINK_FAIL_STOPPED.  The service never aborts the
+   process mid-batch. */
 
 /* an idle pass of a polling loop (FD_SPIN_PAUSE's role in the reference's
    tiles): a pause hint, so a link thread with nothing to do yields its
@@ -1368,21 +1411,83 @@ spin_pause( void ) {
 #endif
 }
 
+static long
+now_ns( void ) {
+  struct timespec ts;
+  clock_gettime( CLOCK_MONOTONIC, &ts );
+  return ts.tv_sec*1000000000L + ts.tv_nsec;
+}
+
+typedef struct {
+  fd_ed25519_hip_shlink_t *        in;
+  fd_ed25519_hip_shlink_t *        out;
+  fd_ed25519_hip_shlink_watch_t    tile;       /* the tile's heartbeat on `in` */
+  long                             tile_stale_ns;
+  int volatile const *             ext_stop;   /* the caller's stop request */
+  _Atomic int *                    dev_stop;   /* a sibling link saw the device fail */
+  unsigned long                    beat;
+  int                              hook_rc;    /* what the idle hook last ended a wait with ... */
+  int                              hook_local; /* ... and whether that is the link's own end     */
+} vsvc_link_t;
+
+/* One liveness pass: ticks the service's heartbeat, then 0 (serve on) or
+   the code the link ends with.  *local = 1 when the cause is the tile's
+   or the caller's (the link alone ends), 0 when a sibling saw the device
+   fail. */
+static int
+vsvc_check( vsvc_link_t * L, int * local ) {
+  fd_ed25519_hip_shlink_heartbeat( L->out, L->beat++ );
+  *local = 1;
+  if( L->ext_stop && *L->ext_stop ) return FD_ED25519_HIP_SHLINK_FAIL_STOPPED;
+  if( L->dev_stop && atomic_load_explicit( L->dev_stop, memory_order_acquire ) ) {
+    *local = 0;
+    return FD_ED25519_HIP_SHLINK_FAIL_STOPPED;
+  }
+  int ts = fd_ed25519_hip_shlink_status( L->in );
+  if( !ts ) ts = fd_ed25519_hip_shlink_status( L->out );
+  if( ts ) return ts;   /* the tile gave up on the link */
+  if( fd_ed25519_hip_shlink_watch( &L->tile, L->in, now_ns(), L->tile_stale_ns )<0 )
+    return FD_ED25519_HIP_SHLINK_FAIL_TILE_GONE;
+  return 0;
+}
+
+/* the vtile's idle hook while every slot is in flight */
+static int
+vsvc_idle( void * ctx ) {
+  vsvc_link_t * L = (vsvc_link_t *)ctx;
+  int local = 1;
+  int rc = vsvc_check( L, &local );
+  if( rc ) { L->hook_rc = rc; L->hook_local = local; }
+  return rc;
+}
+
 static int
 vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
                fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
-               fd_ed25519_hip_vservice_stats_t * stats, _Atomic int * stop ) {
+               fd_ed25519_hip_vservice_stats_t * stats, _Atomic int * stop,
+               fd_ed25519_hip_vservice_opts_t const * opts ) {
   if( !in || !out ) return FD_ED25519_HIP_ERR_INVAL;
+  vsvc_link_t L;
+  memset( &L, 0, sizeof(L) );
+  L.in = in; L.out = out; L.dev_stop = stop; L.beat = 1UL;
+  L.ext_stop      = opts ? opts->stop : NULL;
+  L.tile_stale_ns = !opts || !opts->tile_stale_ns ? FD_ED25519_HIP_VSERVICE_TILE_STALE_NS : opts->tile_stale_ns;
+  long hang_ns    = !opts || !opts->gpu_hang_ns ? FD_ED25519_HIP_VSERVICE_GPU_HANG_NS : opts->gpu_hang_ns;
   fd_ed25519_hip_vtile_t * vt = fd_ed25519_hip_vtile_new( device, slot_cnt, batch_sigs, 16UL, 64UL, flags );
   if( !vt ) {
     fd_ed25519_hip_shlink_fail( in, FD_ED25519_HIP_ERR_INVAL ); fd_ed25519_hip_shlink_fail( out, FD_ED25519_HIP_ERR_INVAL );
+    if( stop ) atomic_store_explicit( stop, 1, memory_order_release );
+    if( stats ) stats->end_code = FD_ED25519_HIP_ERR_INVAL;
     return FD_ED25519_HIP_ERR_INVAL;
   }
   vt->trailer_only = 1;   /* the tile keeps its payloads: verdict frags carry the trailers */
+  vt->idle     = vsvc_idle;
+  vt->idle_ctx = &L;
+  vt->hang_s   = hang_ns>0L ? 1e-9*(double)hang_ns : 0.0;
   unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
   double t0 = now_s(), t_first = 0.0;   /* the stream's time runs from its first frag */
-  unsigned long txns = 0UL, beat = 1UL;
-  int eos = 0, rc = FD_ED25519_HIP_OK;
+  unsigned long txns = 0UL;
+  int eos = 0, rc = FD_ED25519_HIP_OK, local = 0;
   if( !buf ) { rc = FD_ED25519_HIP_ERR_NOMEM; goto fail; }
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
   /* A/B build only: cycles per loop section (printed at the end) */
@@ -1394,11 +1499,7 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
 #define PF_MARK( i ) do {} while(0)
 #endif
   for(;;) {
-    fd_ed25519_hip_shlink_heartbeat( out, beat++ );
-    if( stop && atomic_load_explicit( stop, memory_order_acquire ) ) { rc = FD_ED25519_HIP_SHLINK_FAIL_STOPPED; goto fail; }
-    int ts = fd_ed25519_hip_shlink_status( in );
-    if( !ts ) ts = fd_ed25519_hip_shlink_status( out );
-    if( ts ) { rc = ts; goto fail; }   /* the tile gave up on the link */
+    if( (rc = vsvc_check( &L, &local )) ) goto fail;
     PF_MARK( 0 );
     /* completed batches resolve (in frag order); their verdicts go out as
        far as credits allow: the verdict byte, then (SUCCESS) the trailer
@@ -1413,12 +1514,16 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
       unsigned long tsz = r->verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ? r->frag_sz : 0UL;
       dst[ 0 ] = (unsigned char)r->verdict;
       if( tsz ) memcpy( dst + 1, vt->oa + r->arena_off, tsz );
-      if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + tsz, r->cookie, 0U )) ) goto fail;
+      if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + tsz, r->cookie, 0U )) ) { local = 0; goto fail; }
       vt_pop( vt );
       published = 1;
     }
     PF_MARK( 1 );
-    if( (rc = fd_ed25519_hip_vtile_error( vt )) ) goto fail;
+    if( (rc = fd_ed25519_hip_vtile_error( vt )) ) {
+      /* a wait the idle hook ended is the hook's cause; any other vtile error the device's */
+      local = rc==L.hook_rc ? L.hook_local : 0;
+      goto fail;
+    }
     if( eos && !fd_ed25519_hip_vtile_pending( vt ) ) break;
     /* after_frag for every frag that is ready (copied out of the shared
        dcache first: the tile is not trusted not to change it meanwhile) */
@@ -1434,11 +1539,11 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
       pf_cons += __rdtsc() - c0;
 #endif
       if( r==1 ) break;
-      if( r ) { rc = FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL; goto fail; }   /* overrun: the tile ignored credits */
+      if( r ) { rc = FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL; local = 1; goto fail; }   /* overrun: the tile ignored credits */
       if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { eos = 1; break; }
       if( !txns ) t_first = now_s();
       r = fd_ed25519_hip_vtile_frag( vt, buf, sz, sig );
-      if( r<0 ) { rc = r; goto fail; }
+      if( r<0 ) { rc = r; local = rc==L.hook_rc ? L.hook_local : 0; goto fail; }
       txns++;
       pulled = 1;
     }
@@ -1469,14 +1574,14 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
            (double)vt_resolve_cycles/(double)(txns+1UL) );
 #endif
   while( fd_ed25519_hip_shlink_publish( out, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
-    fd_ed25519_hip_shlink_heartbeat( out, beat++ );
-    if( fd_ed25519_hip_shlink_status( in ) || fd_ed25519_hip_shlink_status( out ) ) break;
+    if( (rc = vsvc_check( &L, &local )) ) goto fail;
+    spin_pause();
   }
   goto done;
 fail:
   fd_ed25519_hip_shlink_fail( in, rc );
   fd_ed25519_hip_shlink_fail( out, rc );
-  if( stop ) atomic_store_explicit( stop, 1, memory_order_release );
+  if( stop && !local ) atomic_store_explicit( stop, 1, memory_order_release );
 done:
   if( stats ) {
     stats->txn_cnt      = txns;
@@ -1484,8 +1589,10 @@ done:
     stats->seconds      = now_s() - ( txns ? t_first : t0 );
     stats->device_bytes = fd_ed25519_hip_vtile_device_bytes( vt );
     stats->shared_device_bytes = fd_ed25519_hip_shared_device_bytes( device );
+    stats->end_code     = rc;
   }
   free( buf );
+  vt->idle = NULL;   /* the delete below may wait for batches in flight */
   fd_ed25519_hip_vtile_delete( vt );
   return rc;
 }
@@ -1494,30 +1601,40 @@ int
 fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
                              fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
                              fd_ed25519_hip_vservice_stats_t * stats ) {
-  return vservice_loop( device, slot_cnt, batch_sigs, flags, in, out, stats, NULL );
+  return vservice_loop( device, slot_cnt, batch_sigs, flags, in, out, stats, NULL, NULL );
 }
 
 typedef struct {
-  int                              device, flags, rc;
-  unsigned                         slot_cnt;
-  unsigned long                    batch_sigs;
-  fd_ed25519_hip_shlink_t *        in;
-  fd_ed25519_hip_shlink_t *        out;
-  fd_ed25519_hip_vservice_stats_t  st;
-  _Atomic int *                    stop;
+  int                                    device, flags, rc;
+  unsigned                               slot_cnt;
+  unsigned long                          batch_sigs;
+  fd_ed25519_hip_shlink_t *              in;
+  fd_ed25519_hip_shlink_t *              out;
+  fd_ed25519_hip_vservice_stats_t        st;
+  _Atomic int *                          stop;
+  fd_ed25519_hip_vservice_opts_t const * opts;
 } vservice_job_t;
 
 static void *
 vservice_main( void * arg ) {
   vservice_job_t * j = (vservice_job_t *)arg;
-  j->rc = vservice_loop( j->device, j->slot_cnt, j->batch_sigs, j->flags, j->in, j->out, &j->st, j->stop );
+  j->rc = vservice_loop( j->device, j->slot_cnt, j->batch_sigs, j->flags, j->in, j->out, &j->st, j->stop, j->opts );
   return NULL;
 }
 
+/* link-local ends: the tile's (protocol, gone, its own status codes) and
+   the caller's stop; everything else is the device's */
+static int
+vsvc_code_is_device( int rc ) {
+  return rc && rc!=FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL && rc!=FD_ED25519_HIP_SHLINK_FAIL_STOPPED &&
+         rc!=FD_ED25519_HIP_SHLINK_FAIL_TILE_GONE;
+}
+
 int
-fd_ed25519_hip_vservice_run_links( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
-                                   fd_ed25519_hip_shlink_t * const * in, fd_ed25519_hip_shlink_t * const * out,
-                                   unsigned link_cnt, fd_ed25519_hip_vservice_stats_t * stats ) {
+fd_ed25519_hip_vservice_serve( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+                               fd_ed25519_hip_shlink_t * const * in, fd_ed25519_hip_shlink_t * const * out,
+                               unsigned link_cnt, fd_ed25519_hip_vservice_stats_t * stats,
+                               fd_ed25519_hip_vservice_opts_t const * opts ) {
   if( !link_cnt || link_cnt>FD_ED25519_HIP_VSERVICE_LINK_MAX || !in || !out ) return FD_ED25519_HIP_ERR_INVAL;
   vservice_job_t * job = (vservice_job_t *)calloc( link_cnt, sizeof(vservice_job_t) );
   pthread_t *      th  = (pthread_t *)calloc( link_cnt, sizeof(pthread_t) );
@@ -1528,25 +1645,38 @@ fd_ed25519_hip_vservice_run_links( int device, unsigned slot_cnt, unsigned long 
   for( unsigned k=0U; k<link_cnt; k++ ) {
     vservice_job_t * j = &job[ k ];
     j->device = device; j->flags = flags; j->slot_cnt = slot_cnt; j->batch_sigs = batch_sigs;
-    j->in = in[ k ]; j->out = out[ k ]; j->stop = &stop;
+    j->in = in[ k ]; j->out = out[ k ]; j->stop = &stop; j->opts = opts;
     if( pthread_create( &th[ k ], NULL, vservice_main, j ) ) {
       rc = FD_ED25519_HIP_ERR_NOMEM;
       atomic_store_explicit( &stop, 1, memory_order_release );
       for( unsigned m=k; m<link_cnt; m++ ) {
         fd_ed25519_hip_shlink_fail( in[ m ], rc ); fd_ed25519_hip_shlink_fail( out[ m ], rc );
+        job[ m ].st.end_code = rc;
       }
       break;
     }
     started++;
   }
+  /* the result: a device-wide failure's code first, else the first
+     link-local end, else OK (every link ended with EOS) */
+  int local_rc = FD_ED25519_HIP_OK;
   for( unsigned k=0U; k<started; k++ ) {
     pthread_join( th[ k ], NULL );
-    /* the first real failure, not the siblings' stop that it caused */
-    if( job[ k ].rc && ( !rc || rc==FD_ED25519_HIP_SHLINK_FAIL_STOPPED ) ) rc = job[ k ].rc;
-    if( stats ) stats[ k ] = job[ k ].st;
+    int r = job[ k ].rc;
+    if( vsvc_code_is_device( r ) ) { if( !vsvc_code_is_device( rc ) ) rc = r; }
+    else if( r && !local_rc ) local_rc = r;
   }
+  if( !rc ) rc = local_rc;
+  if( stats ) for( unsigned k=0U; k<link_cnt; k++ ) stats[ k ] = job[ k ].st;
   free( job ); free( th );
   return rc;
+}
+
+int
+fd_ed25519_hip_vservice_run_links( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+                                   fd_ed25519_hip_shlink_t * const * in, fd_ed25519_hip_shlink_t * const * out,
+                                   unsigned link_cnt, fd_ed25519_hip_vservice_stats_t * stats ) {
+  return fd_ed25519_hip_vservice_serve( device, slot_cnt, batch_sigs, flags, in, out, link_cnt, stats, NULL );
 }
 
 /* ======================================================================

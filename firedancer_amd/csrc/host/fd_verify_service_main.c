@@ -6,45 +6,95 @@
    payloads to this process over two shared-memory links per tile and
    publishes the verdict frags that come back.  One service process serves
    every verify tile of one GPU, so the device's 4 GiB of base tables exist
-   once per GPU, not once per tile (fd_ed25519_hip_vservice_run_links).
+   once per GPU, not once per tile (fd_ed25519_hip_vservice_serve).
 
      fd_verify_hip_service --prefix NAME --tiles K [--gpu G] [--depth D]
                            [--slots S] [--batch B] [--gpu-parse] [--codes portable|avx512]
+                           [--tile-stale-ms T] [--gpu-hang-ms H] [--no-parent-watch]
 
    creates, for k in [0,K), the links NAME<k>_txn (tile -> service) and
    NAME<k>_vd (service -> tile), each of D lines (default 16384), prints
-   "ready K" on stdout once they exist, and serves them until every tile
-   has sent its end-of-stream frag (a validator's tiles never do).  Exit
-   status: 0 after a clean end; 1 on bad arguments or if a link cannot be
-   created (a stale one of the same name exists: a previous service was
-   killed; remove /dev/shm/NAME*); 2 when the service failed -- a GPU or
-   launch failure, or a tile broke the protocol -- after marking every link
-   failed, so each tile stops waiting (its heartbeat check) instead of
-   blocking.  The links are removed on every exit path.
+   "ready K" on stdout once they exist, and serves them until every link
+   has ended.  A link left behind by a service that was killed is reclaimed
+   (fd_ed25519_hip_shlink_create); one whose creator still runs is not.
+
+   Lifecycle (fd_topo_run's supervision, src/disco/topo/fd_topo_run.c:
+   50-100; fd_cnc's heartbeat, src/tango/cnc/fd_cnc.h:63-65,129-130):
+     - a tile whose txn-link heartbeat stops for T ms (default 5000) is
+       gone: its links end and its engines and device memory are freed;
+       once every tile has ended the service exits and unlinks the links;
+     - SIGTERM / SIGINT / SIGHUP end every link (marked STOPPED);
+     - the service exits the same way when the process that started it
+       dies (PR_SET_PDEATHSIG, and its parent pid watched), so a validator
+       that is gone never leaves an orphan holding HBM and shm links;
+     - a batch the GPU has not completed after H ms (default 30000) is a
+       hung GPU and ends every link.
+
+   Exit status: 0 every tile ended its stream (EOS); 1 bad arguments, or a
+   link name a live process already holds; 2 the device failed (GPU,
+   launch or allocation failure, hang) -- every link marked failed; 3 the
+   device was fine but not every link ended with EOS (tiles gone or broke
+   the protocol, or a signal / the parent's death stopped the service).
+   The links are removed on every exit path but a SIGKILL (which the next
+   service's create reclaims).
 
    Each link pair runs slot_cnt engines with one stream each: a process
-   gets GPU_MAX_HW_QUEUES hardware queues (4 by default), so a service for
-   several tiles should be started with that raised to about K x S (at most
-   the device's limit), as tools/ and tests/ do. */
+   gets GPU_MAX_HW_QUEUES hardware queues (4 by default); engines beyond
+   that share queues (their batches still overlap, they queue behind one
+   another on the shared queues). */
 #define _GNU_SOURCE
 #include "../../../include/fd_ed25519_hip_tile.h"
 
+#include <errno.h>
+#include <pthread.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/prctl.h>
+#include <time.h>
+#include <unistd.h>
+
+static volatile int g_stop;           /* read by every link thread (opts.stop) */
+static volatile int g_stop_signal;
+
+static void
+on_signal( int sig ) {
+  g_stop_signal = sig;
+  g_stop        = 1;
+}
+
+/* the parent's death: PR_SET_PDEATHSIG delivers SIGTERM when the thread
+   that started us exits; the pid watch covers a parent that died before
+   the prctl and a launcher thread that is not the parent process's last */
+static pid_t g_parent;
+
+static void *
+parent_watch( void * arg ) {
+  (void)arg;
+  struct timespec ts = { 0, 50L*1000L*1000L };
+  while( !g_stop ) {
+    if( getppid()!=g_parent ) { g_stop_signal = -1; g_stop = 1; break; }
+    nanosleep( &ts, NULL );
+  }
+  return NULL;
+}
 
 static void
 usage( char const * argv0 ) {
   fprintf( stderr, "usage: %s --prefix NAME --tiles K [--gpu G] [--depth D] [--slots S] [--batch B] "
-                   "[--gpu-parse] [--codes portable|avx512]\n", argv0 );
+                   "[--gpu-parse] [--codes portable|avx512] [--tile-stale-ms T] [--gpu-hang-ms H] "
+                   "[--no-parent-watch]\n", argv0 );
 }
 
 int
 main( int argc, char ** argv ) {
+  g_parent = getppid();
   char const *  prefix = NULL;
   unsigned      tiles  = 0U, slots = 3U;
-  int           gpu    = 0, flags = 0;
+  int           gpu    = 0, flags = 0, parent_watch_on = 1;
   unsigned long depth  = 16384UL, batch = 4096UL;
+  long          stale_ms = 0L, hang_ms = 0L;
   for( int i=1; i<argc; i++ ) {
     char const * a = argv[ i ];
     char const * v = i+1<argc ? argv[ i+1 ] : NULL;
@@ -54,6 +104,9 @@ main( int argc, char ** argv ) {
     else if( !strcmp( a, "--depth"  ) && v ) { depth = strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--slots"  ) && v ) { slots = (unsigned)strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--batch"  ) && v ) { batch = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--tile-stale-ms" ) && v ) { stale_ms = strtol( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--gpu-hang-ms" ) && v ) { hang_ms = strtol( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--no-parent-watch" ) ) { parent_watch_on = 0; }
     else if( !strcmp( a, "--gpu-parse" ) )   { flags |= FD_ED25519_HIP_VTILE_GPU_PARSE; }
     else if( !strcmp( a, "--codes" ) && v ) {
       if(      !strcmp( v, "portable" ) ) flags |= FD_ED25519_HIP_FLAG_CODES_PORTABLE;
@@ -63,6 +116,27 @@ main( int argc, char ** argv ) {
     else { usage( argv[0] ); return 1; }
   }
   if( !prefix || !tiles || tiles>FD_ED25519_HIP_VSERVICE_LINK_MAX || strlen( prefix )>96 ) { usage( argv[0] ); return 1; }
+  if( fd_ed25519_hip_abi_check( FD_ED25519_HIP_ABI_VERSION, sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
+                                sizeof(fd_ed25519_hip_vservice_stats_t) ) ) {
+    fprintf( stderr, "fd_verify_hip_service: %s\n", fd_ed25519_hip_last_error() );
+    return 1;
+  }
+
+  struct sigaction sa;
+  memset( &sa, 0, sizeof(sa) );
+  sa.sa_handler = on_signal;
+  sigemptyset( &sa.sa_mask );
+  sigaction( SIGTERM, &sa, NULL );
+  sigaction( SIGINT,  &sa, NULL );
+  sigaction( SIGHUP,  &sa, NULL );
+  signal( SIGPIPE, SIG_IGN );   /* a launcher that died with our stdout: still end cleanly */
+  pthread_t watcher;
+  int watching = 0;
+  if( parent_watch_on ) {
+    prctl( PR_SET_PDEATHSIG, SIGTERM );
+    if( getppid()!=g_parent ) { fprintf( stderr, "fd_verify_hip_service: the parent exited at start-up\n" ); return 3; }
+    watching = !pthread_create( &watcher, NULL, parent_watch, NULL );
+  }
 
   fd_ed25519_hip_shlink_t * in [ FD_ED25519_HIP_VSERVICE_LINK_MAX ];
   fd_ed25519_hip_shlink_t * out[ FD_ED25519_HIP_VSERVICE_LINK_MAX ];
@@ -72,41 +146,62 @@ main( int argc, char ** argv ) {
     char name[ 128 ];
     snprintf( name, sizeof(name), "%s%u_txn", prefix, k );
     in[ k ] = fd_ed25519_hip_shlink_create( name, depth );
+    int e = errno;
     snprintf( name, sizeof(name), "%s%u_vd", prefix, k );
-    out[ k ] = fd_ed25519_hip_shlink_create( name, depth );
+    if( in[ k ] ) { out[ k ] = fd_ed25519_hip_shlink_create( name, depth ); e = errno; }
     if( !in[ k ] || !out[ k ] ) {
-      fprintf( stderr, "fd_verify_hip_service: cannot create the links of tile %u (%s*: stale from a killed service?)\n",
-               k, prefix );
+      fprintf( stderr, "fd_verify_hip_service: cannot create the links of tile %u (%s*): %s\n", k, prefix,
+               e==EEXIST ? "a running process holds them" : strerror( e ) );
       rc = 1;
       break;
     }
   }
   if( !rc ) {
+    char const * q = getenv( "GPU_MAX_HW_QUEUES" );
+    unsigned long queues = q && *q ? strtoul( q, NULL, 0 ) : 4UL;
+    if( (unsigned long)tiles*slots>queues )
+      fprintf( stderr, "fd_verify_hip_service: note: %u tiles x %u slots = %u engine streams on %lu hardware queues "
+                       "(GPU_MAX_HW_QUEUES, at most 32): streams share queues\n", tiles, slots, tiles*slots, queues );
     printf( "ready %u\n", tiles );
     fflush( stdout );
     fd_ed25519_hip_vservice_stats_t st[ FD_ED25519_HIP_VSERVICE_LINK_MAX ];
     memset( st, 0, sizeof(st) );
-    int err = fd_ed25519_hip_vservice_run_links( gpu, slots, batch, flags, in, out, tiles, st );
-    /* one JSON line for tools and tests: per-tile device memory and the
-       base tables this one process holds for all of them */
+    fd_ed25519_hip_vservice_opts_t opts;
+    memset( &opts, 0, sizeof(opts) );
+    opts.stop          = &g_stop;
+    opts.tile_stale_ns = stale_ms>0L ? stale_ms*1000000L : stale_ms<0L ? -1L : 0L;
+    opts.gpu_hang_ns   = hang_ms>0L ? hang_ms*1000000L : 0L;
+    int err = fd_ed25519_hip_vservice_serve( gpu, slots, batch, flags, in, out, tiles, st, &opts );
+    /* one JSON line for tools and tests: per-tile device memory, how each
+       link ended, and the base tables this one process holds for all */
     unsigned long shared = 0UL;
     for( unsigned k=0U; k<tiles; k++ ) if( st[ k ].shared_device_bytes>shared ) shared = st[ k ].shared_device_bytes;
     printf( "{\"tiles\": %u, \"shared_device_bytes\": %lu, \"tile_device_bytes\": [", tiles, shared );
     for( unsigned k=0U; k<tiles; k++ ) printf( "%s%lu", k ? ", " : "", st[ k ].device_bytes );
     printf( "], \"txns\": [" );
     for( unsigned k=0U; k<tiles; k++ ) printf( "%s%lu", k ? ", " : "", st[ k ].txn_cnt );
-    printf( "], \"rc\": %d}\n", err );
+    printf( "], \"end_codes\": [" );
+    for( unsigned k=0U; k<tiles; k++ ) printf( "%s%d", k ? ", " : "", st[ k ].end_code );
+    printf( "], \"signal\": %d, \"rc\": %d}\n", g_stop_signal, err );
     fflush( stdout );
-    if( err ) {
+    int device = err && err!=FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL && err!=FD_ED25519_HIP_SHLINK_FAIL_STOPPED &&
+                 err!=FD_ED25519_HIP_SHLINK_FAIL_TILE_GONE;
+    if( device ) {
       fprintf( stderr, "fd_verify_hip_service: FAILED: %s (%d): %s; every link is marked failed\n",
                fd_ed25519_hip_strerror( err ), err, fd_ed25519_hip_last_error() );
       rc = 2;
     } else {
       for( unsigned k=0U; k<tiles; k++ )
-        fprintf( stderr, "fd_verify_hip_service: tile %u: %lu txns in %lu batches, %.3f s, %lu device bytes\n", k,
-                 st[ k ].txn_cnt, st[ k ].batches, st[ k ].seconds, st[ k ].device_bytes );
+        fprintf( stderr, "fd_verify_hip_service: tile %u: %lu txns in %lu batches, %.3f s, %lu device bytes, %s (%d)\n", k,
+                 st[ k ].txn_cnt, st[ k ].batches, st[ k ].seconds, st[ k ].device_bytes,
+                 !st[ k ].end_code ? "ended" : st[ k ].end_code==FD_ED25519_HIP_SHLINK_FAIL_TILE_GONE ? "tile gone" :
+                 st[ k ].end_code==FD_ED25519_HIP_SHLINK_FAIL_STOPPED ? "stopped" : "tile broke the protocol",
+                 st[ k ].end_code );
+      rc = err ? 3 : 0;
     }
   }
+  g_stop = 1;
+  if( watching ) pthread_join( watcher, NULL );
   for( unsigned k=0U; k<tiles; k++ ) {
     fd_ed25519_hip_shlink_leave( in [ k ], 1 );
     fd_ed25519_hip_shlink_leave( out[ k ], 1 );

@@ -42,7 +42,7 @@ if not os.path.exists(LIB_PATH):
     raise ImportError(f"libfd_ed25519_hip not built: {LIB_PATH} missing "
                       "(run `python -c 'import __graft_entry__ as g; g.build()'`); there is no CPU fallback")
 
-_lib = ctypes.CDLL(LIB_PATH)
+_lib = ctypes.CDLL(LIB_PATH, use_errno=True)   # errno: shlink create / join report why they failed
 
 _u8p = ctypes.c_void_p
 _lib.fd_ed25519_verify.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_void_p]
@@ -296,6 +296,14 @@ class DeviceBuffer:
         out = np.empty(count, dtype=dtype)
         assert offset_bytes + out.nbytes <= self.nbytes
         _check(_lib.fd_ed25519_hip_memcpy(self.engine._h, out.ctypes.data, self.ptr + offset_bytes, out.nbytes, 1))
+        return out
+
+    def download_into(self, out, offset_bytes=0):
+        """D2H straight into a caller's contiguous array (e.g. a slice of a
+        page-locked host window), no intermediate copy."""
+        assert out.flags["C_CONTIGUOUS"] and offset_bytes + out.nbytes <= self.nbytes
+        if out.nbytes:
+            _check(_lib.fd_ed25519_hip_memcpy(self.engine._h, out.ctypes.data, self.ptr + offset_bytes, out.nbytes, 1))
         return out
 
     def free(self):

@@ -521,13 +521,14 @@ def h2d_gbps(device=0, nbytes=256 << 20, reps=8):
 # ---- shlink + verify service (the GPU process behind a sandboxed tile) ----
 
 SHLINK_CTL_EOS = 1
-PRODUCER_BIN = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)),
-                                          "_lib", "fd_shlink_producer")
+PRODUCER_BIN = (__import__("os").environ.get("FD_SHLINK_PRODUCER") or   # the sanitizer run's build
+                __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)),
+                                           "_lib", "fd_shlink_producer"))
 
 
 class VServiceStats(ctypes.Structure):
     _fields_ = [("txn_cnt", ctypes.c_ulong), ("batches", ctypes.c_ulong), ("seconds", ctypes.c_double),
-                ("device_bytes", ctypes.c_ulong), ("shared_device_bytes", ctypes.c_ulong)]
+                ("device_bytes", ctypes.c_ulong), ("shared_device_bytes", ctypes.c_ulong), ("end_code", ctypes.c_int)]
 
 
 _lib.fd_ed25519_hip_shlink_create.argtypes = [ctypes.c_char_p, ctypes.c_ulong]
@@ -546,7 +547,7 @@ _lib.fd_ed25519_hip_vservice_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes
                                              ctypes.POINTER(VServiceStats)]
 # the library and these ctypes mirrors must describe the same ABI
 _lib.fd_ed25519_hip_abi_check.argtypes = [ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong]
-ABI_VERSION = 4   # FD_ED25519_HIP_ABI_VERSION
+ABI_VERSION = 5   # FD_ED25519_HIP_ABI_VERSION
 if _lib.fd_ed25519_hip_abi_check(ABI_VERSION, ctypes.sizeof(Slot), ctypes.sizeof(__import__(
         "firedancer_amd.ed25519", fromlist=["_Info"])._Info), ctypes.sizeof(VServiceStats)) != 0:
     raise ImportError("libfd_ed25519_hip ABI mismatch: " + _lib.fd_ed25519_hip_last_error().decode())
@@ -558,6 +559,21 @@ _lib.fd_ed25519_hip_shlink_status.argtypes = [_v]
 _lib.fd_ed25519_hip_shlink_status.restype = ctypes.c_int
 SHLINK_FAIL_PROTOCOL = -100
 SHLINK_FAIL_STOPPED = -101
+SHLINK_FAIL_TILE_GONE = -102
+SHLINK_PROTO = 5          # FD_ED25519_HIP_SHLINK_PROTO
+
+
+class ShLinkWatch(ctypes.Structure):
+    """fd_ed25519_hip_shlink_watch_t: a consumer's view of its producer's
+    heartbeat; check() -> 1 never ticked, 0 alive, -1 stale."""
+    _fields_ = [("last", ctypes.c_ulong), ("t_ns", ctypes.c_long), ("seen", ctypes.c_int)]
+
+    def check(self, link, now_ns, stale_ns):
+        return _lib.fd_ed25519_hip_shlink_watch(ctypes.byref(self), link._h, int(now_ns), int(stale_ns))
+
+
+_lib.fd_ed25519_hip_shlink_watch.argtypes = [ctypes.POINTER(ShLinkWatch), _v, ctypes.c_long, ctypes.c_long]
+_lib.fd_ed25519_hip_shlink_watch.restype = ctypes.c_int
 
 
 class ShLink:
@@ -569,7 +585,10 @@ class ShLink:
         h = (_lib.fd_ed25519_hip_shlink_create(name.encode(), int(depth)) if create
              else _lib.fd_ed25519_hip_shlink_join(name.encode()))
         if not h:
-            raise HipError(-1, f"shlink {'create' if create else 'join'} {name} failed")
+            import errno as _errno
+            e = ctypes.get_errno()
+            raise HipError(-1, f"shlink {'create' if create else 'join'} {name} failed "
+                               f"({_errno.errorcode.get(e, e)})")
         self._h, self._owner = h, create
         self._buf = ctypes.create_string_buffer(SHLINK_MTU)
 
@@ -629,6 +648,32 @@ def vservice_run(in_link, out_link, device=0, slot_cnt=3, batch_sigs=4096, gpu_p
     _check(_lib.fd_ed25519_hip_vservice_run(int(device), int(slot_cnt), int(batch_sigs), flags, in_link._h,
                                             out_link._h, ctypes.byref(st)))
     return {f: getattr(st, f) for f, _ in VServiceStats._fields_}
+
+
+class VServiceOpts(ctypes.Structure):
+    _fields_ = [("stop", ctypes.c_void_p), ("tile_stale_ns", ctypes.c_long), ("gpu_hang_ns", ctypes.c_long)]
+
+
+_lib.fd_ed25519_hip_vservice_serve.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, ctypes.c_int,
+                                               ctypes.POINTER(_v), ctypes.POINTER(_v), ctypes.c_uint,
+                                               ctypes.POINTER(VServiceStats), ctypes.POINTER(VServiceOpts)]
+
+
+def vservice_serve(in_links, out_links, device=0, slot_cnt=3, batch_sigs=4096, gpu_parse=True, codes="avx512",
+                   tile_stale_s=0.0, gpu_hang_s=0.0):
+    """Several link pairs on one device (fd_ed25519_hip_vservice_serve):
+    -> (status, [stats per pair]); status 0 when every pair ended with EOS,
+    else the device failure's code or the first link-local end."""
+    from .ed25519 import FLAG_CODES_PORTABLE
+    flags = (VTILE_GPU_PARSE if gpu_parse else 0) | (FLAG_CODES_PORTABLE if codes == "portable" else 0)
+    k = len(in_links)
+    ins = (_v * k)(*[l._h for l in in_links])
+    outs = (_v * k)(*[l._h for l in out_links])
+    st = (VServiceStats * k)()
+    opts = VServiceOpts(None, int(tile_stale_s * 1e9), int(gpu_hang_s * 1e9))
+    rc = _lib.fd_ed25519_hip_vservice_serve(int(device), int(slot_cnt), int(batch_sigs), flags, ins, outs, k, st,
+                                            ctypes.byref(opts))
+    return rc, [{f: getattr(x, f) for f, _ in VServiceStats._fields_} for x in st]
 
 
 def parse_producer_frags(blob):

@@ -164,6 +164,33 @@ def ops_per_verify(msg_sz):
     return dict(total=total, hash=hash_, scalar=np.zeros_like(total), decode=np.full_like(total, 2 * sqrt_), dsm=dsm)
 
 
+def box_cores(sysfs="/sys/devices/system/cpu"):
+    """The whole machine's CPUs from its topology in sysfs, not from this
+    process's cgroup or affinity: logical CPUs online, physical cores
+    (distinct package/core pairs) and sockets.  None where unreadable."""
+    import glob
+    import os
+    pairs, pkgs, logical = set(), set(), 0
+    for d in glob.glob(os.path.join(sysfs, "cpu[0-9]*")):
+        try:
+            if open(os.path.join(d, "online")).read().strip() == "0":
+                continue
+        except OSError:
+            pass   # cpu0 often has no "online" file: it is online
+        try:
+            pkg = int(open(os.path.join(d, "topology", "physical_package_id")).read())
+            core = int(open(os.path.join(d, "topology", "core_id")).read())
+        except (OSError, ValueError):
+            continue
+        logical += 1
+        pairs.add((pkg, core))
+        pkgs.add(pkg)
+    if not logical:
+        return {"logical_cpus": None, "physical_cores": None, "sockets": None, "source": sysfs}
+    return {"logical_cpus": logical, "physical_cores": len(pairs), "sockets": len(pkgs),
+            "source": f"{sysfs}/cpu*/topology (the machine, not the lease)"}
+
+
 def host_cores():
     """CPU cores this process may use: the cgroup CPU quota (cpu.max, v2; or
     cpu.cfs_quota_us / cfs_period_us, v1) when one is set, else the

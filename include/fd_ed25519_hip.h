@@ -96,13 +96,14 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    struct layout or a prototype changes (3: round 3 -- engine flags 64..256,
    vservice stats' device bytes, shlink liveness words; 4: a SUCCESS verdict
    frag carries the published frag's trailer only, the tile keeps the
-   payload).  A consumer checks
+   payload; 5: shlink protocol word and creator, vservice lifecycle and
+   end codes).  A consumer checks
    the library it loaded against the header it was built with:
    fd_ed25519_hip_abi_check( FD_ED25519_HIP_ABI_VERSION,
    sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
    sizeof(fd_ed25519_hip_vservice_stats_t) ) returns 0 when they agree,
    FD_ED25519_HIP_ERR_INVAL (with fd_ed25519_hip_last_error) when not. */
-#define FD_ED25519_HIP_ABI_VERSION (4U)
+#define FD_ED25519_HIP_ABI_VERSION (5U)
 
 unsigned
 fd_ed25519_hip_abi_version( void );
@@ -115,6 +116,7 @@ fd_ed25519_hip_abi_check( unsigned version, unsigned long slot_sz, unsigned long
 #define FD_ED25519_HIP_OK          (0)
 #define FD_ED25519_HIP_ERR_INVAL   (-22)   /* bad argument / misaligned device buffer */
 #define FD_ED25519_HIP_ERR_NOMEM   (-12)   /* host or device allocation failed        */
+#define FD_ED25519_HIP_ERR_TIMEOUT (-110)  /* the GPU did not complete a batch in time  */
 #define FD_ED25519_HIP_ERR_HIP     (-1000) /* HIP runtime error: -1000 - hipError_t    */
 
 #define FD_ED25519_HIP_FLAG_CODES_PORTABLE (1)  /* portable-backend error codes */

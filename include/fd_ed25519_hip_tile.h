@@ -335,11 +335,23 @@ fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_c
    `name` (e.g. "/fd_verify_in"): an mcache of depth (power of 2)
    fd_frag_meta_t-shaped lines and a dcache of 64-byte chunks for payloads
    of up to FD_ED25519_HIP_SHLINK_MTU bytes, with credit-based flow control.
-   create makes the object (it must not exist), join maps an existing one;
-   each process keeps its own cursor, so one handle per side.  After the
-   mapping, publish / consume are memory operations only (they may run
-   under seccomp strict mode). */
+   create makes the object, join maps an existing one; each process keeps
+   its own cursor, so one handle per side.  After the mapping, publish /
+   consume are memory operations only (they may run under seccomp strict
+   mode).
+
+   create fails (NULL, errno EEXIST) if a live process's link of that name
+   exists; a link left behind by a creator that has exited (a killed
+   service) is removed and made anew.  join fails with errno ENOENT (no
+   such link), EPROTO (a link of another frag protocol or layout: the two
+   sides were built from different revisions of this header) or EINVAL
+   (bad geometry). */
 typedef struct fd_ed25519_hip_shlink fd_ed25519_hip_shlink_t;
+
+/* The verdict frag protocol and link layout a link speaks, recorded in its
+   header by create and checked by join (1-4: earlier layouts without the
+   word; 5: trailer-only SUCCESS verdicts, below, and the creator's pid). */
+#define FD_ED25519_HIP_SHLINK_PROTO (5UL)
 
 /* the largest frag either direction carries (a verdict frag is smaller
    than this: 1 verdict byte + at most FD_ED25519_HIP_TXN_MAX_SZ + 2) */
@@ -432,6 +444,7 @@ fd_ed25519_hip_shlink_advance( fd_ed25519_hip_shlink_t * link );
    a nonzero status, stops waiting on the link. */
 #define FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL (-100)   /* the peer broke the frag protocol */
 #define FD_ED25519_HIP_SHLINK_FAIL_STOPPED  (-101)   /* the service was told to stop      */
+#define FD_ED25519_HIP_SHLINK_FAIL_TILE_GONE (-102)  /* the tile's heartbeat stopped: the service ended the link */
 
 void
 fd_ed25519_hip_shlink_heartbeat( fd_ed25519_hip_shlink_t * link, unsigned long now );
@@ -445,6 +458,20 @@ fd_ed25519_hip_shlink_fail( fd_ed25519_hip_shlink_t * link, int code );
 int
 fd_ed25519_hip_shlink_status( fd_ed25519_hip_shlink_t const * link );
 
+/* A consumer's view of its producer's heartbeat (zero-initialised):
+   watch returns 1 while the producer has never ticked (0), 0 while its
+   heartbeat changes, -1 once it has not changed for more than stale_ns
+   (<= 0: never stale); now_ns any monotonic clock. */
+typedef struct {
+  unsigned long last;
+  long          t_ns;
+  int           seen;
+} fd_ed25519_hip_shlink_watch_t;
+
+int
+fd_ed25519_hip_shlink_watch( fd_ed25519_hip_shlink_watch_t * w, fd_ed25519_hip_shlink_t const * link, long now_ns,
+                             long stale_ns );
+
 /* ctl bit of the last frag of a stream, both directions */
 #define FD_ED25519_HIP_SHLINK_CTL_EOS (1U)
 
@@ -454,6 +481,7 @@ typedef struct {
   double        seconds;        /* from the first frag consumed to the end of the stream */
   unsigned long device_bytes;   /* the link pair's own device memory (its vtile's) */
   unsigned long shared_device_bytes;   /* the process's base tables on the device, shared by every pair */
+  int           end_code;       /* how the link pair ended: 0 (EOS) or its failure code */
 } fd_ed25519_hip_vservice_stats_t;
 
 /* The GPU side of a sandboxed verify tile: consumes transaction payload
@@ -493,6 +521,46 @@ int
 fd_ed25519_hip_vservice_run_links( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
                                    fd_ed25519_hip_shlink_t * const * in, fd_ed25519_hip_shlink_t * const * out,
                                    unsigned link_cnt, fd_ed25519_hip_vservice_stats_t * stats );
+
+/* run_links with a lifecycle (fd_topo_run.c's supervision of tiles,
+   src/disco/topo/fd_topo_run.c:50-100, and fd_cnc's heartbeat,
+   src/tango/cnc/fd_cnc.h:63-65,129-130, on the service's side):
+
+     stop          while *stop is nonzero every link ends (marked
+                   FD_ED25519_HIP_SHLINK_FAIL_STOPPED): the caller's signal
+                   handler or parent watch sets it (NULL: never)
+     tile_stale_ns a link whose tile has ticked its txn-link heartbeat and
+                   then not changed it for this long is ended (both links
+                   marked FD_ED25519_HIP_SHLINK_FAIL_TILE_GONE, its engines
+                   and device memory freed) while the other links are served
+                   on (0: FD_ED25519_HIP_VSERVICE_TILE_STALE_NS, < 0: never)
+     gpu_hang_ns   a batch that has not completed after this long is a hung
+                   GPU: every link fails with FD_ED25519_HIP_ERR_TIMEOUT
+                   (0: FD_ED25519_HIP_VSERVICE_GPU_HANG_NS)
+
+   Failure domains: what a tile causes (its links marked failed by the
+   tile, an overrun, a stale heartbeat) ends that tile's link pair only; a
+   GPU, launch or allocation failure ends every link (the device is not
+   trusted for anyone).  While the service waits for the GPU it keeps
+   ticking its heartbeats and watching its links, so a slow GPU is never
+   mistaken for a dead service.  Returns FD_ED25519_HIP_OK when every link
+   ended with its tile's EOS, the device-wide failure's code if there was
+   one, else FD_ED25519_HIP_SHLINK_FAIL_TILE_GONE (or _PROTOCOL / _STOPPED:
+   the first link-local end); stats[k].end_code says how each link ended. */
+#define FD_ED25519_HIP_VSERVICE_TILE_STALE_NS (5L*1000L*1000L*1000L)
+#define FD_ED25519_HIP_VSERVICE_GPU_HANG_NS   (30L*1000L*1000L*1000L)
+
+typedef struct {
+  int volatile const * stop;
+  long                 tile_stale_ns;
+  long                 gpu_hang_ns;
+} fd_ed25519_hip_vservice_opts_t;
+
+int
+fd_ed25519_hip_vservice_serve( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+                               fd_ed25519_hip_shlink_t * const * in, fd_ed25519_hip_shlink_t * const * out,
+                               unsigned link_cnt, fd_ed25519_hip_vservice_stats_t * stats,
+                               fd_ed25519_hip_vservice_opts_t const * opts );
 
 /* ---- pool ------------------------------------------------------------- */
 

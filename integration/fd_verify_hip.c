@@ -68,6 +68,7 @@
 
 #include "fd_ed25519_hip_tile.h"
 
+#include <errno.h>
 #include <linux/unistd.h>
 
 #define FD_VERIFY_HIP_BURST    (16UL)
@@ -200,7 +201,7 @@ during_frag( void * _ctx,
     for( ulong spin=1UL;; spin++ ) {
       dst = fd_ed25519_hip_shlink_prepare( ctx->txl );
       if( FD_LIKELY( dst ) ) break;
-      if( !(spin & 1023UL) ) check_service( ctx );
+      if( !(spin & 1023UL) ) { fd_ed25519_hip_shlink_heartbeat( ctx->txl, ++ctx->beat ); check_service( ctx ); }
       FD_SPIN_PAUSE();
     }
   }
@@ -310,7 +311,9 @@ after_credit( void *             _ctx,
   while( n<FD_VERIFY_HIP_BURST && take_verdict( ctx, mux ) ) n++;
   for( ulong spin=1UL; ctx->sent - ctx->answered>=ctx->cap; spin++ ) {
     if( take_verdict( ctx, mux ) ) continue;
-    if( !(spin & 1023UL) ) check_service( ctx );
+    /* alive while it waits: the service ends the links of a tile whose
+       heartbeat stops (fd_ed25519_hip_vservice_serve) */
+    if( !(spin & 1023UL) ) { fd_ed25519_hip_shlink_heartbeat( ctx->txl, ++ctx->beat ); check_service( ctx ); }
     FD_SPIN_PAUSE();
   }
 }
@@ -334,14 +337,23 @@ privileged_init( fd_topo_t *      topo,
   fd_verify_hip_ctx_t * ctx = FD_SCRATCH_ALLOC_APPEND( l, alignof( fd_verify_hip_ctx_t ), sizeof( fd_verify_hip_ctx_t ) );
   fd_memset( ctx, 0, sizeof( fd_verify_hip_ctx_t ) );
 
-  /* map both links before the sandbox: afterwards they are memory only */
+  /* map both links before the sandbox: afterwards they are memory only.
+     The tile links the link code only (no HIP, so no
+     fd_ed25519_hip_abi_check): join itself refuses a link whose frag
+     protocol is not this build's (FD_ED25519_HIP_SHLINK_PROTO), so a tile
+     and a service of different revisions never exchange frags. */
   char name[ 128 ];
-  link_name( name, sizeof(name), topo, tile, "txn" );
-  ctx->txl = fd_ed25519_hip_shlink_join( name );
-  if( FD_UNLIKELY( !ctx->txl ) ) FD_LOG_ERR(( "cannot join %s: is fd_verify_hip_service running for this GPU?", name ));
-  link_name( name, sizeof(name), topo, tile, "vd" );
-  ctx->vdl = fd_ed25519_hip_shlink_join( name );
-  if( FD_UNLIKELY( !ctx->vdl ) ) FD_LOG_ERR(( "cannot join %s: is fd_verify_hip_service running for this GPU?", name ));
+  for( int k=0; k<2; k++ ) {
+    link_name( name, sizeof(name), topo, tile, k ? "vd" : "txn" );
+    fd_ed25519_hip_shlink_t * l = fd_ed25519_hip_shlink_join( name );
+    if( FD_UNLIKELY( !l ) ) {
+      if( errno==EPROTO )
+        FD_LOG_ERR(( "cannot join %s: the service speaks another frag protocol (this tile: %lu); rebuild both from one "
+                     "revision", name, (ulong)FD_ED25519_HIP_SHLINK_PROTO ));
+      FD_LOG_ERR(( "cannot join %s (%s): is fd_verify_hip_service running for this GPU?", name, fd_io_strerror( errno ) ));
+    }
+    if( k ) ctx->vdl = l; else ctx->txl = l;
+  }
   ctx->cap = fd_ulong_min( fd_ed25519_hip_shlink_depth( ctx->txl ), FD_VERIFY_HIP_RING );
 }
 

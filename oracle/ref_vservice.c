@@ -14,6 +14,17 @@
                   [--die-after N]    stop ticking and hang (SIGKILL-like) after N verdicts
                   [--fail-after N]   mark every link failed after N verdicts and exit 2
                   [--hold N]         answer in batches of N (verdicts held until N arrive or input idles)
+                  [--tile-stale-ms T] [--no-parent-watch]
+
+   The lifecycle is the GPU service's (fd_ed25519_hip_vservice_serve,
+   firedancer_amd/csrc/host/fd_verify_service_main.c), with the same link
+   code (create reclaims a killed service's links, the tile-heartbeat
+   watch): a link whose tile marks it failed or overruns it ends alone
+   (both links marked), a tile whose heartbeat stops for T ms (default
+   5000) is gone and its links end, SIGTERM / SIGINT / SIGHUP and the
+   death of the parent process end every link; once every link has ended
+   the links are removed and the exit status is 0 (every tile sent EOS) or
+   3 (some did not).
 
    Like the GPU service it keeps taking frags from the txn link whatever
    the state of the verdict link (the protocol's one rule for a service:
@@ -27,10 +38,13 @@
 #include "disco/quic/fd_tpu.h"
 #include "fd_ed25519_hip_tile.h"
 
+#include <errno.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/prctl.h>
+#include <time.h>
 #include <unistd.h>
 
 #define LINK_MAX (16UL)
@@ -42,6 +56,8 @@ typedef struct {
   uchar *                   tcache_mem;
   uchar                     sha_mem[ FD_TXN_ACTUAL_SIG_MAX ][ FD_SHA512_FOOTPRINT ] __attribute__((aligned(FD_SHA512_ALIGN)));
   int                       eos, eos_sent;
+  int                       end_code;   /* ended without EOS: the code both links carry */
+  fd_ed25519_hip_shlink_watch_t watch;  /* the tile's heartbeat on `in` */
   /* verdict frags not yet published: [q_head, q_cnt); a batch of them is
      released once `hold` are pending (--hold), input idles, or at the end */
   uchar *                   q;
@@ -50,13 +66,39 @@ typedef struct {
   ulong                     q_cnt, q_head, q_cap, q_rel;
 } svc_link_t;
 
+static volatile int g_stop;
+
+static void
+on_signal( int sig ) {
+  (void)sig;
+  g_stop = 1;
+}
+
+static long
+mono_ns( void ) {
+  struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return ts.tv_sec*1000000000L + ts.tv_nsec;
+}
+
+/* a link pair ends without EOS: both links carry the code */
+static void
+end_link( svc_link_t * S, int code ) {
+  S->end_code = code;
+  fd_ed25519_hip_shlink_fail( S->in, code );
+  fd_ed25519_hip_shlink_fail( S->out, code );
+}
+
 /* after_frag + fd_txn_verify of one payload into out (verdict byte, then
    for SUCCESS the published frag's trailer: its bytes after the payload and
    pad, the fd_txn_t and payload_sz -- the tile has the payload); returns
    the verdict frag's size */
 static ulong
 answer( svc_link_t * L, uchar const * payload, ulong payload_sz, uchar * out ) {
-  uchar * frag = out + 1;
+  /* the frag is built where the reference builds it, in an aligned room
+     (a dcache chunk: its fd_txn_t and u16 payload_sz stores are aligned),
+     then its trailer is copied behind the verdict byte */
+  static uchar room[ FD_TPU_DCACHE_MTU ] __attribute__((aligned(64)));
+  uchar * frag = room;
   if( payload_sz>FD_TPU_MTU ) { out[0] = (uchar)(schar)-3; return 1UL; }
   fd_memset( frag, 0, FD_TPU_DCACHE_MTU );
   fd_memcpy( frag, payload, payload_sz );
@@ -80,6 +122,9 @@ main( int argc, char ** argv ) {
   fd_log_private_boot( &argc, &argv );
   char const * prefix = NULL;
   ulong tiles = 0UL, depth = 16384UL, die_after = ~0UL, fail_after = ~0UL, hold = 1UL;
+  long stale_ms = 5000L;
+  int parent_watch = 1;
+  pid_t parent = getppid();
   for( int i=1; i<argc; i++ ) {
     char const * a = argv[i]; char const * v = i+1<argc ? argv[i+1] : NULL;
     if(      !strcmp( a, "--prefix"     ) && v ) { prefix = v; i++; }
@@ -88,9 +133,21 @@ main( int argc, char ** argv ) {
     else if( !strcmp( a, "--die-after"  ) && v ) { die_after = strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--fail-after" ) && v ) { fail_after = strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--hold"       ) && v ) { hold = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--tile-stale-ms" ) && v ) { stale_ms = strtol( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--no-parent-watch" ) ) parent_watch = 0;
     else FD_LOG_ERR(( "bad argument %s", a ));
   }
   FD_TEST( prefix && tiles>=1UL && tiles<=LINK_MAX && hold>=1UL );
+  struct sigaction sa;
+  memset( &sa, 0, sizeof(sa) );
+  sa.sa_handler = on_signal;
+  sigemptyset( &sa.sa_mask );
+  sigaction( SIGTERM, &sa, NULL ); sigaction( SIGINT, &sa, NULL ); sigaction( SIGHUP, &sa, NULL );
+  signal( SIGPIPE, SIG_IGN );   /* a launcher that died with our stdout: still end cleanly */
+  if( parent_watch ) {
+    prctl( PR_SET_PDEATHSIG, SIGTERM );
+    if( getppid()!=parent ) return 3;
+  }
 
   svc_link_t * L = (svc_link_t *)aligned_alloc( 128UL, LINK_MAX*sizeof(svc_link_t) );
   fd_memset( L, 0, LINK_MAX*sizeof(svc_link_t) );
@@ -101,7 +158,10 @@ main( int argc, char ** argv ) {
     L[k].in = fd_ed25519_hip_shlink_create( name, depth );
     snprintf( name, sizeof(name), "%s%lu_vd", prefix, k );
     L[k].out = fd_ed25519_hip_shlink_create( name, depth );
-    if( !L[k].in || !L[k].out ) FD_LOG_ERR(( "cannot create the links of tile %lu (%s*)", k, prefix ));
+    if( !L[k].in || !L[k].out ) {
+      FD_LOG_WARNING(( "cannot create the links of tile %lu (%s*): %s", k, prefix, errno==EEXIST ? "a running process holds them" : fd_io_strerror( errno ) ));
+      return 1;
+    }
     /* the reference tile's dedup state, as unprivileged_init builds it (fd_verify.c:161-179) */
     L[k].tcache_mem = aligned_alloc( FD_TCACHE_ALIGN, FD_TCACHE_FOOTPRINT( VERIFY_TCACHE_DEPTH, VERIFY_TCACHE_MAP_CNT ) );
     fd_tcache_t * tcache = fd_tcache_join( fd_tcache_new( L[k].tcache_mem, VERIFY_TCACHE_DEPTH, VERIFY_TCACHE_MAP_CNT ) );
@@ -125,11 +185,23 @@ main( int argc, char ** argv ) {
   for(;;) {
     ulong done = 0UL;
     int progress = 0;
+    int stop = g_stop || ( parent_watch && getppid()!=parent );
+    long now = mono_ns();
     for( ulong k=0UL; k<tiles; k++ ) {
       svc_link_t * S = &L[k];
+      if( S->eos_sent || S->end_code ) { done++; continue; }
       fd_ed25519_hip_shlink_heartbeat( S->out, beat );
-      if( fd_ed25519_hip_shlink_status( S->in ) ) FD_LOG_ERR(( "tile %lu marked its link failed", k ));
-      if( S->eos_sent ) { done++; continue; }
+      if( stop ) { end_link( S, FD_ED25519_HIP_SHLINK_FAIL_STOPPED ); done++; continue; }
+      int ts = fd_ed25519_hip_shlink_status( S->in );
+      if( !ts ) ts = fd_ed25519_hip_shlink_status( S->out );
+      if( ts ) {   /* the tile gave up on its link: that link ends, the others are served on */
+        FD_LOG_WARNING(( "tile %lu marked its link failed (%d): its links end", k, ts ));
+        end_link( S, ts ); done++; continue;
+      }
+      if( fd_ed25519_hip_shlink_watch( &S->watch, S->in, now, stale_ms>0L ? stale_ms*1000000L : -1L )<0 ) {
+        FD_LOG_WARNING(( "tile %lu heartbeat stale for %ld ms: its links end", k, stale_ms ));
+        end_link( S, FD_ED25519_HIP_SHLINK_FAIL_TILE_GONE ); done++; continue;
+      }
       /* release the held verdicts when `hold` are pending, at the end, or when input idles */
       if( S->q_cnt - S->q_rel>=hold || S->eos || idle>64UL ) S->q_rel = S->q_cnt;
       while( S->q_head<S->q_rel ) {
@@ -158,9 +230,9 @@ main( int argc, char ** argv ) {
         int r = fd_ed25519_hip_shlink_consume( S->in, buf, &sz, &sig, &ctl );
         if( r==1 ) break;
         if( r ) {
-          fd_ed25519_hip_shlink_fail( S->in, FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL );
-          fd_ed25519_hip_shlink_fail( S->out, FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL );
-          FD_LOG_ERR(( "tile %lu overran its txn link", k ));
+          FD_LOG_WARNING(( "tile %lu overran its txn link: its links end", k ));
+          end_link( S, FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL );
+          break;
         }
         if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { S->eos = 1; break; }
         if( S->q_cnt==S->q_cap ) {   /* grow the queue: never wait on the tile */
@@ -180,6 +252,14 @@ main( int argc, char ** argv ) {
     idle = progress ? 0UL : idle+1UL;
     if( done==tiles ) break;
   }
-  for( ulong k=0UL; k<tiles; k++ ) { fd_ed25519_hip_shlink_leave( L[k].in, 1 ); fd_ed25519_hip_shlink_leave( L[k].out, 1 ); }
-  return 0;
+  int clean = 1;
+  printf( "{\"tiles\": %lu, \"end_codes\": [", tiles );
+  for( ulong k=0UL; k<tiles; k++ ) {
+    printf( "%s%d", k ? ", " : "", L[k].end_code );
+    clean &= !L[k].end_code;
+    fd_ed25519_hip_shlink_leave( L[k].in, 1 ); fd_ed25519_hip_shlink_leave( L[k].out, 1 );
+  }
+  printf( "]}\n" );
+  fflush( stdout );
+  return clean ? 0 : 3;
 }

@@ -43,7 +43,9 @@ def driver(tmp_path_factory):
     d = tmp_path_factory.mktemp("fa")
     src, exe = d / "fa.c", d / "fa"
     src.write_text(DRIVER)
-    r = subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(REPO, "include"),
+    san = ([f"-fsanitize={os.environ['FD_TEST_SANITIZE']}", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"]
+           if os.environ.get("FD_TEST_SANITIZE") else [])   # tests/test_sanitizers.py
+    r = subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-Werror", *san, "-I", os.path.join(REPO, "include"),
                         str(src), "-o", str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     return str(exe)

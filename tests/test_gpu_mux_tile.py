@@ -110,31 +110,100 @@ def test_gpu_service_three_tiles_one_process(stream, reference_runs, tmp_path):
     assert all(0 < b < (1 << 30) for b in res["tile_device_bytes"]), res
 
 
-def test_gpu_service_stops_on_tile_failure(tmp_path):
-    """The service's failure policy, driven from the tile side: a tile that
-    marks its txn link failed stops the service, which marks every link
-    failed (the other tile's too) and exits with status 2 instead of
-    serving on."""
-    app = uuid.uuid4().hex[:10]
-    svc = start_service(app, 2)
+def _vram_used():
+    """Bytes of device 0's memory in use (rocm-smi), or None."""
     try:
-        txl = tile.ShLink(f"/fd_vhip_{app}_0_txn")
-        vdl = tile.ShLink(f"/fd_vhip_{app}_0_vd")
-        other = tile.ShLink(f"/fd_vhip_{app}_1_vd")
+        r = subprocess.run(["rocm-smi", "--showmeminfo", "vram", "--json"], capture_output=True, text=True, timeout=30)
+        d = json.loads(r.stdout)
+        card = d[sorted(d)[0]]
+        return int(card["VRAM Total Used Memory (B)"])
+    except Exception:
+        return None
+
+
+def test_gpu_service_tile_failure_ends_its_link_only(stream):
+    """Failure domains: tile 0 marks its txn link failed (as a tile does
+    when the service broke the frag protocol); the service ends that link
+    pair only and keeps serving tile 1, whose transactions still get their
+    verdicts; at the end it exits 3 with end codes [PROTOCOL, 0].  (A
+    device failure still ends every link: test_gpu_service_fault.py.)"""
+    _, frags = stream
+    app = uuid.uuid4().hex[:10]
+    svc = start_service(app, 2, "--batch", "256")
+    links = []
+    try:
+        txl0, vdl0 = tile.ShLink(f"/fd_vhip_{app}_0_txn"), tile.ShLink(f"/fd_vhip_{app}_0_vd")
+        txl1, vdl1 = tile.ShLink(f"/fd_vhip_{app}_1_txn"), tile.ShLink(f"/fd_vhip_{app}_1_vd")
+        links = [txl0, vdl0, txl1, vdl1]
         t0 = time.time()
-        while vdl.heartbeat_query() == 0 and time.time() - t0 < 60:   # the service's first tick
+        while vdl0.heartbeat_query() == 0 and time.time() - t0 < 60:   # the service's first tick
             time.sleep(0.01)
-        assert vdl.heartbeat_query() != 0
-        txl.fail(tile.SHLINK_FAIL_PROTOCOL)
+        txl0.fail(tile.SHLINK_FAIL_PROTOCOL)
+        t0 = time.time()
+        while vdl0.status() == 0 and time.time() - t0 < 30:
+            txl1.heartbeat(int(time.time() * 1e3))
+            time.sleep(0.01)
+        assert vdl0.status() == tile.SHLINK_FAIL_PROTOCOL
+        assert vdl1.status() == 0                        # the other tile's link is untouched
+        # tile 1 carries on: 200 transactions, then its end of stream
+        sent, verdicts, beat = 0, [], 0
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            beat += 1
+            txl1.heartbeat(beat)
+            if sent < 200 and txl1.publish(frags[sent], sent << 32):
+                sent += 1
+            elif sent == 200 and txl1.publish(b"", 0, tile.SHLINK_CTL_EOS):
+                sent += 1
+            f = vdl1.consume()
+            if f is not None:
+                if f[2] & tile.SHLINK_CTL_EOS:
+                    break
+                verdicts.append((f[1] >> 32, f[0][0]))
         rc, res, se = finish_service(svc)
-        status_vd, status_other = vdl.status(), other.status()
-        for link in (txl, vdl, other):
-            link.close(unlink=False)
     finally:
+        for link in links:
+            link.close(unlink=False)
         if svc.poll() is None:
             svc.kill()
         cleanup(app)
-    assert rc == 2, se[-2000:]
-    assert res["rc"] == tile.SHLINK_FAIL_PROTOCOL
-    assert status_vd == tile.SHLINK_FAIL_PROTOCOL
-    assert status_other != 0
+    assert [k for k, _ in verdicts] == list(range(200))
+    assert rc == 3, se[-2000:]
+    assert res["end_codes"] == [tile.SHLINK_FAIL_PROTOCOL, 0]
+    assert res["txns"][1] == 200
+
+
+def test_gpu_service_exits_and_frees_the_device_when_its_tile_dies(stream, tmp_path):
+    """The tile process is killed mid-stream: its heartbeat stops, the
+    service ends the link pair after --tile-stale-ms, and with no tile left
+    it exits (status 3) and removes its links; the device memory it held
+    (4 GiB of base tables plus the pipe) is free again."""
+    path, _ = stream
+    app = uuid.uuid4().hex[:10]
+    before = _vram_used()
+    svc = start_service(app, 1, "--batch", "256", "--tile-stale-ms", "500")
+    p = None
+    try:
+        p = run_harness("verify_hip", path, str(tmp_path / "hip.bin"), app=app, timeout=100, extra=("--rate", "2000"))
+        time.sleep(2.0)
+        during = _vram_used()
+        assert p.poll() is None
+        p.kill()
+        t0 = time.time()
+        rc, res, se = finish_service(svc)
+        dt = time.time() - t0
+        left = sorted(f for f in os.listdir("/dev/shm") if f.startswith(f"fd_vhip_{app}_"))
+        after = _vram_used()
+    finally:
+        if p is not None and p.poll() is None:
+            p.kill()
+        if svc.poll() is None:
+            svc.kill()
+        cleanup(app)
+    assert rc == 3, se[-2000:]
+    assert res["end_codes"] == [tile.SHLINK_FAIL_TILE_GONE]
+    assert left == []
+    assert dt < 15, dt
+    if before is not None and during is not None and after is not None:
+        assert during - before > (4 << 30)          # the service held its tables
+        assert after - before < (256 << 20), (before, during, after)

@@ -35,11 +35,16 @@ def test_service_marks_links_failed_on_launch_failure(tmp_path):
     tag = uuid.uuid4().hex[:12]
     txl = tile.ShLink(f"/fdf_tx_{tag}", 1024, create=True)
     vdl = tile.ShLink(f"/fdf_vd_{tag}", 1024, create=True)
+    # a second tile's link pair on the same service, idle: a device failure
+    # ends it too (the device is not trusted for anyone), marked STOPPED
+    tx2 = tile.ShLink(f"/fdf_tx2_{tag}", 1024, create=True)
+    vd2 = tile.ShLink(f"/fdf_vd2_{tag}", 1024, create=True)
     code = ("import sys; sys.path.insert(0, %r); from firedancer_amd import ed25519, tile; "
             "assert ed25519.LIB_PATH.endswith('libfd_ed25519_hip_faultinj.so'); "
-            "a = tile.ShLink(%r); b = tile.ShLink(%r); "
-            "print(tile.vservice_run(a, b, batch_sigs=256, slot_cnt=3, gpu_parse=False))"
-            % (REPO, txl.name, vdl.name))
+            "a, b = tile.ShLink(%r), tile.ShLink(%r); c, d = tile.ShLink(%r), tile.ShLink(%r); "
+            "rc, st = tile.vservice_serve([a, c], [b, d], batch_sigs=256, slot_cnt=3, gpu_parse=False); "
+            "print(rc, [s['end_code'] for s in st]); sys.exit(1 if rc else 0)"
+            % (REPO, txl.name, vdl.name, tx2.name, vd2.name))
     env = dict(os.environ, FD_ED25519_HIP_LIB=FAULT_LIB)
     t0 = time.time()
     svc = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)
@@ -50,19 +55,24 @@ def test_service_marks_links_failed_on_launch_failure(tmp_path):
         sout, serr = svc.communicate(timeout=60)
         dt = time.time() - t0
         status = (txl.status(), vdl.status())
+        status2 = (tx2.status(), vd2.status())
     finally:
         for p in (prod, svc):
             if p.poll() is None:
                 p.kill()
-        txl.close()
-        vdl.close()
+        for link in (txl, vdl, tx2, vd2):
+            link.close()
     if prod.returncode == 3:
         pytest.skip(f"seccomp strict mode unavailable: {perr.decode()}")
     # the service reports the injected failure (a HIP error code, never an abort)
     assert svc.returncode not in (0, -6), (svc.returncode, serr.decode()[-2000:])
     assert b"injected launch failure" in serr, serr.decode()[-2000:]
-    # both links carry the failure code the service marked
+    # both links carry the failure code the service marked, the other
+    # tile's links the stop it caused
     assert status[0] == status[1] and status[0] < 0, status
+    assert status2 == (tile.SHLINK_FAIL_STOPPED, tile.SHLINK_FAIL_STOPPED), status2
+    rc, ends = sout.decode().split(" ", 1)
+    assert int(rc) == status[0] and ends.strip() == f"[{status[0]}, {tile.SHLINK_FAIL_STOPPED}]", sout
     # the sandboxed tile side saw it and stopped with its defined status
     assert prod.returncode == 4, (prod.returncode, perr.decode())
     assert b"marked a link failed" in perr, perr.decode()

@@ -16,6 +16,12 @@ import pytest
 from firedancer_amd import tile
 
 
+# the sanitizer run (tests/test_sanitizers.py): the sanitizer runtime needs
+# system calls that seccomp strict mode forbids, so the producer runs
+# unsandboxed there (its code and checks are the same)
+NO_SANDBOX = ["--no-sandbox"] if os.environ.get("FD_TEST_SANITIZE") else []
+
+
 def fake_verdict(payload):
     return (len(payload) % 7) - 3
 
@@ -93,6 +99,8 @@ def test_sandboxed_producer_round_trip(tmp_path, sandbox, n, depth):
     txl = tile.ShLink(f"/fdt_tx_{tag}", depth, create=True)
     vdl = tile.ShLink(f"/fdt_vd_{tag}", depth, create=True)
     args = [tile.PRODUCER_BIN, txl.name, vdl.name, path] + ([] if sandbox else ["--no-sandbox"])
+    if NO_SANDBOX and sandbox:
+        args += NO_SANDBOX
     proc = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
     try:
         served = serve_fake(txl, vdl, proc)
@@ -128,7 +136,7 @@ def test_producer_stops_when_service_dies(tmp_path, how):
     tag = uuid.uuid4().hex[:12]
     txl = tile.ShLink(f"/fdt_tx_{tag}", 64, create=True)
     vdl = tile.ShLink(f"/fdt_vd_{tag}", 64, create=True)
-    proc = subprocess.Popen([tile.PRODUCER_BIN, txl.name, vdl.name, path, "--stale-ms", "300"],
+    proc = subprocess.Popen([tile.PRODUCER_BIN, txl.name, vdl.name, path, "--stale-ms", "300", *NO_SANDBOX],
                             stdout=subprocess.PIPE, stderr=subprocess.PIPE)
     try:
         if how == "killed":
@@ -261,3 +269,91 @@ def test_join_rejects_bad_geometry():
                 tile.ShLink(name)
         finally:
             a.close()
+
+
+# ---- versioning, restarts, the consumer's heartbeat watch (ABI 5) ----
+
+SHLINK_HDR_PROTO_OFF = 48     # shlink_hdr_t: magic, depth, chunk_cnt, mtu, heartbeat, status, proto, creator
+SHLINK_HDR_CREATOR_OFF = 56
+
+
+def _hdr_word(name, off, value=None):
+    import mmap
+    import struct
+    with open("/dev/shm" + name, "r+b") as f:
+        m = mmap.mmap(f.fileno(), 64)
+        old = struct.unpack_from("<Q", m, off)[0]
+        if value is not None:
+            struct.pack_into("<Q", m, off, value)
+        m.close()
+    return old
+
+
+def test_link_records_protocol_and_creator_and_join_refuses_another_protocol():
+    """create writes FD_ED25519_HIP_SHLINK_PROTO and its pid into the
+    header; a link of another protocol (a tile or service of another
+    revision) is refused at join with EPROTO instead of exchanging frags."""
+    name = f"/fdt_pr_{uuid.uuid4().hex[:12]}"
+    link = tile.ShLink(name, 64, create=True)
+    try:
+        assert _hdr_word(name, SHLINK_HDR_PROTO_OFF) == tile.SHLINK_PROTO
+        assert _hdr_word(name, SHLINK_HDR_CREATOR_OFF) == os.getpid()
+        peer = tile.ShLink(name)
+        peer.close()
+        _hdr_word(name, SHLINK_HDR_PROTO_OFF, tile.SHLINK_PROTO - 1)   # the verdict protocol of ABI 4
+        with pytest.raises(tile.HipError, match="EPROTO"):
+            tile.ShLink(name)
+    finally:
+        link.close()
+
+
+def test_create_reclaims_a_killed_creators_link_but_not_a_live_ones():
+    """A service killed with SIGKILL leaves its links in /dev/shm: the next
+    create of the same name reclaims them (its creator has exited); while
+    the creator lives, create still refuses (EEXIST)."""
+    import signal
+    import sys
+    name = f"/fdt_rc_{uuid.uuid4().hex[:12]}"
+    code = ("import sys, time; sys.path.insert(0, %r); from firedancer_amd import tile; "
+            "l = tile.ShLink(%r, 64, create=True); print('up', flush=True); time.sleep(60)"
+            % (os.path.dirname(os.path.dirname(os.path.abspath(tile.__file__))), name))
+    p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+    try:
+        assert p.stdout.readline().strip() == "up"
+        assert _hdr_word(name, SHLINK_HDR_CREATOR_OFF) == p.pid
+        with pytest.raises(tile.HipError, match="EEXIST"):
+            tile.ShLink(name, 64, create=True)          # its creator lives
+        p.send_signal(signal.SIGKILL)
+        p.wait(timeout=30)
+        assert os.path.exists("/dev/shm" + name)        # left behind
+        link = tile.ShLink(name, 128, create=True)      # reclaimed, made anew
+        assert link.depth == 128 and _hdr_word(name, SHLINK_HDR_CREATOR_OFF) == os.getpid()
+        link.close()
+        assert not os.path.exists("/dev/shm" + name)
+    finally:
+        if p.poll() is None:
+            p.kill()
+        if os.path.exists("/dev/shm" + name):
+            os.unlink("/dev/shm" + name)
+
+
+def test_heartbeat_watch():
+    """fd_ed25519_hip_shlink_watch: 1 until the producer first ticks, 0
+    while the heartbeat changes, -1 once it has been unchanged for longer
+    than the bound, 0 again when it moves; a bound <= 0 is never stale."""
+    name = f"/fdt_hb_{uuid.uuid4().hex[:12]}"
+    link = tile.ShLink(name, 64, create=True)
+    try:
+        w, ms = tile.ShLinkWatch(), 1000000
+        assert w.check(link, 0, 100 * ms) == 1
+        assert w.check(link, 10_000 * ms, 100 * ms) == 1       # never ticked: not stale, however long
+        link.heartbeat(1)
+        assert w.check(link, 10_001 * ms, 100 * ms) == 0
+        assert w.check(link, 10_100 * ms, 100 * ms) == 0       # at the bound
+        assert w.check(link, 10_102 * ms, 100 * ms) == -1      # past it
+        assert w.check(link, 10_102 * ms, -1) == 0             # no bound
+        link.heartbeat(2)
+        assert w.check(link, 10_103 * ms, 100 * ms) == 0
+        assert w.check(link, 10_150 * ms, 100 * ms) == 0
+    finally:
+        link.close()
