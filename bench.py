@@ -365,6 +365,113 @@ def latency_mode(eng, args, device):
     return out
 
 
+def latency_deployed(eng, args):
+    """C5 on the deployed path: the sandboxed verify
+    tile (integration/fd_verify_hip.c) under the reference's own tile
+    runtime -- fd_mux_tile, its mcache / dcache links and seccomp filter,
+    compiled from the reference's sources as the harness
+    oracle/_ref/mux/mux_harness -- with the product's GPU service process
+    (fd_verify_hip_service, 256-signature batches) behind its shared-memory
+    links.  A producer publishes GPU-signed single-signer transactions into
+    the quic -> verify link at a fixed offered load, each frag's tsorig its
+    due time; the dedup side takes (now - tsorig) for every verified frag
+    the tile publishes (src/disco/mux/fd_mux.c:548-559,
+    src/app/fdctl/run/tiles/fd_verify.c:152-153).  Peak = the same stream
+    unpaced; then 50 / 80 / 95% of it, five runs each, percentiles over all
+    five runs' frags pooled.  Beside it, the reference's own fd_tile_verify
+    (CPU verify, one tile) in the same harness at 50 / 80 / 95% of its own
+    peak: the CPU baseline of this leg.  The headline value is untouched:
+    this leg measures the host runtime the verification plugs into."""
+    import subprocess
+    import tempfile
+    import uuid
+    from firedancer_amd import tile, workload
+    mux = os.path.join(REPO, "oracle", "_ref", "mux", "mux_harness")
+    svc_bin = os.path.join(REPO, "firedancer_amd", "_lib", "fd_verify_hip_service")
+    if not (os.path.exists(mux) and os.path.exists(svc_bin)):
+        return {"error": "oracle/_ref/mux or the service binary not built"}
+    n, n_ref = args.deployed_txns, args.deployed_ref_txns
+    pay, _ = workload.txn_payloads(eng, n, args.seed + 91, msg_sz=200)
+    tmp = tempfile.mkdtemp(prefix="c5dep")
+    path, path_ref = os.path.join(tmp, "pay.bin"), os.path.join(tmp, "pay_ref.bin")
+    tile.write_payload_file(path, pay)
+    tile.write_payload_file(path_ref, pay[:n_ref])
+    svc_mode = ["--zero-copy"] if args.deployed_mode == "zero-copy" else (
+        ["--gpu-parse"] if args.deployed_mode == "gpu-parse" else [])
+
+    def run(kind, rate):
+        """one harness run -> (its JSON line, latencies in ms)"""
+        app = uuid.uuid4().hex[:10]
+        svc = None
+        if kind == "verify_hip":
+            svc = subprocess.Popen([svc_bin, "--prefix", f"/fd_vhip_{app}_", "--tiles", "1", "--batch",
+                                    str(args.latency_batch), "--slots", str(args.latency_slots), *svc_mode],
+                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+            line = svc.stdout.readline()
+            if not line.startswith("ready"):
+                raise RuntimeError(f"service did not start: {line!r} {svc.stderr.read()[-500:]}")
+        lat_path = os.path.join(tmp, f"lat_{app}.bin")
+        try:
+            p = subprocess.run([mux, kind, path if kind == "verify_hip" else path_ref, os.path.join(tmp, "out.bin"),
+                                "--app", app, "--depth", "16384", "--rate", str(rate), "--timeout", "100",
+                                "--log-path", "", "--lat-out", lat_path], capture_output=True, text=True, timeout=150)
+            if p.returncode != 0:
+                raise RuntimeError(f"harness {kind} rc {p.returncode}: {p.stderr[-500:]}")
+            if svc is not None and svc.wait(timeout=60) != 0:
+                raise RuntimeError(f"service rc {svc.returncode}: {svc.stderr.read()[-500:]}")
+        finally:
+            if svc is not None and svc.poll() is None:
+                svc.kill()
+            for f in os.listdir("/dev/shm"):
+                if f.startswith(f"fd_vhip_{app}_"):
+                    try:
+                        os.unlink(os.path.join("/dev/shm", f))
+                    except OSError:
+                        pass
+        res = json.loads(p.stdout.strip().splitlines()[-1])
+        lat = np.fromfile(lat_path, np.uint32).astype(np.float64) * 1e-6
+        os.unlink(lat_path)
+        return res, lat
+
+    def sweep(kind, runs, txns):
+        peak_res, _ = run(kind, 0)
+        peak = peak_res["txn_per_s"]
+        out = {"peak_txn_per_s": peak, "txns_per_run": txns, "loads": [], "published_all": peak_res["published"] == txns}
+        for frac in (0.5, 0.8, 0.95):
+            pooled, per_run = [], []
+            for _ in range(runs):
+                res, lat = run(kind, frac * peak)
+                pooled.append(lat)
+                per_run.append(res)
+                out["published_all"] &= res["published"] == txns
+            ms = np.concatenate(pooled)
+            out["loads"].append({"offered_frac_of_peak": frac, "offered_txn_per_s": frac * peak,
+                                 "achieved_txn_per_s": float(np.mean([r["txn_per_s"] for r in per_run])),
+                                 "p50_ms": float(np.percentile(ms, 50)), "p99_ms": float(np.percentile(ms, 99)),
+                                 "max_ms": float(ms.max()), "samples": int(ms.size),
+                                 "percentiles": f"pooled over {runs} runs",
+                                 "p99_ms_runs": [r["lat_p99_us"] * 1e-3 for r in per_run]})
+        return out
+    try:
+        hip = sweep("verify_hip", 5, n)
+        ref = sweep("verify", 2, n_ref)
+    finally:
+        for f in os.listdir(tmp):
+            os.unlink(os.path.join(tmp, f))
+        os.rmdir(tmp)
+    hip.update({"batch_sigs": args.latency_batch, "slots_in_flight": args.latency_slots,
+                "service_mode": args.deployed_mode, "msg_sz": 200,
+                "path": "producer -> quic_verify mcache/dcache (reference tango) -> fd_tile_verify_hip under the "
+                        "reference's fd_mux_tile, its seccomp filter installed -> shlink -> fd_verify_hip_service "
+                        "(GPU) -> shlink -> after_credit publish -> verify_dedup mcache -> consumer",
+                "latency": "due time (tsorig) -> verified frag received on the out link",
+                "runtime": "the tile runtime (fd_mux, tango, metrics) is the reference's, compiled from its sources "
+                           "as the harness oracle/_ref/mux/mux_harness; verification runs in the product's service"})
+    hip["cpu_baseline_reference_tile"] = dict(ref, tile="the reference's fd_tile_verify (fd_verify.c, CPU verify, "
+                                                        "AVX-512 build) in the same harness, one tile")
+    return hip
+
+
 def host_fed(wl, device, info, world, reps, batch, slots, copies):
     """The host-fed path: the C2 signatures from host memory (page-locked,
     as a deployment registers its dcache once) through the pool's feeder
@@ -702,6 +809,13 @@ def main():
     ap.add_argument("--latency-batch", type=int, default=256)
     ap.add_argument("--latency-slots", type=int, default=4)
     ap.add_argument("--latency-txns", type=int, default=100000, help="0 disables the latency mode")
+    ap.add_argument("--deployed-txns", type=int, default=300000,
+                    help="C5 on the deployed path (the tile under fd_mux_tile + the GPU service): txns per run, "
+                         "0 disables")
+    ap.add_argument("--deployed-ref-txns", type=int, default=40000,
+                    help="the reference tile's runs in the same harness (its CPU baseline)")
+    ap.add_argument("--deployed-mode", default="zero-copy", choices=["zero-copy", "gpu-parse", "host-parse"],
+                    help="the GPU service's mode for the deployed C5 leg")
     ap.add_argument("--host-reps", type=int, default=3, help="host-fed stream passes (0 disables)")
     ap.add_argument("--host-copies", type=int, default=4, help="host-fed stream: the set this many times")
     ap.add_argument("--host-batch", type=int, default=131072)
@@ -916,6 +1030,13 @@ def main():
         except Exception as ex:  # reported, never fatal for the device-resident number
             log(f"latency mode failed: {ex!r}")
             lat = {"error": repr(ex)}
+    lat_dep = None
+    if rank == 0 and world == 1 and args.deployed_txns > 0 and not strong:
+        try:
+            lat_dep = latency_deployed(eng, args)
+        except Exception as ex:  # reported, never fatal for the device-resident number
+            log(f"deployed latency leg failed: {ex!r}")
+            lat_dep = {"error": repr(ex)}
     traffic, traffic_src = pmc_traffic(min(n, info["max_chunk"]))
     # executed (not algorithmic) instruction rate of the dsm kernel: the
     # half-size formulation executes fewer operations than the reference's
@@ -978,6 +1099,7 @@ def main():
                                       "machine, projected from the measured per-core rate)",
             "host_fed": hf,
             "latency_mode": lat,
+            "latency_mode_deployed": lat_dep,
             "config_c1": c1,
             "config_c3": c3,
             "verdicts_match_reference_labels": mism_all == 0,

@@ -90,6 +90,8 @@ typedef struct {
   uint32_t const * msg_sz;   /* [N] message size                              */
   uint8_t const *  sigs;     /* [N][64] R||S, 16-byte aligned                  */
   uint8_t const *  pubs;     /* [N][32] A, 16-byte aligned                     */
+  uint8_t const *  digests;  /* [N][64] SHA-512(R||A||M) computed by the caller,
+                                16-byte aligned (msgs unused); NULL: hashed here */
   int8_t *         out;      /* [N] FD_ED25519_SUCCESS / ERR_* codes           */
   uint64_t         base;
   uint64_t         n;        /* chunk size, <= cap                             */

@@ -167,13 +167,25 @@ FD_DEV void hash_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
     S[0] = q2.x; S[1] = q2.y; S[2] = q2.z; S[3] = q2.w; S[4] = q3.x; S[5] = q3.y; S[6] = q3.z; S[7] = q3.w;
     a[0] = q4.x; a[1] = q4.y; a[2] = q4.z; a[3] = q4.w; a[4] = q5.x; a[5] = q5.y; a[6] = q5.z; a[7] = q5.w;
   }
-  const uintptr_t mp = reinterpret_cast<uintptr_t>(p.msgs + p.msg_off[i]);
-  sha_msg_src m;
-  m.base = reinterpret_cast<const uint32_t*>(mp & ~(uintptr_t)3);
-  m.shift = (uint32_t)(mp & 3);
-  m.sz = p.msg_sz[i];
   uint32_t dig[16], k[8];
-  sha512_ram(dig, r, a, m);
+  if (p.digests) {
+    /* the caller hashed R||A||M (a message the device path's 32-bit sizes
+       cannot carry, fd_ed25519_hip_verify_digests_dev): a uniform branch,
+       the whole launch takes one side */
+    const uint4* dg = reinterpret_cast<const uint4*>(p.digests + 64 * i);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint4 v = dg[q];
+      dig[4 * q] = v.x; dig[4 * q + 1] = v.y; dig[4 * q + 2] = v.z; dig[4 * q + 3] = v.w;
+    }
+  } else {
+    const uintptr_t mp = reinterpret_cast<uintptr_t>(p.msgs + p.msg_off[i]);
+    sha_msg_src m;
+    m.base = reinterpret_cast<const uint32_t*>(mp & ~(uintptr_t)3);
+    m.shift = (uint32_t)(mp & 3);
+    m.sz = p.msg_sz[i];
+    sha512_ram(dig, r, a, m);
+  }
   sc_reduce512(k, dig);
 #pragma unroll
   for (int w = 0; w < 8; w++) p.k[(uint64_t)w * p.cap + j] = k[w];

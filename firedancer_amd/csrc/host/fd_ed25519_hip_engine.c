@@ -558,7 +558,7 @@ verify_chunk( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p, int l
   p->base  = base;
   p->n     = cnt;
   p->small = p->n > e->quad_max ? 0 : (p->n <= e->oct_max ? 2 : 1);
-  p->perm  = p->small ? NULL : e->lane[l].d_perm;
+  p->perm  = ( p->small || p->digests ) ? NULL : e->lane[l].d_perm;   /* digests: no hash lengths to sort by */
   if( e->timing && e->tm_cnt<FD_ED25519_HIP_TIMING_MAX ) {
     /* events bracket each phase kernel on the stream it runs on */
     hipEvent_t * ev = e->tm_ev[ e->tm_cnt++ ];
@@ -601,24 +601,25 @@ verify_chunk( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p, int l
   return FD_ED25519_HIP_OK;
 }
 
-int
-fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
-                           unsigned long n,
-                           unsigned char const * msgs, unsigned long const * msg_off, unsigned int const * msg_sz,
-                           unsigned char const * sigs, unsigned char const * pubs, signed char * out,
-                           void * stream ) {
+/* verify_dev and verify_digests_dev: messages hashed on the device, or
+   the caller's digests of R||A||M (digests != NULL, msgs unused) */
+static int
+verify_common( fd_ed25519_hip_engine_t * e, unsigned long n,
+               unsigned char const * msgs, unsigned long const * msg_off, unsigned int const * msg_sz,
+               unsigned char const * digests, unsigned char const * sigs, unsigned char const * pubs,
+               signed char * out, void * stream ) {
   if( !e ) return FD_ED25519_HIP_ERR_INVAL;
   if( !n ) return FD_ED25519_HIP_OK;
-  if( !msg_off || !msg_sz || !sigs || !pubs || !out ) return FD_ED25519_HIP_ERR_INVAL;
-  if( ((uintptr_t)sigs & 15UL) || ((uintptr_t)pubs & 15UL) ) {
-    snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "sigs/pubs must be 16-byte aligned" );
+  if( ( !digests && ( !msg_off || !msg_sz ) ) || !sigs || !pubs || !out ) return FD_ED25519_HIP_ERR_INVAL;
+  if( ((uintptr_t)sigs & 15UL) || ((uintptr_t)pubs & 15UL) || ((uintptr_t)digests & 15UL) ) {
+    snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "sigs/pubs/digests must be 16-byte aligned" );
     return FD_ED25519_HIP_ERR_INVAL;
   }
   hipStream_t st = stream ? (hipStream_t)stream : e->stream;
   HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
   fd_ed25519_verify_params_t p;
   memset( &p, 0, sizeof(p) );
-  p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz;
+  p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz; p.digests = digests;
   p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
   p.cap = e->max_chunk;
   p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab_lo = e->btabw[0]; p.btab_hi = e->btabw[1];
@@ -656,6 +657,23 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
     }
   }
   return err;
+}
+
+int
+fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
+                           unsigned long n,
+                           unsigned char const * msgs, unsigned long const * msg_off, unsigned int const * msg_sz,
+                           unsigned char const * sigs, unsigned char const * pubs, signed char * out,
+                           void * stream ) {
+  return verify_common( e, n, msgs, msg_off, msg_sz, NULL, sigs, pubs, out, stream );
+}
+
+int
+fd_ed25519_hip_verify_digests_dev( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned char const * digests,
+                                   unsigned char const * sigs, unsigned char const * pubs, signed char * out,
+                                   void * stream ) {
+  if( !digests ) return FD_ED25519_HIP_ERR_INVAL;
+  return verify_common( e, n, NULL, NULL, NULL, digests, sigs, pubs, out, stream );
 }
 
 int
@@ -1011,15 +1029,32 @@ fd_ed25519_hip_verify_txns_host( fd_ed25519_hip_engine_t * e, unsigned long ntxn
 
 typedef struct dropin_req {
   unsigned char const * msg;
-  unsigned int          msg_sz;
+  unsigned long         msg_sz;
   unsigned char const * sigs;
   unsigned char const * pubs;
   unsigned int          cnt;      /* signatures, 1..16                     */
   int                   single;   /* fd_ed25519_verify: the signature's code */
+  int                   hashed;   /* dig holds SHA-512(R_j||A_j||M): the message stays on the host */
   int                   result;
   int                   done;
   struct dropin_req *   next;
+  unsigned char         dig[ 16 ][ 64 ];
 } dropin_req_t;
+
+/* Messages of at least this many bytes are hashed on the host by the
+   calling thread (fd_ed25519_hip_private_challenge) and verified from their
+   digests: the device path's message sizes are 32-bit, and the reference
+   takes any ulong size (src/ballet/ed25519/fd_ed25519.h:96-101).  A test
+   hook moves the limit down (fd_ed25519_hip_dropin_set_host_hash_min). */
+static unsigned long dropin_host_hash_min = 1UL<<32;
+
+void
+fd_ed25519_hip_dropin_set_host_hash_min( unsigned long bytes ) {
+  dropin_host_hash_min = bytes ? bytes : 1UL<<32;
+}
+
+void fd_ed25519_hip_private_challenge( unsigned char const sig[ 64 ], unsigned char const pub[ 32 ],
+                                       unsigned char const * msg, unsigned long msg_sz, unsigned char out[ 64 ] );
 
 static pthread_once_t  dropin_once = PTHREAD_ONCE_INIT;
 static pthread_mutex_t dropin_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -1073,16 +1108,23 @@ static int
 dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   fd_ed25519_hip_engine_t * e = dq.eng[k];
   HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
-  uint64_t nsig = 0UL, bytes = 0UL;
+  /* signatures of requests hashed on the host go after the others: the
+     device hashes [0, nsig_m), takes digests for [nsig_m, nsig) */
+  uint64_t nsig = 0UL, nsig_h = 0UL, bytes = 0UL;
   int multi = 0;
-  for( dropin_req_t * r=list; r; r=r->next ) { nsig += r->cnt; bytes += r->msg_sz; multi |= r->cnt>1U; }
+  for( dropin_req_t * r=list; r; r=r->next ) {
+    nsig += r->cnt; multi |= r->cnt>1U;
+    if( r->hashed ) nsig_h += r->cnt; else bytes += r->msg_sz;
+  }
+  uint64_t nsig_m = nsig - nsig_h;
   uint64_t o_off  = 0UL;
   uint64_t o_sz   = DROPIN_ALIGN16( o_off  + 8UL*nsig );
   uint64_t o_tf   = DROPIN_ALIGN16( o_sz   + 4UL*nsig );
   uint64_t o_tc   = DROPIN_ALIGN16( o_tf   + 4UL*n );
   uint64_t o_sig  = DROPIN_ALIGN16( o_tc   + 4UL*n );
   uint64_t o_pub  = DROPIN_ALIGN16( o_sig  + 64UL*nsig );
-  uint64_t o_msg  = DROPIN_ALIGN16( o_pub  + 32UL*nsig );
+  uint64_t o_dig  = DROPIN_ALIGN16( o_pub  + 32UL*nsig );
+  uint64_t o_msg  = DROPIN_ALIGN16( o_dig  + 64UL*nsig_h );
   uint64_t in_sz  = o_msg + bytes;
   uint64_t o_out  = DROPIN_ALIGN16( in_sz + 16UL );
   uint64_t o_tout = o_out + nsig;
@@ -1102,21 +1144,32 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   unsigned int *  sz  = (unsigned int  *)(h + o_sz);
   uint32_t *      tf  = (uint32_t      *)(h + o_tf);
   uint32_t *      tc  = (uint32_t      *)(h + o_tc);
-  uint64_t pos = 0UL, j = 0UL, t = 0UL;
+  uint64_t pos = 0UL, j = 0UL, jh = nsig_m, t = 0UL;
   for( dropin_req_t * r=list; r; r=r->next, t++ ) {
-    if( r->msg_sz ) memcpy( h + o_msg + pos, r->msg, r->msg_sz );
-    tf[t] = (uint32_t)j;
+    uint64_t s0 = r->hashed ? jh : j;
+    tf[t] = (uint32_t)s0;
     tc[t] = r->cnt;
-    memcpy( h + o_sig + 64UL*j, r->sigs, 64UL*r->cnt );
-    memcpy( h + o_pub + 32UL*j, r->pubs, 32UL*r->cnt );
-    for( uint32_t i=0U; i<r->cnt; i++, j++ ) { off[j] = pos; sz[j] = r->msg_sz; }
-    pos += r->msg_sz;
+    memcpy( h + o_sig + 64UL*s0, r->sigs, 64UL*r->cnt );
+    memcpy( h + o_pub + 32UL*s0, r->pubs, 32UL*r->cnt );
+    if( r->hashed ) {
+      memcpy( h + o_dig + 64UL*(s0 - nsig_m), r->dig, 64UL*r->cnt );
+      for( uint32_t i=0U; i<r->cnt; i++ ) { off[s0+i] = 0UL; sz[s0+i] = 0U; }
+      jh += r->cnt;
+    } else {
+      if( r->msg_sz ) memcpy( h + o_msg + pos, r->msg, r->msg_sz );
+      for( uint32_t i=0U; i<r->cnt; i++ ) { off[s0+i] = pos; sz[s0+i] = (unsigned int)r->msg_sz; }
+      pos += r->msg_sz;
+      j += r->cnt;
+    }
   }
   hipStream_t st = e->stream;
   HIPCHK( hipMemcpyAsync( d, h, in_sz ? in_sz : 1UL, hipMemcpyHostToDevice, st ), "H2D drop-in" );
-  int err = fd_ed25519_hip_verify_dev( e, nsig, d + o_msg, (unsigned long const *)(d + o_off),
+  int err = fd_ed25519_hip_verify_dev( e, nsig_m, d + o_msg, (unsigned long const *)(d + o_off),
                                        (unsigned int const *)(d + o_sz), d + o_sig, d + o_pub,
                                        (signed char *)(d + o_out), st );
+  if( !err && nsig_h )
+    err = fd_ed25519_hip_verify_digests_dev( e, nsig_h, d + o_dig, d + o_sig + 64UL*nsig_m, d + o_pub + 32UL*nsig_m,
+                                             (signed char *)(d + o_out + nsig_m), st );
   if( err ) { hipStreamSynchronize( st ); return err; }
   if( multi ) {
     err = fd_ed25519_hip_txn_combine_dev( e, n, (signed char const *)(d + o_out), (uint32_t const *)(d + o_tf),
@@ -1181,18 +1234,20 @@ fd_ed25519_hip_dropin_device_bytes( void ) {
   return b + fd_ed25519_hip_shared_device_bytes( dq.eng[0]->device );
 }
 
-/* The device path carries message sizes as 32-bit values.  The reference
-   takes any ulong size; a larger message must never be verified as its
-   truncated prefix (that would accept a signature over the prefix), so it
-   fails loudly like any other GPU failure. */
-static unsigned int
-dropin_msg_sz( unsigned long msg_sz ) {
-  if( msg_sz>(unsigned long)UINT32_MAX ) {
-    fprintf( stderr, "libfd_ed25519_hip: FATAL: message of %lu bytes exceeds the GPU path's %u-byte limit\n",
-             msg_sz, (unsigned)UINT32_MAX );
-    abort();
-  }
-  return (unsigned int)msg_sz;
+/* The device path carries message sizes as 32-bit values; the reference
+   takes any ulong size.  A message of dropin_host_hash_min bytes or more
+   (4 GiB: the first size the device cannot carry) is hashed here, in the
+   calling thread, with the library's own SHA-512 (one digest of R_j||A_j||M
+   per signature), before the request is queued; everything after the hash
+   -- the reduction mod L, decompression, the group equation, the batch
+   priority rule -- runs on the GPU as for any other request.  The message
+   is never truncated. */
+static void
+dropin_prepare( dropin_req_t * r ) {
+  r->hashed = r->msg_sz>=dropin_host_hash_min;
+  if( !r->hashed ) return;
+  for( unsigned int j=0U; j<r->cnt; j++ )
+    fd_ed25519_hip_private_challenge( r->sigs + 64UL*j, r->pubs + 32UL*j, r->msg, r->msg_sz, r->dig[ j ] );
 }
 
 int
@@ -1200,7 +1255,8 @@ fd_ed25519_verify( unsigned char const msg[], unsigned long msg_sz, unsigned cha
                    unsigned char const public_key[ 32 ], fd_sha512_t * sha ) {
   (void)sha;
   dropin_req_t r;
-  r.msg = msg; r.msg_sz = dropin_msg_sz( msg_sz ); r.sigs = sig; r.pubs = public_key; r.cnt = 1U; r.single = 1;
+  r.msg = msg; r.msg_sz = msg_sz; r.sigs = sig; r.pubs = public_key; r.cnt = 1U; r.single = 1;
+  dropin_prepare( &r );
   return dropin_submit( &r );
 }
 
@@ -1211,8 +1267,9 @@ fd_ed25519_verify_batch_single_msg( unsigned char const msg[], unsigned long con
   (void)shas;
   if( batch_sz==0 || batch_sz>16 ) return FD_ED25519_ERR_SIG;
   dropin_req_t r;
-  r.msg = msg; r.msg_sz = dropin_msg_sz( msg_sz ); r.sigs = signatures; r.pubs = pubkeys; r.cnt = batch_sz;
+  r.msg = msg; r.msg_sz = msg_sz; r.sigs = signatures; r.pubs = pubkeys; r.cnt = batch_sz;
   r.single = 0;
+  dropin_prepare( &r );
   return dropin_submit( &r );
 }
 

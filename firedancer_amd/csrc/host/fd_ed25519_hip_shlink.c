@@ -225,6 +225,18 @@ fd_ed25519_hip_shlink_depth( fd_ed25519_hip_shlink_t const * l ) {
   return l ? l->depth : 0UL;
 }
 
+unsigned char const *
+fd_ed25519_hip_shlink_dcache( fd_ed25519_hip_shlink_t const * l, unsigned long * sz ) {
+  if( sz ) *sz = l->chunk_cnt*SHLINK_CHUNK;
+  return l->dcache;
+}
+
+void *
+fd_ed25519_hip_shlink_mapping( fd_ed25519_hip_shlink_t const * l, unsigned long * sz ) {
+  if( sz ) *sz = l->map_sz;
+  return l->hdr;
+}
+
 /* The payload room of the next frag if the consumer has returned a credit
    for it, else NULL.  The room is MTU bytes inside this side's dcache; it
    is reused for a later frag only after depth+1 more frags, so it is never

@@ -107,6 +107,13 @@ typedef struct {
   unsigned int *            d_ssz;     /* raw mode: per-signature message size             */
   unsigned char *           d_pok;     /* raw mode: fd_txn_parse accepted                  */
   unsigned long             dev_bytes; /* the staging mirrors' device bytes                */
+  /* raw mode, zero-copy (the verify service): the payloads are DMA'd from
+     up to two spans of page-locked memory the caller owns (a shared txn
+     link's dcache) instead of the staging block, txn_sig_cnt filled by the
+     caller; reset at acquire */
+  unsigned char const *     ext_src[ 2 ];
+  unsigned long             ext_len[ 2 ];
+  int                       ext_counts;
 } pipe_slot_t;
 
 struct fd_ed25519_hip_pipe {
@@ -228,8 +235,14 @@ slot_h2d( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st, unsigne
 #ifndef FD_ED25519_HIP_AB_POOL_PARALLEL_H2D
   if( pipe->h2d_tail ) TCHK( hipStreamWaitEvent( st, pipe->h2d_tail, 0U ), "hipStreamWaitEvent(h2d)" );
 #endif
-  int err = slot_h2d_copies( s, st, sig_cnt, txn_cnt, msg_bytes );
+  int err = slot_h2d_copies( s, st, sig_cnt, txn_cnt, s->ext_src[0] ? 0UL : msg_bytes );
   if( err ) return err;
+  if( s->ext_src[0] ) {   /* zero-copy payloads: straight from the caller's page-locked spans */
+    TCHK( hipMemcpyAsync( s->d_msgs, s->ext_src[0], s->ext_len[0], hipMemcpyHostToDevice, st ), "H2D span 0" );
+    if( s->ext_len[1] )
+      TCHK( hipMemcpyAsync( s->d_msgs + s->ext_len[0], s->ext_src[1], s->ext_len[1], hipMemcpyHostToDevice, st ),
+            "H2D span 1" );
+  }
   TCHK( hipEventRecord( s->ev_h2d, st ), "hipEventRecord(h2d)" );
   pipe->h2d_tail = s->ev_h2d;
   return FD_ED25519_HIP_OK;
@@ -279,6 +292,7 @@ fd_ed25519_hip_pipe_acquire( fd_ed25519_hip_pipe_t * pipe ) {
   s->state = SLOT_FILL;
   pipe->next_acq++;
   s->pub.sig_cnt = 0UL; s->pub.msg_bytes = 0UL; s->pub.txn_cnt = 0UL;
+  s->ext_src[0] = s->ext_src[1] = NULL; s->ext_len[0] = s->ext_len[1] = 0UL; s->ext_counts = 0;
   return &s->pub;
 }
 
@@ -353,12 +367,14 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
   /* signature slots from byte 0 of each payload (its signature count if
      fd_txn_parse accepts it; 0 or > 16 reserve none) */
   unsigned long slots = 0UL;
+  if( s->ext_src[0] && payload_bytes!=s->ext_len[0] + s->ext_len[1] ) return FD_ED25519_HIP_ERR_INVAL;
   for( unsigned long t=0UL; t<txn_cnt; t++ ) {
     if( slot->msg_off[ t ]>payload_bytes || slot->msg_sz[ t ]>payload_bytes - slot->msg_off[ t ] ) {
       fd_ed25519_hip_private_set_error( "pipe_submit_txns: a payload lies outside the staged bytes" );
       return FD_ED25519_HIP_ERR_INVAL;
     }
-    unsigned int c = slot->msg_sz[ t ] ? slot->msgs[ slot->msg_off[ t ] ] : 0U;
+    /* the count from payload byte 0 (zero-copy: the caller read it) */
+    unsigned int c = s->ext_counts ? slot->txn_sig_cnt[ t ] : slot->msg_sz[ t ] ? slot->msgs[ slot->msg_off[ t ] ] : 0U;
     slot->txn_first  [ t ] = (unsigned int)slots;
     slot->txn_sig_cnt[ t ] = c;
     if( c>=1U && c<=16U ) slots += c;
@@ -595,6 +611,7 @@ fd_ed25519_hip_tcache_insert( fd_ed25519_hip_tcache_t * tc, unsigned long tag ) 
 typedef struct {
   unsigned long cookie;
   unsigned long tag;
+  unsigned char const * pay;  /* zero-copy: the payload in the caller's (shared) memory */
   unsigned long slot_seq;   /* submission seq of its batch (pending)  */
   unsigned long arena_off;  /* its frag in the output arena            */
   unsigned      arena_len;  /* bytes reserved there (0: none)          */
@@ -627,6 +644,15 @@ struct fd_ed25519_hip_vtile {
   int                    (* idle)( void * );
   void *                    idle_ctx;
   double                    hang_s;
+  /* zero-copy GPU-parse mode (the verify service, vt_frag_zc): payloads
+     stay in the caller's page-locked memory (the txn link's dcache, base /
+     size below) and the open batch DMAs them from there as up to two
+     spans (the dcache is a ring: one wrap per batch at most) */
+  int                       zero_copy;
+  unsigned char const *     zc_base;
+  unsigned long             zc_size;
+  unsigned long             zc_start[ 2 ], zc_end[ 2 ];   /* the open batch's spans, offsets in the dcache */
+  int                       zc_seg;                       /* spans in use: 0 (empty), 1 or 2 */
 };
 
 fd_ed25519_hip_vtile_t *
@@ -767,8 +793,10 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
     if( vt->gpu_parse && k+4UL<vt->q_cnt ) {
       vrec_t const * a = vq_at( vt, k+4UL );
       if( !a->resolved && a->slot_seq==s->seq && s->txn_sig_cnt[ a->txn_idx ]-1U<16U ) {
-        unsigned char const * pp = vt_payload( vt, s, a );
-        for( unsigned long l=0UL; l<448UL; l+=64UL ) __builtin_prefetch( pp + l, 0, 3 );
+        if( !vt->trailer_only ) {   /* the frag is built from the payload (a service sends the trailer only) */
+          unsigned char const * pp = vt_payload( vt, s, a );
+          for( unsigned long l=0UL; l<448UL; l+=64UL ) __builtin_prefetch( pp + l, 0, 3 );
+        }
         __builtin_prefetch( s->txn_trailer + 64UL*a->txn_idx, 0, 3 );
       }
     }
@@ -796,7 +824,7 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
         poff = s->msg_off[ k ] - mo;
         psz  = s->msg_sz [ k ] + mo;
       }
-      unsigned char const * pay = s->msgs + poff;
+      unsigned char const * pay = vt->zero_copy ? r->pay : s->msgs + poff;
       unsigned char const * tr  = s->txn_trailer + 64UL*ti;
       unsigned long foot = FD_ED25519_HIP_TXN_FOOTPRINT( (unsigned long)tr[18] | ((unsigned long)tr[19]<<8),
                                                          (unsigned long)tr[14] );
@@ -807,8 +835,14 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
       unsigned long fsz;
       if( vt->trailer_only ) {
         if( foot>64UL ) {
+          /* an fd_txn_t longer than the device's 64-byte trailer slot: parsed
+             here, from a private copy (zero-copy: the payload is in memory
+             another process shares) */
+          unsigned char priv[ FD_ED25519_HIP_TXN_MTU ];
           fd_ed25519_hip_txn_t t;
+          if( vt->zero_copy ) { memcpy( priv, pay, psz ); pay = priv; }
           foot = fd_txn_core_parse( pay, psz, &t, o, FD_ED25519_HIP_TXN_MAX_SZ );
+          if( !foot ) { r->verdict = (signed char)FD_ED25519_HIP_TXN_PARSE_FAILED; continue; }   /* changed under us */
         } else {
           memcpy( o, tr, foot );
         }
@@ -863,6 +897,15 @@ static int
 vt_submit_open( fd_ed25519_hip_vtile_t * vt ) {
   fd_ed25519_hip_slot_t * s = vt->open;
   if( !s || !s->txn_cnt ) return 0;
+  if( vt->zero_copy ) {
+    pipe_slot_t * ps = (pipe_slot_t *)s;
+    ps->ext_counts = 1;
+    for( int g=0; g<vt->zc_seg; g++ ) {
+      ps->ext_src[ g ] = vt->zc_base + vt->zc_start[ g ];
+      ps->ext_len[ g ] = vt->zc_end[ g ] - vt->zc_start[ g ];
+    }
+    vt->zc_seg = 0;
+  }
   int err = vt->gpu_parse ? fd_ed25519_hip_pipe_submit_txns( vt->pipe, s, s->txn_cnt, s->msg_bytes )
                           : fd_ed25519_hip_pipe_submit( vt->pipe, s, s->sig_cnt, s->msg_bytes, s->txn_cnt );
   if( err ) {   /* a launch failed: the batch's transactions have no verdicts, and the vtile stops */
@@ -952,6 +995,71 @@ vt_frag_raw( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigne
   r->txn_idx  = (unsigned)ti;
   if( s->sig_cnt>=s->sig_cap || s->txn_cnt>=s->txn_cap ) vt_submit_open( vt );
   return 1;
+}
+
+/* Zero-copy GPU-parse mode (the verify service): the payload is read in
+   place in the caller's page-locked memory [zc_base, zc_base+zc_size) --
+   byte 0 (the signature count, to reserve slots) and bytes 1..8 (the dedup
+   tag) only -- and DMA'd to the device with its batch's span at submit;
+   the device parses it (fd_txn_parse's acceptance) exactly as in GPU-parse
+   mode.  The bytes must stay in place until the frag's verdict is taken
+   (the verify tile's txn link guarantees it: a room is reused only after
+   its frag is answered, integration/fd_verify_hip.c).  Payloads must come
+   in the order they lie in the memory ring (a wrap to its start allowed);
+   a payload out of that order closes the batch. */
+static int
+vt_frag_zc( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned long payload_sz,
+            unsigned long cookie ) {
+  if( vt->err ) return vt->err;
+  if( !payload_sz || payload_sz>FD_ED25519_HIP_TXN_MTU ) {   /* fd_txn_parse rejects these before reading */
+    vrec_t * r = vq_push( vt );
+    if( !r ) return vt->err;
+    r->cookie = cookie; r->verdict = FD_ED25519_HIP_TXN_PARSE_FAILED; r->resolved = 1;
+    vt_advance( vt );
+    return 0;
+  }
+  unsigned long o = (unsigned long)( payload - vt->zc_base ), e = o + payload_sz;
+  if( payload<vt->zc_base || e>vt->zc_size ) { vt->err = FD_ED25519_HIP_ERR_INVAL; return vt->err; }
+  unsigned long c = payload[0], nsig = (c>=1UL && c<=16UL) ? c : 0UL;
+  for( int pass=0;; pass++ ) {
+    if( vt_open( vt ) ) return vt->err;
+    fd_ed25519_hip_slot_t * s = vt->open;
+    /* where this payload goes in the batch's spans */
+    int seg = -1;
+    unsigned long len0 = vt->zc_seg>=1 ? vt->zc_end[0] - vt->zc_start[0] : 0UL;
+    unsigned long len1 = vt->zc_seg>=2 ? vt->zc_end[1] - vt->zc_start[1] : 0UL;
+    if( !vt->zc_seg ) seg = 0;
+    else if( o>=vt->zc_end[ vt->zc_seg-1 ] && o - vt->zc_end[ vt->zc_seg-1 ]<64UL ) seg = vt->zc_seg-1;   /* the next room */
+    else if( vt->zc_seg==1 && e<=vt->zc_start[0] ) seg = 1;                                           /* the ring wrapped */
+    unsigned long grow = seg<0 ? 0UL : !vt->zc_seg ? payload_sz : seg==vt->zc_seg ? payload_sz :
+                         e - vt->zc_end[ seg ];
+    int fits = seg>=0 && ( !s->txn_cnt || ( s->sig_cnt+nsig<=s->sig_cap && s->txn_cnt+1UL<=s->txn_cap &&
+                                            len0+len1+grow<=s->msg_cap ) );
+    if( !fits ) {
+      if( pass || !s->txn_cnt ) { vt->err = FD_ED25519_HIP_ERR_INVAL; return vt->err; }
+      vt_submit_open( vt );   /* a full batch, or a payload out of ring order: a new batch */
+      continue;
+    }
+    unsigned long moff;
+    if( !vt->zc_seg ) { vt->zc_start[0] = o; vt->zc_end[0] = e; vt->zc_seg = 1; moff = 0UL; }
+    else if( seg==vt->zc_seg ) { vt->zc_start[1] = o; vt->zc_end[1] = e; vt->zc_seg = 2; moff = len0; }
+    else { moff = ( seg ? len0 + ( o - vt->zc_start[1] ) : o - vt->zc_start[0] ); vt->zc_end[ seg ] = e; }
+    unsigned long ti = s->txn_cnt++;
+    s->msg_off    [ ti ] = moff;
+    s->msg_sz     [ ti ] = (unsigned int)payload_sz;
+    s->txn_sig_cnt[ ti ] = (unsigned int)c;
+    s->msg_bytes = ( vt->zc_end[0] - vt->zc_start[0] ) + ( vt->zc_seg==2 ? vt->zc_end[1] - vt->zc_start[1] : 0UL );
+    s->sig_cnt  += nsig;
+    vrec_t * r = vq_push( vt );
+    if( !r ) return vt->err;
+    r->cookie = cookie;
+    if( payload_sz>=9UL ) memcpy( &r->tag, payload + 1, 8UL );
+    r->pay      = payload;
+    r->slot_seq = vt->open_seq;
+    r->txn_idx  = (unsigned)ti;
+    if( s->sig_cnt>=s->sig_cap || s->txn_cnt>=s->txn_cap ) vt_submit_open( vt );
+    return 1;
+  }
 }
 
 int
@@ -1381,6 +1489,36 @@ fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_c
   return err;
 }
 
+/* One dummy batch through every launch form a slot uses (a zero
+   signature through the verify kernels, and -- GPU parse -- a one-byte
+   payload through the device parser), on every slot: code objects load
+   and first launches happen here, not under the first transactions. */
+static int
+vt_warm( fd_ed25519_hip_vtile_t * vt ) {
+  fd_ed25519_hip_pipe_t * pipe = vt->pipe;
+  for( unsigned k=0U; k<pipe->slot_cnt; k++ ) {
+    fd_ed25519_hip_slot_t * s = fd_ed25519_hip_pipe_acquire( pipe );
+    if( !s ) return FD_ED25519_HIP_ERR_INVAL;
+    memset( s->sigs, 0, 64UL ); memset( s->pubs, 0, 32UL );
+    s->msg_off[0] = 0UL; s->msg_sz[0] = 0U; s->txn_first[0] = 0U; s->txn_sig_cnt[0] = 1U;
+    int err = fd_ed25519_hip_pipe_submit( pipe, s, 1UL, 0UL, 1UL );
+    if( err ) return err;
+    if( !fd_ed25519_hip_pipe_poll( pipe, 1 ) ) return pipe->err ? pipe->err : FD_ED25519_HIP_ERR_INVAL;
+    fd_ed25519_hip_pipe_release( pipe, s );
+    if( vt->gpu_parse ) {
+      s = fd_ed25519_hip_pipe_acquire( pipe );
+      if( !s ) return FD_ED25519_HIP_ERR_INVAL;
+      s->msgs[0] = 0; s->msg_off[0] = 0UL; s->msg_sz[0] = 1U;
+      err = fd_ed25519_hip_pipe_submit_txns( pipe, s, 1UL, 1UL );
+      if( err ) return err;
+      if( !fd_ed25519_hip_pipe_poll( pipe, 1 ) ) return pipe->err ? pipe->err : FD_ED25519_HIP_ERR_INVAL;
+      fd_ed25519_hip_pipe_release( pipe, s );
+    }
+  }
+  pipe->seq = 0UL;   /* the stream's batches count from 0 */
+  return FD_ED25519_HIP_OK;
+}
+
 /* ======================================================================
    vservice: the GPU process behind a sandboxed verify tile (shlink in,
    shlink out).
@@ -1465,7 +1603,7 @@ static int
 vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
                fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
                fd_ed25519_hip_vservice_stats_t * stats, _Atomic int * stop,
-               fd_ed25519_hip_vservice_opts_t const * opts ) {
+               fd_ed25519_hip_vservice_opts_t const * opts, _Atomic unsigned * ready ) {
   if( !in || !out ) return FD_ED25519_HIP_ERR_INVAL;
   vsvc_link_t L;
   memset( &L, 0, sizeof(L) );
@@ -1478,6 +1616,7 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
     fd_ed25519_hip_shlink_fail( in, FD_ED25519_HIP_ERR_INVAL ); fd_ed25519_hip_shlink_fail( out, FD_ED25519_HIP_ERR_INVAL );
     if( stop ) atomic_store_explicit( stop, 1, memory_order_release );
     if( stats ) stats->end_code = FD_ED25519_HIP_ERR_INVAL;
+    if( ready ) atomic_fetch_add_explicit( ready, 1U, memory_order_release );
     return FD_ED25519_HIP_ERR_INVAL;
   }
   vt->trailer_only = 1;   /* the tile keeps its payloads: verdict frags carry the trailers */
@@ -1488,7 +1627,26 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
   double t0 = now_s(), t_first = 0.0;   /* the stream's time runs from its first frag */
   unsigned long txns = 0UL;
   int eos = 0, rc = FD_ED25519_HIP_OK, local = 0;
+  void * reg = NULL;
   if( !buf ) { rc = FD_ED25519_HIP_ERR_NOMEM; goto fail; }
+  if( flags & FD_ED25519_HIP_VSERVICE_ZERO_COPY ) {
+    /* the txn link's mapping page-locked with the GPU: batches DMA their
+       payloads from the rooms the tile wrote */
+    unsigned long map_sz;
+    void * m = fd_ed25519_hip_shlink_mapping( in, &map_sz );
+    hipError_t he = hipHostRegister( m, map_sz, hipHostRegisterPortable );
+    if( he!=hipSuccess ) { rc = tile_fail( "hipHostRegister(txn link)", he ); goto fail; }
+    reg = m;
+    vt->zero_copy = 1;
+    vt->gpu_parse = 1;
+    vt->zc_base   = fd_ed25519_hip_shlink_dcache( in, &vt->zc_size );
+  }
+  {
+    int we = vt_warm( vt );
+    if( ready ) atomic_fetch_add_explicit( ready, 1U, memory_order_release );   /* ready (or failed): counted once */
+    ready = NULL;
+    if( we ) { rc = we; goto fail; }
+  }
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
   /* A/B build only: cycles per loop section (printed at the end) */
   unsigned long long pf_t[ 5 ] = { 0ULL, 0ULL, 0ULL, 0ULL, 0ULL }, pf_idle = 0ULL, pf_pass = 0ULL, pf_c = __rdtsc(), pf_n;
@@ -1528,7 +1686,26 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
     /* after_frag for every frag that is ready (copied out of the shared
        dcache first: the tile is not trusted not to change it meanwhile) */
     int pulled = 0;
-    while( !eos ) {
+    while( !eos && vt->zero_copy ) {   /* in place: the payload stays in the link's room */
+      unsigned long sz = 0UL, sig = 0UL;
+      unsigned int ctl = 0U;
+      int perr;
+      unsigned char const * src = fd_ed25519_hip_shlink_peek( in, &sz, &sig, &ctl, &perr );
+      if( !src ) {
+        if( perr==1 ) break;
+        rc = FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL; local = 1; goto fail;   /* overrun, or a line out of bounds */
+      }
+      if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { fd_ed25519_hip_shlink_advance( in ); eos = 1; break; }
+      if( !txns ) t_first = now_s();
+      int r = vt_frag_zc( vt, src, sz, sig );
+      if( r<0 ) { rc = r; local = rc==L.hook_rc ? L.hook_local : 0; goto fail; }
+      /* the credit goes back now: the room itself is reused only after its
+         verdict (the tile's bound on unanswered frags) */
+      if( fd_ed25519_hip_shlink_advance( in ) ) { rc = FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL; local = 1; goto fail; }
+      txns++;
+      pulled = 1;
+    }
+    while( !eos && !vt->zero_copy ) {
       unsigned long sz = 0UL, sig = 0UL;
       unsigned int ctl = 0U;
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
@@ -1582,6 +1759,7 @@ fail:
   fd_ed25519_hip_shlink_fail( in, rc );
   fd_ed25519_hip_shlink_fail( out, rc );
   if( stop && !local ) atomic_store_explicit( stop, 1, memory_order_release );
+  if( ready ) atomic_fetch_add_explicit( ready, 1U, memory_order_release );   /* failed before it was ready */
 done:
   if( stats ) {
     stats->txn_cnt      = txns;
@@ -1594,6 +1772,7 @@ done:
   free( buf );
   vt->idle = NULL;   /* the delete below may wait for batches in flight */
   fd_ed25519_hip_vtile_delete( vt );
+  if( reg ) hipHostUnregister( reg );   /* after the batches that read from it */
   return rc;
 }
 
@@ -1601,7 +1780,7 @@ int
 fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
                              fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
                              fd_ed25519_hip_vservice_stats_t * stats ) {
-  return vservice_loop( device, slot_cnt, batch_sigs, flags, in, out, stats, NULL, NULL );
+  return vservice_loop( device, slot_cnt, batch_sigs, flags, in, out, stats, NULL, NULL, NULL );
 }
 
 typedef struct {
@@ -1613,12 +1792,16 @@ typedef struct {
   fd_ed25519_hip_vservice_stats_t        st;
   _Atomic int *                          stop;
   fd_ed25519_hip_vservice_opts_t const * opts;
+  _Atomic unsigned *                     ready;    /* link threads that are ready to serve (or failed) */
+  char                                   errmsg[ 256 ];   /* the link thread's last_error (it is per thread) */
 } vservice_job_t;
 
 static void *
 vservice_main( void * arg ) {
   vservice_job_t * j = (vservice_job_t *)arg;
-  j->rc = vservice_loop( j->device, j->slot_cnt, j->batch_sigs, j->flags, j->in, j->out, &j->st, j->stop, j->opts );
+  j->rc = vservice_loop( j->device, j->slot_cnt, j->batch_sigs, j->flags, j->in, j->out, &j->st, j->stop, j->opts,
+                         j->ready );
+  if( j->rc ) snprintf( j->errmsg, sizeof(j->errmsg), "%s", fd_ed25519_hip_last_error() );
   return NULL;
 }
 
@@ -1640,12 +1823,13 @@ fd_ed25519_hip_vservice_serve( int device, unsigned slot_cnt, unsigned long batc
   pthread_t *      th  = (pthread_t *)calloc( link_cnt, sizeof(pthread_t) );
   if( !job || !th ) { free( job ); free( th ); return FD_ED25519_HIP_ERR_NOMEM; }
   _Atomic int stop = 0;
+  _Atomic unsigned ready = 0U;
   unsigned started = 0U;
   int rc = FD_ED25519_HIP_OK;
   for( unsigned k=0U; k<link_cnt; k++ ) {
     vservice_job_t * j = &job[ k ];
     j->device = device; j->flags = flags; j->slot_cnt = slot_cnt; j->batch_sigs = batch_sigs;
-    j->in = in[ k ]; j->out = out[ k ]; j->stop = &stop; j->opts = opts;
+    j->in = in[ k ]; j->out = out[ k ]; j->stop = &stop; j->opts = opts; j->ready = &ready;
     if( pthread_create( &th[ k ], NULL, vservice_main, j ) ) {
       rc = FD_ED25519_HIP_ERR_NOMEM;
       atomic_store_explicit( &stop, 1, memory_order_release );
@@ -1657,16 +1841,27 @@ fd_ed25519_hip_vservice_serve( int device, unsigned slot_cnt, unsigned long batc
     }
     started++;
   }
+  /* every link thread has built its engines and launched every kernel once */
+  if( started==link_cnt ) {
+    while( atomic_load_explicit( &ready, memory_order_acquire )<link_cnt ) {
+      struct timespec ts = { 0, 1000000L };
+      nanosleep( &ts, NULL );
+    }
+    if( opts && opts->ready ) opts->ready( opts->ready_ctx );
+  }
   /* the result: a device-wide failure's code first, else the first
      link-local end, else OK (every link ended with EOS) */
   int local_rc = FD_ED25519_HIP_OK;
+  int msg_k = -1;
   for( unsigned k=0U; k<started; k++ ) {
     pthread_join( th[ k ], NULL );
     int r = job[ k ].rc;
-    if( vsvc_code_is_device( r ) ) { if( !vsvc_code_is_device( rc ) ) rc = r; }
+    if( vsvc_code_is_device( r ) ) { if( !vsvc_code_is_device( rc ) ) { rc = r; msg_k = (int)k; } }
     else if( r && !local_rc ) local_rc = r;
   }
   if( !rc ) rc = local_rc;
+  /* the failing link thread's message, for the caller's fd_ed25519_hip_last_error */
+  if( msg_k>=0 && job[ msg_k ].errmsg[0] ) fd_ed25519_hip_private_set_error( job[ msg_k ].errmsg );
   if( stats ) for( unsigned k=0U; k<link_cnt; k++ ) stats[ k ] = job[ k ].st;
   free( job ); free( th );
   return rc;

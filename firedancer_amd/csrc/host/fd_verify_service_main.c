@@ -9,13 +9,14 @@
    once per GPU, not once per tile (fd_ed25519_hip_vservice_serve).
 
      fd_verify_hip_service --prefix NAME --tiles K [--gpu G] [--depth D]
-                           [--slots S] [--batch B] [--gpu-parse] [--codes portable|avx512]
+                           [--slots S] [--batch B] [--gpu-parse | --zero-copy] [--codes portable|avx512]
                            [--tile-stale-ms T] [--gpu-hang-ms H] [--no-parent-watch]
 
    creates, for k in [0,K), the links NAME<k>_txn (tile -> service) and
    NAME<k>_vd (service -> tile), each of D lines (default 16384), prints
-   "ready K" on stdout once they exist, and serves them until every link
-   has ended.  A link left behind by a service that was killed is reclaimed
+   "ready K" on stdout once they exist and every link pair can serve (its
+   engines and the base tables built, every kernel launched once), and
+   serves them until every link has ended.  A link left behind by a service that was killed is reclaimed
    (fd_ed25519_hip_shlink_create); one whose creator still runs is not.
 
    Lifecycle (fd_topo_run's supervision, src/disco/topo/fd_topo_run.c:
@@ -29,6 +30,12 @@
        that is gone never leaves an orphan holding HBM and shm links;
      - a batch the GPU has not completed after H ms (default 30000) is a
        hung GPU and ends every link.
+
+   --gpu-parse: the transactions are parsed on the GPU (the service copies
+   each payload out of the link into a batch); --zero-copy: the same, and
+   the payloads are DMA'd from the txn links' rooms as they lie (the links
+   page-locked with the GPU, FD_ED25519_HIP_VSERVICE_ZERO_COPY): the host
+   reads two bytes per transaction and copies none.
 
    Exit status: 0 every tile ended its stream (EOS); 1 bad arguments, or a
    link name a live process already holds; 2 the device failed (GPU,
@@ -80,10 +87,18 @@ parent_watch( void * arg ) {
   return NULL;
 }
 
+/* the service's "ready" line: once every link pair can serve (engines,
+   tables, kernels loaded), so a tile's first frags never wait on set-up */
+static void
+announce_ready( void * ctx ) {
+  printf( "ready %u\n", *(unsigned const *)ctx );
+  fflush( stdout );
+}
+
 static void
 usage( char const * argv0 ) {
   fprintf( stderr, "usage: %s --prefix NAME --tiles K [--gpu G] [--depth D] [--slots S] [--batch B] "
-                   "[--gpu-parse] [--codes portable|avx512] [--tile-stale-ms T] [--gpu-hang-ms H] "
+                   "[--gpu-parse | --zero-copy] [--codes portable|avx512] [--tile-stale-ms T] [--gpu-hang-ms H] "
                    "[--no-parent-watch]\n", argv0 );
 }
 
@@ -108,6 +123,7 @@ main( int argc, char ** argv ) {
     else if( !strcmp( a, "--gpu-hang-ms" ) && v ) { hang_ms = strtol( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--no-parent-watch" ) ) { parent_watch_on = 0; }
     else if( !strcmp( a, "--gpu-parse" ) )   { flags |= FD_ED25519_HIP_VTILE_GPU_PARSE; }
+    else if( !strcmp( a, "--zero-copy" ) )   { flags |= FD_ED25519_HIP_VTILE_GPU_PARSE | FD_ED25519_HIP_VSERVICE_ZERO_COPY; }
     else if( !strcmp( a, "--codes" ) && v ) {
       if(      !strcmp( v, "portable" ) ) flags |= FD_ED25519_HIP_FLAG_CODES_PORTABLE;
       else if( strcmp( v, "avx512" ) ) { usage( argv[0] ); return 1; }
@@ -162,8 +178,6 @@ main( int argc, char ** argv ) {
     if( (unsigned long)tiles*slots>queues )
       fprintf( stderr, "fd_verify_hip_service: note: %u tiles x %u slots = %u engine streams on %lu hardware queues "
                        "(GPU_MAX_HW_QUEUES, at most 32): streams share queues\n", tiles, slots, tiles*slots, queues );
-    printf( "ready %u\n", tiles );
-    fflush( stdout );
     fd_ed25519_hip_vservice_stats_t st[ FD_ED25519_HIP_VSERVICE_LINK_MAX ];
     memset( st, 0, sizeof(st) );
     fd_ed25519_hip_vservice_opts_t opts;
@@ -171,6 +185,8 @@ main( int argc, char ** argv ) {
     opts.stop          = &g_stop;
     opts.tile_stale_ns = stale_ms>0L ? stale_ms*1000000L : stale_ms<0L ? -1L : 0L;
     opts.gpu_hang_ns   = hang_ms>0L ? hang_ms*1000000L : 0L;
+    opts.ready         = announce_ready;
+    opts.ready_ctx     = &tiles;
     int err = fd_ed25519_hip_vservice_serve( gpu, slots, batch, flags, in, out, tiles, st, &opts );
     /* one JSON line for tools and tests: per-tile device memory, how each
        link ended, and the base tables this one process holds for all */

@@ -651,7 +651,8 @@ def vservice_run(in_link, out_link, device=0, slot_cnt=3, batch_sigs=4096, gpu_p
 
 
 class VServiceOpts(ctypes.Structure):
-    _fields_ = [("stop", ctypes.c_void_p), ("tile_stale_ns", ctypes.c_long), ("gpu_hang_ns", ctypes.c_long)]
+    _fields_ = [("stop", ctypes.c_void_p), ("tile_stale_ns", ctypes.c_long), ("gpu_hang_ns", ctypes.c_long),
+                ("ready", ctypes.c_void_p), ("ready_ctx", ctypes.c_void_p)]
 
 
 _lib.fd_ed25519_hip_vservice_serve.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, ctypes.c_int,

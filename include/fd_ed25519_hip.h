@@ -46,7 +46,9 @@ typedef struct fd_sha512_private fd_sha512_t;
    Synchronous; runs on the process-wide default engine (device from
    $FD_ED25519_HIP_DEVICE, default 0; codes from $FD_ED25519_HIP_CODES =
    "avx512" (default) | "portable").  A GPU failure aborts the process with a
-   message on stderr: this path never silently falls back to the CPU. */
+   message on stderr: this path never silently falls back to the CPU.  Any
+   msg_sz is accepted, as by the reference (4 GiB and more: the message is
+   hashed on the host, fd_ed25519_hip_dropin_set_host_hash_min). */
 int
 fd_ed25519_verify( unsigned char const   msg[],
                    unsigned long         msg_sz,
@@ -83,6 +85,15 @@ fd_ed25519_strerror( int err );
    creates them if no call has yet). */
 void
 fd_ed25519_hip_dropin_stats( unsigned long * launches, unsigned long * requests );
+
+/* A message of 4 GiB or more does not fit the device path's 32-bit message
+   sizes: the drop-ins hash it (R_j || A_j || M per signature) on the
+   calling thread with the library's SHA-512 and verify the rest on the GPU
+   from the digests (fd_ed25519_hip_verify_digests_dev); no message is ever
+   truncated or refused.  Test hook: messages of at least `bytes` bytes take
+   that path (0 restores 4 GiB). */
+void
+fd_ed25519_hip_dropin_set_host_hash_min( unsigned long bytes );
 
 unsigned long
 fd_ed25519_hip_dropin_device_bytes( void );
@@ -238,6 +249,26 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * engine,
                            unsigned char const *     pubs,
                            signed char *             out,
                            void *                    stream );
+
+/* The same verification from the caller's digests: signature i's
+   challenge k = SHA-512(R || A || M) mod L is reduced from digests[64 i ..
+   64 i + 64) (the SHA-512 of R || A || M, computed by the caller; 16-byte
+   aligned device memory), everything else as fd_ed25519_hip_verify_dev.
+   For messages the device path's 32-bit sizes cannot carry (the drop-ins
+   use it for messages of 4 GiB and more, hashing them on the host). */
+int
+fd_ed25519_hip_verify_digests_dev( fd_ed25519_hip_engine_t * engine,
+                                   unsigned long             n,
+                                   unsigned char const *     digests,
+                                   unsigned char const *     sigs,
+                                   unsigned char const *     pubs,
+                                   signed char *             out,
+                                   void *                    stream );
+
+/* SHA-512 on the host (FIPS 180-4; the library's own, used for the
+   drop-ins' large messages). */
+void
+fd_ed25519_hip_sha512( void const * data, unsigned long sz, unsigned char out[ 64 ] );
 
 /* Per-transaction combine on the device (fd_ed25519_verify_batch_single_msg
    priority), for transactions whose signatures were verified with

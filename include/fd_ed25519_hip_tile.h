@@ -396,6 +396,15 @@ fd_ed25519_hip_shlink_leave( fd_ed25519_hip_shlink_t * link, int unlink );
 unsigned long
 fd_ed25519_hip_shlink_depth( fd_ed25519_hip_shlink_t const * link );
 
+/* The link's dcache (payload rooms, *sz bytes) and its whole mapping (for
+   page-locking it with the GPU: the zero-copy service DMAs payloads from
+   the rooms, FD_ED25519_HIP_VSERVICE_ZERO_COPY). */
+unsigned char const *
+fd_ed25519_hip_shlink_dcache( fd_ed25519_hip_shlink_t const * link, unsigned long * sz );
+
+void *
+fd_ed25519_hip_shlink_mapping( fd_ed25519_hip_shlink_t const * link, unsigned long * sz );
+
 /* Producer: publishes one frag (payload of sz bytes, sig, ctl).  Returns
    0, 1 if the consumer has not returned a credit yet (retry), or an
    error status. */
@@ -517,6 +526,18 @@ fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_
    with the code and returns it (it never aborts the process). */
 #define FD_ED25519_HIP_VSERVICE_LINK_MAX (64U)
 
+/* Service flag (with the vtile flags): zero-copy GPU parse.  The service
+   does not copy payloads out of the txn link: its dcache is page-locked
+   with the GPU, the service reads only each frag's signature count and
+   dedup tag in place, and each batch's payloads are DMA'd from the link's
+   rooms as they lie (one or two spans) to the device, which parses them
+   (FD_ED25519_HIP_VTILE_GPU_PARSE's parser) and returns the fd_txn_t
+   trailers.  Safe because the tile reuses a room only after its frag is
+   answered (integration/fd_verify_hip.c), and the device parser takes any
+   bytes: a tile that rewrites its own payloads can only change its own
+   verdicts.  Same verdicts and frags as the other modes. */
+#define FD_ED25519_HIP_VSERVICE_ZERO_COPY (4)
+
 int
 fd_ed25519_hip_vservice_run_links( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
                                    fd_ed25519_hip_shlink_t * const * in, fd_ed25519_hip_shlink_t * const * out,
@@ -554,6 +575,12 @@ typedef struct {
   int volatile const * stop;
   long                 tile_stale_ns;
   long                 gpu_hang_ns;
+  /* called once, from the calling thread, when every link pair is ready
+     to serve (engines and base tables built, every kernel launched once
+     on a dummy batch): the service announces itself there, so no tile's
+     first frags wait for the device's set-up (NULL: none) */
+  void              (* ready)( void * ctx );
+  void *               ready_ctx;
 } fd_ed25519_hip_vservice_opts_t;
 
 int

@@ -24,7 +24,7 @@
 
      mux_harness verify|verify_hip PAYLOADS OUT [--app NAME] [--depth D]
                  [--rr-cnt N] [--rr-idx I] [--no-sandbox] [--rate TXN_PER_S]
-                 [--timeout S]
+                 [--timeout S] [--lat-out FILE]
 
    PAYLOADS: u64 n, n x u32 sizes, the payloads.  OUT: every published frag
    in order as u64 sig, u32 sz, sz bytes.  stdout: one JSON line of
@@ -33,7 +33,18 @@
    consumer has drained the out link, and the tile has halted on its cnc;
    the accelerated tile's txn link then carries the end-of-stream frag, so
    the GPU service exits.  A tile that stops (FD_LOG_ERR inside the
-   sandbox) ends the process; exit status 3 on the harness's own timeout. */
+   sandbox) ends the process; exit status 3 on the harness's own timeout.
+
+   Latency (SURVEY.md §8(d) C5 on the deployed path): each frag's tsorig
+   is its due time -- the producer's start plus seq / rate, or its publish
+   time when unpaced -- so a producer held back by credits does not hide
+   the wait (no coordinated omission).  Both tiles publish the frag's
+   tsorig with the verified frag (fd_verify.c:152-153; the accelerated tile
+   echoes it through the service), and the consumer, the dedup tile's
+   side, takes now - fd_frag_meta_ts_decomp( tsorig ) for every frag it
+   receives: due time -> verified frag on the out link.  The JSON line
+   carries p50 / p99 / max in microseconds; --lat-out writes every sample
+   (u32 nanoseconds, in publish order). */
 
 #define _GNU_SOURCE
 #include "disco/tiles.h"
@@ -106,6 +117,8 @@ typedef struct {
   /* consumer output */
   uchar *          res;
   ulong            res_used, res_cap;
+  uint *           lat_ns;       /* per published frag: now - tsorig */
+  double           tick_per_ns;
   volatile ulong   res_cnt;
   volatile ulong   out_seq;      /* next out seq the consumer expects */
   volatile int     producer_done;
@@ -120,14 +133,22 @@ producer_main( void * arg ) {
   ulong wmark  = fd_dcache_compact_wmark ( g_mem, h->in_dcache, FD_TPU_MTU );
   ulong chunk  = chunk0;
   double t0 = now_s();
+  long   k0 = fd_tickcount();
+  double tick_per_s = h->tick_per_ns*1e9;
   for( ulong seq=0UL; seq<h->n && !h->stop; seq++ ) {
-    if( h->rate>0.0 ) while( now_s() < t0 + (double)seq/h->rate ) FD_SPIN_PAUSE();
+    long due = 0L;
+    if( h->rate>0.0 ) {
+      while( now_s() < t0 + (double)seq/h->rate ) FD_SPIN_PAUSE();
+      due = k0 + (long)( (double)seq/h->rate*tick_per_s );
+    }
     /* credits: never more than depth frags ahead of the tile's fseq */
     while( fd_seq_diff( seq, fd_fseq_query( h->in_fseq ) )>=(long)h->in_depth ) { if( h->stop ) return NULL; FD_SPIN_PAUSE(); }
     ulong sz = h->sz[ seq ];
     fd_memcpy( fd_chunk_to_laddr( g_mem, chunk ), h->pay + h->off[ seq ], sz );
-    ulong ts = (ulong)fd_frag_meta_ts_comp( fd_tickcount() );
-    fd_mcache_publish( h->in_mcache, h->in_depth, seq, seq, chunk, sz, fd_frag_meta_ctl( 0UL, 1, 1, 0 ), ts, ts );
+    long  now   = fd_tickcount();
+    ulong ts    = (ulong)fd_frag_meta_ts_comp( now );
+    ulong tsorig = h->rate>0.0 ? (ulong)fd_frag_meta_ts_comp( due ) : ts;   /* the frag's due time */
+    fd_mcache_publish( h->in_mcache, h->in_depth, seq, seq, chunk, sz, fd_frag_meta_ctl( 0UL, 1, 1, 0 ), tsorig, ts );
     chunk = fd_dcache_compact_next( chunk, sz, chunk0, wmark );
   }
   h->producer_done = 1;
@@ -146,7 +167,7 @@ consumer_main( void * arg ) {
     if( d<0L ) { FD_SPIN_PAUSE(); continue; }
     if( d>0L ) { h->consumer_err = 1; return NULL; }       /* overrun: the tile ignored our credits */
     FD_COMPILER_MFENCE();
-    ulong sig = m->sig, chunk = m->chunk, sz = m->sz;
+    ulong sig = m->sig, chunk = m->chunk, sz = m->sz, tsorig = m->tsorig;
     FD_COMPILER_MFENCE();
     if( sz>FD_TPU_DCACHE_MTU || h->res_used + 12UL + sz>h->res_cap ) { h->consumer_err = 2; return NULL; }
     uchar * r = h->res + h->res_used;
@@ -155,6 +176,9 @@ consumer_main( void * arg ) {
     FD_COMPILER_MFENCE();
     if( FD_VOLATILE_CONST( m->seq )!=s0 ) { h->consumer_err = 3; return NULL; }
     h->res_used += 12UL + sz;
+    long lat = fd_tickcount() - fd_frag_meta_ts_decomp( tsorig, fd_tickcount() );
+    double ns = (double)lat / h->tick_per_ns;
+    h->lat_ns[ h->res_cnt ] = ns<0.0 ? 0U : ns>4e9 ? 4000000000U : (uint)ns;
     h->res_cnt++;
     seq++;
     h->out_seq = seq;
@@ -208,13 +232,21 @@ tile_main( void * arg ) {
   return NULL;
 }
 
-static void
+static double
 calibrate_ticks( void ) {
   /* fd_tempo_tick_per_ns, measured before the sandbox (it sleeps) */
   long t0 = fd_log_wallclock(); long k0 = fd_tickcount();
   struct timespec ts = { 0, 50L*1000L*1000L }; nanosleep( &ts, NULL );
   long t1 = fd_log_wallclock(); long k1 = fd_tickcount();
-  fd_tempo_set_tick_per_ns( (double)(k1-k0)/(double)(t1-t0), 0.0 );
+  double tpn = (double)(k1-k0)/(double)(t1-t0);
+  fd_tempo_set_tick_per_ns( tpn, 0.0 );
+  return tpn;
+}
+
+static int
+cmp_uint( void const * a, void const * b ) {
+  uint x = *(uint const *)a, y = *(uint const *)b;
+  return x<y ? -1 : x>y;
 }
 
 int
@@ -228,6 +260,7 @@ main( int argc, char ** argv ) {
   else if( !strcmp( kind, "verify_hip" ) ) h->run = &fd_tile_verify_hip;
   else FD_LOG_ERR(( "unknown tile %s", kind ));
   char const * app = "harness";
+  char const * lat_out = NULL;
   ulong depth = 4096UL, rr_cnt = 1UL, rr_idx = 0UL;
   double timeout = 120.0;
   h->sandbox = 1;
@@ -240,6 +273,7 @@ main( int argc, char ** argv ) {
     else if( !strcmp( a, "--rate"    ) && v ) { h->rate = strtod( v, NULL ); i++; }
     else if( !strcmp( a, "--timeout" ) && v ) { timeout = strtod( v, NULL ); i++; }
     else if( !strcmp( a, "--no-sandbox" ) ) h->sandbox = 0;
+    else if( !strcmp( a, "--lat-out" ) && v ) { lat_out = v; i++; }
     else FD_LOG_ERR(( "bad argument %s", a ));
   }
   FD_TEST( rr_cnt>=1UL && rr_idx<rr_cnt && rr_cnt<=16UL && fd_ulong_is_pow2( depth ) );
@@ -258,7 +292,7 @@ main( int argc, char ** argv ) {
   fclose( f );
   h->pay = pay; h->off = off; h->sz = sz;
 
-  calibrate_ticks();
+  h->tick_per_ns = calibrate_ticks();
 
   /* the workspace region and the objects in it */
   ulong out_depth = depth;
@@ -318,6 +352,9 @@ main( int argc, char ** argv ) {
 
   h->res_cap = 64UL + h->n*(12UL + FD_TPU_DCACHE_MTU);
   h->res     = (uchar *)malloc( h->res_cap );
+  h->lat_ns  = (uint *)malloc( 4UL*(h->n+1UL) );
+  FD_TEST( h->res && h->lat_ns );
+  fd_memset( h->lat_ns, 0, 4UL*(h->n+1UL) );   /* touched before the stream (no first-touch faults inside it) */
 
   /* privileged_init (maps the accelerated tile's links), then the threads */
   if( h->run->privileged_init ) h->run->privileged_init( topo, h->tile, h->scratch );
@@ -368,9 +405,20 @@ main( int argc, char ** argv ) {
   FILE * o = fopen( argv[3], "wb" );
   FD_TEST( o && fwrite( h->res, 1UL, h->res_used, o )==h->res_used );
   fclose( o );
+  ulong nl = h->res_cnt;
+  if( lat_out ) {
+    FILE * lo = fopen( lat_out, "wb" );
+    FD_TEST( lo && fwrite( h->lat_ns, 4UL, nl, lo )==nl );
+    fclose( lo );
+  }
+  qsort( h->lat_ns, nl, 4UL, cmp_uint );
+  double p50 = nl ? 1e-3*(double)h->lat_ns[ (nl-1UL)/2UL ] : 0.0;
+  double p99 = nl ? 1e-3*(double)h->lat_ns[ (ulong)((double)(nl-1UL)*0.99) ] : 0.0;
+  double pmx = nl ? 1e-3*(double)h->lat_ns[ nl-1UL ] : 0.0;
   printf( "{\"tile\": \"%s\", \"frags\": %lu, \"published\": %lu, \"seconds\": %.6f, \"txn_per_s\": %.1f, "
-          "\"rr_cnt\": %lu, \"rr_idx\": %lu, \"sandbox\": %d}\n",
-          kind, h->n, h->res_cnt, t1-t0, (double)h->n/(t1-t0), rr_cnt, rr_idx, h->sandbox );
+          "\"rr_cnt\": %lu, \"rr_idx\": %lu, \"sandbox\": %d, \"rate\": %.1f, \"lat_p50_us\": %.2f, "
+          "\"lat_p99_us\": %.2f, \"lat_max_us\": %.2f}\n",
+          kind, h->n, h->res_cnt, t1-t0, (double)h->n/(t1-t0), rr_cnt, rr_idx, h->sandbox, h->rate, p50, p99, pmx );
   fflush( stdout );
   _exit( h->tile_halted==1 ? 0 : 5 );
 }

@@ -43,7 +43,8 @@ def test_service_marks_links_failed_on_launch_failure(tmp_path):
             "assert ed25519.LIB_PATH.endswith('libfd_ed25519_hip_faultinj.so'); "
             "a, b = tile.ShLink(%r), tile.ShLink(%r); c, d = tile.ShLink(%r), tile.ShLink(%r); "
             "rc, st = tile.vservice_serve([a, c], [b, d], batch_sigs=256, slot_cnt=3, gpu_parse=False); "
-            "print(rc, [s['end_code'] for s in st]); sys.exit(1 if rc else 0)"
+            "print(rc, [s['end_code'] for s in st]); "
+            "print(tile._lib.fd_ed25519_hip_last_error().decode(), file=sys.stderr); sys.exit(1 if rc else 0)"
             % (REPO, txl.name, vdl.name, tx2.name, vd2.name))
     env = dict(os.environ, FD_ED25519_HIP_LIB=FAULT_LIB)
     t0 = time.time()

@@ -64,7 +64,7 @@ def test_service_exits_once_every_tile_is_gone(stream, tmp_path):
     tiles = []
     try:
         tiles = [run_harness("verify_hip", path, str(tmp_path / f"t{k}.bin"), app=app, rr=(2, k),
-                             extra=("--rate", "2000")) for k in range(2)]
+                             extra=("--rate", "500")) for k in range(2)]
         time.sleep(1.0)
         assert all(p.poll() is None for p in tiles)      # mid-stream
         for p in tiles:
@@ -97,7 +97,7 @@ def test_service_serves_on_when_one_tile_dies(stream, reference_runs, tmp_path):
     procs = []
     try:
         procs = [run_harness("verify_hip", path, str(tmp_path / f"hip{k}.bin"), app=app, rr=(3, k),
-                             extra=(("--rate", "1000") if k == 2 else ())) for k in range(3)]
+                             extra=(("--rate", "500") if k == 2 else ())) for k in range(3)]
         time.sleep(0.5)
         procs[2].send_signal(signal.SIGKILL)
         for k in (0, 1):
@@ -193,7 +193,7 @@ def test_sigterm_ends_every_link_and_the_tile_stops(stream, tmp_path):
     app = uuid.uuid4().hex[:10]
     svc = start_standin(app, 1)
     try:
-        p = run_harness("verify_hip", path, str(tmp_path / "hip.bin"), app=app, timeout=60, extra=("--rate", "2000"))
+        p = run_harness("verify_hip", path, str(tmp_path / "hip.bin"), app=app, timeout=60, extra=("--rate", "500"))
         time.sleep(0.8)
         svc.send_signal(signal.SIGTERM)
         wait_exit(svc, 15)

@@ -11,7 +11,7 @@ per-tile stream time runs from its first frag to the end of the stream, and
 the aggregate is all tiles' transactions over the longest stream time (the
 producers start together).  Verdicts are checked (all SUCCESS).
 
-    python tools/service_bench.py [--tiles 1,2,4,6] [--txns 1000000] [--batch 4096] [--gpu-parse]
+    python tools/service_bench.py [--tiles 1,2,4,6] [--txns 1000000] [--batch 4096] [--gpu-parse | --zero-copy]
 """
 import argparse
 import json
@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--slots", type=int, default=3)
     ap.add_argument("--gpu-parse", action="store_true")
+    ap.add_argument("--zero-copy", action="store_true", help="the service DMAs payloads from the txn links in place")
     ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES of the service process")
     ap.add_argument("--service", default=SERVICE, help="service binary (an A/B build's)")
     ap.add_argument("--producer", default=PRODUCER, help="tile-side binary (the same A/B build's: the frag protocol)")
@@ -76,7 +77,8 @@ def main():
         prefix = f"/fd_vhip_{app}_"
         env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.hw_queues))
         svc = subprocess.Popen([args.service, "--prefix", prefix, "--tiles", str(k), "--batch", str(args.batch),
-                                "--slots", str(args.slots), *(["--gpu-parse"] if args.gpu_parse else [])],
+                                "--slots", str(args.slots), *(["--gpu-parse"] if args.gpu_parse else []),
+                                *(["--zero-copy"] if args.zero_copy else [])],
                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, preexec_fn=pin)
         line = svc.stdout.readline()
         if not line.startswith("ready"):
@@ -112,7 +114,7 @@ def main():
                     pass
     for path in paths:
         os.unlink(path)
-    print(json.dumps({"service_bench": out, "batch": args.batch, "slots": args.slots, "gpu_parse": args.gpu_parse,
+    print(json.dumps({"service_bench": out, "batch": args.batch, "slots": args.slots, "gpu_parse": args.gpu_parse, "zero_copy": args.zero_copy,
                       "hw_queues": args.hw_queues, "pin": args.pin, "node_cpus": len(node_cpus)}))
 
 
