@@ -214,7 +214,13 @@ typedef struct {
 int
 fd_ed25519_hip_engine_info( fd_ed25519_hip_engine_t const * engine, fd_ed25519_hip_info_t * info );
 
-/* The engine's HIP stream (a hipStream_t). */
+/* The engine's HIP stream (a hipStream_t).  Engine streams are drawn from
+   one per-device set of GPU_MAX_HW_QUEUES streams that the library creates
+   once and every engine of the process shares (at most 32; 4 by default),
+   so this stream may also carry other engines' work: waiting on it
+   (hipStreamSynchronize, fd_ed25519_hip_engine_sync, events recorded on
+   it) waits for theirs too.  Order your own work with events recorded
+   right after it, not with whole-stream waits, when other engines run. */
 void *
 fd_ed25519_hip_engine_stream( fd_ed25519_hip_engine_t * engine );
 
@@ -429,7 +435,8 @@ fd_ed25519_hip_device_count( void );
 int
 fd_ed25519_hip_device_clock_mhz( fd_ed25519_hip_engine_t * engine );
 
-/* Waits for all work enqueued on the engine's stream. */
+/* Waits for all work enqueued on the engine's stream -- which other
+   engines of the device may share (fd_ed25519_hip_engine_stream). */
 int
 fd_ed25519_hip_engine_sync( fd_ed25519_hip_engine_t * engine );
 
