@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES of the service process")
     ap.add_argument("--service", default=SERVICE, help="service binary (an A/B build's)")
     ap.add_argument("--producer", default=PRODUCER, help="tile-side binary (the same A/B build's: the frag protocol)")
+    ap.add_argument("--producer-profile", action="store_true",
+                    help="the tile side's cycles per txn (fd_shlink_producer --profile: runs unsandboxed)")
     ap.add_argument("--pin", choices=["none", "node"], default="node",
                     help="node: the service and the tile processes on the CPUs of the GPU's NUMA node, as fdctl "
                          "pins its tiles (default); none: wherever the OS puts them")
@@ -84,12 +86,16 @@ def main():
         if not line.startswith("ready"):
             raise SystemExit(f"service did not start: {line!r} {svc.stderr.read()[-2000:]}")
         t0 = time.time()
-        prods = [subprocess.Popen([args.producer, f"{prefix}{i}_txn", f"{prefix}{i}_vd", paths[i]],
+        prods = [subprocess.Popen([args.producer, f"{prefix}{i}_txn", f"{prefix}{i}_vd", paths[i],
+                                   *(["--profile"] if args.producer_profile else [])],
                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, preexec_fn=pin) for i in range(k)]
         ok = True
         for pr in prods:
             so, se = pr.communicate(timeout=300)
             ok &= pr.returncode == 0 and len(so) >= args.txns and so[:args.txns].count(0) == args.txns
+            for ln in se.decode(errors="replace").splitlines():
+                if "profile" in ln:
+                    print(ln, file=sys.stderr)
         wall = time.time() - t0
         so, se = svc.communicate(timeout=120)
         res = json.loads(so.strip().splitlines()[-1])

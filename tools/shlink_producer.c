@@ -5,7 +5,7 @@
    src/app/fdctl/run/tiles/verify.seccomppolicy) and runs the whole stream
    with memory operations only.  Any other system call would kill it.
 
-     shlink_producer IN_LINK OUT_LINK PAYLOAD_FILE [--no-sandbox] [--stale-ms MS]
+     shlink_producer IN_LINK OUT_LINK PAYLOAD_FILE [--no-sandbox] [--stale-ms MS] [--profile]
 
    PAYLOAD_FILE: u64 n, n x u32 sizes, the payloads back to back.  Frag i
    carries sig = i; after the last one an EOS frag.  Verdict frags are
@@ -23,7 +23,10 @@
    mode leaves no clock -- not even the time-stamp counter, which the kernel
    disables for it -- so time is counted in pause instructions, their rate
    measured before the sandbox (the waits only run longer than that, so the
-   bound is a lower bound on the time waited). */
+   bound is a lower bound on the time waited).  --profile (implies
+   --no-sandbox: strict mode disables the time-stamp counter) prints the
+   cycles per transaction spent publishing, taking verdicts (with the frag
+   assembly) and waiting, to stderr at the end. */
 #define _GNU_SOURCE
 #include "../include/fd_ed25519_hip_tile.h"
 
@@ -122,10 +125,11 @@ take_verdicts( fd_ed25519_hip_shlink_t * in, unsigned char * buf, signed char * 
 int
 main( int argc, char ** argv ) {
   if( argc<4 ) { fprintf( stderr, "usage: %s IN_LINK OUT_LINK PAYLOAD_FILE [--no-sandbox] [--stale-ms MS]\n", argv[0] ); return 1; }
-  int sandbox = 1;
+  int sandbox = 1, profile = 0;
   double stale_ms = 1000.0;
   for( int a=4; a<argc; a++ ) {
     if(      !strcmp( argv[a], "--no-sandbox" ) ) sandbox = 0;
+    else if( !strcmp( argv[a], "--profile" ) ) { profile = 1; sandbox = 0; }
     else if( !strcmp( argv[a], "--stale-ms" ) && a+1<argc ) stale_ms = strtod( argv[++a], NULL );
     else { fprintf( stderr, "bad argument %s\n", argv[a] ); return 1; }
   }
@@ -170,18 +174,24 @@ main( int argc, char ** argv ) {
   unsigned long i = 0UL, got = 0UL;
   int eos = 0;
   stream_t st = { pay, off, sz };
+  unsigned long long pf_pub = 0ULL, pf_take = 0ULL, pf_wait = 0ULL, pf_c = profile ? __rdtsc() : 0ULL, pf_n;
+#define PF( acc ) do { if( profile ) { pf_n = __rdtsc(); acc += pf_n - pf_c; pf_c = pf_n; } } while(0)
   while( i<n ) {
     int r = fd_ed25519_hip_shlink_publish( txl, pay + off[ i ], sz[ i ], i, 0U );
+    PF( pf_pub );
     if( r==0 ) {
       /* as the tile's mux loop does (after_credit between frags): the
          verdicts that are back are taken every 16 frags, not only when the
          txn link runs out of credits */
       if( !(++i & 15UL) && ( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr, &st ) || eos ) ) leave( 2 );
+      PF( pf_take );
       continue;
     }
     if( r!=1 ) leave( 2 );
     if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr, &st ) || eos ) leave( 2 );
+    PF( pf_take );
     watch( &wt );
+    PF( pf_wait );
   }
   while( fd_ed25519_hip_shlink_publish( txl, NULL, 0UL, n, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
     if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr, &st ) || eos ) leave( 2 );
@@ -192,6 +202,13 @@ main( int argc, char ** argv ) {
     watch( &wt );
   }
   if( got!=n ) leave( 2 );
+  if( profile ) {
+    char line[ 200 ];
+    int k = snprintf( line, sizeof(line), "shlink_producer profile: cycles per txn: publish %.0f, take verdicts %.0f, "
+                      "wait (no credit) %.0f\n", (double)pf_pub/(double)n, (double)pf_take/(double)n,
+                      (double)pf_wait/(double)n );
+    if( k>0 ) say( line );
+  }
   unsigned long w = 0UL;
   while( w<n ) {
     long k = write( 1, verdict + w, n - w );
