@@ -12,7 +12,13 @@
    re-reads seq to detect an overrun.  Flow control is credit based: the
    consumer publishes how many frags it has taken, and the producer never
    runs more than depth frags ahead (the reference's fctl / fseq pair,
-   reduced to one counter).
+   reduced to one counter).  Both sides touch that counter lazily, as
+   fd_fctl does (src/tango/fctl/fd_fctl.h: credits are refilled only when
+   the cached ones run out, the consumer's fseq is published periodically):
+   the producer re-reads it only when the credits it last saw are spent,
+   and the consumer publishes it every depth/16 frags and whenever it finds
+   the link empty, so the counter's cache line does not move between the
+   two cores on every frag.
 
    Liveness (fd_cnc's heartbeat / signal pair, src/tango/cnc/fd_cnc.h:63-65,
    129-130, reduced to two words): each producer ticks a heartbeat word in
@@ -95,6 +101,9 @@ struct fd_ed25519_hip_shlink {
   uint64_t        seq;
   uint64_t        chunk;
   int             prepared;   /* producer: prepare() found a credit for seq */
+  uint64_t        cr_seen;    /* producer: the consumer's count when last read */
+  uint64_t        cr_pub;     /* consumer: the count last published          */
+  uint64_t        cr_batch;   /* consumer: publish at least every cr_batch frags */
   /* process-local geometry, validated at create / join */
   uint64_t        depth;
   uint64_t        chunk_cnt;
@@ -171,6 +180,7 @@ fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
   }
   l->hdr->depth     = l->depth     = depth;
   l->hdr->chunk_cnt = l->chunk_cnt = chunk_cnt;
+  l->cr_batch       = depth>=16UL ? depth/16UL : 1UL;
   l->hdr->mtu       = l->mtu       = FD_ED25519_HIP_SHLINK_MTU;
   l->hdr->proto     = FD_ED25519_HIP_SHLINK_PROTO;
   l->hdr->creator   = (uint64_t)getpid();
@@ -208,6 +218,7 @@ fd_ed25519_hip_shlink_join( char const * name ) {
     munmap( l->hdr, l->map_sz ); free( l ); errno = EINVAL; return NULL;
   }
   l->depth = depth; l->chunk_cnt = chunk_cnt; l->mtu = mtu;
+  l->cr_batch = depth>=16UL ? depth/16UL : 1UL;
   l->dcache = (unsigned char *)l->mcache + depth * sizeof(shlink_meta_t);
   return l;
 }
@@ -244,8 +255,12 @@ fd_ed25519_hip_shlink_mapping( fd_ed25519_hip_shlink_t const * l, unsigned long 
 unsigned char *
 fd_ed25519_hip_shlink_prepare( fd_ed25519_hip_shlink_t * l ) {
   /* a bogus credit count from the consumer only lets the producer overrun
-     that consumer: every write stays inside the local geometry */
-  if( l->seq - atomic_load_explicit( &l->hdr->consumed, memory_order_acquire )>=l->depth ) return NULL;
+     that consumer: every write stays inside the local geometry.  The count
+     is re-read only when the credits last seen are spent. */
+  if( l->seq - l->cr_seen>=l->depth ) {
+    l->cr_seen = atomic_load_explicit( &l->hdr->consumed, memory_order_acquire );
+    if( l->seq - l->cr_seen>=l->depth ) return NULL;
+  }
   uint64_t mtu_chunks = (l->mtu + SHLINK_CHUNK - 1UL) / SHLINK_CHUNK;
   if( l->chunk + mtu_chunks>l->chunk_cnt ) l->chunk = 0UL;   /* compact wrap */
   l->prepared = 1;
@@ -295,7 +310,14 @@ fd_ed25519_hip_shlink_peek( fd_ed25519_hip_shlink_t * l, unsigned long * sz, uns
   uint64_t seq = l->seq;
   shlink_meta_t * m = &l->mcache[ seq & (l->depth-1UL) ];
   uint64_t s0 = atomic_load_explicit( &m->seq, memory_order_acquire );
-  if( (int64_t)(s0 - seq)<0 ) { *err = 1; return NULL; }     /* not yet published */
+  if( (int64_t)(s0 - seq)<0 ) {                               /* not yet published: */
+    if( l->cr_pub!=seq ) {                                    /* the credits taken so far go back */
+      l->cr_pub = seq;
+      atomic_store_explicit( &l->hdr->consumed, seq, memory_order_release );
+    }
+    *err = 1;
+    return NULL;
+  }
   if( s0!=seq ) { *err = -1; return NULL; }                   /* overrun */
   unsigned long n     = m->sz;
   unsigned long sg    = m->sig;
@@ -315,7 +337,10 @@ fd_ed25519_hip_shlink_advance( fd_ed25519_hip_shlink_t * l ) {
   atomic_thread_fence( memory_order_acquire );
   int ok = atomic_load_explicit( &m->seq, memory_order_relaxed )==seq;
   l->seq = seq + 1UL;
-  atomic_store_explicit( &l->hdr->consumed, l->seq, memory_order_release );
+  if( l->seq - l->cr_pub>=l->cr_batch ) {
+    l->cr_pub = l->seq;
+    atomic_store_explicit( &l->hdr->consumed, l->seq, memory_order_release );
+  }
   return ok ? 0 : -1;
 }
 

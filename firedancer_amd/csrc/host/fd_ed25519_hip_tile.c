@@ -959,6 +959,12 @@ vt_open( fd_ed25519_hip_vtile_t * vt ) {
   return 0;
 }
 
+/* Staged payloads start on a cache line: a copy into cold lines that
+   starts mid-line costs the host about twice as much (split stores and
+   partial-line fills; the staging ring is megabytes, far out of L2), and
+   the few bytes of padding per payload cost the link nothing that matters. */
+#define STAGE_ALIGN( off ) ( ( (off) + 63UL ) & ~63UL )
+
 /* GPU-parse mode: the payload goes to the device as is; the host reads
    only byte 0 (the signature count, to reserve slots) and bytes 1..8 (the
    dedup tag, valid whenever the device's parse accepts the payload). */
@@ -976,16 +982,17 @@ vt_frag_raw( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigne
   unsigned long c = payload[0], nsig = (c>=1UL && c<=16UL) ? c : 0UL;
   if( vt_open( vt ) ) return vt->err;
   fd_ed25519_hip_slot_t * s = vt->open;
-  if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap || s->msg_bytes+payload_sz>s->msg_cap ) ) {
+  if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap ||
+                      STAGE_ALIGN( s->msg_bytes )+payload_sz>s->msg_cap ) ) {
     vt_submit_open( vt );
     if( vt_open( vt ) ) return vt->err;
     s = vt->open;
   }
-  unsigned long ti = s->txn_cnt++;
-  memcpy( s->msgs + s->msg_bytes, payload, payload_sz );
-  s->msg_off[ ti ] = s->msg_bytes;
+  unsigned long ti = s->txn_cnt++, poff = STAGE_ALIGN( s->msg_bytes );
+  memcpy( s->msgs + poff, payload, payload_sz );
+  s->msg_off[ ti ] = poff;
   s->msg_sz [ ti ] = (unsigned int)payload_sz;
-  s->msg_bytes += payload_sz;
+  s->msg_bytes = poff + payload_sz;
   s->sig_cnt   += nsig;
   vrec_t * r = vq_push( vt );
   if( !r ) return vt->err;
@@ -1097,16 +1104,17 @@ fd_ed25519_hip_vtile_frag( fd_ed25519_hip_vtile_t * vt, unsigned char const * pa
     return 0;
   }
   unsigned long nsig = (t.signature_cnt>=1U && t.signature_cnt<=16U) ? t.signature_cnt : 0UL;
-  if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap || s->msg_bytes+payload_sz>s->msg_cap ) ) {
+  if( s->txn_cnt && ( s->sig_cnt+nsig>s->sig_cap || s->txn_cnt+1UL>s->txn_cap ||
+                      STAGE_ALIGN( s->msg_bytes )+payload_sz>s->msg_cap ) ) {
     vt_submit_open( vt );
     if( vt_open( vt ) ) return vt->err;
     s = vt->open;
   }
-  unsigned long poff   = s->msg_bytes;
+  unsigned long poff   = STAGE_ALIGN( s->msg_bytes );
   unsigned long moff   = poff + t.message_off;
   unsigned long msg_sz = payload_sz - t.message_off;
   memcpy( s->msgs + poff, payload, payload_sz );
-  s->msg_bytes += payload_sz;
+  s->msg_bytes = poff + payload_sz;
   unsigned long first = s->sig_cnt;
   for( unsigned long j=0UL; j<nsig; j++ ) {
     unsigned long k = first + j;
@@ -1656,8 +1664,12 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
 #else
 #define PF_MARK( i ) do {} while(0)
 #endif
+  /* the liveness pass (a clock read, the peer's header lines) runs every
+     16th busy pass and on every idle one: microseconds apart either way */
+  unsigned long pass = 0UL;
+  int idle = 1;
   for(;;) {
-    if( (rc = vsvc_check( &L, &local )) ) goto fail;
+    if( ( idle || !(++pass & 15UL) ) && (rc = vsvc_check( &L, &local )) ) goto fail;
     PF_MARK( 0 );
     /* completed batches resolve (in frag order); their verdicts go out as
        far as credits allow: the verdict byte, then (SUCCESS) the trailer
@@ -1726,10 +1738,14 @@ vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flag
     }
     PF_MARK( 3 );
     /* `in` drained: send the open batch if a slot can take it (all of it at the end) */
+    int flushed = 0;
     if( !pulled && vt->open && vt->open->txn_cnt &&
-        ( eos || slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<slot_cnt ) )
+        ( eos || slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<slot_cnt ) ) {
       fd_ed25519_hip_vtile_flush( vt, eos );
-    else if( !pulled && !published ) {
+      flushed = 1;
+    }
+    idle = !pulled && !published && !flushed;
+    if( idle ) {
       spin_pause();
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
       pf_idle++;

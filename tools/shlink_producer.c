@@ -110,13 +110,15 @@ take_verdicts( fd_ed25519_hip_shlink_t * in, unsigned char * buf, signed char * 
     signed char v = (signed char)buf[ 0 ];
     if( (v==FD_ED25519_HIP_TXN_VERIFY_SUCCESS) != (sz>1UL) ) return -1;   /* a frag with every SUCCESS, only then */
     if( sz>1UL ) {
+      /* assembled at a cache-line boundary, as the tile assembles into its
+         out dcache's 64-byte chunks (packed for stdout after the stream) */
       unsigned long k = *next;
-      if( fr->used + 4UL + FD_ED25519_HIP_TPU_DCACHE_MTU > fr->cap ) return -1;
-      unsigned int fsz = (unsigned int)fd_ed25519_hip_frag_assemble( fr->mem + fr->used + 4UL, st->pay + st->off[ k ],
+      if( fr->used + 64UL + FD_ED25519_HIP_TPU_DCACHE_MTU > fr->cap ) return -1;
+      unsigned int fsz = (unsigned int)fd_ed25519_hip_frag_assemble( fr->mem + fr->used + 64UL, st->pay + st->off[ k ],
                                                                      st->sz[ k ], buf + 1, sz - 1UL );
       if( !fsz ) return -1;
       memcpy( fr->mem + fr->used, &fsz, 4UL );
-      fr->used += 4UL + fsz;
+      fr->used += 64UL + ( ( fsz + 63UL ) & ~63UL );
     }
     verdict[ (*next)++ ] = v;
   }
@@ -148,9 +150,10 @@ main( int argc, char ** argv ) {
   signed char * verdict = (signed char *)malloc( n + 1UL );
   unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
   frags_t fr;
-  fr.cap = total + n*(FD_ED25519_HIP_TXN_MAX_SZ + 8UL) + FD_ED25519_HIP_TPU_DCACHE_MTU;   /* every payload + pad, trailer, size word; one frag's room */
+  fr.cap = total + n*(FD_ED25519_HIP_TXN_MAX_SZ + 8UL + 128UL) + FD_ED25519_HIP_TPU_DCACHE_MTU + 64UL;   /* every payload + pad,
+                                                      trailer, size line, alignment; one frag's room */
   fr.used = 0UL;
-  fr.mem = (unsigned char *)malloc( fr.cap );
+  fr.mem = (unsigned char *)aligned_alloc( 64UL, ( fr.cap + 63UL ) & ~63UL );
   if( !fr.mem ) return 1;
   /* touched before the stream: page faults of the output buffers would
      otherwise land inside it (a tile publishes into its out dcache, which
@@ -215,9 +218,19 @@ main( int argc, char ** argv ) {
     if( k<=0 ) leave( 2 );
     w += (unsigned long)k;
   }
+  /* packed in place: u32 size, then the frag */
+  unsigned long packed = 0UL;
+  for( unsigned long e=0UL; e<fr.used; ) {
+    unsigned int fsz;
+    memcpy( &fsz, fr.mem + e, 4UL );
+    memmove( fr.mem + packed, fr.mem + e, 4UL );
+    memmove( fr.mem + packed + 4UL, fr.mem + e + 64UL, fsz );
+    packed += 4UL + fsz;
+    e      += 64UL + ( ( fsz + 63UL ) & ~63UL );
+  }
   w = 0UL;
-  while( w<fr.used ) {
-    long k = write( 1, fr.mem + w, fr.used - w );
+  while( w<packed ) {
+    long k = write( 1, fr.mem + w, packed - w );
     if( k<=0 ) leave( 2 );
     w += (unsigned long)k;
   }
