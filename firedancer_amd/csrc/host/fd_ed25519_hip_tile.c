@@ -1178,7 +1178,7 @@ fd_ed25519_hip_vtile_poll_frags( fd_ed25519_hip_vtile_t * vt, int wait, unsigned
   return n;
 }
 
-/* The service's path (vservice_loop): resolved records are published
+/* The service's path (vsvc_pass): resolved records are published
    straight from the output arena, without poll_frags' copy into a caller
    buffer.  vt_head returns the oldest record once it is resolved (its frag,
    for SUCCESS, at vt->oa + arena_off, frag_sz bytes), vt_pop retires it. */
@@ -1597,7 +1597,8 @@ vsvc_check( vsvc_link_t * L, int * local ) {
   return 0;
 }
 
-/* the vtile's idle hook while every slot is in flight */
+/* the vtile's idle hook, for the rare wait inside a frag (a zero-copy
+   payload out of ring order closes a batch and needs the next slot) */
 static int
 vsvc_idle( void * ctx ) {
   vsvc_link_t * L = (vsvc_link_t *)ctx;
@@ -1607,217 +1608,284 @@ vsvc_idle( void * ctx ) {
   return rc;
 }
 
+/* 1 if the vtile takes one more frag of any shape without waiting for the
+   GPU: the open batch has room for a transaction of 16 signatures and an
+   MTU of bytes, or the next slot is free (completed batches are drained
+   before this is asked) */
 static int
-vservice_loop( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
-               fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
-               fd_ed25519_hip_vservice_stats_t * stats, _Atomic int * stop,
-               fd_ed25519_hip_vservice_opts_t const * opts, _Atomic unsigned * ready ) {
-  if( !in || !out ) return FD_ED25519_HIP_ERR_INVAL;
-  vsvc_link_t L;
-  memset( &L, 0, sizeof(L) );
-  L.in = in; L.out = out; L.dev_stop = stop; L.beat = 1UL;
-  L.ext_stop      = opts ? opts->stop : NULL;
-  L.tile_stale_ns = !opts || !opts->tile_stale_ns ? FD_ED25519_HIP_VSERVICE_TILE_STALE_NS : opts->tile_stale_ns;
-  long hang_ns    = !opts || !opts->gpu_hang_ns ? FD_ED25519_HIP_VSERVICE_GPU_HANG_NS : opts->gpu_hang_ns;
-  fd_ed25519_hip_vtile_t * vt = fd_ed25519_hip_vtile_new( device, slot_cnt, batch_sigs, 16UL, 64UL, flags );
-  if( !vt ) {
-    fd_ed25519_hip_shlink_fail( in, FD_ED25519_HIP_ERR_INVAL ); fd_ed25519_hip_shlink_fail( out, FD_ED25519_HIP_ERR_INVAL );
-    if( stop ) atomic_store_explicit( stop, 1, memory_order_release );
-    if( stats ) stats->end_code = FD_ED25519_HIP_ERR_INVAL;
-    if( ready ) atomic_fetch_add_explicit( ready, 1U, memory_order_release );
-    return FD_ED25519_HIP_ERR_INVAL;
+vt_room( fd_ed25519_hip_vtile_t const * vt ) {
+  if( vt->err ) return 0;
+  fd_ed25519_hip_slot_t const * s = vt->open;
+  if( s && s->sig_cnt+16UL<=s->sig_cap && s->txn_cnt+1UL<=s->txn_cap &&
+      STAGE_ALIGN( s->msg_bytes ) + FD_ED25519_HIP_TXN_MTU + 64UL<=s->msg_cap ) return 1;
+  fd_ed25519_hip_pipe_t const * pipe = vt->pipe;
+  return pipe->slot[ pipe->next_acq % pipe->slot_cnt ].state==SLOT_FREE;
+}
+
+/* One link pair of the verify service.  A service thread serves one or
+   more pairs, a pass over each in turn; a pass never waits for the GPU
+   (frags stay in the txn link while the pair's slots are all in flight),
+   so the pairs of a thread do not hold each other up. */
+typedef struct {
+  vsvc_link_t                       L;
+  fd_ed25519_hip_vtile_t *          vt;
+  unsigned char *                   buf;      /* a frag copied out of the shared dcache (copying modes) */
+  void *                            reg;      /* zero-copy: the txn link's mapping, page-locked */
+  fd_ed25519_hip_vservice_stats_t * stats;
+  _Atomic int *                     stop;
+  unsigned                          slot_cnt;
+  int                               device;
+  double                            t0, t_first, hang_s;
+  unsigned long                     txns, pass;
+  int                               eos, idle, live;
+  char                              errmsg[ 256 ];   /* last_error of a device-wide end (it is per thread) */
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  unsigned long long                pf_t[ 5 ], pf_idle, pf_pass, pf_cons;
+#endif
+} vsvc_t;
+
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+#define PF_MARK( i ) do { pf_n = __rdtsc(); S->pf_t[ i ] += pf_n - pf_c; pf_c = pf_n; } while(0)
+#else
+#define PF_MARK( i ) do {} while(0)
+#endif
+
+/* the pair ends with rc (0: EOS answered): both links marked failed with a
+   failure code, the sibling pairs stopped when the cause is the device's
+   (local = 0), the stats written, the vtile (engines, device memory) freed */
+static void
+vsvc_end( vsvc_t * S, int rc, int local ) {
+  if( rc ) {
+    fd_ed25519_hip_shlink_fail( S->L.in, rc );
+    fd_ed25519_hip_shlink_fail( S->L.out, rc );
+    if( S->stop && !local ) atomic_store_explicit( S->stop, 1, memory_order_release );
+    if( !local ) snprintf( S->errmsg, sizeof(S->errmsg), "%s", fd_ed25519_hip_last_error() );
   }
+  if( S->stats ) {
+    S->stats->txn_cnt      = S->txns;
+    S->stats->batches      = S->vt ? S->vt->pipe->seq : 0UL;
+    S->stats->seconds      = now_s() - ( S->txns ? S->t_first : S->t0 );
+    S->stats->device_bytes = S->vt ? fd_ed25519_hip_vtile_device_bytes( S->vt ) : 0UL;
+    S->stats->shared_device_bytes = fd_ed25519_hip_shared_device_bytes( S->device );
+    S->stats->end_code     = rc;
+  }
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  double d = (double)( S->txns + 1UL );
+  fprintf( stderr, "vservice profile: %lu txns, %llu passes (%llu idle); cycles per txn: status %.0f publish %.0f "
+           "poll %.0f consume+frag %.0f (of which consume %.0f) flush+pause %.0f\n",
+           S->txns, S->pf_pass, S->pf_idle, (double)S->pf_t[0]/d, (double)S->pf_t[1]/d, (double)S->pf_t[2]/d,
+           (double)S->pf_t[3]/d, (double)S->pf_cons/d, (double)S->pf_t[4]/d );
+#endif
+  free( S->buf ); S->buf = NULL;
+  if( S->vt ) {
+    S->vt->idle = NULL;   /* the delete below may wait for batches in flight */
+    fd_ed25519_hip_vtile_delete( S->vt );
+    S->vt = NULL;
+  }
+  if( S->reg ) { hipHostUnregister( S->reg ); S->reg = NULL; }   /* after the batches that read from it */
+  S->live = 0;
+}
+
+/* builds the pair's vtile (and, zero-copy, page-locks the txn link) and
+   runs every kernel once; 0, or the pair has ended with the code */
+static int
+vsvc_open( vsvc_t * S, int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+           fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out, fd_ed25519_hip_vservice_stats_t * stats,
+           _Atomic int * stop, fd_ed25519_hip_vservice_opts_t const * opts ) {
+  memset( S, 0, sizeof(*S) );
+  S->L.in = in; S->L.out = out; S->L.dev_stop = stop; S->L.beat = 1UL;
+  S->L.ext_stop      = opts ? opts->stop : NULL;
+  S->L.tile_stale_ns = !opts || !opts->tile_stale_ns ? FD_ED25519_HIP_VSERVICE_TILE_STALE_NS : opts->tile_stale_ns;
+  long hang_ns       = !opts || !opts->gpu_hang_ns ? FD_ED25519_HIP_VSERVICE_GPU_HANG_NS : opts->gpu_hang_ns;
+  S->hang_s   = hang_ns>0L ? 1e-9*(double)hang_ns : 0.0;
+  S->stats = stats; S->stop = stop; S->slot_cnt = slot_cnt; S->device = device;
+  S->t0 = now_s(); S->idle = 1; S->live = 1;
+  if( !in || !out ) { vsvc_end( S, FD_ED25519_HIP_ERR_INVAL, 0 ); return FD_ED25519_HIP_ERR_INVAL; }
+  S->vt = fd_ed25519_hip_vtile_new( device, slot_cnt, batch_sigs, 16UL, 64UL, flags );
+  if( !S->vt ) { vsvc_end( S, FD_ED25519_HIP_ERR_INVAL, 0 ); return FD_ED25519_HIP_ERR_INVAL; }
+  fd_ed25519_hip_vtile_t * vt = S->vt;
   vt->trailer_only = 1;   /* the tile keeps its payloads: verdict frags carry the trailers */
   vt->idle     = vsvc_idle;
-  vt->idle_ctx = &L;
-  vt->hang_s   = hang_ns>0L ? 1e-9*(double)hang_ns : 0.0;
-  unsigned char * buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
-  double t0 = now_s(), t_first = 0.0;   /* the stream's time runs from its first frag */
-  unsigned long txns = 0UL;
-  int eos = 0, rc = FD_ED25519_HIP_OK, local = 0;
-  void * reg = NULL;
-  if( !buf ) { rc = FD_ED25519_HIP_ERR_NOMEM; goto fail; }
+  vt->idle_ctx = &S->L;
+  vt->hang_s   = S->hang_s;
+  S->buf = (unsigned char *)malloc( FD_ED25519_HIP_SHLINK_MTU );
+  if( !S->buf ) { vsvc_end( S, FD_ED25519_HIP_ERR_NOMEM, 0 ); return FD_ED25519_HIP_ERR_NOMEM; }
   if( flags & FD_ED25519_HIP_VSERVICE_ZERO_COPY ) {
     /* the txn link's mapping page-locked with the GPU: batches DMA their
        payloads from the rooms the tile wrote */
     unsigned long map_sz;
     void * m = fd_ed25519_hip_shlink_mapping( in, &map_sz );
     hipError_t he = hipHostRegister( m, map_sz, hipHostRegisterPortable );
-    if( he!=hipSuccess ) { rc = tile_fail( "hipHostRegister(txn link)", he ); goto fail; }
-    reg = m;
+    if( he!=hipSuccess ) { int rc = tile_fail( "hipHostRegister(txn link)", he ); vsvc_end( S, rc, 0 ); return rc; }
+    S->reg = m;
     vt->zero_copy = 1;
     vt->gpu_parse = 1;
     vt->zc_base   = fd_ed25519_hip_shlink_dcache( in, &vt->zc_size );
   }
-  {
-    int we = vt_warm( vt );
-    if( ready ) atomic_fetch_add_explicit( ready, 1U, memory_order_release );   /* ready (or failed): counted once */
-    ready = NULL;
-    if( we ) { rc = we; goto fail; }
-  }
+  int we = vt_warm( vt );
+  if( we ) { vsvc_end( S, we, 0 ); return we; }
+  return 0;
+}
+
+/* the oldest batch in flight has been on the GPU longer than the bound */
+static int
+vsvc_hung( vsvc_t const * S ) {
+  fd_ed25519_hip_pipe_t const * pipe = S->vt->pipe;
+  if( S->hang_s<=0.0 || !pipe->in_flight ) return 0;
+  pipe_slot_t const * o = &pipe->slot[ pipe->next_poll % pipe->slot_cnt ];
+  return o->state==SLOT_BUSY && now_s() - o->pub.t_submit>S->hang_s;
+}
+
+/* One pass over a live pair: liveness, completed batches resolved and
+   their verdicts published, then as many frags staged as the vtile takes
+   without waiting.  Ends the pair (vsvc_end) on EOS or failure. */
+static void
+vsvc_pass( vsvc_t * S ) {
+  fd_ed25519_hip_vtile_t * vt = S->vt;
+  int rc, local = 1;
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
-  /* A/B build only: cycles per loop section (printed at the end) */
-  unsigned long long pf_t[ 5 ] = { 0ULL, 0ULL, 0ULL, 0ULL, 0ULL }, pf_idle = 0ULL, pf_pass = 0ULL, pf_c = __rdtsc(), pf_n;
-  unsigned long long pf_cons = 0ULL;
-  vt_wait_cycles = vt_resolve_cycles = vt_blocks = 0ULL;
-#define PF_MARK( i ) do { pf_n = __rdtsc(); pf_t[ i ] += pf_n - pf_c; pf_c = pf_n; } while(0)
-#else
-#define PF_MARK( i ) do {} while(0)
+  unsigned long long pf_c = __rdtsc(), pf_n;
 #endif
   /* the liveness pass (a clock read, the peer's header lines) runs every
      16th busy pass and on every idle one: microseconds apart either way */
-  unsigned long pass = 0UL;
-  int idle = 1;
-  for(;;) {
-    if( ( idle || !(++pass & 15UL) ) && (rc = vsvc_check( &L, &local )) ) goto fail;
-    PF_MARK( 0 );
-    /* completed batches resolve (in frag order); their verdicts go out as
-       far as credits allow: the verdict byte, then (SUCCESS) the trailer
-       of the frag the tile publishes (its fd_txn_t and payload_sz, from
-       the frag in the vtile's arena: the tile has the payload) */
-    while( vt_drain_one( vt, 0 ) ) {}
-    PF_MARK( 2 );
-    int published = 0;
-    for( vrec_t const * r; (r = vt_head( vt )); ) {
-      unsigned char * dst = fd_ed25519_hip_shlink_prepare( out );
-      if( !dst ) break;
-      unsigned long tsz = r->verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ? r->frag_sz : 0UL;
-      dst[ 0 ] = (unsigned char)r->verdict;
-      if( tsz ) memcpy( dst + 1, vt->oa + r->arena_off, tsz );
-      if( (rc = fd_ed25519_hip_shlink_commit( out, 1UL + tsz, r->cookie, 0U )) ) { local = 0; goto fail; }
-      vt_pop( vt );
-      published = 1;
+  if( S->idle || !(++S->pass & 15UL) ) {
+    if( (rc = vsvc_check( &S->L, &local )) ) { vsvc_end( S, rc, local ); return; }
+    if( vsvc_hung( S ) ) {
+      char msg[ 128 ];
+      snprintf( msg, sizeof(msg), "vservice: batch %lu did not complete within %.1f s (GPU hang)",
+                vt->pipe->seq - vt->pipe->in_flight, S->hang_s );
+      fd_ed25519_hip_private_set_error( msg );
+      vsvc_end( S, FD_ED25519_HIP_ERR_TIMEOUT, 0 );
+      return;
     }
-    PF_MARK( 1 );
-    if( (rc = fd_ed25519_hip_vtile_error( vt )) ) {
-      /* a wait the idle hook ended is the hook's cause; any other vtile error the device's */
-      local = rc==L.hook_rc ? L.hook_local : 0;
-      goto fail;
-    }
-    if( eos && !fd_ed25519_hip_vtile_pending( vt ) ) break;
-    /* after_frag for every frag that is ready (copied out of the shared
-       dcache first: the tile is not trusted not to change it meanwhile) */
-    int pulled = 0;
-    while( !eos && vt->zero_copy ) {   /* in place: the payload stays in the link's room */
-      unsigned long sz = 0UL, sig = 0UL;
-      unsigned int ctl = 0U;
-      int perr;
-      unsigned char const * src = fd_ed25519_hip_shlink_peek( in, &sz, &sig, &ctl, &perr );
-      if( !src ) {
-        if( perr==1 ) break;
-        rc = FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL; local = 1; goto fail;   /* overrun, or a line out of bounds */
-      }
-      if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { fd_ed25519_hip_shlink_advance( in ); eos = 1; break; }
-      if( !txns ) t_first = now_s();
-      int r = vt_frag_zc( vt, src, sz, sig );
-      if( r<0 ) { rc = r; local = rc==L.hook_rc ? L.hook_local : 0; goto fail; }
-      /* the credit goes back now: the room itself is reused only after its
-         verdict (the tile's bound on unanswered frags) */
-      if( fd_ed25519_hip_shlink_advance( in ) ) { rc = FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL; local = 1; goto fail; }
-      txns++;
-      pulled = 1;
-    }
-    while( !eos && !vt->zero_copy ) {
-      unsigned long sz = 0UL, sig = 0UL;
-      unsigned int ctl = 0U;
-#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
-      unsigned long long c0 = __rdtsc();
-#endif
-      int r = fd_ed25519_hip_shlink_consume( in, buf, &sz, &sig, &ctl );
-#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
-      pf_cons += __rdtsc() - c0;
-#endif
-      if( r==1 ) break;
-      if( r ) { rc = FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL; local = 1; goto fail; }   /* overrun: the tile ignored credits */
-      if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { eos = 1; break; }
-      if( !txns ) t_first = now_s();
-      r = fd_ed25519_hip_vtile_frag( vt, buf, sz, sig );
-      if( r<0 ) { rc = r; local = rc==L.hook_rc ? L.hook_local : 0; goto fail; }
-      txns++;
-      pulled = 1;
-    }
-    PF_MARK( 3 );
-    /* `in` drained: send the open batch if a slot can take it (all of it at the end) */
-    int flushed = 0;
-    if( !pulled && vt->open && vt->open->txn_cnt &&
-        ( eos || slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<slot_cnt ) ) {
-      fd_ed25519_hip_vtile_flush( vt, eos );
-      flushed = 1;
-    }
-    idle = !pulled && !published && !flushed;
-    if( idle ) {
-      spin_pause();
-#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
-      pf_idle++;
-#endif
-    }
-    PF_MARK( 4 );
-#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
-    pf_pass++;
-#endif
   }
-#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
-  fprintf( stderr, "vservice profile: %lu txns, %llu passes (%llu idle); cycles per txn: status %.0f publish %.0f "
-           "poll %.0f consume+frag %.0f (of which consume %.0f, waits on the GPU %.0f in %llu waits) flush+pause %.0f; "
-           "resolve (any section) %.0f\n",
-           txns, pf_pass, pf_idle,
-           (double)pf_t[0]/(double)(txns+1UL), (double)pf_t[1]/(double)(txns+1UL), (double)pf_t[2]/(double)(txns+1UL),
-           (double)pf_t[3]/(double)(txns+1UL), (double)pf_cons/(double)(txns+1UL),
-           (double)vt_wait_cycles/(double)(txns+1UL), vt_blocks, (double)pf_t[4]/(double)(txns+1UL),
-           (double)vt_resolve_cycles/(double)(txns+1UL) );
-#endif
-  while( fd_ed25519_hip_shlink_publish( out, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
-    if( (rc = vsvc_check( &L, &local )) ) goto fail;
+  PF_MARK( 0 );
+  /* completed batches resolve (in frag order); their verdicts go out as
+     far as credits allow: the verdict byte, then (SUCCESS) the trailer of
+     the frag the tile publishes (its fd_txn_t and payload_sz, from the
+     vtile's arena: the tile has the payload) */
+  while( vt_drain_one( vt, 0 ) ) {}
+  PF_MARK( 2 );
+  int published = 0;
+  for( vrec_t const * r; (r = vt_head( vt )); ) {
+    unsigned char * dst = fd_ed25519_hip_shlink_prepare( S->L.out );
+    if( !dst ) break;
+    unsigned long tsz = r->verdict==FD_ED25519_HIP_TXN_VERIFY_SUCCESS ? r->frag_sz : 0UL;
+    dst[ 0 ] = (unsigned char)r->verdict;
+    if( tsz ) memcpy( dst + 1, vt->oa + r->arena_off, tsz );
+    if( (rc = fd_ed25519_hip_shlink_commit( S->L.out, 1UL + tsz, r->cookie, 0U )) ) { vsvc_end( S, rc, 0 ); return; }
+    vt_pop( vt );
+    published = 1;
+  }
+  PF_MARK( 1 );
+  if( (rc = fd_ed25519_hip_vtile_error( vt )) ) {
+    /* a wait the idle hook ended is the hook's cause; any other vtile error the device's */
+    vsvc_end( S, rc, rc==S->L.hook_rc ? S->L.hook_local : 0 );
+    return;
+  }
+  if( S->eos && !fd_ed25519_hip_vtile_pending( vt ) ) {
+    /* every frag answered: the EOS frag when the verdict link has credit */
+    int r = fd_ed25519_hip_shlink_publish( S->L.out, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS );
+    if( !r ) { vsvc_end( S, FD_ED25519_HIP_OK, 1 ); return; }
+    if( r!=1 ) { vsvc_end( S, r, 0 ); return; }
+    S->idle = 1;
     spin_pause();
+    return;
   }
-  goto done;
-fail:
-  fd_ed25519_hip_shlink_fail( in, rc );
-  fd_ed25519_hip_shlink_fail( out, rc );
-  if( stop && !local ) atomic_store_explicit( stop, 1, memory_order_release );
-  if( ready ) atomic_fetch_add_explicit( ready, 1U, memory_order_release );   /* failed before it was ready */
-done:
-  if( stats ) {
-    stats->txn_cnt      = txns;
-    stats->batches      = vt->pipe->seq;
-    stats->seconds      = now_s() - ( txns ? t_first : t0 );
-    stats->device_bytes = fd_ed25519_hip_vtile_device_bytes( vt );
-    stats->shared_device_bytes = fd_ed25519_hip_shared_device_bytes( device );
-    stats->end_code     = rc;
+  /* after_frag for every frag that is ready and fits without a wait */
+  int pulled = 0;
+  while( !S->eos && vt->zero_copy && vt_room( vt ) ) {   /* in place: the payload stays in the link's room */
+    unsigned long sz = 0UL, sig = 0UL;
+    unsigned int ctl = 0U;
+    int perr;
+    unsigned char const * src = fd_ed25519_hip_shlink_peek( S->L.in, &sz, &sig, &ctl, &perr );
+    if( !src ) {
+      if( perr==1 ) break;
+      vsvc_end( S, FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL, 1 );   /* overrun, or a line out of bounds */
+      return;
+    }
+    if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { fd_ed25519_hip_shlink_advance( S->L.in ); S->eos = 1; break; }
+    if( !S->txns ) S->t_first = now_s();
+    int r = vt_frag_zc( vt, src, sz, sig );
+    if( r<0 ) { vsvc_end( S, r, r==S->L.hook_rc ? S->L.hook_local : 0 ); return; }
+    /* the credit goes back now: the room itself is reused only after its
+       verdict (the tile's bound on unanswered frags) */
+    if( fd_ed25519_hip_shlink_advance( S->L.in ) ) { vsvc_end( S, FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL, 1 ); return; }
+    S->txns++;
+    pulled = 1;
   }
-  free( buf );
-  vt->idle = NULL;   /* the delete below may wait for batches in flight */
-  fd_ed25519_hip_vtile_delete( vt );
-  if( reg ) hipHostUnregister( reg );   /* after the batches that read from it */
-  return rc;
+  while( !S->eos && !vt->zero_copy && vt_room( vt ) ) {
+    unsigned long sz = 0UL, sig = 0UL;
+    unsigned int ctl = 0U;
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+    unsigned long long c0 = __rdtsc();
+#endif
+    /* copied out of the shared dcache first: the tile is not trusted not
+       to change it meanwhile */
+    int r = fd_ed25519_hip_shlink_consume( S->L.in, S->buf, &sz, &sig, &ctl );
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+    S->pf_cons += __rdtsc() - c0;
+#endif
+    if( r==1 ) break;
+    if( r ) { vsvc_end( S, FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL, 1 ); return; }   /* overrun: the tile ignored credits */
+    if( ctl & FD_ED25519_HIP_SHLINK_CTL_EOS ) { S->eos = 1; break; }
+    if( !S->txns ) S->t_first = now_s();
+    r = fd_ed25519_hip_vtile_frag( vt, S->buf, sz, sig );
+    if( r<0 ) { vsvc_end( S, r, r==S->L.hook_rc ? S->L.hook_local : 0 ); return; }
+    S->txns++;
+    pulled = 1;
+  }
+  PF_MARK( 3 );
+  /* `in` drained (or the vtile full): send the open batch if a slot can
+     take it (all of it at the end) */
+  int flushed = 0;
+  if( !pulled && vt->open && vt->open->txn_cnt &&
+      ( S->eos || S->slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<S->slot_cnt ) ) {
+    fd_ed25519_hip_vtile_flush( vt, S->eos );
+    flushed = 1;
+  }
+  S->idle = !pulled && !published && !flushed;
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  S->pf_idle += (unsigned long long)S->idle;
+  S->pf_pass++;
+#endif
+  PF_MARK( 4 );
 }
-
-int
-fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
-                             fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
-                             fd_ed25519_hip_vservice_stats_t * stats ) {
-  return vservice_loop( device, slot_cnt, batch_sigs, flags, in, out, stats, NULL, NULL, NULL );
-}
+#undef PF_MARK
 
 typedef struct {
-  int                                    device, flags, rc;
-  unsigned                               slot_cnt;
+  int                                    device, flags;
+  unsigned                               slot_cnt, k0, k1;   /* the thread serves link pairs [k0, k1) */
   unsigned long                          batch_sigs;
-  fd_ed25519_hip_shlink_t *              in;
-  fd_ed25519_hip_shlink_t *              out;
-  fd_ed25519_hip_vservice_stats_t        st;
+  fd_ed25519_hip_shlink_t * const *      in;
+  fd_ed25519_hip_shlink_t * const *      out;
+  vsvc_t *                               pair;      /* [link_cnt], this thread's [k0, k1) */
+  fd_ed25519_hip_vservice_stats_t *      st;        /* [link_cnt] */
   _Atomic int *                          stop;
   fd_ed25519_hip_vservice_opts_t const * opts;
-  _Atomic unsigned *                     ready;    /* link threads that are ready to serve (or failed) */
-  char                                   errmsg[ 256 ];   /* the link thread's last_error (it is per thread) */
+  _Atomic unsigned *                     ready;     /* link pairs that are ready to serve (or ended) */
 } vservice_job_t;
 
 static void *
 vservice_main( void * arg ) {
   vservice_job_t * j = (vservice_job_t *)arg;
-  j->rc = vservice_loop( j->device, j->slot_cnt, j->batch_sigs, j->flags, j->in, j->out, &j->st, j->stop, j->opts,
-                         j->ready );
-  if( j->rc ) snprintf( j->errmsg, sizeof(j->errmsg), "%s", fd_ed25519_hip_last_error() );
+  for( unsigned k=j->k0; k<j->k1; k++ ) {
+    vsvc_open( &j->pair[ k ], j->device, j->slot_cnt, j->batch_sigs, j->flags, j->in[ k ], j->out[ k ], &j->st[ k ],
+               j->stop, j->opts );
+    atomic_fetch_add_explicit( j->ready, 1U, memory_order_release );   /* ready (or ended): counted once */
+  }
+  for( int live=1; live; ) {
+    live = 0;
+    int busy = 0;
+    for( unsigned k=j->k0; k<j->k1; k++ ) {
+      vsvc_t * S = &j->pair[ k ];
+      if( !S->live ) continue;
+      vsvc_pass( S );
+      live |= S->live;
+      busy |= S->live && !S->idle;
+    }
+    if( !busy ) spin_pause();
+  }
   return NULL;
 }
 
@@ -1835,52 +1903,66 @@ fd_ed25519_hip_vservice_serve( int device, unsigned slot_cnt, unsigned long batc
                                unsigned link_cnt, fd_ed25519_hip_vservice_stats_t * stats,
                                fd_ed25519_hip_vservice_opts_t const * opts ) {
   if( !link_cnt || link_cnt>FD_ED25519_HIP_VSERVICE_LINK_MAX || !in || !out ) return FD_ED25519_HIP_ERR_INVAL;
-  vservice_job_t * job = (vservice_job_t *)calloc( link_cnt, sizeof(vservice_job_t) );
-  pthread_t *      th  = (pthread_t *)calloc( link_cnt, sizeof(pthread_t) );
-  if( !job || !th ) { free( job ); free( th ); return FD_ED25519_HIP_ERR_NOMEM; }
+  unsigned per = opts && opts->links_per_thread ? opts->links_per_thread : 1U;
+  if( per>link_cnt ) per = link_cnt;
+  unsigned thread_cnt = ( link_cnt + per - 1U ) / per;
+  vservice_job_t *                  job  = (vservice_job_t *)calloc( thread_cnt, sizeof(vservice_job_t) );
+  pthread_t *                       th   = (pthread_t *)calloc( thread_cnt, sizeof(pthread_t) );
+  vsvc_t *                          pair = (vsvc_t *)calloc( link_cnt, sizeof(vsvc_t) );
+  fd_ed25519_hip_vservice_stats_t * st   = (fd_ed25519_hip_vservice_stats_t *)calloc( link_cnt, sizeof(*st) );
+  if( !job || !th || !pair || !st ) { free( job ); free( th ); free( pair ); free( st ); return FD_ED25519_HIP_ERR_NOMEM; }
   _Atomic int stop = 0;
   _Atomic unsigned ready = 0U;
   unsigned started = 0U;
   int rc = FD_ED25519_HIP_OK;
-  for( unsigned k=0U; k<link_cnt; k++ ) {
-    vservice_job_t * j = &job[ k ];
+  for( unsigned t=0U; t<thread_cnt; t++ ) {
+    vservice_job_t * j = &job[ t ];
     j->device = device; j->flags = flags; j->slot_cnt = slot_cnt; j->batch_sigs = batch_sigs;
-    j->in = in[ k ]; j->out = out[ k ]; j->stop = &stop; j->opts = opts; j->ready = &ready;
-    if( pthread_create( &th[ k ], NULL, vservice_main, j ) ) {
+    j->k0 = t*per; j->k1 = j->k0 + per<link_cnt ? j->k0 + per : link_cnt;
+    j->in = in; j->out = out; j->pair = pair; j->st = st; j->stop = &stop; j->opts = opts; j->ready = &ready;
+    if( pthread_create( &th[ t ], NULL, vservice_main, j ) ) {
       rc = FD_ED25519_HIP_ERR_NOMEM;
       atomic_store_explicit( &stop, 1, memory_order_release );
-      for( unsigned m=k; m<link_cnt; m++ ) {
+      for( unsigned m=j->k0; m<link_cnt; m++ ) {
         fd_ed25519_hip_shlink_fail( in[ m ], rc ); fd_ed25519_hip_shlink_fail( out[ m ], rc );
-        job[ m ].st.end_code = rc;
+        st[ m ].end_code = rc;
       }
       break;
     }
     started++;
   }
-  /* every link thread has built its engines and launched every kernel once */
-  if( started==link_cnt ) {
+  /* every link pair has built its engines and launched every kernel once */
+  if( started==thread_cnt ) {
     while( atomic_load_explicit( &ready, memory_order_acquire )<link_cnt ) {
       struct timespec ts = { 0, 1000000L };
       nanosleep( &ts, NULL );
     }
     if( opts && opts->ready ) opts->ready( opts->ready_ctx );
   }
+  for( unsigned t=0U; t<started; t++ ) pthread_join( th[ t ], NULL );
   /* the result: a device-wide failure's code first, else the first
      link-local end, else OK (every link ended with EOS) */
   int local_rc = FD_ED25519_HIP_OK;
   int msg_k = -1;
-  for( unsigned k=0U; k<started; k++ ) {
-    pthread_join( th[ k ], NULL );
-    int r = job[ k ].rc;
+  unsigned served = started==thread_cnt ? link_cnt : started*per;
+  for( unsigned k=0U; k<served; k++ ) {
+    int r = st[ k ].end_code;
     if( vsvc_code_is_device( r ) ) { if( !vsvc_code_is_device( rc ) ) { rc = r; msg_k = (int)k; } }
     else if( r && !local_rc ) local_rc = r;
   }
   if( !rc ) rc = local_rc;
-  /* the failing link thread's message, for the caller's fd_ed25519_hip_last_error */
-  if( msg_k>=0 && job[ msg_k ].errmsg[0] ) fd_ed25519_hip_private_set_error( job[ msg_k ].errmsg );
-  if( stats ) for( unsigned k=0U; k<link_cnt; k++ ) stats[ k ] = job[ k ].st;
-  free( job ); free( th );
+  /* the failing pair's message, for the caller's fd_ed25519_hip_last_error */
+  if( msg_k>=0 && pair[ msg_k ].errmsg[0] ) fd_ed25519_hip_private_set_error( pair[ msg_k ].errmsg );
+  if( stats ) for( unsigned k=0U; k<link_cnt; k++ ) stats[ k ] = st[ k ];
+  free( job ); free( th ); free( pair ); free( st );
   return rc;
+}
+
+int
+fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_sigs, int flags,
+                             fd_ed25519_hip_shlink_t * in, fd_ed25519_hip_shlink_t * out,
+                             fd_ed25519_hip_vservice_stats_t * stats ) {
+  return fd_ed25519_hip_vservice_serve( device, slot_cnt, batch_sigs, flags, &in, &out, 1U, stats, NULL );
 }
 
 int

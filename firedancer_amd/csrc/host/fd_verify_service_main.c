@@ -10,7 +10,7 @@
 
      fd_verify_hip_service --prefix NAME --tiles K [--gpu G] [--depth D]
                            [--slots S] [--batch B] [--gpu-parse | --zero-copy] [--codes portable|avx512]
-                           [--tile-stale-ms T] [--gpu-hang-ms H] [--no-parent-watch]
+                           [--tile-stale-ms T] [--gpu-hang-ms H] [--no-parent-watch] [--links-per-thread L]
 
    creates, for k in [0,K), the links NAME<k>_txn (tile -> service) and
    NAME<k>_vd (service -> tile), each of D lines (default 16384), prints
@@ -36,6 +36,11 @@
    the payloads are DMA'd from the txn links' rooms as they lie (the links
    page-locked with the GPU, FD_ED25519_HIP_VSERVICE_ZERO_COPY): the host
    reads two bytes per transaction and copies none.
+
+   --links-per-thread L: one service thread serves L tiles' link pairs in
+   turn (default 1, a thread per tile); a pass over a pair never waits for
+   the GPU, so the pairs of a thread do not hold each other up, and a
+   service whose threads would mostly spin idle takes fewer cores.
 
    Exit status: 0 every tile ended its stream (EOS); 1 bad arguments, or a
    link name a live process already holds; 2 the device failed (GPU,
@@ -99,14 +104,14 @@ static void
 usage( char const * argv0 ) {
   fprintf( stderr, "usage: %s --prefix NAME --tiles K [--gpu G] [--depth D] [--slots S] [--batch B] "
                    "[--gpu-parse | --zero-copy] [--codes portable|avx512] [--tile-stale-ms T] [--gpu-hang-ms H] "
-                   "[--no-parent-watch]\n", argv0 );
+                   "[--no-parent-watch] [--links-per-thread L]\n", argv0 );
 }
 
 int
 main( int argc, char ** argv ) {
   g_parent = getppid();
   char const *  prefix = NULL;
-  unsigned      tiles  = 0U, slots = 3U;
+  unsigned      tiles  = 0U, slots = 3U, per_thread = 1U;
   int           gpu    = 0, flags = 0, parent_watch_on = 1;
   unsigned long depth  = 16384UL, batch = 4096UL;
   long          stale_ms = 0L, hang_ms = 0L;
@@ -122,6 +127,7 @@ main( int argc, char ** argv ) {
     else if( !strcmp( a, "--tile-stale-ms" ) && v ) { stale_ms = strtol( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--gpu-hang-ms" ) && v ) { hang_ms = strtol( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--no-parent-watch" ) ) { parent_watch_on = 0; }
+    else if( !strcmp( a, "--links-per-thread" ) && v ) { per_thread = (unsigned)strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--gpu-parse" ) )   { flags |= FD_ED25519_HIP_VTILE_GPU_PARSE; }
     else if( !strcmp( a, "--zero-copy" ) )   { flags |= FD_ED25519_HIP_VTILE_GPU_PARSE | FD_ED25519_HIP_VSERVICE_ZERO_COPY; }
     else if( !strcmp( a, "--codes" ) && v ) {
@@ -187,6 +193,7 @@ main( int argc, char ** argv ) {
     opts.gpu_hang_ns   = hang_ms>0L ? hang_ms*1000000L : 0L;
     opts.ready         = announce_ready;
     opts.ready_ctx     = &tiles;
+    opts.links_per_thread = per_thread;
     int err = fd_ed25519_hip_vservice_serve( gpu, slots, batch, flags, in, out, tiles, st, &opts );
     /* one JSON line for tools and tests: per-tile device memory, how each
        link ended, and the base tables this one process holds for all */

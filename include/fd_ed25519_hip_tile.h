@@ -512,9 +512,11 @@ fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_
 /* One service process for several verify tiles of a GPU (the reference
    runs verify_tile_count tiles, src/app/fdctl/config/default.toml:535):
    link_cnt (1..FD_ED25519_HIP_VSERVICE_LINK_MAX) link pairs, each served as
-   by vservice_run on a thread of its own with its own vtile (engines,
+   by vservice_run with its own vtile (engines,
    streams, tcache), all sharing the device's base tables -- one copy of the
-   4 GiB per GPU instead of one per tile process.  Returns when every link
+   4 GiB per GPU instead of one per tile process; a thread per pair, or
+   several pairs per thread (fd_ed25519_hip_vservice_serve's
+   links_per_thread).  Returns when every link
    pair has ended (EOS), or on the first failure, which stops the others
    (their links marked FD_ED25519_HIP_SHLINK_FAIL_STOPPED); stats[k] per
    pair (optional).
@@ -581,6 +583,12 @@ typedef struct {
      first frags wait for the device's set-up (NULL: none) */
   void              (* ready)( void * ctx );
   void *               ready_ctx;
+  /* link pairs one service thread serves (0: 1, a thread per tile).  A
+     thread passes over its pairs in turn and never waits for the GPU on
+     one pair while another has frags, so several tiles per thread cost
+     the service fewer cores where its threads would otherwise spin idle
+     (ABI 6) */
+  unsigned             links_per_thread;
 } fd_ed25519_hip_vservice_opts_t;
 
 int

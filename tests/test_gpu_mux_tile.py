@@ -86,14 +86,18 @@ def test_gpu_service_tile_matches_reference_tile(stream, reference_runs, tmp_pat
     assert_same_frags(reference_runs[(1, 0)], parse_out(out))
 
 
-def test_gpu_service_three_tiles_one_process(stream, reference_runs, tmp_path):
-    """Three verify tiles (seq % 3) on one zero-copy service process: each
-    publishes what the reference tile at its position does; the device's base tables
-    (2 x 2 GiB) exist once in that process, and each further tile costs its
-    own pipe only (batch-sized lane tables: well under 1 GiB)."""
+@pytest.mark.parametrize("mode", [["--zero-copy"], ["--zero-copy", "--links-per-thread", "3"],
+                                  ["--links-per-thread", "2"]],
+                         ids=["zero-copy", "zero-copy-one-thread", "host-parse-two-per-thread"])
+def test_gpu_service_three_tiles_one_process(stream, reference_runs, tmp_path, mode):
+    """Three verify tiles (seq % 3) on one service process (a thread per
+    tile, or several tiles per thread): each publishes what the reference
+    tile at its position does; the device's base tables (2 x 2 GiB) exist
+    once in that process, and each further tile costs its own pipe only
+    (batch-sized lane tables: well under 1 GiB)."""
     path, _ = stream
     app = uuid.uuid4().hex[:10]
-    svc = start_service(app, 3, "--batch", "512", "--zero-copy")
+    svc = start_service(app, 3, "--batch", "512", *mode)
     try:
         procs = [(k, run_harness("verify_hip", path, str(tmp_path / f"hip{k}.bin"), app=app, rr=(3, k), timeout=100))
                  for k in range(3)]
@@ -123,15 +127,17 @@ def _vram_used():
         return None
 
 
-def test_gpu_service_tile_failure_ends_its_link_only(stream):
+@pytest.mark.parametrize("per_thread", ["1", "2"], ids=["thread-per-tile", "one-thread"])
+def test_gpu_service_tile_failure_ends_its_link_only(stream, per_thread):
     """Failure domains: tile 0 marks its txn link failed (as a tile does
     when the service broke the frag protocol); the service ends that link
     pair only and keeps serving tile 1, whose transactions still get their
-    verdicts; at the end it exits 3 with end codes [PROTOCOL, 0].  (A
-    device failure still ends every link: test_gpu_service_fault.py.)"""
+    verdicts -- also when one service thread serves both; at the end it
+    exits 3 with end codes [PROTOCOL, 0].  (A device failure still ends
+    every link: test_gpu_service_fault.py.)"""
     _, frags = stream
     app = uuid.uuid4().hex[:10]
-    svc = start_service(app, 2, "--batch", "256")
+    svc = start_service(app, 2, "--batch", "256", "--links-per-thread", per_thread)
     links = []
     try:
         txl0, vdl0 = tile.ShLink(f"/fd_vhip_{app}_0_txn"), tile.ShLink(f"/fd_vhip_{app}_0_vd")

@@ -23,7 +23,8 @@ pytestmark = pytest.mark.gpu
 FAULT_LIB = os.path.join(REPO, "firedancer_amd", "_lib", "libfd_ed25519_hip_faultinj.so")
 
 
-def test_service_marks_links_failed_on_launch_failure(tmp_path):
+@pytest.mark.parametrize("per_thread", [1, 2], ids=["thread-per-tile", "one-thread"])
+def test_service_marks_links_failed_on_launch_failure(tmp_path, per_thread):
     if not os.path.exists(FAULT_LIB):
         pytest.fail(f"{FAULT_LIB} not built (make -C firedancer_amd/csrc)")
     from firedancer_amd import ed25519, tile, workload
@@ -42,10 +43,10 @@ def test_service_marks_links_failed_on_launch_failure(tmp_path):
     code = ("import sys; sys.path.insert(0, %r); from firedancer_amd import ed25519, tile; "
             "assert ed25519.LIB_PATH.endswith('libfd_ed25519_hip_faultinj.so'); "
             "a, b = tile.ShLink(%r), tile.ShLink(%r); c, d = tile.ShLink(%r), tile.ShLink(%r); "
-            "rc, st = tile.vservice_serve([a, c], [b, d], batch_sigs=256, slot_cnt=3, gpu_parse=False); "
+            "rc, st = tile.vservice_serve([a, c], [b, d], batch_sigs=256, slot_cnt=3, gpu_parse=False, links_per_thread=%d); "
             "print(rc, [s['end_code'] for s in st]); "
             "print(tile._lib.fd_ed25519_hip_last_error().decode(), file=sys.stderr); sys.exit(1 if rc else 0)"
-            % (REPO, txl.name, vdl.name, tx2.name, vd2.name))
+            % (REPO, txl.name, vdl.name, tx2.name, vd2.name, per_thread))
     env = dict(os.environ, FD_ED25519_HIP_LIB=FAULT_LIB)
     t0 = time.time()
     svc = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)

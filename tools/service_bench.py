@@ -12,6 +12,7 @@ the aggregate is all tiles' transactions over the longest stream time (the
 producers start together).  Verdicts are checked (all SUCCESS).
 
     python tools/service_bench.py [--tiles 1,2,4,6] [--txns 1000000] [--batch 4096] [--gpu-parse | --zero-copy]
+                                  [--links-per-thread L]
 """
 import argparse
 import json
@@ -50,6 +51,7 @@ def main():
     ap.add_argument("--slots", type=int, default=3)
     ap.add_argument("--gpu-parse", action="store_true")
     ap.add_argument("--zero-copy", action="store_true", help="the service DMAs payloads from the txn links in place")
+    ap.add_argument("--links-per-thread", type=int, default=1, help="tiles one service thread serves")
     ap.add_argument("--hw-queues", type=int, default=16, help="GPU_MAX_HW_QUEUES of the service process")
     ap.add_argument("--service", default=SERVICE, help="service binary (an A/B build's)")
     ap.add_argument("--producer", default=PRODUCER, help="tile-side binary (the same A/B build's: the frag protocol)")
@@ -66,8 +68,19 @@ def main():
     q = ctx.Queue()
     p = ctx.Process(target=gen, args=(paths, args.txns, q))
     p.start()
-    node_cpus = q.get(timeout=600)
-    q.get(timeout=600)
+
+    def take():
+        """the generator's next message; fails at once if it died"""
+        import queue
+        for _ in range(600):
+            try:
+                return q.get(timeout=1)
+            except queue.Empty:
+                if not p.is_alive():
+                    raise SystemExit(f"payload generator exited with {p.exitcode}")
+        raise SystemExit("payload generator: no answer in 600 s")
+    node_cpus = take()
+    take()
     p.join(timeout=60)
     pin = None
     if args.pin == "node" and node_cpus:
@@ -80,7 +93,8 @@ def main():
         env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.hw_queues))
         svc = subprocess.Popen([args.service, "--prefix", prefix, "--tiles", str(k), "--batch", str(args.batch),
                                 "--slots", str(args.slots), *(["--gpu-parse"] if args.gpu_parse else []),
-                                *(["--zero-copy"] if args.zero_copy else [])],
+                                *(["--zero-copy"] if args.zero_copy else []),
+                                *(["--links-per-thread", str(args.links_per_thread)] if args.links_per_thread != 1 else [])],
                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, preexec_fn=pin)
         line = svc.stdout.readline()
         if not line.startswith("ready"):
@@ -121,6 +135,7 @@ def main():
     for path in paths:
         os.unlink(path)
     print(json.dumps({"service_bench": out, "batch": args.batch, "slots": args.slots, "gpu_parse": args.gpu_parse, "zero_copy": args.zero_copy,
+                      "links_per_thread": args.links_per_thread,
                       "hw_queues": args.hw_queues, "pin": args.pin, "node_cpus": len(node_cpus)}))
 
 
