@@ -125,6 +125,7 @@ struct fd_ed25519_hip_pipe {
   unsigned      in_flight;
   hipEvent_t    h2d_tail;    /* ev_h2d of the last batch submitted (one batch on the link at a time, as the pool) */
   int           err;         /* sticky: a batch failed on the GPU (FD_ED25519_HIP_ERR_HIP - hipError_t) */
+  int           warming;     /* vt_warm's dummy batches (not the stream's) */
   pipe_slot_t   slot[ PIPE_SLOT_MAX ];
 };
 
@@ -335,9 +336,9 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   int err = slot_h2d( pipe, s, st, sig_cnt, txn_cnt, msg_bytes );
   if( err ) return err;
 #ifdef FD_ED25519_HIP_HOST_FAULT
-  /* test build only (tests/test_gpu_service_fault.py): the third batch's
-     launch fails after its copies are enqueued */
-  if( slot->seq==2UL ) {
+  /* test build only (tests/test_gpu_service_fault.py): the stream's third
+     batch's launch fails after its copies are enqueued */
+  if( slot->seq==2UL && !pipe->warming ) {
     fd_ed25519_hip_private_set_error( "pipe: injected launch failure (fault-injection build)" );
     return FD_ED25519_HIP_ERR_HIP - (int)hipErrorLaunchFailure;
   }
@@ -1504,6 +1505,7 @@ fd_ed25519_hip_latency_run_tiles( int device, unsigned tile_cnt, unsigned slot_c
 static int
 vt_warm( fd_ed25519_hip_vtile_t * vt ) {
   fd_ed25519_hip_pipe_t * pipe = vt->pipe;
+  pipe->warming = 1;
   for( unsigned k=0U; k<pipe->slot_cnt; k++ ) {
     fd_ed25519_hip_slot_t * s = fd_ed25519_hip_pipe_acquire( pipe );
     if( !s ) return FD_ED25519_HIP_ERR_INVAL;
@@ -1522,8 +1524,20 @@ vt_warm( fd_ed25519_hip_vtile_t * vt ) {
       if( !fd_ed25519_hip_pipe_poll( pipe, 1 ) ) return pipe->err ? pipe->err : FD_ED25519_HIP_ERR_INVAL;
       fd_ed25519_hip_pipe_release( pipe, s );
     }
+    if( vt->zero_copy ) {   /* and the DMA from the caller's page-locked memory, once per slot */
+      s = fd_ed25519_hip_pipe_acquire( pipe );
+      if( !s ) return FD_ED25519_HIP_ERR_INVAL;
+      pipe_slot_t * ps = (pipe_slot_t *)s;
+      ps->ext_src[0] = vt->zc_base; ps->ext_len[0] = 1UL; ps->ext_counts = 1;
+      s->msg_off[0] = 0UL; s->msg_sz[0] = 1U; s->txn_sig_cnt[0] = 0U;
+      err = fd_ed25519_hip_pipe_submit_txns( pipe, s, 1UL, 1UL );
+      if( err ) return err;
+      if( !fd_ed25519_hip_pipe_poll( pipe, 1 ) ) return pipe->err ? pipe->err : FD_ED25519_HIP_ERR_INVAL;
+      fd_ed25519_hip_pipe_release( pipe, s );
+    }
   }
   pipe->seq = 0UL;   /* the stream's batches count from 0 */
+  pipe->warming = 0;
   return FD_ED25519_HIP_OK;
 }
 
