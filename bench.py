@@ -818,7 +818,7 @@ def main():
                          "0 disables")
     ap.add_argument("--deployed-ref-txns", type=int, default=40000,
                     help="the reference tile's runs in the same harness (its CPU baseline)")
-    ap.add_argument("--deployed-mode", default="zero-copy", choices=["zero-copy", "gpu-parse", "host-parse"],
+    ap.add_argument("--deployed-mode", default="host-parse", choices=["zero-copy", "gpu-parse", "host-parse"],
                     help="the GPU service's mode for the deployed C5 leg")
     ap.add_argument("--host-reps", type=int, default=3, help="host-fed stream passes (0 disables)")
     ap.add_argument("--host-copies", type=int, default=4, help="host-fed stream: the set this many times")
