@@ -39,41 +39,12 @@ __device__ static inline uint4 load16_any(const uint8_t* src) {
                     __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
 }
 
-/* One wave per 64 transactions.  The parse is a chain of dependent byte
-   loads (each offset comes from the bytes before it), ~30 per one-signer
-   transaction: from HBM / L2 that chain is the kernel's whole time.  So the
-   wave first copies the byte span its payloads occupy (staged back to back,
-   or the tile's consecutive rooms) into LDS with coalesced 16-byte loads,
-   and every lane parses and gathers from there.  A span larger than the LDS
-   budget (large payloads far apart) is parsed from global memory. */
-#define STAGE_WAVE      64u
-#define STAGE_LDS_BYTES (88u * 1024u)   /* 64 payloads of up to 1232 bytes on 64-byte boundaries */
-
-__global__ void __launch_bounds__(STAGE_WAVE)
+__global__ void __launch_bounds__(256)
 fd_ed25519_txn_stage_kernel(fd_ed25519_txn_stage_params_t p) {
-  __shared__ uint4 lds[STAGE_LDS_BYTES / 16u + 2u];
-  const uint64_t t = (uint64_t)blockIdx.x * STAGE_WAVE + threadIdx.x;
-  const bool live = t < p.ntxn;
-  const uint64_t off = live ? p.pay_off[t] : ~(uint64_t)0;
-  const uint32_t sz = live ? p.pay_sz[t] : 0u;
-  /* the wave's span [lo, hi) */
-  uint64_t lo = off, hi = live ? off + sz : 0u;
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint64_t l2 = __shfl_xor(lo, d, STAGE_WAVE), h2 = __shfl_xor(hi, d, STAGE_WAVE);
-    lo = l2 < lo ? l2 : lo;
-    hi = h2 > hi ? h2 : hi;
-  }
-  lo &= ~(uint64_t)15;
-  const uint64_t span = hi > lo ? hi - lo : 0u;
-  const bool in_lds = span + 16u <= STAGE_LDS_BYTES;   /* load16_any reads up to 16 bytes past a payload */
-  if (in_lds) {
-    const uint4* src = reinterpret_cast<const uint4*>(p.payloads + lo);
-    const uint32_t n16 = (uint32_t)((span + 31u) / 16u);
-    for (uint32_t i = threadIdx.x; i < n16; i += STAGE_WAVE) lds[i] = src[i];
-    __syncthreads();
-  }
-  if (!live) return;
-  const uint8_t* pay = in_lds ? reinterpret_cast<const uint8_t*>(lds) + (off - lo) : p.payloads + off;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.ntxn) return;
+  const uint8_t* pay = p.payloads + p.pay_off[t];
+  const uint32_t sz = p.pay_sz[t];
   fd_ed25519_hip_txn_t tx;
   const int good = fd_txn_core_parse(pay, sz, &tx, p.trailer ? p.trailer + 64 * t : nullptr, 64) != 0;
   p.parse_ok[t] = (uint8_t)good;
@@ -91,7 +62,7 @@ fd_ed25519_txn_stage_kernel(fd_ed25519_txn_stage_params_t p) {
       for (int q = 0; q < 4; q++) sg[q] = load16_any(s + 16 * q);
       pk[0] = load16_any(a);
       pk[1] = load16_any(a + 16);
-      p.msg_off[k] = off + tx.message_off;
+      p.msg_off[k] = p.pay_off[t] + tx.message_off;
       p.msg_sz[k] = sz - tx.message_off;
     } else {
       const uint4 z = make_uint4(0u, 0u, 0u, 0u);
@@ -99,7 +70,7 @@ fd_ed25519_txn_stage_kernel(fd_ed25519_txn_stage_params_t p) {
       for (int q = 0; q < 4; q++) sg[q] = z;
       pk[0] = z;
       pk[1] = z;
-      p.msg_off[k] = off;
+      p.msg_off[k] = p.pay_off[t];
       p.msg_sz[k] = 0u;
     }
   }
@@ -132,8 +103,9 @@ fd_ed25519_txn_finish_kernel(const int8_t* sig_codes, const uint32_t* txn_first,
 
 extern "C" int fd_ed25519_hip_launch_txn_stage(const fd_ed25519_txn_stage_params_t* p, void* stream) {
   if (!p->ntxn) return 0;
-  hipLaunchKernelGGL(fd_ed25519_txn_stage_kernel, dim3((uint32_t)((p->ntxn + STAGE_WAVE - 1) / STAGE_WAVE)),
-                     dim3(STAGE_WAVE), 0, (hipStream_t)stream, *p);
+  const uint32_t blk = 256;
+  hipLaunchKernelGGL(fd_ed25519_txn_stage_kernel, dim3((uint32_t)((p->ntxn + blk - 1) / blk)), dim3(blk), 0,
+                     (hipStream_t)stream, *p);
   return (int)hipGetLastError();
 }
 
