@@ -869,6 +869,8 @@ vt_resolve( fd_ed25519_hip_vtile_t * vt, fd_ed25519_hip_slot_t * s ) {
 
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
 static __thread unsigned long long vt_wait_cycles, vt_resolve_cycles, vt_blocks;   /* A/B build only */
+static __thread unsigned long long vt_submit_cycles, vt_submits, vt_rtt_n;
+static __thread double             vt_rtt_s, vt_rtt_max_s;
 #endif
 
 static int
@@ -886,6 +888,9 @@ vt_drain_one( fd_ed25519_hip_vtile_t * vt, int wait ) {
     if( fd_ed25519_hip_pipe_error( vt->pipe ) ) vt->err = fd_ed25519_hip_pipe_error( vt->pipe );
     return 0;
   }
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  { double rt = s->t_done - s->t_submit; vt_rtt_s += rt; vt_rtt_n++; if( rt>vt_rtt_max_s ) vt_rtt_max_s = rt; }
+#endif
   vt_resolve( vt, s );
   fd_ed25519_hip_pipe_release( vt->pipe, s );
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
@@ -907,8 +912,14 @@ vt_submit_open( fd_ed25519_hip_vtile_t * vt ) {
     }
     vt->zc_seg = 0;
   }
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  unsigned long long sc0 = __rdtsc();
+#endif
   int err = vt->gpu_parse ? fd_ed25519_hip_pipe_submit_txns( vt->pipe, s, s->txn_cnt, s->msg_bytes )
                           : fd_ed25519_hip_pipe_submit( vt->pipe, s, s->sig_cnt, s->msg_bytes, s->txn_cnt );
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  vt_submit_cycles += __rdtsc() - sc0; vt_submits++;
+#endif
   if( err ) {   /* a launch failed: the batch's transactions have no verdicts, and the vtile stops */
     vt->err = err;
     return 0;
@@ -1686,9 +1697,12 @@ vsvc_end( vsvc_t * S, int rc, int local ) {
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
   double d = (double)( S->txns + 1UL );
   fprintf( stderr, "vservice profile: %lu txns, %llu passes (%llu idle); cycles per txn: status %.0f publish %.0f "
-           "poll %.0f consume+frag %.0f (of which consume %.0f) flush+pause %.0f\n",
+           "poll %.0f consume+frag %.0f (of which consume %.0f) flush+pause %.0f; %llu batches: submit %.0f cycles each, "
+           "round trip avg %.3f ms max %.3f ms\n",
            S->txns, S->pf_pass, S->pf_idle, (double)S->pf_t[0]/d, (double)S->pf_t[1]/d, (double)S->pf_t[2]/d,
-           (double)S->pf_t[3]/d, (double)S->pf_cons/d, (double)S->pf_t[4]/d );
+           (double)S->pf_t[3]/d, (double)S->pf_cons/d, (double)S->pf_t[4]/d, vt_submits,
+           (double)vt_submit_cycles/(double)( vt_submits + 1ULL ), 1e3*vt_rtt_s/(double)( vt_rtt_n + 1ULL ),
+           1e3*vt_rtt_max_s );
 #endif
   free( S->buf ); S->buf = NULL;
   if( S->vt ) {

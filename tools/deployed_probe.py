@@ -32,10 +32,12 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--slow-ms", type=float, default=5.0)
+    ap.add_argument("--service", default=os.path.join(REPO, "firedancer_amd", "_lib", "fd_verify_hip_service"),
+                    help="service binary (an A/B build's; its stderr profile lines are printed)")
     args = ap.parse_args()
     from firedancer_amd import ed25519, tile, workload
     mux = os.path.join(REPO, "oracle", "_ref", "mux", "mux_harness")
-    svc_bin = os.path.join(REPO, "firedancer_amd", "_lib", "fd_verify_hip_service")
+    svc_bin = args.service
     eng = ed25519.Engine(0, max_chunk=1 << 16)
     pay, _ = workload.txn_payloads(eng, args.txns, 4711, msg_sz=200)
     eng.close()
@@ -60,6 +62,9 @@ def main():
             if p.returncode != 0:
                 raise SystemExit(f"harness rc {p.returncode}: {p.stderr[-500:]}")
             svc.wait(timeout=60)
+            for ln in svc.stderr.read().splitlines():
+                if "profile" in ln:
+                    print(ln, flush=True)
         finally:
             if svc.poll() is None:
                 svc.kill()
