@@ -182,6 +182,24 @@ typedef struct {
 } fd_ed25519_txn_stage_params_t;
 
 int fd_ed25519_hip_launch_txn_stage( fd_ed25519_txn_stage_params_t const * p, void * stream );
+
+/* H2D without the copy engines: one launch in which the device reads up to
+   FD_ED25519_PULL_SPAN_MAX spans of page-locked host memory (device-visible
+   addresses, 16-byte aligned) and writes them to device memory (16-byte
+   aligned), exactly n bytes each.  A launch is asynchronous; a
+   hipMemcpyAsync H2D issued by a thread whose stream shares the device with
+   busy compute streams can hold the calling thread for the copy's
+   duration (measured in the verify service: tools/ubench/h2d_call_probe.hip,
+   DESIGN.md 3c). */
+#define FD_ED25519_PULL_SPAN_MAX 8
+typedef struct {
+  uint8_t const * src[ FD_ED25519_PULL_SPAN_MAX ];
+  uint8_t *       dst[ FD_ED25519_PULL_SPAN_MAX ];
+  uint64_t        n  [ FD_ED25519_PULL_SPAN_MAX ];
+  uint32_t        cnt;
+} fd_ed25519_pull_params_t;
+
+int fd_ed25519_hip_launch_pull( fd_ed25519_pull_params_t const * p, void * stream );
 int fd_ed25519_hip_launch_txn_finish( int8_t const * d_sig_codes, uint32_t const * d_txn_first,
                                       uint32_t const * d_txn_cnt, uint8_t const * d_parse_ok, int8_t * d_txn_out,
                                       uint64_t ntxn, void * stream );

@@ -118,3 +118,32 @@ extern "C" int fd_ed25519_hip_launch_txn_finish(const int8_t* d_sig_codes, const
                      (hipStream_t)stream, d_sig_codes, d_txn_first, d_txn_cnt, d_parse_ok, d_txn_out, ntxn);
   return (int)hipGetLastError();
 }
+
+/* fd_ed25519_hip_launch_pull (fd_ed25519_hip_internal.h): blockIdx.y picks
+   the span, the x blocks stride over its 16-byte words; the last n % 16
+   bytes are copied one by one (never a byte past the span: a span can end
+   at the last byte of a registered mapping). */
+__global__ void __launch_bounds__(256)
+fd_ed25519_pull_kernel(fd_ed25519_pull_params_t p) {
+  const uint32_t k = blockIdx.y;
+  if (k >= p.cnt) return;
+  const uint8_t* src = p.src[k];
+  uint8_t* dst = p.dst[k];
+  const uint64_t n = p.n[k], n16 = n / 16u;
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+    d4[i] = s4[i];
+  if (blockIdx.x == 0 && threadIdx.x < (n & 15u)) dst[16u * n16 + threadIdx.x] = src[16u * n16 + threadIdx.x];
+}
+
+extern "C" int fd_ed25519_hip_launch_pull(const fd_ed25519_pull_params_t* p, void* stream) {
+  if (!p->cnt) return 0;
+  uint64_t most = 0;
+  for (uint32_t k = 0; k < p->cnt; k++) most = p->n[k] > most ? p->n[k] : most;
+  /* ~8 words per thread, at most 256 blocks per span */
+  uint64_t blocks = (most / 16u + 2047u) / 2048u;
+  blocks = blocks < 1u ? 1u : blocks > 256u ? 256u : blocks;
+  hipLaunchKernelGGL(fd_ed25519_pull_kernel, dim3((uint32_t)blocks, p->cnt), dim3(256), 0, (hipStream_t)stream, *p);
+  return (int)hipGetLastError();
+}

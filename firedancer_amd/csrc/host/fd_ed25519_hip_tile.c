@@ -72,6 +72,21 @@ fd_ed25519_hip_abi_check( unsigned version, unsigned long slot_sz, unsigned long
 
 #define PIPE_SLOT_MAX 8
 
+/* Staged payloads start on a cache line: a copy into cold lines that
+   starts mid-line costs the host about twice as much (split stores and
+   partial-line fills; the staging ring is megabytes, far out of L2), and
+   the few bytes of padding per payload cost the link nothing that matters. */
+#define STAGE_ALIGN( off ) ( ( (off) + 63UL ) & ~63UL )
+
+
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+/* A/B build only: host cycles inside each part of a batch submit */
+static __thread unsigned long long pf_sub_h2d, pf_sub_launch, pf_sub_d2h, pf_sub_n, pf_sub_wait;
+#define PF_SUB( acc, stmt ) do { unsigned long long c_ = __rdtsc(); stmt; acc += __rdtsc() - c_; } while(0)
+#else
+#define PF_SUB( acc, stmt ) do { stmt; } while(0)
+#endif
+
 #define SLOT_FREE 0
 #define SLOT_FILL 1
 #define SLOT_BUSY 2
@@ -112,8 +127,10 @@ typedef struct {
      link's dcache) instead of the staging block, txn_sig_cnt filled by the
      caller; reset at acquire */
   unsigned char const *     ext_src[ 2 ];
+  unsigned char const *     ext_dev[ 2 ];   /* ... the same spans' device-visible addresses */
   unsigned long             ext_len[ 2 ];
   int                       ext_counts;
+  unsigned char *           h_in_dev;       /* h_in's device-visible address */
 } pipe_slot_t;
 
 struct fd_ed25519_hip_pipe {
@@ -176,6 +193,7 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   TCHK( hipHostMalloc( (void **)&s->h_in,   in_sz,  hipHostMallocDefault ), "hipHostMalloc" );
   TCHK( hipHostMalloc( (void **)&s->h_outb, out_sz, hipHostMallocDefault ), "hipHostMalloc" );
   TCHK( hipMalloc(     (void **)&s->d_in,   in_sz                        ), "hipMalloc" );
+  TCHK( hipHostGetDevicePointer( (void **)&s->h_in_dev, s->h_in, 0U ), "hipHostGetDevicePointer" );
   TCHK( hipMalloc(     (void **)&s->d_outb, out_sz                       ), "hipMalloc" );
   p->sigs        = s->h_in + o_sigs;                   s->d_sigs   = s->d_in + o_sigs;
   p->pubs        = s->h_in + o_pubs;                   s->d_pubs   = s->d_in + o_pubs;
@@ -224,55 +242,82 @@ fd_ed25519_hip_pipe_new( int device, unsigned slot_cnt, unsigned long sig_cap, u
    counts the signature arrays in use, oc_cnt the msg_off/msg_sz entries. */
 #define SLOT_ONE_COPY_SLACK (256UL << 10)
 
-static int slot_h2d_copies( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt,
-                            unsigned long msg_bytes );
+typedef struct {
+  unsigned char const * src;   /* host address (page-locked) */
+  unsigned char const * dev;   /* ... as the device sees it  */
+  unsigned char *       dst;
+  unsigned long         n;
+} h2d_span_t;
 
-/* ... after the previous batch's copies (two batches on the link at once
-   move fewer bytes than one: DESIGN.md 3b); the batch's kernels still
-   overlap the next batch's copy */
-static int
-slot_h2d( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt,
-          unsigned long txn_cnt, unsigned long msg_bytes ) {
-#ifndef FD_ED25519_HIP_AB_POOL_PARALLEL_H2D
-  if( pipe->h2d_tail ) TCHK( hipStreamWaitEvent( st, pipe->h2d_tail, 0U ), "hipStreamWaitEvent(h2d)" );
-#endif
-  int err = slot_h2d_copies( s, st, sig_cnt, txn_cnt, s->ext_src[0] ? 0UL : msg_bytes );
-  if( err ) return err;
-  if( s->ext_src[0] ) {   /* zero-copy payloads: straight from the caller's page-locked spans */
-    TCHK( hipMemcpyAsync( s->d_msgs, s->ext_src[0], s->ext_len[0], hipMemcpyHostToDevice, st ), "H2D span 0" );
-    if( s->ext_len[1] )
-      TCHK( hipMemcpyAsync( s->d_msgs + s->ext_len[0], s->ext_src[1], s->ext_len[1], hipMemcpyHostToDevice, st ),
-            "H2D span 1" );
-  }
-  TCHK( hipEventRecord( s->ev_h2d, st ), "hipEventRecord(h2d)" );
-  pipe->h2d_tail = s->ev_h2d;
-  return FD_ED25519_HIP_OK;
-}
-
-static int
-slot_h2d_copies( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt,
-                 unsigned long msg_bytes ) {
+/* the staging block's spans a batch moves: its prefix whole, or the arrays
+   in use one by one; returns the count (at most 7) */
+static unsigned
+slot_h2d_spans( pipe_slot_t * s, unsigned long sig_cnt, unsigned long txn_cnt, unsigned long msg_bytes,
+                h2d_span_t * sp ) {
   fd_ed25519_hip_slot_t * p = &s->pub;
   unsigned long oc_cnt = sig_cnt > txn_cnt ? sig_cnt : txn_cnt;
   unsigned long used = 96UL*sig_cnt + 12UL*oc_cnt + 8UL*txn_cnt + msg_bytes;
   unsigned long whole = s->in_msgs + msg_bytes;
+  unsigned k = 0U;
+#define SPAN( host, dptr, bytes ) do { sp[ k ].src = (unsigned char const *)(host);                                  \
+                                       sp[ k ].dev = s->h_in_dev + ( (unsigned char const *)(host) - s->h_in );      \
+                                       sp[ k ].dst = (unsigned char *)(dptr); sp[ k ].n = (bytes); k++; } while(0)
   if( whole - used <= SLOT_ONE_COPY_SLACK ) {
-    TCHK( hipMemcpyAsync( s->d_in, s->h_in, whole ? whole : 1UL, hipMemcpyHostToDevice, st ), "H2D batch" );
-    return FD_ED25519_HIP_OK;
+    SPAN( s->h_in, s->d_in, whole ? whole : 1UL );
+    return k;
   }
-  if( msg_bytes ) TCHK( hipMemcpyAsync( s->d_msgs, p->msgs, msg_bytes, hipMemcpyHostToDevice, st ), "H2D msgs" );
+  if( msg_bytes ) SPAN( p->msgs, s->d_msgs, msg_bytes );
   if( oc_cnt ) {
-    TCHK( hipMemcpyAsync( s->d_off, p->msg_off, 8UL*oc_cnt, hipMemcpyHostToDevice, st ), "H2D off" );
-    TCHK( hipMemcpyAsync( s->d_sz,  p->msg_sz,  4UL*oc_cnt, hipMemcpyHostToDevice, st ), "H2D sz" );
+    SPAN( p->msg_off, s->d_off, 8UL*oc_cnt );
+    SPAN( p->msg_sz,  s->d_sz,  4UL*oc_cnt );
   }
   if( sig_cnt ) {
-    TCHK( hipMemcpyAsync( s->d_sigs, p->sigs, 64UL*sig_cnt, hipMemcpyHostToDevice, st ), "H2D sigs" );
-    TCHK( hipMemcpyAsync( s->d_pubs, p->pubs, 32UL*sig_cnt, hipMemcpyHostToDevice, st ), "H2D pubs" );
+    SPAN( p->sigs, s->d_sigs, 64UL*sig_cnt );
+    SPAN( p->pubs, s->d_pubs, 32UL*sig_cnt );
   }
   if( txn_cnt ) {
-    TCHK( hipMemcpyAsync( s->d_tfirst, p->txn_first,   4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tfirst" );
-    TCHK( hipMemcpyAsync( s->d_tcnt,   p->txn_sig_cnt, 4UL*txn_cnt, hipMemcpyHostToDevice, st ), "H2D tcnt" );
+    SPAN( p->txn_first,   s->d_tfirst, 4UL*txn_cnt );
+    SPAN( p->txn_sig_cnt, s->d_tcnt,   4UL*txn_cnt );
   }
+#undef SPAN
+  return k;
+}
+
+/* H2D of a batch after the previous batch's copies (two batches on the
+   link at once move fewer bytes than one: DESIGN.md 3b; the batch's
+   kernels still overlap the next batch's copy): the staging block's spans
+   and, zero-copy, the payload spans from the caller's page-locked memory
+   (the second at a 64-byte boundary after the first). */
+static int
+slot_h2d( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt,
+          unsigned long txn_cnt, unsigned long msg_bytes ) {
+#ifndef FD_ED25519_HIP_AB_POOL_PARALLEL_H2D
+  if( pipe->h2d_tail ) {
+    hipError_t we_;
+    PF_SUB( pf_sub_wait, we_ = hipStreamWaitEvent( st, pipe->h2d_tail, 0U ) );
+    TCHK( we_, "hipStreamWaitEvent(h2d)" );
+  }
+#endif
+  h2d_span_t sp[ 9 ];
+  unsigned k = slot_h2d_spans( s, sig_cnt, txn_cnt, s->ext_src[0] ? 0UL : msg_bytes, sp );
+  for( int g=0; g<2 && s->ext_src[g] && s->ext_len[g]; g++ ) {   /* zero-copy payloads */
+    sp[ k ].src = s->ext_src[g]; sp[ k ].dev = s->ext_dev[g]; sp[ k ].n = s->ext_len[g];
+    sp[ k ].dst = s->d_msgs + ( g ? STAGE_ALIGN( s->ext_len[0] ) : 0UL );
+    k++;
+  }
+#ifdef FD_ED25519_HIP_AB_PULL_H2D
+  fd_ed25519_pull_params_t pp;
+  memset( &pp, 0, sizeof(pp) );
+  for( unsigned i=0U; i<k; i++ ) { pp.src[ i ] = sp[ i ].dev; pp.dst[ i ] = sp[ i ].dst; pp.n[ i ] = sp[ i ].n; }
+  pp.cnt = k;
+  int le = fd_ed25519_hip_launch_pull( &pp, st );
+  if( le ) return tile_fail( "H2D pull launch", (hipError_t)le );
+#else
+  for( unsigned i=0U; i<k; i++ )
+    TCHK( hipMemcpyAsync( sp[ i ].dst, sp[ i ].src, sp[ i ].n, hipMemcpyHostToDevice, st ), "H2D batch" );
+#endif
+  TCHK( hipEventRecord( s->ev_h2d, st ), "hipEventRecord(h2d)" );
+  pipe->h2d_tail = s->ev_h2d;
   return FD_ED25519_HIP_OK;
 }
 
@@ -293,7 +338,8 @@ fd_ed25519_hip_pipe_acquire( fd_ed25519_hip_pipe_t * pipe ) {
   s->state = SLOT_FILL;
   pipe->next_acq++;
   s->pub.sig_cnt = 0UL; s->pub.msg_bytes = 0UL; s->pub.txn_cnt = 0UL;
-  s->ext_src[0] = s->ext_src[1] = NULL; s->ext_len[0] = s->ext_len[1] = 0UL; s->ext_counts = 0;
+  s->ext_src[0] = s->ext_src[1] = NULL; s->ext_dev[0] = s->ext_dev[1] = NULL;
+  s->ext_len[0] = s->ext_len[1] = 0UL; s->ext_counts = 0;
   return &s->pub;
 }
 
@@ -333,7 +379,8 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   slot->sig_cnt = sig_cnt; slot->msg_bytes = msg_bytes; slot->txn_cnt = txn_cnt;
   slot->seq = pipe->seq++;
   slot->t_submit = now_s();
-  int err = slot_h2d( pipe, s, st, sig_cnt, txn_cnt, msg_bytes );
+  int err;
+  PF_SUB( pf_sub_h2d, err = slot_h2d( pipe, s, st, sig_cnt, txn_cnt, msg_bytes ) );
   if( err ) return err;
 #ifdef FD_ED25519_HIP_HOST_FAULT
   /* test build only (tests/test_gpu_service_fault.py): the stream's third
@@ -344,15 +391,20 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   }
 #endif
   if( sig_cnt ) {
-    err = fd_ed25519_hip_verify_dev( s->eng, sig_cnt, s->d_msgs, s->d_off, s->d_sz, s->d_sigs, s->d_pubs, s->d_out, st );
+    PF_SUB( pf_sub_launch, err = fd_ed25519_hip_verify_dev( s->eng, sig_cnt, s->d_msgs, s->d_off, s->d_sz, s->d_sigs,
+                                                             s->d_pubs, s->d_out, st ) );
     if( err ) return err;
   }
   if( txn_cnt ) {
-    err = fd_ed25519_hip_txn_combine_dev( s->eng, txn_cnt, s->d_out, s->d_tfirst, s->d_tcnt, s->d_tout, st );
+    PF_SUB( pf_sub_launch, err = fd_ed25519_hip_txn_combine_dev( s->eng, txn_cnt, s->d_out, s->d_tfirst, s->d_tcnt,
+                                                                 s->d_tout, st ) );
     if( err ) return err;
   }
-  err = slot_d2h( s, st, sig_cnt, txn_cnt, 0 );
+  PF_SUB( pf_sub_d2h, err = slot_d2h( s, st, sig_cnt, txn_cnt, 0 ) );
   if( err ) return err;
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+  pf_sub_n++;
+#endif
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
   s->state = SLOT_BUSY;
   pipe->in_flight++;
@@ -368,7 +420,8 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
   /* signature slots from byte 0 of each payload (its signature count if
      fd_txn_parse accepts it; 0 or > 16 reserve none) */
   unsigned long slots = 0UL;
-  if( s->ext_src[0] && payload_bytes!=s->ext_len[0] + s->ext_len[1] ) return FD_ED25519_HIP_ERR_INVAL;
+  if( s->ext_src[0] && payload_bytes!=( s->ext_len[1] ? STAGE_ALIGN( s->ext_len[0] ) + s->ext_len[1] : s->ext_len[0] ) )
+    return FD_ED25519_HIP_ERR_INVAL;
   for( unsigned long t=0UL; t<txn_cnt; t++ ) {
     if( slot->msg_off[ t ]>payload_bytes || slot->msg_sz[ t ]>payload_bytes - slot->msg_off[ t ] ) {
       fd_ed25519_hip_private_set_error( "pipe_submit_txns: a payload lies outside the staged bytes" );
@@ -390,23 +443,28 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
     /* the per-transaction offsets / sizes travel in msg_off / msg_sz; the
        device writes the per-signature ones (and the signatures and keys)
        into arrays of its own */
-    int err = slot_h2d( pipe, s, st, 0UL, txn_cnt, payload_bytes );
+    int err;
+    PF_SUB( pf_sub_h2d, err = slot_h2d( pipe, s, st, 0UL, txn_cnt, payload_bytes ) );
     if( err ) return err;
     fd_ed25519_txn_stage_params_t sp;
     sp.payloads = s->d_msgs; sp.pay_off = s->d_off; sp.pay_sz = s->d_sz; sp.txn_first = s->d_tfirst;
     sp.txn_cnt = s->d_tcnt; sp.ntxn = txn_cnt; sp.sigs = s->d_sigs; sp.pubs = s->d_pubs; sp.msg_off = s->d_soff;
     sp.msg_sz = s->d_ssz; sp.parse_ok = s->d_pok; sp.trailer = s->d_trailer;
-    err = fd_ed25519_hip_launch_txn_stage( &sp, st );
+    PF_SUB( pf_sub_launch, err = fd_ed25519_hip_launch_txn_stage( &sp, st ) );
     if( err ) return tile_fail( "txn_stage launch", (hipError_t)err );
     if( slots ) {
-      err = fd_ed25519_hip_verify_dev( s->eng, slots, s->d_msgs, s->d_soff, s->d_ssz, s->d_sigs, s->d_pubs, s->d_out,
-                                       st );
+      PF_SUB( pf_sub_launch, err = fd_ed25519_hip_verify_dev( s->eng, slots, s->d_msgs, s->d_soff, s->d_ssz, s->d_sigs,
+                                                               s->d_pubs, s->d_out, st ) );
       if( err ) return err;
     }
-    err = fd_ed25519_hip_launch_txn_finish( s->d_out, s->d_tfirst, s->d_tcnt, s->d_pok, s->d_tout, txn_cnt, st );
+    PF_SUB( pf_sub_launch, err = fd_ed25519_hip_launch_txn_finish( s->d_out, s->d_tfirst, s->d_tcnt, s->d_pok, s->d_tout,
+                                                                   txn_cnt, st ) );
     if( err ) return tile_fail( "txn_finish launch", (hipError_t)err );
-    err = slot_d2h( s, st, slots, txn_cnt, 1 );
+    PF_SUB( pf_sub_d2h, err = slot_d2h( s, st, slots, txn_cnt, 1 ) );
     if( err ) return err;
+#ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
+    pf_sub_n++;
+#endif
   }
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
   s->state = SLOT_BUSY;
@@ -651,6 +709,7 @@ struct fd_ed25519_hip_vtile {
      spans (the dcache is a ring: one wrap per batch at most) */
   int                       zero_copy;
   unsigned char const *     zc_base;
+  unsigned char const *     zc_dev;       /* zc_base as the device sees it */
   unsigned long             zc_size;
   unsigned long             zc_start[ 2 ], zc_end[ 2 ];   /* the open batch's spans, offsets in the dcache */
   int                       zc_seg;                       /* spans in use: 0 (empty), 1 or 2 */
@@ -908,6 +967,7 @@ vt_submit_open( fd_ed25519_hip_vtile_t * vt ) {
     ps->ext_counts = 1;
     for( int g=0; g<vt->zc_seg; g++ ) {
       ps->ext_src[ g ] = vt->zc_base + vt->zc_start[ g ];
+      ps->ext_dev[ g ] = vt->zc_dev  + vt->zc_start[ g ];
       ps->ext_len[ g ] = vt->zc_end[ g ] - vt->zc_start[ g ];
     }
     vt->zc_seg = 0;
@@ -970,12 +1030,6 @@ vt_open( fd_ed25519_hip_vtile_t * vt ) {
   vt->open_seq = vt->pipe->seq;
   return 0;
 }
-
-/* Staged payloads start on a cache line: a copy into cold lines that
-   starts mid-line costs the host about twice as much (split stores and
-   partial-line fills; the staging ring is megabytes, far out of L2), and
-   the few bytes of padding per payload cost the link nothing that matters. */
-#define STAGE_ALIGN( off ) ( ( (off) + 63UL ) & ~63UL )
 
 /* GPU-parse mode: the payload goes to the device as is; the host reads
    only byte 0 (the signature count, to reserve slots) and bytes 1..8 (the
@@ -1050,10 +1104,13 @@ vt_frag_zc( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned
     if( !vt->zc_seg ) seg = 0;
     else if( o>=vt->zc_end[ vt->zc_seg-1 ] && o - vt->zc_end[ vt->zc_seg-1 ]<64UL ) seg = vt->zc_seg-1;   /* the next room */
     else if( vt->zc_seg==1 && e<=vt->zc_start[0] ) seg = 1;                                           /* the ring wrapped */
-    unsigned long grow = seg<0 ? 0UL : !vt->zc_seg ? payload_sz : seg==vt->zc_seg ? payload_sz :
-                         e - vt->zc_end[ seg ];
+    /* the batch's payload bytes with this one: span 0, then span 1 from a
+       64-byte boundary (slot_h2d) */
+    unsigned long need = seg<0 ? 0UL : !vt->zc_seg ? payload_sz : seg==vt->zc_seg ? STAGE_ALIGN( len0 ) + payload_sz :
+                         seg==0 ? e - vt->zc_start[0] : STAGE_ALIGN( len0 ) + ( e - vt->zc_start[1] );
+    (void)len1;
     int fits = seg>=0 && ( !s->txn_cnt || ( s->sig_cnt+nsig<=s->sig_cap && s->txn_cnt+1UL<=s->txn_cap &&
-                                            len0+len1+grow<=s->msg_cap ) );
+                                            need<=s->msg_cap ) );
     if( !fits ) {
       if( pass || !s->txn_cnt ) { vt->err = FD_ED25519_HIP_ERR_INVAL; return vt->err; }
       vt_submit_open( vt );   /* a full batch, or a payload out of ring order: a new batch */
@@ -1061,13 +1118,14 @@ vt_frag_zc( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned
     }
     unsigned long moff;
     if( !vt->zc_seg ) { vt->zc_start[0] = o; vt->zc_end[0] = e; vt->zc_seg = 1; moff = 0UL; }
-    else if( seg==vt->zc_seg ) { vt->zc_start[1] = o; vt->zc_end[1] = e; vt->zc_seg = 2; moff = len0; }
-    else { moff = ( seg ? len0 + ( o - vt->zc_start[1] ) : o - vt->zc_start[0] ); vt->zc_end[ seg ] = e; }
+    else if( seg==vt->zc_seg ) { vt->zc_start[1] = o; vt->zc_end[1] = e; vt->zc_seg = 2; moff = STAGE_ALIGN( len0 ); }
+    else { moff = ( seg ? STAGE_ALIGN( len0 ) + ( o - vt->zc_start[1] ) : o - vt->zc_start[0] ); vt->zc_end[ seg ] = e; }
     unsigned long ti = s->txn_cnt++;
     s->msg_off    [ ti ] = moff;
     s->msg_sz     [ ti ] = (unsigned int)payload_sz;
     s->txn_sig_cnt[ ti ] = (unsigned int)c;
-    s->msg_bytes = ( vt->zc_end[0] - vt->zc_start[0] ) + ( vt->zc_seg==2 ? vt->zc_end[1] - vt->zc_start[1] : 0UL );
+    s->msg_bytes = vt->zc_seg==2 ? STAGE_ALIGN( vt->zc_end[0] - vt->zc_start[0] ) + ( vt->zc_end[1] - vt->zc_start[1] )
+                                 : vt->zc_end[0] - vt->zc_start[0];
     s->sig_cnt  += nsig;
     vrec_t * r = vq_push( vt );
     if( !r ) return vt->err;
@@ -1539,7 +1597,7 @@ vt_warm( fd_ed25519_hip_vtile_t * vt ) {
       s = fd_ed25519_hip_pipe_acquire( pipe );
       if( !s ) return FD_ED25519_HIP_ERR_INVAL;
       pipe_slot_t * ps = (pipe_slot_t *)s;
-      ps->ext_src[0] = vt->zc_base; ps->ext_len[0] = 1UL; ps->ext_counts = 1;
+      ps->ext_src[0] = vt->zc_base; ps->ext_dev[0] = vt->zc_dev; ps->ext_len[0] = 1UL; ps->ext_counts = 1;
       s->msg_off[0] = 0UL; s->msg_sz[0] = 1U; s->txn_sig_cnt[0] = 0U;
       err = fd_ed25519_hip_pipe_submit_txns( pipe, s, 1UL, 1UL );
       if( err ) return err;
@@ -1698,11 +1756,13 @@ vsvc_end( vsvc_t * S, int rc, int local ) {
   double d = (double)( S->txns + 1UL );
   fprintf( stderr, "vservice profile: %lu txns, %llu passes (%llu idle); cycles per txn: status %.0f publish %.0f "
            "poll %.0f consume+frag %.0f (of which consume %.0f) flush+pause %.0f; %llu batches: submit %.0f cycles each, "
-           "round trip avg %.3f ms max %.3f ms\n",
+           "round trip avg %.3f ms max %.3f ms; submit parts per batch: h2d %.0f (wait %.0f) launches %.0f d2h %.0f\n",
            S->txns, S->pf_pass, S->pf_idle, (double)S->pf_t[0]/d, (double)S->pf_t[1]/d, (double)S->pf_t[2]/d,
            (double)S->pf_t[3]/d, (double)S->pf_cons/d, (double)S->pf_t[4]/d, vt_submits,
            (double)vt_submit_cycles/(double)( vt_submits + 1ULL ), 1e3*vt_rtt_s/(double)( vt_rtt_n + 1ULL ),
-           1e3*vt_rtt_max_s );
+           1e3*vt_rtt_max_s, (double)pf_sub_h2d/(double)( pf_sub_n + 1ULL ),
+           (double)pf_sub_wait/(double)( pf_sub_n + 1ULL ), (double)pf_sub_launch/(double)( pf_sub_n + 1ULL ),
+           (double)pf_sub_d2h/(double)( pf_sub_n + 1ULL ) );
 #endif
   free( S->buf ); S->buf = NULL;
   if( S->vt ) {
@@ -1743,12 +1803,16 @@ vsvc_open( vsvc_t * S, int device, unsigned slot_cnt, unsigned long batch_sigs, 
        payloads from the rooms the tile wrote */
     unsigned long map_sz;
     void * m = fd_ed25519_hip_shlink_mapping( in, &map_sz );
-    hipError_t he = hipHostRegister( m, map_sz, hipHostRegisterPortable );
+    hipError_t he = hipHostRegister( m, map_sz, hipHostRegisterPortable | hipHostRegisterMapped );
     if( he!=hipSuccess ) { int rc = tile_fail( "hipHostRegister(txn link)", he ); vsvc_end( S, rc, 0 ); return rc; }
     S->reg = m;
+    void * m_dev = NULL;
+    he = hipHostGetDevicePointer( &m_dev, m, 0U );
+    if( he!=hipSuccess ) { int rc = tile_fail( "hipHostGetDevicePointer(txn link)", he ); vsvc_end( S, rc, 0 ); return rc; }
     vt->zero_copy = 1;
     vt->gpu_parse = 1;
     vt->zc_base   = fd_ed25519_hip_shlink_dcache( in, &vt->zc_size );
+    vt->zc_dev    = (unsigned char const *)m_dev + ( vt->zc_base - (unsigned char const *)m );
   }
   int we = vt_warm( vt );
   if( we ) { vsvc_end( S, we, 0 ); return we; }

@@ -28,7 +28,7 @@ now( void ) {
   return (double)t.tv_sec + 1e-9*(double)t.tv_nsec;
 }
 
-__global__ void empty_kernel( int * p ) { if( p && threadIdx.x==1234 ) p[0] = 1; }
+__global__ void empty_kernel( int * p ) { if( p && blockIdx.x==0 && threadIdx.x<64 ) p[threadIdx.x] = (int)threadIdx.x; }
 
 static void
 copy_calls( char const * kind, unsigned char * src, void * dst, size_t sz, hipStream_t st, int reps ) {
@@ -53,6 +53,7 @@ typedef struct {
   void *          dst;
   size_t          sz;
   int             reps;
+  int             kernels;   /* a launch after each copy */
   double          call_us;
   double          launch_us;
 } th_arg_t;
@@ -69,7 +70,7 @@ th_main( void * a ) {
     double c0 = now();
     CK( hipMemcpyAsync( t->dst, t->src, t->sz, hipMemcpyHostToDevice, st ) );
     double c1 = now();
-    hipLaunchKernelGGL( empty_kernel, dim3( 16 ), dim3( 256 ), 0, st, (int *)NULL );
+    if( t->kernels ) hipLaunchKernelGGL( empty_kernel, dim3( 16 ), dim3( 256 ), 0, st, (int *)NULL );
     double c2 = now();
     call += c1 - c0; launch += c2 - c1;
     if( !(r & 7) ) CK( hipStreamSynchronize( st ) );
@@ -136,23 +137,75 @@ main( void ) {
   fflush( stdout );
 
   /* several threads submitting at once (1 MiB copies + a launch each) */
-  int counts[] = { 1, 4, 8 };
-  for( unsigned c=0; c<3; c++ ) {
-    int n = counts[c];
+  int counts[] = { 1, 4, 8, 1, 8 };
+  for( unsigned c=0; c<5; c++ ) {
+    int n = counts[c], kernels = c<3;
     pthread_t th[ 8 ];
     th_arg_t ta[ 8 ];
     unsigned char * srcs[ 8 ];
     for( int k=0; k<n; k++ ) {
       CK( hipHostMalloc( (void **)&srcs[k], 1UL << 20, hipHostMallocDefault ) );
       memset( srcs[k], k, 1UL << 20 );
-      ta[k].src = srcs[k]; ta[k].dst = (unsigned char *)d + (size_t)k * cap; ta[k].sz = 1UL << 20; ta[k].reps = 256;
+      ta[k].src = srcs[k]; ta[k].dst = (unsigned char *)d + (size_t)k * cap; ta[k].sz = 1UL << 20; ta[k].reps = 256; ta[k].kernels = kernels;
       pthread_create( &th[k], NULL, th_main, &ta[k] );
     }
     double call = 0.0, launch = 0.0;
     for( int k=0; k<n; k++ ) { pthread_join( th[k], NULL ); call += ta[k].call_us; launch += ta[k].launch_us; }
-    printf( "{\"probe\": \"threads\", \"threads\": %d, \"h2d_1MiB_call_us\": %.2f, \"launch_us\": %.2f}\n", n, call/n, launch/n );
+    printf( "{\"probe\": \"threads\", \"threads\": %d, \"kernel_after_each_copy\": %d, \"h2d_1MiB_call_us\": %.2f, "
+            "\"launch_us\": %.2f, \"HSA_ENABLE_SDMA\": \"%s\"}\n", n, kernels, call/n, launch/n,
+            getenv( "HSA_ENABLE_SDMA" ) ? getenv( "HSA_ENABLE_SDMA" ) : "" );
     fflush( stdout );
     for( int k=0; k<n; k++ ) CK( hipHostFree( srcs[k] ) );
+  }
+  /* submit patterns of one batch (1 thread): which call blocks the host */
+  {
+    hipStream_t s1, s2;
+    CK( hipStreamCreateWithFlags( &s1, hipStreamNonBlocking ) );
+    CK( hipStreamCreateWithFlags( &s2, hipStreamNonBlocking ) );
+    hipEvent_t e1, e2;
+    CK( hipEventCreateWithFlags( &e1, hipEventDisableTiming ) );
+    CK( hipEventCreateWithFlags( &e2, hipEventDisableTiming ) );
+    size_t in = 1UL << 20, out = 16UL << 10;
+    for( int pat=0; pat<5; pat++ ) {
+      double t_h2d = 0.0, t_k = 0.0, t_d2h = 0.0;
+      int reps = 128;
+      for( int r=0; r<reps; r++ ) {
+        double c0 = now(), c1, c2, c3;
+        if( pat==0 ) {          /* one stream: H2D, kernel, D2H (the pipe today) */
+          CK( hipMemcpyAsync( d, hm, in, hipMemcpyHostToDevice, s1 ) ); c1 = now();
+          hipLaunchKernelGGL( empty_kernel, dim3( 64 ), dim3( 256 ), 0, s1, (int *)NULL ); c2 = now();
+          CK( hipMemcpyAsync( hm + in, d, out, hipMemcpyDeviceToHost, s1 ) ); c3 = now();
+        } else if( pat==1 ) {   /* copies on s2, kernel on s1, joined by events */
+          CK( hipMemcpyAsync( d, hm, in, hipMemcpyHostToDevice, s2 ) );
+          CK( hipEventRecord( e1, s2 ) ); c1 = now();
+          CK( hipStreamWaitEvent( s1, e1, 0 ) );
+          hipLaunchKernelGGL( empty_kernel, dim3( 64 ), dim3( 256 ), 0, s1, (int *)NULL );
+          CK( hipEventRecord( e2, s1 ) ); c2 = now();
+          CK( hipStreamWaitEvent( s2, e2, 0 ) );
+          CK( hipMemcpyAsync( hm + in, d, out, hipMemcpyDeviceToHost, s2 ) ); c3 = now();
+        } else if( pat==2 ) {   /* H2D on s2, kernel on s1, no D2H (the kernel writes host memory) */
+          CK( hipMemcpyAsync( d, hm, in, hipMemcpyHostToDevice, s2 ) );
+          CK( hipEventRecord( e1, s2 ) ); c1 = now();
+          CK( hipStreamWaitEvent( s1, e1, 0 ) );
+          hipLaunchKernelGGL( empty_kernel, dim3( 64 ), dim3( 256 ), 0, s1, (int *)(hm + in) );
+          CK( hipEventRecord( e2, s1 ) ); c2 = now(); c3 = c2;
+        } else if( pat==3 ) {   /* one stream: H2D, kernel (no D2H) */
+          CK( hipMemcpyAsync( d, hm, in, hipMemcpyHostToDevice, s1 ) ); c1 = now();
+          hipLaunchKernelGGL( empty_kernel, dim3( 64 ), dim3( 256 ), 0, s1, (int *)(hm + in) ); c2 = now(); c3 = c2;
+        } else {                /* one stream: kernel, D2H only */
+          c1 = c0;
+          hipLaunchKernelGGL( empty_kernel, dim3( 64 ), dim3( 256 ), 0, s1, (int *)NULL ); c2 = now();
+          CK( hipMemcpyAsync( hm + in, d, out, hipMemcpyDeviceToHost, s1 ) ); c3 = now();
+        }
+        t_h2d += c1 - c0; t_k += c2 - c1; t_d2h += c3 - c2;
+        if( (r & 3)==3 ) { CK( hipStreamSynchronize( s1 ) ); CK( hipStreamSynchronize( s2 ) ); }
+      }
+      CK( hipStreamSynchronize( s1 ) ); CK( hipStreamSynchronize( s2 ) );
+      printf( "{\"probe\": \"pattern\", \"pattern\": %d, \"h2d_call_us\": %.2f, \"kernel_call_us\": %.2f, "
+              "\"d2h_call_us\": %.2f, \"HSA_ENABLE_SDMA\": \"%s\"}\n", pat, 1e6*t_h2d/reps, 1e6*t_k/reps,
+              1e6*t_d2h/reps, getenv( "HSA_ENABLE_SDMA" ) ? getenv( "HSA_ENABLE_SDMA" ) : "" );
+      fflush( stdout );
+    }
   }
   CK( hipHostUnregister( sm ) );
   CK( hipHostUnregister( rm ) );
