@@ -130,7 +130,8 @@ typedef struct {
   unsigned char const *     ext_dev[ 2 ];   /* ... the same spans' device-visible addresses */
   unsigned long             ext_len[ 2 ];
   int                       ext_counts;
-  unsigned char *           h_in_dev;       /* h_in's device-visible address */
+  unsigned char *           h_in_dev;       /* h_in's device-visible address   */
+  unsigned char *           h_outb_dev;     /* h_outb's device-visible address */
 } pipe_slot_t;
 
 struct fd_ed25519_hip_pipe {
@@ -191,9 +192,10 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   s->out_trl = (sig_cap + tc + 63UL) & ~63UL;
   unsigned long out_sz = s->out_trl + 64UL*tc;
   TCHK( hipHostMalloc( (void **)&s->h_in,   in_sz,  hipHostMallocDefault ), "hipHostMalloc" );
-  TCHK( hipHostMalloc( (void **)&s->h_outb, out_sz, hipHostMallocDefault ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&s->h_outb, out_sz, hipHostMallocCoherent ), "hipHostMalloc" );
   TCHK( hipMalloc(     (void **)&s->d_in,   in_sz                        ), "hipMalloc" );
   TCHK( hipHostGetDevicePointer( (void **)&s->h_in_dev, s->h_in, 0U ), "hipHostGetDevicePointer" );
+  TCHK( hipHostGetDevicePointer( (void **)&s->h_outb_dev, s->h_outb, 0U ), "hipHostGetDevicePointer" );
   TCHK( hipMalloc(     (void **)&s->d_outb, out_sz                       ), "hipMalloc" );
   p->sigs        = s->h_in + o_sigs;                   s->d_sigs   = s->d_in + o_sigs;
   p->pubs        = s->h_in + o_pubs;                   s->d_pubs   = s->d_in + o_pubs;
@@ -305,7 +307,7 @@ slot_h2d( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st, unsigne
     sp[ k ].dst = s->d_msgs + ( g ? STAGE_ALIGN( s->ext_len[0] ) : 0UL );
     k++;
   }
-#ifdef FD_ED25519_HIP_AB_PULL_H2D
+#ifndef FD_ED25519_HIP_AB_COPY_ENGINES
   fd_ed25519_pull_params_t pp;
   memset( &pp, 0, sizeof(pp) );
   for( unsigned i=0U; i<k; i++ ) { pp.src[ i ] = sp[ i ].dev; pp.dst[ i ] = sp[ i ].dst; pp.n[ i ] = sp[ i ].n; }
@@ -323,11 +325,23 @@ slot_h2d( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st, unsigne
 
 /* D2H of the codes: [sig_out | txn_out] in one copy when transactions are
    combined (txn_out sits after sig_cap signature codes), else sig_out;
-   with the device-parsed trailers too (raw mode) */
+   with the device-parsed trailers too (raw mode).  Like the H2D, a launch
+   that writes the page-locked block through its device-visible address,
+   not a copy-engine copy: a hipMemcpyAsync here held the service's link
+   thread for the copy. */
 static int
 slot_d2h( pipe_slot_t * s, hipStream_t st, unsigned long sig_cnt, unsigned long txn_cnt, int trailers ) {
   unsigned long n = trailers ? s->out_trl + 64UL*txn_cnt : (txn_cnt ? s->pub.sig_cap + txn_cnt : sig_cnt);
-  if( n ) TCHK( hipMemcpyAsync( s->h_outb, s->d_outb, n, hipMemcpyDeviceToHost, st ), "D2H codes" );
+  if( !n ) return FD_ED25519_HIP_OK;
+#ifndef FD_ED25519_HIP_AB_COPY_ENGINES
+  fd_ed25519_pull_params_t pp;
+  memset( &pp, 0, sizeof(pp) );
+  pp.src[0] = (unsigned char const *)s->d_outb; pp.dst[0] = s->h_outb_dev; pp.n[0] = n; pp.cnt = 1U;
+  int le = fd_ed25519_hip_launch_pull( &pp, st );
+  if( le ) return tile_fail( "D2H push launch", (hipError_t)le );
+#else
+  TCHK( hipMemcpyAsync( s->h_outb, s->d_outb, n, hipMemcpyDeviceToHost, st ), "D2H codes" );
+#endif
   return FD_ED25519_HIP_OK;
 }
 
