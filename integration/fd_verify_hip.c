@@ -164,6 +164,8 @@ during_housekeeping( void * _ctx ) {
   check_service( ctx );
 }
 
+/* Reference tile plumbing, kept verbatim so the tile sits in the same
+   topology position: src/app/fdctl/run/tiles/fd_verify.c:36-47. */
 static void
 before_frag( void * _ctx,
              ulong  in_idx,
@@ -193,6 +195,7 @@ during_frag( void * _ctx,
 
   fd_verify_hip_ctx_t * ctx = (fd_verify_hip_ctx_t *)_ctx;
 
+  /* verbatim: src/app/fdctl/run/tiles/fd_verify.c:67-68 */
   if( FD_UNLIKELY( chunk<ctx->in[in_idx].chunk0 || chunk>ctx->in[in_idx].wmark || sz>FD_TPU_MTU ) )
     FD_LOG_ERR(( "chunk %lu %lu corrupt, not in range [%lu,%lu]", chunk, sz, ctx->in[in_idx].chunk0, ctx->in[in_idx].wmark ));
 
@@ -364,6 +367,7 @@ unprivileged_init( fd_topo_t *      topo,
   FD_SCRATCH_ALLOC_INIT( l, scratch );
   fd_verify_hip_ctx_t * ctx = FD_SCRATCH_ALLOC_APPEND( l, alignof( fd_verify_hip_ctx_t ), sizeof( fd_verify_hip_ctx_t ) );
 
+  /* in / out link setup verbatim from src/app/fdctl/run/tiles/fd_verify.c:181-200 */
   ctx->round_robin_cnt = fd_topo_tile_name_cnt( topo, tile->name );
   ctx->round_robin_idx = tile->kind_id;
 
@@ -394,11 +398,14 @@ unprivileged_init( fd_topo_t *      topo,
   ctx->hb_last     = fd_ed25519_hip_shlink_heartbeat_query( ctx->vdl );
   ctx->hb_tick     = fd_tickcount();
 
+  /* verbatim: src/app/fdctl/run/tiles/fd_verify.c:202-204 */
   ulong scratch_top = FD_SCRATCH_ALLOC_FINI( l, 1UL );
   if( FD_UNLIKELY( scratch_top > (ulong)scratch + scratch_footprint( tile ) ) )
     FD_LOG_ERR(( "scratch overflow %lu %lu %lu", scratch_top - (ulong)scratch - scratch_footprint( tile ), scratch_top, (ulong)scratch + scratch_footprint( tile ) ));
 }
 
+/* The reference tile's sandbox, unchanged (the tile needs nothing more):
+   verbatim from src/app/fdctl/run/tiles/fd_verify.c:207-228. */
 static ulong
 populate_allowed_seccomp( void *               scratch,
                           ulong                out_cnt,
