@@ -711,11 +711,14 @@ def c4_host_fed(eng, device, info, rank, world, n, index_base, cfg, seed, window
             wl.free()
     pool = tile.Pool([device], batch, slots)
     st = {}
+    calls = [0]
 
     def run(msgs, off, sz, sigs, pubs, out):
         _, sec, s = pool.run(msgs, off, sz, sigs, pubs, out)
-        for k, v in s.items():
-            st[k] = st.get(k, 0) + v
+        calls[0] += 1
+        if calls[0] > 1:   # host_stream's first call is its untimed warm-up pass: not in the byte count
+            for k, v in s.items():
+                st[k] = st.get(k, 0) + v
         return sec
     try:
         res, codes = host_stream(n, sizes, window, C4_CHUNK, fill, run, world, alloc=alloc,
