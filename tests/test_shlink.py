@@ -186,6 +186,41 @@ def test_link_credits_and_overrun_free():
         a.close()
 
 
+def test_credits_come_back_in_groups_and_when_the_link_runs_empty():
+    """Lazy credit exchange (fd_fctl's refill, src/tango/fctl/fd_fctl.h):
+    the consumer publishes its count every depth/16 frags and whenever it
+    finds the link empty; the producer never runs more than depth ahead of
+    the count it last saw, so a credit can arrive late but never early."""
+    name = f"/fdt_lz_{uuid.uuid4().hex[:12]}"
+    depth = 64                                   # credits come back 4 at a time
+    a = tile.ShLink(name, depth, create=True)
+    b = tile.ShLink(name)
+    try:
+        sent = 0
+        while a.publish(b"q", sent):
+            sent += 1
+        assert sent == depth
+        for i in range(3):                        # fewer than depth/16: no credit returned yet
+            assert b.consume()[1] == i
+        assert not a.publish(b"x", 0)
+        assert b.consume()[1] == 3                # the 4th frag: 4 credits come back
+        for _ in range(4):
+            assert a.publish(b"q", sent)
+            sent += 1
+        assert not a.publish(b"x", 0)
+        got = []
+        while (f := b.consume()) is not None:     # drained: the empty poll returns the rest
+            got.append(f[1])
+        assert got == list(range(4, sent))
+        for _ in range(depth):                    # the whole window is free again
+            assert a.publish(b"q", sent)
+            sent += 1
+        assert not a.publish(b"x", 0)
+    finally:
+        b.close()
+        a.close()
+
+
 def test_join_missing_fails():
     with pytest.raises(Exception):
         tile.ShLink(f"/fdt_missing_{uuid.uuid4().hex[:12]}")
