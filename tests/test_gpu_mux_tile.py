@@ -61,13 +61,16 @@ def reference_runs(stream, tmp_path_factory):
     return runs
 
 
-@pytest.mark.parametrize("mode", [[], ["--gpu-parse"], ["--zero-copy"]], ids=["host-parse", "gpu-parse", "zero-copy"])
+@pytest.mark.parametrize("mode", [[], ["--gpu-parse"], ["--zero-copy"], ["--zero-copy", "--depth", "64"]],
+                         ids=["host-parse", "gpu-parse", "zero-copy", "zero-copy-small-ring"])
 def test_gpu_service_tile_matches_reference_tile(stream, reference_runs, tmp_path, mode):
     """The sandboxed tile under fd_mux_tile, the GPU service verifying in
     batches of 256 signatures with 3 in flight: the reference tile's frags,
     byte for byte and in order -- with the host parsing, the GPU parsing
-    copies, and the GPU parsing payloads DMA'd in place from the txn link
-    (the ring's wrap included: 2600 frags through a 4096-line link)."""
+    copies, and the GPU parsing payloads read in place from the txn link
+    (the ring's wrap included: 2600 frags through a 1024-line link, and
+    through a 64-line link whose ~84 KB dcache wraps every few batches, so
+    batches take their payloads as two spans)."""
     path, frags = stream
     app = uuid.uuid4().hex[:10]
     svc = start_service(app, 1, "--batch", "256", "--depth", "1024", *mode)
