@@ -1016,14 +1016,14 @@ fd_ed25519_hip_verify_txns_host( fd_ed25519_hip_engine_t * e, unsigned long ntxn
    message, with batch_single_msg's combine -- and hands every caller its
    code; the others wait on a condition variable.  One caller alone pays
    one GPU round trip as before; N concurrent callers share a round trip,
-   and two engines keep a second batch filling while one is on the GPU, so
+   and four engines keep batches filling while others are on the GPU, so
    calls per second grow with the caller count instead of serialising on
    one lock.  The engines use the compact base tables
    (FD_ED25519_HIP_FLAG_COMPACT_TABLES: 2 x 8 MiB instead of 2 x 2 GiB) and
    small chunks, so a process that only uses the drop-ins holds well under
    600 MB of device memory. */
 
-#define DROPIN_ENGINES   2
+#define DROPIN_ENGINES   4
 #define DROPIN_BATCH_MAX 4096UL
 #define DROPIN_CHUNK     16384UL
 
@@ -1062,7 +1062,8 @@ static pthread_cond_t  dropin_cv   = PTHREAD_COND_INITIALIZER;
 static struct {
   fd_ed25519_hip_engine_t * eng[ DROPIN_ENGINES ];
   int                       busy[ DROPIN_ENGINES ];
-  unsigned char *           h_blk[ DROPIN_ENGINES ];   /* pinned: one launch's inputs, then its codes */
+  unsigned char *           h_blk[ DROPIN_ENGINES ];   /* pinned, coherent: one launch's inputs, then its codes */
+  unsigned char *           h_dev[ DROPIN_ENGINES ];   /* h_blk as the device sees it */
   unsigned char *           d_blk[ DROPIN_ENGINES ];
   uint64_t                  blk_cap[ DROPIN_ENGINES ];
   dropin_req_t *            head;
@@ -1133,8 +1134,9 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     uint64_t cap = dq.blk_cap[k] ? dq.blk_cap[k] : (1UL<<20);
     while( cap<need ) cap *= 2UL;
     hipHostFree( dq.h_blk[k] ); hipFree( dq.d_blk[k] );
-    dq.h_blk[k] = NULL; dq.d_blk[k] = NULL; dq.blk_cap[k] = 0UL;
-    HIPCHK( hipHostMalloc( (void **)&dq.h_blk[k], cap, hipHostMallocDefault ), "hipHostMalloc(drop-in)" );
+    dq.h_blk[k] = NULL; dq.h_dev[k] = NULL; dq.d_blk[k] = NULL; dq.blk_cap[k] = 0UL;
+    HIPCHK( hipHostMalloc( (void **)&dq.h_blk[k], cap, hipHostMallocCoherent ), "hipHostMalloc(drop-in)" );
+    HIPCHK( hipHostGetDevicePointer( (void **)&dq.h_dev[k], dq.h_blk[k], 0U ), "hipHostGetDevicePointer(drop-in)" );
     HIPCHK( hipMalloc( (void **)&dq.d_blk[k], cap ), "hipMalloc(drop-in)" );
     dq.blk_cap[k] = cap;
   }
@@ -1163,7 +1165,13 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     }
   }
   hipStream_t st = e->stream;
-  HIPCHK( hipMemcpyAsync( d, h, in_sz ? in_sz : 1UL, hipMemcpyHostToDevice, st ), "H2D drop-in" );
+  /* the block crosses by device launches (fd_ed25519_hip_launch_pull), not
+     copy-engine calls: several drop-in engines submit from their callers'
+     threads at once */
+  fd_ed25519_pull_params_t pp;
+  memset( &pp, 0, sizeof(pp) );
+  pp.src[0] = dq.h_dev[k]; pp.dst[0] = d; pp.n[0] = in_sz ? in_sz : 1UL; pp.cnt = 1U;
+  HIPCHK( (hipError_t)fd_ed25519_hip_launch_pull( &pp, st ), "H2D drop-in" );
   int err = fd_ed25519_hip_verify_dev( e, nsig_m, d + o_msg, (unsigned long const *)(d + o_off),
                                        (unsigned int const *)(d + o_sz), d + o_sig, d + o_pub,
                                        (signed char *)(d + o_out), st );
@@ -1176,7 +1184,8 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
                                           (uint32_t const *)(d + o_tc), (signed char *)(d + o_tout), st );
     if( err ) { hipStreamSynchronize( st ); return err; }
   }
-  HIPCHK( hipMemcpyAsync( h + o_out, d + o_out, multi ? nsig + n : nsig, hipMemcpyDeviceToHost, st ), "D2H drop-in" );
+  pp.src[0] = d + o_out; pp.dst[0] = dq.h_dev[k] + o_out; pp.n[0] = multi ? nsig + n : nsig;
+  HIPCHK( (hipError_t)fd_ed25519_hip_launch_pull( &pp, st ), "D2H drop-in" );
   HIPCHK( hipStreamSynchronize( st ), "drop-in verify" );
   signed char const * codes = (signed char const *)(h + o_out);
   signed char const * tcode = (signed char const *)(h + o_tout);
