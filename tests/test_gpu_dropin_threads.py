@@ -128,7 +128,7 @@ def test_dropin_calls_scale_with_threads(fd):
 
 
 def test_dropin_only_process_device_bytes():
-    """A process that only calls the drop-ins: its device memory is the two
+    """A process that only calls the drop-ins: its device memory is the four
     drop-in engines plus the compact base tables (2 x 8 MiB), well under
     600 MB -- not the 2 x 2 GiB wide tables."""
     code = ("import sys; sys.path.insert(0, %r); from firedancer_amd import ed25519 as e; "
