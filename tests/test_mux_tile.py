@@ -223,6 +223,16 @@ def test_tile_refuses_protocol_violations(stream, tmp_path, bad):
         p = run_harness("verify_hip", path, str(tmp_path / "hip.bin"), app=app, timeout=60)
         t0 = time.time()
         n, beat = 0, 0
+
+        def answer(body, sig):
+            """publish a verdict frag, waiting for credit while the tile
+            lives (it returns credits in groups, or when it finds the
+            verdict link empty); False once it has exited"""
+            while not vdl.publish(body, sig):
+                if p.poll() is not None:
+                    return False
+                vdl.heartbeat(beat)
+            return True
         while p.poll() is None and time.time() - t0 < 60:
             beat += 1
             vdl.heartbeat(beat)
@@ -231,15 +241,17 @@ def test_tile_refuses_protocol_violations(stream, tmp_path, bad):
                 continue
             payload, sig, ctl = f
             if n < 20:   # a few good filtered answers first
-                assert vdl.publish(bytes([0xFF]), sig)
+                ok = answer(bytes([0xFF]), sig)
             elif bad == "order":
-                assert vdl.publish(bytes([0xFF]), sig + (1 << 32))
+                ok = answer(bytes([0xFF]), sig + (1 << 32))
             elif bad == "size":
-                assert vdl.publish(b"\0", sig)   # SUCCESS without the trailer
+                ok = answer(b"\0", sig)   # SUCCESS without the trailer
             elif bad == "trailer":   # fd_txn_t-sized, but its payload_sz is not this payload's
-                assert vdl.publish(b"\0" + bytes(64) + (len(payload) + 1).to_bytes(2, "little"), sig)
+                ok = answer(b"\0" + bytes(64) + (len(payload) + 1).to_bytes(2, "little"), sig)
             else:
-                assert vdl.publish(bytes([0x05]), sig)
+                ok = answer(bytes([0x05]), sig)
+            if not ok:
+                break
             n += 1
         so, se = p.communicate(timeout=30)
         status = txl.status()
