@@ -308,12 +308,15 @@ slot_h2d( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st, unsigne
     k++;
   }
 #ifndef FD_ED25519_HIP_AB_COPY_ENGINES
-  fd_ed25519_pull_params_t pp;
-  memset( &pp, 0, sizeof(pp) );
-  for( unsigned i=0U; i<k; i++ ) { pp.src[ i ] = sp[ i ].dev; pp.dst[ i ] = sp[ i ].dst; pp.n[ i ] = sp[ i ].n; }
-  pp.cnt = k;
-  int le = fd_ed25519_hip_launch_pull( &pp, st );
-  if( le ) return tile_fail( "H2D pull launch", (hipError_t)le );
+  for( unsigned i0=0U; i0<k; i0+=FD_ED25519_PULL_SPAN_MAX ) {   /* one launch moves up to 8 spans (9 at most here) */
+    fd_ed25519_pull_params_t pp;
+    memset( &pp, 0, sizeof(pp) );
+    for( unsigned i=i0; i<k && i-i0<FD_ED25519_PULL_SPAN_MAX; i++ ) {
+      pp.src[ pp.cnt ] = sp[ i ].dev; pp.dst[ pp.cnt ] = sp[ i ].dst; pp.n[ pp.cnt ] = sp[ i ].n; pp.cnt++;
+    }
+    int le = fd_ed25519_hip_launch_pull( &pp, st );
+    if( le ) return tile_fail( "H2D pull launch", (hipError_t)le );
+  }
 #else
   for( unsigned i=0U; i<k; i++ )
     TCHK( hipMemcpyAsync( sp[ i ].dst, sp[ i ].src, sp[ i ].n, hipMemcpyHostToDevice, st ), "H2D batch" );
