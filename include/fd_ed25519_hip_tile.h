@@ -522,7 +522,8 @@ fd_ed25519_hip_vservice_run( int device, unsigned slot_cnt, unsigned long batch_
    pair (optional).
 
    Liveness and failure policy, both entry points: the service ticks the
-   heartbeat of each `out` link on every pass of its loop; on a GPU or
+   heartbeat of each `out` link on every idle pass of its loop and every
+   16th busy one (microseconds apart either way); on a GPU or
    launch failure, an allocation failure, a tile that overran its own link
    or marked a link failed, it stops publishing, marks both links failed
    with the code and returns it (it never aborts the process). */
