@@ -398,6 +398,13 @@ def latency_deployed(eng, args):
     tile.write_payload_file(path_ref, pay[:n_ref])
     svc_mode = ["--zero-copy"] if args.deployed_mode == "zero-copy" else (
         ["--gpu-parse"] if args.deployed_mode == "gpu-parse" else [])
+    # the service and the tile's harness on the CPUs of the GPU's NUMA node,
+    # as fdctl pins its tiles (tools/service_bench.py does the same)
+    node = sorted(tile.device_cpus(eng.info()))
+
+    def pin():
+        if node:
+            os.sched_setaffinity(0, node)
 
     def run(kind, rate):
         """one harness run -> (its JSON line, latencies in ms)"""
@@ -406,7 +413,7 @@ def latency_deployed(eng, args):
         if kind == "verify_hip":
             svc = subprocess.Popen([svc_bin, "--prefix", f"/fd_vhip_{app}_", "--tiles", "1", "--batch",
                                     str(args.latency_batch), "--slots", str(args.latency_slots), *svc_mode],
-                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, preexec_fn=pin)
             line = svc.stdout.readline()
             if not line.startswith("ready"):
                 raise RuntimeError(f"service did not start: {line!r} {svc.stderr.read()[-500:]}")
@@ -414,7 +421,8 @@ def latency_deployed(eng, args):
         try:
             p = subprocess.run([mux, kind, path if kind == "verify_hip" else path_ref, os.path.join(tmp, "out.bin"),
                                 "--app", app, "--depth", "16384", "--rate", str(rate), "--timeout", "100",
-                                "--log-path", "", "--lat-out", lat_path], capture_output=True, text=True, timeout=150)
+                                "--log-path", "", "--lat-out", lat_path], capture_output=True, text=True, timeout=150,
+                               preexec_fn=pin)
             if p.returncode != 0:
                 raise RuntimeError(f"harness {kind} rc {p.returncode}: {p.stderr[-500:]}")
             if svc is not None and svc.wait(timeout=60) != 0:
@@ -460,6 +468,7 @@ def latency_deployed(eng, args):
             os.unlink(os.path.join(tmp, f))
         os.rmdir(tmp)
     hip.update({"batch_sigs": args.latency_batch, "slots_in_flight": args.latency_slots,
+                "cpus": f"{len(node)} CPUs of the GPU's NUMA node (service and harness pinned)" if node else "unpinned",
                 "service_mode": args.deployed_mode, "msg_sz": 200,
                 "path": "producer -> quic_verify mcache/dcache (reference tango) -> fd_tile_verify_hip under the "
                         "reference's fd_mux_tile, its seccomp filter installed -> shlink -> fd_verify_hip_service "
