@@ -1964,6 +1964,7 @@ vsvc_pass( vsvc_t * S ) {
 
 typedef struct {
   int                                    device, flags;
+  int                                    cpu;      /* the CPU the thread runs on, or -1 */
   unsigned                               slot_cnt, k0, k1;   /* the thread serves link pairs [k0, k1) */
   unsigned long                          batch_sigs;
   fd_ed25519_hip_shlink_t * const *      in;
@@ -1978,6 +1979,25 @@ typedef struct {
 static void *
 vservice_main( void * arg ) {
   vservice_job_t * j = (vservice_job_t *)arg;
+  if( j->cpu>=0 ) {   /* before anything allocates: first touch lands on the thread's own node */
+    cpu_set_t set;
+    CPU_ZERO( &set );
+    CPU_SET( j->cpu, &set );
+    if( pthread_setaffinity_np( pthread_self(), sizeof(set), &set ) ) {
+      char msg[ 96 ];
+      snprintf( msg, sizeof(msg), "vservice: cannot run a service thread on CPU %d", j->cpu );
+      fd_ed25519_hip_private_set_error( msg );
+      for( unsigned k=j->k0; k<j->k1; k++ ) {
+        vsvc_t * S = &j->pair[ k ];
+        memset( S, 0, sizeof(*S) );
+        S->L.in = j->in[ k ]; S->L.out = j->out[ k ]; S->stats = &j->st[ k ]; S->stop = j->stop; S->device = j->device;
+        S->t0 = now_s();
+        vsvc_end( S, FD_ED25519_HIP_ERR_INVAL, 0 );
+        atomic_fetch_add_explicit( j->ready, 1U, memory_order_release );
+      }
+      return NULL;
+    }
+  }
   for( unsigned k=j->k0; k<j->k1; k++ ) {
     vsvc_open( &j->pair[ k ], j->device, j->slot_cnt, j->batch_sigs, j->flags, j->in[ k ], j->out[ k ], &j->st[ k ],
                j->stop, j->opts );
@@ -2028,6 +2048,7 @@ fd_ed25519_hip_vservice_serve( int device, unsigned slot_cnt, unsigned long batc
     vservice_job_t * j = &job[ t ];
     j->device = device; j->flags = flags; j->slot_cnt = slot_cnt; j->batch_sigs = batch_sigs;
     j->k0 = t*per; j->k1 = j->k0 + per<link_cnt ? j->k0 + per : link_cnt;
+    j->cpu = opts && opts->link_cpu_cnt && opts->link_cpus ? opts->link_cpus[ t % opts->link_cpu_cnt ] : -1;
     j->in = in; j->out = out; j->pair = pair; j->st = st; j->stop = &stop; j->opts = opts; j->ready = &ready;
     if( pthread_create( &th[ t ], NULL, vservice_main, j ) ) {
       rc = FD_ED25519_HIP_ERR_NOMEM;

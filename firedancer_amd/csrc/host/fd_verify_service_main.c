@@ -11,6 +11,7 @@
      fd_verify_hip_service --prefix NAME --tiles K [--gpu G] [--depth D]
                            [--slots S] [--batch B] [--gpu-parse | --zero-copy] [--codes portable|avx512]
                            [--tile-stale-ms T] [--gpu-hang-ms H] [--no-parent-watch] [--links-per-thread L]
+                           [--cpus LIST]
 
    creates, for k in [0,K), the links NAME<k>_txn (tile -> service) and
    NAME<k>_vd (service -> tile), each of D lines (default 16384), prints
@@ -41,6 +42,8 @@
    turn (default 1, a thread per tile); a pass over a pair never waits for
    the GPU, so the pairs of a thread do not hold each other up, and a
    service whose threads would mostly spin idle takes fewer cores.
+   --cpus LIST (e.g. 8-15 or 8,10,12): service thread t runs on the t-th
+   CPU of the list (cyclically), as fdctl pins each tile to a core.
 
    Exit status: 0 every tile ended its stream (EOS); 1 bad arguments, or a
    link name a live process already holds; 2 the device failed (GPU,
@@ -104,7 +107,29 @@ static void
 usage( char const * argv0 ) {
   fprintf( stderr, "usage: %s --prefix NAME --tiles K [--gpu G] [--depth D] [--slots S] [--batch B] "
                    "[--gpu-parse | --zero-copy] [--codes portable|avx512] [--tile-stale-ms T] [--gpu-hang-ms H] "
-                   "[--no-parent-watch] [--links-per-thread L]\n", argv0 );
+                   "[--no-parent-watch] [--links-per-thread L] [--cpus LIST]\n", argv0 );
+}
+
+/* "a,b,c-d" -> cpus (at most max); the count, or -1 on a malformed list */
+static int
+parse_cpus( char const * s, int * cpus, int max ) {
+  int n = 0;
+  while( *s ) {
+    char * e;
+    long a = strtol( s, &e, 10 );
+    if( e==s || a<0 || a>=CPU_SETSIZE ) return -1;
+    long b = a;
+    if( *e=='-' ) {
+      s = e + 1;
+      b = strtol( s, &e, 10 );
+      if( e==s || b<a || b>=CPU_SETSIZE ) return -1;
+    }
+    for( long c=a; c<=b; c++ ) { if( n>=max ) return -1; cpus[ n++ ] = (int)c; }
+    if( *e==',' ) e++;
+    else if( *e ) return -1;
+    s = e;
+  }
+  return n;
 }
 
 int
@@ -112,6 +137,8 @@ main( int argc, char ** argv ) {
   g_parent = getppid();
   char const *  prefix = NULL;
   unsigned      tiles  = 0U, slots = 3U, per_thread = 1U;
+  int           cpus[ 256 ];
+  int           cpu_cnt = 0;
   int           gpu    = 0, flags = 0, parent_watch_on = 1;
   unsigned long depth  = 16384UL, batch = 4096UL;
   long          stale_ms = 0L, hang_ms = 0L;
@@ -128,6 +155,11 @@ main( int argc, char ** argv ) {
     else if( !strcmp( a, "--gpu-hang-ms" ) && v ) { hang_ms = strtol( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--no-parent-watch" ) ) { parent_watch_on = 0; }
     else if( !strcmp( a, "--links-per-thread" ) && v ) { per_thread = (unsigned)strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--cpus" ) && v ) {
+      cpu_cnt = parse_cpus( v, cpus, 256 );
+      if( cpu_cnt<=0 ) { fprintf( stderr, "fd_verify_hip_service: bad --cpus list %s\n", v ); return 1; }
+      i++;
+    }
     else if( !strcmp( a, "--gpu-parse" ) )   { flags |= FD_ED25519_HIP_VTILE_GPU_PARSE; }
     else if( !strcmp( a, "--zero-copy" ) )   { flags |= FD_ED25519_HIP_VTILE_GPU_PARSE | FD_ED25519_HIP_VSERVICE_ZERO_COPY; }
     else if( !strcmp( a, "--codes" ) && v ) {
@@ -194,6 +226,8 @@ main( int argc, char ** argv ) {
     opts.ready         = announce_ready;
     opts.ready_ctx     = &tiles;
     opts.links_per_thread = per_thread;
+    opts.link_cpus        = cpu_cnt ? cpus : NULL;
+    opts.link_cpu_cnt     = (unsigned)cpu_cnt;
     int err = fd_ed25519_hip_vservice_serve( gpu, slots, batch, flags, in, out, tiles, st, &opts );
     /* one JSON line for tools and tests: per-tile device memory, how each
        link ended, and the base tables this one process holds for all */

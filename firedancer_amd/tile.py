@@ -547,7 +547,7 @@ _lib.fd_ed25519_hip_vservice_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes
                                              ctypes.POINTER(VServiceStats)]
 # the library and these ctypes mirrors must describe the same ABI
 _lib.fd_ed25519_hip_abi_check.argtypes = [ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong]
-ABI_VERSION = 6   # FD_ED25519_HIP_ABI_VERSION
+ABI_VERSION = 7   # FD_ED25519_HIP_ABI_VERSION
 if _lib.fd_ed25519_hip_abi_check(ABI_VERSION, ctypes.sizeof(Slot), ctypes.sizeof(__import__(
         "firedancer_amd.ed25519", fromlist=["_Info"])._Info), ctypes.sizeof(VServiceStats)) != 0:
     raise ImportError("libfd_ed25519_hip ABI mismatch: " + _lib.fd_ed25519_hip_last_error().decode())
@@ -652,7 +652,8 @@ def vservice_run(in_link, out_link, device=0, slot_cnt=3, batch_sigs=4096, gpu_p
 
 class VServiceOpts(ctypes.Structure):
     _fields_ = [("stop", ctypes.c_void_p), ("tile_stale_ns", ctypes.c_long), ("gpu_hang_ns", ctypes.c_long),
-                ("ready", ctypes.c_void_p), ("ready_ctx", ctypes.c_void_p), ("links_per_thread", ctypes.c_uint)]
+                ("ready", ctypes.c_void_p), ("ready_ctx", ctypes.c_void_p), ("links_per_thread", ctypes.c_uint),
+                ("link_cpus", ctypes.POINTER(ctypes.c_int)), ("link_cpu_cnt", ctypes.c_uint)]
 
 
 _lib.fd_ed25519_hip_vservice_serve.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_ulong, ctypes.c_int,
@@ -661,9 +662,10 @@ _lib.fd_ed25519_hip_vservice_serve.argtypes = [ctypes.c_int, ctypes.c_uint, ctyp
 
 
 def vservice_serve(in_links, out_links, device=0, slot_cnt=3, batch_sigs=4096, gpu_parse=True, codes="avx512",
-                   tile_stale_s=0.0, gpu_hang_s=0.0, links_per_thread=1):
+                   tile_stale_s=0.0, gpu_hang_s=0.0, links_per_thread=1, cpus=None):
     """Several link pairs on one device (fd_ed25519_hip_vservice_serve),
-    links_per_thread pairs per service thread:
+    links_per_thread pairs per service thread, thread t on cpus[t % len]
+    (None: the process's affinity):
     -> (status, [stats per pair]); status 0 when every pair ended with EOS,
     else the device failure's code or the first link-local end."""
     from .ed25519 import FLAG_CODES_PORTABLE
@@ -672,7 +674,9 @@ def vservice_serve(in_links, out_links, device=0, slot_cnt=3, batch_sigs=4096, g
     ins = (_v * k)(*[l._h for l in in_links])
     outs = (_v * k)(*[l._h for l in out_links])
     st = (VServiceStats * k)()
-    opts = VServiceOpts(None, int(tile_stale_s * 1e9), int(gpu_hang_s * 1e9), None, None, int(links_per_thread))
+    cpu_arr = (ctypes.c_int * len(cpus))(*cpus) if cpus else None
+    opts = VServiceOpts(None, int(tile_stale_s * 1e9), int(gpu_hang_s * 1e9), None, None, int(links_per_thread),
+                        cpu_arr, len(cpus) if cpus else 0)
     rc = _lib.fd_ed25519_hip_vservice_serve(int(device), int(slot_cnt), int(batch_sigs), flags, ins, outs, k, st,
                                             ctypes.byref(opts))
     return rc, [{f: getattr(x, f) for f, _ in VServiceStats._fields_} for x in st]

@@ -114,7 +114,7 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
    sizeof(fd_ed25519_hip_vservice_stats_t) ) returns 0 when they agree,
    FD_ED25519_HIP_ERR_INVAL (with fd_ed25519_hip_last_error) when not. */
-#define FD_ED25519_HIP_ABI_VERSION (6U)
+#define FD_ED25519_HIP_ABI_VERSION (7U)
 
 unsigned
 fd_ed25519_hip_abi_version( void );

@@ -590,6 +590,12 @@ typedef struct {
      the service fewer cores where its threads would otherwise spin idle
      (ABI 6) */
   unsigned             links_per_thread;
+  /* CPUs for the service threads (fdctl pins each tile to a core): thread
+     t runs on link_cpus[t % link_cpu_cnt] (0 entries: the process's
+     affinity, as before).  A CPU outside the process's affinity fails the
+     thread's pairs with FD_ED25519_HIP_ERR_INVAL.  (ABI 7) */
+  int const *          link_cpus;
+  unsigned             link_cpu_cnt;
 } fd_ed25519_hip_vservice_opts_t;
 
 int

@@ -90,8 +90,8 @@ def test_gpu_service_tile_matches_reference_tile(stream, reference_runs, tmp_pat
 
 
 @pytest.mark.parametrize("mode", [["--zero-copy"], ["--zero-copy", "--links-per-thread", "3"],
-                                  ["--links-per-thread", "2"]],
-                         ids=["zero-copy", "zero-copy-one-thread", "host-parse-two-per-thread"])
+                                  ["--links-per-thread", "2"], ["--zero-copy", "--cpus", "AFFINITY3"]],
+                         ids=["zero-copy", "zero-copy-one-thread", "host-parse-two-per-thread", "zero-copy-pinned"])
 def test_gpu_service_three_tiles_one_process(stream, reference_runs, tmp_path, mode):
     """Three verify tiles (seq % 3) on one service process (a thread per
     tile, or several tiles per thread): each publishes what the reference
@@ -100,7 +100,8 @@ def test_gpu_service_three_tiles_one_process(stream, reference_runs, tmp_path, m
     (batch-sized lane tables: well under 1 GiB)."""
     path, _ = stream
     app = uuid.uuid4().hex[:10]
-    svc = start_service(app, 3, "--batch", "512", *mode)
+    cpus = ",".join(str(c) for c in sorted(os.sched_getaffinity(0))[-3:])   # a service thread per tile, each on its CPU
+    svc = start_service(app, 3, "--batch", "512", *[cpus if m == "AFFINITY3" else m for m in mode])
     try:
         procs = [(k, run_harness("verify_hip", path, str(tmp_path / f"hip{k}.bin"), app=app, rr=(3, k), timeout=100))
                  for k in range(3)]

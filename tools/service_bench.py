@@ -43,6 +43,21 @@ def gen(paths, txns, q):
     q.put(True)
 
 
+def physical_cores(cpus):
+    """one logical CPU per physical core among cpus (the lowest SMT
+    sibling), in order"""
+    out, seen = [], set()
+    for c in sorted(cpus):
+        try:
+            sib = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+        except OSError:
+            sib = str(c)
+        if sib not in seen:
+            seen.add(sib)
+            out.append(c)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", default="1,2,4,6")
@@ -57,9 +72,10 @@ def main():
     ap.add_argument("--producer", default=PRODUCER, help="tile-side binary (the same A/B build's: the frag protocol)")
     ap.add_argument("--producer-profile", action="store_true",
                     help="the tile side's cycles per txn (fd_shlink_producer --profile: runs unsandboxed)")
-    ap.add_argument("--pin", choices=["none", "node"], default="node",
-                    help="node: the service and the tile processes on the CPUs of the GPU's NUMA node, as fdctl "
-                         "pins its tiles (default); none: wherever the OS puts them")
+    ap.add_argument("--pin", choices=["none", "node", "cores"], default="node",
+                    help="node: the service and the tile processes on the CPUs of the GPU's NUMA node (default); "
+                         "cores: each tile process and each service link thread on a physical core of its own "
+                         "there, as fdctl pins tiles; none: wherever the OS puts them")
     args = ap.parse_args()
     ks = [int(x) for x in args.tiles.split(",")]
     tmp = tempfile.mkdtemp(prefix="svcb")
@@ -83,15 +99,17 @@ def main():
     take()
     p.join(timeout=60)
     pin = None
-    if args.pin == "node" and node_cpus:
+    if args.pin in ("node", "cores") and node_cpus:
         def pin():
             os.sched_setaffinity(0, node_cpus)
+    cores = physical_cores(node_cpus) if args.pin == "cores" else []
     out = []
     for k in ks:
         app = uuid.uuid4().hex[:10]
         prefix = f"/fd_vhip_{app}_"
         env = dict(os.environ, GPU_MAX_HW_QUEUES=str(args.hw_queues))
-        svc = subprocess.Popen([args.service, "--prefix", prefix, "--tiles", str(k), "--batch", str(args.batch),
+        svc_cpus = ["--cpus", ",".join(str(c) for c in cores[k:2 * k])] if len(cores) >= 2 * k else []
+        svc = subprocess.Popen([args.service, "--prefix", prefix, "--tiles", str(k), "--batch", str(args.batch), *svc_cpus,
                                 "--slots", str(args.slots), *(["--gpu-parse"] if args.gpu_parse else []),
                                 *(["--zero-copy"] if args.zero_copy else []),
                                 *(["--links-per-thread", str(args.links_per_thread)] if args.links_per_thread != 1 else [])],
@@ -100,9 +118,12 @@ def main():
         if not line.startswith("ready"):
             raise SystemExit(f"service did not start: {line!r} {svc.stderr.read()[-2000:]}")
         t0 = time.time()
+        def pin_core(c):
+            return lambda: os.sched_setaffinity(0, {c})
         prods = [subprocess.Popen([args.producer, f"{prefix}{i}_txn", f"{prefix}{i}_vd", paths[i],
                                    *(["--profile"] if args.producer_profile else [])],
-                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, preexec_fn=pin) for i in range(k)]
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                  preexec_fn=pin_core(cores[i]) if len(cores) >= 2 * k else pin) for i in range(k)]
         ok = True
         for pr in prods:
             so, se = pr.communicate(timeout=300)
@@ -136,7 +157,7 @@ def main():
         os.unlink(path)
     print(json.dumps({"service_bench": out, "batch": args.batch, "slots": args.slots, "gpu_parse": args.gpu_parse, "zero_copy": args.zero_copy,
                       "links_per_thread": args.links_per_thread,
-                      "hw_queues": args.hw_queues, "pin": args.pin, "node_cpus": len(node_cpus)}))
+                      "hw_queues": args.hw_queues, "pin": args.pin, "cores_used": 2 * max(ks) if args.pin == "cores" else None, "node_cpus": len(node_cpus)}))
 
 
 if __name__ == "__main__":
