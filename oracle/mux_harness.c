@@ -124,6 +124,8 @@ typedef struct {
   volatile int     producer_done;
   volatile int     stop;
   volatile int     consumer_err;
+  ulong            credit_spins;   /* producer: pauses waiting for the tile's fseq (the tile is behind) */
+  ulong            idle_spins;     /* consumer: pauses with nothing published (the tile is not ahead) */
 } harness_t;
 
 static void *
@@ -142,7 +144,11 @@ producer_main( void * arg ) {
       due = k0 + (long)( (double)seq/h->rate*tick_per_s );
     }
     /* credits: never more than depth frags ahead of the tile's fseq */
-    while( fd_seq_diff( seq, fd_fseq_query( h->in_fseq ) )>=(long)h->in_depth ) { if( h->stop ) return NULL; FD_SPIN_PAUSE(); }
+    while( fd_seq_diff( seq, fd_fseq_query( h->in_fseq ) )>=(long)h->in_depth ) {
+      if( h->stop ) return NULL;
+      h->credit_spins++;
+      FD_SPIN_PAUSE();
+    }
     ulong sz = h->sz[ seq ];
     fd_memcpy( fd_chunk_to_laddr( g_mem, chunk ), h->pay + h->off[ seq ], sz );
     long  now   = fd_tickcount();
@@ -164,7 +170,7 @@ consumer_main( void * arg ) {
     fd_frag_meta_t const * m = h->out_mcache + fd_mcache_line_idx( seq, h->out_depth );
     ulong s0 = FD_VOLATILE_CONST( m->seq );
     long d = fd_seq_diff( s0, seq );
-    if( d<0L ) { FD_SPIN_PAUSE(); continue; }
+    if( d<0L ) { h->idle_spins++; FD_SPIN_PAUSE(); continue; }
     if( d>0L ) { h->consumer_err = 1; return NULL; }       /* overrun: the tile ignored our credits */
     FD_COMPILER_MFENCE();
     ulong sig = m->sig, chunk = m->chunk, sz = m->sz, tsorig = m->tsorig;
@@ -417,8 +423,9 @@ main( int argc, char ** argv ) {
   double pmx = nl ? 1e-3*(double)h->lat_ns[ nl-1UL ] : 0.0;
   printf( "{\"tile\": \"%s\", \"frags\": %lu, \"published\": %lu, \"seconds\": %.6f, \"txn_per_s\": %.1f, "
           "\"rr_cnt\": %lu, \"rr_idx\": %lu, \"sandbox\": %d, \"rate\": %.1f, \"lat_p50_us\": %.2f, "
-          "\"lat_p99_us\": %.2f, \"lat_max_us\": %.2f}\n",
-          kind, h->n, h->res_cnt, t1-t0, (double)h->n/(t1-t0), rr_cnt, rr_idx, h->sandbox, h->rate, p50, p99, pmx );
+          "\"lat_p99_us\": %.2f, \"lat_max_us\": %.2f, \"producer_credit_spins\": %lu, \"consumer_idle_spins\": %lu}\n",
+          kind, h->n, h->res_cnt, t1-t0, (double)h->n/(t1-t0), rr_cnt, rr_idx, h->sandbox, h->rate, p50, p99, pmx,
+          h->credit_spins, h->idle_spins );
   fflush( stdout );
   _exit( h->tile_halted==1 ? 0 : 5 );
 }

@@ -74,6 +74,8 @@ def main():
         tenths = np.bincount((slow * 10) // max(len(ms), 1), minlength=10).tolist() if slow.size else [0] * 10
         np.save(os.path.join(REPO, "gpurun_out", f"dprobe_{args.mode}_{r}.npy"), ms.astype(np.float32))
         print(json.dumps({"mode": args.mode, "run": r, "rate": args.rate, "achieved": res["txn_per_s"],
+                          "producer_credit_spins": res.get("producer_credit_spins"),
+                          "consumer_idle_spins": res.get("consumer_idle_spins"),
                           "p50_ms": float(np.percentile(ms, 50)), "p99_ms": float(np.percentile(ms, 99)),
                           "max_ms": float(ms.max()), "slow_frags": int(slow.size),
                           "slow_first_last": [int(slow[0]), int(slow[-1])] if slow.size else None,
