@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--slow-ms", type=float, default=5.0)
+    ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for the service (0: HIP's default)")
+    ap.add_argument("--pin", action="store_true", help="service and harness on the GPU's NUMA-node CPUs (as bench.py)")
     ap.add_argument("--service", default=os.path.join(REPO, "firedancer_amd", "_lib", "fd_verify_hip_service"),
                     help="service binary (an A/B build's; its stderr profile lines are printed)")
     args = ap.parse_args()
@@ -40,17 +42,25 @@ def main():
     svc_bin = args.service
     eng = ed25519.Engine(0, max_chunk=1 << 16)
     pay, _ = workload.txn_payloads(eng, args.txns, 4711, msg_sz=200)
+    node = sorted(tile.device_cpus(eng.info())) if args.pin else []
     eng.close()
+
+    def pin():
+        if node:
+            os.sched_setaffinity(0, node)
     tmp = tempfile.mkdtemp(prefix="dprobe")
     path = os.path.join(tmp, "pay.bin")
     tile.write_payload_file(path, pay)
     mode = {"zero-copy": ["--zero-copy"], "gpu-parse": ["--gpu-parse"], "host-parse": []}[args.mode]
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    env = dict(os.environ)
+    if args.hw_queues:
+        env["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     for r in range(args.runs):
         app = uuid.uuid4().hex[:10]
         svc = subprocess.Popen([svc_bin, "--prefix", f"/fd_vhip_{app}_", "--tiles", "1", "--batch", str(args.batch),
                                 "--slots", str(args.slots), *mode], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                               text=True)
+                               text=True, preexec_fn=pin, env=env)
         line = svc.stdout.readline()
         if not line.startswith("ready"):
             raise SystemExit(f"service did not start: {line!r} {svc.stderr.read()[-500:]}")
@@ -58,7 +68,7 @@ def main():
         try:
             p = subprocess.run([mux, "verify_hip", path, os.path.join(tmp, "out.bin"), "--app", app, "--depth", "16384",
                                 "--rate", str(args.rate), "--timeout", "100", "--log-path", "", "--lat-out", lat_path],
-                               capture_output=True, text=True, timeout=150)
+                               capture_output=True, text=True, timeout=150, preexec_fn=pin)
             if p.returncode != 0:
                 raise SystemExit(f"harness rc {p.returncode}: {p.stderr[-500:]}")
             svc.wait(timeout=60)
@@ -73,7 +83,7 @@ def main():
         slow = np.nonzero(ms > args.slow_ms)[0]
         tenths = np.bincount((slow * 10) // max(len(ms), 1), minlength=10).tolist() if slow.size else [0] * 10
         np.save(os.path.join(REPO, "gpurun_out", f"dprobe_{args.mode}_{r}.npy"), ms.astype(np.float32))
-        print(json.dumps({"mode": args.mode, "run": r, "rate": args.rate, "achieved": res["txn_per_s"],
+        print(json.dumps({"mode": args.mode, "batch": args.batch, "slots": args.slots, "hw_queues": args.hw_queues, "pinned": bool(node), "run": r, "rate": args.rate, "achieved": res["txn_per_s"],
                           "producer_credit_spins": res.get("producer_credit_spins"),
                           "consumer_idle_spins": res.get("consumer_idle_spins"),
                           "p50_ms": float(np.percentile(ms, 50)), "p99_ms": float(np.percentile(ms, 99)),
