@@ -371,7 +371,8 @@ def latency_deployed(eng, args):
     runtime -- fd_mux_tile, its mcache / dcache links and seccomp filter,
     compiled from the reference's sources as the harness
     oracle/_ref/mux/mux_harness -- with the product's GPU service process
-    (fd_verify_hip_service, 256-signature batches) behind its shared-memory
+    (fd_verify_hip_service, 256-signature batches, --deployed-slots of them
+    in flight, each on its own hardware queue) behind its shared-memory
     links.  A producer publishes GPU-signed single-signer transactions into
     the quic -> verify link at a fixed offered load, each frag's tsorig its
     due time; the dedup side takes (now - tsorig) for every verified frag
@@ -412,7 +413,8 @@ def latency_deployed(eng, args):
         svc = None
         if kind == "verify_hip":
             svc = subprocess.Popen([svc_bin, "--prefix", f"/fd_vhip_{app}_", "--tiles", "1", "--batch",
-                                    str(args.latency_batch), "--slots", str(args.latency_slots), *svc_mode],
+                                    str(args.latency_batch), "--slots", str(args.deployed_slots),
+                                    "--hw-queues", str(max(4, args.deployed_slots)), *svc_mode],
                                    stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, preexec_fn=pin)
             line = svc.stdout.readline()
             if not line.startswith("ready"):
@@ -467,7 +469,8 @@ def latency_deployed(eng, args):
         for f in os.listdir(tmp):
             os.unlink(os.path.join(tmp, f))
         os.rmdir(tmp)
-    hip.update({"batch_sigs": args.latency_batch, "slots_in_flight": args.latency_slots,
+    hip.update({"batch_sigs": args.latency_batch, "slots_in_flight": args.deployed_slots,
+                "hw_queues": max(4, args.deployed_slots),
                 "cpus": f"{len(node)} CPUs of the GPU's NUMA node (service and harness pinned)" if node else "unpinned",
                 "service_mode": args.deployed_mode, "msg_sz": 200,
                 "path": "producer -> quic_verify mcache/dcache (reference tango) -> fd_tile_verify_hip under the "
@@ -830,6 +833,9 @@ def main():
                          "0 disables")
     ap.add_argument("--deployed-ref-txns", type=int, default=40000,
                     help="the reference tile's runs in the same harness (its CPU baseline)")
+    ap.add_argument("--deployed-slots", type=int, default=8,
+                    help="batches in flight in the deployed C5 leg's service (one hardware queue each): 8 carries "
+                         "4.5M txn/s at the 4-slot p50, 4 saturate at 2.7M (profiles/r4_deployed_batch_slots_curve.txt)")
     ap.add_argument("--deployed-mode", default="host-parse", choices=["zero-copy", "gpu-parse", "host-parse"],
                     help="the GPU service's mode for the deployed C5 leg")
     ap.add_argument("--host-reps", type=int, default=3, help="host-fed stream passes (0 disables)")

@@ -14,6 +14,8 @@
                   [--die-after N]    stop ticking and hang (SIGKILL-like) after N verdicts
                   [--fail-after N]   mark every link failed after N verdicts and exit 2
                   [--hold N]         answer in batches of N (verdicts held until N arrive or input idles)
+                  [--parse-only]     skip fd_txn_verify (every parsed frag SUCCESS): the ceiling
+                                     of the tile / mux / link chain with an instant verifier
                   [--tile-stale-ms T] [--no-parent-watch]
 
    The lifecycle is the GPU service's (fd_ed25519_hip_vservice_serve,
@@ -67,6 +69,7 @@ typedef struct {
 } svc_link_t;
 
 static volatile int g_stop;
+static int          g_parse_only;
 
 static void
 on_signal( int sig ) {
@@ -110,7 +113,7 @@ answer( svc_link_t * L, uchar const * payload, ulong payload_sz, uchar * out ) {
   *payload_sz_p = (ushort)payload_sz;
   ulong new_sz = ( (ulong)payload_sz_p + sizeof(ushort) ) - (ulong)frag;
   ulong txn_sig;
-  int res = fd_txn_verify( &L->vctx, frag, (ushort)payload_sz, txn_t, &txn_sig );
+  int res = g_parse_only ? FD_TXN_VERIFY_SUCCESS : fd_txn_verify( &L->vctx, frag, (ushort)payload_sz, txn_t, &txn_sig );
   if( res!=FD_TXN_VERIFY_SUCCESS ) { out[0] = (uchar)(schar)res; return 1UL; }
   out[0] = 0;
   memmove( out + 1, frag + txnt_off, new_sz - txnt_off );
@@ -135,6 +138,7 @@ main( int argc, char ** argv ) {
     else if( !strcmp( a, "--hold"       ) && v ) { hold = strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--tile-stale-ms" ) && v ) { stale_ms = strtol( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--no-parent-watch" ) ) parent_watch = 0;
+    else if( !strcmp( a, "--parse-only" ) ) g_parse_only = 1;
     else FD_LOG_ERR(( "bad argument %s", a ));
   }
   FD_TEST( prefix && tiles>=1UL && tiles<=LINK_MAX && hold>=1UL );
