@@ -173,7 +173,7 @@ main( int argc, char ** argv ) {
     }
     else { usage( argv[0] ); return 1; }
   }
-  if( !prefix || !tiles || tiles>FD_ED25519_HIP_VSERVICE_LINK_MAX || strlen( prefix )>96 || hw_queues>32U ) { usage( argv[0] ); return 1; }
+  if( !prefix || !tiles || tiles>FD_ED25519_HIP_VSERVICE_LINK_MAX || strlen( prefix )>96 || hw_queues>32U || !slots || slots>8U ) { usage( argv[0] ); return 1; }
   /* read by the HIP runtime when it starts, at the service's first HIP call (below) */
   {
     unsigned long q = hw_queues;
