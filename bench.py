@@ -948,7 +948,9 @@ def main():
     # pool's slots do): 4 one-stream engines measured 107.7-108.7M/s against
     # 104.9-105.5M/s for 2 engines with the decode side stream
     # (profiles/r2_inflight_streams_ab.txt; extra streams share the process's
-    # 4 hardware queues).
+    # 4 hardware queues).  With 8 queues (--hw-queues), 4 / 6 / 8 one-stream
+    # engines measured 100.4 / 98.0 / 100.6M/s on one box: 4 stays
+    # (profiles/r4h_inflight_ab_hwq8.jsonl).
     if one_stream:
         engines = [ed25519.Engine(device=device, max_chunk=min(n, 1 << 20), half=args.half, one_stream=True)
                    for _ in range(inflight)]
