@@ -408,7 +408,7 @@ def latency_deployed(eng, args):
         if node:
             os.sched_setaffinity(0, node)
 
-    def run(kind, rate):
+    def run(kind, rate, pay_path=None):
         """one harness run -> (its JSON line, latencies in ms)"""
         app = uuid.uuid4().hex[:10]
         svc = None
@@ -422,7 +422,8 @@ def latency_deployed(eng, args):
                 raise RuntimeError(f"service did not start: {line!r} {svc.stderr.read()[-500:]}")
         lat_path = os.path.join(tmp, f"lat_{app}.bin")
         try:
-            p = subprocess.run([mux, kind, path if kind == "verify_hip" else path_ref, os.path.join(tmp, "out.bin"),
+            pay_path = pay_path or (path if kind == "verify_hip" else path_ref)
+            p = subprocess.run([mux, kind, pay_path, os.path.join(tmp, "out.bin"),
                                 "--app", app, "--depth", "16384", "--rate", str(rate), "--timeout", "100",
                                 "--log-path", "", "--lat-out", lat_path], capture_output=True, text=True, timeout=150,
                                preexec_fn=pin)
@@ -463,9 +464,33 @@ def latency_deployed(eng, args):
                                  "percentiles": f"pooled over {runs} runs",
                                  "p99_ms_runs": [r["lat_p99_us"] * 1e-3 for r in per_run]})
         return out
+    def at_rates(rates, runs):
+        """the GPU tile at absolute offered loads (the reference tile's own
+        rates and multiples of its peak): pooled p50 / p99 / max per rate.
+        A run lasts about a second at the reference's rates (its 40K-txn
+        file), 0.5 s at ten times its peak (the 300K file)."""
+        out, rp = [], ref["peak_txn_per_s"]
+        for label, rate in rates:
+            f = path_ref if rate <= rp else path   # the reference tile's own transactions at its rates
+            txns = n_ref if f == path_ref else n
+            pooled, per_run = [], []
+            for _ in range(runs):
+                res, lat = run("verify_hip", rate, f)
+                pooled.append(lat)
+                per_run.append(res)
+            ms = np.concatenate(pooled)
+            out.append({"load": label, "offered_txn_per_s": rate, "txns_per_run": txns,
+                        "achieved_txn_per_s": float(np.mean([r["txn_per_s"] for r in per_run])),
+                        "published_all": all(r["published"] == txns for r in per_run),
+                        "p50_ms": float(np.percentile(ms, 50)), "p99_ms": float(np.percentile(ms, 99)),
+                        "max_ms": float(ms.max()), "samples": int(ms.size), "percentiles": f"pooled over {runs} runs"})
+        return out
     try:
         hip = sweep("verify_hip", 5, n)
         ref = sweep("verify", 2, n_ref)
+        rp = ref["peak_txn_per_s"]
+        matched = at_rates([(f"{f:g} x reference tile peak", f * rp) for f in (0.5, 0.8, 0.95, 10.0, 100.0)],
+                           args.deployed_matched_runs) if args.deployed_matched_runs > 0 else None
     finally:
         for f in os.listdir(tmp):
             os.unlink(os.path.join(tmp, f))
@@ -482,6 +507,19 @@ def latency_deployed(eng, args):
                            "as the harness oracle/_ref/mux/mux_harness; verification runs in the product's service"})
     hip["cpu_baseline_reference_tile"] = dict(ref, tile="the reference's fd_tile_verify (fd_verify.c, CPU verify, "
                                                         "AVX-512 build) in the same harness, one tile")
+    if matched is not None:
+        # the two tiles at the same absolute offered load: the reference
+        # tile's 50 / 80 / 95% (its loads above), then 10x and 100x its peak
+        # (100x is above the GPU tile's own peak when that is below ~5.8M:
+        # then it measures the backlog of an overloaded tile)
+        ref_at = {l["offered_frac_of_peak"]: l for l in ref["loads"]}
+        for m in matched:
+            f = m["offered_txn_per_s"] / rp
+            r = ref_at.get(round(f, 2))
+            m["reference_tile"] = ({"p50_ms": r["p50_ms"], "p99_ms": r["p99_ms"], "max_ms": r["max_ms"]} if r
+                                   else "above the reference tile's peak: it cannot carry this load")
+            m["above_gpu_tile_peak"] = m["offered_txn_per_s"] > hip["peak_txn_per_s"]
+        hip["loads_at_reference_rates"] = matched
     return hip
 
 
@@ -722,12 +760,14 @@ def c4_host_fed(eng, device, info, rank, world, n, index_base, cfg, seed, window
             return wl.expect.download(np.int8, m)
         finally:
             wl.free()
-    pool = tile.Pool([device], batch, slots)
+    pool = []   # made by the first (warm-up) call, under host_stream's guard: a rank whose pool fails is agreed on
     st = {}
     calls = [0]
 
     def run(msgs, off, sz, sigs, pubs, out):
-        _, sec, s = pool.run(msgs, off, sz, sigs, pubs, out)
+        if not pool:
+            pool.append(tile.Pool([device], batch, slots))
+        _, sec, s = pool[0].run(msgs, off, sz, sigs, pubs, out)
         calls[0] += 1
         if calls[0] > 1:   # host_stream's first call is its untimed warm-up pass: not in the byte count
             for k, v in s.items():
@@ -737,7 +777,8 @@ def c4_host_fed(eng, device, info, rank, world, n, index_base, cfg, seed, window
         res, codes = host_stream(n, sizes, window, C4_CHUNK, fill, run, world, alloc=alloc,
                                  register=tile.HostRegistration)
     finally:
-        pool.close()
+        for p in pool:
+            p.close()
     digests = all_gather(res["rank_digest"], world)
     if world > 1:
         everything = all_gather(codes.tobytes(), world)
@@ -769,6 +810,32 @@ def c4_host_fed(eng, device, info, rank, world, n, index_base, cfg, seed, window
             "digest_equal": (stream_digest == C4_STREAM_DIGEST) if whole else None,
             "path": "page-locked host window -> per-batch H2D (messages as one DMA of their span) -> verify -> D2H "
                     "codes; fd_ed25519_hip_pool_run, one feeder thread on the GPU's NUMA node, per rank"}
+
+
+def config_c4(eng, device, info, rank, world, args):
+    """C4 in the default run (BASELINE.json configs[3]): the 64M-signature
+    stream (seed 0xC4C4) sharded over the N ranks of this job, rank r its
+    contiguous 64M/N, each streamed from bounded page-locked host windows
+    through its own GPU's feeder (c4_host_fed), so that every `bench.py
+    --gpus N` line -- the driver's SCALE runs included -- carries north
+    star's C4 curve point beside the C2 headline (strong scaling: the
+    stream's size is fixed, its time is the max over ranks per window).
+    The concatenated verdict digest is compared with the one whose every
+    code the reference's AVX-512 verify checked (C4_STREAM_DIGEST)."""
+    from firedancer_amd import workload
+    cfg = dict(workload.CONFIGS["C4"])
+    total = args.c4_signatures
+    if total % world:
+        raise ValueError(f"--c4-signatures {total} does not split over {world} ranks")
+    cfg["n"] = total
+    n = total // world
+    res = c4_host_fed(eng, device, info, rank, world, n, rank * n, cfg, C4_STREAM_SEED, args.host_window,
+                      args.host_batch, args.host_slots)
+    res.update({"scaling": "strong", "signatures_total": total, "signatures_per_rank": n,
+                "shard": "rank r streams signatures [r*n, (r+1)*n) of the stream (fd_verify.c:46's seq % "
+                         "verify_tile_count, as contiguous shards so each rank's host window is one range)",
+                "rss_note": "peak RSS of the whole bench process (the C2 host-fed leg's 4 x 1M set included)"})
+    return res
 
 
 def pmc_traffic(n):
@@ -842,6 +909,9 @@ def main():
     ap.add_argument("--deployed-slots", type=int, default=8,
                     help="batches in flight in the deployed C5 leg's service (one hardware queue each): 8 carries "
                          "4.5M txn/s at the 4-slot p50, 4 saturate at 2.7M (profiles/r4_deployed_batch_slots_curve.txt)")
+    ap.add_argument("--deployed-matched-runs", type=int, default=3,
+                    help="runs per load of the deployed GPU tile at the reference tile's own absolute rates "
+                         "(loads_at_reference_rates); 0 disables")
     ap.add_argument("--deployed-mode", default="host-parse", choices=["zero-copy", "gpu-parse", "host-parse"],
                     help="the GPU service's mode for the deployed C5 leg")
     ap.add_argument("--host-reps", type=int, default=3, help="host-fed stream passes (0 disables)")
@@ -853,6 +923,9 @@ def main():
     ap.add_argument("--host-first", action="store_true", help="run the host-fed leg first (A/B)")
     ap.add_argument("--host-window", type=int, default=8 << 20,
                     help="C4 host-fed stream: signatures per page-locked host window (the host holds one)")
+    ap.add_argument("--c4-signatures", type=int, default=64 << 20,
+                    help="the C4 stream leg of a C2 run (config_c4): signatures in the whole stream, split over the "
+                         "ranks; 0 disables")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight on the GPU (steps alternate between this many engines); "
                          "0: 4 for C2-like configs, 2 for a strong-scaling stream (one call of many chunks, "
@@ -1058,6 +1131,13 @@ def main():
                               args.host_copies)
         except Exception as ex:  # reported, never fatal for the device-resident number
             log(f"[rank {rank}] host-fed leg failed: {ex!r}")
+    c4 = None
+    if not strong and args.c4_signatures > 0:
+        try:
+            c4 = config_c4(eng, device, info, rank, world, args)
+        except Exception as ex:  # the same on every rank (the stream agrees on every stage); never fatal
+            log(f"[rank {rank}] C4 stream leg failed: {ex!r}")
+            c4 = {"error": repr(ex)}
     lat = None
     if rank == 0 and world == 1 and args.latency_txns > 0 and not strong:
         try:
@@ -1133,6 +1213,7 @@ def main():
             "gpu_over_box_cpu_scope": "these GPUs against cpu_baseline.box_projection (every physical core of the "
                                       "machine, projected from the measured per-core rate)",
             "host_fed": hf,
+            "config_c4": c4,
             "latency_mode": lat,
             "latency_mode_deployed": lat_dep,
             "config_c1": c1,

@@ -200,6 +200,10 @@ typedef struct {
 } fd_ed25519_pull_params_t;
 
 int fd_ed25519_hip_launch_pull( fd_ed25519_pull_params_t const * p, void * stream );
+
+/* fault-injection build only (-DFD_ED25519_HALF_FAULT=1): one wave that
+   sleeps for ms milliseconds (at most 10 s) of the device's wall clock */
+int fd_ed25519_hip_launch_stall( unsigned ms, void * stream );
 int fd_ed25519_hip_launch_txn_finish( int8_t const * d_sig_codes, uint32_t const * d_txn_first,
                                       uint32_t const * d_txn_cnt, uint8_t const * d_parse_ok, int8_t * d_txn_out,
                                       uint64_t ntxn, void * stream );

@@ -1249,6 +1249,28 @@ __global__ void fd_ed25519_txn_combine_kernel(const int8_t* sig_codes, const uin
   out[t] = (int8_t)code;
 }
 
+#if FD_ED25519_HALF_FAULT
+/* Fault-injection build only (tests/test_gpu_service_fault.py): a stand-in
+   for a hung batch.  One wave sleeps until `ticks` of the constant-rate
+   wall clock have passed since it started, then exits: every wave reaches
+   that exit, so the grid always drains (a bounded stall, never a real
+   hang). */
+__global__ void fd_ed25519_stall_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+extern "C" int fd_ed25519_hip_launch_stall(unsigned ms, void* stream) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+      khz <= 0)
+    khz = 100000;
+  if (ms > 10000u) ms = 10000u;   /* bounded whatever the caller asks */
+  hipLaunchKernelGGL(fd_ed25519_stall_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (uint64_t)ms * (uint64_t)khz);
+  return (int)hipGetLastError();
+}
+#endif
+
 /* ------------------------------------------------------------------------
    C-ABI launchers */
 

@@ -46,9 +46,16 @@ fd_ed25519_txn_stage_kernel(fd_ed25519_txn_stage_params_t p) {
   const uint8_t* pay = p.payloads + p.pay_off[t];
   const uint32_t sz = p.pay_sz[t];
   fd_ed25519_hip_txn_t tx;
-  const int good = fd_txn_core_parse(pay, sz, &tx, p.trailer ? p.trailer + 64 * t : nullptr, 64) != 0;
-  p.parse_ok[t] = (uint8_t)good;
   const uint32_t cnt = p.txn_cnt[t];
+  /* the host reserved cnt signature slots from its own read of the
+     signature count; the copy parsed here may differ from that read when
+     the payload sat in a room the tile can still write (zero-copy).  The
+     slots are filled from this parse's offsets, so a count that disagrees
+     with the host's -- or an account list shorter than it -- is a parse
+     failure: nothing is read past what this parse validated */
+  const int good = fd_txn_core_parse(pay, sz, &tx, p.trailer ? p.trailer + 64 * t : nullptr, 64) != 0 &&
+                   (uint32_t)tx.signature_cnt == cnt && (uint32_t)tx.acct_addr_cnt >= cnt;
+  p.parse_ok[t] = (uint8_t)good;
   const uint32_t slots = (cnt >= 1u && cnt <= 16u) ? cnt : 0u;  /* the host reserved these */
   const uint32_t first = p.txn_first[t];
   for (uint32_t j = 0; j < slots; j++) {

@@ -1048,9 +1048,11 @@ typedef struct dropin_req {
    hook moves the limit down (fd_ed25519_hip_dropin_set_host_hash_min). */
 static unsigned long dropin_host_hash_min = 1UL<<32;
 
+/* clamped to 4 GiB: a limit above that would leave messages the device's
+   32-bit sizes cannot carry on the device path */
 void
 fd_ed25519_hip_dropin_set_host_hash_min( unsigned long bytes ) {
-  dropin_host_hash_min = bytes ? bytes : 1UL<<32;
+  dropin_host_hash_min = ( bytes && bytes<(1UL<<32) ) ? bytes : 1UL<<32;
 }
 
 void fd_ed25519_hip_private_challenge( unsigned char const sig[ 64 ], unsigned char const pub[ 32 ],
@@ -1069,29 +1071,81 @@ static struct {
   dropin_req_t *            head;
   dropin_req_t *            tail;
   unsigned long             launches, requests;   /* for fd_ed25519_hip_dropin_stats */
+  int                       device, flags;        /* what the engines are made with */
+  /* failure policy (fd_ed25519_hip_dropin_set_on_lost), under dropin_lock */
+  int                       on_lost;
+  int                       lost;                 /* 0, or the code that lost the device */
+  unsigned long             recoveries;
 } dq;
+
+/* the message, then abort(): the ABORT policy's end */
+static void
+dropin_fatal( int err, char const * what ) {
+  fprintf( stderr, "libfd_ed25519_hip: FATAL: %s: %s (%d): %s; the device is lost to the drop-ins (policy: abort)\n",
+           what, fd_ed25519_hip_strerror( err ), err, fd_ed25519_hip_last_error() );
+  abort();
+}
+
+/* engine k anew (its staging block too): any previous one is deleted
+   first.  0 or the creation's error code (dq.eng[k] then NULL). */
+static int
+dropin_engine_make( int k ) {
+  if( dq.eng[k] ) { fd_ed25519_hip_engine_delete( dq.eng[k] ); dq.eng[k] = NULL; }
+  hipHostFree( dq.h_blk[k] ); hipFree( dq.d_blk[k] );
+  dq.h_blk[k] = NULL; dq.h_dev[k] = NULL; dq.d_blk[k] = NULL; dq.blk_cap[k] = 0UL;
+  dq.eng[k] = fd_ed25519_hip_engine_new( dq.device, DROPIN_CHUNK, dq.flags );
+  return dq.eng[k] ? FD_ED25519_HIP_OK : FD_ED25519_HIP_ERR_INVAL;
+}
+
+/* every engine, each with one more attempt if its first creation fails */
+static int
+dropin_engines_make( void ) {
+  for( int k=0; k<DROPIN_ENGINES; k++ ) {
+    int err = dropin_engine_make( k );
+    if( err ) err = dropin_engine_make( k );
+    if( err ) return err;
+  }
+  return FD_ED25519_HIP_OK;
+}
 
 static void
 dropin_init( void ) {
   char const * dev_s   = getenv( "FD_ED25519_HIP_DEVICE" );
   char const * codes_s = getenv( "FD_ED25519_HIP_CODES" );
-  int dev   = dev_s ? atoi( dev_s ) : 0;
-  int flags = FD_ED25519_HIP_FLAG_COMPACT_TABLES | FD_ED25519_HIP_FLAG_ONE_STREAM |
+  dq.device = dev_s ? atoi( dev_s ) : 0;
+  dq.flags  = FD_ED25519_HIP_FLAG_COMPACT_TABLES | FD_ED25519_HIP_FLAG_ONE_STREAM |
               ((codes_s && !strcmp( codes_s, "portable" )) ? FD_ED25519_HIP_FLAG_CODES_PORTABLE : 0);
-  for( int k=0; k<DROPIN_ENGINES; k++ ) {
-    dq.eng[k] = fd_ed25519_hip_engine_new( dev, DROPIN_CHUNK, flags );
-    if( !dq.eng[k] ) {
-      fprintf( stderr, "libfd_ed25519_hip: FATAL: cannot create the GPU engine: %s\n", fd_ed25519_hip_last_error() );
-      abort();
-    }
+  int err = dropin_engines_make();
+  if( err ) {
+    pthread_mutex_lock( &dropin_lock );
+    dq.lost = err;
+    int abort_now = dq.on_lost==FD_ED25519_HIP_DROPIN_ON_LOST_ABORT;
+    pthread_mutex_unlock( &dropin_lock );
+    if( abort_now ) dropin_fatal( err, "cannot create the drop-in GPU engines" );
+    fprintf( stderr, "libfd_ed25519_hip: cannot create the drop-in GPU engines: %s; every drop-in call returns "
+                     "FD_ED25519_ERR_SIG (policy: reject) until fd_ed25519_hip_dropin_reset\n",
+             fd_ed25519_hip_last_error() );
   }
 }
 
-static void
-dropin_fatal( int err ) {
-  fprintf( stderr, "libfd_ed25519_hip: FATAL: GPU verify failed: %s (%s)\n", fd_ed25519_hip_strerror( err ),
-           fd_ed25519_hip_last_error() );
-  abort();
+int
+fd_ed25519_hip_dropin_set_on_lost( int policy ) {
+  if( policy!=FD_ED25519_HIP_DROPIN_ON_LOST_ABORT && policy!=FD_ED25519_HIP_DROPIN_ON_LOST_REJECT )
+    return FD_ED25519_HIP_ERR_INVAL;
+  pthread_mutex_lock( &dropin_lock );
+  int prev = dq.on_lost;
+  dq.on_lost = policy;
+  pthread_mutex_unlock( &dropin_lock );
+  return prev;
+}
+
+int
+fd_ed25519_hip_dropin_status( unsigned long * recoveries ) {
+  pthread_mutex_lock( &dropin_lock );
+  int lost = dq.lost;
+  if( recoveries ) *recoveries = dq.recoveries;
+  pthread_mutex_unlock( &dropin_lock );
+  return lost;
 }
 
 /* One combined launch of the requests in list (n of them) on drop-in
@@ -1105,9 +1159,30 @@ dropin_fatal( int err ) {
    its request's result. */
 #define DROPIN_ALIGN16( x ) (((x) + 15UL) & ~15UL)
 
+#ifdef FD_ED25519_HIP_HOST_FAULT
+/* test build only (tests/test_gpu_dropin_fault.py): with
+   $FD_ED25519_HIP_FAULT_DROPIN = "a:b", drop-in launches a .. a+b-1 (counted
+   from 1 over the process, retries included) fail as a launch failure
+   would, after their inputs are staged */
+static int
+dropin_fault( void ) {
+  static unsigned long cnt;
+  char const * f = getenv( "FD_ED25519_HIP_FAULT_DROPIN" );
+  unsigned long i = __atomic_add_fetch( &cnt, 1UL, __ATOMIC_RELAXED );
+  if( !f || !*f ) return 0;
+  char * e;
+  unsigned long a = strtoul( f, &e, 10 ), b = *e==':' ? strtoul( e+1, NULL, 10 ) : 1UL;
+  return i>=a && i<a+b;
+}
+#endif
+
 static int
 dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   fd_ed25519_hip_engine_t * e = dq.eng[k];
+  if( !e ) {
+    snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "drop-in engine %d was not created", k );
+    return FD_ED25519_HIP_ERR_INVAL;
+  }
   HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
   /* signatures of requests hashed on the host go after the others: the
      device hashes [0, nsig_m), takes digests for [nsig_m, nsig) */
@@ -1165,6 +1240,13 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     }
   }
   hipStream_t st = e->stream;
+#ifdef FD_ED25519_HIP_HOST_FAULT
+  if( dropin_fault() ) {
+    snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf),
+              "drop-in: injected launch failure (fault-injection build)" );
+    return FD_ED25519_HIP_ERR_HIP - (int)hipErrorLaunchFailure;
+  }
+#endif
   /* the block crosses by device launches (fd_ed25519_hip_launch_pull), not
      copy-engine calls: several drop-in engines submit from their callers'
      threads at once */
@@ -1195,11 +1277,36 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   return FD_ED25519_HIP_OK;
 }
 
+/* a failed launch on engine k: the engine is made anew and the launch run
+   once more (outside the lock, engine k is this thread's while busy) */
+static int
+dropin_retry( int k, dropin_req_t * list, unsigned long n, int err ) {
+  fprintf( stderr, "libfd_ed25519_hip: drop-in launch failed: %s (%d): %s; re-creating engine %d and retrying once\n",
+           fd_ed25519_hip_strerror( err ), err, fd_ed25519_hip_last_error(), k );
+  int e2 = dropin_engine_make( k );
+  if( !e2 ) e2 = dropin_run( k, list, n );
+  return e2;
+}
+
+/* the device is lost (under dropin_lock): the ABORT policy ends here; the
+   REJECT one fails every queued request closed */
+static void
+dropin_lose( int err ) {
+  if( !dq.lost ) dq.lost = err;
+  if( dq.on_lost==FD_ED25519_HIP_DROPIN_ON_LOST_ABORT ) dropin_fatal( err, "GPU verify failed twice (after a retry)" );
+  for( dropin_req_t * q=dq.head; q; ) { dropin_req_t * nx = q->next; q->result = FD_ED25519_ERR_SIG; q->done = 1; q = nx; }
+  dq.head = dq.tail = NULL;
+}
+
 static int
 dropin_submit( dropin_req_t * r ) {
   pthread_once( &dropin_once, dropin_init );
   r->done = 0; r->next = NULL;
   pthread_mutex_lock( &dropin_lock );
+  if( dq.lost ) {   /* fail closed (REJECT; ABORT never gets here) */
+    pthread_mutex_unlock( &dropin_lock );
+    return FD_ED25519_ERR_SIG;
+  }
   if( dq.tail ) dq.tail->next = r; else dq.head = r;
   dq.tail = r;
   while( !r->done ) {
@@ -1216,9 +1323,15 @@ dropin_submit( dropin_req_t * r ) {
     dq.busy[k] = 1;
     dq.launches++; dq.requests += n;
     pthread_mutex_unlock( &dropin_lock );
-    int err = dropin_run( k, list, n );
-    if( err ) dropin_fatal( err );
+    int err = dropin_run( k, list, n ), retried = 0;
+    if( err ) { err = dropin_retry( k, list, n, err ); retried = 1; }
     pthread_mutex_lock( &dropin_lock );
+    if( err ) {
+      for( dropin_req_t * q=list; q; q=q->next ) q->result = FD_ED25519_ERR_SIG;
+      dropin_lose( err );
+    } else if( retried ) {
+      dq.recoveries++;
+    }
     for( dropin_req_t * q=list; q; ) { dropin_req_t * nx = q->next; q->done = 1; q = nx; }
     dq.busy[k] = 0;
     pthread_cond_broadcast( &dropin_cv );
@@ -1239,8 +1352,31 @@ unsigned long
 fd_ed25519_hip_dropin_device_bytes( void ) {
   pthread_once( &dropin_once, dropin_init );
   unsigned long b = 0UL;
-  for( int k=0; k<DROPIN_ENGINES; k++ ) b += dq.eng[k]->device_bytes + dq.blk_cap[k];
-  return b + fd_ed25519_hip_shared_device_bytes( dq.eng[0]->device );
+  for( int k=0; k<DROPIN_ENGINES; k++ ) if( dq.eng[k] ) b += dq.eng[k]->device_bytes + dq.blk_cap[k];
+  return b + fd_ed25519_hip_shared_device_bytes( dq.device );
+}
+
+int
+fd_ed25519_hip_dropin_reset( void ) {
+  pthread_once( &dropin_once, dropin_init );
+  pthread_mutex_lock( &dropin_lock );
+  /* every engine idle, then held: no launch starts while they are re-made */
+  for( ;; ) {
+    int any = 0;
+    for( int k=0; k<DROPIN_ENGINES; k++ ) any |= dq.busy[k];
+    if( !any ) break;
+    pthread_cond_wait( &dropin_cv, &dropin_lock );
+  }
+  for( int k=0; k<DROPIN_ENGINES; k++ ) dq.busy[k] = 1;
+  pthread_mutex_unlock( &dropin_lock );
+  int err = dropin_engines_make();
+  pthread_mutex_lock( &dropin_lock );
+  if( !err ) dq.lost = 0;
+  else if( !dq.lost ) dq.lost = err;
+  for( int k=0; k<DROPIN_ENGINES; k++ ) dq.busy[k] = 0;
+  pthread_cond_broadcast( &dropin_cv );
+  pthread_mutex_unlock( &dropin_lock );
+  return err;
 }
 
 /* The device path carries message sizes as 32-bit values; the reference
@@ -1253,7 +1389,9 @@ fd_ed25519_hip_dropin_device_bytes( void ) {
    is never truncated. */
 static void
 dropin_prepare( dropin_req_t * r ) {
-  r->hashed = r->msg_sz>=dropin_host_hash_min;
+  /* the second test is the guard whatever the limit says: a size the
+     device path would truncate is never sent there */
+  r->hashed = r->msg_sz>=dropin_host_hash_min || r->msg_sz>(unsigned long)UINT32_MAX;
   if( !r->hashed ) return;
   for( unsigned int j=0U; j<r->cnt; j++ )
     fd_ed25519_hip_private_challenge( r->sigs + 64UL*j, r->pubs + 32UL*j, r->msg, r->msg_sz, r->dig[ j ] );

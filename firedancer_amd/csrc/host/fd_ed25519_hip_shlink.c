@@ -42,10 +42,17 @@
    Versioning and restarts: the header carries the frag protocol both
    sides speak (FD_ED25519_HIP_SHLINK_PROTO); join refuses a link of
    another protocol (errno EPROTO), so a tile and a service built from
-   different revisions of the verdict protocol never exchange frags.  It
-   also records the creating process: create reclaims a same-name link
-   whose creator has exited (a service that was killed leaves its links
-   behind) instead of failing, and still refuses one whose creator lives.
+   different revisions of the verdict protocol never exchange frags.  The
+   creator holds an exclusive flock on the link's object for the link's
+   lifetime (the kernel drops it when the creator exits, however it
+   exits): create reclaims a same-name link whose lock it can take (a
+   service that was killed leaves its links behind) instead of failing,
+   and still refuses one whose creator holds the lock.  The lock lives on
+   the object, not on a pid, so it means the same in every PID namespace
+   that maps /dev/shm; the reclaimer holds it while it unlinks, and only
+   unlinks the object it inspected (same inode), so two creators racing
+   for one stale name cannot remove each other's new link.  The creator's
+   pid is still recorded (diagnostics).
 
    No HIP: this file is also linked into the standalone sandboxed producer
    (tools/shlink_producer.c). */
@@ -60,6 +67,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/file.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -96,6 +104,7 @@ struct fd_ed25519_hip_shlink {
   unsigned char * dcache;
   size_t          map_sz;
   char            name[ 128 ];
+  int             lock_fd;    /* creator: the object's fd holding its flock (-1: a joined link) */
   /* process-local cursor: the next seq to publish (producer) or take
      (consumer), and the producer's next dcache chunk */
   uint64_t        seq;
@@ -131,31 +140,34 @@ shlink_map( char const * name, int fd, size_t sz ) {
   l->mcache = (shlink_meta_t *)( (unsigned char *)m + sizeof(shlink_hdr_t) );
   l->map_sz = sz;
   snprintf( l->name, sizeof(l->name), "%s", name );
+  l->lock_fd = -1;
   return l;
 }
 
-/* 1 if the object `name` is a link of this layout whose creating process
-   has exited (kill(pid, 0) fails with ESRCH): left behind by a process that
-   was killed, safe to remove.  A link whose creator lives (or cannot be
-   told apart: no creator recorded, another layout, a pid of another user)
-   is not. */
+/* Removes `name` if it is a link of this layout left behind by a creator
+   that has exited: its flock can be taken.  The lock is held across the
+   unlink, and the name is removed only while it still refers to the
+   object inspected (same device and inode).  1 if removed. */
 static int
-shlink_orphaned( char const * name ) {
+shlink_reclaim( char const * name ) {
   int fd = shm_open( name, O_RDONLY, 0 );
   if( fd<0 ) return 0;
+  int removed = 0;
   struct stat st;
-  int orphan = 0;
-  if( !fstat( fd, &st ) && (size_t)st.st_size>=sizeof(shlink_hdr_t) ) {
+  if( !flock( fd, LOCK_EX | LOCK_NB ) && !fstat( fd, &st ) && (size_t)st.st_size>=sizeof(shlink_hdr_t) ) {
     void * m = mmap( NULL, sizeof(shlink_hdr_t), PROT_READ, MAP_SHARED, fd, 0 );
     if( m!=MAP_FAILED ) {
-      shlink_hdr_t const * h = (shlink_hdr_t const *)m;
-      uint64_t pid = h->creator;
-      if( h->magic==SHLINK_MAGIC && pid && pid<(1UL<<31) && kill( (pid_t)pid, 0 ) && errno==ESRCH ) orphan = 1;
+      int ours = ((shlink_hdr_t const *)m)->magic==SHLINK_MAGIC;   /* a half-made object is its creator's, locked */
       munmap( m, sizeof(shlink_hdr_t) );
+      char path[ 160 ];
+      struct stat now;
+      snprintf( path, sizeof(path), "/dev/shm/%s", name[0]=='/' ? name + 1 : name );
+      if( ours && !stat( path, &now ) && now.st_ino==st.st_ino && now.st_dev==st.st_dev && !shm_unlink( name ) )
+        removed = 1;
     }
   }
-  close( fd );
-  return orphan;
+  close( fd );   /* drops the lock */
+  return removed;
 }
 
 fd_ed25519_hip_shlink_t *
@@ -164,16 +176,27 @@ fd_ed25519_hip_shlink_create( char const * name, unsigned long depth ) {
   uint64_t chunk_cnt  = (depth + 2UL) * shlink_mtu_chunks();
   size_t   sz         = shlink_footprint( depth, chunk_cnt );
   int fd = shm_open( name, O_RDWR | O_CREAT | O_EXCL, 0600 );
-  if( fd<0 && errno==EEXIST && shlink_orphaned( name ) ) {
+  if( fd<0 && errno==EEXIST ) {
     /* a previous creator's link: reclaimed (a peer that still maps it keeps
-       the old object, whose heartbeat has stopped) */
-    shm_unlink( name );
-    fd = shm_open( name, O_RDWR | O_CREAT | O_EXCL, 0600 );
+       the old object, whose heartbeat has stopped); a live creator's stays */
+    if( shlink_reclaim( name ) ) fd = shm_open( name, O_RDWR | O_CREAT | O_EXCL, 0600 );
+    else                         errno = EEXIST;
   }
   if( fd<0 ) return NULL;   /* errno EEXIST: a live process's link of that name */
-  if( ftruncate( fd, (off_t)sz ) ) { close( fd ); shm_unlink( name ); return NULL; }
-  fd_ed25519_hip_shlink_t * l = shlink_map( name, fd, sz );
-  if( !l ) { shm_unlink( name ); return NULL; }
+  /* the creator's lock, before the object has a size or a magic: a
+     reclaimer that got in first sees no magic and lets go (blocking here
+     only for that moment) */
+  int lk;
+  do lk = flock( fd, LOCK_EX ); while( lk && errno==EINTR );
+  int mfd = lk ? -1 : dup( fd );
+  if( lk || mfd<0 || ftruncate( fd, (off_t)sz ) ) {
+    int e = errno;
+    if( mfd>=0 ) close( mfd );
+    close( fd ); shm_unlink( name ); errno = e; return NULL;
+  }
+  fd_ed25519_hip_shlink_t * l = shlink_map( name, mfd, sz );
+  if( !l ) { close( fd ); shm_unlink( name ); return NULL; }
+  l->lock_fd = fd;
   l->dcache = (unsigned char *)l->mcache + depth * sizeof(shlink_meta_t);
   for( uint64_t k=0UL; k<depth; k++ ) {
     atomic_store_explicit( &l->mcache[ k ].seq, k - depth, memory_order_relaxed );
@@ -228,6 +251,7 @@ fd_ed25519_hip_shlink_leave( fd_ed25519_hip_shlink_t * l, int unlink ) {
   if( !l ) return;
   if( unlink ) shm_unlink( l->name );
   munmap( l->hdr, l->map_sz );
+  if( l->lock_fd>=0 ) close( l->lock_fd );   /* the creator's lock goes last */
   free( l );
 }
 

@@ -401,10 +401,18 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   if( err ) return err;
 #ifdef FD_ED25519_HIP_HOST_FAULT
   /* test build only (tests/test_gpu_service_fault.py): the stream's third
-     batch's launch fails after its copies are enqueued */
+     batch's launch fails after its copies are enqueued -- or, with
+     $FD_ED25519_HIP_FAULT_STALL_MS, is held on the device that long (a
+     bounded stand-in for a hung GPU) before its kernels */
   if( slot->seq==2UL && !pipe->warming ) {
-    fd_ed25519_hip_private_set_error( "pipe: injected launch failure (fault-injection build)" );
-    return FD_ED25519_HIP_ERR_HIP - (int)hipErrorLaunchFailure;
+    char const * stall = getenv( "FD_ED25519_HIP_FAULT_STALL_MS" );
+    if( stall && *stall ) {
+      err = fd_ed25519_hip_launch_stall( (unsigned)strtoul( stall, NULL, 10 ), st );
+      if( err ) return tile_fail( "stall launch", (hipError_t)err );
+    } else {
+      fd_ed25519_hip_private_set_error( "pipe: injected launch failure (fault-injection build)" );
+      return FD_ED25519_HIP_ERR_HIP - (int)hipErrorLaunchFailure;
+    }
   }
 #endif
   if( sig_cnt ) {
@@ -1111,6 +1119,18 @@ vt_frag_zc( fd_ed25519_hip_vtile_t * vt, unsigned char const * payload, unsigned
   unsigned long o = (unsigned long)( payload - vt->zc_base ), e = o + payload_sz;
   if( payload<vt->zc_base || e>vt->zc_size ) { vt->err = FD_ED25519_HIP_ERR_INVAL; return vt->err; }
   unsigned long c = payload[0], nsig = (c>=1UL && c<=16UL) ? c : 0UL;
+#ifdef FD_ED25519_HIP_HOST_FAULT
+  /* test build only (tests/test_gpu_service_fault.py): with
+     $FD_ED25519_HIP_FAULT_ZC_COUNT=k every 5th frag's signature count reads
+     as k here, as if the tile had rewritten byte 0 of the room between this
+     read and the batch's DMA (and back): the device's parse must reject
+     the transaction instead of staging k signatures from it */
+  {
+    static unsigned long fault_zc_n;
+    char const * f = getenv( "FD_ED25519_HIP_FAULT_ZC_COUNT" );
+    if( f && *f && (fault_zc_n++ % 5UL)==2UL ) { c = strtoul( f, NULL, 10 ); nsig = (c>=1UL && c<=16UL) ? c : 0UL; }
+  }
+#endif
   for( int pass=0;; pass++ ) {
     if( vt_open( vt ) ) return vt->err;
     fd_ed25519_hip_slot_t * s = vt->open;
@@ -1752,15 +1772,34 @@ typedef struct {
 
 /* the pair ends with rc (0: EOS answered): both links marked failed with a
    failure code, the sibling pairs stopped when the cause is the device's
-   (local = 0), the stats written, the vtile (engines, device memory) freed */
+   (local = 0), the stats written, the vtile (engines, device memory) freed.
+
+   A hung device (a batch past the hang bound, FD_ED25519_HIP_ERR_TIMEOUT)
+   is different: freeing the vtile synchronises its streams, which never
+   returns while the GPU is hung, and a sibling's streams may sit behind
+   the hung queue too.  The stop word then says VSVC_STOP_HUNG, and every
+   pair that ends under it leaves its vtile and its page-locked mapping as
+   they are (host and device memory leak until the process exits, which
+   the service does right away) so that the call returns and the links
+   carry the code. */
+#define VSVC_STOP_FAILED 1
+#define VSVC_STOP_HUNG   2
+
 static void
 vsvc_end( vsvc_t * S, int rc, int local ) {
   if( rc ) {
     fd_ed25519_hip_shlink_fail( S->L.in, rc );
     fd_ed25519_hip_shlink_fail( S->L.out, rc );
-    if( S->stop && !local ) atomic_store_explicit( S->stop, 1, memory_order_release );
+    if( S->stop && !local ) {
+      int want = rc==FD_ED25519_HIP_ERR_TIMEOUT ? VSVC_STOP_HUNG : VSVC_STOP_FAILED;
+      int cur  = atomic_load_explicit( S->stop, memory_order_acquire );
+      while( cur<want && !atomic_compare_exchange_weak_explicit( S->stop, &cur, want, memory_order_acq_rel,
+                                                                 memory_order_acquire ) ) {}
+    }
     if( !local ) snprintf( S->errmsg, sizeof(S->errmsg), "%s", fd_ed25519_hip_last_error() );
   }
+  int hung = rc==FD_ED25519_HIP_ERR_TIMEOUT ||
+             ( S->stop && atomic_load_explicit( S->stop, memory_order_acquire )==VSVC_STOP_HUNG );
   if( S->stats ) {
     S->stats->txn_cnt      = S->txns;
     S->stats->batches      = S->vt ? S->vt->pipe->seq : 0UL;
@@ -1782,6 +1821,11 @@ vsvc_end( vsvc_t * S, int rc, int local ) {
            (double)pf_sub_d2h/(double)( pf_sub_n + 1ULL ) );
 #endif
   free( S->buf ); S->buf = NULL;
+  if( hung ) {   /* nothing that waits on the device: left for the process exit */
+    S->vt = NULL; S->reg = NULL; S->live = 0;
+    if( S->stats ) S->stats->leaked_on_hang = 1U;
+    return;
+  }
   if( S->vt ) {
     S->vt->idle = NULL;   /* the delete below may wait for batches in flight */
     fd_ed25519_hip_vtile_delete( S->vt );

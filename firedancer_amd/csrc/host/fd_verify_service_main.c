@@ -30,7 +30,10 @@
        dies (PR_SET_PDEATHSIG, and its parent pid watched), so a validator
        that is gone never leaves an orphan holding HBM and shm links;
      - a batch the GPU has not completed after H ms (default 30000) is a
-       hung GPU and ends every link.
+       hung GPU and ends every link (marked FD_ED25519_HIP_ERR_TIMEOUT,
+       or STOPPED for the other tiles'); the service then exits with
+       status 2 at once, without freeing its engines or running the HIP
+       runtime's teardown (both would wait on the hung device).
 
    --gpu-parse: the transactions are parsed on the GPU (the service copies
    each payload out of the link into a batch); --zero-copy: the same, and
@@ -69,6 +72,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/prctl.h>
 #include <time.h>
 #include <unistd.h>
@@ -257,8 +261,25 @@ main( int argc, char ** argv ) {
     for( unsigned k=0U; k<tiles; k++ ) printf( "%s%lu", k ? ", " : "", st[ k ].txn_cnt );
     printf( "], \"end_codes\": [" );
     for( unsigned k=0U; k<tiles; k++ ) printf( "%s%d", k ? ", " : "", st[ k ].end_code );
-    printf( "], \"signal\": %d, \"rc\": %d}\n", g_stop_signal, err );
+    unsigned leaked = 0U;
+    for( unsigned k=0U; k<tiles; k++ ) leaked |= st[ k ].leaked_on_hang;
+    printf( "], \"signal\": %d, \"rc\": %d, \"gpu_hang\": %s}\n", g_stop_signal, err, leaked ? "true" : "false" );
     fflush( stdout );
+    if( leaked ) {
+      /* a hung GPU: the link pairs left their engines as they were (freeing
+         them would wait on the device), and so would the HIP runtime's own
+         teardown at exit.  Remove the links' names, say why, and leave
+         without running any exit handler: the kernel reclaims the process's
+         device memory and queues. */
+      fprintf( stderr, "fd_verify_hip_service: FAILED: %s (%d): %s; every link is marked failed, exiting without "
+                       "device teardown\n", fd_ed25519_hip_strerror( err ), err, fd_ed25519_hip_last_error() );
+      for( unsigned k=0U; k<tiles; k++ ) {
+        char name[ 128 ];
+        snprintf( name, sizeof(name), "%s%u_txn", prefix, k ); shm_unlink( name );
+        snprintf( name, sizeof(name), "%s%u_vd",  prefix, k ); shm_unlink( name );
+      }
+      _exit( 2 );
+    }
     int device = err && err!=FD_ED25519_HIP_SHLINK_FAIL_PROTOCOL && err!=FD_ED25519_HIP_SHLINK_FAIL_STOPPED &&
                  err!=FD_ED25519_HIP_SHLINK_FAIL_TILE_GONE;
     if( device ) {

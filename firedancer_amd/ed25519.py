@@ -368,6 +368,30 @@ def dropin_stats():
     return a.value, b.value
 
 
+DROPIN_ON_LOST_ABORT, DROPIN_ON_LOST_REJECT = 0, 1
+_lib.fd_ed25519_hip_dropin_set_on_lost.argtypes = [ctypes.c_int]
+_lib.fd_ed25519_hip_dropin_status.argtypes = [ctypes.POINTER(ctypes.c_ulong)]
+
+
+def dropin_set_on_lost(policy):
+    """The drop-ins' lost-device policy (fd_ed25519_hip_dropin_set_on_lost):
+    DROPIN_ON_LOST_ABORT (default) or DROPIN_ON_LOST_REJECT; returns the previous."""
+    return _lib.fd_ed25519_hip_dropin_set_on_lost(int(policy))
+
+
+def dropin_status():
+    """(lost, recoveries): 0 or the code that lost the device, and the launches
+    that succeeded on a re-created engine (fd_ed25519_hip_dropin_status)."""
+    r = ctypes.c_ulong()
+    lost = _lib.fd_ed25519_hip_dropin_status(ctypes.byref(r))
+    return lost, r.value
+
+
+def dropin_reset():
+    """Re-creates the drop-in engines (fd_ed25519_hip_dropin_reset): 0 or an error code."""
+    return _lib.fd_ed25519_hip_dropin_reset()
+
+
 def dropin_device_bytes():
     """Device memory the drop-ins hold: their engines plus the process's shared base tables."""
     return _lib.fd_ed25519_hip_dropin_device_bytes()

@@ -528,7 +528,8 @@ PRODUCER_BIN = (__import__("os").environ.get("FD_SHLINK_PRODUCER") or   # the sa
 
 class VServiceStats(ctypes.Structure):
     _fields_ = [("txn_cnt", ctypes.c_ulong), ("batches", ctypes.c_ulong), ("seconds", ctypes.c_double),
-                ("device_bytes", ctypes.c_ulong), ("shared_device_bytes", ctypes.c_ulong), ("end_code", ctypes.c_int)]
+                ("device_bytes", ctypes.c_ulong), ("shared_device_bytes", ctypes.c_ulong), ("end_code", ctypes.c_int),
+                ("leaked_on_hang", ctypes.c_uint)]
 
 
 _lib.fd_ed25519_hip_shlink_create.argtypes = [ctypes.c_char_p, ctypes.c_ulong]
@@ -547,7 +548,7 @@ _lib.fd_ed25519_hip_vservice_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes
                                              ctypes.POINTER(VServiceStats)]
 # the library and these ctypes mirrors must describe the same ABI
 _lib.fd_ed25519_hip_abi_check.argtypes = [ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong]
-ABI_VERSION = 7   # FD_ED25519_HIP_ABI_VERSION
+ABI_VERSION = 8   # FD_ED25519_HIP_ABI_VERSION
 if _lib.fd_ed25519_hip_abi_check(ABI_VERSION, ctypes.sizeof(Slot), ctypes.sizeof(__import__(
         "firedancer_amd.ed25519", fromlist=["_Info"])._Info), ctypes.sizeof(VServiceStats)) != 0:
     raise ImportError("libfd_ed25519_hip ABI mismatch: " + _lib.fd_ed25519_hip_last_error().decode())

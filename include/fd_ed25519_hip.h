@@ -45,8 +45,11 @@ typedef struct fd_sha512_private fd_sha512_t;
    NULL if msg_sz==0.  Returns FD_ED25519_SUCCESS or FD_ED25519_ERR_*.
    Synchronous; runs on the process-wide default engine (device from
    $FD_ED25519_HIP_DEVICE, default 0; codes from $FD_ED25519_HIP_CODES =
-   "avx512" (default) | "portable").  A GPU failure aborts the process with a
-   message on stderr: this path never silently falls back to the CPU.  Any
+   "avx512" (default) | "portable").  A failed launch is retried once on a
+   re-created engine; a device that fails again is lost, and the process's
+   policy decides (fd_ed25519_hip_dropin_set_on_lost below: abort with a
+   message, the default, or fail closed); this path never falls back to
+   the CPU.  Any
    msg_sz is accepted, as by the reference (4 GiB and more: the message is
    hashed on the host, fd_ed25519_hip_dropin_set_host_hash_min). */
 int
@@ -78,7 +81,7 @@ char const *
 fd_ed25519_strerror( int err );
 
 /* The drop-ins above serve any number of calling threads: concurrent calls
-   are coalesced into shared launches on the process's two drop-in engines
+   are coalesced into shared launches on the process's four drop-in engines
    (compact tables, 16K-signature chunks).  dropin_stats reports the
    launches made and the calls they carried; dropin_device_bytes the device
    memory the drop-ins hold (their engines plus the compact tables; it
@@ -98,6 +101,52 @@ fd_ed25519_hip_dropin_set_host_hash_min( unsigned long bytes );
 unsigned long
 fd_ed25519_hip_dropin_device_bytes( void );
 
+/* Failure policy of the drop-ins.  The reference's verify cannot fail: it
+   returns only the codes above (src/ballet/ed25519/fd_ed25519_user.c:
+   134-229), and its tile stops the process only on input it cannot trust
+   (FD_LOG_ERR, src/app/fdctl/run/tiles/fd_verify.c:67-68).  Here the GPU
+   can fail.  When a drop-in launch fails (a kernel launch, a copy, the
+   completion wait) -- or a drop-in engine cannot be created -- the failing
+   engine is deleted, created anew and the same launch run once more: a
+   transient failure costs the callers of that launch one retry and shows
+   only in fd_ed25519_hip_dropin_status's recovery count.  If the retry
+   fails as well, the device is lost to the drop-ins and the policy set
+   here decides:
+
+     FD_ED25519_HIP_DROPIN_ON_LOST_ABORT (the default): a message on stderr
+       naming the failure, then abort() -- fail-stop, as a tile that cannot
+       do its work stops the validator;
+     FD_ED25519_HIP_DROPIN_ON_LOST_REJECT: fail closed -- the calls of the
+       failed launch, the calls queued behind it and every later call return
+       FD_ED25519_ERR_SIG without touching the device, so no signature is
+       ever accepted unverified; fd_ed25519_hip_dropin_status reports the
+       loss, and the caller alerts, restarts the process or calls
+       fd_ed25519_hip_dropin_reset.
+
+   There is no CPU fallback in either case: the library has one verify
+   implementation, the GPU's.
+
+   set_on_lost returns the previous policy (FD_ED25519_HIP_ERR_INVAL for an
+   unknown one, nothing changed).  dropin_status returns 0 while the
+   drop-ins are usable, else the error code that lost the device (an
+   FD_ED25519_HIP_ERR_* code; fd_ed25519_hip_last_error in the thread that
+   lost it has the message), and the count of launches that succeeded on a
+   re-created engine in *recoveries (optional).  dropin_reset waits for the
+   launches in flight, deletes and re-creates every drop-in engine and, if
+   that succeeds, makes the drop-ins usable again: 0, or the creation's
+   error code (still lost). */
+#define FD_ED25519_HIP_DROPIN_ON_LOST_ABORT  (0)
+#define FD_ED25519_HIP_DROPIN_ON_LOST_REJECT (1)
+
+int
+fd_ed25519_hip_dropin_set_on_lost( int policy );
+
+int
+fd_ed25519_hip_dropin_status( unsigned long * recoveries );
+
+int
+fd_ed25519_hip_dropin_reset( void );
+
 /* ---- Part 2: batch engine -------------------------------------------- */
 
 typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
@@ -108,13 +157,15 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    vservice stats' device bytes, shlink liveness words; 4: a SUCCESS verdict
    frag carries the published frag's trailer only, the tile keeps the
    payload; 5: shlink protocol word and creator, vservice lifecycle and
-   end codes).  A consumer checks
+   end codes; 6: vservice links_per_thread; 7: vservice link_cpus; 8:
+   vservice stats' leaked_on_hang, the drop-ins' device-lost state).  A
+   consumer checks
    the library it loaded against the header it was built with:
    fd_ed25519_hip_abi_check( FD_ED25519_HIP_ABI_VERSION,
    sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
    sizeof(fd_ed25519_hip_vservice_stats_t) ) returns 0 when they agree,
    FD_ED25519_HIP_ERR_INVAL (with fd_ed25519_hip_last_error) when not. */
-#define FD_ED25519_HIP_ABI_VERSION (7U)
+#define FD_ED25519_HIP_ABI_VERSION (8U)
 
 unsigned
 fd_ed25519_hip_abi_version( void );

@@ -491,6 +491,9 @@ typedef struct {
   unsigned long device_bytes;   /* the link pair's own device memory (its vtile's) */
   unsigned long shared_device_bytes;   /* the process's base tables on the device, shared by every pair */
   int           end_code;       /* how the link pair ended: 0 (EOS) or its failure code */
+  unsigned      leaked_on_hang; /* 1: the pair ended under a GPU hang (FD_ED25519_HIP_ERR_TIMEOUT) and left its
+                                   engines and device memory unfreed -- freeing them waits on the hung device --
+                                   for the process exit to reclaim (the service exits at once) */
 } fd_ed25519_hip_vservice_stats_t;
 
 /* The GPU side of a sandboxed verify tile: consumes transaction payload

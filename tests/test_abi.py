@@ -151,4 +151,5 @@ def test_reference_tests_bind_to_the_dropin(prog, tmp_path):
     r = subprocess.run([os.path.join(DROPIN, prog)], capture_output=True, text=True, timeout=120, cwd=tmp_path,
                        env=dict(os.environ, TMPDIR=str(tmp_path), HIP_VISIBLE_DEVICES="-1"))
     assert r.returncode != 0
-    assert "libfd_ed25519_hip: FATAL: cannot create the GPU engine" in r.stderr, r.stderr[-2000:]
+    assert "libfd_ed25519_hip: FATAL: cannot create the drop-in GPU engines" in r.stderr, r.stderr[-2000:]
+    assert "(policy: abort)" in r.stderr, r.stderr[-2000:]

@@ -149,3 +149,133 @@ def test_two_ranks_stream_their_shards_and_agree():
 def test_a_failure_on_one_rank_fails_both(fail_rank, fail):
     out = _world2(800, fail_rank, fail)
     assert all(o[0] == "raised" and o[1].startswith("host stream failed on a rank") for o in out), out
+
+
+# ---- config_c4: the C4 stream leg of every default (C2) bench line --------
+
+C4_TOTAL = 4000
+
+
+def _c4_fakes(setattr_=setattr):
+    """bench.config_c4 with the GPU replaced: a DeviceWorkload fake that
+    writes C4's layout (the stream's own message sizes, seed 0xC4C4) and a
+    pool fake that recomputes each code from the window as laid out."""
+    import contextlib
+    from firedancer_amd import ed25519, tile, workload
+
+    class Buf:
+        def __init__(self, a):
+            self.a = a
+
+        def download_into(self, dst):
+            dst[:] = self.a
+
+        def download(self, dtype, n):
+            return self.a[:n].astype(dtype)
+
+    class DeviceWorkload:
+        def __init__(self, eng, m, lo, hi, ppm, seed, index_base):
+            g = np.arange(index_base, index_base + m, dtype=np.uint64)
+            sz = workload.msg_sizes(seed, index_base, m, lo, hi)
+            self.msg_bytes = int(sz.sum())
+            self.msgs = Buf(np.repeat(((g * np.uint64(7) + np.uint64(1)) % np.uint64(256)).astype(np.uint8), sz))
+            s = np.zeros((m, 64), np.uint8)
+            s[:, :8] = g.view(np.uint8).reshape(m, 8)
+            s[:, 8] = _code(g).view(np.uint8)
+            self.sigs, self.pubs = Buf(s.reshape(-1)), Buf(np.zeros(32 * m, np.uint8))
+            self.expect = Buf(_code(g))
+
+        def free(self):
+            pass
+
+    class Pool:
+        def __init__(self, *a):
+            pass
+
+        def run(self, msgs, off, sz, sigs, pubs, out):
+            s = sigs.reshape(-1, 64)
+            for i in range(len(out)):
+                g = int(s[i, :8].view(np.uint64)[0])
+                ok = int(sz[i]) == int(workload.msg_sizes(SEED, g, 1, 64, 1232)[0]) and \
+                    bool((msgs[int(off[i]):int(off[i]) + int(sz[i])] == (7 * g + 1) % 256).all())
+                out[i] = s[i, 8].view(np.int8) if ok else 99
+            return out, 0.001, {"h2d_bytes": 760 * len(out), "direct_batches": 1, "staged_batches": 0}
+
+        def close(self):
+            pass
+
+    class Near:
+        cpus = [0]
+
+        def __init__(self, info):
+            pass
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+    setattr_(ed25519, "DeviceWorkload", DeviceWorkload)
+    setattr_(tile, "Pool", Pool)
+    setattr_(tile, "NearDevice", Near)
+    setattr_(tile, "HostRegistration", lambda *a: contextlib.nullcontext())
+    setattr_(tile, "h2d_gbps", lambda *a: 57.0)
+
+
+class _Args:
+    c4_signatures = C4_TOTAL
+    host_window = 900
+    host_batch = 256
+    host_slots = 2
+
+
+def _c4_whole_digest():
+    return hashlib.sha256(_code(np.arange(C4_TOTAL, dtype=np.uint64)).tobytes()).hexdigest()
+
+
+def _c4_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import bench
+    from firedancer_amd import workload
+    _c4_fakes()
+    workload.CONFIGS["C4"] = dict(workload.CONFIGS["C4"])
+    bench.C4_STREAM_DIGEST = _c4_whole_digest()   # the fake stream's own whole-stream digest
+    r, _, w = bench.dist_setup(world)
+    res = bench.config_c4(None, 0, {}, r, w, _Args())
+    bench.barrier(w)
+    import torch.distributed as dist
+    dist.destroy_process_group()
+    q.put((r, res))
+
+
+def test_config_c4_one_rank_carries_the_whole_stream_digest(monkeypatch):
+    import bench
+    _c4_fakes(monkeypatch.setattr)
+    monkeypatch.setattr(bench, "C4_STREAM_DIGEST", _c4_whole_digest())
+    res = bench.config_c4(None, 0, {}, 0, 1, _Args())
+    assert res["digest_equal"] is True and res["stream_digest"] == _c4_whole_digest()
+    assert res["scaling"] == "strong" and res["signatures_per_rank"] == C4_TOTAL
+    assert res["label_mismatches"] == 0 and res["rank_digests"] == [res["stream_digest"]]
+    assert res["frac_of_pcie_bound"] is not None and res["peak_rss_bytes_max_over_ranks"] > 0
+
+
+def test_config_c4_two_ranks_agree_on_the_concatenated_digest():
+    """World 2 (gloo): the config_c4 key is present on both ranks, each
+    streamed its own half, and both report the same concatenated digest,
+    equal to the one-rank stream's (digest_equal true)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [o for _, o in sorted(q.get(timeout=180) for _ in procs)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r["digest_equal"] is True for r in res), res
+    assert res[0]["stream_digest"] == res[1]["stream_digest"] == _c4_whole_digest()
+    assert res[0]["rank_digests"] == res[1]["rank_digests"] and len(res[0]["rank_digests"]) == 2
+    assert all(r["signatures_per_rank"] == C4_TOTAL // 2 and r["n_gpus"] == 2 for r in res)

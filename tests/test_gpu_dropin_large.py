@@ -68,8 +68,12 @@ def test_host_hashed_dropins_match_the_reference_codes(ed, vectors, oracle):
 def test_message_past_4gib_is_verified_whole(ed, oracle):
     """4 GiB + 1000 bytes: the drop-in accepts the signature, rejects it
     with ERR_MSG once a byte past the 4 GiB mark changes, and agrees with
-    the reference's fd_ed25519_verify (compiled from its sources) on both."""
+    the reference's fd_ed25519_verify (compiled from its sources) on both.
+    The test hook's limit is set above 4 GiB first: it is
+    clamped, and a size the device's 32-bit lengths would truncate is
+    hashed on the host whatever the limit says."""
     ed25519, lib = ed
+    lib.fd_ed25519_hip_dropin_set_host_hash_min(1 << 40)
     ref_path = os.path.join(REPO, "oracle", "_ref", "libfdref_avx512.so")
     sz = (1 << 32) + 1000
     m = mmap.mmap(-1, sz, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)

@@ -82,3 +82,120 @@ def test_service_marks_links_failed_on_launch_failure(tmp_path, per_thread):
     # it never got a verdict that was not SUCCESS (the stream is all valid);
     # it wrote nothing (it exits before its output on a failure)
     assert len(pout) == 0 or (np.frombuffer(pout[:2000], np.int8) == 0).all()
+
+
+SERVICE_BIN = os.path.join(REPO, "firedancer_amd", "_lib", "fd_verify_hip_service")
+
+
+def test_service_exits_on_a_gpu_hang_without_waiting_on_the_device(tmp_path):
+    """a hung GPU must not hang the service.  The fault-injection
+    build holds the third batch on the device for 4 s (a bounded stand-in
+    for a hang: one sleeping wave that exits on its own) and the service's
+    hang bound is 0.5 s: the service must mark every link failed
+    (FD_ED25519_HIP_ERR_TIMEOUT on the tile's pair, STOPPED on the idle
+    second tile's), print its JSON line with gpu_hang true and exit with
+    status 2 well before the stalled batch would have finished -- freeing
+    its engines, or the HIP runtime's teardown, would wait on the device."""
+    if not os.path.exists(FAULT_LIB):
+        pytest.fail(f"{FAULT_LIB} not built (make -C firedancer_amd/csrc)")
+    from firedancer_amd import ed25519, tile, workload
+    eng = ed25519.Engine(0, max_chunk=1 << 14)
+    pay, _ = workload.txn_payloads(eng, 3000, 4343, msg_sz=200)
+    eng.close()
+    path = str(tmp_path / "payloads.bin")
+    tile.write_payload_file(path, pay)
+    libdir = tmp_path / "lib"
+    libdir.mkdir()
+    (libdir / "libfd_ed25519_hip.so").symlink_to(FAULT_LIB)   # the name the service's RUNPATH loads
+    env = dict(os.environ, LD_LIBRARY_PATH=str(libdir), FD_ED25519_HIP_FAULT_STALL_MS="4000")
+    prefix = f"/fdh_{uuid.uuid4().hex[:10]}_"
+    svc = subprocess.Popen([SERVICE_BIN, "--prefix", prefix, "--tiles", "2", "--batch", "256", "--slots", "3",
+                            "--gpu-hang-ms", "500", "--no-parent-watch"], stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, env=env, text=True)
+    prod = None
+    try:
+        line = svc.stdout.readline()
+        assert line.startswith("ready 2"), (line, svc.stderr.read()[-2000:] if svc.poll() is not None else "")
+        txl, vdl = tile.ShLink(prefix + "0_txn"), tile.ShLink(prefix + "0_vd")
+        tx2, vd2 = tile.ShLink(prefix + "1_txn"), tile.ShLink(prefix + "1_vd")
+        t0 = time.time()
+        prod = subprocess.Popen([tile.PRODUCER_BIN, txl.name, vdl.name, path], stdout=subprocess.PIPE,
+                                stderr=subprocess.PIPE)
+        sout, serr = svc.communicate(timeout=30)
+        dt = time.time() - t0
+        pout, perr = prod.communicate(timeout=30)
+        status, status2 = (txl.status(), vdl.status()), (tx2.status(), vd2.status())
+        left = [f for f in os.listdir("/dev/shm") if f.startswith(prefix[1:])]
+        for link in (txl, vdl, tx2, vd2):
+            link.close(unlink=False)
+    finally:
+        for p in (prod, svc):
+            if p is not None and p.poll() is None:
+                p.kill()
+        for f in os.listdir("/dev/shm"):
+            if f.startswith(prefix[1:]):
+                os.unlink(os.path.join("/dev/shm", f))
+    if prod.returncode == 3:
+        pytest.skip(f"seccomp strict mode unavailable: {perr.decode()}")
+    assert svc.returncode == 2, (svc.returncode, serr[-2000:])
+    assert "did not complete within 0.5 s (GPU hang)" in serr and "exiting without device teardown" in serr, serr[-2000:]
+    import json
+    res = json.loads(sout.strip().splitlines()[-1])
+    assert res["gpu_hang"] is True and res["end_codes"] == [-110, tile.SHLINK_FAIL_STOPPED], res
+    assert status == (-110, -110) and status2 == (tile.SHLINK_FAIL_STOPPED, tile.SHLINK_FAIL_STOPPED), (status, status2)
+    # out within the hang bound and a margin, not after the 4 s the device holds the batch
+    assert dt < 3.5, dt
+    assert prod.returncode == 4 and b"marked a link failed" in perr, (prod.returncode, perr.decode())
+    # the links' names went with the service (the mappings joined above stay valid until closed)
+    assert not left, left
+
+
+def test_zero_copy_count_changed_after_staging_is_a_parse_failure(tmp_path):
+    """in zero-copy mode the host reads a payload's signature
+    count (byte 0) from the live room when it stages the frag, the device
+    parses the bytes the batch DMAs later.  The fault-injection build makes
+    every 5th frag's count read as 12 at staging (as if the tile had
+    rewritten byte 0 between the two reads and back): the device must
+    reject those transactions as parse failures -- it copies signatures
+    only from what its own parse validated -- and every other verdict is
+    the one the stream has anyway (SUCCESS)."""
+    if not os.path.exists(FAULT_LIB):
+        pytest.fail(f"{FAULT_LIB} not built (make -C firedancer_amd/csrc)")
+    from firedancer_amd import ed25519, tile, workload
+    n = 1500
+    eng = ed25519.Engine(0, max_chunk=1 << 14)
+    pay, _ = workload.txn_payloads(eng, n, 4444, msg_sz=200)
+    eng.close()
+    path = str(tmp_path / "payloads.bin")
+    tile.write_payload_file(path, pay)
+    libdir = tmp_path / "lib"
+    libdir.mkdir()
+    (libdir / "libfd_ed25519_hip.so").symlink_to(FAULT_LIB)
+    env = dict(os.environ, LD_LIBRARY_PATH=str(libdir), FD_ED25519_HIP_FAULT_ZC_COUNT="12")
+    prefix = f"/fdz_{uuid.uuid4().hex[:10]}_"
+    svc = subprocess.Popen([SERVICE_BIN, "--prefix", prefix, "--tiles", "1", "--batch", "256", "--slots", "3",
+                            "--zero-copy", "--no-parent-watch"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           env=env, text=True)
+    prod = None
+    try:
+        line = svc.stdout.readline()
+        assert line.startswith("ready 1"), (line, svc.stderr.read()[-2000:] if svc.poll() is not None else "")
+        prod = subprocess.Popen([tile.PRODUCER_BIN, prefix + "0_txn", prefix + "0_vd", path], stdout=subprocess.PIPE,
+                                stderr=subprocess.PIPE)
+        pout, perr = prod.communicate(timeout=120)
+        sout, serr = svc.communicate(timeout=60)
+    finally:
+        for p in (prod, svc):
+            if p is not None and p.poll() is None:
+                p.kill()
+        for f in os.listdir("/dev/shm"):
+            if f.startswith(prefix[1:]):
+                os.unlink(os.path.join("/dev/shm", f))
+    if prod.returncode == 3:
+        pytest.skip(f"seccomp strict mode unavailable: {perr.decode()}")
+    assert prod.returncode == 0 and svc.returncode == 0, (prod.returncode, perr.decode()[-1000:], svc.returncode,
+                                                          serr[-2000:])
+    v = np.frombuffer(pout[:n], np.int8)
+    tampered = np.arange(n) % 5 == 2
+    assert (v[tampered] == tile.TXN_PARSE_FAILED).all(), np.unique(v[tampered], return_counts=True)
+    assert (v[~tampered] == 0).all(), np.unique(v[~tampered], return_counts=True)

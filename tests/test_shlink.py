@@ -392,3 +392,25 @@ def test_heartbeat_watch():
         assert w.check(link, 10_150 * ms, 100 * ms) == 0
     finally:
         link.close()
+
+
+def test_a_live_creators_link_is_not_reclaimed_whatever_its_pid_says():
+    """a pid is not meaningful across PID namespaces.  The
+    creator's claim is an exclusive flock held on the link's object for the
+    link's lifetime: a creator whose recorded pid names no process here (as
+    a live service in another PID namespace would look) still keeps its
+    link, and create refuses with EEXIST; once the creator closes it the
+    name is free."""
+    name = f"/fdt_ns_{uuid.uuid4().hex[:12]}"
+    link = tile.ShLink(name, 64, create=True)
+    try:
+        _hdr_word(name, SHLINK_HDR_CREATOR_OFF, (1 << 31) - 7)   # no such process in this namespace
+        with pytest.raises(tile.HipError, match="EEXIST"):
+            tile.ShLink(name, 64, create=True)
+        peer = tile.ShLink(name)   # the link itself still works for its peers
+        peer.close()
+    finally:
+        link.close()
+    assert not os.path.exists("/dev/shm" + name)
+    again = tile.ShLink(name, 64, create=True)
+    again.close()

@@ -179,7 +179,19 @@ main( int argc, char ** argv ) {
   stream_t st = { pay, off, sz };
   unsigned long long pf_pub = 0ULL, pf_take = 0ULL, pf_wait = 0ULL, pf_c = profile ? __rdtsc() : 0ULL, pf_n;
 #define PF( acc ) do { if( profile ) { pf_n = __rdtsc(); acc += pf_n - pf_c; pf_c = pf_n; } } while(0)
+  /* unanswered frags stay below the txn link's depth, as the tile's cap
+     does (integration/fd_verify_hip.c): a zero-copy service hands credits
+     back when it stages a frag, and the room itself is reused only after
+     the verdict, so a producer limited by credits alone could overwrite a
+     payload before its batch reached the GPU */
+  unsigned long depth = fd_ed25519_hip_shlink_depth( txl );
   while( i<n ) {
+    if( i - got>=depth ) {
+      if( take_verdicts( vdl, buf, verdict, n, &got, &eos, &fr, &st ) || eos ) leave( 2 );
+      PF( pf_take );
+      if( i - got>=depth ) { watch( &wt ); PF( pf_wait ); }
+      continue;
+    }
     int r = fd_ed25519_hip_shlink_publish( txl, pay + off[ i ], sz[ i ], i, 0U );
     PF( pf_pub );
     if( r==0 ) {
