@@ -120,12 +120,21 @@ typedef struct {
                                       full-length items by a scan of hflag          */
   int              bw_bits;        /* radix of btab_lo / btab_hi: FD_ED25519_BTABW_BITS or
                                       FD_ED25519_BTABC_BITS (compact)                 */
+  /* A/B build only (-DFD_ED25519_AB_LDS_BASE=1): the base
+     tables staged in LDS instead, [0..256)B and [0..256)[2^136]B, 32 KiB
+     each, radix-2^8 unsigned digits of s' split at 2^136 */
+  int32_t const *  btab8_lo;
+  int32_t const *  btab8_hi;
 } fd_ed25519_verify_params_t;
+
+#define FD_ED25519_BTAB8_SHIFT 136   /* A/B LDS tables: s' = lo (17 digits) + 2^136 hi (15 digits) */
 
 /* All launchers are asynchronous on `stream` (a hipStream_t) and return a
    hipError_t value (0 on success). */
 int fd_ed25519_hip_launch_gen_btab( int32_t * d_btab, void * stream );
 int fd_ed25519_hip_launch_gen_btab16( int32_t * d_btab16, int base_doublings, void * stream );
+/* [0..256)[2^base_doublings]B, 128-byte entries (the LDS A/B's tables) */
+int fd_ed25519_hip_launch_gen_btab8( int32_t * d_tab, int base_doublings, void * stream );
 /* [0..2^bits)[2^base_doublings]B into d_tab (bits FD_ED25519_BTABW_BITS or
    FD_ED25519_BTABC_BITS); d_scratch holds 2^bits*10 + 40 int32 */
 int fd_ed25519_hip_launch_gen_btabw( int32_t * d_tab, int base_doublings, int bits, int32_t * d_scratch, void * stream );

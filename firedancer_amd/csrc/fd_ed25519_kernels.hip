@@ -392,6 +392,9 @@ FD_DEV bool half_pair_ok(const uint32_t (&k)[8], const uint32_t (&c)[FD_HALF_TW]
    items and a bit of |d| above bit 0 for another 1/8, after the search and
    before the check, so that the check -- not luck -- keeps the verdicts
    bit-exact (tests/test_gpu_halfcheck.py). */
+#ifndef FD_ED25519_AB_LDS_BASE
+#define FD_ED25519_AB_LDS_BASE 0
+#endif
 #ifndef FD_ED25519_HALF_FAULT
 #define FD_ED25519_HALF_FAULT 0
 #endif
@@ -705,6 +708,90 @@ FD_DEV int dsm_half_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
   return code;
 }
 
+#if FD_ED25519_AB_LDS_BASE
+/* A/B build only ("tables staged in LDS"): the base
+   tables in LDS.  2 x 256 entries x 128 B = 64 KiB per block, i.e. radix
+   2^8: s' = s_lo + 2^144 s_hi is re-split at 2^136 into 17 + 15 unsigned
+   8-bit digits at windows 32, 30, .., 0 and 28, .., 0 -- 32 mixed
+   additions from LDS against 11 from the 2 x 2 GiB HBM tables.  Same
+   lane tables, doublings and identity test as dsm_half_one. */
+FD_DEV int dsm_half_one_lds(const fd_ed25519_verify_params_t& p, uint64_t j, int4* tabA, int4* tabR,
+                            const int4* s_lo8, const int4* s_hi8) {
+  int code = precheck(p, j);
+  const uint32_t hf = p.hflag[j];
+  {
+    fe x, y;
+    load_pt(x, y, p, 0, j);
+    table_build<true, true>(tabA, x, y, true);
+    load_pt(x, y, p, 1, j);
+    table_build<true, true>(tabR, x, y, !(hf & FD_HF_DNEG));
+  }
+  uint32_t cd[5], dd[5], ld[5], hd[5];
+  int W = 33;
+  {
+    uint32_t x[5], t[5], sl[5], sh[5];
+    load_hs(x, p, 5, 5, j);
+    const int wl = (fd_half_bitlen<5>(x) + 4) >> 2;
+#pragma unroll
+    for (int w = 34; w <= (FD_HALF_DBITS_MAX + 4) / 4; w++) W += __ballot(wl >= w) != 0ull;
+    const int shv = 160 - 4 * W;
+    shl160v(t, x, shv); recode160<4>(dd, t);
+    load_hs(x, p, 0, 5, j);  shl160v(t, x, shv); recode160<4>(cd, t);
+    load_hs(sl, p, 10, 5, j);
+    load_hs(sh, p, 15, 4, j);
+    static_assert(FD_ED25519_BTABW_SHIFT - FD_ED25519_BTAB8_SHIFT == 8, "re-split of s' by one byte");
+    uint32_t lo[5] = {sl[0], sl[1], sl[2], sl[3], sl[4] & 0xffu};
+    uint32_t hi[5] = {(sl[4] >> 8) | (sh[0] << 8), (sh[0] >> 24) | (sh[1] << 8), (sh[1] >> 24) | (sh[2] << 8),
+                      (sh[2] >> 24) | (sh[3] << 8), sh[3] >> 24};
+    shl160<160 - 17 * 8>(ld, lo);
+    shl160<160 - 15 * 8>(hd, hi);
+  }
+  ge_p3 P;
+  ge_p3_0(P);
+  ge_p1p1 Rt;
+  ge_p2 Q;
+#pragma clang loop unroll(disable)
+  for (int it = W - 1; it >= 0; it--) {
+    int ea = pop160<4>(cd), er = pop160<4>(dd);
+    if (it == W - 1) { ea &= 15; er &= 15; }
+    ge_cached ca, cr;
+    const bool blo = it <= 32 && !(it & 1), bhi = it <= 28 && !(it & 1);
+    ge_precomp b1, b2;
+    atab_load(ca, tab_entry<true>(tabA, ea), 0);
+    if (it != W - 1) {
+#pragma clang loop unroll(disable)
+      for (int dbl = 0; dbl < 4; dbl++) {
+        ge_p2_dbl(Rt, Q);
+        if (dbl < 3) ge_p1p1_to_p2(Q, Rt);
+      }
+      ge_p1p1_to_p3_u(P, Rt);
+    }
+    atab_load(cr, tab_entry<true>(tabR, er), 0);
+    ge_cached_cneg(ca, ea < 0);
+    ge_add<true>(Rt, P, ca);
+    ge_p1p1_to_p3_u(P, Rt);
+    if (blo) btab16_load(b1, s_lo8, (int)pop160u<8>(ld));
+    if (bhi) btab16_load(b2, s_hi8, (int)pop160u<8>(hd));
+    ge_cached_cneg(cr, er < 0);
+    ge_add<true>(Rt, P, cr);
+    if (blo) {
+      ge_p1p1_to_p3_uxyt(P, Rt);
+      ge_madd(Rt, P, b1);
+    }
+    if (bhi) {
+      ge_p1p1_to_p3_uxyt(P, Rt);
+      ge_madd(Rt, P, b2);
+    }
+    ge_p1p1_to_p2(Q, Rt);
+  }
+  fe t;
+  fe_sub(t, Q.Y, Q.Z);
+  const bool ident = fe_iszero(Q.X) && fe_iszero(t);
+  if (code == FD_PENDING) code = ident ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  return code;
+}
+#endif
+
 /* The reference's own form, for the few signatures whose k has no
    half-size pair: R' = [k](-A) + [S]B with k in radix 16 (252 doublings,
    64 additions of [0..8](-A)) and S in radix 2^16 (16 mixed additions),
@@ -783,6 +870,16 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
   int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + wave * FD_ED25519_ATAB_BYTES_PER_WAVE) +
                lane * (2 * FD_ED25519_ATAB_STRIDE * 10);
   int4* tabR = tabA + FD_ED25519_ATAB_STRIDE * 10;   /* the full-length form uses tabA's 9 entries, into tabR's space */
+#if FD_ED25519_AB_LDS_BASE
+  __shared__ int4 s_b8[2 * 256 * (FD_ED25519_BTAB16_STRIDE / 4)];
+  {
+    const int4* g_lo = reinterpret_cast<const int4*>(p.btab8_lo);
+    const int4* g_hi = reinterpret_cast<const int4*>(p.btab8_hi);
+    constexpr int N = 256 * (FD_ED25519_BTAB16_STRIDE / 4);
+    for (int i = threadIdx.x; i < N; i += blockDim.x) { s_b8[i] = g_lo[i]; s_b8[N + i] = g_hi[i]; }
+    __syncthreads();
+  }
+#endif
   if (p.small) {
     /* after dsm4: the full-length items only, found by their flag (a
        static stride: the work counter is not reset for small chunks) */
@@ -805,7 +902,12 @@ fd_ed25519_dsm_kernel(fd_ed25519_verify_params_t p) {
       p.out[p.base + j] = (int8_t)dsm_full_one(p, j, tabA);
     } else if (t >= head && t < total) {
       const uint64_t j = t - head;
+#if FD_ED25519_AB_LDS_BASE
+      if (!(p.hflag[j] & FD_HF_FULL))
+        p.out[p.base + j] = (int8_t)dsm_half_one_lds(p, j, tabA, tabR, s_b8, s_b8 + 256 * (FD_ED25519_BTAB16_STRIDE / 4));
+#else
       if (!(p.hflag[j] & FD_HF_FULL)) p.out[p.base + j] = (int8_t)dsm_half_one<BW>(p, j, tabA, tabR);
+#endif
     }
   }
 }
@@ -1277,6 +1379,12 @@ extern "C" int fd_ed25519_hip_launch_stall(unsigned ms, void* stream) {
 extern "C" int fd_ed25519_hip_launch_gen_btab(int32_t* d_btab, void* stream) {
   hipLaunchKernelGGL(fd_ed25519_gen_btab_kernel, dim3(3), dim3(64), 0, (hipStream_t)stream, d_btab,
                      FD_ED25519_BTAB_ENTRIES, FD_ED25519_BTAB_STRIDE, 8, 0);
+  return (int)hipGetLastError();
+}
+
+extern "C" int fd_ed25519_hip_launch_gen_btab8(int32_t* d_tab, int base_dbl, void* stream) {
+  hipLaunchKernelGGL(fd_ed25519_gen_btab_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, d_tab, 256,
+                     FD_ED25519_BTAB16_STRIDE, 8, base_dbl);
   return (int)hipGetLastError();
 }
 

@@ -47,6 +47,7 @@ struct fd_ed25519_hip_engine {
 
   int32_t *    d_btab;
   int32_t *    d_btab16;     /* [0..2^15]B, the verify kernels' wide B table  */
+  int32_t *    d_btab8[2];   /* A/B build only (FD_ED25519_AB_LDS_BASE): the LDS-staged tables */
   int32_t *    btabw[2];    /* shared per device: [0..2^24)B, [0..2^24)[2^144]B */
   /* Pipeline lanes: the per-chunk scratch of a chunk in flight, and the
      streams its phases run on.  Lane 0 runs on the caller's stream (or the
@@ -316,7 +317,7 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
     if( e->lane[l].stream ) hipStreamSynchronize( e->lane[l].stream );
     if( e->lane[l].side   ) hipStreamSynchronize( e->lane[l].side );
   }
-  hipFree( e->d_btab ); hipFree( e->d_btab16 );
+  hipFree( e->d_btab ); hipFree( e->d_btab16 ); hipFree( e->d_btab8[0] ); hipFree( e->d_btab8[1] );
   for( int l=0; l<2; l++ ) { hipFree( e->lane[l].d_atab ); hipFree( e->lane[l].d_work ); }
   if( e->btabw[0] ) btabw_release( e->device, engine_btab_kind( e ) );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
@@ -463,6 +464,13 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   if( err ) return hip_fail( (hipError_t)err, "gen_btab launch" );
   err = fd_ed25519_hip_launch_gen_btab16( e->d_btab16, 0, e->stream );
   if( err ) return hip_fail( (hipError_t)err, "gen_btab16 launch" );
+#ifdef FD_ED25519_AB_LDS_BASE
+  for( int t=0; t<2; t++ ) {
+    HIPCHK( hipMalloc( (void **)&e->d_btab8[t], sizeof(int32_t) * 256UL * FD_ED25519_BTAB16_STRIDE ), "hipMalloc(btab8)" );
+    err = fd_ed25519_hip_launch_gen_btab8( e->d_btab8[t], t ? FD_ED25519_BTAB8_SHIFT : 0, e->stream );
+    if( err ) return hip_fail( (hipError_t)err, "gen_btab8 launch" );
+  }
+#endif
   HIPCHK( hipStreamSynchronize( e->stream ), "gen_btab" );
   int32_t * tw[2] = { NULL, NULL };
   err = btabw_acquire( e->device, engine_btab_kind( e ), e->stream, tw );
@@ -623,6 +631,7 @@ verify_common( fd_ed25519_hip_engine_t * e, unsigned long n,
   p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
   p.cap = e->max_chunk;
   p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab_lo = e->btabw[0]; p.btab_hi = e->btabw[1];
+  p.btab8_lo = e->d_btab8[0]; p.btab8_hi = e->d_btab8[1];
   p.bw_bits = engine_btab_kind( e ) ? FD_ED25519_BTABC_BITS : FD_ED25519_BTABW_BITS;
   p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   p.half_dbits     = engine_half_dbits( e );

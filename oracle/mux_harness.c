@@ -1,6 +1,6 @@
 /* mux_harness.c -- TEST INFRASTRUCTURE ONLY (oracle/Makefile ref-mux).
 
-   Runs one verify tile -- the reference's own fd_tile_verify
+   Runs verify tiles -- the reference's own fd_tile_verify
    (src/app/fdctl/run/tiles/fd_verify.c:230-244, compiled from its sources,
    CPU verify) or the accelerated fd_tile_verify_hip
    (integration/fd_verify_hip.c, GPU service behind shared-memory links) --
@@ -13,26 +13,38 @@
      reference's run loop, src/disco/mux/fd_mux.c:90-710) with the tile's
      mux_flags, burst and callbacks,
 
-   over a topology with the quic -> verify link (mcache + compact dcache of
-   FD_TPU_MTU frags, reliable, fseq flow control) and the verify -> dedup
-   link (FD_TPU_DCACHE_MTU frags).  round_robin_cnt verify tiles exist in
-   the topology; the one of kind id round_robin_idx runs.  A producer thread
-   publishes the payloads of a file into the in link with the reference's
-   fd_mcache_publish (sig = seq, at an optional rate); a consumer thread is
-   the dedup tile's side: it reads every published frag (sig, sz, bytes)
-   and returns credits through its fseq.
+   over the topology fdctl builds for them (src/app/fdctl/topology.c: one
+   quic -> verify link that every verify tile reads, each with its own
+   reliable fseq, keeping the frags with seq % verify_tile_count == its
+   kind id, fd_verify.c:36-47; one verify -> dedup link per verify tile,
+   all read by the dedup tile).  A producer thread is the quic tile: it
+   publishes the payloads of a file into the shared link with the
+   reference's fd_mcache_publish (sig = seq, at an optional rate), its
+   credits the minimum over every verify tile's fseq (fd_fctl's rule for
+   reliable consumers).  A consumer thread is the dedup tile's side: it
+   polls every verify -> dedup link in turn, reads each published frag (sig,
+   sz, bytes) and returns credits through that link's fseq.
 
      mux_harness verify|verify_hip PAYLOADS OUT [--app NAME] [--depth D]
-                 [--rr-cnt N] [--rr-idx I] [--no-sandbox] [--rate TXN_PER_S]
-                 [--timeout S] [--lat-out FILE]
+                 [--tiles K | --rr-cnt N --rr-idx I] [--no-sandbox]
+                 [--rate TXN_PER_S] [--timeout S] [--lat-out FILE]
+                 [--cpus LIST]
+
+   --tiles K: K verify tiles (kind ids 0..K-1) each run on a thread of its
+   own (default 1).  --rr-cnt N --rr-idx I: the topology has N verify tiles
+   and only the one of kind id I runs (it sees every frag and keeps its
+   share; the producer's credits are that tile's).  --cpus LIST (e.g.
+   8-19 or 8,9,12): the producer, the consumer and tile k run on the 1st,
+   2nd and (k+3)-th CPU of the list, as fdctl pins each tile to a core.
 
    PAYLOADS: u64 n, n x u32 sizes, the payloads.  OUT: every published frag
-   in order as u64 sig, u32 sz, sz bytes.  stdout: one JSON line of
-   counts.  The run ends when the tile has consumed every frag and has
-   nothing pending (fd_verify_hip_pending for the accelerated tile), the
-   consumer has drained the out link, and the tile has halted on its cnc;
-   the accelerated tile's txn link then carries the end-of-stream frag, so
-   the GPU service exits.  A tile that stops (FD_LOG_ERR inside the
+   in the order the consumer took it (per out link in order, the links
+   interleaved as polled) as u64 sig, u32 sz, sz bytes.  stdout: one JSON
+   line of counts.  The run ends when every tile has consumed every frag and
+   has nothing pending (fd_verify_hip_pending for the accelerated tile), the
+   consumer has drained every out link, and every tile has halted on its
+   cnc; each accelerated tile's txn link then carries the end-of-stream
+   frag, so the GPU service exits.  A tile that stops (FD_LOG_ERR inside the
    sandbox) ends the process; exit status 3 on the harness's own timeout.
 
    Latency (SURVEY.md §8(d) C5 on the deployed path): each frag's tsorig
@@ -44,7 +56,7 @@
    side, takes now - fd_frag_meta_ts_decomp( tsorig ) for every frag it
    receives: due time -> verified frag on the out link.  The JSON line
    carries p50 / p99 / max in microseconds; --lat-out writes every sample
-   (u32 nanoseconds, in publish order). */
+   (u32 nanoseconds, in the order received). */
 
 #define _GNU_SOURCE
 #include "disco/tiles.h"
@@ -54,6 +66,7 @@
 #include <linux/filter.h>
 #include <linux/seccomp.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -67,6 +80,7 @@ ulong fd_verify_hip_pending( void const * ctx );
 fd_ed25519_hip_shlink_t * fd_verify_hip_txn_link( void * ctx );
 
 #define OUT_BURST (16UL)
+#define TILE_MAX  (16UL)
 
 static double
 now_s( void ) {
@@ -93,58 +107,94 @@ woff( void const * p ) {
   return (ulong)((uchar const *)p - g_mem);
 }
 
-typedef struct {
+typedef struct harness harness_t;
+
+typedef struct {               /* one running verify tile */
+  harness_t *          h;
+  ulong                k;      /* its kind id */
+  fd_topo_tile_t *     tile;
+  fd_frag_meta_t *     out_mcache;  uchar * out_dcache;  ulong * out_fseq;
+  ulong *              in_fseq;
+  fd_cnc_t *           cnc;
+  void *               scratch;
+  void *               mux_scratch;
+  void *               ctx;
+  int                  cpu;
+  volatile int         halted;
+  ulong                out_seq;   /* consumer: next out seq expected on this tile's link */
+} tile_run_t;
+
+struct harness {
   /* input */
   ulong            n;
   uchar const *    pay;
   ulong const *    off;
   uint const *     sz;
   double           rate;
-  /* links */
-  fd_frag_meta_t * in_mcache;   ulong in_depth;  uchar * in_dcache;  ulong * in_fseq;
-  fd_frag_meta_t * out_mcache;  ulong out_depth; uchar * out_dcache; ulong * out_fseq;
-  /* tile */
+  /* the shared quic -> verify link */
+  fd_frag_meta_t * in_mcache;   ulong in_depth;  uchar * in_dcache;
+  ulong            out_depth;
+  /* tiles */
   fd_topo_t *          topo;
-  fd_topo_tile_t *     tile;
   fd_topo_run_tile_t * run;
-  void *               scratch;
-  void *               mux_scratch;
-  fd_cnc_t *           cnc;
+  tile_run_t           t[ TILE_MAX ];
+  ulong                t_cnt;
   int                  sandbox;
-  void *               ctx;
-  volatile int         tile_booted;
-  volatile int         tile_halted;
+  int                  cpu_prod, cpu_cons;
   /* consumer output */
   uchar *          res;
   ulong            res_used, res_cap;
   uint *           lat_ns;       /* per published frag: now - tsorig */
   double           tick_per_ns;
   volatile ulong   res_cnt;
-  volatile ulong   out_seq;      /* next out seq the consumer expects */
   volatile int     producer_done;
   volatile int     stop;
   volatile int     consumer_err;
-  ulong            credit_spins;   /* producer: pauses waiting for the tile's fseq (the tile is behind) */
-  ulong            idle_spins;     /* consumer: pauses with nothing published (the tile is not ahead) */
-} harness_t;
+  ulong            credit_spins;   /* producer: pauses waiting for the tiles' fseqs (a tile is behind) */
+  ulong            idle_spins;     /* consumer: passes over every out link with nothing published */
+};
+
+static void
+pin_cpu( int cpu ) {
+  if( cpu<0 ) return;
+  cpu_set_t set;
+  CPU_ZERO( &set );
+  CPU_SET( cpu, &set );
+  if( pthread_setaffinity_np( pthread_self(), sizeof(set), &set ) ) FD_LOG_ERR(( "cannot run on CPU %d", cpu ));
+}
+
+/* the slowest tile's fseq: the producer's credits (fd_fctl, reliable consumers) */
+static ulong
+min_fseq( harness_t const * h ) {
+  ulong m = fd_fseq_query( h->t[0].in_fseq );
+  for( ulong k=1UL; k<h->t_cnt; k++ ) {
+    ulong q = fd_fseq_query( h->t[k].in_fseq );
+    if( fd_seq_lt( q, m ) ) m = q;
+  }
+  return m;
+}
 
 static void *
 producer_main( void * arg ) {
   harness_t * h = (harness_t *)arg;
+  pin_cpu( h->cpu_prod );
   ulong chunk0 = fd_dcache_compact_chunk0( g_mem, h->in_dcache );
   ulong wmark  = fd_dcache_compact_wmark ( g_mem, h->in_dcache, FD_TPU_MTU );
   ulong chunk  = chunk0;
   double t0 = now_s();
   long   k0 = fd_tickcount();
   double tick_per_s = h->tick_per_ns*1e9;
+  ulong  cr = 0UL;   /* seq up to which the tiles have room (refreshed when used up) */
   for( ulong seq=0UL; seq<h->n && !h->stop; seq++ ) {
     long due = 0L;
     if( h->rate>0.0 ) {
       while( now_s() < t0 + (double)seq/h->rate ) FD_SPIN_PAUSE();
       due = k0 + (long)( (double)seq/h->rate*tick_per_s );
     }
-    /* credits: never more than depth frags ahead of the tile's fseq */
-    while( fd_seq_diff( seq, fd_fseq_query( h->in_fseq ) )>=(long)h->in_depth ) {
+    /* credits: never more than depth frags ahead of the slowest tile */
+    while( fd_seq_ge( seq, cr ) ) {
+      cr = min_fseq( h ) + h->in_depth;
+      if( fd_seq_lt( seq, cr ) ) break;
       if( h->stop ) return NULL;
       h->credit_spins++;
       FD_SPIN_PAUSE();
@@ -161,34 +211,41 @@ producer_main( void * arg ) {
   return NULL;
 }
 
-/* the dedup tile's side of the out link: every frag, in order */
+/* the dedup tile's side of the out links: every frag of each, in order */
 static void *
 consumer_main( void * arg ) {
   harness_t * h = (harness_t *)arg;
-  ulong seq = 0UL;
+  pin_cpu( h->cpu_cons );
   while( !h->stop ) {
-    fd_frag_meta_t const * m = h->out_mcache + fd_mcache_line_idx( seq, h->out_depth );
-    ulong s0 = FD_VOLATILE_CONST( m->seq );
-    long d = fd_seq_diff( s0, seq );
-    if( d<0L ) { h->idle_spins++; FD_SPIN_PAUSE(); continue; }
-    if( d>0L ) { h->consumer_err = 1; return NULL; }       /* overrun: the tile ignored our credits */
-    FD_COMPILER_MFENCE();
-    ulong sig = m->sig, chunk = m->chunk, sz = m->sz, tsorig = m->tsorig;
-    FD_COMPILER_MFENCE();
-    if( sz>FD_TPU_DCACHE_MTU || h->res_used + 12UL + sz>h->res_cap ) { h->consumer_err = 2; return NULL; }
-    uchar * r = h->res + h->res_used;
-    fd_memcpy( r, &sig, 8UL ); uint usz = (uint)sz; fd_memcpy( r+8, &usz, 4UL );
-    fd_memcpy( r+12, fd_chunk_to_laddr_const( g_mem, chunk ), sz );
-    FD_COMPILER_MFENCE();
-    if( FD_VOLATILE_CONST( m->seq )!=s0 ) { h->consumer_err = 3; return NULL; }
-    h->res_used += 12UL + sz;
-    long lat = fd_tickcount() - fd_frag_meta_ts_decomp( tsorig, fd_tickcount() );
-    double ns = (double)lat / h->tick_per_ns;
-    h->lat_ns[ h->res_cnt ] = ns<0.0 ? 0U : ns>4e9 ? 4000000000U : (uint)ns;
-    h->res_cnt++;
-    seq++;
-    h->out_seq = seq;
-    fd_fseq_update( h->out_fseq, seq );
+    int took = 0;
+    for( ulong k=0UL; k<h->t_cnt; k++ ) {
+      tile_run_t * t = &h->t[k];
+      ulong seq = t->out_seq;
+      fd_frag_meta_t const * m = t->out_mcache + fd_mcache_line_idx( seq, h->out_depth );
+      ulong s0 = FD_VOLATILE_CONST( m->seq );
+      long d = fd_seq_diff( s0, seq );
+      if( d<0L ) continue;
+      if( d>0L ) { h->consumer_err = 1; return NULL; }       /* overrun: the tile ignored our credits */
+      FD_COMPILER_MFENCE();
+      ulong sig = m->sig, chunk = m->chunk, sz = m->sz, tsorig = m->tsorig;
+      FD_COMPILER_MFENCE();
+      if( sz>FD_TPU_DCACHE_MTU || h->res_used + 12UL + sz>h->res_cap ) { h->consumer_err = 2; return NULL; }
+      uchar * r = h->res + h->res_used;
+      fd_memcpy( r, &sig, 8UL ); uint usz = (uint)sz; fd_memcpy( r+8, &usz, 4UL );
+      fd_memcpy( r+12, fd_chunk_to_laddr_const( g_mem, chunk ), sz );
+      FD_COMPILER_MFENCE();
+      if( FD_VOLATILE_CONST( m->seq )!=s0 ) { h->consumer_err = 3; return NULL; }
+      h->res_used += 12UL + sz;
+      long lat = fd_tickcount() - fd_frag_meta_ts_decomp( tsorig, fd_tickcount() );
+      double ns = (double)lat / h->tick_per_ns;
+      h->lat_ns[ h->res_cnt ] = ns<0.0 ? 0U : ns>4e9 ? 4000000000U : (uint)ns;
+      h->res_cnt++;
+      seq++;
+      FD_VOLATILE( t->out_seq ) = seq;
+      fd_fseq_update( t->out_fseq, seq );
+      took = 1;
+    }
+    if( !took ) { h->idle_spins++; FD_SPIN_PAUSE(); }
   }
   return NULL;
 }
@@ -196,14 +253,16 @@ consumer_main( void * arg ) {
 /* fd_topo_run_tile's sequence on this thread (src/disco/topo/fd_topo_run.c) */
 static void *
 tile_main( void * arg ) {
-  harness_t * h = (harness_t *)arg;
+  tile_run_t * t = (tile_run_t *)arg;
+  harness_t *  h = t->h;
+  pin_cpu( t->cpu );   /* before the sandbox: the affinity call is not in the tile's policy */
   fd_log_cpu_set( NULL );
   fd_log_thread_set( h->run==&fd_tile_verify ? "verify:ref" : "verify:hip" );
-  FD_LOG_NOTICE(( "booting tile" ));   /* as fd_topo_run_tile does: warms the logger (thread state, time zone) before the sandbox */
+  FD_LOG_NOTICE(( "booting tile %lu", t->k ));   /* as fd_topo_run_tile does: warms the logger (thread state, time zone) before the sandbox */
 
   if( h->sandbox && h->run->populate_allowed_seccomp ) {
     struct sock_filter filter[ 128 ];
-    ulong cnt = h->run->populate_allowed_seccomp( h->scratch, 128UL, filter );
+    ulong cnt = h->run->populate_allowed_seccomp( t->scratch, 128UL, filter );
     struct sock_fprog prog = { .len = (ushort)cnt, .filter = filter };
     /* this thread only (no TSYNC): the harness's other threads stay free to
        write the result; the tile itself runs under exactly its policy */
@@ -211,8 +270,8 @@ tile_main( void * arg ) {
       FD_LOG_ERR(( "seccomp filter install failed" ));
   }
 
-  fd_metrics_register( (ulong *)h->tile->metrics );
-  if( h->run->unprivileged_init ) h->run->unprivileged_init( h->topo, h->tile, h->scratch );
+  fd_metrics_register( (ulong *)t->tile->metrics );
+  if( h->run->unprivileged_init ) h->run->unprivileged_init( h->topo, t->tile, t->scratch );
 
   fd_mux_callbacks_t callbacks = {
     .during_housekeeping = h->run->mux_during_housekeeping,
@@ -223,16 +282,14 @@ tile_main( void * arg ) {
     .after_frag          = h->run->mux_after_frag,
     .metrics_write       = h->run->mux_metrics_write,
   };
-  h->ctx = h->run->mux_ctx ? h->run->mux_ctx( h->scratch ) : NULL;
   fd_frag_meta_t const * in_mcache[1] = { h->in_mcache };
-  ulong *                in_fseq[1]   = { h->in_fseq };
-  ulong *                out_fseq[1]  = { h->out_fseq };
+  ulong *                in_fseq[1]   = { t->in_fseq };
+  ulong *                out_fseq[1]  = { t->out_fseq };
   fd_rng_t rng[1];
-  h->tile_booted = 1;
-  int ret = fd_mux_tile( h->cnc, h->run->mux_flags, 1UL, in_mcache, in_fseq, h->out_mcache, 1UL, out_fseq,
-                         h->run->burst, 0UL, 0L, fd_rng_join( fd_rng_new( rng, 0U, 0UL ) ), h->mux_scratch, h->ctx,
-                         &callbacks );
-  h->tile_halted = ret ? -1 : 1;
+  int ret = fd_mux_tile( t->cnc, h->run->mux_flags, 1UL, in_mcache, in_fseq, t->out_mcache, 1UL, out_fseq,
+                         h->run->burst, 0UL, 0L, fd_rng_join( fd_rng_new( rng, (uint)t->k, 0UL ) ), t->mux_scratch,
+                         t->ctx, &callbacks );
+  t->halted = ret ? -1 : 1;
   /* a sandboxed thread may not even exit: park until the process ends */
   for(;;) FD_SPIN_PAUSE();
   return NULL;
@@ -255,11 +312,29 @@ cmp_uint( void const * a, void const * b ) {
   return x<y ? -1 : x>y;
 }
 
+/* "a,b,c-d" -> cpus (at most max); the count, or -1 */
+static int
+parse_cpus( char const * s, int * cpus, int max ) {
+  int n = 0;
+  while( *s ) {
+    char * e;
+    long a = strtol( s, &e, 10 ), b = a;
+    if( e==s || a<0 ) return -1;
+    if( *e=='-' ) { s = e + 1; b = strtol( s, &e, 10 ); if( e==s || b<a ) return -1; }
+    for( long c=a; c<=b; c++ ) { if( n>=max ) return -1; cpus[ n++ ] = (int)c; }
+    if( *e==',' ) e++;
+    else if( *e ) return -1;
+    s = e;
+  }
+  return n;
+}
+
 int
 main( int argc, char ** argv ) {
   fd_log_private_boot( &argc, &argv );
-  if( argc<4 ) FD_LOG_ERR(( "usage: %s verify|verify_hip PAYLOADS OUT [--app NAME] [--depth D] [--rr-cnt N] [--rr-idx I] "
-                            "[--no-sandbox] [--rate TXN_PER_S] [--timeout S]", argv[0] ));
+  if( argc<4 ) FD_LOG_ERR(( "usage: %s verify|verify_hip PAYLOADS OUT [--app NAME] [--depth D] [--tiles K | --rr-cnt N "
+                            "--rr-idx I] [--no-sandbox] [--rate TXN_PER_S] [--timeout S] [--lat-out FILE] [--cpus LIST]",
+                            argv[0] ));
   harness_t * h = (harness_t *)calloc( 1, sizeof(harness_t) );
   char const * kind = argv[1];
   if(      !strcmp( kind, "verify"     ) ) h->run = &fd_tile_verify;
@@ -267,22 +342,37 @@ main( int argc, char ** argv ) {
   else FD_LOG_ERR(( "unknown tile %s", kind ));
   char const * app = "harness";
   char const * lat_out = NULL;
-  ulong depth = 4096UL, rr_cnt = 1UL, rr_idx = 0UL;
+  ulong depth = 4096UL, rr_cnt = 0UL, rr_idx = 0UL, tiles = 0UL;
   double timeout = 120.0;
+  int cpus[ 64 ];
+  int cpu_cnt = 0;
   h->sandbox = 1;
   for( int i=4; i<argc; i++ ) {
     char const * a = argv[i]; char const * v = i+1<argc ? argv[i+1] : NULL;
     if(      !strcmp( a, "--app"     ) && v ) { app = v; i++; }
     else if( !strcmp( a, "--depth"   ) && v ) { depth = strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--tiles"   ) && v ) { tiles = strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--rr-cnt"  ) && v ) { rr_cnt = strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--rr-idx"  ) && v ) { rr_idx = strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--rate"    ) && v ) { h->rate = strtod( v, NULL ); i++; }
     else if( !strcmp( a, "--timeout" ) && v ) { timeout = strtod( v, NULL ); i++; }
     else if( !strcmp( a, "--no-sandbox" ) ) h->sandbox = 0;
     else if( !strcmp( a, "--lat-out" ) && v ) { lat_out = v; i++; }
+    else if( !strcmp( a, "--cpus" ) && v ) {
+      cpu_cnt = parse_cpus( v, cpus, 64 );
+      if( cpu_cnt<=0 ) FD_LOG_ERR(( "bad --cpus list %s", v ));
+      i++;
+    }
     else FD_LOG_ERR(( "bad argument %s", a ));
   }
-  FD_TEST( rr_cnt>=1UL && rr_idx<rr_cnt && rr_cnt<=16UL && fd_ulong_is_pow2( depth ) );
+  if( tiles && rr_cnt ) FD_LOG_ERR(( "--tiles and --rr-cnt exclude each other" ));
+  ulong first = 0UL;               /* kind id of the first tile that runs */
+  if( tiles ) { rr_cnt = tiles; h->t_cnt = tiles; }
+  else if( rr_cnt ) { h->t_cnt = 1UL; first = rr_idx; }
+  else { rr_cnt = 1UL; h->t_cnt = 1UL; }
+  FD_TEST( rr_cnt>=1UL && rr_cnt<=TILE_MAX && first<rr_cnt && fd_ulong_is_pow2( depth ) );
+  h->cpu_prod = cpu_cnt>0 ? cpus[0] : -1;
+  h->cpu_cons = cpu_cnt>1 ? cpus[1] : -1;
 
   /* payloads */
   FILE * f = fopen( argv[2], "rb" );
@@ -301,30 +391,25 @@ main( int argc, char ** argv ) {
   h->tick_per_ns = calibrate_ticks();
 
   /* the workspace region and the objects in it */
+  ulong K = h->t_cnt;
   ulong out_depth = depth;
   ulong in_data  = fd_dcache_req_data_sz( FD_TPU_MTU,        depth,     1UL,       1 );
   ulong out_data = fd_dcache_req_data_sz( FD_TPU_DCACHE_MTU, out_depth, OUT_BURST, 1 );
-  g_cap = 64UL*1024UL*1024UL + fd_dcache_footprint( in_data, 0UL ) + fd_dcache_footprint( out_data, 0UL ) +
-          fd_mcache_footprint( depth, 0UL ) + fd_mcache_footprint( out_depth, 0UL ) +
-          h->run->scratch_footprint( NULL ) + FD_MUX_TILE_SCRATCH_FOOTPRINT( 1UL, 1UL );
+  g_cap = 64UL*1024UL*1024UL + fd_dcache_footprint( in_data, 0UL ) + fd_mcache_footprint( depth, 0UL ) +
+          K*( fd_dcache_footprint( out_data, 0UL ) + fd_mcache_footprint( out_depth, 0UL ) +
+              h->run->scratch_footprint( NULL ) + FD_MUX_TILE_SCRATCH_FOOTPRINT( 1UL, 1UL ) + 6UL*4096UL +
+              FD_METRICS_FOOTPRINT( 1UL, 1UL ) );
   FD_TEST( !posix_memalign( (void **)&g_mem, 4096UL, g_cap ) );
   fd_memset( g_mem, 0, g_cap );
 
   h->in_depth   = depth;
+  h->out_depth  = out_depth;
   h->in_mcache  = fd_mcache_join( fd_mcache_new( walloc( fd_mcache_align(), fd_mcache_footprint( depth, 0UL ) ), depth, 0UL, 0UL ) );
   h->in_dcache  = fd_dcache_join( fd_dcache_new( walloc( fd_dcache_align(), fd_dcache_footprint( in_data, 0UL ) ), in_data, 0UL ) );
-  h->in_fseq    = fd_fseq_join( fd_fseq_new( walloc( fd_fseq_align(), fd_fseq_footprint() ), 0UL ) );
-  h->out_depth  = out_depth;
-  h->out_mcache = fd_mcache_join( fd_mcache_new( walloc( fd_mcache_align(), fd_mcache_footprint( out_depth, 0UL ) ), out_depth, 0UL, 0UL ) );
-  h->out_dcache = fd_dcache_join( fd_dcache_new( walloc( fd_dcache_align(), fd_dcache_footprint( out_data, 0UL ) ), out_data, 0UL ) );
-  h->out_fseq   = fd_fseq_join( fd_fseq_new( walloc( fd_fseq_align(), fd_fseq_footprint() ), 0UL ) );
-  h->cnc        = fd_cnc_join( fd_cnc_new( walloc( fd_cnc_align(), fd_cnc_footprint( 64UL ) ), 64UL, 0UL, fd_tickcount() ) );
-  ulong * metrics = fd_metrics_new( walloc( FD_METRICS_ALIGN, FD_METRICS_FOOTPRINT( 1UL, 1UL ) ), 1UL, 1UL );
-  h->scratch     = walloc( h->run->scratch_align(), h->run->scratch_footprint( NULL ) );
-  h->mux_scratch = walloc( FD_MUX_TILE_SCRATCH_ALIGN, FD_MUX_TILE_SCRATCH_FOOTPRINT( 1UL, 1UL ) );
-  FD_TEST( h->in_mcache && h->in_dcache && h->in_fseq && h->out_mcache && h->out_dcache && h->out_fseq && h->cnc );
+  FD_TEST( h->in_mcache && h->in_dcache );
 
-  /* the topology the tile's init reads */
+  /* the topology the tiles' init reads: objects 0, 1 the shared in link,
+     2+2k, 3+2k tile k's out link */
   fd_topo_t * topo = (fd_topo_t *)calloc( 1, sizeof(fd_topo_t) );
   h->topo = topo;
   FD_TEST( fd_cstr_printf_check( topo->app_name, sizeof(topo->app_name), NULL, "%s", app ) );
@@ -332,29 +417,47 @@ main( int argc, char ** argv ) {
   topo->workspaces[0].id = 0UL;
   strcpy( topo->workspaces[0].name, "harness" );
   topo->workspaces[0].wksp = (fd_wksp_t *)g_mem;
-  void * objs[4] = { h->in_mcache, h->in_dcache, h->out_mcache, h->out_dcache };
-  for( ulong o=0UL; o<4UL; o++ ) {
-    topo->objs[o].id = o; topo->objs[o].wksp_id = 0UL; topo->objs[o].offset = woff( objs[o] );
-  }
-  topo->obj_cnt  = 4UL;
-  topo->link_cnt = 2UL;
+  topo->objs[0].id = 0UL; topo->objs[0].wksp_id = 0UL; topo->objs[0].offset = woff( h->in_mcache );
+  topo->objs[1].id = 1UL; topo->objs[1].wksp_id = 0UL; topo->objs[1].offset = woff( h->in_dcache );
+  topo->link_cnt = 1UL;
   fd_topo_link_t * lin = &topo->links[0];
   lin->id = 0UL; strcpy( lin->name, "quic_verify" ); lin->depth = depth; lin->mtu = FD_TPU_MTU; lin->burst = 1UL;
   lin->mcache_obj_id = 0UL; lin->dcache_obj_id = 1UL; lin->mcache = h->in_mcache; lin->dcache = h->in_dcache;
-  fd_topo_link_t * lout = &topo->links[1];
-  lout->id = 1UL; strcpy( lout->name, "verify_dedup" ); lout->depth = out_depth; lout->mtu = FD_TPU_DCACHE_MTU;
-  lout->burst = OUT_BURST; lout->mcache_obj_id = 2UL; lout->dcache_obj_id = 3UL;
-  lout->mcache = h->out_mcache; lout->dcache = h->out_dcache;
   topo->tile_cnt = rr_cnt;
+  topo->obj_cnt  = 2UL;
   for( ulong k=0UL; k<rr_cnt; k++ ) {
-    fd_topo_tile_t * t = &topo->tiles[k];
-    t->id = k; strcpy( t->name, "verify" ); t->kind_id = k;
-    t->in_cnt = 1UL; t->in_link_id[0] = 0UL; t->in_link_reliable[0] = 1; t->in_link_poll[0] = 1;
-    t->out_link_id_primary = 1UL;
-    t->in_link_fseq[0] = h->in_fseq;
-    t->cnc = h->cnc; t->metrics = metrics;
+    fd_topo_tile_t * tt = &topo->tiles[k];
+    tt->id = k; strcpy( tt->name, "verify" ); tt->kind_id = k;
+    tt->in_cnt = 1UL; tt->in_link_id[0] = 0UL; tt->in_link_reliable[0] = 1; tt->in_link_poll[0] = 1;
   }
-  h->tile = &topo->tiles[ rr_idx ];
+  for( ulong j=0UL; j<K; j++ ) {
+    tile_run_t * t = &h->t[j];
+    t->h = h; t->k = first + j;
+    t->cpu = cpu_cnt ? cpus[ (2 + (int)j) % cpu_cnt ] : -1;
+    t->out_mcache = fd_mcache_join( fd_mcache_new( walloc( fd_mcache_align(), fd_mcache_footprint( out_depth, 0UL ) ), out_depth, 0UL, 0UL ) );
+    t->out_dcache = fd_dcache_join( fd_dcache_new( walloc( fd_dcache_align(), fd_dcache_footprint( out_data, 0UL ) ), out_data, 0UL ) );
+    t->out_fseq   = fd_fseq_join( fd_fseq_new( walloc( fd_fseq_align(), fd_fseq_footprint() ), 0UL ) );
+    t->in_fseq    = fd_fseq_join( fd_fseq_new( walloc( fd_fseq_align(), fd_fseq_footprint() ), 0UL ) );
+    t->cnc        = fd_cnc_join( fd_cnc_new( walloc( fd_cnc_align(), fd_cnc_footprint( 64UL ) ), 64UL, 0UL, fd_tickcount() ) );
+    ulong * metrics = fd_metrics_new( walloc( FD_METRICS_ALIGN, FD_METRICS_FOOTPRINT( 1UL, 1UL ) ), 1UL, 1UL );
+    t->scratch     = walloc( h->run->scratch_align(), h->run->scratch_footprint( NULL ) );
+    t->mux_scratch = walloc( FD_MUX_TILE_SCRATCH_ALIGN, FD_MUX_TILE_SCRATCH_FOOTPRINT( 1UL, 1UL ) );
+    FD_TEST( t->out_mcache && t->out_dcache && t->out_fseq && t->in_fseq && t->cnc && metrics );
+    ulong o = topo->obj_cnt;
+    topo->objs[o  ].id = o;   topo->objs[o  ].wksp_id = 0UL; topo->objs[o  ].offset = woff( t->out_mcache );
+    topo->objs[o+1].id = o+1; topo->objs[o+1].wksp_id = 0UL; topo->objs[o+1].offset = woff( t->out_dcache );
+    topo->obj_cnt += 2UL;
+    ulong li = topo->link_cnt++;
+    fd_topo_link_t * lout = &topo->links[li];
+    lout->id = li; strcpy( lout->name, "verify_dedup" ); lout->kind_id = j; lout->depth = out_depth;
+    lout->mtu = FD_TPU_DCACHE_MTU; lout->burst = OUT_BURST; lout->mcache_obj_id = o; lout->dcache_obj_id = o+1;
+    lout->mcache = t->out_mcache; lout->dcache = t->out_dcache;
+    fd_topo_tile_t * tt = &topo->tiles[ t->k ];
+    tt->out_link_id_primary = li;
+    tt->in_link_fseq[0] = t->in_fseq;
+    tt->cnc = t->cnc; tt->metrics = metrics;
+    t->tile = tt;
+  }
 
   h->res_cap = 64UL + h->n*(12UL + FD_TPU_DCACHE_MTU);
   h->res     = (uchar *)malloc( h->res_cap );
@@ -362,49 +465,64 @@ main( int argc, char ** argv ) {
   FD_TEST( h->res && h->lat_ns );
   fd_memset( h->lat_ns, 0, 4UL*(h->n+1UL) );   /* touched before the stream (no first-touch faults inside it) */
 
-  /* privileged_init (maps the accelerated tile's links), then the threads */
-  if( h->run->privileged_init ) h->run->privileged_init( topo, h->tile, h->scratch );
+  /* privileged_init (maps the accelerated tiles' links), then the threads */
+  for( ulong j=0UL; j<K; j++ ) {
+    if( h->run->privileged_init ) h->run->privileged_init( topo, h->t[j].tile, h->t[j].scratch );
+    h->t[j].ctx = h->run->mux_ctx ? h->run->mux_ctx( h->t[j].scratch ) : NULL;
+  }
   double t_start = now_s();
-  pthread_t tt, tp, tc;
+  pthread_t tp, tc, tt[ TILE_MAX ];
   FD_TEST( !pthread_create( &tc, NULL, consumer_main, h ) );
-  FD_TEST( !pthread_create( &tt, NULL, tile_main, h ) );
-  while( fd_cnc_signal_query( h->cnc )!=FD_CNC_SIGNAL_RUN ) {
-    if( now_s() - t_start > timeout ) { printf( "{\"error\": \"tile did not boot\"}\n" ); fflush( stdout ); _exit( 3 ); }
-    FD_SPIN_PAUSE();
+  for( ulong j=0UL; j<K; j++ ) FD_TEST( !pthread_create( &tt[j], NULL, tile_main, &h->t[j] ) );
+  for( ulong j=0UL; j<K; j++ ) {
+    while( fd_cnc_signal_query( h->t[j].cnc )!=FD_CNC_SIGNAL_RUN ) {
+      if( now_s() - t_start > timeout ) { printf( "{\"error\": \"tile did not boot\"}\n" ); fflush( stdout ); _exit( 3 ); }
+      FD_SPIN_PAUSE();
+    }
   }
   double t0 = now_s();
   FD_TEST( !pthread_create( &tp, NULL, producer_main, h ) );
 
-  /* quiescence: every frag consumed by the tile, nothing pending inside it,
-     the consumer caught up with what was published */
+  /* quiescence: every frag consumed by every tile, nothing pending inside
+     them, the consumer caught up with what each published */
   int hip = h->run==&fd_tile_verify_hip;
   for(;;) {
     if( now_s() - t_start > timeout ) { printf( "{\"error\": \"timeout\", \"published\": %lu}\n", h->res_cnt ); fflush( stdout ); _exit( 3 ); }
     if( h->consumer_err ) { printf( "{\"error\": \"consumer %d\"}\n", h->consumer_err ); fflush( stdout ); _exit( 4 ); }
-    if( !h->producer_done || fd_fseq_query( h->in_fseq )<h->n ) { FD_SPIN_PAUSE(); continue; }
-    if( hip && fd_verify_hip_pending( h->ctx ) ) { FD_SPIN_PAUSE(); continue; }
-    /* all of the tile's publishes happened before what was just read;
-       the consumer has them once the next line is still unpublished */
+    if( !h->producer_done || fd_seq_lt( min_fseq( h ), h->n ) ) { FD_SPIN_PAUSE(); continue; }
+    int busy = 0;
+    for( ulong j=0UL; j<K && !busy; j++ ) busy = hip && fd_verify_hip_pending( h->t[j].ctx );
+    if( busy ) { FD_SPIN_PAUSE(); continue; }
+    /* all of the tiles' publishes happened before what was just read; the
+       consumer has them once each link's next line is still unpublished */
     FD_COMPILER_MFENCE();
-    ulong seq = h->out_seq;
-    fd_frag_meta_t const * m = h->out_mcache + fd_mcache_line_idx( seq, h->out_depth );
-    if( fd_seq_diff( FD_VOLATILE_CONST( m->seq ), seq )>=0L ) { FD_SPIN_PAUSE(); continue; }
+    int behind = 0;
+    for( ulong j=0UL; j<K && !behind; j++ ) {
+      ulong seq = FD_VOLATILE_CONST( h->t[j].out_seq );
+      fd_frag_meta_t const * m = h->t[j].out_mcache + fd_mcache_line_idx( seq, h->out_depth );
+      behind = fd_seq_diff( FD_VOLATILE_CONST( m->seq ), seq )>=0L;
+    }
+    if( behind ) { FD_SPIN_PAUSE(); continue; }
     break;
   }
   double t1 = now_s();
-  fd_cnc_signal( h->cnc, FD_CNC_SIGNAL_HALT );
-  while( !h->tile_halted ) {
-    if( now_s() - t_start > timeout ) { printf( "{\"error\": \"halt timeout\"}\n" ); fflush( stdout ); _exit( 3 ); }
-    FD_SPIN_PAUSE();
+  for( ulong j=0UL; j<K; j++ ) fd_cnc_signal( h->t[j].cnc, FD_CNC_SIGNAL_HALT );
+  for( ulong j=0UL; j<K; j++ ) {
+    while( !h->t[j].halted ) {
+      if( now_s() - t_start > timeout ) { printf( "{\"error\": \"halt timeout\"}\n" ); fflush( stdout ); _exit( 3 ); }
+      FD_SPIN_PAUSE();
+    }
   }
   h->stop = 1;
   pthread_join( tc, NULL );
   pthread_join( tp, NULL );
-  if( hip ) {   /* end the service's stream */
-    fd_ed25519_hip_shlink_t * txl = fd_verify_hip_txn_link( h->ctx );
-    while( fd_ed25519_hip_shlink_publish( txl, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
-      if( now_s() - t_start > timeout ) break;
-      FD_SPIN_PAUSE();
+  if( hip ) {   /* end each service stream */
+    for( ulong j=0UL; j<K; j++ ) {
+      fd_ed25519_hip_shlink_t * txl = fd_verify_hip_txn_link( h->t[j].ctx );
+      while( fd_ed25519_hip_shlink_publish( txl, NULL, 0UL, 0UL, FD_ED25519_HIP_SHLINK_CTL_EOS )==1 ) {
+        if( now_s() - t_start > timeout ) break;
+        FD_SPIN_PAUSE();
+      }
     }
   }
 
@@ -421,11 +539,14 @@ main( int argc, char ** argv ) {
   double p50 = nl ? 1e-3*(double)h->lat_ns[ (nl-1UL)/2UL ] : 0.0;
   double p99 = nl ? 1e-3*(double)h->lat_ns[ (ulong)((double)(nl-1UL)*0.99) ] : 0.0;
   double pmx = nl ? 1e-3*(double)h->lat_ns[ nl-1UL ] : 0.0;
+  int halted_ok = 1;
+  for( ulong j=0UL; j<K; j++ ) halted_ok &= h->t[j].halted==1;
   printf( "{\"tile\": \"%s\", \"frags\": %lu, \"published\": %lu, \"seconds\": %.6f, \"txn_per_s\": %.1f, "
-          "\"rr_cnt\": %lu, \"rr_idx\": %lu, \"sandbox\": %d, \"rate\": %.1f, \"lat_p50_us\": %.2f, "
-          "\"lat_p99_us\": %.2f, \"lat_max_us\": %.2f, \"producer_credit_spins\": %lu, \"consumer_idle_spins\": %lu}\n",
-          kind, h->n, h->res_cnt, t1-t0, (double)h->n/(t1-t0), rr_cnt, rr_idx, h->sandbox, h->rate, p50, p99, pmx,
-          h->credit_spins, h->idle_spins );
+          "\"rr_cnt\": %lu, \"rr_idx\": %lu, \"tiles_running\": %lu, \"threads\": %lu, \"pinned\": %d, \"sandbox\": %d, "
+          "\"rate\": %.1f, \"lat_p50_us\": %.2f, \"lat_p99_us\": %.2f, \"lat_max_us\": %.2f, "
+          "\"producer_credit_spins\": %lu, \"consumer_idle_spins\": %lu}\n",
+          kind, h->n, h->res_cnt, t1-t0, (double)h->n/(t1-t0), rr_cnt, first, K, K + 2UL, cpu_cnt>0, h->sandbox,
+          h->rate, p50, p99, pmx, h->credit_spins, h->idle_spins );
   fflush( stdout );
-  _exit( h->tile_halted==1 ? 0 : 5 );
+  _exit( halted_ok ? 0 : 5 );
 }

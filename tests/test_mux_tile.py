@@ -43,7 +43,7 @@ SANITIZE = bool(os.environ.get("FD_TEST_SANITIZE"))
 
 
 def run_harness(kind, payloads, out, app="harness", rr=(1, 0), depth=4096, timeout=120, extra=()):
-    args = [HARNESS, kind, payloads, out, "--app", app, "--rr-cnt", str(rr[0]), "--rr-idx", str(rr[1]),
+    args = [HARNESS, kind, payloads, out, "--app", app, *(["--rr-cnt", str(rr[0]), "--rr-idx", str(rr[1])] if rr else []),
             "--depth", str(depth), "--timeout", str(timeout), "--log-path", "", *extra,
             *(["--no-sandbox"] if SANITIZE else [])]
     return subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
@@ -171,6 +171,48 @@ def test_three_tiles_round_robin_one_service(stream, reference_runs, tmp_path):
     # the three positions partition the stream: together they publish what
     # one tile would, up to dedup (each tile has its own tcache, as in the reference)
     assert total >= len(reference_runs[(1, 0)][1])
+
+
+def _normalized(frags):
+    """(sig, bytes) with the alignment pad byte zeroed (assert_same_frags),
+    sorted: the published set, whatever order the links were read in"""
+    out = []
+    for sig, b in frags:
+        psz = struct.unpack_from("<H", b, len(b) - 2)[0]
+        if psz % 2:
+            b = b[:psz] + b"\0" + b[psz + 1:]
+        out.append((sig, bytes(b)))
+    return sorted(out)
+
+
+@pytest.mark.parametrize("kind", ["verify", "verify_hip"])
+def test_shared_quic_link_k_tiles_in_one_topology(stream, reference_runs, tmp_path, kind):
+    """fdctl's topology: one quic -> verify link that three
+    verify tiles read, each keeping seq % 3 == its kind id (fd_verify.c:
+    36-47) and publishing to its own verify -> dedup link, one consumer
+    reading all three -- five spinning threads, not three harnesses.  The
+    reference tile and the accelerated one (stand-in service, three link
+    pairs) publish together exactly what the three single-position
+    reference runs publish."""
+    path, frags = stream
+    app = uuid.uuid4().hex[:10]
+    svc = start_standin(app, 3) if kind == "verify_hip" else None
+    try:
+        out = str(tmp_path / "k3.bin")
+        p = run_harness(kind, path, out, app=app, rr=None, extra=("--tiles", "3"))
+        so, se = p.communicate(timeout=180)
+        assert p.returncode == 0, se[-2000:]
+        if svc is not None:
+            assert svc.wait(timeout=30) == 0, svc.stderr.read()[-2000:]
+    finally:
+        if svc is not None and svc.poll() is None:
+            svc.kill()
+        cleanup(app)
+    res = json.loads(so.strip().splitlines()[-1])
+    assert res["tiles_running"] == 3 and res["threads"] == 5 and res["frags"] == len(frags)
+    want = [f for k in range(3) for f in reference_runs[(3, k)][1]]
+    assert res["published"] == len(want)
+    assert _normalized(parse_out(out)) == _normalized(want)
 
 
 def _expect_tile_stops(stream, tmp_path, svc_args, needle, bound_s):

@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 N=$1; shift
-P="python3 $R/bench.py --n $N --steps 2 --warmup 0 --no-cpu-baseline --latency-txns 0"
+P="python3 $R/bench.py --n $N --steps 2 --warmup 0 --no-cpu-baseline --latency-txns 0 --deployed-txns 0 --host-reps 0 --c4-signatures 0"
 for name in "$@"; do
   lib=$R/build/variants/$name/libfd_ed25519_hip.so
   [ "$name" = "main" ] && lib=$R/firedancer_amd/_lib/libfd_ed25519_hip.so

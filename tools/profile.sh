@@ -13,10 +13,10 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 # one batch in flight: each kernel runs alone, so the trace durations are
 # comparable with the bench's per-phase HIP events
-B="python3 $R/bench.py --steps 3 --warmup 1 --inflight 1 --no-cpu-baseline --latency-txns 0 --host-reps 0"
+B="python3 $R/bench.py --steps 3 --warmup 1 --inflight 1 --no-cpu-baseline --latency-txns 0 --host-reps 0 --deployed-txns 0 --c4-signatures 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B \
   > $O/trace_bench.json 2> $O/trace.err || exit $?
-P="python3 $R/bench.py --n $N --steps 2 --warmup 0 --no-cpu-baseline --latency-txns 0 --host-reps 0"
+P="python3 $R/bench.py --n $N --steps 2 --warmup 0 --no-cpu-baseline --latency-txns 0 --host-reps 0 --deployed-txns 0 --c4-signatures 0"
 i=0
 for set in "SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVES SQ_INSTS_SALU GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE" \
