@@ -43,7 +43,7 @@ def _run(policy, fault, calls, *extra):
 def test_one_failed_launch_is_retried_on_a_new_engine():
     rc, rows, err = _run("reject", "3:1", 6)
     assert rc == 0, err[-2000:]
-    assert [r["got"] for r in rows] == [r["want"] for r in rows] == [0, -1] * 3
+    assert [r["got"] for r in rows] == [r["want"] for r in rows] == [0, -3] * 3
     assert all(r["lost"] == 0 for r in rows)
     assert [r["recoveries"] for r in rows] == [0, 0, 1, 1, 1, 1]
     assert "injected launch failure" in err and "re-creating engine" in err
@@ -53,13 +53,13 @@ def test_lost_device_fails_closed_and_reset_recovers():
     rc, rows, err = _run("reject", "3:2", 4, "reset")
     assert rc == 0, err[-2000:]
     before, reset, after = rows[:4], rows[4], rows[5:]
-    assert [r["got"] for r in before[:2]] == [r["want"] for r in before[:2]] == [0, -1]
+    assert [r["got"] for r in before[:2]] == [r["want"] for r in before[:2]] == [0, -3]
     # launch 3 and its retry failed: lost, every call rejected, the valid one included, no device work
     assert [r["got"] for r in before[2:]] == [-1, -1] and before[2]["want"] == 0
     assert all(r["lost"] < 0 for r in before[2:])
     assert before[3]["launches"] == before[2]["launches"]
     assert reset == {"reset": 0}
-    assert [r["got"] for r in after] == [r["want"] for r in after] == [0, -1, 0, -1]
+    assert [r["got"] for r in after] == [r["want"] for r in after] == [0, -3, 0, -3]
     assert all(r["lost"] == 0 for r in after)
     assert "injected launch failure" in err
 
@@ -67,5 +67,5 @@ def test_lost_device_fails_closed_and_reset_recovers():
 def test_lost_device_aborts_by_default():
     rc, rows, err = _run("abort", "3:2", 4)
     assert rc == -6, (rc, err[-2000:])
-    assert [r["got"] for r in rows] == [r["want"] for r in rows] == [0, -1]   # the calls before the loss
+    assert [r["got"] for r in rows] == [r["want"] for r in rows] == [0, -3]   # the calls before the loss
     assert "FATAL" in err and "policy: abort" in err and "injected launch failure" in err
