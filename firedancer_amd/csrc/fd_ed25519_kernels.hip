@@ -1146,6 +1146,110 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
 }
 
 /* ------------------------------------------------------------------------
+   dsm16: the same equation with the field arithmetic spread over the
+   lanes (fd25519_r16.h), for the smallest chunks -- a drop-in call, a
+   latency-mode batch of a few hundred signatures -- where dsm8 leaves most
+   SIMDs idle and each batch waits for one lane's serial chain of products.
+   Two waves per signature, one per Straus half as in dsm8 (wave 0: [c](-A)
+   + [s_lo]B, wave 1: [|d|](-+R) + [s_hi]B'), a point per wave (row q =
+   coordinate q, lane c = limb c), the [0..8] table in nine registers and
+   every digit wave-uniform (one signature per wave), so a table lookup is
+   a scalar branch.  Base entries are the wide / compact tables' (radix
+   2^25.5, converted per lane).  Wave 1 hands its point to wave 0 through
+   LDS for the last addition and the identity test.  Same digits, windows,
+   tables, additions and order as dsm8. */
+#include "fd25519_r16.h"
+
+/* this lane's r16 limb of its row's coordinate of base entry e, as qc
+   (y-x, y+x, 2dxy, 2) */
+FD_DEV uint32_t btab16_r16(const int32_t* g_btab, int e, const r16ctx& k) {
+  if (k.row == 3u) return r16_small(2u, k);
+  const int off = k.row == 0u ? 10 : (k.row == 1u ? 0 : 20);
+  const int2* src = reinterpret_cast<const int2*>(g_btab + (size_t)e * FD_ED25519_BTAB16_STRIDE + off);
+  fe c;
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const int2 x = src[q];
+    c.v[2 * q] = x.x;
+    c.v[2 * q + 1] = x.y;
+  }
+  return r16_from_fe(c, k);
+}
+
+template <int BW>
+__global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t j = blockIdx.x;   /* a block (two waves) per signature: every return below is block-uniform */
+  if (j >= p.n) return;
+  const uint32_t hf = p.hflag[j];
+  if (hf & FD_HF_FULL) return;     /* the dsm kernel's (full-length form) */
+  const int half = (int)(threadIdx.x >> 6);   /* 0: -A and B, 1: -+R and B' */
+  r16ctx k;
+  r16_init(k);
+  const uint32_t d2 = r16_from_fe(fe{FE_D2}, k);
+  int code = precheck(p, j);
+  uint32_t tab[9];
+  {
+    fe x, y;
+    load_pt(x, y, p, half, j);
+    table16_build(tab, r16_from_fe(x, k), r16_from_fe(y, k), half ? !(hf & FD_HF_DNEG) : true, d2, k);
+  }
+  uint32_t sd[5], bd[5];
+  int W = 33;
+  {
+    uint32_t x[5], t[5];
+    load_hs(x, p, 5, 5, j);
+    W = (fd_half_bitlen<5>(x) + 4) >> 2;
+    W = W < 33 ? 33 : W;
+    if (!half) load_hs(x, p, 0, 5, j);
+    shl160v(t, x, 160 - 4 * W); recode160<4>(sd, t);
+    if (half) {
+      load_hs(x, p, 15, 4, j);
+      shl160<fd_bw<BW>::HI_SHL>(bd, x);
+    } else {
+      load_hs(x, p, 10, 5, j);
+      shl160<fd_bw<BW>::LO_SHL>(bd, x);
+    }
+  }
+  W = __builtin_amdgcn_readfirstlane(W);
+  const int32_t* btab = half ? p.btab_hi : p.btab_lo;
+  const uint32_t one = r16_small(1u, k);
+  uint32_t P = (k.row == 1u || k.row == 2u) ? one : 0u;   /* identity (0, 1, 1, 0) */
+#pragma clang loop unroll(disable)
+  for (int it = W - 1; it >= 0; it--) {
+    int e = pop160<4>(sd);
+    if (it == W - 1) e &= 15;
+    e = __builtin_amdgcn_readfirstlane(e);
+    const bool badd = half ? fd_bw<BW>::hi_at(it) : fd_bw<BW>::lo_at(it);
+    const uint32_t bdig = (uint32_t)__builtin_amdgcn_readfirstlane((int)(badd ? pop160u<BW>(bd) : 0u));
+    const uint32_t ce = table16_at(tab, e < 0 ? -e : e);
+    if (it != W - 1) {
+#pragma clang loop unroll(disable)
+      for (int dbl = 0; dbl < 4; dbl++) P = ge16_to_p3(ge16_dbl(P, k), k);
+    }
+    uint32_t b = 0u;
+    if (badd) b = btab16_r16(btab, (int)bdig, k);
+    P = ge16_cneg4(P, k.row == 0u || k.row == 3u, e < 0, k);
+    uint32_t Rt = ge16_add(P, ce, k);
+    Rt = ge16_cneg8(Rt, k.row == 0u, e < 0, k);
+    P = ge16_to_p3(Rt, k);
+    if (badd) P = ge16_to_p3(ge16_add(P, b, k), k);
+  }
+  /* wave 1's point as an addend of wave 0's */
+  __shared__ uint32_t hand[64];
+  if (half) hand[threadIdx.x & 63u] = ge16_to_qc(P, d2, k);
+  __syncthreads();
+  if (half) return;
+  P = ge16_to_p3(ge16_add(P, hand[threadIdx.x], k), k);
+  /* identity: X == 0 (row 0) and Y == Z (row 1: Y + 4p - Z) */
+  const uint32_t z = r16_rp<2, 2, 2, 2>(P, k);
+  const bool zero = r16_iszero(k.row == 1u ? P + k.p4 - z : P);
+  const uint64_t bal = __ballot(zero);
+  const bool ident = (bal & 1ull) && (bal & (1ull << 16));
+  if (code == FD_PENDING) code = ident ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  if (threadIdx.x == 0u) p.out[p.base + j] = (int8_t)code;
+}
+
+/* ------------------------------------------------------------------------
    Base tables [0..entries)B as (y+x, y-x, 2dxy), one entry per lane:
    [e]B by double-and-add over `bits` bits, then affine. */
 
@@ -1469,7 +1573,11 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
          a scan of the flags */
       const bool compact = p->bw_bits == FD_ED25519_BTABC_BITS;
       const dim3 g8((uint32_t)((8 * p->n + 255) / 256)), g4((uint32_t)((4 * p->n + 255) / 256));
-      if (p->small == 2) {
+      if (p->small == 3) {
+        const dim3 g16((uint32_t)p->n);
+        if (compact) hipLaunchKernelGGL(fd_ed25519_dsm16_kernel<FD_ED25519_BTABC_BITS>, g16, dim3(128), 0, st, *p);
+        else         hipLaunchKernelGGL(fd_ed25519_dsm16_kernel<FD_ED25519_BTABW_BITS>, g16, dim3(128), 0, st, *p);
+      } else if (p->small == 2) {
         if (compact) hipLaunchKernelGGL(fd_ed25519_dsm8_kernel<FD_ED25519_BTABC_BITS>, g8, dim3(256), 0, st, *p);
         else         hipLaunchKernelGGL(fd_ed25519_dsm8_kernel<FD_ED25519_BTABW_BITS>, g8, dim3(256), 0, st, *p);
       } else {

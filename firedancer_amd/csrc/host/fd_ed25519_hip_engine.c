@@ -40,6 +40,7 @@ struct fd_ed25519_hip_engine {
   uint32_t     dsm_grid;
   uint64_t     quad_max;   /* chunks of at most this many signatures run dsm4 */
   uint64_t     oct_max;    /* ... and of at most this many, dsm8            */
+  uint64_t     r16_max;    /* ... and of at most this many, dsm16           */
   uint64_t     max_chunk;
   uint64_t     device_bytes;
   char         arch[ 64 ];
@@ -449,9 +450,11 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   uint64_t quad_cap = atab_sz / (4UL * FD_ED25519_QUAD_LANE_BYTES);
   e->quad_max = FD_ED25519_HIP_QUAD_MAX_DEFAULT;
   e->oct_max  = FD_ED25519_HIP_OCT_MAX_DEFAULT;
-  if( flags & FD_ED25519_HIP_FLAG_DSM_QUAD ) { e->quad_max = ~0UL; e->oct_max = 0UL; }
-  if( flags & FD_ED25519_HIP_FLAG_DSM_OCT  ) { e->quad_max = ~0UL; e->oct_max = ~0UL; }
-  if( flags & FD_ED25519_HIP_FLAG_DSM_WIDE ) e->quad_max = 0UL;
+  e->r16_max  = FD_ED25519_HIP_R16_MAX_DEFAULT;
+  if( flags & FD_ED25519_HIP_FLAG_DSM_R16  ) { e->quad_max = ~0UL; e->oct_max = ~0UL; e->r16_max = ~0UL; }
+  if( flags & FD_ED25519_HIP_FLAG_DSM_QUAD ) { e->quad_max = ~0UL; e->oct_max = 0UL; e->r16_max = 0UL; }
+  if( flags & FD_ED25519_HIP_FLAG_DSM_OCT  ) { e->quad_max = ~0UL; e->oct_max = ~0UL; e->r16_max = 0UL; }
+  if( flags & FD_ED25519_HIP_FLAG_DSM_WIDE ) { e->quad_max = 0UL; e->r16_max = 0UL; }
   if( e->quad_max > quad_cap ) e->quad_max = quad_cap;
   /* a throughput engine pipelines its multi-chunk calls: the second lane
      up front, so verify_dev never allocates (fd_ed25519_hip.h) */
@@ -497,6 +500,14 @@ fd_ed25519_hip_engine_set_forms( fd_ed25519_hip_engine_t * e, unsigned long quad
   }
   e->quad_max = quad_max;
   e->oct_max  = oct_max;
+  if( e->r16_max > oct_max ) e->r16_max = oct_max;
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_engine_set_r16_max( fd_ed25519_hip_engine_t * e, unsigned long n ) {
+  if( !e || n>e->oct_max ) return FD_ED25519_HIP_ERR_INVAL;
+  e->r16_max = n;
   return FD_ED25519_HIP_OK;
 }
 
@@ -565,7 +576,7 @@ verify_chunk( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p, int l
   p->hist = e->lane[l].d_hist; p->atab = e->lane[l].d_atab;
   p->base  = base;
   p->n     = cnt;
-  p->small = p->n > e->quad_max ? 0 : (p->n <= e->oct_max ? 2 : 1);
+  p->small = p->n > e->quad_max ? 0 : p->n <= e->r16_max ? 3 : (p->n <= e->oct_max ? 2 : 1);
   p->perm  = ( p->small || p->digests ) ? NULL : e->lane[l].d_perm;   /* digests: no hash lengths to sort by */
   if( e->timing && e->tm_cnt<FD_ED25519_HIP_TIMING_MAX ) {
     /* events bracket each phase kernel on the stream it runs on */

@@ -31,6 +31,7 @@ FLAG_ONE_STREAM = 32     # no decode side stream / second lane: for engines whos
 FLAG_NO_OVERLAP = 64     # a large chunk's phases in sequence (no decode side stream): tests / A-B
 FLAG_NO_PIPELINE = 128   # a multi-chunk call on one set of work arrays (no second lane): tests / A-B
 FLAG_COMPACT_TABLES = 256  # radix-2^16 base tables (2 x 8 MiB, shared) instead of radix 2^24 (2 x 2 GiB)
+FLAG_DSM_R16 = 512       # dsm16 (field arithmetic over 16 lanes, two waves per signature) at every chunk size
 
 # phases of a verify launch (FD_ED25519_HIP_PHASE_CNT, include/fd_ed25519_hip.h)
 PHASES = ("hash", "scalar", "decode", "dsm")
@@ -56,6 +57,7 @@ _lib.fd_ed25519_hip_engine_new.argtypes = [ctypes.c_int, ctypes.c_ulong, ctypes.
 _lib.fd_ed25519_hip_engine_new.restype = ctypes.c_void_p
 _lib.fd_ed25519_hip_engine_delete.argtypes = [ctypes.c_void_p]
 _lib.fd_ed25519_hip_engine_set_forms.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_ulong]
+_lib.fd_ed25519_hip_engine_set_r16_max.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
 _lib.fd_ed25519_hip_engine_stream.argtypes = [ctypes.c_void_p]
 _lib.fd_ed25519_hip_engine_stream.restype = ctypes.c_void_p
 _lib.fd_ed25519_hip_engine_sync.argtypes = [ctypes.c_void_p]
@@ -144,20 +146,22 @@ class Engine:
     """A libfd_ed25519_hip engine bound to one GPU."""
 
     def __init__(self, device=0, max_chunk=0, codes="avx512", half="extended", dsm="auto", one_stream=False,
-                 overlap=True, pipeline=True, forms=None, compact=False):
+                 overlap=True, pipeline=True, forms=None, compact=False, r16_max=None):
         flags = FLAG_CODES_PORTABLE if codes == "portable" else 0
         flags |= FLAG_ONE_STREAM if one_stream else 0
         flags |= 0 if overlap else FLAG_NO_OVERLAP
         flags |= 0 if pipeline else FLAG_NO_PIPELINE
         flags |= FLAG_COMPACT_TABLES if compact else 0
         flags |= FLAG_HALF_STRICT if half == "strict" else 0
-        flags |= {"auto": 0, "quad": FLAG_DSM_QUAD, "wide": FLAG_DSM_WIDE, "oct": FLAG_DSM_OCT}[dsm]
+        flags |= {"auto": 0, "quad": FLAG_DSM_QUAD, "wide": FLAG_DSM_WIDE, "oct": FLAG_DSM_OCT, "r16": FLAG_DSM_R16}[dsm]
         self._h = _lib.fd_ed25519_hip_engine_new(int(device), int(max_chunk), flags)
         if not self._h:
             raise HipError(f"engine_new failed: {_lib.fd_ed25519_hip_last_error().decode()}")
         self.codes = codes
         if forms is not None:   # (quad_max, oct_max): fd_ed25519_hip_engine_set_forms
             _check(_lib.fd_ed25519_hip_engine_set_forms(self._h, int(forms[0]), int(forms[1])))
+        if r16_max is not None:   # dsm16 up to this chunk size: fd_ed25519_hip_engine_set_r16_max
+            _check(_lib.fd_ed25519_hip_engine_set_r16_max(self._h, int(r16_max)))
 
     def close(self):
         if self._h:

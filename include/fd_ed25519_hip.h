@@ -158,8 +158,8 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    frag carries the published frag's trailer only, the tile keeps the
    payload; 5: shlink protocol word and creator, vservice lifecycle and
    end codes; 6: vservice links_per_thread; 7: vservice link_cpus; 8:
-   vservice stats' leaked_on_hang, the drop-ins' device-lost state).  A
-   consumer checks
+   vservice stats' leaked_on_hang, the drop-ins' device-lost state, the
+   dsm16 form and its flag).  A consumer checks
    the library it loaded against the header it was built with:
    fd_ed25519_hip_abi_check( FD_ED25519_HIP_ABI_VERSION,
    sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
@@ -215,8 +215,16 @@ fd_ed25519_hip_abi_check( unsigned version, unsigned long slot_sz, unsigned long
    mixed additions per signature, same verdicts.  For processes that verify
    little and should not hold 4 GiB of device memory; the drop-ins use it. */
 #define FD_ED25519_HIP_FLAG_COMPACT_TABLES (256)
+/* dsm16 at every chunk size (tests / A-B): the field arithmetic itself
+   spread over 16 lanes, two waves per signature (fd25519_r16.h), the
+   default for chunks of at most FD_ED25519_HIP_R16_MAX_DEFAULT signatures,
+   where a batch's latency is one signature's chain of group operations
+   (fd_ed25519_hip_engine_set_r16_max moves the threshold).  FLAG_DSM_QUAD,
+   _OCT and _WIDE exclude it. */
+#define FD_ED25519_HIP_FLAG_DSM_R16        (512)
 #define FD_ED25519_HIP_QUAD_MAX_DEFAULT    (32768UL)
 #define FD_ED25519_HIP_OCT_MAX_DEFAULT     (8192UL)
+#define FD_ED25519_HIP_R16_MAX_DEFAULT     (512UL)
 /* Overlap: a large chunk's decode phase (A and R need neither the hash nor
    the scalars) runs on a side stream beside its hash and scalar phases, dsm
    after both: +1% at 1M, measured.  Per-phase timing runs the phases in
@@ -247,6 +255,11 @@ fd_ed25519_hip_shared_device_bytes( int device );
    hold.  For tests and tuning; the defaults are the measured crossovers. */
 int
 fd_ed25519_hip_engine_set_forms( fd_ed25519_hip_engine_t * engine, unsigned long quad_max, unsigned long oct_max );
+
+/* Chunks of at most n signatures run dsm16 (0: never); n <= the oct
+   threshold.  FD_ED25519_HIP_ERR_INVAL otherwise. */
+int
+fd_ed25519_hip_engine_set_r16_max( fd_ed25519_hip_engine_t * engine, unsigned long n );
 
 typedef struct {
   int           device;

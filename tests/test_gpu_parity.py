@@ -25,7 +25,8 @@ def fd():
 # quad (up to FD_ED25519_HIP_QUAD_MAX_DEFAULT) and one lane per signature;
 # each with the wide radix-2^24 base tables and with the compact radix-2^16
 # ones (FD_ED25519_HIP_FLAG_COMPACT_TABLES, the drop-ins' engines).
-@pytest.fixture(scope="module", params=["oct", "quad", "wide", "oct-compact", "quad-compact", "wide-compact"])
+@pytest.fixture(scope="module", params=["r16", "oct", "quad", "wide", "r16-compact", "oct-compact", "quad-compact",
+                                        "wide-compact"])
 def eng(fd, request):
     form, _, compact = request.param.partition("-")
     e = fd.Engine(0, max_chunk=1 << 16, dsm=form, compact=bool(compact))
@@ -33,7 +34,7 @@ def eng(fd, request):
     e.close()
 
 
-@pytest.fixture(scope="module", params=["oct", "quad", "wide"])
+@pytest.fixture(scope="module", params=["r16", "oct", "quad", "wide"])
 def eng_portable(fd, request):
     e = fd.Engine(0, max_chunk=1 << 14, codes="portable", dsm=request.param)
     yield e
@@ -176,11 +177,12 @@ def test_chunking(fd, oracle):
 
 def test_dsm_form_by_size(fd, oracle):
     """The automatic choice by chunk size (thresholds lowered with
-    fd_ed25519_hip_engine_set_forms so the test stays small): a batch of two
-    chunks (1000 wide, 600 quad), one of 600 (quad) and one of 300 (oct),
+    fd_ed25519_hip_engine_set_forms / _set_r16_max so the test stays small):
+    a batch of two chunks (1000 wide, 600 quad), one of 600 (quad), one of
+    300 (oct), one of 100 (r16) and a batch of 1100 (1000 wide + 100 r16),
     against the oracle."""
-    e = fd.Engine(0, max_chunk=1000, forms=(600, 300))
-    for n, seed in ((1600, 15), (600, 16), (300, 17)):
+    e = fd.Engine(0, max_chunk=1000, forms=(600, 300), r16_max=100)
+    for n, seed in ((1600, 15), (600, 16), (300, 17), (100, 18), (1100, 21)):
         d = _random_set(oracle, n, seed=seed)
         _check(_run(e, d), oracle_many(oracle, d, 0))
     e.close()
@@ -231,7 +233,7 @@ def test_strerror(fd):
     assert fd.strerror(0) == "success" and fd.strerror(-3) == "bad message" and fd.strerror(5) == "unknown"
 
 
-@pytest.fixture(scope="module", params=["oct", "quad", "wide"])
+@pytest.fixture(scope="module", params=["r16", "oct", "quad", "wide"])
 def eng_strict(fd, request):
     e = fd.Engine(0, max_chunk=1 << 14, half="strict", dsm=request.param)
     yield e

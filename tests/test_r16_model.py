@@ -1,0 +1,251 @@
+"""CPU model of the lane-split field and group arithmetic
+(firedancer_amd/csrc/fd25519_r16.h, fd_ed25519_dsm16_kernel): every limb
+operation restated on Python integers in the device's order, with the
+header's bounds asserted at every step -- the 32-bit lanes never wrap, the
+64-bit column sums never overflow, every multiplication input stays below
+2^19, every subtraction's 4p / 8p offset is above what it subtracts -- and
+the results checked against exact arithmetic: products mod p, and the
+dsm16 window loop's group element against [c](-A) + [s]B computed by
+plain affine Edwards arithmetic.  Worst cases (all limbs at their bound)
+are run alongside random ones."""
+import random
+
+import pytest
+
+P = 2**255 - 19
+D = (-121665 * pow(121666, P - 2, P)) % P
+D2 = 2 * D % P
+M32, M64 = 2**32, 2**64
+B_IN = 2**19            # mul / sq input bound
+TIGHT = 2**16 + 64      # mul / sq output bound
+P4 = [2**17 - 76] + [2**17 - 2] * 15
+P8 = [2**18 - 152] + [2**18 - 4] * 15
+assert sum(l << (16 * c) for c, l in enumerate(P4)) == 4 * P
+assert sum(l << (16 * c) for c, l in enumerate(P8)) == 8 * P
+
+
+def val(x):
+    return sum(l << (16 * c) for c, l in enumerate(x)) % P
+
+
+def limbs(v):
+    v %= P
+    return [(v >> (16 * c)) & 0xffff for c in range(16)]
+
+
+def ror(x, t):
+    """row_ror:t -- lane c gets lane (c - t) mod 16"""
+    return [x[(c - t) % 16] for c in range(16)]
+
+
+def m(t):
+    return [38 if c < t else 1 for c in range(16)]
+
+
+def r16_mul(f, g):
+    assert all(0 <= v < B_IN for v in f + g), (max(f), max(g))
+    acc = [0] * 16
+    for t in range(16):
+        rt = ror(f, t)
+        for c in range(16):
+            assert rt[c] < 2**24                 # v_mul_u32_u24: 24-bit inputs ...
+            r = rt[c] * m(t)[c]
+            assert r < M32                       # ... and the product's low 32 bits are all of it
+            acc[c] += g[t] * r
+    assert all(a < M64 for a in acc)
+    # round 1: 32-bit lo + (hi rotated) * m1, the product formed in 64 bits, the sum kept in 32
+    lo = [a & 0xffff for a in acc]
+    hi = [a >> 16 for a in acc]
+    assert all(h < M32 for h in hi)
+    hr = ror(hi, 1)
+    l = [lo[c] + hr[c] * m(1)[c] for c in range(16)]
+    assert all(v < M32 for v in l), max(l)
+    for _ in range(2):   # rounds 2, 3: 24-bit multiplies
+        lo = [v & 0xffff for v in l]
+        hi = ror([v >> 16 for v in l], 1)
+        assert all(h < 2**24 for h in hi)
+        l = [lo[c] + hi[c] * m(1)[c] for c in range(16)]
+        assert all(v < M32 for v in l)
+    assert all(v < TIGHT for v in l), max(l)
+    return l
+
+
+def sub(x, y, off):
+    assert all(o >= v for o, v in zip(off, y)), "offset below the subtrahend: a lane would wrap"
+    return [a + o - b for a, o, b in zip(x, off, y)]
+
+
+def add(x, y):
+    return [a + b for a, b in zip(x, y)]
+
+
+def neg(x, off):
+    """off - x (4p or 8p minus x, limb by limb)"""
+    assert all(o >= v for o, v in zip(off, x)), "offset below the negated value: a lane would wrap"
+    return [o - v for o, v in zip(off, x)]
+
+
+# ---- points: 4 rows, row q = coordinate q, as fd25519_ge4.h / fd25519_r16.h
+
+def rp(pt, src):
+    return [pt[s] for s in src]
+
+
+def to_p3(r):
+    a, b = rp(r, (0, 1, 2, 0)), rp(r, (3, 2, 3, 1))
+    return [r16_mul(a[q], b[q]) for q in range(4)]
+
+
+def dbl(p):
+    a, b = rp(p, (0, 1, 0, 2)), rp(p, (0, 0, 1, 0))
+    u = [a[0], a[1], add(a[2], b[2]), a[3]]
+    s = [r16_mul(x, x) for x in u]
+    s[3] = add(s[3], s[3])
+    w = rp(s, (1, 0, 3, 2))
+    t = [add(s[0], w[0]), sub(s[1], w[1], P4), s[2], s[3]]
+    x, y = rp(t, (2, 0, 1, 3)), rp(t, (0, 0, 0, 1))
+    return [sub(x[0], y[0], P8), x[1], x[2], sub(x[3], y[3], P8)]
+
+
+def padd(p, qc):
+    v = rp(p, (1, 0, 3, 2))
+    o = [sub(v[0], p[0], P4), add(v[1], p[1]), v[2], v[3]]
+    pr = [r16_mul(o[q], qc[q]) for q in range(4)]
+    w = rp(pr, (1, 0, 3, 2))
+    return [sub(w[0], pr[0], P4), add(w[1], pr[1]), add(w[2], pr[2]), sub(pr[3], w[3], P4)]
+
+
+def to_qc(p, d2):
+    v = rp(p, (1, 0, 3, 2))
+    t = r16_mul(v[2], d2)
+    return [sub(v[0], p[0], P4), add(v[1], p[1]), t, add(v[3], v[3])]
+
+
+def cneg(pt, rows, negate, off):
+    return [neg(x, off) if (q in rows and negate) else x for q, x in enumerate(pt)]
+
+
+def ext(pt):
+    """(X, Y, Z, T) p3 -> affine (x, y)"""
+    X, Y, Z, T = (val(c) for c in pt)
+    zi = pow(Z, P - 2, P)
+    assert X * Y % P == T * Z % P
+    return X * zi % P, Y * zi % P
+
+
+def edwards_add(a, b):
+    (x1, y1), (x2, y2) = a, b
+    t = D * x1 * x2 * y1 * y2 % P
+    return ((x1 * y2 + x2 * y1) * pow(1 + t, P - 2, P) % P, (y1 * y2 + x1 * x2) * pow(1 - t, P - 2, P) % P)
+
+
+def edwards_mul(k, pt):
+    r, q = (0, 1), pt
+    while k:
+        if k & 1:
+            r = edwards_add(r, q)
+        q = edwards_add(q, q)
+        k >>= 1
+    return r
+
+
+BY = 4 * pow(5, P - 2, P) % P
+
+
+def recover_x(y, sign):
+    u, v = (y * y - 1) % P, (D * y * y + 1) % P
+    x = u * pow(v, 3, P) * pow(u * pow(v, 7, P), (P - 5) // 8, P) % P
+    if (v * x * x - u) % P:
+        x = x * pow(2, (P - 1) // 4, P) % P
+    return P - x if (x & 1) != sign else x
+
+
+BASE = (recover_x(BY, 0), BY)
+
+
+def table(x, y, negate, d2):
+    xs = neg(x, P4) if negate else x
+    xy = r16_mul(xs, y)
+    one, zero, two = limbs(1), [0] * 16, limbs(2)
+    p0 = [xs, y, one, xy]
+    tab = [[one, one, zero, two]]
+    c1 = to_qc(p0, d2)
+    tab.append(c1)
+    cur = p0
+    for _ in range(2, 9):
+        cur = to_p3(padd(cur, c1))
+        tab.append(to_qc(cur, d2))
+    return tab
+
+
+def test_mul_exact_and_bounded():
+    rng = random.Random(5)
+    worst = [B_IN - 1] * 16
+    for f, g in [(worst, worst), ([TIGHT - 1] * 16, worst)] + \
+                [([rng.randrange(B_IN) for _ in range(16)], [rng.randrange(B_IN) for _ in range(16)]) for _ in range(300)]:
+        assert val(r16_mul(f, g)) == val(f) * val(g) % P
+
+
+def test_group_ops_on_worst_and_random_inputs():
+    """dbl / add / to_p3 / to_qc / cneg: exact group law, bounds held, from
+    a point whose limbs are pushed to the top of their range (4p added
+    limb-wise to a tight point keeps its value and maximises every sum)"""
+    rng = random.Random(6)
+    d2 = limbs(D2)
+    for _ in range(6):
+        k = rng.randrange(1, 2**64)
+        x, y = edwards_mul(k, BASE)
+        p3 = [limbs(x), limbs(y), limbs(1), limbs(x * y)]
+        q = edwards_mul(rng.randrange(1, 2**64), BASE)
+        qc = to_qc([limbs(q[0]), limbs(q[1]), limbs(1), limbs(q[0] * q[1])], d2)
+        assert ext(to_p3(dbl(p3))) == edwards_add((x, y), (x, y))
+        assert ext(to_p3(padd(p3, qc))) == edwards_add((x, y), q)
+        # negated P (rows 0, 3: 4p - x), then the p1p1's row 0 negated (8p - x), as the dsm loop does
+        pn = cneg(p3, (0, 3), True, P4)
+        r = cneg(padd(pn, qc), (0,), True, P8)
+        assert ext(to_p3(r)) == edwards_add((x, y), ((P - q[0]) % P, q[1]))
+        # tight limbs at their top: the value + 0 with every limb ~2^16 + 63
+        hi = [[min(TIGHT - 1, l + 0) for l in c] for c in p3]
+        assert all(v < TIGHT for c in hi for v in c)
+        dbl(hi), padd(hi, qc)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_window_loop_matches_scalar_multiplication(seed):
+    """One half of dsm16: the [0..8](-A) table, W = 33 signed 4-bit windows
+    of c (4 doublings each), a table addition per window and an unsigned
+    radix-2^24 base addition every 6th window, exactly as the kernel
+    orders them -- against [c](-A) + [s]B."""
+    rng = random.Random(seed)
+    d2 = limbs(D2)
+    A = edwards_mul(rng.randrange(1, 2**250), BASE)
+    c = rng.randrange(2**130)
+    s = rng.randrange(2**144)
+    ax, ay = limbs(A[0]), limbs(A[1])
+    tab = table(ax, ay, True, d2)
+    # c in 33 signed radix-16 digits, most significant first (the top one in [0, 8])
+    digs, carry = [], 0
+    for i in range(33):
+        e = ((c >> (4 * i)) & 15) + carry
+        carry = (e + 8) >> 4
+        digs.append(e - 16 * carry)
+    assert carry == 0 and digs[-1] >= 0
+    sdigs = [(s >> (24 * i)) & (2**24 - 1) for i in range(6)]
+    pt = [limbs(0), limbs(1), limbs(1), limbs(0)]
+    for it in range(32, -1, -1):
+        e = digs[it]
+        if it != 32:
+            for _ in range(4):
+                pt = to_p3(dbl(pt))
+        ce = tab[abs(e)]
+        pt = cneg(pt, (0, 3), e < 0, P4)
+        rt = padd(pt, ce)
+        rt = cneg(rt, (0,), e < 0, P8)
+        pt = to_p3(rt)
+        if it % 6 == 0:
+            b = edwards_mul(sdigs[it // 6], BASE)
+            ypx, ymx, xy2d = (b[1] + b[0]) % P, (b[1] - b[0]) % P, 2 * D * b[0] * b[1] % P
+            pt = to_p3(padd(pt, [limbs(ymx), limbs(ypx), limbs(xy2d), limbs(2)]))
+    negA = ((P - A[0]) % P, A[1])
+    want = edwards_add(edwards_mul(c, negA), edwards_mul(s, BASE))
+    assert ext(pt) == want
