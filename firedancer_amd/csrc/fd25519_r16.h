@@ -20,8 +20,9 @@
 
    A point is four rows of one wave: row q holds coordinate q, as lane q of
    a quad does in fd25519_ge4.h, whose formulas (same products, same order)
-   are followed step for step; operands move between rows with
-   ds_bpermute (r16_rp).
+   are followed step for step; operands move between rows with gfx950's
+   permlane swaps and per-row bit selects (ds_bpermute, r16_rp, only for
+   the final identity test).
 
    Bounds (every limb is unsigned; "tight" = < 2^16 + 64):
      r16_mul / r16_sq take limbs < 2^19 and return tight limbs:
@@ -42,12 +43,15 @@
 #define R16_BC(x, t)  ((uint32_t)__builtin_amdgcn_mov_dpp((int)(x), 0x150 + (t), 0xf, 0xf, true))   /* row_newbcast:t */
 #define R16_ROR(x, t) ((uint32_t)__builtin_amdgcn_mov_dpp((int)(x), 0x120 + (t), 0xf, 0xf, true))   /* row_ror:t      */
 
-/* per-lane constants, made once per kernel */
+/* per-lane constants, made once per kernel.  Everything that differs by
+   row is selected with these masks (and, or): a branch on the row would
+   make the wave run each row's side in turn. */
 struct r16ctx {
   uint32_t m[16];     /* m[t] = 38 if c < t else 1: the wrap factor of term t in lane c */
   uint32_t p4, p8;    /* limb c of 4p / 8p (all limbs positive, above any tight / < 2^18 - 152 limb) */
   uint32_t c;         /* lane in row */
   uint32_t row;       /* row (coordinate) in the wave */
+  uint32_t r0, r1, r2, r3, r03, r12;   /* all ones in rows 0 / 1 / 2 / 3 / 0 and 3 / 1 and 2, else 0 */
 };
 
 FD_DEV void r16_init(r16ctx& k) {
@@ -57,6 +61,9 @@ FD_DEV void r16_init(r16ctx& k) {
   for (int t = 0; t < 16; t++) k.m[t] = k.c < (uint32_t)t ? 38u : 1u;
   k.p4 = k.c ? (1u << 17) - 2u : (1u << 17) - 76u;
   k.p8 = k.c ? (1u << 18) - 4u : (1u << 18) - 152u;
+  k.r0 = 0u - (uint32_t)(k.row == 0u); k.r1 = 0u - (uint32_t)(k.row == 1u);
+  k.r2 = 0u - (uint32_t)(k.row == 2u); k.r3 = 0u - (uint32_t)(k.row == 3u);
+  k.r03 = k.r0 | k.r3; k.r12 = k.r1 | k.r2;
 }
 
 /* three carry rounds of a column sum < 2^47.2 (see the header) */
@@ -88,8 +95,36 @@ FD_DEV uint32_t r16_sq(uint32_t f, const r16ctx& k) { return r16_mul(f, f, k); }
    broadcast of the four rows, one instruction) */
 template <int S0, int S1, int S2, int S3>
 FD_DEV uint32_t r16_rp(uint32_t x, const r16ctx& k) {
-  const uint32_t src = k.row == 0u ? (uint32_t)S0 : k.row == 1u ? (uint32_t)S1 : k.row == 2u ? (uint32_t)S2 : (uint32_t)S3;
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((src << 4) | k.c) << 2), (int)x);
+  constexpr uint32_t PACK = (uint32_t)(S0 | (S1 << 2) | (S2 << 4) | (S3 << 6));
+  const uint32_t src = (PACK >> (2u * k.row)) & 3u;
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((src << 6) | (k.c << 2)), (int)x);
+}
+
+/* Row moves without LDS: gfx950's v_permlane16_swap / v_permlane32_swap
+   with both operands x (measured, tools/ubench/permlane_probe.hip):
+     swap16 -> e = (x0, x0, x2, x2), o = (x1, x1, x3, x3)
+     swap32 -> l = (x0, x1, x0, x1), h = (x2, x3, x2, x3)
+   (xq = row q of x), combined with per-row bit selects (v_bfi_b32).  A
+   VALU op each, where a ds_bpermute waits on the LDS pipe. */
+struct r16_eo { uint32_t e, o; };
+struct r16_lh { uint32_t l, h; };
+
+FD_DEV r16_eo r16_swap16(uint32_t x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return {(uint32_t)r[0], (uint32_t)r[1]};
+}
+FD_DEV r16_lh r16_swap32(uint32_t x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return {(uint32_t)r[0], (uint32_t)r[1]};
+}
+
+/* bits of a where m, of b elsewhere */
+FD_DEV uint32_t r16_bsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+
+/* (x1, x0, x3, x2) */
+FD_DEV uint32_t r16_xor1(uint32_t x, const r16ctx& k) {
+  const r16_eo s = r16_swap16(x);
+  return r16_bsel(k.r1 | k.r3, s.e, s.o);
 }
 
 /* ---- conversions with the one-lane radix-2^25.5 form ------------------- */
@@ -136,12 +171,15 @@ FD_DEV bool r16_iszero(uint32_t x) {
 
 /* ---- group operations (fd25519_ge4.h's, a row per coordinate) ---------- */
 
-/* x in rows where sel, else y */
-FD_DEV uint32_t r16_sel(bool sel, uint32_t x, uint32_t y) { return sel ? x : y; }
-
 /* p1p1 -> p3 (or p2): (X T, Y Z, Z T, X Y); r < 2^19 in, tight out */
 FD_DEV uint32_t ge16_to_p3(uint32_t r, const r16ctx& k) {
-  const uint32_t a = r16_rp<0, 1, 2, 0>(r, k), b = r16_rp<3, 2, 3, 1>(r, k);
+  /* a = (r0, r1, r2, r0): row 3 takes the broadcast of r0 (swap32 of swap16's e) */
+  const uint32_t b0 = r16_swap32(r16_swap16(r).e).l;
+  const uint32_t a = r16_bsel(k.r3, b0, r);
+  /* b = (r3, r2, r3, r1): the broadcasts of r2, r3 (swap16 of swap32's h), r1 from swap32's l */
+  const r16_lh s = r16_swap32(r);
+  const r16_eo t = r16_swap16(s.h);
+  const uint32_t b = r16_bsel(k.r3, s.l, r16_bsel(k.r1, t.e, t.o));
   return r16_mul(a, b, k);
 }
 
@@ -149,46 +187,55 @@ FD_DEV uint32_t ge16_to_p3(uint32_t r, const r16ctx& k) {
    rows 0..3, then (X+Y)^2 - (X^2+Y^2), X^2+Y^2, Y^2-X^2, 2Z^2-(Y^2-X^2)
    (ge4_dbl, ge_p2_dbl) */
 FD_DEV uint32_t ge16_dbl(uint32_t p, const r16ctx& k) {
-  const uint32_t a = r16_rp<0, 1, 0, 2>(p, k), b = r16_rp<0, 0, 1, 0>(p, k);
-  const uint32_t u = a + (k.row == 2u ? b : 0u);                /* X, Y, X+Y, Z      < 2^17.1 */
+  /* u = (X, Y, X+Y, Z): swap32's l is (X, Y, X, Y), the broadcast of Y
+     (swap32 of swap16's o) is added in row 2, row 3 takes swap16's e (Z) */
+  const r16_eo pe = r16_swap16(p);
+  const uint32_t by = r16_swap32(pe.o).l;
+  const uint32_t u = r16_bsel(k.r3, pe.e, r16_swap32(p).l + (by & k.r2));   /* < 2^17.1 */
   uint32_t s = r16_sq(u, k);                                    /* tight             */
-  s = k.row == 3u ? s + s : s;                                  /* 2Z^2              < 2^17.1 */
-  const uint32_t w = r16_rp<1, 0, 3, 2>(s, k);                  /* s1, s0, s3, s2    */
+  s += s & k.r3;                                                /* 2Z^2              < 2^17.1 */
+  const uint32_t w = r16_xor1(s, k);                            /* s1, s0, s3, s2    */
   /* row 0: s0 + s1 (< 2^17.1), row 1: s1 - s0 (s1 + 4p - s0 < 2^17.6), rows 2, 3: s2, s3 */
-  const uint32_t t = k.row == 0u ? s + w : k.row == 1u ? s + k.p4 - w : s;
-  const uint32_t x = r16_rp<2, 0, 1, 3>(t, k);                  /* s2, t0, t1, s3    */
-  const uint32_t y = r16_rp<0, 0, 0, 1>(t, k);                  /* t0 (row 0), t1 (row 3) */
+  const uint32_t t = s + ((w & k.r0) | ((k.p4 - w) & k.r1));
+  /* x = (t2, t0, t1, t3): swap32's h, swap16's e, the broadcast of t1, t;
+     y = (t0, -, -, t1) = swap32's l */
+  const r16_lh tl = r16_swap32(t);
+  const r16_eo te = r16_swap16(t);
+  const uint32_t b1 = r16_swap32(te.o).l;
+  const uint32_t x = r16_bsel(k.r0, tl.h, r16_bsel(k.r1, te.e, r16_bsel(k.r2, b1, t)));
+  const uint32_t y = tl.l;
   /* row 0: s2 + 8p - t0, row 3: s3 + 8p - t1 (t0, t1 < 2^17.6 < 2^18 - 152): < 2^18.6 */
-  return (k.row == 0u || k.row == 3u) ? x + k.p8 - y : x;
+  return x + ((k.p8 - y) & k.r03);
 }
 
-/* r = p + q (p3 in, tight; q in qc form (Y-X, Y+X, 2dT, 2Z), < 2^19; p1p1
-   out): b = (Y-X)(Y2-X2), a = (Y+X)(Y2+X2), c = T 2dT2, t = Z 2Z2 in rows
-   0..3, then (a - b, a + b, t + c, t - c) (ge4_add) */
+/* r = p + q (p3 in, limbs < 2^17 -- tight, or 4p - tight where negated;
+   q in qc form (Y-X, Y+X, 2dT, 2Z), < 2^19; p1p1 out): b = (Y-X)(Y2-X2),
+   a = (Y+X)(Y2+X2), c = T 2dT2, t = Z 2Z2 in rows 0..3, then
+   (a - b, a + b, t + c, t - c) (ge4_add) */
 FD_DEV uint32_t ge16_add(uint32_t p, uint32_t qc, const r16ctx& k) {
-  const uint32_t v = r16_rp<1, 0, 3, 2>(p, k);                  /* Y, X, T, Z        */
-  /* row 0: Y + 4p - X (< 2^17.6), row 1: X + Y (< 2^17.1), rows 2, 3: T, Z */
-  const uint32_t o = k.row == 0u ? v + k.p4 - p : k.row == 1u ? v + p : v;
+  const uint32_t v = r16_xor1(p, k);                            /* Y, X, T, Z        */
+  /* row 0: Y + 4p - X (< 2^18), row 1: X + Y (< 2^18), rows 2, 3: T, Z */
+  const uint32_t o = v + (((k.p4 - p) & k.r0) | (p & k.r1));
   const uint32_t pr = r16_mul(o, qc, k);                        /* b, a, c, t: tight */
-  const uint32_t w = r16_rp<1, 0, 3, 2>(pr, k);                 /* a, b, t, c        */
+  const uint32_t w = r16_xor1(pr, k);                           /* a, b, t, c        */
   /* row 0: a + 4p - b, row 1: a + b, row 2: c + t, row 3: t + 4p - c: < 2^17.6 */
-  return k.row == 0u ? w + k.p4 - pr : k.row == 3u ? pr + k.p4 - w : w + pr;
+  return ((w + pr) & k.r12) | ((w + k.p4 - pr) & k.r0) | ((pr + k.p4 - w) & k.r3);
 }
 
-/* -P in the rows of `rows` when neg: 4p - x for tight x (p3), 8p - x for
-   x < 2^18 - 152 (a p1p1's row 0) */
-FD_DEV uint32_t ge16_cneg4(uint32_t x, bool rows, bool neg, const r16ctx& k) {
-  return (rows && neg) ? k.p4 - x : x;
+/* -x in the rows of the mask `rows` when neg (wave-uniform): 4p - x for
+   tight x (p3), 8p - x for x < 2^18 - 152 (a p1p1's row 0) */
+FD_DEV uint32_t ge16_cneg4(uint32_t x, uint32_t rows, bool neg, const r16ctx& k) {
+  return neg ? (x ^ ((x ^ (k.p4 - x)) & rows)) : x;
 }
-FD_DEV uint32_t ge16_cneg8(uint32_t x, bool rows, bool neg, const r16ctx& k) {
-  return (rows && neg) ? k.p8 - x : x;
+FD_DEV uint32_t ge16_cneg8(uint32_t x, uint32_t rows, bool neg, const r16ctx& k) {
+  return neg ? (x ^ ((x ^ (k.p8 - x)) & rows)) : x;
 }
 
-/* qc of a p3 (tight): (Y-X, Y+X, 2dT, 2Z), < 2^17.6 */
+/* qc of a p3 (limbs < 2^17): (Y-X, Y+X, 2dT, 2Z), < 2^18 */
 FD_DEV uint32_t ge16_to_qc(uint32_t p, uint32_t d2, const r16ctx& k) {
-  const uint32_t v = r16_rp<1, 0, 3, 2>(p, k);                  /* Y, X, T, Z        */
+  const uint32_t v = r16_xor1(p, k);                            /* Y, X, T, Z        */
   const uint32_t t = r16_mul(v, d2, k);                         /* row 2: 2d T       */
-  return k.row == 0u ? v + k.p4 - p : k.row == 1u ? v + p : k.row == 2u ? t : v + v;
+  return ((v + k.p4 - p) & k.r0) | ((v + p) & k.r1) | (t & k.r2) | ((v + v) & k.r3);
 }
 
 /* limb c of the constant 1 / 2 (row-independent) */
@@ -201,9 +248,9 @@ FD_DEV void table16_build(uint32_t (&tab)[9], uint32_t x, uint32_t y, bool negat
   const uint32_t xs = negate ? k.p4 - x : x;                    /* < 2^17 */
   const uint32_t xy = r16_mul(xs, y, k);
   const uint32_t one = r16_small(1u, k);
-  const uint32_t p0 = k.row == 0u ? xs : k.row == 1u ? y : k.row == 2u ? one : xy;   /* (x, y, 1, xy) */
+  const uint32_t p0 = (xs & k.r0) | (y & k.r1) | (one & k.r2) | (xy & k.r3);   /* (x, y, 1, xy) */
   /* the identity (1, 1, 0, 2) */
-  tab[0] = k.row == 2u ? 0u : k.row == 3u ? r16_small(2u, k) : one;
+  tab[0] = (one & (k.r0 | k.r1)) | (r16_small(2u, k) & k.r3);
   const uint32_t c1 = ge16_to_qc(p0, d2, k);
   tab[1] = c1;
   uint32_t cur = p0;

@@ -1163,8 +1163,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
 /* this lane's r16 limb of its row's coordinate of base entry e, as qc
    (y-x, y+x, 2dxy, 2) */
 FD_DEV uint32_t btab16_r16(const int32_t* g_btab, int e, const r16ctx& k) {
-  if (k.row == 3u) return r16_small(2u, k);
-  const int off = k.row == 0u ? 10 : (k.row == 1u ? 0 : 20);
+  const int off = (int)((k.r0 & 10u) | (k.r2 & 20u));   /* row 3 loads row 1's (y+x) and drops it */
   const int2* src = reinterpret_cast<const int2*>(g_btab + (size_t)e * FD_ED25519_BTAB16_STRIDE + off);
   fe c;
 #pragma unroll
@@ -1173,7 +1172,7 @@ FD_DEV uint32_t btab16_r16(const int32_t* g_btab, int e, const r16ctx& k) {
     c.v[2 * q] = x.x;
     c.v[2 * q + 1] = x.y;
   }
-  return r16_from_fe(c, k);
+  return (r16_from_fe(c, k) & ~k.r3) | (r16_small(2u, k) & k.r3);
 }
 
 template <int BW>
@@ -1213,7 +1212,7 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
   W = __builtin_amdgcn_readfirstlane(W);
   const int32_t* btab = half ? p.btab_hi : p.btab_lo;
   const uint32_t one = r16_small(1u, k);
-  uint32_t P = (k.row == 1u || k.row == 2u) ? one : 0u;   /* identity (0, 1, 1, 0) */
+  uint32_t P = one & k.r12;   /* identity (0, 1, 1, 0) */
 #pragma clang loop unroll(disable)
   for (int it = W - 1; it >= 0; it--) {
     int e = pop160<4>(sd);
@@ -1228,9 +1227,9 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
     }
     uint32_t b = 0u;
     if (badd) b = btab16_r16(btab, (int)bdig, k);
-    P = ge16_cneg4(P, k.row == 0u || k.row == 3u, e < 0, k);
+    P = ge16_cneg4(P, k.r03, e < 0, k);
     uint32_t Rt = ge16_add(P, ce, k);
-    Rt = ge16_cneg8(Rt, k.row == 0u, e < 0, k);
+    Rt = ge16_cneg8(Rt, k.r0, e < 0, k);
     P = ge16_to_p3(Rt, k);
     if (badd) P = ge16_to_p3(ge16_add(P, b, k), k);
   }
@@ -1242,7 +1241,7 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
   P = ge16_to_p3(ge16_add(P, hand[threadIdx.x], k), k);
   /* identity: X == 0 (row 0) and Y == Z (row 1: Y + 4p - Z) */
   const uint32_t z = r16_rp<2, 2, 2, 2>(P, k);
-  const bool zero = r16_iszero(k.row == 1u ? P + k.p4 - z : P);
+  const bool zero = r16_iszero(P + ((k.p4 - z) & k.r1));
   const uint64_t bal = __ballot(zero);
   const bool ident = (bal & 1ull) && (bal & (1ull << 16));
   if (code == FD_PENDING) code = ident ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;

@@ -249,3 +249,45 @@ def test_window_loop_matches_scalar_multiplication(seed):
     negA = ((P - A[0]) % P, A[1])
     want = edwards_add(edwards_mul(c, negA), edwards_mul(s, BASE))
     assert ext(pt) == want
+
+
+# ---- the device's row moves (fd25519_r16.h): gfx950's permlane swaps as
+# measured by tools/ubench/permlane_probe.hip, composed with per-row selects
+
+def swap16(x):
+    """v_permlane16_swap_b32 with both operands x -> (e, o)"""
+    return [x[0], x[0], x[2], x[2]], [x[1], x[1], x[3], x[3]]
+
+
+def swap32(x):
+    """v_permlane32_swap_b32 with both operands x -> (l, h)"""
+    return [x[0], x[1], x[0], x[1]], [x[2], x[3], x[2], x[3]]
+
+
+def bsel(rows, a, b):
+    return [a[q] if q in rows else b[q] for q in range(4)]
+
+
+def test_row_moves_compose_the_quad_permutations():
+    x = ["x0", "x1", "x2", "x3"]
+    # r16_xor1
+    e, o = swap16(x)
+    assert bsel((1, 3), e, o) == rp(x, (1, 0, 3, 2))
+    # ge16_to_p3's a = (x0, x1, x2, x0) and b = (x3, x2, x3, x1)
+    b0 = swap32(swap16(x)[0])[0]
+    assert bsel((3,), b0, x) == rp(x, (0, 1, 2, 0))
+    l, h = swap32(x)
+    te, to = swap16(h)
+    assert bsel((3,), l, bsel((1,), te, to)) == rp(x, (3, 2, 3, 1))
+    # ge16_dbl's u = (x0, x1, x0 + x1, x2)
+    pe, po = swap16(x)
+    by = swap32(po)[0]
+    u = bsel((3,), pe, [a + ("+" + b if q == 2 else "") for q, (a, b) in enumerate(zip(swap32(x)[0], by))])
+    assert u == ["x0", "x1", "x0+x1", "x2"]
+    # ... its x = (t2, t0, t1, t3) and y = (t0, -, -, t1)
+    tl, th = swap32(x)
+    te, to = swap16(x)
+    b1 = swap32(to)[0]
+    assert bsel((0,), th, bsel((1,), te, bsel((2,), b1, x))) == rp(x, (2, 0, 1, 3))
+    y = tl
+    assert (y[0], y[3]) == ("x0", "x1")
