@@ -169,6 +169,141 @@ FD_DEV bool r16_iszero(uint32_t x) {
   return z == 0u || q == 0u;
 }
 
+/* limb c of the constant 1 / 2 (row-independent) */
+FD_DEV uint32_t r16_small(uint32_t v, const r16ctx& k) { return k.c ? 0u : v; }
+
+/* the canonical 16-bit digits of the row's element (limbs < 2^19), in every
+   lane of the row: r16_iszero's folds, then value - p when value >= p
+   (value + 19 reaches bit 255) */
+FD_DEV void r16_digits(uint32_t (&l)[16], uint32_t x) {
+  l[0] = R16_BC(x, 0); l[1] = R16_BC(x, 1); l[2] = R16_BC(x, 2); l[3] = R16_BC(x, 3);
+  l[4] = R16_BC(x, 4); l[5] = R16_BC(x, 5); l[6] = R16_BC(x, 6); l[7] = R16_BC(x, 7);
+  l[8] = R16_BC(x, 8); l[9] = R16_BC(x, 9); l[10] = R16_BC(x, 10); l[11] = R16_BC(x, 11);
+  l[12] = R16_BC(x, 12); l[13] = R16_BC(x, 13); l[14] = R16_BC(x, 14); l[15] = R16_BC(x, 15);
+  uint64_t acc = 0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) { acc += l[c]; l[c] = (uint32_t)acc & 0xffffu; acc >>= 16; }
+#pragma unroll
+  for (int pass = 0; pass < 2; pass++) {
+    acc = acc * 38u + 19u * (l[15] >> 15);
+    l[15] &= 0x7fffu;
+#pragma unroll
+    for (int c = 0; c < 16; c++) { acc += l[c]; l[c] = (uint32_t)acc & 0xffffu; acc >>= 16; }
+  }
+  /* < 2^255 + 2^6 */
+  uint32_t t[16], a = 19u;
+#pragma unroll
+  for (int c = 0; c < 16; c++) { a += l[c]; t[c] = a & 0xffffu; a >>= 16; }
+  const bool ge = (t[15] >> 15) != 0u;
+  t[15] &= 0x7fffu;
+#pragma unroll
+  for (int c = 0; c < 16; c++) l[c] = ge ? t[c] : l[c];
+}
+
+/* digits -> 8 little-endian words */
+FD_DEV void r16_words(uint32_t (&w)[8], const uint32_t (&l)[16]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = l[2 * i] | (l[2 * i + 1] << 16);
+}
+
+FD_DEV uint32_t r16_sqn(uint32_t x, int n, const r16ctx& k) {
+#pragma clang loop unroll(disable)
+  for (int i = 0; i < n; i++) x = r16_sq(x, k);
+  return x;
+}
+
+/* z^(2^252-3): fe_pow22523's chain (fd_f25519_pow22523,
+   src/ballet/ed25519/fd_f25519.c:11-59), 250 squarings and 11 products */
+FD_DEV uint32_t r16_pow22523(uint32_t z, const r16ctx& k) {
+  uint32_t t0 = r16_sq(z, k);
+  uint32_t t1 = r16_sqn(t0, 2, k);
+  t1 = r16_mul(z, t1, k);
+  t0 = r16_mul(t0, t1, k);
+  t0 = r16_sq(t0, k);
+  t0 = r16_mul(t1, t0, k);
+  t1 = r16_sqn(t0, 5, k);
+  t0 = r16_mul(t1, t0, k);
+  t1 = r16_sqn(t0, 10, k);
+  t1 = r16_mul(t1, t0, k);
+  uint32_t t2 = r16_sqn(t1, 20, k);
+  t1 = r16_mul(t2, t1, k);
+  t1 = r16_sqn(t1, 10, k);
+  t0 = r16_mul(t1, t0, k);
+  t1 = r16_sqn(t0, 50, k);
+  t1 = r16_mul(t1, t0, k);
+  t2 = r16_sqn(t1, 100, k);
+  t1 = r16_mul(t2, t1, k);
+  t1 = r16_sqn(t1, 50, k);
+  t0 = r16_mul(t1, t0, k);
+  t0 = r16_sqn(t0, 2, k);
+  return r16_mul(t0, z, k);
+}
+
+/* ---- point decompression, a row per point (fd25519_dsm.h ge_decode) -----
+
+   y: the row's encoding as limbs (lane c: bits 16c..16c+15, bit 255
+   cleared), sign: bit 255.  Returns x's canonical words before its sign is
+   applied (the caller negates when `neg`), and ge_decode's fail / small
+   verdicts: x = u v^3 (u v^7)^((p-5)/8), u = y^2 - 1, v = d y^2 + 1; a root
+   when v x^2 = u, times sqrt(-1) when v x^2 = -u, else no root; the
+   AVX-512 rule also rejects x = 0 with the sign set; small order on the
+   canonical y (x = 0, y = 0 or y = the order-8 points' y).  Every operand
+   stays < 2^19: u + 4p - 1 < 2^17.6, v + 1 < 2^16 + 65, v x^2 + 8p - u
+   (u < 2^18 - 152) < 2^18.4, v x^2 + u < 2^17.7. */
+struct r16_dec {
+  uint32_t x[8];
+  bool neg, fail, small;
+};
+
+FD_DEV void decode16(r16_dec& o, uint32_t y, uint32_t sign, bool avx_rule, uint32_t d, uint32_t sqrtm1,
+                     const r16ctx& k) {
+  const uint32_t one = r16_small(1u, k);
+  uint32_t u = r16_sq(y, k);
+  uint32_t v = r16_mul(u, d, k) + one;                          /* d y^2 + 1  */
+  u = u + k.p4 - one;                                           /* y^2 - 1    */
+  const uint32_t v3 = r16_mul(r16_sq(v, k), v, k);              /* v^3        */
+  uint32_t x = r16_mul(r16_mul(r16_sq(v3, k), v, k), u, k);     /* u v^7      */
+  x = r16_pow22523(x, k);
+  x = r16_mul(r16_mul(x, v3, k), u, k);
+  const uint32_t vxx = r16_mul(r16_sq(x, k), v, k);
+  uint32_t l[16];
+  uint32_t z = 0u;
+  r16_digits(l, vxx + k.p8 - u);
+#pragma unroll
+  for (int c = 0; c < 16; c++) z |= l[c];
+  const bool root = z == 0u;
+  z = 0u;
+  r16_digits(l, vxx + u);
+#pragma unroll
+  for (int c = 0; c < 16; c++) z |= l[c];
+  const bool iroot = z == 0u;
+  const uint32_t xi = r16_mul(x, sqrtm1, k);
+  r16_digits(l, root ? x : xi);
+  z = 0u;
+#pragma unroll
+  for (int c = 0; c < 16; c++) z |= l[c];
+  const bool x0 = z == 0u;
+  r16_words(o.x, l);
+  o.fail = !(root || iroot) || (avx_rule && x0 && sign);
+  o.neg = (l[0] & 1u) != sign;
+  /* small order on the canonical y */
+  r16_digits(l, y);
+  uint32_t yw[8];
+  r16_words(yw, l);
+  const uint32_t y0[8] = {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u,
+                          0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du};
+  const uint32_t y1[8] = {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du,
+                          0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u};
+  uint32_t zy = 0u, e0 = 0u, e1 = 0u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    zy |= yw[i];
+    e0 |= yw[i] ^ y0[i];
+    e1 |= yw[i] ^ y1[i];
+  }
+  o.small = x0 || zy == 0u || e0 == 0u || e1 == 0u;
+}
+
 /* ---- group operations (fd25519_ge4.h's, a row per coordinate) ---------- */
 
 /* p1p1 -> p3 (or p2): (X T, Y Z, Z T, X Y); r < 2^19 in, tight out */
@@ -237,9 +372,6 @@ FD_DEV uint32_t ge16_to_qc(uint32_t p, uint32_t d2, const r16ctx& k) {
   const uint32_t t = r16_mul(v, d2, k);                         /* row 2: 2d T       */
   return ((v + k.p4 - p) & k.r0) | ((v + p) & k.r1) | (t & k.r2) | ((v + v) & k.r3);
 }
-
-/* limb c of the constant 1 / 2 (row-independent) */
-FD_DEV uint32_t r16_small(uint32_t v, const r16ctx& k) { return k.c ? 0u : v; }
 
 /* [0..8](sign P) as qc entries, one register per entry (the lane's limb
    of its row's coordinate), for the affine point (x, y) given as r16

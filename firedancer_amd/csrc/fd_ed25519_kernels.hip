@@ -1249,6 +1249,62 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
 }
 
 /* ------------------------------------------------------------------------
+   prep16: the dsm16 chunks' prep, with the decompressions spread over the
+   lanes as dsm16's products are.  The one-lane decode is a chain of 250
+   dependent squarings (~490 cycles each, fe_sq_u); a row of 16 lanes runs
+   one in ~300 (profiles/r5_lanesplit_ubench.txt), so a wave decodes four
+   points (row q: point 4w + q, A and R of two signatures) in about 60% of
+   the time.  One wave per block: the first hash_waves blocks hash and find
+   the half-size scalars of 64 signatures each (prep's wave 0), the others
+   decode.  Outputs are decode_one's: x in fe_mul's carried form with its
+   sign applied, y as fe_frombytes of the encoding, the flags. */
+FD_DEV void decode16_wave(const fd_ed25519_verify_params_t& p, uint64_t dw) {
+  r16ctx k;
+  r16_init(k);
+  const uint64_t pt = 4u * dw + k.row;
+  const int which = (int)(pt & 1u);   /* 0: A (public key), 1: R */
+  const bool live = (pt >> 1) < p.n;
+  const uint64_t j = live ? pt >> 1 : p.n - 1u;   /* an idle row repeats a live point, its result dropped */
+  const uint64_t i = p.base + j;
+  const uint32_t* src = which ? reinterpret_cast<const uint32_t*>(p.sigs + 64 * i)
+                              : reinterpret_cast<const uint32_t*>(p.pubs + 32 * i);
+  const uint32_t wd = src[k.c >> 1], w7 = src[7];
+  uint32_t y = (k.c & 1u) ? wd >> 16 : wd & 0xffffu;
+  y &= k.c == 15u ? 0x7fffu : 0xffffu;
+  const uint32_t d = r16_from_fe(fe{FE_D}, k), sqrtm1 = r16_from_fe(fe{FE_SQRTM1}, k);
+  r16_dec o;
+  decode16(o, y, w7 >> 31, !p.codes_portable, d, sqrtm1, k);
+  if (live && k.c == 0u) {
+    uint32_t s[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) s[q] = src[q];
+    fe x, fy, t;
+    fe_frombytes(t, o.x);
+    fe_carry(x, t);
+    if (o.neg) fe_neg(x, x);
+    fe_frombytes(fy, s);
+    int32_t* dst = p.pts + (uint64_t)which * 20 * p.cap + j;
+#pragma unroll
+    for (int l = 0; l < 10; l++) {
+      dst[(uint64_t)l * p.cap] = x.v[l];
+      dst[(uint64_t)(10 + l) * p.cap] = fy.v[l];
+    }
+    p.pflag[(uint64_t)which * p.cap + j] = (uint8_t)((o.fail ? FD_PF_FAIL : 0u) | (o.small ? FD_PF_SMALL : 0u));
+  }
+}
+
+__global__ void __launch_bounds__(64) fd_ed25519_prep16_kernel(fd_ed25519_verify_params_t p, uint32_t hash_waves) {
+  if (blockIdx.x < hash_waves) {
+    const uint64_t t = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (t >= p.n) return;
+    hash_one(p, t);
+    scalar_one(p, t);
+    return;
+  }
+  decode16_wave(p, blockIdx.x - hash_waves);
+}
+
+/* ------------------------------------------------------------------------
    Base tables [0..entries)B as (y+x, y-x, 2dxy), one entry per lane:
    [e]B by double-and-add over `bits` bits, then affine. */
 
@@ -1539,6 +1595,11 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
   const uint32_t blk = 256;
   switch (phase) {
   case FD_ED25519_PHASE_HASH: {
+    if (p->small == 3) {   /* dsm16 chunks: the decompressions lane-split too */
+      const uint32_t hw = (uint32_t)((p->n + 63) / 64), dw = (uint32_t)((p->n + 1) / 2);
+      hipLaunchKernelGGL(fd_ed25519_prep16_kernel, dim3(hw + dw), dim3(64), 0, st, *p, hw);
+      break;
+    }
     if (p->small) {
       hipLaunchKernelGGL(fd_ed25519_prep_kernel, dim3((uint32_t)((p->n + 63) / 64)), dim3(192), 0, st, *p);
       break;

@@ -291,3 +291,104 @@ def test_row_moves_compose_the_quad_permutations():
     assert bsel((0,), th, bsel((1,), te, bsel((2,), b1, x))) == rp(x, (2, 0, 1, 3))
     y = tl
     assert (y[0], y[3]) == ("x0", "x1")
+
+
+# ---- prep16's decompression (fd25519_r16.h decode16, a row per point)
+
+def digits(x):
+    """r16_digits: the canonical digits from limbs < 2^19, in the device's steps"""
+    assert all(0 <= v < B_IN for v in x)
+    l, acc = list(x), 0
+    for c in range(16):
+        acc += l[c]
+        l[c], acc = acc & 0xffff, acc >> 16
+    for _ in range(2):
+        acc = acc * 38 + 19 * (l[15] >> 15)
+        l[15] &= 0x7fff
+        for c in range(16):
+            acc += l[c]
+            l[c], acc = acc & 0xffff, acc >> 16
+    assert acc == 0
+    v = sum(d << (16 * c) for c, d in enumerate(l))
+    assert v < 2**255 + 2**6, "the folds leave less than 2^255 + 2^6"
+    t, a = [], 19
+    for c in range(16):
+        a += l[c]
+        t.append(a & 0xffff)
+        a >>= 16
+    if t[15] >> 15:
+        t[15] &= 0x7fff
+        l = t
+    assert sum(d << (16 * c) for c, d in enumerate(l)) == v % P
+    return l
+
+
+SQRTM1 = pow(2, (P - 1) // 4, P)
+Y0 = 0x05fc536d880238b13933c6d305acdfd5f098eff289f4c345b027b2c28f95e826
+Y1 = 0x7a03ac9277fdc74ec6cc392cfa53202a0f67100d760b3cba4fd84d3d706a17c7
+
+
+def decode16(enc, avx_rule):
+    """decode16's steps on the model's limbs -> (x with its sign applied, fail, small)"""
+    y = [(enc >> (16 * c)) & 0xffff for c in range(16)]
+    y[15] &= 0x7fff
+    sign = enc >> 255
+    one = limbs(1)
+    u = r16_mul(y, y)
+    v = add(r16_mul(u, limbs(D)), one)
+    u = sub(u, one, P4)
+    v3 = r16_mul(r16_mul(v, v), v)
+    x = r16_mul(r16_mul(r16_mul(v3, v3), v), u)
+    # the addition chain's value (r16_pow22523 is r16_mul / r16_sq, modelled above)
+    x = limbs(pow(val(x), 2**252 - 3, P))
+    x = r16_mul(r16_mul(x, v3), u)
+    vxx = r16_mul(r16_mul(x, x), v)
+    root = not any(digits(sub(vxx, u, P8)))
+    iroot = not any(digits(add(vxx, u)))
+    xi = r16_mul(x, limbs(SQRTM1))
+    xd = digits(x if root else xi)
+    x0 = not any(xd)
+    xv = sum(d << (16 * c) for c, d in enumerate(xd))
+    fail = not (root or iroot) or (avx_rule and x0 and sign == 1)
+    xv = (P - xv) % P if (xd[0] & 1) != sign else xv
+    yc = sum(d << (16 * c) for c, d in enumerate(digits(y)))
+    small = x0 or yc in (0, Y0, Y1)
+    return xv, fail, small
+
+
+def decode_ref(enc, avx_rule):
+    """ge_decode's rules (fd25519_dsm.h; fd_ed25519_point_frombytes_2x and
+    fd_ed25519_affine_is_small_order) on Python integers"""
+    y, sign = enc & (2**255 - 1), enc >> 255
+    u, v = (y * y - 1) % P, (D * y * y + 1) % P
+    x = u * pow(v, 3, P) * pow(u * pow(v, 7, P), (P - 5) // 8, P) % P
+    vxx = v * x * x % P
+    root, iroot = vxx == u, vxx == (P - u) % P
+    if not root:
+        x = x * SQRTM1 % P
+    x0 = x == 0
+    fail = not (root or iroot) or (avx_rule and x0 and sign == 1)
+    if (x & 1) != sign:
+        x = (P - x) % P
+    return x, fail, x0 or y % P in (0, Y0, Y1)
+
+
+def test_decode16_matches_ge_decode():
+    rng = random.Random(16)
+    encs = []
+    for _ in range(40):   # points of the group, both signs of x
+        x, y = edwards_mul(rng.randrange(1, 2**252), BASE)
+        encs.append(y | ((x & 1) << 255))
+        encs.append(y | (((x & 1) ^ 1) << 255))
+    encs += [rng.randrange(2**256) for _ in range(40)]          # mostly no root
+    specials = [0, 1, P - 1, P, P + 1, 2**255 - 1, Y0, Y1, P - Y0 % P, 2**255 - 20, 2**255 - 19]
+    encs += specials + [s | (1 << 255) for s in specials]
+    for enc in encs:
+        for avx_rule in (True, False):
+            xv, fail, small = decode16(enc, avx_rule)
+            want = decode_ref(enc, avx_rule)
+            if want[1]:
+                assert fail, hex(enc)          # x is not used when the point fails
+                assert small == want[2], hex(enc)
+            else:
+                assert (xv, fail, small) == want, hex(enc)
