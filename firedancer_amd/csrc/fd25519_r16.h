@@ -19,10 +19,11 @@
    chip would otherwise idle.
 
    A point is four rows of one wave: row q holds coordinate q, as lane q of
-   a quad does in fd25519_ge4.h, whose formulas (same products, same order)
-   are followed step for step; operands move between rows with gfx950's
-   permlane swaps and per-row bit selects (ds_bpermute, r16_rp, only for
-   the final identity test).
+   a quad does in fd25519_ge4.h.  Each group operation is two rounds of
+   four products (one per row); between them every row gets all four
+   products of the first round (gfx950's permlane swaps, ge16_dbl2 /
+   ge16_add2) and picks its operands with per-row bit selects (ds_bpermute,
+   r16_rp, only for the final identity test).
 
    Bounds (every limb is unsigned; "tight" = < 2^16 + 64):
      r16_mul / r16_sq take limbs < 2^19 and return tight limbs:
@@ -79,8 +80,10 @@ FD_DEV uint32_t r16_carry(uint64_t acc, const r16ctx& k) {
 
 #define R16_STEP(a, t) a += (uint64_t)R16_BC(g, t) * __umul24(R16_ROR(f, t), k.m[t]);
 
-/* f*g, limbs < 2^19 in, tight out; two accumulators (even / odd t) so that
-   two multiply-add chains are in flight */
+/* f*g, limbs < 2^19 in, tight out.  Two accumulators in the source; LLVM
+   merges them into one dependent chain of multiply-adds, and keeping them
+   apart (use-only asm barriers) or four chains measured no faster
+   (profiles/r5_ab_r16_routing.txt): the chain is issue-bound. */
 FD_DEV uint32_t r16_mul(uint32_t f, uint32_t g, const r16ctx& k) {
   uint64_t acc = (uint64_t)R16_BC(g, 0) * f, acc2 = (uint64_t)R16_BC(g, 1) * __umul24(R16_ROR(f, 1), k.m[1]);
   R16_STEP(acc, 2) R16_STEP(acc2, 3) R16_STEP(acc, 4) R16_STEP(acc2, 5) R16_STEP(acc, 6) R16_STEP(acc2, 7)
@@ -167,6 +170,65 @@ FD_DEV bool r16_iszero(uint32_t x) {
 #pragma unroll
   for (int c = 1; c < 15; c++) q |= l[c] ^ 0xffffu;
   return z == 0u || q == 0u;
+}
+
+/* ---- group operations with broadcast routing (round 5) -----------------
+
+   Each group operation ends in the four products that finish it (a p1p1 to
+   a p3, one product per row).  Their operands are linear combinations of
+   the previous four products (the squarings of a doubling, the products
+   of an addition): instead of moving rows pairwise into place (a swap, a
+   select and a register copy per move, ~30 operations per doubling),
+   r16_bcast4 spreads the four products over every row with three swaps,
+   every lane forms the few combinations it needs, and two selects per
+   operand pick its row's. */
+
+/* rows (x0, x1, x2, x3) of x, each broadcast over the wave */
+struct r16_b4 { uint32_t v0, v1, v2, v3; };
+FD_DEV r16_b4 r16_bcast4(uint32_t x) {
+  const r16_eo e = r16_swap16(x);                        /* (x0, x0, x2, x2), (x1, x1, x3, x3) */
+  const r16_lh a = r16_swap32(e.e), b = r16_swap32(e.o);
+  return {a.l, b.l, a.h, b.h};
+}
+
+/* 2P (dbl-2008-hwcd, a = -1).  P is a p3 (X, Y, Z, T) or, LX, (X, Y, Z, X);
+   tight in, tight out.  The squarings f g = (X^2, Y^2, Z^2, XY) with
+   f = (X, Y, Z, X), g = (X, Y, Z, Y); then, every square in every row,
+     E = 2XY,  G = Y^2 - X^2,  -H = X^2 + Y^2,  -F = 2Z^2 - G
+   (< 2^17.1, 2^17.6, 2^17.1, 2^18.6: G < 2^18 - 152), and the products
+   (E -F, G -H, -F G, E -H) = -(X3, Y3, Z3, T3): the same point; or, not
+   WANT_T, (X3, Y3, Z3, X3) negated, for the next doubling. */
+template <bool LX, bool WANT_T>
+FD_DEV uint32_t ge16_dbl2(uint32_t p, const r16ctx& k) {
+  const uint32_t f = LX ? p : r16_bsel(k.r3, r16_swap32(r16_swap16(p).e).l, p);   /* row 3 <- X */
+  const uint32_t g = r16_bsel(k.r3, r16_swap32(p).l, p);                          /* row 3 <- Y */
+  const r16_b4 q = r16_bcast4(r16_mul(f, g, k));
+  const uint32_t nh = q.v0 + q.v1;
+  const uint32_t gg = q.v1 + k.p4 - q.v0;
+  const uint32_t e = q.v3 + q.v3;
+  const uint32_t nf = q.v2 + q.v2 + k.p8 - gg;
+  const uint32_t a = r16_bsel(k.r1, gg, r16_bsel(k.r2, nf, e));                   /* (E, G, -F, E)        */
+  const uint32_t b = r16_bsel(k.r1, nh, r16_bsel(k.r2, gg, WANT_T ? r16_bsel(k.r3, nh, nf) : nf));
+  return r16_mul(a, b, k);                                                         /* b: (-F, -H, G, -H|-F) */
+}
+
+/* P + Q, P a p3 with limbs < 2^17 (tight, or 4p - tight where ge16_cneg4
+   negated it), Q in qc form (Y2 - X2, Y2 + X2, 2dT2, 2Z2), < 2^19: the
+   products (Y-X)(Y2-X2), (Y+X)(Y2+X2), T 2dT2, Z 2Z2 = (b, a, c, t), then
+   R = (a - b, a + b, t + c, t - c) (< 2^17.6; NEG: b - a in the first,
+   which with X and T of P negated adds -Q) and the products
+   (R0 R3, R1 R2, R2 R3, R0 R1) = (X3, Y3, Z3, T3) -- ge16_add then
+   ge16_to_p3 -- or (X3, Y3, Z3, X3) without WANT_T */
+template <bool WANT_T>
+FD_DEV uint32_t ge16_add2(uint32_t p, uint32_t qc, bool neg, const r16ctx& k) {
+  const uint32_t v = r16_xor1(p, k);                                              /* Y, X, T, Z */
+  const uint32_t o = v + (((k.p4 - p) & k.r0) | (p & k.r1));                      /* < 2^18     */
+  const r16_b4 q = r16_bcast4(r16_mul(o, qc, k));
+  const uint32_t r0 = neg ? q.v0 + k.p4 - q.v1 : q.v1 + k.p4 - q.v0;
+  const uint32_t r1 = q.v1 + q.v0, r2 = q.v3 + q.v2, r3 = q.v3 + k.p4 - q.v2;
+  const uint32_t a = r16_bsel(k.r1, r1, r16_bsel(k.r2, r2, r0));                  /* (R0, R1, R2, R0)    */
+  const uint32_t b = r16_bsel(k.r1, r2, WANT_T ? r16_bsel(k.r3, r1, r3) : r3);    /* (R3, R2, R3, R1|R3) */
+  return r16_mul(a, b, k);
 }
 
 /* limb c of the constant 1 / 2 (row-independent) */
@@ -304,66 +366,12 @@ FD_DEV void decode16(r16_dec& o, uint32_t y, uint32_t sign, bool avx_rule, uint3
   o.small = x0 || zy == 0u || e0 == 0u || e1 == 0u;
 }
 
-/* ---- group operations (fd25519_ge4.h's, a row per coordinate) ---------- */
-
-/* p1p1 -> p3 (or p2): (X T, Y Z, Z T, X Y); r < 2^19 in, tight out */
-FD_DEV uint32_t ge16_to_p3(uint32_t r, const r16ctx& k) {
-  /* a = (r0, r1, r2, r0): row 3 takes the broadcast of r0 (swap32 of swap16's e) */
-  const uint32_t b0 = r16_swap32(r16_swap16(r).e).l;
-  const uint32_t a = r16_bsel(k.r3, b0, r);
-  /* b = (r3, r2, r3, r1): the broadcasts of r2, r3 (swap16 of swap32's h), r1 from swap32's l */
-  const r16_lh s = r16_swap32(r);
-  const r16_eo t = r16_swap16(s.h);
-  const uint32_t b = r16_bsel(k.r3, s.l, r16_bsel(k.r1, t.e, t.o));
-  return r16_mul(a, b, k);
-}
-
-/* r = 2p (p2 or p3 in, tight; p1p1 out): squares X^2, Y^2, (X+Y)^2, 2Z^2 in
-   rows 0..3, then (X+Y)^2 - (X^2+Y^2), X^2+Y^2, Y^2-X^2, 2Z^2-(Y^2-X^2)
-   (ge4_dbl, ge_p2_dbl) */
-FD_DEV uint32_t ge16_dbl(uint32_t p, const r16ctx& k) {
-  /* u = (X, Y, X+Y, Z): swap32's l is (X, Y, X, Y), the broadcast of Y
-     (swap32 of swap16's o) is added in row 2, row 3 takes swap16's e (Z) */
-  const r16_eo pe = r16_swap16(p);
-  const uint32_t by = r16_swap32(pe.o).l;
-  const uint32_t u = r16_bsel(k.r3, pe.e, r16_swap32(p).l + (by & k.r2));   /* < 2^17.1 */
-  uint32_t s = r16_sq(u, k);                                    /* tight             */
-  s += s & k.r3;                                                /* 2Z^2              < 2^17.1 */
-  const uint32_t w = r16_xor1(s, k);                            /* s1, s0, s3, s2    */
-  /* row 0: s0 + s1 (< 2^17.1), row 1: s1 - s0 (s1 + 4p - s0 < 2^17.6), rows 2, 3: s2, s3 */
-  const uint32_t t = s + ((w & k.r0) | ((k.p4 - w) & k.r1));
-  /* x = (t2, t0, t1, t3): swap32's h, swap16's e, the broadcast of t1, t;
-     y = (t0, -, -, t1) = swap32's l */
-  const r16_lh tl = r16_swap32(t);
-  const r16_eo te = r16_swap16(t);
-  const uint32_t b1 = r16_swap32(te.o).l;
-  const uint32_t x = r16_bsel(k.r0, tl.h, r16_bsel(k.r1, te.e, r16_bsel(k.r2, b1, t)));
-  const uint32_t y = tl.l;
-  /* row 0: s2 + 8p - t0, row 3: s3 + 8p - t1 (t0, t1 < 2^17.6 < 2^18 - 152): < 2^18.6 */
-  return x + ((k.p8 - y) & k.r03);
-}
-
-/* r = p + q (p3 in, limbs < 2^17 -- tight, or 4p - tight where negated;
-   q in qc form (Y-X, Y+X, 2dT, 2Z), < 2^19; p1p1 out): b = (Y-X)(Y2-X2),
-   a = (Y+X)(Y2+X2), c = T 2dT2, t = Z 2Z2 in rows 0..3, then
-   (a - b, a + b, t + c, t - c) (ge4_add) */
-FD_DEV uint32_t ge16_add(uint32_t p, uint32_t qc, const r16ctx& k) {
-  const uint32_t v = r16_xor1(p, k);                            /* Y, X, T, Z        */
-  /* row 0: Y + 4p - X (< 2^18), row 1: X + Y (< 2^18), rows 2, 3: T, Z */
-  const uint32_t o = v + (((k.p4 - p) & k.r0) | (p & k.r1));
-  const uint32_t pr = r16_mul(o, qc, k);                        /* b, a, c, t: tight */
-  const uint32_t w = r16_xor1(pr, k);                           /* a, b, t, c        */
-  /* row 0: a + 4p - b, row 1: a + b, row 2: c + t, row 3: t + 4p - c: < 2^17.6 */
-  return ((w + pr) & k.r12) | ((w + k.p4 - pr) & k.r0) | ((pr + k.p4 - w) & k.r3);
-}
+/* ---- negation, cached form, tables ------------------------------------ */
 
 /* -x in the rows of the mask `rows` when neg (wave-uniform): 4p - x for
-   tight x (p3), 8p - x for x < 2^18 - 152 (a p1p1's row 0) */
+   tight x (a p3's X and T: -P before ge16_add2 with neg) */
 FD_DEV uint32_t ge16_cneg4(uint32_t x, uint32_t rows, bool neg, const r16ctx& k) {
   return neg ? (x ^ ((x ^ (k.p4 - x)) & rows)) : x;
-}
-FD_DEV uint32_t ge16_cneg8(uint32_t x, uint32_t rows, bool neg, const r16ctx& k) {
-  return neg ? (x ^ ((x ^ (k.p8 - x)) & rows)) : x;
 }
 
 /* qc of a p3 (limbs < 2^17): (Y-X, Y+X, 2dT, 2Z), < 2^18 */
@@ -388,7 +396,7 @@ FD_DEV void table16_build(uint32_t (&tab)[9], uint32_t x, uint32_t y, bool negat
   uint32_t cur = p0;
 #pragma unroll
   for (int e = 2; e <= 8; e++) {
-    cur = ge16_to_p3(ge16_add(cur, c1, k), k);
+    cur = ge16_add2<true>(cur, c1, false, k);
     tab[e] = ge16_to_qc(cur, d2, k);
   }
 }

@@ -1222,23 +1222,23 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
     const uint32_t bdig = (uint32_t)__builtin_amdgcn_readfirstlane((int)(badd ? pop160u<BW>(bd) : 0u));
     const uint32_t ce = table16_at(tab, e < 0 ? -e : e);
     if (it != W - 1) {
-#pragma clang loop unroll(disable)
-      for (int dbl = 0; dbl < 4; dbl++) P = ge16_to_p3(ge16_dbl(P, k), k);
+      P = ge16_dbl2<false, false>(P, k);   /* (X, Y, Z, X) between doublings: T only before an addition */
+      P = ge16_dbl2<true, false>(P, k);
+      P = ge16_dbl2<true, false>(P, k);
+      P = ge16_dbl2<true, true>(P, k);
     }
     uint32_t b = 0u;
     if (badd) b = btab16_r16(btab, (int)bdig, k);
     P = ge16_cneg4(P, k.r03, e < 0, k);
-    uint32_t Rt = ge16_add(P, ce, k);
-    Rt = ge16_cneg8(Rt, k.r0, e < 0, k);
-    P = ge16_to_p3(Rt, k);
-    if (badd) P = ge16_to_p3(ge16_add(P, b, k), k);
+    P = ge16_add2<true>(P, ce, e < 0, k);
+    if (badd) P = ge16_add2<true>(P, b, false, k);
   }
   /* wave 1's point as an addend of wave 0's */
   __shared__ uint32_t hand[64];
   if (half) hand[threadIdx.x & 63u] = ge16_to_qc(P, d2, k);
   __syncthreads();
   if (half) return;
-  P = ge16_to_p3(ge16_add(P, hand[threadIdx.x], k), k);
+  P = ge16_add2<true>(P, hand[threadIdx.x], false, k);
   /* identity: X == 0 (row 0) and Y == Z (row 1: Y + 4p - Z) */
   const uint32_t z = r16_rp<2, 2, 2, 2>(P, k);
   const bool zero = r16_iszero(P + ((k.p4 - z) & k.r1));

@@ -91,30 +91,6 @@ def rp(pt, src):
     return [pt[s] for s in src]
 
 
-def to_p3(r):
-    a, b = rp(r, (0, 1, 2, 0)), rp(r, (3, 2, 3, 1))
-    return [r16_mul(a[q], b[q]) for q in range(4)]
-
-
-def dbl(p):
-    a, b = rp(p, (0, 1, 0, 2)), rp(p, (0, 0, 1, 0))
-    u = [a[0], a[1], add(a[2], b[2]), a[3]]
-    s = [r16_mul(x, x) for x in u]
-    s[3] = add(s[3], s[3])
-    w = rp(s, (1, 0, 3, 2))
-    t = [add(s[0], w[0]), sub(s[1], w[1], P4), s[2], s[3]]
-    x, y = rp(t, (2, 0, 1, 3)), rp(t, (0, 0, 0, 1))
-    return [sub(x[0], y[0], P8), x[1], x[2], sub(x[3], y[3], P8)]
-
-
-def padd(p, qc):
-    v = rp(p, (1, 0, 3, 2))
-    o = [sub(v[0], p[0], P4), add(v[1], p[1]), v[2], v[3]]
-    pr = [r16_mul(o[q], qc[q]) for q in range(4)]
-    w = rp(pr, (1, 0, 3, 2))
-    return [sub(w[0], pr[0], P4), add(w[1], pr[1]), add(w[2], pr[2]), sub(pr[3], w[3], P4)]
-
-
 def to_qc(p, d2):
     v = rp(p, (1, 0, 3, 2))
     t = r16_mul(v[2], d2)
@@ -173,7 +149,7 @@ def table(x, y, negate, d2):
     tab.append(c1)
     cur = p0
     for _ in range(2, 9):
-        cur = to_p3(padd(cur, c1))
+        cur = add2(cur, c1, False, True)
         tab.append(to_qc(cur, d2))
     return tab
 
@@ -184,71 +160,6 @@ def test_mul_exact_and_bounded():
     for f, g in [(worst, worst), ([TIGHT - 1] * 16, worst)] + \
                 [([rng.randrange(B_IN) for _ in range(16)], [rng.randrange(B_IN) for _ in range(16)]) for _ in range(300)]:
         assert val(r16_mul(f, g)) == val(f) * val(g) % P
-
-
-def test_group_ops_on_worst_and_random_inputs():
-    """dbl / add / to_p3 / to_qc / cneg: exact group law, bounds held, from
-    a point whose limbs are pushed to the top of their range (4p added
-    limb-wise to a tight point keeps its value and maximises every sum)"""
-    rng = random.Random(6)
-    d2 = limbs(D2)
-    for _ in range(6):
-        k = rng.randrange(1, 2**64)
-        x, y = edwards_mul(k, BASE)
-        p3 = [limbs(x), limbs(y), limbs(1), limbs(x * y)]
-        q = edwards_mul(rng.randrange(1, 2**64), BASE)
-        qc = to_qc([limbs(q[0]), limbs(q[1]), limbs(1), limbs(q[0] * q[1])], d2)
-        assert ext(to_p3(dbl(p3))) == edwards_add((x, y), (x, y))
-        assert ext(to_p3(padd(p3, qc))) == edwards_add((x, y), q)
-        # negated P (rows 0, 3: 4p - x), then the p1p1's row 0 negated (8p - x), as the dsm loop does
-        pn = cneg(p3, (0, 3), True, P4)
-        r = cneg(padd(pn, qc), (0,), True, P8)
-        assert ext(to_p3(r)) == edwards_add((x, y), ((P - q[0]) % P, q[1]))
-        # tight limbs at their top: the value + 0 with every limb ~2^16 + 63
-        hi = [[min(TIGHT - 1, l + 0) for l in c] for c in p3]
-        assert all(v < TIGHT for c in hi for v in c)
-        dbl(hi), padd(hi, qc)
-
-
-@pytest.mark.parametrize("seed", [1, 2])
-def test_window_loop_matches_scalar_multiplication(seed):
-    """One half of dsm16: the [0..8](-A) table, W = 33 signed 4-bit windows
-    of c (4 doublings each), a table addition per window and an unsigned
-    radix-2^24 base addition every 6th window, exactly as the kernel
-    orders them -- against [c](-A) + [s]B."""
-    rng = random.Random(seed)
-    d2 = limbs(D2)
-    A = edwards_mul(rng.randrange(1, 2**250), BASE)
-    c = rng.randrange(2**130)
-    s = rng.randrange(2**144)
-    ax, ay = limbs(A[0]), limbs(A[1])
-    tab = table(ax, ay, True, d2)
-    # c in 33 signed radix-16 digits, most significant first (the top one in [0, 8])
-    digs, carry = [], 0
-    for i in range(33):
-        e = ((c >> (4 * i)) & 15) + carry
-        carry = (e + 8) >> 4
-        digs.append(e - 16 * carry)
-    assert carry == 0 and digs[-1] >= 0
-    sdigs = [(s >> (24 * i)) & (2**24 - 1) for i in range(6)]
-    pt = [limbs(0), limbs(1), limbs(1), limbs(0)]
-    for it in range(32, -1, -1):
-        e = digs[it]
-        if it != 32:
-            for _ in range(4):
-                pt = to_p3(dbl(pt))
-        ce = tab[abs(e)]
-        pt = cneg(pt, (0, 3), e < 0, P4)
-        rt = padd(pt, ce)
-        rt = cneg(rt, (0,), e < 0, P8)
-        pt = to_p3(rt)
-        if it % 6 == 0:
-            b = edwards_mul(sdigs[it // 6], BASE)
-            ypx, ymx, xy2d = (b[1] + b[0]) % P, (b[1] - b[0]) % P, 2 * D * b[0] * b[1] % P
-            pt = to_p3(padd(pt, [limbs(ymx), limbs(ypx), limbs(xy2d), limbs(2)]))
-    negA = ((P - A[0]) % P, A[1])
-    want = edwards_add(edwards_mul(c, negA), edwards_mul(s, BASE))
-    assert ext(pt) == want
 
 
 # ---- the device's row moves (fd25519_r16.h): gfx950's permlane swaps as
@@ -273,24 +184,9 @@ def test_row_moves_compose_the_quad_permutations():
     # r16_xor1
     e, o = swap16(x)
     assert bsel((1, 3), e, o) == rp(x, (1, 0, 3, 2))
-    # ge16_to_p3's a = (x0, x1, x2, x0) and b = (x3, x2, x3, x1)
-    b0 = swap32(swap16(x)[0])[0]
-    assert bsel((3,), b0, x) == rp(x, (0, 1, 2, 0))
-    l, h = swap32(x)
-    te, to = swap16(h)
-    assert bsel((3,), l, bsel((1,), te, to)) == rp(x, (3, 2, 3, 1))
-    # ge16_dbl's u = (x0, x1, x0 + x1, x2)
-    pe, po = swap16(x)
-    by = swap32(po)[0]
-    u = bsel((3,), pe, [a + ("+" + b if q == 2 else "") for q, (a, b) in enumerate(zip(swap32(x)[0], by))])
-    assert u == ["x0", "x1", "x0+x1", "x2"]
-    # ... its x = (t2, t0, t1, t3) and y = (t0, -, -, t1)
-    tl, th = swap32(x)
-    te, to = swap16(x)
-    b1 = swap32(to)[0]
-    assert bsel((0,), th, bsel((1,), te, bsel((2,), b1, x))) == rp(x, (2, 0, 1, 3))
-    y = tl
-    assert (y[0], y[3]) == ("x0", "x1")
+    # ge16_dbl2's operands from a p3: f row 3 <- X, g row 3 <- Y
+    assert bsel((3,), swap32(swap16(x)[0])[0], x) == ["x0", "x1", "x2", "x0"]
+    assert bsel((3,), swap32(x)[0], x) == ["x0", "x1", "x2", "x1"]
 
 
 # ---- prep16's decompression (fd25519_r16.h decode16, a row per point)
@@ -392,3 +288,116 @@ def test_decode16_matches_ge_decode():
                 assert small == want[2], hex(enc)
             else:
                 assert (xv, fail, small) == want, hex(enc)
+
+
+# ---- the broadcast-routed group operations (ge16_dbl2 / ge16_add2), with
+# the permlane swaps modelled as the probe measured them
+
+def bcast4(x):
+    """r16_bcast4: swap16, then swap32 of both halves -> every row of x in every row"""
+    e, o = swap16(x)
+    (al, ah), (bl, bh) = swap32(e), swap32(o)
+    return al, bl, ah, bh
+
+
+def bsel_rows(rows, a, b):
+    return [a[q] if q in rows else b[q] for q in range(4)]
+
+
+def dbl2(p, lx, want_t):
+    f = p if lx else bsel_rows((3,), swap32(swap16(p)[0])[0], p)
+    g = bsel_rows((3,), swap32(p)[0], p)
+    s = [r16_mul(f[q], g[q]) for q in range(4)]
+    assert [b[0] for b in bcast4([0, 1, 2, 3])] == [0, 1, 2, 3]   # which row each broadcast holds
+    nh = add(s[0], s[1])
+    gg = sub(s[1], s[0], P4)
+    e = add(s[3], s[3])
+    nf = sub(add(s[2], s[2]), gg, P8)
+    a = [e, gg, nf, e]
+    b = [nf, nh, gg, nh if want_t else nf]
+    assert all(v < B_IN for x in a + b for v in x)
+    return [r16_mul(a[q], b[q]) for q in range(4)]
+
+
+def add2(p, qc, neg, want_t):
+    v = rp(p, (1, 0, 3, 2))
+    o = [sub(v[0], p[0], P4), add(v[1], p[1]), v[2], v[3]]
+    q = [r16_mul(o[i], qc[i]) for i in range(4)]
+    r0 = sub(q[0], q[1], P4) if neg else sub(q[1], q[0], P4)
+    r1, r2, r3 = add(q[1], q[0]), add(q[3], q[2]), sub(q[3], q[2], P4)
+    a = [r0, r1, r2, r0]
+    b = [r3, r2, r3, r1 if want_t else r3]
+    assert all(x < B_IN for y in a + b for x in y)
+    return [r16_mul(a[i], b[i]) for i in range(4)]
+
+
+def proj(pt):
+    """(X, Y, Z, .) -> affine (x, y)"""
+    X, Y, Z = (val(c) for c in pt[:3])
+    zi = pow(Z, P - 2, P)
+    return X * zi % P, Y * zi % P
+
+
+def test_broadcast_rows():
+    x = [["x0"], ["x1"], ["x2"], ["x3"]]
+    b = bcast4(x)
+    assert [list(r) for r in b] == [[["x0"]] * 4, [["x1"]] * 4, [["x2"]] * 4, [["x3"]] * 4]
+
+
+def test_dbl2_add2_group_law_and_bounds():
+    rng = random.Random(21)
+    d2 = limbs(D2)
+    for _ in range(6):
+        x, y = edwards_mul(rng.randrange(1, 2**64), BASE)
+        p3 = [limbs(x), limbs(y), limbs(1), limbs(x * y)]
+        q = edwards_mul(rng.randrange(1, 2**64), BASE)
+        qc = to_qc([limbs(q[0]), limbs(q[1]), limbs(1), limbs(q[0] * q[1])], d2)
+        two = edwards_add((x, y), (x, y))
+        r = dbl2(p3, False, True)
+        assert ext(r) == two                                     # T consistent: a p3
+        l = dbl2(p3, False, False)
+        assert proj(l) == two and val(l[3]) == val(l[0])         # (X, Y, Z, X)
+        assert ext(dbl2(l, True, True)) == edwards_add(two, two)
+        assert ext(add2(p3, qc, False, True)) == edwards_add((x, y), q)
+        pn = cneg(p3, (0, 3), True, P4)
+        assert ext(add2(pn, qc, True, True)) == edwards_add((x, y), ((P - q[0]) % P, q[1]))
+        # limbs at the top of their ranges
+        hi = [[TIGHT - 1] * 16 for _ in range(4)]
+        dbl2(hi, False, True), dbl2(hi, True, False), add2(hi, qc, False, True)
+        add2(cneg(hi, (0, 3), True, P4), qc, True, True)
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_window_loop2_matches_scalar_multiplication(seed):
+    """dsm16's loop as the kernel now runs it: per window four doublings
+    (p3 in, (X, Y, Z, X) between them, T again before the addition), the
+    digit's table addition with the negation folded into it, the base
+    addition every 6th window -- against [c](-A) + [s]B"""
+    rng = random.Random(seed)
+    d2 = limbs(D2)
+    A = edwards_mul(rng.randrange(1, 2**250), BASE)
+    c = rng.randrange(2**130)
+    s = rng.randrange(2**144)
+    tab = table(limbs(A[0]), limbs(A[1]), True, d2)
+    digs, carry = [], 0
+    for i in range(33):
+        e = ((c >> (4 * i)) & 15) + carry
+        carry = (e + 8) >> 4
+        digs.append(e - 16 * carry)
+    sdigs = [(s >> (24 * i)) & (2**24 - 1) for i in range(6)]
+    pt = [limbs(0), limbs(1), limbs(1), limbs(0)]
+    for it in range(32, -1, -1):
+        e = digs[it]
+        if it != 32:
+            pt = dbl2(pt, False, False)
+            pt = dbl2(pt, True, False)
+            pt = dbl2(pt, True, False)
+            pt = dbl2(pt, True, True)
+        pt = cneg(pt, (0, 3), e < 0, P4)
+        pt = add2(pt, tab[abs(e)], e < 0, True)
+        if it % 6 == 0:
+            b = edwards_mul(sdigs[it // 6], BASE)
+            ypx, ymx, xy2d = (b[1] + b[0]) % P, (b[1] - b[0]) % P, 2 * D * b[0] * b[1] % P
+            pt = add2(pt, [limbs(ymx), limbs(ypx), limbs(xy2d), limbs(2)], False, True)
+    negA = ((P - A[0]) % P, A[1])
+    assert ext(pt) == edwards_add(edwards_mul(c, negA), edwards_mul(s, BASE))
