@@ -8,6 +8,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I firedancer_amd/csrc -o tools/ubench/prep_parts_ubench tools/ubench/prep_parts_ubench.hip
 #include "../../firedancer_amd/csrc/fd_ed25519_kernels.hip"
+#include "half_timed.inc"
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -16,7 +17,7 @@
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
 
 __global__ void __launch_bounds__(64) k_parts(const uint8_t* sigs, const uint8_t* pubs, const uint8_t* msgs, int msz,
-                                              int lanes, uint64_t* stamps, uint32_t* sink) {
+                                              int lanes, uint64_t* stamps, uint32_t* sink, uint64_t* htm) {
   const int j = threadIdx.x;
   if (j >= lanes) return;
   uint64_t t[6];
@@ -43,7 +44,8 @@ __global__ void __launch_bounds__(64) k_parts(const uint8_t* sigs, const uint8_t
   t[2] = __builtin_amdgcn_s_memtime();
   uint32_t cw[FD_HALF_TW], dm[FD_HALF_TW];
   int dneg = 0;
-  const int found = fd_half_scalars(k, cw, dm, &dneg, FD_HALF_DBITS_MAX);
+  uint64_t hq[6];
+  const int found = half_scalars_timed(hq, k, cw, dm, &dneg, FD_HALF_DBITS_MAX);
   asm volatile("" :: "v"(cw[0]), "v"(dm[0]));
   t[3] = __builtin_amdgcn_s_memtime();
   const bool ok = found && half_pair_ok(k, cw, dm, dneg, FD_HALF_DBITS_MAX);
@@ -71,6 +73,7 @@ __global__ void __launch_bounds__(64) k_parts(const uint8_t* sigs, const uint8_t
   sink[j] = acc;
   if (j == 0)
     for (int q = 0; q < 6; q++) stamps[q] = t[q];
+  for (int q = 0; q < 6; q++) htm[6 * j + q] = hq[q];
 }
 
 int main(int argc, char** argv) {
@@ -86,6 +89,8 @@ int main(int argc, char** argv) {
   uint8_t *d_sig, *d_pub, *d_msg;
   uint64_t* d_st;
   uint32_t* d_sink;
+  uint64_t* d_htm;
+  CHECK(hipMalloc(&d_htm, 64 * 6 * sizeof(uint64_t)));
   CHECK(hipMalloc(&d_sig, h_sig.size()));
   CHECK(hipMalloc(&d_pub, h_pub.size()));
   CHECK(hipMalloc(&d_msg, h_msg.size() + 64));
@@ -102,7 +107,7 @@ int main(int argc, char** argv) {
       CHECK(hipEventCreate(&a));
       CHECK(hipEventCreate(&b));
       CHECK(hipEventRecord(a));
-      hipLaunchKernelGGL(k_parts, dim3(1), dim3(64), 0, 0, d_sig, d_pub, d_msg, msz, lanes, d_st, d_sink);
+      hipLaunchKernelGGL(k_parts, dim3(1), dim3(64), 0, 0, d_sig, d_pub, d_msg, msz, lanes, d_st, d_sink, d_htm);
       CHECK(hipEventRecord(b));
       CHECK(hipEventSynchronize(b));
       float ms = 0;
@@ -112,6 +117,17 @@ int main(int argc, char** argv) {
       if (rep < 2) continue;   /* warm-up: code fetch, clocks */
       printf("{\"lanes\": %d, \"kernel_us\": %.2f", lanes, ms * 1e3);
       for (int q = 0; q < 5; q++) printf(", \"%s_clk\": %llu", nm[q], (unsigned long long)(st[q + 1] - st[q]));
+      uint64_t hq[64 * 6];
+      CHECK(hipMemcpy(hq, d_htm, sizeof(hq), hipMemcpyDeviceToHost));
+      printf(", \"lehmer_clk\": %llu, \"single_clk\": %llu, \"final_clk\": %llu, \"rounds\": %llu, \"inner\": %llu, \"singles\": %llu",
+             (unsigned long long)hq[0], (unsigned long long)hq[1], (unsigned long long)hq[2], (unsigned long long)hq[3],
+             (unsigned long long)hq[4], (unsigned long long)hq[5]);
+      if (lanes == 64) {
+        uint64_t mx[6] = {0, 0, 0, 0, 0, 0};
+        for (int j = 0; j < 64; j++) for (int q = 3; q < 6; q++) mx[q] = hq[6 * j + q] > mx[q] ? hq[6 * j + q] : mx[q];
+        printf(", \"max_rounds\": %llu, \"max_inner\": %llu, \"max_singles\": %llu", (unsigned long long)mx[3],
+               (unsigned long long)mx[4], (unsigned long long)mx[5]);
+      }
       printf("}\n");
       CHECK(hipEventDestroy(a));
       CHECK(hipEventDestroy(b));
