@@ -1046,6 +1046,9 @@ fd_ed25519_hip_verify_txns_host( fd_ed25519_hip_engine_t * e, unsigned long ntxn
 #define DROPIN_ENGINES   4
 #define DROPIN_BATCH_MAX 4096UL
 #define DROPIN_CHUNK     16384UL
+#ifndef DROPIN_DIRECT_MAX
+#define DROPIN_DIRECT_MAX 64UL   /* launches of at most this many signatures read the pinned block in place */
+#endif
 
 typedef struct dropin_req {
   unsigned char const * msg;
@@ -1267,27 +1270,39 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     return FD_ED25519_HIP_ERR_HIP - (int)hipErrorLaunchFailure;
   }
 #endif
-  /* the block crosses by device launches (fd_ed25519_hip_launch_pull), not
-     copy-engine calls: several drop-in engines submit from their callers'
-     threads at once */
+  /* A launch of a few signatures (one caller alone, the latency case) has
+     the kernels read its inputs and write its codes through the pinned
+     block's device-visible address: no copy launches, two kernels fewer on
+     the call's path (the hash's first loads wait on the link instead, a
+     few hundred bytes).  A larger combined launch moves the block by
+     device launches (fd_ed25519_hip_launch_pull), not copy-engine calls:
+     several drop-in engines submit from their callers' threads at once
+     (DESIGN.md 3c), and one bulk read beats every lane reading over the
+     link. */
+  int direct = nsig<=DROPIN_DIRECT_MAX && !multi;
+  unsigned char * src = direct ? dq.h_dev[k] : d;
   fd_ed25519_pull_params_t pp;
   memset( &pp, 0, sizeof(pp) );
-  pp.src[0] = dq.h_dev[k]; pp.dst[0] = d; pp.n[0] = in_sz ? in_sz : 1UL; pp.cnt = 1U;
-  HIPCHK( (hipError_t)fd_ed25519_hip_launch_pull( &pp, st ), "H2D drop-in" );
-  int err = fd_ed25519_hip_verify_dev( e, nsig_m, d + o_msg, (unsigned long const *)(d + o_off),
-                                       (unsigned int const *)(d + o_sz), d + o_sig, d + o_pub,
-                                       (signed char *)(d + o_out), st );
+  if( !direct ) {
+    pp.src[0] = dq.h_dev[k]; pp.dst[0] = d; pp.n[0] = in_sz ? in_sz : 1UL; pp.cnt = 1U;
+    HIPCHK( (hipError_t)fd_ed25519_hip_launch_pull( &pp, st ), "H2D drop-in" );
+  }
+  int err = fd_ed25519_hip_verify_dev( e, nsig_m, src + o_msg, (unsigned long const *)(src + o_off),
+                                       (unsigned int const *)(src + o_sz), src + o_sig, src + o_pub,
+                                       (signed char *)(src + o_out), st );
   if( !err && nsig_h )
-    err = fd_ed25519_hip_verify_digests_dev( e, nsig_h, d + o_dig, d + o_sig + 64UL*nsig_m, d + o_pub + 32UL*nsig_m,
-                                             (signed char *)(d + o_out + nsig_m), st );
+    err = fd_ed25519_hip_verify_digests_dev( e, nsig_h, src + o_dig, src + o_sig + 64UL*nsig_m,
+                                             src + o_pub + 32UL*nsig_m, (signed char *)(src + o_out + nsig_m), st );
   if( err ) { hipStreamSynchronize( st ); return err; }
   if( multi ) {
     err = fd_ed25519_hip_txn_combine_dev( e, n, (signed char const *)(d + o_out), (uint32_t const *)(d + o_tf),
                                           (uint32_t const *)(d + o_tc), (signed char *)(d + o_tout), st );
     if( err ) { hipStreamSynchronize( st ); return err; }
   }
-  pp.src[0] = d + o_out; pp.dst[0] = dq.h_dev[k] + o_out; pp.n[0] = multi ? nsig + n : nsig;
-  HIPCHK( (hipError_t)fd_ed25519_hip_launch_pull( &pp, st ), "D2H drop-in" );
+  if( !direct ) {
+    pp.src[0] = d + o_out; pp.dst[0] = dq.h_dev[k] + o_out; pp.n[0] = multi ? nsig + n : nsig;
+    HIPCHK( (hipError_t)fd_ed25519_hip_launch_pull( &pp, st ), "D2H drop-in" );
+  }
   HIPCHK( hipStreamSynchronize( st ), "drop-in verify" );
   signed char const * codes = (signed char const *)(h + o_out);
   signed char const * tcode = (signed char const *)(h + o_tout);
