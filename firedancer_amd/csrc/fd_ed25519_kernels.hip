@@ -156,6 +156,16 @@ __global__ void __launch_bounds__(256) fd_ed25519_sort_scatter_kernel(fd_ed25519
   }
 }
 
+/* k = digest mod L and the S < L flag, into the work arrays */
+FD_DEV void hash_finish(const fd_ed25519_verify_params_t& p, uint64_t j, const uint32_t (&dig)[16],
+                        const uint32_t (&S)[8]) {
+  uint32_t k[8];
+  sc_reduce512(k, dig);
+#pragma unroll
+  for (int w = 0; w < 8; w++) p.k[(uint64_t)w * p.cap + j] = k[w];
+  p.sflag[j] = sc_is_canonical(S) ? 1 : 0;
+}
+
 FD_DEV void hash_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
   const uint64_t i = p.base + j;
   uint32_t r[8], S[8], a[8];
@@ -167,7 +177,7 @@ FD_DEV void hash_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
     S[0] = q2.x; S[1] = q2.y; S[2] = q2.z; S[3] = q2.w; S[4] = q3.x; S[5] = q3.y; S[6] = q3.z; S[7] = q3.w;
     a[0] = q4.x; a[1] = q4.y; a[2] = q4.z; a[3] = q4.w; a[4] = q5.x; a[5] = q5.y; a[6] = q5.z; a[7] = q5.w;
   }
-  uint32_t dig[16], k[8];
+  uint32_t dig[16];
   if (p.digests) {
     /* the caller hashed R||A||M (a message the device path's 32-bit sizes
        cannot carry, fd_ed25519_hip_verify_digests_dev): a uniform branch,
@@ -186,10 +196,7 @@ FD_DEV void hash_one(const fd_ed25519_verify_params_t& p, uint64_t j) {
     m.sz = p.msg_sz[i];
     sha512_ram(dig, r, a, m);
   }
-  sc_reduce512(k, dig);
-#pragma unroll
-  for (int w = 0; w < 8; w++) p.k[(uint64_t)w * p.cap + j] = k[w];
-  p.sflag[j] = sc_is_canonical(S) ? 1 : 0;
+  hash_finish(p, j, dig, S);
 }
 
 __global__ void __launch_bounds__(256, FD_ED25519_HASH_WAVES_PER_SIMD)
@@ -1293,15 +1300,71 @@ FD_DEV void decode16_wave(const fd_ed25519_verify_params_t& p, uint64_t dw) {
   }
 }
 
-__global__ void __launch_bounds__(64) fd_ed25519_prep16_kernel(fd_ed25519_verify_params_t p, uint32_t hash_waves) {
-  if (blockIdx.x < hash_waves) {
-    const uint64_t t = (uint64_t)blockIdx.x * 64u + threadIdx.x;
-    if (t >= p.n) return;
-    hash_one(p, t);
-    scalar_one(p, t);
+/* The hash blocks: 128 threads for 32 signatures, wave 1 building the
+   message schedules into LDS, wave 0 running the rounds from them
+   (sha512_sched_wave / sha512_rounds_wave), then k and the half-size
+   scalars.  Every lane of both waves reaches every barrier: lanes past the
+   chunk repeat the last signature and store nothing. */
+FD_DEV void hash16_block(const fd_ed25519_verify_params_t& p, uint64_t* sched) {
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint64_t t = (uint64_t)blockIdx.x * SHA2W_LANES + (threadIdx.x & (SHA2W_LANES - 1u));
+  const bool live = t < p.n && (threadIdx.x & 63u) < SHA2W_LANES;
+  const uint64_t j = live ? t : p.n - 1u;
+  const uint64_t i = p.base + j;
+  uint32_t pre[16], S[8];
+  {
+    const uint4* sg = reinterpret_cast<const uint4*>(p.sigs + 64 * i);
+    const uint4* pk = reinterpret_cast<const uint4*>(p.pubs + 32 * i);
+    const uint4 q0 = sg[0], q1 = sg[1], q2 = sg[2], q3 = sg[3], q4 = pk[0], q5 = pk[1];
+    pre[0] = q0.x; pre[1] = q0.y; pre[2] = q0.z; pre[3] = q0.w; pre[4] = q1.x; pre[5] = q1.y; pre[6] = q1.z;
+    pre[7] = q1.w;
+    pre[8] = q4.x; pre[9] = q4.y; pre[10] = q4.z; pre[11] = q4.w; pre[12] = q5.x; pre[13] = q5.y; pre[14] = q5.z;
+    pre[15] = q5.w;
+    S[0] = q2.x; S[1] = q2.y; S[2] = q2.z; S[3] = q2.w; S[4] = q3.x; S[5] = q3.y; S[6] = q3.z; S[7] = q3.w;
+  }
+  sha_msg_src m = {nullptr, 0u, 0u};
+  uint32_t nblk = 0u;
+  if (!p.digests) {
+    const uintptr_t mp = reinterpret_cast<uintptr_t>(p.msgs + p.msg_off[i]);
+    m.base = reinterpret_cast<const uint32_t*>(mp & ~(uintptr_t)3);
+    m.shift = (uint32_t)(mp & 3);
+    m.sz = p.msg_sz[i];
+    nblk = (m.sz + 64u + 17u + 127u) >> 7;
+  }
+  /* the wave's largest block count, the same in both waves: the barrier count */
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)nblk, off);
+    nblk = o > nblk ? o : nblk;
+  }
+  const uint32_t nblk_wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)nblk);
+  if (wave == 1u) {
+    sha512_sched_wave<16>(pre, m, nblk_wave, sched);
     return;
   }
-  decode16_wave(p, blockIdx.x - hash_waves);
+  uint32_t dig[16];
+  if (p.digests) {
+    const uint4* dg = reinterpret_cast<const uint4*>(p.digests + 64 * i);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint4 v = dg[q];
+      dig[4 * q] = v.x; dig[4 * q + 1] = v.y; dig[4 * q + 2] = v.z; dig[4 * q + 3] = v.w;
+    }
+  } else {
+    sha512_rounds_wave<16>(dig, m, nblk_wave, sched);
+  }
+  if (!live) return;
+  hash_finish(p, j, dig, S);
+  scalar_one(p, j);
+}
+
+__global__ void __launch_bounds__(128) fd_ed25519_prep16_kernel(fd_ed25519_verify_params_t p, uint32_t hash_blocks) {
+  __shared__ uint64_t sched[2 * SHA2W_WORDS];
+  if (blockIdx.x < hash_blocks) {
+    hash16_block(p, sched);
+    return;
+  }
+  decode16_wave(p, 2u * (blockIdx.x - hash_blocks) + (threadIdx.x >> 6));
 }
 
 /* ------------------------------------------------------------------------
@@ -1595,9 +1658,9 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
   const uint32_t blk = 256;
   switch (phase) {
   case FD_ED25519_PHASE_HASH: {
-    if (p->small == 3) {   /* dsm16 chunks: the decompressions lane-split too */
-      const uint32_t hw = (uint32_t)((p->n + 63) / 64), dw = (uint32_t)((p->n + 1) / 2);
-      hipLaunchKernelGGL(fd_ed25519_prep16_kernel, dim3(hw + dw), dim3(64), 0, st, *p, hw);
+    if (p->small == 3) {   /* dsm16 chunks: the decompressions lane-split too, the hash over two waves */
+      const uint32_t hb = (uint32_t)((p->n + SHA2W_LANES - 1) / SHA2W_LANES), dw = (uint32_t)((p->n + 1) / 2);
+      hipLaunchKernelGGL(fd_ed25519_prep16_kernel, dim3(hb + (dw + 1) / 2), dim3(128), 0, st, *p, hb);
       break;
     }
     if (p->small) {

@@ -238,6 +238,92 @@ FD_DEV void sha512_pre(uint32_t (&out)[16], const uint32_t (&pre)[NPRE], const s
   }
 }
 
+/* ---- the hash over two waves (the latency form's prep16) ----------------
+
+   A lane's hash is a chain of 80 rounds per block, and at one wave per
+   SIMD the wave issues every instruction of it in turn: the message
+   schedule (~20 of the ~50 VALU operations of a round) sits in that
+   chain only because the same lane computes it.  Here a second wave of
+   the block builds each block's 80 schedule words into LDS (one buffer
+   per block parity) while the first runs the rounds of the block before
+   from the other buffer; one workgroup barrier per block hands a buffer
+   over.  Same digest, bit for bit (the words and rounds are the
+   one-wave form's).  32 messages per pair of waves (lanes 32..63 repeat
+   lanes 0..31), so the two buffers are 40 KiB and four blocks fit a CU. */
+#define SHA2W_LANES 32
+#define SHA2W_WORDS (80 * SHA2W_LANES)   /* one buffer: [word][lane], 64-bit */
+
+/* wave 1: the schedules of blocks 0 .. nblk_wave - 1 of this lane's
+   PRE || M, block b into buf[b & 1], a barrier after each */
+template <int NPRE>
+FD_DEV void sha512_sched_wave(const uint32_t (&pre)[NPRE], const sha_msg_src& m, uint32_t nblk_wave, uint64_t* lds) {
+  constexpr int PB = 4 * NPRE;
+  const uint32_t lane = threadIdx.x & (SHA2W_LANES - 1u);
+  const bool writer = (threadIdx.x & 63u) < SHA2W_LANES;
+  const uint32_t nblk = (m.sz + PB + 17u + 127u) >> 7;
+  const uint64_t bitlen = (uint64_t)(PB + m.sz) << 3;
+  if (!nblk_wave) return;
+  uint4 cur[SHA_CHUNKS];
+  uint64_t w[16];
+  sha_load_block(cur, m, -NPRE);
+#pragma clang loop unroll(disable)
+  for (uint32_t b = 0; b < nblk_wave; b++) {
+    if (b == 0) sha_build_w<NPRE, true>(w, cur, pre, m, 0u, nblk, bitlen);
+    else if (b + 2 < nblk) sha_build_w<NPRE, false, true>(w, cur, pre, m, b, nblk, bitlen);
+    else sha_build_w<NPRE, false>(w, cur, pre, m, b, nblk, bitlen);
+    if (b + 1 < nblk) sha_load_block(cur, m, 32 * (int)(b + 1) - NPRE);
+    uint64_t* dst = lds + (b & 1u) * SHA2W_WORDS + lane;
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+      if (writer) dst[SHA2W_LANES * t] = w[t];
+#pragma unroll 16
+    for (int t = 16; t < 80; t++) {
+      const uint64_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+      const uint64_t s0 = sha_bitop3<SHA_XOR3>(sha_ror(w15, 1), sha_ror(w15, 8), sha_shr(w15, 7));
+      const uint64_t s1 = sha_bitop3<SHA_XOR3>(sha_ror(w2, 19), sha_ror(w2, 61), sha_shr(w2, 6));
+      w[t & 15] += s0 + w[(t + 9) & 15] + s1;
+      if (writer) dst[SHA2W_LANES * t] = w[t & 15];
+    }
+    __syncthreads();
+  }
+}
+
+/* wave 0: 80 rounds per block from the schedule in LDS, a barrier before
+   each; the digest of this lane's PRE || M as sha512_pre returns it
+   (blocks past the lane's own count are run and dropped) */
+template <int NPRE>
+FD_DEV void sha512_rounds_wave(uint32_t (&out)[16], const sha_msg_src& m, uint32_t nblk_wave, const uint64_t* lds) {
+  constexpr int PB = 4 * NPRE;
+  const uint32_t lane = threadIdx.x & (SHA2W_LANES - 1u);
+  const uint32_t nblk = (m.sz + PB + 17u + 127u) >> 7;
+  uint64_t h[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                   0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                   0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+#pragma clang loop unroll(disable)
+  for (uint32_t b = 0; b < nblk_wave; b++) {
+    __syncthreads();
+    const uint64_t* src = lds + (b & 1u) * SHA2W_WORDS + lane;
+    uint64_t v[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = h[i];
+#pragma clang loop unroll(disable)
+    for (int r0 = 0; r0 < 80; r0 += 16) {
+      uint64_t w[16];
+#pragma unroll
+      for (int r = 0; r < 16; r++) w[r] = src[SHA2W_LANES * (r0 + r)];
+      sha512_rounds16<false>(v, w, r0);
+    }
+    const bool mine = b < nblk;
+#pragma unroll
+    for (int i = 0; i < 8; i++) h[i] += mine ? v[i] : 0ull;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    out[2 * i] = bswap32((uint32_t)(h[i] >> 32));
+    out[2 * i + 1] = bswap32((uint32_t)h[i]);
+  }
+}
+
 /* digest of R(32) || A(32) || M(sz): the verify challenge */
 FD_DEV void sha512_ram(uint32_t (&out)[16], const uint32_t (&r)[8], const uint32_t (&a)[8],
                        const sha_msg_src& m) {
