@@ -1167,9 +1167,11 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm8_kernel(fd_ed25519_verify_
    tables, additions and order as dsm8. */
 #include "fd25519_r16.h"
 
-/* this lane's r16 limb of its row's coordinate of base entry e, as qc
-   (y-x, y+x, 2dxy, 2) */
-FD_DEV uint32_t btab16_r16(const int32_t* g_btab, int e, const r16ctx& k) {
+/* base entry e's coordinate for this lane's row, fetched (btab16_fetch,
+   issued a window ahead of its use: the wide tables are 2 GiB, so the
+   load usually misses the TLB) and then converted to this lane's r16 limb
+   of the qc form (y-x, y+x, 2dxy, 2) */
+FD_DEV fe btab16_fetch(const int32_t* g_btab, int e, const r16ctx& k) {
   const int off = (int)((k.r0 & 10u) | (k.r2 & 20u));   /* row 3 loads row 1's (y+x) and drops it */
   const int2* src = reinterpret_cast<const int2*>(g_btab + (size_t)e * FD_ED25519_BTAB16_STRIDE + off);
   fe c;
@@ -1179,6 +1181,9 @@ FD_DEV uint32_t btab16_r16(const int32_t* g_btab, int e, const r16ctx& k) {
     c.v[2 * q] = x.x;
     c.v[2 * q + 1] = x.y;
   }
+  return c;
+}
+FD_DEV uint32_t btab16_r16(const fe& c, const r16ctx& k) {
   return (r16_from_fe(c, k) & ~k.r3) | (r16_small(2u, k) & k.r3);
 }
 
@@ -1228,6 +1233,8 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
     const bool badd = half ? fd_bw<BW>::hi_at(it) : fd_bw<BW>::lo_at(it);
     const uint32_t bdig = (uint32_t)__builtin_amdgcn_readfirstlane((int)(badd ? pop160u<BW>(bd) : 0u));
     const uint32_t ce = table16_at(tab, e < 0 ? -e : e);
+    fe braw;
+    if (badd) braw = btab16_fetch(btab, (int)bdig, k);   /* in flight during the doublings */
     if (it != W - 1) {
       P = ge16_dbl2<false, false>(P, k);   /* (X, Y, Z, X) between doublings: T only before an addition */
       P = ge16_dbl2<true, false>(P, k);
@@ -1235,7 +1242,7 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
       P = ge16_dbl2<true, true>(P, k);
     }
     uint32_t b = 0u;
-    if (badd) b = btab16_r16(btab, (int)bdig, k);
+    if (badd) b = btab16_r16(braw, k);
     P = ge16_cneg4(P, k.r03, e < 0, k);
     P = ge16_add2<true>(P, ce, e < 0, k);
     if (badd) P = ge16_add2<true>(P, b, false, k);

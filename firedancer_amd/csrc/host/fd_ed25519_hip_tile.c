@@ -87,6 +87,23 @@ static __thread unsigned long long pf_sub_h2d, pf_sub_launch, pf_sub_d2h, pf_sub
 #define PF_SUB( acc, stmt ) do { stmt; } while(0)
 #endif
 
+/* May a partial batch (the input drained before the batch filled) go out
+   with in_flight batches already on the GPU?  Only while a slot stays free
+   for a full one, and only while fewer than VTILE_PARTIAL_MAX are in
+   flight: at a low offered load every transaction would otherwise leave
+   alone on its own slot, and eight slots' kernel chains on eight hardware
+   queues at once made each batch's round trip twice as long (in-process
+   latency mode at 28K txn/s: p50 0.36 ms with 8 slots, 0.18 ms with 4,
+   profiles/r5_latency_low_load.txt; at most 2 / 3 / 4 / 7 in flight:
+   p50 0.21 / 0.19 / 0.18 / 0.31-0.35 ms).  Full batches are not limited. */
+#ifndef VTILE_PARTIAL_MAX
+#define VTILE_PARTIAL_MAX 4U
+#endif
+static inline int
+partial_ok( unsigned in_flight, unsigned slot_cnt ) {
+  return in_flight+1U<slot_cnt && in_flight<VTILE_PARTIAL_MAX;
+}
+
 #define SLOT_FREE 0
 #define SLOT_FILL 1
 #define SLOT_BUSY 2
@@ -478,7 +495,7 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
     PF_SUB( pf_sub_launch, err = fd_ed25519_hip_launch_txn_stage( &sp, st ) );
     if( err ) return tile_fail( "txn_stage launch", (hipError_t)err );
     if( slots ) {
-      PF_SUB( pf_sub_launch, err = fd_ed25519_hip_verify_dev( s->eng, slots, s->d_msgs, s->d_soff, s->d_ssz, s->d_sigs,
+        PF_SUB( pf_sub_launch, err = fd_ed25519_hip_verify_dev( s->eng, slots, s->d_msgs, s->d_soff, s->d_ssz, s->d_sigs,
                                                                s->d_pubs, s->d_out, st ) );
       if( err ) return err;
     }
@@ -1489,7 +1506,7 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
     batches0 = vt->pipe->seq;
     /* ring drained: send the open batch if a slot can take it */
     if( !pulled && vt->open && vt->open->txn_cnt &&
-        ( slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<slot_cnt || next==txn_cnt ) )
+        ( slot_cnt==1U || partial_ok( fd_ed25519_hip_pipe_in_flight( vt->pipe ), slot_cnt ) || next==txn_cnt ) )
       fd_ed25519_hip_vtile_flush( vt, 0 );
     unsigned long got = fd_ed25519_hip_vtile_poll( vt, 0, 4096UL, ck, vd, NULL );
     double t = now_s();
@@ -1993,7 +2010,7 @@ vsvc_pass( vsvc_t * S ) {
      take it (all of it at the end) */
   int flushed = 0;
   if( !pulled && vt->open && vt->open->txn_cnt &&
-      ( S->eos || S->slot_cnt==1U || fd_ed25519_hip_pipe_in_flight( vt->pipe )+1U<S->slot_cnt ) ) {
+      ( S->eos || S->slot_cnt==1U || partial_ok( fd_ed25519_hip_pipe_in_flight( vt->pipe ), S->slot_cnt ) ) ) {
     fd_ed25519_hip_vtile_flush( vt, S->eos );
     flushed = 1;
   }

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""The in-process latency mode (C5's vtile + ring, no processes or shared-
+memory links) at fixed offered rates from the reference tile's load to the
+GPU path's: p50 / p99 and the mean batch size at each, to separate the GPU
+round trip from the deployed path's host chain (run on the box).
+
+    python tools/latency_rates_probe.py [--rates 28000,57000,570000,2400000] [--txns 40000] [--slots 8]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rates", default="28000,57000,570000,2400000")
+    ap.add_argument("--txns", type=int, default=40000)
+    ap.add_argument("--slots", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--runs", type=int, default=3)
+    args = ap.parse_args()
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(args.slots))
+    from firedancer_amd import ed25519, tile, workload
+    eng = ed25519.Engine(0, max_chunk=1 << 16)
+    pay, _ = workload.txn_payloads(eng, args.txns, 4242, msg_sz=200)
+    eng.close()
+    for rate in [float(r) for r in args.rates.split(",")]:
+        pooled, batches, achieved = [], 0, []
+        for _ in range(args.runs):
+            n = min(args.txns, max(2000, int(rate * 0.5))) if rate > 0 else args.txns
+            lat, v, res = tile.latency_run(pay[:n] if isinstance(pay, list) else pay, rate, slot_cnt=args.slots,
+                                           batch_sigs=args.batch, ring_depth=4096)
+            pooled.append(lat * 1e3)
+            batches += res["batches"]
+            achieved.append(res["achieved_txn_per_s"])
+        ms = np.concatenate(pooled)
+        print(json.dumps({"rate": rate, "txns": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
+                          "p99_ms": float(np.percentile(ms, 99)), "mean_batch": ms.size / max(batches, 1),
+                          "achieved_txn_per_s": float(np.mean(achieved))}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
