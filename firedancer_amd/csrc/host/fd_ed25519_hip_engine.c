@@ -511,7 +511,6 @@ fd_ed25519_hip_engine_set_r16_max( fd_ed25519_hip_engine_t * e, unsigned long n 
   return FD_ED25519_HIP_OK;
 }
 
-
 int
 fd_ed25519_hip_engine_info( fd_ed25519_hip_engine_t const * e, fd_ed25519_hip_info_t * info ) {
   if( !e || !info ) return FD_ED25519_HIP_ERR_INVAL;
