@@ -206,6 +206,34 @@ FD_HALF_FN double fd_half_fdiv(double x, double y) {
   return q;
 }
 
+/* floor(x / y) for integers 0 <= x, 0 < y < 2^53 held in doubles, from a
+   single-precision estimate (relative error < 2^-21.4: off by at most one
+   below quotients of 2^20) and one exact correction (fma(-q, y, x) is
+   exact here); -1 when the result is still not exact -- a quotient too
+   large for the estimate, which ends the caller's Lehmer round */
+#ifndef FD_HALF_RCPF
+#define FD_HALF_RCPF(y) (1.0f / (y))
+#endif
+FD_HALF_FN double fd_half_fdiv32(double x, double y) {
+  double q = __builtin_floor((double)((float)x * FD_HALF_RCPF((float)y)));
+  double rem = __builtin_fma(-q, y, x);
+  q = rem < 0.0 ? q - 1.0 : (rem >= y ? q + 1.0 : q);
+  rem = __builtin_fma(-q, y, x);
+  return (rem >= 0.0 && rem < y) ? q : -1.0;
+}
+
+/* the Lehmer inner step's form: 0 the two-branch double-precision
+   division (fd_half_fdiv), 1 one branch per step with fd_half_fdiv,
+   2 one branch with fd_half_fdiv32 */
+#ifndef FD_HALF_INNER
+#define FD_HALF_INNER 2
+#endif
+#if FD_HALF_INNER == 2
+#define FD_HALF_QUOT(x, y) fd_half_fdiv32((x), (y))
+#else
+#define FD_HALF_QUOT(x, y) fd_half_fdiv((x), (y))
+#endif
+
 /* |x| of a 160-bit two's complement value into mag, returns the sign */
 FD_HALF_FN int fd_half_abs(uint32_t (&mag)[FD_HALF_TW], const uint32_t (&x)[FD_HALF_TW]) {
   const int neg = (int)(x[FD_HALF_TW - 1] >> 31);
@@ -246,11 +274,20 @@ FD_HALF_FN int fd_half_scalars(const uint32_t (&k)[8], uint32_t (&c)[FD_HALF_TW]
     double Af = 1.0, Bf = 0.0, Cf = 0.0, Df = 1.0;
     for (int inner = 0; inner < 64; inner++) {
       const double x1 = uh + Af, y1 = vh + Cf, x2 = uh + Bf, y2 = vh + Df;
+#if FD_HALF_INNER == 0
       if (!(y1 > 0.0 && y2 > 0.0 && x1 >= 0.0 && x2 >= 0.0)) break;
       const double q = fd_half_fdiv(x1, y1);
       if (q != fd_half_fdiv(x2, y2)) break;
       const double nv = __builtin_fma(-q, vh, uh);
       if (nv < floor_v) break;
+#else
+      /* every test of the step folded into one branch, both quotients
+         computed side by side (the step is a latency chain at one wave) */
+      const bool valid = (y1 > 0.0) & (y2 > 0.0) & (x1 >= 0.0) & (x2 >= 0.0);
+      const double q = FD_HALF_QUOT(x1, valid ? y1 : 1.0), q2 = FD_HALF_QUOT(x2, valid ? y2 : 1.0);
+      const double nv = __builtin_fma(-q, vh, uh);
+      if (!(valid & (q >= 0.0) & (q == q2) & (nv >= floor_v))) break;
+#endif
       double T = __builtin_fma(-q, Cf, Af); Af = Cf; Cf = T;
       T = __builtin_fma(-q, Df, Bf); Bf = Df; Df = T;
       uh = vh; vh = nv;

@@ -38,6 +38,7 @@
 #include "fd_sha512_dev.h"
 #define FD_HALF_FN __device__ static inline
 #define FD_HALF_RCP(y) __builtin_amdgcn_rcp(y)
+#define FD_HALF_RCPF(y) __builtin_amdgcn_rcpf(y)
 #include "fd25519_half.h"
 
 
