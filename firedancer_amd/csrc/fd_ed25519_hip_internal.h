@@ -118,6 +118,9 @@ typedef struct {
   int              small;          /* small chunk: fused prep kernel, no sort, dsm4 (1: a
                                       quad of lanes per signature) or dsm8 (2: two quads),
                                       full-length items by a scan of hflag          */
+  int              full_in_prep;   /* small == 3 and atab holds a lane per signature:
+                                      prep16's hash waves run the full-length items
+                                      (atab slot j) and no scan follows dsm16          */
   int              bw_bits;        /* radix of btab_lo / btab_hi: FD_ED25519_BTABW_BITS or
                                       FD_ED25519_BTABC_BITS (compact)                 */
   /* A/B build only (-DFD_ED25519_AB_LDS_BASE=1): the base
@@ -126,6 +129,12 @@ typedef struct {
   int32_t const *  btab8_lo;
   int32_t const *  btab8_hi;
 } fd_ed25519_verify_params_t;
+
+/* 0: prep16 leaves the full-length items to a flag scan after dsm16 (A/B
+   build) */
+#ifndef FD_ED25519_FULL_IN_PREP
+#define FD_ED25519_FULL_IN_PREP 1
+#endif
 
 #define FD_ED25519_BTAB8_SHIFT 136   /* A/B LDS tables: s' = lo (17 digits) + 2^136 hi (15 digits) */
 

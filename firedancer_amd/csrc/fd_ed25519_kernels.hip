@@ -805,14 +805,10 @@ FD_DEV int dsm_half_one_lds(const fd_ed25519_verify_params_t& p, uint64_t j, int
    64 additions of [0..8](-A)) and S in radix 2^16 (16 mixed additions),
    then R' == R projectively (fd_ed25519_point_eq_z1: X' == x_R Z',
    Y' == y_R Z'). */
-FD_DEV int dsm_full_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* tabA) {
+FD_DEV int dsm_full_core(const fd_ed25519_verify_params_t& p, uint64_t j, int4* tabA, int code, const fe& ax,
+                         const fe& ay, const fe& rx, const fe& ry) {
   const uint64_t i = p.base + j;
-  const int code = precheck(p, j);
-  {
-    fe x, y;
-    load_pt(x, y, p, 0, j);
-    table_build<false>(tabA, x, y, true);
-  }
+  table_build<false>(tabA, ax, ay, true);
   uint32_t kd[8], sd[8];
   {
     uint32_t k[8], S[8];
@@ -853,8 +849,7 @@ FD_DEV int dsm_full_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
     }
     ge_p1p1_to_p2(Q, Rt);
   }
-  fe rx, ry, t1, t2;
-  load_pt(rx, ry, p, 1, j);
+  fe t1, t2;
   fe_mul(t1, rx, Q.Z);
   fe_sub(t1, t1, Q.X);
   fe_mul(t2, ry, Q.Z);
@@ -862,6 +857,13 @@ FD_DEV int dsm_full_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* t
   const bool eq = fe_iszero(t1) && fe_iszero(t2);
   if (code != FD_PENDING) return code;
   return eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+FD_DEV int dsm_full_one(const fd_ed25519_verify_params_t& p, uint64_t j, int4* tabA) {
+  fe ax, ay, rx, ry;
+  load_pt(ax, ay, p, 0, j);
+  load_pt(rx, ry, p, 1, j);
+  return dsm_full_core(p, j, tabA, precheck(p, j), ax, ay, rx, ry);
 }
 
 /* Persistent over fix_cnt (rounded up to whole waves) + n items, handed
@@ -1364,6 +1366,30 @@ FD_DEV void hash16_block(const fd_ed25519_verify_params_t& p, uint64_t* sched) {
   if (!live) return;
   hash_finish(p, j, dig, S);
   scalar_one(p, j);
+#if FD_ED25519_FULL_IN_PREP
+  /* the rare signature without a half-size pair (~1e-6): the full-length
+     form right here, on points this lane decodes itself (decode16's
+     blocks write the same points concurrently, in another
+     representation), so that no flag-scan launch follows dsm16 */
+  if (p.full_in_prep && (p.hflag[j] & FD_HF_FULL)) {
+    const bool avx = !p.codes_portable;
+    uint32_t sa[8], sr[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) { sa[w] = pre[8 + w]; sr[w] = pre[w]; }
+    decoded_pt da, dr;
+    ge_decode(da, sa, avx);
+    ge_decode(dr, sr, avx);
+    int code = FD_PENDING;   /* precheck's order, from this lane's own flags */
+    if (!p.sflag[j]) code = FD_ED25519_ERR_SIG;
+    else if (da.fail) code = p.codes_portable ? FD_ED25519_ERR_PUBKEY : FD_ED25519_ERR_SIG;
+    else if (dr.fail) code = FD_ED25519_ERR_SIG;
+    else if (da.small) code = FD_ED25519_ERR_PUBKEY;
+    else if (dr.small) code = FD_ED25519_ERR_SIG;
+    int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + (j >> 6) * FD_ED25519_ATAB_BYTES_PER_WAVE) +
+                 (j & 63u) * (2 * FD_ED25519_ATAB_STRIDE * 10);
+    p.out[p.base + j] = (int8_t)dsm_full_core(p, j, tabA, code, da.x, da.y, dr.x, dr.y);
+  }
+#endif
 }
 
 __global__ void __launch_bounds__(128) fd_ed25519_prep16_kernel(fd_ed25519_verify_params_t p, uint32_t hash_blocks) {
@@ -1708,6 +1734,7 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
         const dim3 g16((uint32_t)p->n);
         if (compact) hipLaunchKernelGGL(fd_ed25519_dsm16_kernel<FD_ED25519_BTABC_BITS>, g16, dim3(128), 0, st, *p);
         else         hipLaunchKernelGGL(fd_ed25519_dsm16_kernel<FD_ED25519_BTABW_BITS>, g16, dim3(128), 0, st, *p);
+        if (p->full_in_prep) break;   /* the full-length items were done in prep16: no scan */
       } else if (p->small == 2) {
         if (compact) hipLaunchKernelGGL(fd_ed25519_dsm8_kernel<FD_ED25519_BTABC_BITS>, g8, dim3(256), 0, st, *p);
         else         hipLaunchKernelGGL(fd_ed25519_dsm8_kernel<FD_ED25519_BTABW_BITS>, g8, dim3(256), 0, st, *p);

@@ -74,7 +74,7 @@ def main():
     res[f"fd_ed25519_verify_reference_cpu_{flavour}_one_core"] = pct(t_ref)
     res["msg_sz"] = 200
     res["note"] = ("synchronous per-call latency through ctypes (~1 us of the GPU figure is the call itself); the GPU "
-                   "call is one H2D, the small-chunk kernels (prep, dsm8) and one D2H")
+                   "call is one H2D, the small-chunk kernels (prep16, dsm16) and one D2H")
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
     print(json.dumps(res))
