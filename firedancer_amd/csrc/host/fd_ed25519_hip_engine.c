@@ -577,6 +577,8 @@ verify_chunk( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p, int l
   p->base  = base;
   p->n     = cnt;
   p->small = p->n > e->quad_max ? 0 : p->n <= e->r16_max ? 3 : (p->n <= e->oct_max ? 2 : 1);
+  /* always true when small==3: quad_max <= the quad tables' room, which is
+     below one 2.5 KB atab slot per signature; kept as the kernel's bound */
   p->full_in_prep = FD_ED25519_FULL_IN_PREP && p->small==3 && p->n <= lane_atab_bytes( e ) / (fd_ed25519_hip_atab_bytes_per_wave() / 64UL);
   p->perm  = ( p->small || p->digests ) ? NULL : e->lane[l].d_perm;   /* digests: no hash lengths to sort by */
   if( e->timing && e->tm_cnt<FD_ED25519_HIP_TIMING_MAX ) {
