@@ -171,3 +171,25 @@ def test_fixture_k_need_long_d(half):
         assert ok and (c - dd * k) % N8L == 0 and 0 <= c < 2**BITS, tag
         assert (abs(dd).bit_length() + 4) // 4 == w, (tag, abs(dd).bit_length())
         assert not run(half, k, 139)[0], tag
+
+
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_inner_step_forms_agree(half, tmp_path, form):
+    """The Lehmer inner step's earlier forms (FD_HALF_INNER 0-2: the
+    double-precision division, one branch per step, the single-precision
+    estimate with an exactness test) give the same (ok, c, d) as the
+    default (3: the estimate bounded below 2^20, operand checks in the
+    branch) -- the remainder sequence is unique, only where a round ends
+    may differ."""
+    out = str(tmp_path / ("half%d.so" % form))
+    subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-DFD_HALF_INNER=%d" % form,
+                           "-I", os.path.join(REPO, "firedancer_amd", "csrc"),
+                           os.path.join(REPO, "tests", "half_harness.cpp"), "-o", out])
+    other = ctypes.CDLL(out)
+    other.half_scalars.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int]
+    other.half_scalars.restype = ctypes.c_int
+    rng = random.Random(17 + form)
+    ks = [rng.randrange(L) for _ in range(20000)] + [0, 1, L - 1, 2**BITS, 2**252 - 1]
+    for k in ks:
+        for dbits in (BITS, DBITS_EXT):
+            assert run(half, k, dbits) == run(other, k, dbits), (hex(k), dbits)
