@@ -241,11 +241,11 @@ FD_HALF_FN double fd_half_fdiv20(double x, double y) {
    division (fd_half_fdiv), 1 one branch per step with fd_half_fdiv,
    2 one branch with fd_half_fdiv32, 3 one branch with fd_half_fdiv20 on
    unguarded operands (the operand checks only in the branch) and the
-   cofactor updates ahead of it */
+   cofactor updates ahead of it, 4 as 3 with two steps per branch */
 #ifndef FD_HALF_INNER
-#define FD_HALF_INNER 3
+#define FD_HALF_INNER 4
 #endif
-#if FD_HALF_INNER == 3
+#if FD_HALF_INNER >= 3
 #define FD_HALF_QUOT(x, y) fd_half_fdiv20((x), (y))
 #elif FD_HALF_INNER == 2
 #define FD_HALF_QUOT(x, y) fd_half_fdiv32((x), (y))
@@ -299,6 +299,30 @@ FD_HALF_FN int fd_half_scalars(const uint32_t (&k)[8], uint32_t (&c)[FD_HALF_TW]
       if (q != fd_half_fdiv(x2, y2)) break;
       const double nv = __builtin_fma(-q, vh, uh);
       if (nv < floor_v) break;
+#elif FD_HALF_INNER == 4
+      /* two steps per branch: the second computed from the first's
+         state as if the first passed; on a failed test the state falls
+         back to the last step that passed */
+      const bool valid = (y1 > 0.0) & (y2 > 0.0) & (x1 >= 0.0) & (x2 >= 0.0);
+      const double q = fd_half_fdiv20(x1, y1), q2 = fd_half_fdiv20(x2, y2);
+      const double nv = __builtin_fma(-q, vh, uh);
+      const double nC = __builtin_fma(-q, Cf, Af), nD = __builtin_fma(-q, Df, Bf);
+      const bool ok1 = valid & (q >= 0.0) & (q == q2) & (nv >= floor_v);
+      /* step 2 on (vh, nv, Cf, nC, Df, nD) */
+      const double x1b = vh + Cf, y1b = nv + nC, x2b = vh + Df, y2b = nv + nD;
+      const bool validb = (y1b > 0.0) & (y2b > 0.0) & (x1b >= 0.0) & (x2b >= 0.0);
+      const double qb = fd_half_fdiv20(x1b, y1b), q2b = fd_half_fdiv20(x2b, y2b);
+      const double nvb = __builtin_fma(-qb, nv, vh);
+      const double nCb = __builtin_fma(-qb, nC, Cf), nDb = __builtin_fma(-qb, nD, Df);
+      const bool ok2 = validb & (qb >= 0.0) & (qb == q2b) & (nvb >= floor_v);
+      if (!(ok1 & ok2)) {
+        if (ok1) { Af = Cf; Cf = nC; Bf = Df; Df = nD; uh = vh; vh = nv; }
+        break;
+      }
+      Af = nC; Cf = nCb; Bf = nD; Df = nDb;
+      uh = nv; vh = nvb;
+      inner++;
+      continue;
 #elif FD_HALF_INNER == 3
       /* the quotients straight from the operands: when an operand check
          fails, whatever they are is discarded with the step */

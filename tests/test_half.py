@@ -173,14 +173,15 @@ def test_fixture_k_need_long_d(half):
         assert not run(half, k, 139)[0], tag
 
 
-@pytest.mark.parametrize("form", [0, 1, 2])
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
 def test_inner_step_forms_agree(half, tmp_path, form):
-    """The Lehmer inner step's earlier forms (FD_HALF_INNER 0-2: the
+    """The Lehmer inner step's earlier forms (FD_HALF_INNER 0-3: the
     double-precision division, one branch per step, the single-precision
-    estimate with an exactness test) give the same (ok, c, d) as the
-    default (3: the estimate bounded below 2^20, operand checks in the
-    branch) -- the remainder sequence is unique, only where a round ends
-    may differ."""
+    estimate with an exactness test, the estimate bounded below 2^20 with
+    the operand checks in the branch) give the same (ok, c, d) as the
+    default (4: that with two steps per branch, falling back to the last
+    step that passed) -- the remainder sequence is unique, only where a
+    round ends may differ."""
     out = str(tmp_path / ("half%d.so" % form))
     subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-DFD_HALF_INNER=%d" % form,
                            "-I", os.path.join(REPO, "firedancer_amd", "csrc"),
