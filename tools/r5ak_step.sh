@@ -1,7 +1,7 @@
 #!/bin/bash
-# Lehmer inner step: two-wave SHA rounds reading each 16 words a group ahead (pf) vs not; prep16 stamps, interleaved x3
+# SHA rounds with h+K+W added first (pf: FD_SHA_T1_EARLY) vs not; prep16 stamps, interleaved x3
 set -o pipefail
-O=gpurun_out/r5aj; mkdir -p $O
+O=gpurun_out/r5ak; mkdir -p $O
 for r in 1 2 3; do
   for v in "" _pf; do
     echo "== base$v" >> $O/stamps.txt
