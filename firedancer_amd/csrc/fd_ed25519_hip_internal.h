@@ -116,8 +116,9 @@ typedef struct {
   int              codes_portable; /* 0: AVX-512 backend codes, 1: portable  */
   int              half_dbits;     /* longest |d| of the half-size form (fd25519_half.h) */
   int              small;          /* small chunk: fused prep kernel, no sort, dsm4 (1: a
-                                      quad of lanes per signature) or dsm8 (2: two quads),
-                                      full-length items by a scan of hflag          */
+                                      quad of lanes per signature), dsm8 (2: two quads)
+                                      or dsm16 (3: two waves, prep16 before it); the
+                                      full-length items by a scan of hflag (1, 2)    */
   int              full_in_prep;   /* small == 3 and atab holds a lane per signature:
                                       prep16's hash waves run the full-length items
                                       (atab slot j) and no scan follows dsm16          */

@@ -1726,8 +1726,9 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
     break;
   case FD_ED25519_PHASE_DSM: {
     if (p->small) {
-      /* a quad per signature, then the (rare) full-length items, found by
-         a scan of the flags */
+      /* a quad / two quads / two waves per signature, then the (rare)
+         full-length items, found by a scan of the flags -- unless prep16
+         ran them (full_in_prep) */
       const bool compact = p->bw_bits == FD_ED25519_BTABC_BITS;
       const dim3 g8((uint32_t)((8 * p->n + 255) / 256)), g4((uint32_t)((4 * p->n + 255) / 256));
       if (p->small == 3) {
