@@ -72,6 +72,42 @@ def test_c2_full_size(ref):
     assert 0.015 < (want != 0).mean() < 0.025
 
 
+@pytest.fixture(scope="module")
+def c2_small_chunks(ref):
+    """the C2 workload and the reference's codes for it, once for the
+    small-chunk forms below"""
+    from firedancer_amd import ed25519, workload
+    cfg = workload.CONFIGS["C2"]
+    threads, _ = workload.host_cores()
+    eng = ed25519.Engine(0, max_chunk=1 << 20)
+    wl = ed25519.DeviceWorkload(eng, cfg["n"], cfg["lo"], cfg["hi"], cfg["ppm"], seed=0x5EED)
+    want, _ = _ref_codes(ref, wl, wl.n, threads)
+    yield wl, want
+    wl.free()
+    eng.close()
+
+
+@pytest.mark.parametrize("chunk", [256, 4096, 16384], ids=["r16", "oct", "quad"])
+def test_c2_full_size_small_chunks(c2_small_chunks, chunk):
+    """The whole C2 workload through an engine of small chunks -- the
+    latency forms a tile slot or a drop-in launch takes: 256 signatures a
+    chunk (prep16 + dsm16), 4096 (dsm8), 16384 (dsm4) -- code by code
+    against the reference."""
+    from firedancer_amd import ed25519
+    wl, want = c2_small_chunks
+    eng = ed25519.Engine(0, max_chunk=chunk)
+    out = eng.alloc(wl.n)
+    try:
+        eng.verify_dev(wl.n, wl.msgs.ptr, wl.off.ptr, wl.sz.ptr, wl.sigs.ptr, wl.pubs.ptr, out.ptr)
+        eng.sync()
+        got = out.download(np.int8, wl.n)
+    finally:
+        out.free()
+        eng.close()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]]
+
+
 def test_c4_stream_12m(ref):
     """>= 10M signatures (12M: 12 chunks of 1M, seed 0xC4C4, the 64M
     stream's first 12M) code by code against the reference."""
