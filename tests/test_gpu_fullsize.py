@@ -108,6 +108,27 @@ def test_c2_full_size_small_chunks(c2_small_chunks, chunk):
     assert len(bad) == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]]
 
 
+def test_dropin_on_c2_sample(c2_small_chunks):
+    """fd_ed25519_verify, one synchronous call per signature (the drop-in's
+    latency path: a one-signature launch reading the pinned block in place),
+    over the first 20,000 signatures of the C2 workload -- its invalid
+    classes included -- against the reference's codes."""
+    from firedancer_amd import ed25519
+    wl, want = c2_small_chunks
+    n = 20000
+    sizes = wl.sizes[:n].astype(np.uint64)
+    off = np.zeros(n, np.uint64)
+    np.cumsum(sizes[:-1], out=off[1:])
+    msgs = wl.msgs.download(np.uint8, int(sizes.sum()))
+    sigs = wl.sigs.download(np.uint8, 64 * n).reshape(n, 64)
+    pubs = wl.pubs.download(np.uint8, 32 * n).reshape(n, 32)
+    got = np.array([ed25519.verify(msgs[int(off[i]):int(off[i] + sizes[i])].tobytes(), sigs[i].tobytes(),
+                                   pubs[i].tobytes()) for i in range(n)], np.int8)
+    assert (want[:n] != 0).sum() > 100   # the sample holds every invalid class several times over
+    bad = np.nonzero(got != want[:n])[0]
+    assert len(bad) == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]]
+
+
 def test_c4_stream_12m(ref):
     """>= 10M signatures (12M: 12 chunks of 1M, seed 0xC4C4, the 64M
     stream's first 12M) code by code against the reference."""
