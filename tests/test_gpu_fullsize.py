@@ -129,6 +129,37 @@ def test_dropin_on_c2_sample(c2_small_chunks):
     assert len(bad) == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]]
 
 
+def test_c2_full_size_portable_codes(c2_small_chunks):
+    """The C2 workload with FD_ED25519_HIP_FLAG_CODES_PORTABLE (the
+    reference's portable backend's error codes: a public key that does not
+    decode is ERR_PUBKEY there, ERR_SIG in the AVX-512 backend), code by
+    code against the reference's portable build; the verdicts (zero or
+    not) equal the AVX-512 reference's."""
+    from firedancer_amd import ed25519, workload
+    wl, want_avx = c2_small_chunks
+    path = os.path.join(REPO, "oracle", "_ref", "libfdref_portable.so")
+    if not os.path.exists(path):
+        pytest.fail(f"{path} not built")
+    lib = ctypes.CDLL(path)
+    lib.fdref_verify_many.restype = ctypes.c_long
+    lib.fdref_verify_many.argtypes = [ctypes.c_ulong] + [ctypes.c_void_p] * 6 + [ctypes.c_int, ctypes.c_ulong]
+    threads, _ = workload.host_cores()
+    want, _ = _ref_codes(lib, wl, wl.n, threads)
+    eng = ed25519.Engine(0, max_chunk=1 << 20, codes="portable")
+    out = eng.alloc(wl.n)
+    try:
+        eng.verify_dev(wl.n, wl.msgs.ptr, wl.off.ptr, wl.sz.ptr, wl.sigs.ptr, wl.pubs.ptr, out.ptr)
+        eng.sync()
+        got = out.download(np.int8, wl.n)
+    finally:
+        out.free()
+        eng.close()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:8]]
+    assert np.array_equal(want != 0, want_avx != 0)
+    assert (want != want_avx).any()   # the workload holds the classes whose codes differ
+
+
 def test_c4_stream_12m(ref):
     """>= 10M signatures (12M: 12 chunks of 1M, seed 0xC4C4, the 64M
     stream's first 12M) code by code against the reference."""
