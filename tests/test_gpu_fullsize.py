@@ -87,15 +87,20 @@ def c2_small_chunks(ref):
     eng.close()
 
 
-@pytest.mark.parametrize("chunk", [256, 4096, 16384], ids=["r16", "oct", "quad"])
-def test_c2_full_size_small_chunks(c2_small_chunks, chunk):
+@pytest.mark.parametrize("chunk,opts", [(256, {}), (4096, {}), (16384, {}), (1 << 20, {"compact": True}),
+                                        (1 << 20, {"half": "strict"}), (256, {"half": "strict"})],
+                         ids=["r16", "oct", "quad", "wide-compact", "wide-strict", "r16-strict"])
+def test_c2_full_size_small_chunks(c2_small_chunks, chunk, opts):
     """The whole C2 workload through an engine of small chunks -- the
     latency forms a tile slot or a drop-in launch takes: 256 signatures a
-    chunk (prep16 + dsm16), 4096 (dsm8), 16384 (dsm4) -- code by code
-    against the reference."""
+    chunk (prep16 + dsm16), 4096 (dsm8), 16384 (dsm4) -- and through the
+    throughput form with the compact base tables (the drop-ins') or with
+    FLAG_HALF_STRICT (every k without a 131-bit pair, ~0.16%, in the
+    full-length form: the one-lane dsm kernel's items, or prep16's lanes at
+    256 a chunk), code by code against the reference."""
     from firedancer_amd import ed25519
     wl, want = c2_small_chunks
-    eng = ed25519.Engine(0, max_chunk=chunk)
+    eng = ed25519.Engine(0, max_chunk=chunk, **opts)
     out = eng.alloc(wl.n)
     try:
         eng.verify_dev(wl.n, wl.msgs.ptr, wl.off.ptr, wl.sz.ptr, wl.sigs.ptr, wl.pubs.ptr, out.ptr)
