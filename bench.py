@@ -331,13 +331,20 @@ def latency_mode(eng, args, device):
     from firedancer_amd import tile, workload
     n = args.latency_txns
     pay, _ = workload.txn_payloads(eng, n, args.seed + 77, msg_sz=200)
-    lat, v, res = tile.latency_run(pay, 0.0, device=device, slot_cnt=args.latency_slots,
-                                   batch_sigs=args.latency_batch, ring_depth=4096)
-    peak = res["achieved_txn_per_s"]
+    # the peak: the median of three unpaced runs, so that 95% of it is a
+    # load the path sustains rather than 95% of one lucky run
+    peaks, ok = [], True
+    for _ in range(3):
+        lat, v, res = tile.latency_run(pay, 0.0, device=device, slot_cnt=args.latency_slots,
+                                       batch_sigs=args.latency_batch, ring_depth=4096)
+        peaks.append(res["achieved_txn_per_s"])
+        ok &= bool((v == 0).all())
+    peak = float(np.median(peaks))
     out = {"batch_sigs": args.latency_batch, "slots_in_flight": args.latency_slots,
            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES") or 4), "txns_per_run": n,
-           "msg_sz": 200, "peak_txn_per_s": peak, "ring": "tango-style mcache/dcache, depth 4096",
-           "verdicts_ok": bool((v == 0).all()), "loads": []}
+           "msg_sz": 200, "peak_txn_per_s": peak, "peak_runs_txn_per_s": peaks,
+           "peak": "median of 3 unpaced runs", "ring": "tango-style mcache/dcache, depth 4096",
+           "verdicts_ok": ok, "loads": []}
     # each load five times; p50 / p99 / max are over every transaction of
     # the five runs pooled (a run is ~0.05-0.1 s, so one host hiccup of a
     # few milliseconds is its whole p99: pooling keeps such events in the
@@ -446,9 +453,13 @@ def latency_deployed(eng, args):
         return res, lat
 
     def sweep(kind, runs, txns):
-        peak_res, _ = run(kind, 0)
-        peak = peak_res["txn_per_s"]
-        out = {"peak_txn_per_s": peak, "txns_per_run": txns, "loads": [], "published_all": peak_res["published"] == txns}
+        # the peak: the median of three unpaced runs (as latency_mode)
+        peak_runs = [run(kind, 0)[0] for _ in range(3)]
+        peaks = [r["txn_per_s"] for r in peak_runs]
+        peak = float(np.median(peaks))
+        out = {"peak_txn_per_s": peak, "peak_runs_txn_per_s": peaks, "peak": "median of 3 unpaced runs",
+               "txns_per_run": txns, "loads": [],
+               "published_all": all(r["published"] == txns for r in peak_runs)}
         for frac in (0.5, 0.8, 0.95):
             pooled, per_run = [], []
             for _ in range(runs):
