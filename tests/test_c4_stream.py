@@ -260,22 +260,24 @@ def test_config_c4_one_rank_carries_the_whole_stream_digest(monkeypatch):
     assert res["frac_of_pcie_bound"] is not None and res["peak_rss_bytes_max_over_ranks"] > 0
 
 
-def test_config_c4_two_ranks_agree_on_the_concatenated_digest():
-    """World 2 (gloo): the config_c4 key is present on both ranks, each
-    streamed its own half, and both report the same concatenated digest,
-    equal to the one-rank stream's (digest_equal true)."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_config_c4_ranks_agree_on_the_concatenated_digest(world):
+    """World 2 / 4 / 8 (gloo, the driver's scaling runs): the config_c4 key
+    is present on every rank, each streamed its own contiguous shard, and
+    all report the same concatenated digest, equal to the one-rank
+    stream's (digest_equal true)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_c4_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_c4_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [o for _, o in sorted(q.get(timeout=180) for _ in procs)]
+    res = [o for _, o in sorted(q.get(timeout=240) for _ in procs)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(r["digest_equal"] is True for r in res), res
-    assert res[0]["stream_digest"] == res[1]["stream_digest"] == _c4_whole_digest()
-    assert res[0]["rank_digests"] == res[1]["rank_digests"] and len(res[0]["rank_digests"]) == 2
-    assert all(r["signatures_per_rank"] == C4_TOTAL // 2 and r["n_gpus"] == 2 for r in res)
+    assert all(r["stream_digest"] == _c4_whole_digest() for r in res)
+    assert all(r["rank_digests"] == res[0]["rank_digests"] for r in res) and len(res[0]["rank_digests"]) == world
+    assert all(r["signatures_per_rank"] == C4_TOTAL // world and r["n_gpus"] == world for r in res)

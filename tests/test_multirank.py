@@ -69,22 +69,25 @@ def _worker(rank, world, port, q):
     q.put((r, local, w, tmax, msum))
 
 
-def test_gloo_world2_coordination():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_coordination(world):
+    """bench.py's rank setup, barrier and max / sum over ranks at the
+    driver's scaling worlds (gloo on the CPU)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=120) for _ in procs)
+    res = sorted(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert [x[0] for x in res] == [0, 1]
-    assert all(x[2] == 2 for x in res)
-    assert all(x[3] == 2.0 for x in res)      # max over ranks of (1 + rank)
-    assert all(x[4] == 3.0 for x in res)      # sum over ranks of 3 * rank
+    assert [x[0] for x in res] == list(range(world))
+    assert all(x[2] == world for x in res)
+    assert all(x[3] == float(world) for x in res)                        # max over ranks of (1 + rank)
+    assert all(x[4] == 3.0 * world * (world - 1) / 2 for x in res)      # sum over ranks of 3 * rank
 
 
 def test_bench_spawns_its_ranks_without_a_launcher():
