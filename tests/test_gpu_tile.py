@@ -54,6 +54,32 @@ def test_vtile_matches_reference_tile(tile, ref, frags, batch_sigs, slot_cnt, gp
     assert any(f is not None and len(f) - 2 - ((len(fr) + 1) & ~1) > 64 for f, fr in zip(want_frags, frags))
 
 
+@pytest.fixture(scope="module")
+def frags_30k(oracle, ref):
+    frags = tile_workload(oracle, 5150, 30000)
+    return frags, ref_vtile_frags(ref, frags)
+
+
+@pytest.mark.parametrize("gpu_parse", [False, True])
+def test_vtile_at_scale_in_the_c5_shape(tile, frags_30k, gpu_parse):
+    """30,000 frags (about 90,000 signatures: bad signatures, duplicates
+    near and across tcache evictions, unparseable and 17+-signer payloads)
+    through the C5 shape -- 256-signature batches, 8 slots, so every batch
+    takes the r16 form -- against the reference tile replayed on the same
+    frags: verdicts, dedup tags and published frags."""
+    frags, (want, want_tags, want_frags) = frags_30k
+    vt = tile.VerifyTile(0, slot_cnt=8, batch_sigs=256, gpu_parse=gpu_parse)
+    got, tags, got_frags = vt.run(frags, frags=True)
+    vt.close()
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [(int(i), int(got[i]), int(want[i])) for i in bad[:10]]
+    ok = want != -3
+    assert np.array_equal(tags[ok], want_tags[ok])
+    bad = [i for i in range(len(frags)) if got_frags[i] != want_frags[i]]
+    assert not bad, bad[:5]
+    assert (want == 0).sum() > len(frags) // 2 and (want != 0).sum() > len(frags) // 20
+
+
 def test_vtile_dedup_across_batches(tile, ref, oracle):
     """Duplicates of a transaction in an earlier batch and in the same batch,
     and copies that come back after the tcache (depth 16) evicted them."""
