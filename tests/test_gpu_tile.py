@@ -230,14 +230,19 @@ def test_device_parse_on_mutated_fixtures(tile, ref):
 
 
 @pytest.mark.parametrize("gpu_parse", [False, True])
-def test_sandboxed_tile_with_gpu_service(tile, ref, frags, tmp_path, gpu_parse):
+@pytest.mark.parametrize("load", ["frags", "frags_30k"])
+def test_sandboxed_tile_with_gpu_service(tile, ref, request, tmp_path, gpu_parse, load):
     """the verify tile in seccomp strict mode (the
     standalone producer: memory operations, write and _exit only) and the
     GPU in a separate service process, connected by two shared-memory
-    links.  The verdict stream equals the reference tile's."""
+    links.  The verdict stream equals the reference tile's -- on the 3000
+    fixture frags and on the 30,000-frag workload."""
     import subprocess
     import sys
     import uuid
+    frags = request.getfixturevalue(load)
+    if load == "frags_30k":
+        frags = frags[0]
     frags = [p for p in frags if len(p) <= tile.TXN_MTU]
     want, _, want_frags = ref_vtile_frags(ref, frags)
     path = str(tmp_path / "payloads.bin")
