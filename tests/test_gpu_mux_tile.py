@@ -89,6 +89,43 @@ def test_gpu_service_tile_matches_reference_tile(stream, reference_runs, tmp_pat
     assert_same_frags(reference_runs[(1, 0)], parse_out(out))
 
 
+@pytest.fixture(scope="module")
+def stream_30k(oracle, tmp_path_factory):
+    """30,000 frags of the same mix, and the reference tile's output on them"""
+    frags = [p for p in tile_workload(oracle, 30303, 30000) if len(p) <= MTU]
+    d = tmp_path_factory.mktemp("gmux30k")
+    path = str(d / "payloads.bin")
+    tile.write_payload_file(path, frags)
+    out = str(d / "ref.bin")
+    p = run_harness("verify", path, out, rr=(1, 0))
+    so, se = p.communicate(timeout=240)
+    assert p.returncode == 0, se[-2000:]
+    return path, frags, parse_out(out)
+
+
+@pytest.mark.parametrize("mode", [[], ["--zero-copy"]], ids=["host-parse", "zero-copy"])
+def test_gpu_service_tile_matches_reference_tile_at_scale(stream_30k, tmp_path, mode):
+    """30,000 frags (≈90,000 signatures) through the sandboxed tile under
+    fd_mux_tile and the GPU service (256-signature batches, the r16 form):
+    the reference tile's frags byte for byte and in order."""
+    path, frags, want = stream_30k
+    app = uuid.uuid4().hex[:10]
+    svc = start_service(app, 1, "--batch", "256", "--depth", "1024", *mode)
+    try:
+        out = str(tmp_path / "hip.bin")
+        p = run_harness("verify_hip", path, out, app=app, timeout=200)
+        so, se = p.communicate(timeout=240)
+        assert p.returncode == 0, se[-2000:]
+        rc, res, se2 = finish_service(svc)
+        assert rc == 0, se2[-2000:]
+    finally:
+        if svc.poll() is None:
+            svc.kill()
+        cleanup(app)
+    assert res["txns"] == [len(frags)]
+    assert_same_frags(want, parse_out(out))
+
+
 @pytest.mark.parametrize("mode", [["--zero-copy"], ["--zero-copy", "--links-per-thread", "3"],
                                   ["--links-per-thread", "2"], ["--zero-copy", "--cpus", "AFFINITY3"]],
                          ids=["zero-copy", "zero-copy-one-thread", "host-parse-two-per-thread", "zero-copy-pinned"])
