@@ -98,3 +98,14 @@ def test_c3_batch_single_msg_priority(oracle, codes):
     assert np.array_equal(got_sig[:len(want_sig)], want_sig)
     # every code class occurs
     assert {0, -1, -2, -3} <= set(np.unique(want_txn).tolist())
+    if codes == "avx512":
+        # the same transactions through the drop-in, one synchronous
+        # fd_ed25519_verify_batch_single_msg call each (the drop-in engines
+        # keep the AVX-512 backend's codes unless FD_ED25519_HIP_CODES says
+        # otherwise at their creation)
+        got_drop = np.array([ed25519.verify_batch_single_msg(bytes(msgs[t_off[t]:t_off[t] + t_sz[t]]),
+                                                              bytes(sigs[64 * first[t]:64 * (first[t] + cnt[t])]),
+                                                              bytes(pubs[32 * first[t]:32 * (first[t] + cnt[t])]))
+                             for t in range(len(cnt))], np.int8)
+        bad = np.nonzero(got_drop != want_txn)[0]
+        assert len(bad) == 0, [(int(t), int(cnt[t]), int(got_drop[t]), int(want_txn[t])) for t in bad[:10]]
