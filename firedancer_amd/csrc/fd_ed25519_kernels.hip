@@ -1246,8 +1246,10 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
     }
     uint32_t b = 0u;
     if (badd) b = btab16_r16(braw, k);
-    P = ge16_cneg4(P, k.r03, e < 0, k);
-    P = ge16_add2<true>(P, ce, e < 0, k);
+    if (e != 0) {   /* a zero digit (~1 in 16) adds the identity: skipped, the digit is wave-uniform */
+      P = ge16_cneg4(P, k.r03, e < 0, k);
+      P = ge16_add2<true>(P, ce, e < 0, k);
+    }
     if (badd) P = ge16_add2<true>(P, b, false, k);
   }
   /* wave 1's point as an addend of wave 0's */
