@@ -1049,6 +1049,7 @@ fd_ed25519_hip_verify_txns_host( fd_ed25519_hip_engine_t * e, unsigned long ntxn
 #define DROPIN_ENGINES   4
 #define DROPIN_BATCH_MAX 4096UL
 #define DROPIN_CHUNK     16384UL
+#define DROPIN_PENDING 0x55   /* a direct launch's codes before the kernels write them */
 #ifndef DROPIN_DIRECT_MAX
 #define DROPIN_DIRECT_MAX 64UL   /* launches of at most this many signatures read the pinned block in place */
 #endif
@@ -1234,6 +1235,7 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   if( need>dq.blk_cap[k] ) {
     uint64_t cap = dq.blk_cap[k] ? dq.blk_cap[k] : (1UL<<20);
     while( cap<need ) cap *= 2UL;
+    hipStreamSynchronize( e->stream );   /* a direct launch may still be ending (see below) */
     hipHostFree( dq.h_blk[k] ); hipFree( dq.d_blk[k] );
     dq.h_blk[k] = NULL; dq.h_dev[k] = NULL; dq.d_blk[k] = NULL; dq.blk_cap[k] = 0UL;
     HIPCHK( hipHostMalloc( (void **)&dq.h_blk[k], cap, hipHostMallocCoherent ), "hipHostMalloc(drop-in)" );
@@ -1284,6 +1286,7 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
      link. */
   int direct = nsig<=DROPIN_DIRECT_MAX && !multi;
   unsigned char * src = direct ? dq.h_dev[k] : d;
+  if( direct ) memset( h + o_out, DROPIN_PENDING, nsig );   /* no code is this value */
   fd_ed25519_pull_params_t pp;
   memset( &pp, 0, sizeof(pp) );
   if( !direct ) {
@@ -1306,7 +1309,35 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     pp.src[0] = d + o_out; pp.dst[0] = dq.h_dev[k] + o_out; pp.n[0] = multi ? nsig + n : nsig;
     HIPCHK( (hipError_t)fd_ed25519_hip_launch_pull( &pp, st ), "D2H drop-in" );
   }
-  HIPCHK( hipStreamSynchronize( st ), "drop-in verify" );
+  if( direct ) {
+    /* The codes land in the pinned block as the kernels write them: the
+       call returns when all are there, without waiting for the stream's
+       completion signal (the kernels read nothing of this block after
+       writing a code, and the engine's next launch is ordered behind
+       them on its stream).  The stream is queried every 64 polls, so a
+       failed launch still ends the wait with its error. */
+    volatile signed char const * c = (volatile signed char const *)(h + o_out);
+    for( unsigned long spin=1UL;; spin++ ) {
+      unsigned long i = 0UL;
+      while( i<nsig && c[ i ]!=(signed char)DROPIN_PENDING ) i++;
+      if( i==nsig ) break;
+      if( !(spin & 63UL) ) {
+        hipError_t q = hipStreamQuery( st );
+        if( q==hipErrorNotReady ) continue;
+        HIPCHK( q, "drop-in verify" );
+        /* the stream is done: every code must be there */
+        for( i=0UL; i<nsig && c[ i ]!=(signed char)DROPIN_PENDING; i++ ) ;
+        if( i<nsig ) {
+          snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf), "drop-in: a launch ended without a code" );
+          return FD_ED25519_HIP_ERR_HIP - (int)hipErrorLaunchFailure;
+        }
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+  } else {
+    HIPCHK( hipStreamSynchronize( st ), "drop-in verify" );
+  }
   signed char const * codes = (signed char const *)(h + o_out);
   signed char const * tcode = (signed char const *)(h + o_tout);
   t = 0UL;
