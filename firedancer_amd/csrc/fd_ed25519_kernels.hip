@@ -1264,6 +1264,13 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
   const uint64_t bal = __ballot(zero);
   const bool ident = (bal & 1ull) && (bal & (1ull << 16));
   if (code == FD_PENDING) code = ident ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  /* Write-code-last invariant: a signature's code is the last thing any
+     kernel of its launch does with that signature; no kernel reads the
+     inputs (or anything else in the drop-in's pinned block) after the code
+     is written.  The drop-in's direct launches return once every code has
+     landed in that block (host/fd_ed25519_hip_engine.c, dropin_run) and the
+     next call restages it; a kernel added after dsm16 that reads the block
+     would break that silently. */
   if (threadIdx.x == 0u) p.out[p.base + j] = (int8_t)code;
 }
 
@@ -1389,6 +1396,7 @@ FD_DEV void hash16_block(const fd_ed25519_verify_params_t& p, uint64_t* sched) {
     else if (dr.small) code = FD_ED25519_ERR_SIG;
     int4* tabA = reinterpret_cast<int4*>(static_cast<char*>(p.atab) + (j >> 6) * FD_ED25519_ATAB_BYTES_PER_WAVE) +
                  (j & 63u) * (2 * FD_ED25519_ATAB_STRIDE * 10);
+    /* the code last: see the write-code-last invariant at dsm16's end */
     p.out[p.base + j] = (int8_t)dsm_full_core(p, j, tabA, code, da.x, da.y, dr.x, dr.y);
   }
 #endif

@@ -1053,6 +1053,13 @@ fd_ed25519_hip_verify_txns_host( fd_ed25519_hip_engine_t * e, unsigned long ntxn
 #ifndef DROPIN_DIRECT_MAX
 #define DROPIN_DIRECT_MAX 64UL   /* launches of at most this many signatures read the pinned block in place */
 #endif
+/* ... and of at most this many input bytes: the hash kernels read a direct
+   launch's messages word by word over the link from uncached coherent
+   pinned memory, which pays for a few hundred bytes but not for a
+   multi-MB message (one bulk pull into HBM first is faster there). */
+#ifndef DROPIN_DIRECT_MAX_BYTES
+#define DROPIN_DIRECT_MAX_BYTES 65536UL
+#endif
 
 typedef struct dropin_req {
   unsigned char const * msg;
@@ -1095,6 +1102,7 @@ static struct {
   unsigned char *           h_dev[ DROPIN_ENGINES ];   /* h_blk as the device sees it */
   unsigned char *           d_blk[ DROPIN_ENGINES ];
   uint64_t                  blk_cap[ DROPIN_ENGINES ];
+  int                       direct_pending[ DROPIN_ENGINES ];   /* last launch returned before its stream ended */
   dropin_req_t *            head;
   dropin_req_t *            tail;
   unsigned long             launches, requests;   /* for fd_ed25519_hip_dropin_stats */
@@ -1120,6 +1128,7 @@ dropin_engine_make( int k ) {
   if( dq.eng[k] ) { fd_ed25519_hip_engine_delete( dq.eng[k] ); dq.eng[k] = NULL; }
   hipHostFree( dq.h_blk[k] ); hipFree( dq.d_blk[k] );
   dq.h_blk[k] = NULL; dq.h_dev[k] = NULL; dq.d_blk[k] = NULL; dq.blk_cap[k] = 0UL;
+  dq.direct_pending[k] = 0;
   dq.eng[k] = fd_ed25519_hip_engine_new( dq.device, DROPIN_CHUNK, dq.flags );
   return dq.eng[k] ? FD_ED25519_HIP_OK : FD_ED25519_HIP_ERR_INVAL;
 }
@@ -1211,6 +1220,21 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     return FD_ED25519_HIP_ERR_INVAL;
   }
   HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  /* A direct launch returned when its codes landed, before its stream's
+     completion signal (below): an error raised after that (a wave faulting
+     on its way out) surfaces here, before this launch restages the block.
+     It is reported as the earlier launch's, and this launch then runs on a
+     re-created engine (dropin_retry). */
+  if( dq.direct_pending[k] ) {
+    dq.direct_pending[k] = 0;
+    hipError_t q = hipStreamQuery( e->stream );
+    if( q!=hipSuccess && q!=hipErrorNotReady ) {
+      snprintf( fd_ed25519_hip_errbuf, sizeof(fd_ed25519_hip_errbuf),
+                "drop-in: engine %d's previous direct launch ended with %s after its codes landed", k,
+                hipGetErrorString( q ) );
+      return FD_ED25519_HIP_ERR_HIP - (int)q;
+    }
+  }
   /* signatures of requests hashed on the host go after the others: the
      device hashes [0, nsig_m), takes digests for [nsig_m, nsig) */
   uint64_t nsig = 0UL, nsig_h = 0UL, bytes = 0UL;
@@ -1284,7 +1308,7 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
      several drop-in engines submit from their callers' threads at once
      (DESIGN.md 3c), and one bulk read beats every lane reading over the
      link. */
-  int direct = nsig<=DROPIN_DIRECT_MAX && !multi;
+  int direct = nsig<=DROPIN_DIRECT_MAX && !multi && in_sz<=DROPIN_DIRECT_MAX_BYTES;
   unsigned char * src = direct ? dq.h_dev[k] : d;
   if( direct ) memset( h + o_out, DROPIN_PENDING, nsig );   /* no code is this value */
   fd_ed25519_pull_params_t pp;
@@ -1335,6 +1359,7 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
       }
       __builtin_ia32_pause();
     }
+    dq.direct_pending[k] = 1;
   } else {
     HIPCHK( hipStreamSynchronize( st ), "drop-in verify" );
   }

@@ -157,7 +157,12 @@ shlink_reclaim( char const * name ) {
   if( !flock( fd, LOCK_EX | LOCK_NB ) && !fstat( fd, &st ) && (size_t)st.st_size>=sizeof(shlink_hdr_t) ) {
     void * m = mmap( NULL, sizeof(shlink_hdr_t), PROT_READ, MAP_SHARED, fd, 0 );
     if( m!=MAP_FAILED ) {
-      int ours = ((shlink_hdr_t const *)m)->magic==SHLINK_MAGIC;   /* a half-made object is its creator's, locked */
+      shlink_hdr_t const * h = (shlink_hdr_t const *)m;
+      int ours = h->magic==SHLINK_MAGIC;   /* a half-made object is its creator's, locked */
+      /* A creator of protocol 5 held no flock: for its links the free lock
+         says nothing, and only a creator pid that no longer exists does. */
+      if( ours && h->proto<FD_ED25519_HIP_SHLINK_PROTO &&
+          ( !h->creator || !kill( (pid_t)h->creator, 0 ) || errno!=ESRCH ) ) ours = 0;
       munmap( m, sizeof(shlink_hdr_t) );
       char path[ 160 ];
       struct stat now;

@@ -548,7 +548,7 @@ _lib.fd_ed25519_hip_vservice_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes
                                              ctypes.POINTER(VServiceStats)]
 # the library and these ctypes mirrors must describe the same ABI
 _lib.fd_ed25519_hip_abi_check.argtypes = [ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong]
-ABI_VERSION = 8   # FD_ED25519_HIP_ABI_VERSION
+ABI_VERSION = 9   # FD_ED25519_HIP_ABI_VERSION
 if _lib.fd_ed25519_hip_abi_check(ABI_VERSION, ctypes.sizeof(Slot), ctypes.sizeof(__import__(
         "firedancer_amd.ed25519", fromlist=["_Info"])._Info), ctypes.sizeof(VServiceStats)) != 0:
     raise ImportError("libfd_ed25519_hip ABI mismatch: " + _lib.fd_ed25519_hip_last_error().decode())
@@ -561,7 +561,7 @@ _lib.fd_ed25519_hip_shlink_status.restype = ctypes.c_int
 SHLINK_FAIL_PROTOCOL = -100
 SHLINK_FAIL_STOPPED = -101
 SHLINK_FAIL_TILE_GONE = -102
-SHLINK_PROTO = 5          # FD_ED25519_HIP_SHLINK_PROTO
+SHLINK_PROTO = 6          # FD_ED25519_HIP_SHLINK_PROTO
 
 
 class ShLinkWatch(ctypes.Structure):

@@ -134,7 +134,17 @@ fd_ed25519_hip_dropin_device_bytes( void );
    re-created engine in *recoveries (optional).  dropin_reset waits for the
    launches in flight, deletes and re-creates every drop-in engine and, if
    that succeeds, makes the drop-ins usable again: 0, or the creation's
-   error code (still lost). */
+   error code (still lost).
+
+   What a retry or a reset can recover: a failure that leaves the HIP
+   context usable (an allocation or a launch refused, a queue that could
+   not be made, an error the library raised itself).  A device fault inside
+   a kernel (an illegal address, a memory violation, a hardware exception)
+   is sticky on ROCm: the process's context stays failed, so the retry
+   fails too, the device is lost, and dropin_reset keeps returning the
+   context's error code.  Only a process restart recovers from that, and a
+   caller that sees dropin_reset fail should restart the process (the
+   ABORT policy's default does exactly that, by ending it). */
 #define FD_ED25519_HIP_DROPIN_ON_LOST_ABORT  (0)
 #define FD_ED25519_HIP_DROPIN_ON_LOST_REJECT (1)
 
@@ -159,13 +169,14 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    payload; 5: shlink protocol word and creator, vservice lifecycle and
    end codes; 6: vservice links_per_thread; 7: vservice link_cpus; 8:
    vservice stats' leaked_on_hang, the drop-ins' device-lost state, the
-   dsm16 form and its flag).  A consumer checks
+   dsm16 form and its flag; 9: shlink protocol 6, flock-owned links).  A
+   consumer checks
    the library it loaded against the header it was built with:
    fd_ed25519_hip_abi_check( FD_ED25519_HIP_ABI_VERSION,
    sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
    sizeof(fd_ed25519_hip_vservice_stats_t) ) returns 0 when they agree,
    FD_ED25519_HIP_ERR_INVAL (with fd_ed25519_hip_last_error) when not. */
-#define FD_ED25519_HIP_ABI_VERSION (8U)
+#define FD_ED25519_HIP_ABI_VERSION (9U)
 
 unsigned
 fd_ed25519_hip_abi_version( void );

@@ -350,8 +350,11 @@ typedef struct fd_ed25519_hip_shlink fd_ed25519_hip_shlink_t;
 
 /* The verdict frag protocol and link layout a link speaks, recorded in its
    header by create and checked by join (1-4: earlier layouts without the
-   word; 5: trailer-only SUCCESS verdicts, below, and the creator's pid). */
-#define FD_ED25519_HIP_SHLINK_PROTO (5UL)
+   word; 5: trailer-only SUCCESS verdicts, below, and the creator's pid;
+   6: the creator holds a flock on the object for its lifetime, and a link
+   whose lock can be taken is reclaimable -- a protocol-5 link only when
+   its creator pid is gone, since its creator held no lock). */
+#define FD_ED25519_HIP_SHLINK_PROTO (6UL)
 
 /* the largest frag either direction carries (a verdict frag is smaller
    than this: 1 verdict byte + at most FD_ED25519_HIP_TXN_MAX_SZ + 2) */

@@ -84,3 +84,8 @@ def halfsize():
 @pytest.fixture(scope="session")
 def longd():
     return load_golden("longd")
+
+
+@pytest.fixture(scope="session")
+def mixed_order():
+    return load_golden("mixed_order")

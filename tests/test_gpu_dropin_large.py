@@ -111,3 +111,26 @@ def test_message_past_4gib_is_verified_whole(ed, oracle):
         m.close()
     assert (got_ok, got_bad) == (want_ok, want_bad) == (0, -3)
     assert got_batch == -3
+
+
+@pytest.mark.parametrize("sz", [65536 - 400, 65536 - 160, 65536 - 159, 1 << 20, 8 << 20],
+                         ids=["below-direct-limit", "at-direct-limit", "past-direct-limit", "1MiB", "8MiB"])
+def test_device_hashed_large_message_dropin(ed, oracle, sz):
+    """MB-scale messages stay on the device hash (below the 4 GiB host-hash
+    limit): a launch whose staged block is at most 64 KiB reads it in place
+    over the link (the direct path), a larger one is pulled into HBM first
+    (ADVICE r5).  The sizes straddle that limit (a one-signature block is
+    160 bytes of offsets, sizes, signature and key, then the message);
+    valid verifies, a flipped last byte gives ERR_MSG."""
+    ed25519, lib = ed
+    lib.fd_ed25519_hip_dropin_set_host_hash_min(0)
+    rng = np.random.default_rng(sz)
+    m = bytearray(rng.integers(0, 256, sz, dtype=np.uint8).tobytes())
+    priv = bytes(rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+    pub, sig = ctypes.create_string_buffer(32), ctypes.create_string_buffer(64)
+    oracle.oracle_ed25519_public_from_private(pub, priv)
+    oracle.oracle_ed25519_sign(sig, bytes(m), sz, pub.raw, priv)
+    assert ed25519.verify(bytes(m), sig.raw, pub.raw) == 0
+    m[-1] ^= 1
+    assert ed25519.verify(bytes(m), sig.raw, pub.raw) == -3
+    assert oracle.oracle_ed25519_verify(bytes(m), sz, sig.raw, pub.raw, 0) == -3

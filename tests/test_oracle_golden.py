@@ -105,3 +105,26 @@ def test_halfsize_fallback_codes(oracle, halfsize, codes, key):
     got = oracle_many(oracle, halfsize, codes)
     bad = np.nonzero(got != halfsize[key])[0]
     assert len(bad) == 0, [(str(halfsize["tags"][i]), int(got[i]), int(halfsize[key][i])) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("codes,key", [(0, "codes_avx512"), (1, "codes_portable")])
+def test_mixed_order_codes(oracle, mixed_order, codes, key):
+    """A and R carrying an 8-torsion component (gen_mixed.py): accepted only
+    when it cancels in the cofactorless equation; 10,240 signatures."""
+    d = mixed_order
+    got = oracle_many(oracle, d, codes)
+    bad = np.nonzero(got != d[key])[0]
+    assert len(bad) == 0, [(str(d["tags"][i]), int(got[i]), int(d[key][i])) for i in bad[:10]]
+    assert int((d[key] == 0).sum()) >= 1000 and len(got) >= 10000
+
+
+@pytest.mark.parametrize("codes,key", [(0, "b_codes_avx512"), (1, "b_codes_portable")])
+def test_mixed_order_batch_codes(oracle, mixed_order, codes, key):
+    d = mixed_order
+    for t in range(len(d["b_txn_cnt"])):
+        off, sz = int(d["b_txn_msg_off"][t]), int(d["b_txn_msg_sz"][t])
+        f, n = int(d["b_txn_first"][t]), int(d["b_txn_cnt"][t])
+        got = oracle.oracle_ed25519_verify_batch_single_msg(bytes(d["b_msgs"][off:off + sz]), sz,
+                                                            d["b_sigs"][f:f + n].tobytes(),
+                                                            d["b_pubs"][f:f + n].tobytes(), n, codes)
+        assert got == int(d[key][t]), (t, str(d["b_tags"][t]), got, int(d[key][t]))

@@ -414,3 +414,28 @@ def test_a_live_creators_link_is_not_reclaimed_whatever_its_pid_says():
     assert not os.path.exists("/dev/shm" + name)
     again = tile.ShLink(name, 64, create=True)
     again.close()
+
+
+def test_protocol5_link_reclaimed_only_when_its_creator_is_gone():
+    """A protocol-5 creator held no flock on its link, so a free lock on such
+    a link does not mean its creator exited: create reclaims it only when
+    the recorded creator pid no longer exists."""
+    import struct
+    name = f"/fdt_p5_{uuid.uuid4().hex[:12]}"
+    path = "/dev/shm" + name
+    hdr = bytearray(4096)
+    struct.pack_into("<QQQQ", hdr, 0, 0xfd25519517a4c0df, 64, 128, 1232)
+    struct.pack_into("<QQ", hdr, SHLINK_HDR_PROTO_OFF, 5, os.getpid())   # a live creator, no lock held
+    with open(path, "wb") as f:
+        f.write(hdr)
+    try:
+        with pytest.raises(tile.HipError, match="EEXIST"):
+            tile.ShLink(name, 64, create=True)
+        assert os.path.exists(path)
+        _hdr_word(name, SHLINK_HDR_CREATOR_OFF, (1 << 31) - 7)   # no such process in this namespace
+        link = tile.ShLink(name, 64, create=True)
+        assert _hdr_word(name, SHLINK_HDR_PROTO_OFF) == tile.SHLINK_PROTO == 6
+        link.close()
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
