@@ -87,6 +87,39 @@ static __thread unsigned long long pf_sub_h2d, pf_sub_launch, pf_sub_d2h, pf_sub
 #define PF_SUB( acc, stmt ) do { stmt; } while(0)
 #endif
 
+#ifdef FD_ED25519_HIP_AB_STAGE_TRACE
+/* A/B build only (tools/stage_trace_probe.py): per batch, the host time of
+   each stage of its round trip -- submit entered, last launch enqueued,
+   poll saw it done, its records resolved -- and the slots in flight when
+   it went out; per frag of a latency run, when the producer actually
+   published it and when the tile pulled it.  Read with
+   fd_ed25519_hip_stage_trace_read. */
+#define STAGE_TRACE_MAX (1UL<<18)
+typedef struct {
+  double t_submit, t_enq, t_done, t_resolved;
+  double seq, sig_cnt, txn_cnt, in_flight;
+} stage_rec_t;
+static stage_rec_t   stage_rec[ STAGE_TRACE_MAX ];
+static unsigned long stage_cnt;
+static double *        stage_frag_due;    /* per frag: its due time (latency counts from here) */
+static double *        stage_frag_pub;    /* per frag: producer's publish time   */
+static double *        stage_frag_pull;   /* per frag: the tile's pull time      */
+static unsigned long * stage_frag_batch;  /* per frag: the batch (pipe seq) it went into */
+
+void
+fd_ed25519_hip_stage_trace_frags( double * t_due, double * t_pub, double * t_pull, unsigned long * batch ) {
+  stage_frag_due = t_due; stage_frag_pub = t_pub; stage_frag_pull = t_pull; stage_frag_batch = batch;
+}
+
+unsigned long
+fd_ed25519_hip_stage_trace_read( double * out, unsigned long max, int reset ) {
+  unsigned long n = stage_cnt < max ? stage_cnt : max;
+  memcpy( out, stage_rec, n*sizeof(stage_rec_t) );
+  if( reset ) stage_cnt = 0UL;
+  return n;
+}
+#endif
+
 /* May a partial batch (the input drained before the batch filled) go out
    with in_flight batches already on the GPU?  Only while a slot stays free
    for a full one, and only while fewer than VTILE_PARTIAL_MAX are in
@@ -115,6 +148,10 @@ typedef struct {
   hipEvent_t                ev;
   hipEvent_t                ev_h2d;    /* the slot's batch has crossed the link */
   int                       state;
+#ifdef FD_ED25519_HIP_AB_STAGE_TRACE
+  double                    t_enq;         /* the batch's last launch enqueued */
+  unsigned                  in_flight0;    /* batches in flight when it went out */
+#endif
   /* staging: the public host arrays live in one pinned block laid out as
      [sigs | pubs | msg_off | msg_sz | txn_first | txn_sig_cnt | msgs], its
      device mirror has the same layout, so a batch goes over in one copy;
@@ -457,6 +494,9 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   pf_sub_n++;
 #endif
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
+#ifdef FD_ED25519_HIP_AB_STAGE_TRACE
+  s->t_enq = now_s(); s->in_flight0 = pipe->in_flight;
+#endif
   s->state = SLOT_BUSY;
   pipe->in_flight++;
   return FD_ED25519_HIP_OK;
@@ -518,6 +558,9 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
 #endif
   }
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
+#ifdef FD_ED25519_HIP_AB_STAGE_TRACE
+  s->t_enq = now_s(); s->in_flight0 = pipe->in_flight;
+#endif
   s->state = SLOT_BUSY;
   pipe->in_flight++;
   return FD_ED25519_HIP_OK;
@@ -1002,6 +1045,15 @@ vt_drain_one( fd_ed25519_hip_vtile_t * vt, int wait ) {
   { double rt = s->t_done - s->t_submit; vt_rtt_s += rt; vt_rtt_n++; if( rt>vt_rtt_max_s ) vt_rtt_max_s = rt; }
 #endif
   vt_resolve( vt, s );
+#ifdef FD_ED25519_HIP_AB_STAGE_TRACE
+  if( stage_cnt<STAGE_TRACE_MAX ) {
+    pipe_slot_t const * ps = (pipe_slot_t const *)s;
+    stage_rec_t * r = &stage_rec[ stage_cnt++ ];
+    r->t_submit = s->t_submit; r->t_enq = ps->t_enq; r->t_done = s->t_done; r->t_resolved = now_s();
+    r->seq = (double)s->seq; r->sig_cnt = (double)s->sig_cnt; r->txn_cnt = (double)s->txn_cnt;
+    r->in_flight = (double)ps->in_flight0;
+  }
+#endif
   fd_ed25519_hip_pipe_release( vt->pipe, s );
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
   vt_resolve_cycles += __rdtsc() - w1;
@@ -1427,6 +1479,9 @@ producer_main( void * arg ) {
     m->sig = i; m->chunk = (uint32_t)chunk; m->sz = (uint16_t)sz; m->ctl = 0; m->tsorig = 0; m->tspub = 0;
     pr->t_pub[ i ] = due;
     atomic_store_explicit( &m->seq, i, memory_order_release );
+#ifdef FD_ED25519_HIP_AB_STAGE_TRACE
+    if( stage_frag_pub ) { stage_frag_pub[ i ] = now_s(); stage_frag_due[ i ] = due; }
+#endif
     chunk += nch;
   }
   return NULL;
@@ -1507,6 +1562,12 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
       }
       if( sz && buf[0]<=16U ) sigs += buf[0];
       fd_ed25519_hip_vtile_frag( vt, buf, sz, cookie );
+#ifdef FD_ED25519_HIP_AB_STAGE_TRACE
+      if( stage_frag_pull ) {
+        stage_frag_pull [ next ] = now_s();
+        stage_frag_batch[ next ] = vt->open ? vt->open_seq : vt->pipe->seq - 1UL;
+      }
+#endif
       next++;
       atomic_store_explicit( &pr.consumed, next, memory_order_release );
       pulled = 1;
