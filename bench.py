@@ -354,6 +354,13 @@ def latency_mode(eng, args, device):
     n = args.latency_txns
     pay, _ = workload.txn_payloads(eng, n, args.seed + 77, msg_sz=200)
     ok = True
+    # the producer and the tile each on a physical core of its own on the
+    # GPU's node, as fdctl pins tiles: floating, the two threads can share a
+    # core (SMT siblings, or other work), and the tile's per-frag rate then
+    # varied run to run by 1.6x (profiles/r6_c5_stage_trace.txt)
+    cores = tile.physical_cores(tile.device_cpus(eng.info()))
+    if args.pin_threads and len(cores) >= 2:
+        tile.latency_set_cpus(cores[0], cores[1])
 
     def run_at(rate):
         nonlocal ok
@@ -362,13 +369,24 @@ def latency_mode(eng, args, device):
         ok &= bool((v == 0).all())
         return res["achieved_txn_per_s"]
 
+    try:
+        return latency_mode_loads(args, run_at, pay, n, device, lambda: ok,
+                                  cores[:2] if args.pin_threads and len(cores) >= 2 else None)
+    finally:
+        tile.latency_set_cpus(-1, -1)
+
+
+def latency_mode_loads(args, run_at, pay, n, device, verdicts_ok, cpus):
+    from firedancer_amd import tile
     unpaced = [run_at(0.0) for _ in range(3)]
     peak, trail = sustained_rate(run_at, float(np.median(unpaced)))
     out = {"batch_sigs": args.latency_batch, "slots_in_flight": args.latency_slots,
+           "threads": (f"producer on CPU {cpus[0]}, tile on CPU {cpus[1]} (physical cores of the GPU's node)"
+                       if cpus else "unpinned"),
            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES") or 4), "txns_per_run": n,
            "msg_sz": 200, "peak_txn_per_s": peak, "peak": SUSTAINED_PEAK, "peak_search": trail,
            "unpaced_median_txn_per_s": float(np.median(unpaced)), "unpaced_runs_txn_per_s": unpaced,
-           "ring": "tango-style mcache/dcache, depth 4096", "verdicts_ok": ok, "loads": []}
+           "ring": "tango-style mcache/dcache, depth 4096", "verdicts_ok": verdicts_ok(), "loads": []}
     # each load five times; p50 / p99 / max are over every transaction of
     # the five runs pooled (a run is ~0.05-0.1 s, so one host hiccup of a
     # few milliseconds is its whole p99: pooling keeps such events in the
@@ -435,6 +453,13 @@ def latency_deployed(eng, args):
     # the service and the tile's harness on the CPUs of the GPU's NUMA node,
     # as fdctl pins its tiles (tools/service_bench.py does the same)
     node = sorted(tile.device_cpus(eng.info()))
+    # and each spinning thread on a physical core of its own (the harness's
+    # producer, consumer and tile; the service's link thread), as fdctl pins
+    # one tile per core
+    cores = tile.physical_cores(node)
+    per_thread = args.pin_threads and len(cores) >= 4
+    harness_cpus = ["--cpus", ",".join(map(str, cores[:3]))] if per_thread else []
+    service_cpus = ["--cpus", str(cores[3])] if per_thread else []
 
     def pin():
         if node:
@@ -447,7 +472,7 @@ def latency_deployed(eng, args):
         if kind == "verify_hip":
             svc = subprocess.Popen([svc_bin, "--prefix", f"/fd_vhip_{app}_", "--tiles", "1", "--batch",
                                     str(args.latency_batch), "--slots", str(args.deployed_slots),
-                                    "--hw-queues", str(max(4, args.deployed_slots)), *svc_mode],
+                                    "--hw-queues", str(max(4, args.deployed_slots)), *svc_mode, *service_cpus],
                                    stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, preexec_fn=pin)
             line = svc.stdout.readline()
             if not line.startswith("ready"):
@@ -457,7 +482,8 @@ def latency_deployed(eng, args):
             pay_path = pay_path or (path if kind == "verify_hip" else path_ref)
             p = subprocess.run([mux, kind, pay_path, os.path.join(tmp, "out.bin"),
                                 "--app", app, "--depth", "16384", "--rate", str(rate), "--timeout", "100",
-                                "--log-path", "", "--lat-out", lat_path], capture_output=True, text=True, timeout=150,
+                                "--log-path", "", "--lat-out", lat_path, *harness_cpus], capture_output=True, text=True,
+                               timeout=150,
                                preexec_fn=pin)
             if p.returncode != 0:
                 raise RuntimeError(f"harness {kind} rc {p.returncode}: {p.stderr[-500:]}")
@@ -541,6 +567,8 @@ def latency_deployed(eng, args):
     hip.update({"batch_sigs": args.latency_batch, "slots_in_flight": args.deployed_slots,
                 "hw_queues": max(4, args.deployed_slots),
                 "cpus": f"{len(node)} CPUs of the GPU's NUMA node (service and harness pinned)" if node else "unpinned",
+                "threads": (f"harness producer / consumer / tile on CPUs {cores[:3]}, service link thread on CPU "
+                            f"{cores[3]} (physical cores)" if per_thread else "not pinned per thread"),
                 "service_mode": args.deployed_mode, "msg_sz": 200,
                 "path": "producer -> quic_verify mcache/dcache (reference tango) -> fd_tile_verify_hip under the "
                         "reference's fd_mux_tile, its seccomp filter installed -> shlink -> fd_verify_hip_service "
@@ -944,6 +972,8 @@ def main():
                     help="GPU_MAX_HW_QUEUES of this process (HIP's default is 4), set before its first HIP call "
                          "unless the environment names more; 0 leaves it")
     ap.add_argument("--latency-txns", type=int, default=400000, help="0 disables the latency mode")
+    ap.add_argument("--no-pin-threads", dest="pin_threads", action="store_false",
+                    help="C5 legs: leave the producer / tile / service threads unpinned (A/B)")
     ap.add_argument("--deployed-txns", type=int, default=300000,
                     help="C5 on the deployed path (the tile under fd_mux_tile + the GPU service): txns per run, "
                          "0 disables")

@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #ifdef FD_ED25519_HIP_AB_SERVICE_PROFILE
 #include <x86intrin.h>
@@ -1446,12 +1447,36 @@ typedef struct {
   _Atomic int           stop;       /* the consumer gave up (its vtile failed) */
   _Atomic uint64_t      consumed;   /* frags the consumer has taken (credits) */
   double                t0;
+  int                   cpu;        /* pinned to this CPU (-1: not pinned) */
 } producer_t;
+
+/* CPUs for latency_run's producer and tile threads (-1: unpinned):
+   fd_ed25519_hip_latency_set_cpus */
+static int lat_cpu_prod = -1, lat_cpu_tile = -1;
+
+static int
+pin_self( int cpu ) {
+  if( cpu<0 ) return 0;
+  cpu_set_t set;
+  CPU_ZERO( &set );
+  CPU_SET( cpu, &set );
+  return pthread_setaffinity_np( pthread_self(), sizeof(set), &set );
+}
+
+int
+fd_ed25519_hip_latency_set_cpus( int producer_cpu, int tile_cpu ) {
+  if( producer_cpu>=CPU_SETSIZE || tile_cpu>=CPU_SETSIZE || ( producer_cpu>=0 && producer_cpu==tile_cpu ) )
+    return FD_ED25519_HIP_ERR_INVAL;
+  lat_cpu_prod = producer_cpu < 0 ? -1 : producer_cpu;
+  lat_cpu_tile = tile_cpu < 0 ? -1 : tile_cpu;
+  return FD_ED25519_HIP_OK;
+}
 
 static void *
 producer_main( void * arg ) {
   producer_t * pr = (producer_t *)arg;
   ring_t * rg = pr->ring;
+  pin_self( pr->cpu );
   while( !atomic_load_explicit( &pr->go, memory_order_acquire ) ) {}
   unsigned long chunk = 0UL;
   double t0 = now_s();
@@ -1487,12 +1512,34 @@ producer_main( void * arg ) {
   return NULL;
 }
 
+static int
+latency_run( int device, unsigned slot_cnt, unsigned long batch_sigs, unsigned char const * payloads,
+             unsigned long const * payload_off, unsigned int const * payload_sz, unsigned long txn_cnt,
+             double offered_txn_per_s, unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
+             fd_ed25519_hip_latency_result_t * res, int cpu_prod );
+
+/* One tile: the calling thread is the tile, pinned for the run when
+   fd_ed25519_hip_latency_set_cpus named a CPU (its affinity restored after). */
 int
 fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_sigs,
                             unsigned char const * payloads, unsigned long const * payload_off,
                             unsigned int const * payload_sz, unsigned long txn_cnt, double offered_txn_per_s,
                             unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
                             fd_ed25519_hip_latency_result_t * res ) {
+  cpu_set_t saved;
+  int restore = lat_cpu_tile>=0 && !pthread_getaffinity_np( pthread_self(), sizeof(saved), &saved );
+  if( restore && pin_self( lat_cpu_tile ) ) restore = 0;
+  int err = latency_run( device, slot_cnt, batch_sigs, payloads, payload_off, payload_sz, txn_cnt, offered_txn_per_s,
+                         ring_depth, flags, lat_s, verdict, res, lat_cpu_prod );
+  if( restore ) pthread_setaffinity_np( pthread_self(), sizeof(saved), &saved );
+  return err;
+}
+
+static int
+latency_run( int device, unsigned slot_cnt, unsigned long batch_sigs, unsigned char const * payloads,
+             unsigned long const * payload_off, unsigned int const * payload_sz, unsigned long txn_cnt,
+             double offered_txn_per_s, unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
+             fd_ed25519_hip_latency_result_t * res, int cpu_prod ) {
   if( !txn_cnt || !ring_depth || (ring_depth & (ring_depth-1UL)) || !lat_s || !verdict || !res )
     return FD_ED25519_HIP_ERR_INVAL;
   for( unsigned long i=0UL; i<txn_cnt; i++ )
@@ -1528,7 +1575,7 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
   producer_t pr;
   memset( &pr, 0, sizeof(pr) );
   pr.ring = &rg; pr.payloads = payloads; pr.off = payload_off; pr.sz = payload_sz; pr.n = txn_cnt;
-  pr.rate = offered_txn_per_s; pr.t_pub = t_pub;
+  pr.rate = offered_txn_per_s; pr.t_pub = t_pub; pr.cpu = cpu_prod;
   pthread_t th;
   if( pthread_create( &th, NULL, producer_main, &pr ) ) {
     free( rg.mcache ); free( rg.dcache ); free( t_pub ); free( ck ); free( vd ); free( buf );
@@ -1628,8 +1675,8 @@ typedef struct {
 static void *
 tile_main( void * arg ) {
   tile_job_t * j = (tile_job_t *)arg;
-  j->err = fd_ed25519_hip_latency_run( j->device, j->slot_cnt, j->batch_sigs, j->payloads, j->off, j->sz, j->n, j->rate,
-                                       j->ring_depth, j->flags, j->lat, j->verdict, &j->res );
+  j->err = latency_run( j->device, j->slot_cnt, j->batch_sigs, j->payloads, j->off, j->sz, j->n, j->rate,
+                       j->ring_depth, j->flags, j->lat, j->verdict, &j->res, -1 );
   if( j->err ) snprintf( j->errmsg, sizeof(j->errmsg), "%s", fd_ed25519_hip_last_error() );
   return NULL;
 }

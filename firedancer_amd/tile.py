@@ -312,6 +312,30 @@ def pack_payloads(payloads):
     return buf, off, sz
 
 
+_lib.fd_ed25519_hip_latency_set_cpus.argtypes = [ctypes.c_int, ctypes.c_int]
+
+
+def latency_set_cpus(producer_cpu=-1, tile_cpu=-1):
+    """fd_ed25519_hip_latency_set_cpus: pin latency_run's producer and tile
+    threads (one tile) to these CPUs for each run; -1 leaves one unpinned."""
+    _check(_lib.fd_ed25519_hip_latency_set_cpus(int(producer_cpu), int(tile_cpu)))
+
+
+def physical_cores(cpus):
+    """one logical CPU per physical core among cpus (the lowest SMT
+    sibling), in order"""
+    out, seen = [], set()
+    for c in sorted(cpus):
+        try:
+            sib = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+        except OSError:
+            sib = str(c)
+        if sib not in seen:
+            seen.add(sib)
+            out.append(c)
+    return out
+
+
 def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=256, ring_depth=4096, gpu_parse=False,
                 tiles=1):
     """Latency mode (C5): a producer thread publishes the payloads into a

@@ -315,6 +315,16 @@ fd_ed25519_hip_latency_run( int device, unsigned slot_cnt, unsigned long batch_s
                             unsigned long ring_depth, int flags, double * lat_s, signed char * verdict,
                             fd_ed25519_hip_latency_result_t * res );
 
+/* Pins fd_ed25519_hip_latency_run's producer thread to producer_cpu and
+   its tile (the calling thread, for the run; its affinity restored after)
+   to tile_cpu, as fdctl pins each tile to a core of its own; -1 leaves a
+   thread unpinned (the default).  Both on one CPU is refused
+   (FD_ED25519_HIP_ERR_INVAL).  Threads that float can land on the two SMT
+   siblings of one core, or share a core with other work, and the tile's
+   per-frag rate then varies run to run. */
+int
+fd_ed25519_hip_latency_set_cpus( int producer_cpu, int tile_cpu );
+
 /* Several verify tiles on one GPU (the reference runs
    verify_tile_count of them, src/app/fdctl/config/default.toml:535, frag
    seq going to tile seq % count, src/app/fdctl/run/tiles/fd_verify.c:46):

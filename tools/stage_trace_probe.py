@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--slots", type=int, default=8)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--slow-ms", type=float, default=0.45)
+    ap.add_argument("--pin", action="store_true", help="producer and tile on two physical cores of the GPU's node")
     ap.add_argument("--lib", default=os.path.join(REPO, "build", "variants", "stagetrace", "libfd_ed25519_hip.so"))
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "stage"))
     args = ap.parse_args()
@@ -56,6 +57,10 @@ def main():
     lib.fd_ed25519_hip_stage_trace_read.restype = ctypes.c_ulong
     os.makedirs(args.out, exist_ok=True)
     eng = ed25519.Engine(0, max_chunk=1 << 16)
+    if args.pin:
+        cores = tile.physical_cores(tile.device_cpus(eng.info()))
+        tile.latency_set_cpus(cores[0], cores[1])
+        print("pinned producer / tile to CPUs", cores[:2], flush=True)
     n = args.txns
     pay, _ = workload.txn_payloads(eng, n, 4242, msg_sz=200)
     eng.close()
@@ -79,7 +84,7 @@ def main():
         peaks = [run(0.0)["res"]["achieved_txn_per_s"] for _ in range(3)]
         rate = args.frac * float(np.median(peaks))
         print(f"unpaced peaks {[round(p / 1e6, 3) for p in peaks]} M -> offered {rate / 1e6:.3f} M", flush=True)
-    summary = {"offered_txn_per_s": rate, "runs": []}
+    summary = {"offered_txn_per_s": rate, "pinned": args.pin, "runs": []}
     for k in range(args.runs):
         r = run(rate)
         b = r["batches"]   # t_submit, t_enq, t_done, t_resolved, seq, sig_cnt, txn_cnt, in_flight
@@ -97,6 +102,8 @@ def main():
         rec = {"achieved_txn_per_s": r["res"]["achieved_txn_per_s"], "p50_ms": float(np.percentile(ms, 50)),
                "p99_ms": float(np.percentile(ms, 99)), "max_ms": float(ms.max()), "slow_frags": int(slow.sum()),
                "batches": int(len(b)), "mean_batch_txns": float(b[:, 6].mean()),
+               "in_flight_at_submit_hist": np.bincount(b[:, 7].astype(int), minlength=9).tolist(),
+               "tile_ns_per_frag_p50": float(np.median(np.diff(r["pull"])) * 1e9),
                "parts_ms_typical": dict(zip(PARTS, np.round(parts[~slow & ok].mean(0), 4).tolist())),
                "parts_ms_slow": dict(zip(PARTS, np.round(parts[slow].mean(0), 4).tolist())) if slow.any() else None,
                "gpu_ms_batches_p50_p99_max": np.round(np.percentile((b[:, 2] - b[:, 1]) * 1e3, [50, 99, 100]), 4).tolist(),
