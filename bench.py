@@ -401,6 +401,7 @@ def latency_mode_loads(args, run_at, pay, n, device, verdicts_ok, cpus):
             pooled.append(ms)
             runs.append({"offered_txn_per_s": res["offered_txn_per_s"], "achieved_txn_per_s": res["achieved_txn_per_s"],
                          "p99_ms": float(np.percentile(ms, 99)), "batches": res["batches"],
+                         "ratio": res["achieved_txn_per_s"] / res["offered_txn_per_s"],
                          "ring_overruns": res["ring_overruns"]})
             out["verdicts_ok"] &= bool((v == 0).all())
         ms = np.concatenate(pooled)
@@ -411,6 +412,7 @@ def latency_mode_loads(args, run_at, pay, n, device, verdicts_ok, cpus):
                              "p50_ms": float(np.percentile(ms, 50)), "p99_ms": float(np.percentile(ms, 99)),
                              "max_ms": float(ms.max()), "samples": int(ms.size), "percentiles": "pooled over 5 runs",
                              "p99_ms_runs": [r["p99_ms"] for r in runs],
+                             "achieved_over_offered_runs": [round(r["ratio"], 4) for r in runs],
                              "batches": sum(r["batches"] for r in runs),
                              "ring_overruns": sum(r["ring_overruns"] for r in runs)})
     return out
@@ -531,7 +533,9 @@ def latency_deployed(eng, args):
                                  "p50_ms": float(np.percentile(ms, 50)), "p99_ms": float(np.percentile(ms, 99)),
                                  "max_ms": float(ms.max()), "samples": int(ms.size),
                                  "percentiles": f"pooled over {runs} runs",
-                                 "p99_ms_runs": [r["lat_p99_us"] * 1e-3 for r in per_run]})
+                                 "p99_ms_runs": [r["lat_p99_us"] * 1e-3 for r in per_run],
+                                 "achieved_over_offered_runs": [round(r["txn_per_s"] / (frac * peak), 4)
+                                                                for r in per_run]})
         return out
     def at_rates(rates, runs):
         """the GPU tile at absolute offered loads (the reference tile's own

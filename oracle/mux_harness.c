@@ -463,7 +463,12 @@ main( int argc, char ** argv ) {
   h->res     = (uchar *)malloc( h->res_cap );
   h->lat_ns  = (uint *)malloc( 4UL*(h->n+1UL) );
   FD_TEST( h->res && h->lat_ns );
-  fd_memset( h->lat_ns, 0, 4UL*(h->n+1UL) );   /* touched before the stream (no first-touch faults inside it) */
+  /* both touched before the stream: the consumer appends every published
+     frag to res, and a first-touch fault there (a 2 MiB huge page zeroed
+     every ~6K frags) held it for a few hundred us at a time, which every
+     frag it then read late carried as latency */
+  fd_memset( h->lat_ns, 0, 4UL*(h->n+1UL) );
+  fd_memset( h->res, 0, h->res_cap );
 
   /* privileged_init (maps the accelerated tiles' links), then the threads */
   for( ulong j=0UL; j<K; j++ ) {

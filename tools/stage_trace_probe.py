@@ -66,8 +66,11 @@ def main():
     eng.close()
 
     def run(rate, keep=True):
-        due, pub, pull = (np.zeros(n) for _ in range(3))
-        bat = np.zeros(n, np.uint64)
+        # np.full, not np.zeros: zeros come from untouched pages, and the
+        # first touch inside the run (a huge page zeroed) stalled the thread
+        # that stamps them
+        due, pub, pull = (np.full(n, -1.0) for _ in range(3))
+        bat = np.full(n, 0, np.uint64)
         lib.fd_ed25519_hip_stage_trace_frags(due.ctypes.data, pub.ctypes.data, pull.ctypes.data, bat.ctypes.data)
         buf = np.zeros((1 << 18, 8))
         lib.fd_ed25519_hip_stage_trace_read(buf.ctypes.data, 0, 1)   # reset
