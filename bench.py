@@ -803,6 +803,53 @@ def host_stream(n, sizes, window, chunk, fill, pool_run, world, alloc=np.zeros, 
             "rank_digest": dig.hexdigest()}, codes
 
 
+def _mem_available():
+    """MemAvailable of this node in bytes (/proc/meminfo), or None"""
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return None
+
+
+def _memlock_limit():
+    """RLIMIT_MEMLOCK's soft limit in bytes, or None when unlimited"""
+    import resource
+    soft, _ = resource.getrlimit(resource.RLIMIT_MEMLOCK)
+    return None if soft == resource.RLIM_INFINITY else int(soft)
+
+
+def c4_window_preflight(window, sizes, world, chunk, local_world=None):
+    """Before any rank pins its C4 window: the windows of
+    all the node's ranks must fit in half of its MemAvailable, and each in
+    RLIMIT_MEMLOCK when that is finite.  A window that does not fit shrinks
+    (to a multiple of `chunk` when at least one chunk fits): the stream is
+    counter-based per signature, so the verdicts and the digest do not
+    depend on the window.  Every rank takes the smallest rank's window, so
+    all run the same number of windows (their barriers pair up), and all
+    fail together, before pinning anything, when not one signature fits.
+    -> (window, record)"""
+    n = len(sizes)
+    W = max(1, min(window, n))
+    bps = (float(np.mean(sizes)) if n else 0.0) + 8 + 4 + 64 + 32 + 1   # message, off, sz, sig, pub, code
+    avail, memlock = _mem_available(), _memlock_limit()
+    local = int(local_world or os.environ.get("LOCAL_WORLD_SIZE") or world)
+    budget = None if avail is None else 0.5 * avail / max(local, 1)
+    if memlock is not None:
+        budget = memlock if budget is None else min(budget, memlock)
+    fit = W if budget is None else int(budget // bps)
+    W2 = W if fit >= W else ((fit // chunk) * chunk if fit >= chunk else fit)
+    W2 = int(-allreduce_max(-float(W2), world))
+    rec = {"requested_window": int(window), "window": W2, "bytes_per_signature_est": round(bps, 1),
+           "ranks_on_node": local, "mem_available_bytes": avail, "memlock_limit_bytes": memlock,
+           "budget_bytes_per_rank": budget, "shrunk": W2 < W}
+    if W2 < 1:
+        raise RuntimeError(f"C4 pre-flight: no window fits ({rec})")
+    return W2, rec
+
+
 def c4_host_fed(eng, device, info, rank, world, n, index_base, cfg, seed, window, batch, slots):
     """C4 as north_star defines it: the 64M-signature stream sharded over
     the GPUs with per-GPU host feeders (src/app/fdctl/run/tiles/
@@ -848,6 +895,7 @@ def c4_host_fed(eng, device, info, rank, world, n, index_base, cfg, seed, window
             for k, v in s.items():
                 st[k] = st.get(k, 0) + v
         return sec
+    window, preflight = c4_window_preflight(window, sizes, world, C4_CHUNK)
     try:
         res, codes = host_stream(n, sizes, window, C4_CHUNK, fill, run, world, alloc=alloc,
                                  register=tile.HostRegistration)
@@ -874,6 +922,7 @@ def c4_host_fed(eng, device, info, rank, world, n, index_base, cfg, seed, window
             "stream_seconds": res["stream_seconds"], "window_seconds_max_over_ranks": res["window_seconds_max_over_ranks"],
             "wall_seconds_with_refill": res["wall_seconds_with_refill"],
             "host_window_bytes_per_rank": res["host_window_bytes"], "peak_rss_bytes_max_over_ranks": rss,
+            "window_preflight": preflight,
             "batch_sigs": batch, "slots_in_flight": slots,
             "h2d_bytes_per_signature": bps, "achieved_h2d_GBps_per_gpu": rate / world * bps / 1e9,
             "pinned_copy_h2d_GBps": h2d, "pcie_bound_verifies_per_s_per_gpu": bound,

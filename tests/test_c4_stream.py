@@ -281,3 +281,77 @@ def test_config_c4_ranks_agree_on_the_concatenated_digest(world):
     assert all(r["stream_digest"] == _c4_whole_digest() for r in res)
     assert all(r["rank_digests"] == res[0]["rank_digests"] for r in res) and len(res[0]["rank_digests"]) == world
     assert all(r["signatures_per_rank"] == C4_TOTAL // world and r["n_gpus"] == world for r in res)
+
+
+# ---- config_c4's window pre-flight -------------------------
+
+def _preflight_worker(rank, world, port, q, avail):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import bench
+    from firedancer_amd import workload
+    _c4_fakes()
+    workload.CONFIGS["C4"] = dict(workload.CONFIGS["C4"])
+    bench.C4_STREAM_DIGEST = _c4_whole_digest()
+    # the node's free memory as the pre-flight sees it: rank 3's is smaller
+    bench._mem_available = lambda: avail * (0.5 if rank == 3 else 1.0)
+    bench._memlock_limit = lambda: None
+    r, _, w = bench.dist_setup(world)
+    try:
+        res = bench.config_c4(None, 0, {}, r, w, _Args())
+        out = ("ok", res["window_preflight"], res["stream_digest"], res["digest_equal"], res["host_window_bytes_per_rank"])
+    except RuntimeError as ex:
+        out = ("raised", str(ex)[:40])
+    bench.barrier(w)
+    import torch.distributed as dist
+    dist.destroy_process_group()
+    q.put((r, out))
+
+
+def _world8_preflight(avail):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_preflight_worker, args=(r, 8, port, q, avail)) for r in range(8)]
+    for p in procs:
+        p.start()
+    res = [o for _, o in sorted(q.get(timeout=240) for _ in procs)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_preflight_shrinks_every_ranks_window_alike_and_keeps_the_digest():
+    """World 8, 500 signatures per rank, --host-window 900: a node whose
+    free memory holds (for 8 ranks, half of it) about 240 signatures per
+    rank -- and rank 3 sees half that -- makes every rank stream in the
+    smallest rank's window (the barriers pair up), before anything is
+    pinned; the digest is the whole stream's."""
+    bps = 648 + 109                            # C4's mean message (64..1232 B) + the rest of a signature
+    res = _world8_preflight(avail=2 * 8 * 240 * bps)
+    assert all(o[0] == "ok" for o in res), res
+    pf = [o[1] for o in res]
+    assert all(p["shrunk"] and p["requested_window"] == 900 for p in pf)
+    assert len({p["window"] for p in pf}) == 1 and 90 <= pf[0]["window"] <= 130   # rank 3's ~120
+    assert all(o[2] == _c4_whole_digest() and o[3] is True for o in res)
+    assert all(o[4] < 140 * (1232 + 109) for o in res)   # one shrunk window of host memory each
+
+
+def test_preflight_fails_every_rank_before_pinning_when_nothing_fits():
+    res = _world8_preflight(avail=1000)
+    assert all(o[0] == "raised" and o[1].startswith("C4 pre-flight: no window fits") for o in res), res
+
+
+def test_preflight_keeps_a_window_that_fits(monkeypatch):
+    import bench
+    monkeypatch.setattr(bench, "_mem_available", lambda: 1 << 40)
+    monkeypatch.setattr(bench, "_memlock_limit", lambda: None)
+    from firedancer_amd import workload
+    sizes = workload.msg_sizes(SEED, 0, 5000, 64, 1232)
+    w, rec = bench.c4_window_preflight(2000, sizes, 1, 1 << 20)
+    assert w == 2000 and not rec["shrunk"]
+    monkeypatch.setattr(bench, "_memlock_limit", lambda: 300 * 760)   # a finite RLIMIT_MEMLOCK binds
+    w, rec = bench.c4_window_preflight(2000, sizes, 1, 1 << 20)
+    assert rec["shrunk"] and 250 <= w <= 300

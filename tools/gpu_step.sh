@@ -15,6 +15,7 @@
 #   small_trace          rocprofv3 kernel trace of 1- and 256-signature batches
 #   py=script,args       python -u script args     -> OUTDIR/<script>.txt
 #   trace=script,args    rocprofv3 --kernel-trace --stats of python3 script args
+#   env=NAME=VALUE       export NAME=VALUE for the steps after it (unset=NAME: unset)
 #
 # Round 5 ran one hand-written script per session (tools/r5*_step.sh, cited
 # by some profiles/r5_* records); they are in git history at 55c5e83.
@@ -26,6 +27,8 @@ n=0
 for step in "$@"; do
   n=$((n + 1))
   name=${step%%[=@]*}
+  if [ "$name" = env ]; then export "${step#env=}"; echo "export ${step#env=}"; continue; fi
+  if [ "$name" = unset ]; then unset "${step#unset=}"; continue; fi
   secs=300
   [[ $step == *@* ]] && secs=${step##*@} && step=${step%@*}
   args=""
