@@ -460,6 +460,8 @@ def latency_deployed(eng, args):
     # one tile per core
     cores = tile.physical_cores(node)
     per_thread = args.pin_threads and len(cores) >= 4
+    # two hardware queues per slot, as the in-process leg (--hw-queues)
+    svc_queues = min(32, max(4, 2 * args.deployed_slots))
     harness_cpus = ["--cpus", ",".join(map(str, cores[:3]))] if per_thread else []
     service_cpus = ["--cpus", str(cores[3])] if per_thread else []
 
@@ -474,7 +476,7 @@ def latency_deployed(eng, args):
         if kind == "verify_hip":
             svc = subprocess.Popen([svc_bin, "--prefix", f"/fd_vhip_{app}_", "--tiles", "1", "--batch",
                                     str(args.latency_batch), "--slots", str(args.deployed_slots),
-                                    "--hw-queues", str(max(4, args.deployed_slots)), *svc_mode, *service_cpus],
+                                    "--hw-queues", str(svc_queues), *svc_mode, *service_cpus],
                                    stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, preexec_fn=pin)
             line = svc.stdout.readline()
             if not line.startswith("ready"):
@@ -569,7 +571,7 @@ def latency_deployed(eng, args):
             os.unlink(os.path.join(tmp, f))
         os.rmdir(tmp)
     hip.update({"batch_sigs": args.latency_batch, "slots_in_flight": args.deployed_slots,
-                "hw_queues": max(4, args.deployed_slots),
+                "hw_queues": svc_queues,
                 "cpus": f"{len(node)} CPUs of the GPU's NUMA node (service and harness pinned)" if node else "unpinned",
                 "threads": (f"harness producer / consumer / tile on CPUs {cores[:3]}, service link thread on CPU "
                             f"{cores[3]} (physical cores)" if per_thread else "not pinned per thread"),
@@ -1021,9 +1023,11 @@ def main():
     ap.add_argument("--latency-slots", type=int, default=8,
                     help="latency-mode batches in flight, one hardware queue each (see --hw-queues): 8 peak at "
                          "4.4M txn/s with the 4-slot p99, 4 at 3.3M")
-    ap.add_argument("--hw-queues", type=int, default=8,
+    ap.add_argument("--hw-queues", type=int, default=16,
                     help="GPU_MAX_HW_QUEUES of this process (HIP's default is 4), set before its first HIP call "
-                         "unless the environment names more; 0 leaves it")
+                         "unless the environment names more; 0 leaves it.  16 for the 8 latency slots: with 8, "
+                         "every ~675 batches the slots' launches took 3x longer for ~100 batches, a 2 ms tail "
+                         "(profiles/r6_c5_launch_bump.txt)")
     ap.add_argument("--latency-txns", type=int, default=400000, help="0 disables the latency mode")
     ap.add_argument("--no-pin-threads", dest="pin_threads", action="store_false",
                     help="C5 legs: leave the producer / tile / service threads unpinned (A/B)")
