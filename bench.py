@@ -460,8 +460,10 @@ def latency_deployed(eng, args):
     # one tile per core
     cores = tile.physical_cores(node)
     per_thread = args.pin_threads and len(cores) >= 4
-    # two hardware queues per slot, as the in-process leg (--hw-queues)
-    svc_queues = min(32, max(4, 2 * args.deployed_slots))
+    # a hardware queue per slot: with two per slot (16), every batch of the
+    # service's took ~0.8 ms at p99 even at the reference tile's loads
+    # (profiles/r6_c5_launch_bump.txt)
+    svc_queues = max(4, args.deployed_slots)
     harness_cpus = ["--cpus", ",".join(map(str, cores[:3]))] if per_thread else []
     service_cpus = ["--cpus", str(cores[3])] if per_thread else []
 
