@@ -1025,11 +1025,13 @@ def main():
     ap.add_argument("--latency-slots", type=int, default=8,
                     help="latency-mode batches in flight, one hardware queue each (see --hw-queues): 8 peak at "
                          "4.4M txn/s with the 4-slot p99, 4 at 3.3M")
-    ap.add_argument("--hw-queues", type=int, default=16,
+    ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES of this process (HIP's default is 4), set before its first HIP call "
-                         "unless the environment names more; 0 leaves it.  16 for the 8 latency slots: with 8, "
-                         "every ~675 batches the slots' launches took 3x longer for ~100 batches, a 2 ms tail "
+                         "unless the environment names more; 0 leaves it.  8, a queue per latency slot: 16 here "
+                         "beside the deployed leg's service (8) put every deployed batch at ~0.7 ms p99 "
                          "(profiles/r6_c5_launch_bump.txt)")
+    ap.add_argument("--dev-kernargs", action="store_true",
+                    help="leave HIP's kernel arguments in device memory (its default on this GPU; A/B)")
     ap.add_argument("--latency-txns", type=int, default=400000, help="0 disables the latency mode")
     ap.add_argument("--no-pin-threads", dest="pin_threads", action="store_false",
                     help="C5 legs: leave the producer / tile / service threads unpinned (A/B)")
@@ -1073,6 +1075,12 @@ def main():
     # on HIP's default 4 (a batch on a shared queue waits for the one ahead)
     if args.hw_queues and int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < args.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
+    # kernel arguments in host memory, as the verify service runs (unless
+    # the environment says otherwise): the in-process tile's five launches
+    # per batch take ~7 us instead of ~15 us; C2's few launches per 1M
+    # signatures do not notice (profiles/r6_c5_launch_bump.txt)
+    if not args.dev_kernargs:
+        os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "0")
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args.gpus)

@@ -191,6 +191,12 @@ main( int argc, char ** argv ) {
     char qs[ 16 ];
     snprintf( qs, sizeof(qs), "%lu", q );
     setenv( "GPU_MAX_HW_QUEUES", qs, 1 );
+    /* kernel arguments in host memory (unless the environment says
+       otherwise): a batch's five launches then take the link thread ~7 us
+       instead of ~15 us (device-memory kernargs need a write over the link
+       and a flush per launch), and the GPU fetches the few hundred bytes
+       itself (profiles/r6_c5_launch_bump.txt) */
+    setenv( "HIP_FORCE_DEV_KERNARG", "0", 0 );
   }
   if( fd_ed25519_hip_abi_check( FD_ED25519_HIP_ABI_VERSION, sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
                                 sizeof(fd_ed25519_hip_vservice_stats_t) ) ) {
