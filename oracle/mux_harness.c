@@ -25,10 +25,16 @@
    polls every verify -> dedup link in turn, reads each published frag (sig,
    sz, bytes) and returns credits through that link's fseq.
 
-     mux_harness verify|verify_hip PAYLOADS OUT [--app NAME] [--depth D]
+     mux_harness verify|verify_hip|filter_all|publish_only PAYLOADS OUT [--app NAME] [--depth D]
                  [--tiles K | --rr-cnt N --rr-idx I] [--no-sandbox]
                  [--rate TXN_PER_S] [--timeout S] [--lat-out FILE]
                  [--cpus LIST]
+
+   filter_all runs the reference's fd_mux_tile with a tile that filters
+   every frag in before_frag (the run loop's own per-frag cost, no verify
+   behind it); publish_only runs the producer alone (its publish rate with
+   no reader): together they say whether the multi-tile deployed rate is
+   the run loop's or the producer's.
 
    --tiles K: K verify tiles (kind ids 0..K-1) each run on a thread of its
    own (default 1).  --rr-cnt N --rr-idx I: the topology has N verify tiles
@@ -81,6 +87,27 @@ fd_ed25519_hip_shlink_t * fd_verify_hip_txn_link( void * ctx );
 
 #define OUT_BURST (16UL)
 #define TILE_MAX  (16UL)
+
+/* filter_all: the reference's fd_mux_tile loop with a tile whose
+   before_frag filters every frag -- what the run loop
+   alone costs per frag of the shared quic -> verify link, with no verify
+   work behind it (fd_mux.c:387 calls before_frag on every frag; the
+   verify tiles keep seq % verify_tile_count, fd_verify.c:36-47) */
+static ulong filter_all_align( void ) { return 128UL; }
+static ulong filter_all_footprint( fd_topo_tile_t const * tile ) { (void)tile; return 128UL; }
+static void
+filter_all_before_frag( void * ctx, ulong in_idx, ulong seq, ulong sig, int * opt_filter ) {
+  (void)ctx; (void)in_idx; (void)seq; (void)sig;
+  *opt_filter = 1;
+}
+static fd_topo_run_tile_t fd_tile_filter_all = {
+  .name              = "filter",
+  .mux_flags         = FD_MUX_FLAG_COPY | FD_MUX_FLAG_MANUAL_PUBLISH,
+  .burst             = 1UL,
+  .mux_before_frag   = filter_all_before_frag,
+  .scratch_align     = filter_all_align,
+  .scratch_footprint = filter_all_footprint,
+};
 
 static double
 now_s( void ) {
@@ -166,6 +193,7 @@ pin_cpu( int cpu ) {
 /* the slowest tile's fseq: the producer's credits (fd_fctl, reliable consumers) */
 static ulong
 min_fseq( harness_t const * h ) {
+  if( !h->t_cnt ) return h->n;   /* publish_only: no reader, no credit limit */
   ulong m = fd_fseq_query( h->t[0].in_fseq );
   for( ulong k=1UL; k<h->t_cnt; k++ ) {
     ulong q = fd_fseq_query( h->t[k].in_fseq );
@@ -257,7 +285,7 @@ tile_main( void * arg ) {
   harness_t *  h = t->h;
   pin_cpu( t->cpu );   /* before the sandbox: the affinity call is not in the tile's policy */
   fd_log_cpu_set( NULL );
-  fd_log_thread_set( h->run==&fd_tile_verify ? "verify:ref" : "verify:hip" );
+  fd_log_thread_set( h->run==&fd_tile_verify ? "verify:ref" : h->run==&fd_tile_filter_all ? "filter" : "verify:hip" );
   FD_LOG_NOTICE(( "booting tile %lu", t->k ));   /* as fd_topo_run_tile does: warms the logger (thread state, time zone) before the sandbox */
 
   if( h->sandbox && h->run->populate_allowed_seccomp ) {
@@ -332,13 +360,16 @@ parse_cpus( char const * s, int * cpus, int max ) {
 int
 main( int argc, char ** argv ) {
   fd_log_private_boot( &argc, &argv );
-  if( argc<4 ) FD_LOG_ERR(( "usage: %s verify|verify_hip PAYLOADS OUT [--app NAME] [--depth D] [--tiles K | --rr-cnt N "
+  if( argc<4 ) FD_LOG_ERR(( "usage: %s verify|verify_hip|filter_all|publish_only PAYLOADS OUT [--app NAME] [--depth D] [--tiles K | --rr-cnt N "
                             "--rr-idx I] [--no-sandbox] [--rate TXN_PER_S] [--timeout S] [--lat-out FILE] [--cpus LIST]",
                             argv[0] ));
   harness_t * h = (harness_t *)calloc( 1, sizeof(harness_t) );
   char const * kind = argv[1];
-  if(      !strcmp( kind, "verify"     ) ) h->run = &fd_tile_verify;
-  else if( !strcmp( kind, "verify_hip" ) ) h->run = &fd_tile_verify_hip;
+  int publish_only = 0;   /* the producer alone: no tile reads the link (its publish rate) */
+  if(      !strcmp( kind, "verify"       ) ) h->run = &fd_tile_verify;
+  else if( !strcmp( kind, "verify_hip"   ) ) h->run = &fd_tile_verify_hip;
+  else if( !strcmp( kind, "filter_all"   ) ) h->run = &fd_tile_filter_all;
+  else if( !strcmp( kind, "publish_only" ) ) { h->run = &fd_tile_filter_all; publish_only = 1; }
   else FD_LOG_ERR(( "unknown tile %s", kind ));
   char const * app = "harness";
   char const * lat_out = NULL;
@@ -370,6 +401,7 @@ main( int argc, char ** argv ) {
   if( tiles ) { rr_cnt = tiles; h->t_cnt = tiles; }
   else if( rr_cnt ) { h->t_cnt = 1UL; first = rr_idx; }
   else { rr_cnt = 1UL; h->t_cnt = 1UL; }
+  if( publish_only ) h->t_cnt = 0UL;
   FD_TEST( rr_cnt>=1UL && rr_cnt<=TILE_MAX && first<rr_cnt && fd_ulong_is_pow2( depth ) );
   h->cpu_prod = cpu_cnt>0 ? cpus[0] : -1;
   h->cpu_cons = cpu_cnt>1 ? cpus[1] : -1;
