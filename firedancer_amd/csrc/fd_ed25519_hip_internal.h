@@ -124,6 +124,11 @@ typedef struct {
                                       (atab slot j) and no scan follows dsm16          */
   int              bw_bits;        /* radix of btab_lo / btab_hi: FD_ED25519_BTABW_BITS or
                                       FD_ED25519_BTABC_BITS (compact)                 */
+  int              hs_host;        /* small == 3 only: the scalars came from the calling
+                                      thread (host/fd_ed25519_hip_hsrec.cc): prep16 runs
+                                      its decode blocks only, and dsm16's sflag / hs /
+                                      hflag point at the caller's page-locked block (the
+                                      same [field][cap] layout); never a full-length item */
   /* A/B build only (-DFD_ED25519_AB_LDS_BASE=1): the base
      tables staged in LDS instead, [0..256)B and [0..256)[2^136]B, 32 KiB
      each, radix-2^8 unsigned digits of s' split at 2^136 */

@@ -1703,7 +1703,8 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
   switch (phase) {
   case FD_ED25519_PHASE_HASH: {
     if (p->small == 3) {   /* dsm16 chunks: the decompressions lane-split too, the hash over two waves */
-      const uint32_t hb = (uint32_t)((p->n + SHA2W_LANES - 1) / SHA2W_LANES), dw = (uint32_t)((p->n + 1) / 2);
+      const uint32_t hb = p->hs_host ? 0u : (uint32_t)((p->n + SHA2W_LANES - 1) / SHA2W_LANES),
+                     dw = (uint32_t)((p->n + 1) / 2);
       hipLaunchKernelGGL(fd_ed25519_prep16_kernel, dim3(hb + (dw + 1) / 2), dim3(128), 0, st, *p, hb);
       break;
     }
@@ -1745,7 +1746,8 @@ extern "C" int fd_ed25519_hip_launch_phase(const fd_ed25519_verify_params_t* p, 
         const dim3 g16((uint32_t)p->n);
         if (compact) hipLaunchKernelGGL(fd_ed25519_dsm16_kernel<FD_ED25519_BTABC_BITS>, g16, dim3(128), 0, st, *p);
         else         hipLaunchKernelGGL(fd_ed25519_dsm16_kernel<FD_ED25519_BTABW_BITS>, g16, dim3(128), 0, st, *p);
-        if (p->full_in_prep) break;   /* the full-length items were done in prep16: no scan */
+        if (p->full_in_prep || p->hs_host) break;   /* the full-length items were done in prep16, or there are
+                                                       none (host scalars): no scan */
       } else if (p->small == 2) {
         if (compact) hipLaunchKernelGGL(fd_ed25519_dsm8_kernel<FD_ED25519_BTABC_BITS>, g8, dim3(256), 0, st, *p);
         else         hipLaunchKernelGGL(fd_ed25519_dsm8_kernel<FD_ED25519_BTABW_BITS>, g8, dim3(256), 0, st, *p);

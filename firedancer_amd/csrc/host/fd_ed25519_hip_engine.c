@@ -623,6 +623,18 @@ verify_chunk( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p, int l
   return FD_ED25519_HIP_OK;
 }
 
+/* the engine-wide part of a launch's parameters: capacity, base tables,
+   code flavour, half-size bound */
+static void
+params_tables( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p ) {
+  p->cap = e->max_chunk;
+  p->btab = e->d_btab; p->btab16 = e->d_btab16; p->btab_lo = e->btabw[0]; p->btab_hi = e->btabw[1];
+  p->btab8_lo = e->d_btab8[0]; p->btab8_hi = e->d_btab8[1];
+  p->bw_bits = engine_btab_kind( e ) ? FD_ED25519_BTABC_BITS : FD_ED25519_BTABW_BITS;
+  p->codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
+  p->half_dbits     = engine_half_dbits( e );
+}
+
 /* verify_dev and verify_digests_dev: messages hashed on the device, or
    the caller's digests of R||A||M (digests != NULL, msgs unused) */
 static int
@@ -643,12 +655,7 @@ verify_common( fd_ed25519_hip_engine_t * e, unsigned long n,
   memset( &p, 0, sizeof(p) );
   p.msgs = msgs; p.msg_off = (uint64_t const *)msg_off; p.msg_sz = msg_sz; p.digests = digests;
   p.sigs = sigs; p.pubs = pubs; p.out = (int8_t *)out;
-  p.cap = e->max_chunk;
-  p.btab = e->d_btab; p.btab16 = e->d_btab16; p.btab_lo = e->btabw[0]; p.btab_hi = e->btabw[1];
-  p.btab8_lo = e->d_btab8[0]; p.btab8_hi = e->d_btab8[1];
-  p.bw_bits = engine_btab_kind( e ) ? FD_ED25519_BTABC_BITS : FD_ED25519_BTABW_BITS;
-  p.codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
-  p.half_dbits     = engine_half_dbits( e );
+  params_tables( e, &p );
   uint64_t chunk = e->max_chunk;
   /* a multi-chunk call alternates its chunks between the two lanes; lane 1
      starts after the work already queued on the call's stream and the
@@ -689,6 +696,54 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_engine_t * e,
                            unsigned char const * sigs, unsigned char const * pubs, signed char * out,
                            void * stream ) {
   return verify_common( e, n, msgs, msg_off, msg_sz, NULL, sigs, pubs, out, stream );
+}
+
+/* The drop-in's host-scalar launches (dropin_run, a few signatures): the
+   decompressions first (prep16's decode blocks only), and the group
+   equation (dsm16) once the calling thread has written each signature's
+   scalars (fd_ed25519_hip_private_hsrec) into page-locked memory the device
+   reads in place -- sflag [cap], hflag [cap] and hs [19][cap], the work
+   arrays' layout.  The caller computes while the decompressions run. */
+static int
+hs_params( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p, unsigned long n, unsigned char const * sigs,
+           unsigned char const * pubs, signed char * out ) {
+  if( !e || !n || n>e->r16_max || n>e->max_chunk || !sigs || !pubs || !out ||
+      ((uintptr_t)sigs & 15UL) || ((uintptr_t)pubs & 15UL) ) return FD_ED25519_HIP_ERR_INVAL;
+  memset( p, 0, sizeof(*p) );
+  p->sigs = sigs; p->pubs = pubs; p->out = (int8_t *)out;
+  params_tables( e, p );
+  p->k = e->lane[0].d_k; p->sflag = e->lane[0].d_sflag; p->pflag = e->lane[0].d_pflag; p->pts = e->lane[0].d_pts;
+  p->fix_list = e->lane[0].d_fix; p->fix_cnt = e->lane[0].d_hist + 2*FD_ED25519_SORT_BUCKETS;
+  p->work_ctr = p->fix_cnt + 1; p->hs = e->lane[0].d_hs; p->hflag = e->lane[0].d_hflag;
+  p->hist = e->lane[0].d_hist; p->atab = e->lane[0].d_atab;
+  p->n = n; p->small = 3; p->hs_host = 1;
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_private_hs_decode( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned char const * sigs,
+                                  unsigned char const * pubs, signed char * out, void * stream ) {
+  fd_ed25519_verify_params_t p;
+  int err = hs_params( e, &p, n, sigs, pubs, out );
+  if( err ) return err;
+  HIPCHK( hipSetDevice( e->device ), "hipSetDevice" );
+  err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_HASH, e->dsm_grid, stream ? (hipStream_t)stream : e->stream );
+  if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_private_hs_dsm( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned char const * sigs,
+                               unsigned char const * pubs, signed char * out, unsigned char const * sflag,
+                               unsigned char const * hflag, unsigned int const * hs, void * stream ) {
+  fd_ed25519_verify_params_t p;
+  int err = hs_params( e, &p, n, sigs, pubs, out );
+  if( err ) return err;
+  if( !sflag || !hflag || !hs ) return FD_ED25519_HIP_ERR_INVAL;
+  p.sflag = (uint8_t *)sflag; p.hflag = (uint8_t *)hflag; p.hs = (uint32_t *)hs;
+  err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, stream ? (hipStream_t)stream : e->stream );
+  if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+  return FD_ED25519_HIP_OK;
 }
 
 int
@@ -1091,6 +1146,23 @@ fd_ed25519_hip_dropin_set_host_hash_min( unsigned long bytes ) {
 
 void fd_ed25519_hip_private_challenge( unsigned char const sig[ 64 ], unsigned char const pub[ 32 ],
                                        unsigned char const * msg, unsigned long msg_sz, unsigned char out[ 64 ] );
+int  fd_ed25519_hip_private_hsrec( unsigned char const sig[ 64 ], unsigned char const pub[ 32 ],
+                                   unsigned char const * msg, unsigned long msg_sz, int dbits, uint32_t rec[ 32 ] );
+
+/* Direct launches of at most this many signatures take their scalars from
+   the calling thread (host/fd_ed25519_hip_hsrec.cc, ~8 us each) while the
+   device decompresses A and R, instead of prep16's hash -> search chain of
+   one lane; more would cost the caller more than the chain.  Test hook:
+   fd_ed25519_hip_dropin_set_host_scalars (0 turns the mode off). */
+#ifndef DROPIN_HS_MAX
+#define DROPIN_HS_MAX 2UL
+#endif
+static unsigned long dropin_hs_max = DROPIN_HS_MAX;
+
+void
+fd_ed25519_hip_dropin_set_host_scalars( unsigned long max_sigs ) {
+  dropin_hs_max = max_sigs>DROPIN_DIRECT_MAX ? DROPIN_DIRECT_MAX : max_sigs;
+}
 
 static pthread_once_t  dropin_once = PTHREAD_ONCE_INIT;
 static pthread_mutex_t dropin_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -1256,6 +1328,13 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   uint64_t o_out  = DROPIN_ALIGN16( in_sz + 16UL );
   uint64_t o_tout = o_out + nsig;
   uint64_t need   = o_tout + n + 16UL;
+  /* host scalars (a direct launch of a few single-signature requests): the
+     device reads sflag / hflag [cap] and hs [19][cap] in the block, the
+     work arrays' stride (only the first nsig of each row are written) */
+  int hsmode = nsig<=dropin_hs_max && !multi && !nsig_h && nsig<=DROPIN_DIRECT_MAX && in_sz<=DROPIN_DIRECT_MAX_BYTES;
+  uint64_t cap_hs = e->max_chunk;
+  uint64_t o_hsf = DROPIN_ALIGN16( need ), o_hhf = DROPIN_ALIGN16( o_hsf + cap_hs ), o_hs = DROPIN_ALIGN16( o_hhf + cap_hs );
+  if( hsmode ) need = o_hs + 19UL*4UL*cap_hs;
   if( need>dq.blk_cap[k] ) {
     uint64_t cap = dq.blk_cap[k] ? dq.blk_cap[k] : (1UL<<20);
     while( cap<need ) cap *= 2UL;
@@ -1317,9 +1396,39 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     pp.src[0] = dq.h_dev[k]; pp.dst[0] = d; pp.n[0] = in_sz ? in_sz : 1UL; pp.cnt = 1U;
     HIPCHK( (hipError_t)fd_ed25519_hip_launch_pull( &pp, st ), "H2D drop-in" );
   }
-  int err = fd_ed25519_hip_verify_dev( e, nsig_m, src + o_msg, (unsigned long const *)(src + o_off),
-                                       (unsigned int const *)(src + o_sz), src + o_sig, src + o_pub,
-                                       (signed char *)(src + o_out), st );
+  int err = FD_ED25519_HIP_OK, hsdone = 0;
+  if( direct && hsmode ) {
+    /* decompressions now; the scalars on this thread meanwhile; the group
+       equation after (a signature without a half-size pair, ~1e-6, sends
+       the launch down the device's own path instead) */
+    err = fd_ed25519_hip_private_hs_decode( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out), st );
+    if( err ) { hipStreamSynchronize( st ); return err; }
+    uint8_t *  hsf = (uint8_t *)(h + o_hsf);
+    uint8_t *  hhf = (uint8_t *)(h + o_hhf);
+    uint32_t * hs  = (uint32_t *)(h + o_hs);
+    int all = 1;
+    int dbits = engine_half_dbits( e );
+    t = 0UL;
+    for( dropin_req_t * r=list; r && all; r=r->next, t++ ) {
+      uint32_t rec[ 32 ];
+      all = fd_ed25519_hip_private_hsrec( r->sigs, r->pubs, r->msg, r->msg_sz, dbits, rec );
+      if( !all ) break;
+      uint64_t j = tf[ t ];
+      for( int w=0; w<19; w++ ) hs[ (uint64_t)w*cap_hs + j ] = rec[ 8 + w ];
+      hsf[ j ] = (uint8_t)rec[ 27 ];
+      hhf[ j ] = (uint8_t)rec[ 28 ];
+    }
+    if( all ) {
+      err = fd_ed25519_hip_private_hs_dsm( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
+                                           src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs), st );
+      if( err ) { hipStreamSynchronize( st ); return err; }
+      hsdone = 1;
+    }
+  }
+  if( !hsdone )
+    err = fd_ed25519_hip_verify_dev( e, nsig_m, src + o_msg, (unsigned long const *)(src + o_off),
+                                     (unsigned int const *)(src + o_sz), src + o_sig, src + o_pub,
+                                     (signed char *)(src + o_out), st );
   if( !err && nsig_h )
     err = fd_ed25519_hip_verify_digests_dev( e, nsig_h, src + o_dig, src + o_sig + 64UL*nsig_m,
                                              src + o_pub + 32UL*nsig_m, (signed char *)(src + o_out + nsig_m), st );

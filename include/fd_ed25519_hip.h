@@ -98,6 +98,15 @@ fd_ed25519_hip_dropin_stats( unsigned long * launches, unsigned long * requests 
 void
 fd_ed25519_hip_dropin_set_host_hash_min( unsigned long bytes );
 
+/* A direct drop-in launch (one caller alone, at most a few signatures)
+   computes each signature's scalars -- k = SHA-512(R||A||M) mod L, S < L,
+   the half-size pair -- on the calling thread while the GPU decompresses A
+   and R, instead of in one GPU lane before them (the latency path's
+   longest chain).  Test hook: launches of at most `max_sigs` signatures
+   take that path (0: never; the default is 2). */
+void
+fd_ed25519_hip_dropin_set_host_scalars( unsigned long max_sigs );
+
 unsigned long
 fd_ed25519_hip_dropin_device_bytes( void );
 
