@@ -1195,12 +1195,18 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
   const uint64_t j = blockIdx.x;   /* a block (two waves) per signature: every return below is block-uniform */
   if (j >= p.n) return;
   const uint32_t hf = p.hflag[j];
-  if (hf & FD_HF_FULL) return;     /* the dsm kernel's (full-length form) */
   const int half = (int)(threadIdx.x >> 6);   /* 0: -A and B, 1: -+R and B' */
+  /* the scalars loaded first, used after the table build: with host
+     scalars (p.hs_host) they sit in page-locked host memory, and their
+     link round trips then overlap the table build instead of following it */
+  uint32_t hd[5], hx[5], hb[5];
+  load_hs(hd, p, 5, 5, j);                    /* |d|                     */
+  load_hs(hx, p, half ? 5 : 0, 5, j);         /* c (wave 0), |d| (wave 1) */
+  load_hs(hb, p, half ? 15 : 10, half ? 4 : 5, j);   /* s_hi / s_lo        */
+  if (hf & FD_HF_FULL) return;     /* the dsm kernel's (full-length form) */
   r16ctx k;
   r16_init(k);
   const uint32_t d2 = r16_from_fe(fe{FE_D2}, k);
-  int code = precheck(p, j);
   uint32_t tab[9];
   {
     fe x, y;
@@ -1210,19 +1216,12 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
   uint32_t sd[5], bd[5];
   int W = 33;
   {
-    uint32_t x[5], t[5];
-    load_hs(x, p, 5, 5, j);
-    W = (fd_half_bitlen<5>(x) + 4) >> 2;
+    uint32_t t[5];
+    W = (fd_half_bitlen<5>(hd) + 4) >> 2;
     W = W < 33 ? 33 : W;
-    if (!half) load_hs(x, p, 0, 5, j);
-    shl160v(t, x, 160 - 4 * W); recode160<4>(sd, t);
-    if (half) {
-      load_hs(x, p, 15, 4, j);
-      shl160<fd_bw<BW>::HI_SHL>(bd, x);
-    } else {
-      load_hs(x, p, 10, 5, j);
-      shl160<fd_bw<BW>::LO_SHL>(bd, x);
-    }
+    shl160v(t, hx, 160 - 4 * W); recode160<4>(sd, t);
+    if (half) shl160<fd_bw<BW>::HI_SHL>(bd, hb);
+    else      shl160<fd_bw<BW>::LO_SHL>(bd, hb);
   }
   W = __builtin_amdgcn_readfirstlane(W);
   const int32_t* btab = half ? p.btab_hi : p.btab_lo;
@@ -1263,6 +1262,7 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
   const bool zero = r16_iszero(P + ((k.p4 - z) & k.r1));
   const uint64_t bal = __ballot(zero);
   const bool ident = (bal & 1ull) && (bal & (1ull << 16));
+  int code = precheck(p, j);   /* S < L, decode failures, small order: the reference's order */
   if (code == FD_PENDING) code = ident ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
   /* Write-code-last invariant: a signature's code is the last thing any
      kernel of its launch does with that signature; no kernel reads the

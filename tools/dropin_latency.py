@@ -63,6 +63,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=2000)
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "dropin_latency.json"))
+    ap.add_argument("--host-scalars", type=int, default=None,
+                    help="fd_ed25519_hip_dropin_set_host_scalars (A/B; default: the library's)")
     ap.add_argument("--large", default="16384,65376,65377,1048576,8388608",
                     help="message sizes (bytes) for the device-hashed large-message latencies")
     args = ap.parse_args()
@@ -76,6 +78,10 @@ def main():
     eng.close()
     lib = ed25519.library()
     res = {}
+    if args.host_scalars is not None:
+        lib.fd_ed25519_hip_dropin_set_host_scalars.argtypes = [ctypes.c_ulong]
+        lib.fd_ed25519_hip_dropin_set_host_scalars(args.host_scalars)
+        res["host_scalars_max_sigs"] = args.host_scalars
     for _ in range(20):   # warm-up: the default engine, code objects
         ed25519.verify(msgs[:200].tobytes(), sigs[0].tobytes(), pubs[0].tobytes())
     t_one = []
