@@ -167,6 +167,30 @@ int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t
 #define FD_ED25519_PHASE_DSM    3
 #define FD_ED25519_PHASE_CNT    4
 int fd_ed25519_hip_launch_phase( fd_ed25519_verify_params_t const * p, int phase, uint32_t grid, void * stream );
+
+/* Host scalars (host/fd_ed25519_hip_hsrec.cc, host/fd_ed25519_hip_engine.c):
+   a launch of a few signatures whose k, S < L and half-size pair the
+   calling thread computes while the device decompresses A and R.
+   hsrec: 1 and the 32-word record (k[8], hs[19], sflag, hflag), or 0 when
+   k has no half-size pair within dbits (the launch then takes the device's
+   own path).  hs_decode: prep16's decode blocks; hs_dsm: dsm16 with
+   sflag [cap], hflag [cap], hs [19][cap] read in place (cap = the engine's
+   max_chunk).  The engine's dsm16 form must take n (n <= its r16 bound). */
+#ifdef __cplusplus
+extern "C" {
+#endif
+struct fd_ed25519_hip_engine;
+int fd_ed25519_hip_private_hsrec( unsigned char const sig[ 64 ], unsigned char const pub[ 32 ],
+                                  unsigned char const * msg, unsigned long msg_sz, int dbits, uint32_t rec[ 32 ] );
+int fd_ed25519_hip_private_half_dbits( struct fd_ed25519_hip_engine const * e );
+int fd_ed25519_hip_private_hs_decode( struct fd_ed25519_hip_engine * e, unsigned long n, unsigned char const * sigs,
+                                      unsigned char const * pubs, signed char * out, void * stream );
+int fd_ed25519_hip_private_hs_dsm( struct fd_ed25519_hip_engine * e, unsigned long n, unsigned char const * sigs,
+                                   unsigned char const * pubs, signed char * out, unsigned char const * sflag,
+                                   unsigned char const * hflag, unsigned int const * hs, void * stream );
+#ifdef __cplusplus
+}
+#endif
 int fd_ed25519_hip_verify_occupancy( int * blocks_per_cu );
 /* lane-table bytes per dsm wave as compiled into the kernels (the host
    sizes the atab scratch from this, never from its own copy of the macro) */

@@ -721,6 +721,11 @@ hs_params( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p, unsigned
 }
 
 int
+fd_ed25519_hip_private_half_dbits( fd_ed25519_hip_engine_t const * e ) {
+  return engine_half_dbits( e );
+}
+
+int
 fd_ed25519_hip_private_hs_decode( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned char const * sigs,
                                   unsigned char const * pubs, signed char * out, void * stream ) {
   fd_ed25519_verify_params_t p;
@@ -1146,8 +1151,6 @@ fd_ed25519_hip_dropin_set_host_hash_min( unsigned long bytes ) {
 
 void fd_ed25519_hip_private_challenge( unsigned char const sig[ 64 ], unsigned char const pub[ 32 ],
                                        unsigned char const * msg, unsigned long msg_sz, unsigned char out[ 64 ] );
-int  fd_ed25519_hip_private_hsrec( unsigned char const sig[ 64 ], unsigned char const pub[ 32 ],
-                                   unsigned char const * msg, unsigned long msg_sz, int dbits, uint32_t rec[ 32 ] );
 
 /* Direct launches of at most this many signatures take their scalars from
    the calling thread (host/fd_ed25519_hip_hsrec.cc, ~8 us each) while the

@@ -187,7 +187,32 @@ typedef struct {
   int                       ext_counts;
   unsigned char *           h_in_dev;       /* h_in's device-visible address   */
   unsigned char *           h_outb_dev;     /* h_outb's device-visible address */
+  /* host-scalar batches (at most PIPE_HS_MAX signatures, pipe_submit_hs):
+     sflag [sig_cap], hflag [sig_cap], hs [19][sig_cap] written by the
+     submitting thread and read in place by dsm16; the transactions' codes
+     combined on the host when the batch completes */
+  unsigned char *           h_hs;
+  unsigned char *           h_hs_dev;
+  int                       host_combine;
 } pipe_slot_t;
+
+/* Batches of at most this many signatures (a verify tile at a low load:
+   one or two transactions each) take their scalars from the submitting
+   thread (host/fd_ed25519_hip_hsrec.cc, ~8 us a signature) while the GPU
+   decompresses A and R, read their signatures and keys from the staging
+   block in place, write their codes into the page-locked output block, and
+   have their transactions' codes combined on the host: two launches
+   (prep16's decode blocks, dsm16) instead of five (pull, prep16, dsm16,
+   combine, push).  0 turns it off (fd_ed25519_hip_pipe_set_host_scalars). */
+#ifndef PIPE_HS_MAX
+#define PIPE_HS_MAX 2UL
+#endif
+static unsigned long pipe_hs_max = PIPE_HS_MAX;
+
+void
+fd_ed25519_hip_pipe_set_host_scalars( unsigned long max_sigs ) {
+  pipe_hs_max = max_sigs;
+}
 
 struct fd_ed25519_hip_pipe {
   int           device;
@@ -204,7 +229,7 @@ struct fd_ed25519_hip_pipe {
 
 static void
 pipe_slot_free( pipe_slot_t * s ) {
-  hipHostFree( s->h_in ); hipHostFree( s->h_outb );
+  hipHostFree( s->h_in ); hipHostFree( s->h_outb ); hipHostFree( s->h_hs );
   hipFree( s->d_in ); hipFree( s->d_outb );
   hipFree( s->d_soff ); hipFree( s->d_ssz ); hipFree( s->d_pok );
   if( s->ev ) hipEventDestroy( s->ev );
@@ -251,6 +276,8 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   TCHK( hipMalloc(     (void **)&s->d_in,   in_sz                        ), "hipMalloc" );
   TCHK( hipHostGetDevicePointer( (void **)&s->h_in_dev, s->h_in, 0U ), "hipHostGetDevicePointer" );
   TCHK( hipHostGetDevicePointer( (void **)&s->h_outb_dev, s->h_outb, 0U ), "hipHostGetDevicePointer" );
+  TCHK( hipHostMalloc( (void **)&s->h_hs, (2UL + 19UL*4UL)*sig_cap, hipHostMallocCoherent ), "hipHostMalloc" );
+  TCHK( hipHostGetDevicePointer( (void **)&s->h_hs_dev, s->h_hs, 0U ), "hipHostGetDevicePointer" );
   TCHK( hipMalloc(     (void **)&s->d_outb, out_sz                       ), "hipMalloc" );
   p->sigs        = s->h_in + o_sigs;                   s->d_sigs   = s->d_in + o_sigs;
   p->pubs        = s->h_in + o_pubs;                   s->d_pubs   = s->d_in + o_pubs;
@@ -448,6 +475,66 @@ slot_check( fd_ed25519_hip_slot_t const * slot, unsigned long sig_cnt, unsigned 
   return FD_ED25519_HIP_OK;
 }
 
+/* A host-scalar batch (PIPE_HS_MAX above): the decompressions launched
+   first, the scalars computed meanwhile, then dsm16 writing the signature
+   codes into the page-locked output block.  1: submitted; 0: a signature
+   has no half-size pair (~1e-6), nothing but the decode launch was queued
+   and the caller takes the device's own path; < 0: a launch failed. */
+static int
+pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) {
+  fd_ed25519_hip_slot_t * slot = &s->pub;
+  unsigned long n = slot->sig_cnt, cap = slot->sig_cap;
+  unsigned long o_sigs = (unsigned long)( slot->sigs - s->h_in ), o_pubs = (unsigned long)( slot->pubs - s->h_in );
+  int err;
+  PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_decode( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
+                                                                 (signed char *)s->h_outb_dev, st ) );
+  if( err ) return err;
+  unsigned char * hsf = s->h_hs, * hhf = s->h_hs + cap;
+  uint32_t *      hs  = (uint32_t *)( s->h_hs + 2UL*cap );
+  int dbits = fd_ed25519_hip_private_half_dbits( s->eng );
+  for( unsigned long i=0UL; i<n; i++ ) {
+    uint32_t rec[ 32 ];
+    if( !fd_ed25519_hip_private_hsrec( slot->sigs + 64UL*i, slot->pubs + 32UL*i, slot->msgs + slot->msg_off[ i ],
+                                       slot->msg_sz[ i ], dbits, rec ) ) return 0;
+    for( int w=0; w<19; w++ ) hs[ (unsigned long)w*cap + i ] = rec[ 8 + w ];
+    hsf[ i ] = (unsigned char)rec[ 27 ];
+    hhf[ i ] = (unsigned char)rec[ 28 ];
+  }
+  PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
+                                                              (signed char *)s->h_outb_dev, s->h_hs_dev,
+                                                              s->h_hs_dev + cap, (unsigned int const *)( s->h_hs_dev + 2UL*cap ),
+                                                              st ) );
+  if( err ) return err;
+  s->host_combine = slot->txn_cnt ? 1 : 0;
+  TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
+#ifdef FD_ED25519_HIP_AB_STAGE_TRACE
+  s->t_enq = now_s(); s->in_flight0 = pipe->in_flight;
+#endif
+  s->state = SLOT_BUSY;
+  pipe->in_flight++;
+  return 1;
+}
+
+/* batch_single_msg's rule per transaction (fd_ed25519_user.c:231-309, the
+   device's fd_ed25519_txn_combine_kernel): 0 or > 16 signatures ERR_SIG;
+   else the first error other than ERR_MSG in signature order, else ERR_MSG
+   if any signature had it, else SUCCESS */
+static void
+host_combine( fd_ed25519_hip_slot_t * slot ) {
+  for( unsigned long t=0UL; t<slot->txn_cnt; t++ ) {
+    unsigned int f = slot->txn_first[ t ], n = slot->txn_sig_cnt[ t ];
+    int code = FD_ED25519_SUCCESS, msg_fail = 0;
+    if( n==0U || n>16U ) code = FD_ED25519_ERR_SIG;
+    else for( unsigned int j=0U; j<n; j++ ) {
+      int c = slot->sig_out[ f + j ];
+      if( c==FD_ED25519_ERR_MSG ) msg_fail = 1;
+      else if( c!=FD_ED25519_SUCCESS ) { code = c; break; }
+    }
+    if( code==FD_ED25519_SUCCESS && msg_fail ) code = FD_ED25519_ERR_MSG;
+    slot->txn_out[ t ] = (signed char)code;
+  }
+}
+
 int
 fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t * slot,
                             unsigned long sig_cnt, unsigned long msg_bytes, unsigned long txn_cnt ) {
@@ -460,7 +547,13 @@ fd_ed25519_hip_pipe_submit( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_slot_t 
   slot->sig_cnt = sig_cnt; slot->msg_bytes = msg_bytes; slot->txn_cnt = txn_cnt;
   slot->seq = pipe->seq++;
   slot->t_submit = now_s();
+  s->host_combine = 0;
   int err;
+  if( sig_cnt && sig_cnt<=pipe_hs_max && !s->ext_src[0] && !pipe->warming ) {
+    err = pipe_submit_hs( pipe, s, st );
+    if( err<0 ) return err;
+    if( err==1 ) return FD_ED25519_HIP_OK;   /* 0: a signature without a half-size pair, the device's own path below */
+  }
   PF_SUB( pf_sub_h2d, err = slot_h2d( pipe, s, st, sig_cnt, txn_cnt, msg_bytes ) );
   if( err ) return err;
 #ifdef FD_ED25519_HIP_HOST_FAULT
@@ -583,6 +676,7 @@ fd_ed25519_hip_pipe_poll( fd_ed25519_hip_pipe_t * pipe, int wait ) {
     return NULL;
   }
   s->pub.t_done = now_s();
+  if( s->host_combine ) host_combine( &s->pub );
   s->state = SLOT_DONE;
   pipe->next_poll++;
   pipe->in_flight--;

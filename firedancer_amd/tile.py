@@ -313,6 +313,13 @@ def pack_payloads(payloads):
 
 
 _lib.fd_ed25519_hip_latency_set_cpus.argtypes = [ctypes.c_int, ctypes.c_int]
+_lib.fd_ed25519_hip_pipe_set_host_scalars.argtypes = [ctypes.c_ulong]
+
+
+def pipe_set_host_scalars(max_sigs):
+    """fd_ed25519_hip_pipe_set_host_scalars: pipe batches of at most
+    max_sigs signatures take the host-scalar path (0: none; default 2)"""
+    _lib.fd_ed25519_hip_pipe_set_host_scalars(int(max_sigs))
 
 
 def latency_set_cpus(producer_cpu=-1, tile_cpu=-1):

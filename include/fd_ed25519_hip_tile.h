@@ -141,6 +141,17 @@ fd_ed25519_hip_pipe_error( fd_ed25519_hip_pipe_t const * pipe );
 unsigned long
 fd_ed25519_hip_pipe_device_bytes( fd_ed25519_hip_pipe_t const * pipe );
 
+/* Batches of at most max_sigs signatures (a tile at a low load: one or two
+   transactions each; default 2, 0: none) take each signature's scalars --
+   k = SHA-512(R||A||M) mod L, S < L, the half-size pair -- from the
+   submitting thread while the GPU decompresses A and R, are read by the
+   kernels from the staging block in place, write their codes straight into
+   the page-locked output, and have their transactions' codes combined on
+   the host at poll: two kernel launches instead of five.  Process-wide;
+   raw (GPU-parse) and zero-copy batches keep the device path. */
+void
+fd_ed25519_hip_pipe_set_host_scalars( unsigned long max_sigs );
+
 /* ---- txn -------------------------------------------------------------- */
 
 /* The fields of fd_txn_t (src/ballet/txn/fd_txn.h) the verify tile reads. */

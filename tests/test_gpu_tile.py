@@ -347,3 +347,76 @@ def test_pipe_stages_in_place_and_rejects_out_of_range(tile, adversarial):
     a["msg_off"][0], a["msg_sz"][0] = 10, 100      # raw mode: payload past the 64 bytes staged
     assert p.submit_txns(s, 1, 64) != 0
     p.close()
+
+
+@pytest.mark.parametrize("hs", [2, 0], ids=["host-scalars", "device-path"])
+def test_pipe_tiny_batches_both_paths(tile, adversarial, mixed_order, batch, hs):
+    """Batches of one or two signatures (a tile at a low load), through the
+    host-scalar path (prep16's decode blocks + dsm16 reading the staged
+    block in place, transaction codes combined on the host) and through the
+    device path: single signatures of the adversarial and mixed-order sets,
+    and the batch_single_msg transactions of one or two signatures (the
+    priority rule included), against the reference's codes."""
+    tile.pipe_set_host_scalars(hs)
+    try:
+        p = tile.Pipe(0, slot_cnt=3, sig_cap=256, msg_cap=256 * 1300, txn_cap=256)
+        jobs = []   # (msgs [(bytes)], sigs, pubs, txn?, want)
+        for d in (adversarial, mixed_order):
+            n = len(d["msg_sz"])
+            for i in range(0, n, 5):
+                o, z = int(d["msg_off"][i]), int(d["msg_sz"][i])
+                k = 2 if i % 3 == 0 and i + 1 < n else 1
+                idx = list(range(i, i + k))
+                jobs.append(([bytes(d["msgs"][int(d["msg_off"][j]):int(d["msg_off"][j]) + int(d["msg_sz"][j])])
+                              for j in idx], [d["sigs"][j] for j in idx], [d["pubs"][j] for j in idx], False,
+                             [int(d["codes_avx512"][j]) for j in idx]))
+        for b, pre in ((batch, ""), (mixed_order, "b_")):
+            for t in range(len(b[pre + "txn_cnt"])):
+                c = int(b[pre + "txn_cnt"][t])
+                if c < 1 or c > 2:
+                    continue
+                o, z, f = int(b[pre + "txn_msg_off"][t]), int(b[pre + "txn_msg_sz"][t]), int(b[pre + "txn_first"][t])
+                m = bytes(b[pre + "msgs"][o:o + z])
+                jobs.append(([m] * c, [b[pre + "sigs"][f + j] for j in range(c)],
+                             [b[pre + "pubs"][f + j] for j in range(c)], True, [int(b[pre + "codes_avx512"][t])]))
+        assert sum(j[3] for j in jobs) > 40
+
+        results = {}
+
+        def drain(wait):
+            done = p.poll(wait)
+            if done is None:
+                return False
+            k = done.contents.user
+            a = tile.Pipe.arrays(done)
+            results[k] = (list(a["txn_out"][:1]) if jobs[k][3] else list(a["sig_out"][:done.contents.sig_cnt]))
+            p.release(done)
+            return True
+
+        for k, (msgs, sigs, pubs, txn, want) in enumerate(jobs):
+            s = p.acquire()
+            while s is None:
+                drain(True)
+                s = p.acquire()
+            a = tile.Pipe.arrays(s)
+            pos = 0
+            for q, (m, sg, pk) in enumerate(zip(msgs, sigs, pubs)):
+                if txn and q:   # one shared message
+                    a["msg_off"][q], a["msg_sz"][q] = a["msg_off"][0], len(m)
+                else:
+                    a["msgs"][pos:pos + len(m)] = np.frombuffer(m, np.uint8)
+                    a["msg_off"][q], a["msg_sz"][q] = pos, len(m)
+                    pos += len(m)
+                a["sigs"][64 * q:64 * q + 64] = sg
+                a["pubs"][32 * q:32 * q + 32] = pk
+            if txn:
+                a["txn_first"][0], a["txn_sig_cnt"][0] = 0, len(sigs)
+            s.contents.user = k
+            assert p.submit(s, len(sigs), pos, txn_cnt=1 if txn else 0) == 0
+        while drain(True):
+            pass
+        p.close()
+        bad = [(k, results.get(k), j[4]) for k, j in enumerate(jobs) if [int(x) for x in results.get(k, [])] != j[4]]
+        assert not bad, bad[:10]
+    finally:
+        tile.pipe_set_host_scalars(2)
