@@ -1158,7 +1158,7 @@ void fd_ed25519_hip_private_challenge( unsigned char const sig[ 64 ], unsigned c
    one lane; more would cost the caller more than the chain.  Test hook:
    fd_ed25519_hip_dropin_set_host_scalars (0 turns the mode off). */
 #ifndef DROPIN_HS_MAX
-#define DROPIN_HS_MAX 2UL
+#define DROPIN_HS_MAX 4UL
 #endif
 static unsigned long dropin_hs_max = DROPIN_HS_MAX;
 

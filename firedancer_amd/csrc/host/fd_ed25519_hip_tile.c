@@ -205,7 +205,7 @@ typedef struct {
    (prep16's decode blocks, dsm16) instead of five (pull, prep16, dsm16,
    combine, push).  0 turns it off (fd_ed25519_hip_pipe_set_host_scalars). */
 #ifndef PIPE_HS_MAX
-#define PIPE_HS_MAX 2UL
+#define PIPE_HS_MAX 4UL
 #endif
 static unsigned long pipe_hs_max = PIPE_HS_MAX;
 

@@ -318,7 +318,7 @@ _lib.fd_ed25519_hip_pipe_set_host_scalars.argtypes = [ctypes.c_ulong]
 
 def pipe_set_host_scalars(max_sigs):
     """fd_ed25519_hip_pipe_set_host_scalars: pipe batches of at most
-    max_sigs signatures take the host-scalar path (0: none; default 2)"""
+    max_sigs signatures take the host-scalar path (0: none; default 4)"""
     _lib.fd_ed25519_hip_pipe_set_host_scalars(int(max_sigs))
 
 

@@ -103,7 +103,7 @@ fd_ed25519_hip_dropin_set_host_hash_min( unsigned long bytes );
    the half-size pair -- on the calling thread while the GPU decompresses A
    and R, instead of in one GPU lane before them (the latency path's
    longest chain).  Test hook: launches of at most `max_sigs` signatures
-   take that path (0: never; the default is 2). */
+   take that path (0: never; the default is 4). */
 void
 fd_ed25519_hip_dropin_set_host_scalars( unsigned long max_sigs );
 

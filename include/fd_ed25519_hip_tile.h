@@ -142,7 +142,7 @@ unsigned long
 fd_ed25519_hip_pipe_device_bytes( fd_ed25519_hip_pipe_t const * pipe );
 
 /* Batches of at most max_sigs signatures (a tile at a low load: one or two
-   transactions each; default 2, 0: none) take each signature's scalars --
+   transactions each; default 4, 0: none) take each signature's scalars --
    k = SHA-512(R||A||M) mod L, S < L, the half-size pair -- from the
    submitting thread while the GPU decompresses A and R, are read by the
    kernels from the staging block in place, write their codes straight into

@@ -23,14 +23,14 @@ def ed():
     lib = ed25519.library()
     lib.fd_ed25519_hip_dropin_set_host_scalars.argtypes = [ctypes.c_ulong]
     yield ed25519, lib
-    lib.fd_ed25519_hip_dropin_set_host_scalars(2)
+    lib.fd_ed25519_hip_dropin_set_host_scalars(4)
 
 
 def _run(ed25519, d, idx):
     return np.array([ed25519.verify(*case(d, i)) for i in idx], np.int8)
 
 
-@pytest.mark.parametrize("mode", [2, 0], ids=["host-scalars", "device-scalars"])
+@pytest.mark.parametrize("mode", [4, 0], ids=["host-scalars", "device-scalars"])
 @pytest.mark.parametrize("fixture", ["vectors", "adversarial", "mixed_order", "halfsize", "longd"])
 def test_dropin_codes_both_scalar_paths(ed, request, mode, fixture):
     ed25519, lib = ed
@@ -48,7 +48,7 @@ def test_dropin_host_scalars_two_callers(ed, adversarial):
     """Two threads calling at once: their requests may combine into one
     launch of two signatures (still a host-scalar launch) -- codes exact."""
     ed25519, lib = ed
-    lib.fd_ed25519_hip_dropin_set_host_scalars(2)
+    lib.fd_ed25519_hip_dropin_set_host_scalars(4)
     n = len(adversarial["msg_sz"])
     out = np.zeros(n, np.int8)
 

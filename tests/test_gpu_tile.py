@@ -349,13 +349,13 @@ def test_pipe_stages_in_place_and_rejects_out_of_range(tile, adversarial):
     p.close()
 
 
-@pytest.mark.parametrize("hs", [2, 0], ids=["host-scalars", "device-path"])
+@pytest.mark.parametrize("hs", [4, 0], ids=["host-scalars", "device-path"])
 def test_pipe_tiny_batches_both_paths(tile, adversarial, mixed_order, batch, hs):
-    """Batches of one or two signatures (a tile at a low load), through the
+    """Batches of one to four signatures (a tile at a low load), through the
     host-scalar path (prep16's decode blocks + dsm16 reading the staged
     block in place, transaction codes combined on the host) and through the
     device path: single signatures of the adversarial and mixed-order sets,
-    and the batch_single_msg transactions of one or two signatures (the
+    and the batch_single_msg transactions of one to four signatures (the
     priority rule included), against the reference's codes."""
     tile.pipe_set_host_scalars(hs)
     try:
@@ -365,7 +365,7 @@ def test_pipe_tiny_batches_both_paths(tile, adversarial, mixed_order, batch, hs)
             n = len(d["msg_sz"])
             for i in range(0, n, 5):
                 o, z = int(d["msg_off"][i]), int(d["msg_sz"][i])
-                k = 2 if i % 3 == 0 and i + 1 < n else 1
+                k = min(1 + (i // 5) % 4, n - i)   # 1..4 signatures a batch
                 idx = list(range(i, i + k))
                 jobs.append(([bytes(d["msgs"][int(d["msg_off"][j]):int(d["msg_off"][j]) + int(d["msg_sz"][j])])
                               for j in idx], [d["sigs"][j] for j in idx], [d["pubs"][j] for j in idx], False,
@@ -373,7 +373,7 @@ def test_pipe_tiny_batches_both_paths(tile, adversarial, mixed_order, batch, hs)
         for b, pre in ((batch, ""), (mixed_order, "b_")):
             for t in range(len(b[pre + "txn_cnt"])):
                 c = int(b[pre + "txn_cnt"][t])
-                if c < 1 or c > 2:
+                if c < 1 or c > 4:
                     continue
                 o, z, f = int(b[pre + "txn_msg_off"][t]), int(b[pre + "txn_msg_sz"][t]), int(b[pre + "txn_first"][t])
                 m = bytes(b[pre + "msgs"][o:o + z])
@@ -419,4 +419,4 @@ def test_pipe_tiny_batches_both_paths(tile, adversarial, mixed_order, batch, hs)
         bad = [(k, results.get(k), j[4]) for k, j in enumerate(jobs) if [int(x) for x in results.get(k, [])] != j[4]]
         assert not bad, bad[:10]
     finally:
-        tile.pipe_set_host_scalars(2)
+        tile.pipe_set_host_scalars(4)
