@@ -1161,10 +1161,23 @@ void fd_ed25519_hip_private_challenge( unsigned char const sig[ 64 ], unsigned c
 #define DROPIN_HS_MAX 4UL
 #endif
 static unsigned long dropin_hs_max = DROPIN_HS_MAX;
+#define FD_HALF_DBITS_HOST_MAX 151   /* fd25519_half.h FD_HALF_DBITS_MAX */
 
 void
 fd_ed25519_hip_dropin_set_host_scalars( unsigned long max_sigs ) {
   dropin_hs_max = max_sigs>DROPIN_DIRECT_MAX ? DROPIN_DIRECT_MAX : max_sigs;
+}
+
+/* Test hook: the host search's bound on |d| (0: the engine's, 151).  No
+   random k without a pair at 151 bits turned up in 40M trials, so tests
+   reach the launch's fallback (the device path from the digests, at the
+   engine's bound) with k that have no pair at 131 bits
+   (tests/golden/halfsize.npz). */
+static int dropin_hs_dbits;
+
+void
+fd_ed25519_hip_dropin_set_host_scalars_dbits( int dbits ) {
+  dropin_hs_dbits = dbits>0 && dbits<=FD_HALF_DBITS_HOST_MAX ? dbits : 0;
 }
 
 static pthread_once_t  dropin_once = PTHREAD_ONCE_INIT;
@@ -1319,6 +1332,15 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     if( r->hashed ) nsig_h += r->cnt; else bytes += r->msg_sz;
   }
   uint64_t nsig_m = nsig - nsig_h;
+  /* host scalars (a launch of a few single-signature requests, any message
+     size below the host-hash limit): the calling thread hashes and finds
+     the scalars, the device reads sflag / hflag [cap] and hs [19][cap] in
+     the block (the work arrays' stride, the first nsig of each row
+     written) and never the messages, which are not staged; a signature
+     without a half-size pair (~1e-6) takes the device path from its
+     digest (room for nsig digests) */
+  int hsmode = nsig<=dropin_hs_max && !multi && !nsig_h;
+  uint64_t ndig   = hsmode ? nsig : nsig_h;
   uint64_t o_off  = 0UL;
   uint64_t o_sz   = DROPIN_ALIGN16( o_off  + 8UL*nsig );
   uint64_t o_tf   = DROPIN_ALIGN16( o_sz   + 4UL*nsig );
@@ -1326,15 +1348,11 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   uint64_t o_sig  = DROPIN_ALIGN16( o_tc   + 4UL*n );
   uint64_t o_pub  = DROPIN_ALIGN16( o_sig  + 64UL*nsig );
   uint64_t o_dig  = DROPIN_ALIGN16( o_pub  + 32UL*nsig );
-  uint64_t o_msg  = DROPIN_ALIGN16( o_dig  + 64UL*nsig_h );
-  uint64_t in_sz  = o_msg + bytes;
+  uint64_t o_msg  = DROPIN_ALIGN16( o_dig  + 64UL*ndig );
+  uint64_t in_sz  = o_msg + ( hsmode ? 0UL : bytes );
   uint64_t o_out  = DROPIN_ALIGN16( in_sz + 16UL );
   uint64_t o_tout = o_out + nsig;
   uint64_t need   = o_tout + n + 16UL;
-  /* host scalars (a direct launch of a few single-signature requests): the
-     device reads sflag / hflag [cap] and hs [19][cap] in the block, the
-     work arrays' stride (only the first nsig of each row are written) */
-  int hsmode = nsig<=dropin_hs_max && !multi && !nsig_h && nsig<=DROPIN_DIRECT_MAX && in_sz<=DROPIN_DIRECT_MAX_BYTES;
   uint64_t cap_hs = e->max_chunk;
   uint64_t o_hsf = DROPIN_ALIGN16( need ), o_hhf = DROPIN_ALIGN16( o_hsf + cap_hs ), o_hs = DROPIN_ALIGN16( o_hhf + cap_hs );
   if( hsmode ) need = o_hs + 19UL*4UL*cap_hs;
@@ -1366,6 +1384,9 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
       memcpy( h + o_dig + 64UL*(s0 - nsig_m), r->dig, 64UL*r->cnt );
       for( uint32_t i=0U; i<r->cnt; i++ ) { off[s0+i] = 0UL; sz[s0+i] = 0U; }
       jh += r->cnt;
+    } else if( hsmode ) {   /* the device never reads the message */
+      for( uint32_t i=0U; i<r->cnt; i++ ) { off[s0+i] = 0UL; sz[s0+i] = 0U; }
+      j += r->cnt;
     } else {
       if( r->msg_sz ) memcpy( h + o_msg + pos, r->msg, r->msg_sz );
       for( uint32_t i=0U; i<r->cnt; i++ ) { off[s0+i] = pos; sz[s0+i] = (unsigned int)r->msg_sz; }
@@ -1390,7 +1411,7 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
      several drop-in engines submit from their callers' threads at once
      (DESIGN.md 3c), and one bulk read beats every lane reading over the
      link. */
-  int direct = nsig<=DROPIN_DIRECT_MAX && !multi && in_sz<=DROPIN_DIRECT_MAX_BYTES;
+  int direct = hsmode || ( nsig<=DROPIN_DIRECT_MAX && !multi && in_sz<=DROPIN_DIRECT_MAX_BYTES );
   unsigned char * src = direct ? dq.h_dev[k] : d;
   if( direct ) memset( h + o_out, DROPIN_PENDING, nsig );   /* no code is this value */
   fd_ed25519_pull_params_t pp;
@@ -1410,7 +1431,7 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     uint8_t *  hhf = (uint8_t *)(h + o_hhf);
     uint32_t * hs  = (uint32_t *)(h + o_hs);
     int all = 1;
-    int dbits = engine_half_dbits( e );
+    int dbits = dropin_hs_dbits ? dropin_hs_dbits : engine_half_dbits( e );
     t = 0UL;
     for( dropin_req_t * r=list; r && all; r=r->next, t++ ) {
       uint32_t rec[ 32 ];
@@ -1424,9 +1445,15 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     if( all ) {
       err = fd_ed25519_hip_private_hs_dsm( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
                                            src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs), st );
-      if( err ) { hipStreamSynchronize( st ); return err; }
-      hsdone = 1;
+    } else {   /* the device path from the digests (the messages were not staged) */
+      t = 0UL;
+      for( dropin_req_t * r=list; r; r=r->next, t++ )
+        fd_ed25519_hip_private_challenge( r->sigs, r->pubs, r->msg, r->msg_sz, h + o_dig + 64UL*tf[ t ] );
+      err = fd_ed25519_hip_verify_digests_dev( e, nsig, src + o_dig, src + o_sig, src + o_pub,
+                                               (signed char *)(src + o_out), st );
     }
+    if( err ) { hipStreamSynchronize( st ); return err; }
+    hsdone = 1;
   }
   if( !hsdone )
     err = fd_ed25519_hip_verify_dev( e, nsig_m, src + o_msg, (unsigned long const *)(src + o_off),

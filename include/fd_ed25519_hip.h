@@ -107,6 +107,14 @@ fd_ed25519_hip_dropin_set_host_hash_min( unsigned long bytes );
 void
 fd_ed25519_hip_dropin_set_host_scalars( unsigned long max_sigs );
 
+/* Test hook: the bound on |d| the calling thread's search uses (0 restores
+   the engine's, 151).  A signature whose k has no pair within it sends the
+   launch down the device path from its digest, whose own search runs at
+   the engine's bound -- the fallback a test reaches with k that have no
+   pair at 131 bits. */
+void
+fd_ed25519_hip_dropin_set_host_scalars_dbits( int dbits );
+
 unsigned long
 fd_ed25519_hip_dropin_device_bytes( void );
 

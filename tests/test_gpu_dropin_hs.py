@@ -61,3 +61,25 @@ def test_dropin_host_scalars_two_callers(ed, adversarial):
     for t in ths:
         t.join()
     assert np.array_equal(out, adversarial["codes_avx512"])
+
+
+def test_dropin_host_scalars_fallback_to_the_device_path(ed, halfsize, adversarial):
+    """A signature whose k has no pair within the host search's bound sends
+    its launch down the device path from its digest (the messages are not
+    staged in host-scalar launches).  With the host bound lowered to 131
+    bits (test hook) every halfsize.npz signature takes that fallback, whose
+    device search runs at 151 bits; the codes stay the reference's, and the
+    adversarial set (pairs within 131 bits for most) is unaffected."""
+    ed25519, lib = ed
+    lib.fd_ed25519_hip_dropin_set_host_scalars.argtypes = [ctypes.c_ulong]
+    lib.fd_ed25519_hip_dropin_set_host_scalars_dbits.argtypes = [ctypes.c_int]
+    lib.fd_ed25519_hip_dropin_set_host_scalars(4)
+    lib.fd_ed25519_hip_dropin_set_host_scalars_dbits(131)
+    try:
+        for d in (halfsize, adversarial):
+            idx = list(range(len(d["msg_sz"])))
+            got = _run(ed25519, d, idx)
+            bad = np.nonzero(got != d["codes_avx512"])[0]
+            assert len(bad) == 0, [(str(d["tags"][i]), int(got[i]), int(d["codes_avx512"][i])) for i in bad[:10]]
+    finally:
+        lib.fd_ed25519_hip_dropin_set_host_scalars_dbits(0)
