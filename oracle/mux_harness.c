@@ -180,6 +180,7 @@ struct harness {
   ulong            credit_spins;   /* producer: pauses waiting for the tiles' fseqs (a tile is behind) */
   ulong            idle_spins;     /* consumer: passes over every out link with nothing published */
   long             last_recv_tick; /* consumer: when it took the last frag it received */
+  long             prod_k0;        /* producer: its start (frag 0's due time)           */
 };
 
 static void
@@ -212,6 +213,7 @@ producer_main( void * arg ) {
   ulong chunk  = chunk0;
   double t0 = now_s();
   long   k0 = fd_tickcount();
+  h->prod_k0 = k0;   /* the stream's start: frag seq is due at k0 + seq / rate */
   double tick_per_s = h->tick_per_ns*1e9;
   ulong  cr = 0UL;   /* seq up to which the tiles have room (refreshed when used up) */
   for( ulong seq=0UL; seq<h->n && !h->stop; seq++ ) {
@@ -520,7 +522,6 @@ main( int argc, char ** argv ) {
     }
   }
   double t0 = now_s();
-  long   k0 = fd_tickcount();
   FD_TEST( !pthread_create( &tp, NULL, producer_main, h ) );
 
   /* quiescence: every frag consumed by every tile, nothing pending inside
@@ -581,10 +582,12 @@ main( int argc, char ** argv ) {
   double pmx = nl ? 1e-3*(double)h->lat_ns[ nl-1UL ] : 0.0;
   int halted_ok = 1;
   for( ulong j=0UL; j<K; j++ ) halted_ok &= h->t[j].halted==1;
-  /* the stream's own span: start to the last verified frag delivered (the
-     quiescence check after it waits up to a housekeeping interval of each
-     tile for its fseq, which is not the stream's) */
-  double delivered_s = h->last_recv_tick ? (double)(h->last_recv_tick - k0) / h->tick_per_ns * 1e-9 : t1 - t0;
+  /* the stream's own span: the producer's start (frag 0 due) to the last
+     verified frag delivered -- not the thread's start-up before it, nor the
+     quiescence check after it, which waits up to a housekeeping interval of
+     each tile for its fseq */
+  double delivered_s = h->last_recv_tick && h->prod_k0 ? (double)(h->last_recv_tick - h->prod_k0) / h->tick_per_ns * 1e-9
+                                                        : t1 - t0;
   printf( "{\"tile\": \"%s\", \"frags\": %lu, \"published\": %lu, \"seconds\": %.6f, \"txn_per_s\": %.1f, "
           "\"delivered_seconds\": %.6f, \"txn_per_s_delivered\": %.1f, "
           "\"rr_cnt\": %lu, \"rr_idx\": %lu, \"tiles_running\": %lu, \"threads\": %lu, \"pinned\": %d, \"sandbox\": %d, "

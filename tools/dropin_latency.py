@@ -54,7 +54,7 @@ def large_messages(ed25519, lib, ref, sizes, reps):
             t_cpu.append(time.perf_counter() - t)
             assert rc == 0, (sz, rc)
         out[str(sz)] = {"gpu_dropin": pct(t_gpu[2:]), "reference_cpu_one_core": pct(t_cpu[2:]),
-                        "path": "direct" if sz + 160 <= 65536 else "pull"}
+                        "path": "host scalars (message hashed on the calling thread, not staged)"}
     eng.close()
     return out
 
@@ -117,10 +117,10 @@ def main():
     res["msg_sz"] = 200
     res["large_messages"] = large_messages(ed25519, lib, ref, args.large, max(4, args.calls // 100))
     res["note"] = ("synchronous per-call latency through ctypes (~1 us of the GPU figure is the call itself); a call "
-                   "of at most 64 signatures whose staged block is at most 64 KiB (the 200-byte case) is the direct "
-                   "path: no copy launches, the kernels (prep16, dsm16) read the pinned block in place and the host "
-                   "polls the block for the codes; a larger block (large_messages past 64 KiB) is pulled into HBM "
-                   "by one device launch first and its codes pushed back by another")
+                   "of at most 4 single-signature requests (every case here) takes host scalars: the calling thread "
+                   "hashes R||A||M and finds the half-size scalars while prep16's decode blocks run, dsm16 reads them "
+                   "and the signature and key from the pinned block in place, no copy launches, and the host polls "
+                   "the block for the codes; the message is never staged for the device")
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
     print(json.dumps(res))
