@@ -36,8 +36,8 @@ def main():
         cores = tile.physical_cores(tile.device_cpus(eng.info()))
         tile.latency_set_cpus(cores[0], cores[1])
     eng.close()
-    hs_values = [None] if args.host_scalars is None else [int(x) for x in args.host_scalars.split(",")]
-    for hs, rate in [(h, float(r)) for h in hs_values for r in args.rates.split(",")]:
+    hs_values = [None] if args.host_scalars is None else [int(x) for x in args.host_scalars.replace(":", ",").split(",")]
+    for hs, rate in [(h, float(r)) for h in hs_values for r in args.rates.replace(":", ",").split(",")]:
         if hs is not None:
             tile.pipe_set_host_scalars(hs)
         pooled, batches, achieved = [], 0, []
