@@ -624,6 +624,7 @@ fd_ed25519_hip_pipe_submit_txns( fd_ed25519_hip_pipe_t * pipe, fd_ed25519_hip_sl
   slot->sig_cnt = slots; slot->msg_bytes = payload_bytes; slot->txn_cnt = txn_cnt;
   slot->seq = pipe->seq++;
   slot->t_submit = now_s();
+  s->host_combine = 0;   /* the device combines raw batches (txn_finish) */
   if( txn_cnt ) {
     /* the per-transaction offsets / sizes travel in msg_off / msg_sz; the
        device writes the per-signature ones (and the signatures and keys)
