@@ -6,7 +6,7 @@
 #   tools/gpu_step.sh OUTDIR STEP [STEP ...]
 #
 # STEP is NAME[=ARGS][@SECONDS]; ARGS is comma-separated (commas become
-# spaces):
+# spaces, then '+' becomes ',' for a list inside one argument):
 #   tests[=targets]      python -m pytest -m gpu (default: tests)
 #   smoke                __graft_entry__.smoke()
 #   bench[=args]         python bench.py args      -> OUTDIR/bench.json
@@ -32,7 +32,7 @@ for step in "$@"; do
   secs=300
   [[ $step == *@* ]] && secs=${step##*@} && step=${step%@*}
   args=""
-  [[ $step == *=* ]] && args=${step#*=} && args=${args//,/ }
+  [[ $step == *=* ]] && args=${step#*=} && args=${args//,/ } && args=${args//+/,}
   log="$out/$n-$name.log"
   echo "[$(date +%T)] step $n: $name $args (limit ${secs}s)"
   case $name in
