@@ -175,7 +175,11 @@ int fd_ed25519_hip_launch_phase( fd_ed25519_verify_params_t const * p, int phase
    k has no half-size pair within dbits (the launch then takes the device's
    own path).  hs_decode: prep16's decode blocks; hs_dsm: dsm16 with
    sflag [cap], hflag [cap], hs [19][cap] read in place (cap = the engine's
-   max_chunk).  The engine's dsm16 form must take n (n <= its r16 bound). */
+   max_chunk).  The engine's dsm16 form must take n (n <= its r16 bound).
+   Host decompressions (host/fd_ed25519_hip_hsdec.cc) for the fewest
+   signatures: hsdec_n writes each point's 20 limbs and flags as the decode
+   blocks would, and hs_dsm then reads pts [2][20][cap] and pflag [2][cap]
+   in place too (pts NULL: the decode blocks' arrays on the device). */
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -183,11 +187,15 @@ struct fd_ed25519_hip_engine;
 int fd_ed25519_hip_private_hsrec( unsigned char const sig[ 64 ], unsigned char const pub[ 32 ],
                                   unsigned char const * msg, unsigned long msg_sz, int dbits, uint32_t rec[ 32 ] );
 int fd_ed25519_hip_private_half_dbits( struct fd_ed25519_hip_engine const * e );
+int fd_ed25519_hip_private_codes_portable( struct fd_ed25519_hip_engine const * e );
 int fd_ed25519_hip_private_hs_decode( struct fd_ed25519_hip_engine * e, unsigned long n, unsigned char const * sigs,
                                       unsigned char const * pubs, signed char * out, void * stream );
 int fd_ed25519_hip_private_hs_dsm( struct fd_ed25519_hip_engine * e, unsigned long n, unsigned char const * sigs,
                                    unsigned char const * pubs, signed char * out, unsigned char const * sflag,
-                                   unsigned char const * hflag, unsigned int const * hs, void * stream );
+                                   unsigned char const * hflag, unsigned int const * hs, int const * pts,
+                                   unsigned char const * pflag, void * stream );
+void fd_ed25519_hip_private_hsdec_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
+                                     unsigned char * flags );
 #ifdef __cplusplus
 }
 #endif

@@ -726,6 +726,11 @@ fd_ed25519_hip_private_half_dbits( fd_ed25519_hip_engine_t const * e ) {
 }
 
 int
+fd_ed25519_hip_private_codes_portable( fd_ed25519_hip_engine_t const * e ) {
+  return (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
+}
+
+int
 fd_ed25519_hip_private_hs_decode( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned char const * sigs,
                                   unsigned char const * pubs, signed char * out, void * stream ) {
   fd_ed25519_verify_params_t p;
@@ -740,12 +745,14 @@ fd_ed25519_hip_private_hs_decode( fd_ed25519_hip_engine_t * e, unsigned long n, 
 int
 fd_ed25519_hip_private_hs_dsm( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned char const * sigs,
                                unsigned char const * pubs, signed char * out, unsigned char const * sflag,
-                               unsigned char const * hflag, unsigned int const * hs, void * stream ) {
+                               unsigned char const * hflag, unsigned int const * hs, int const * pts,
+                               unsigned char const * pflag, void * stream ) {
   fd_ed25519_verify_params_t p;
   int err = hs_params( e, &p, n, sigs, pubs, out );
   if( err ) return err;
-  if( !sflag || !hflag || !hs ) return FD_ED25519_HIP_ERR_INVAL;
+  if( !sflag || !hflag || !hs || !pts!=!pflag ) return FD_ED25519_HIP_ERR_INVAL;
   p.sflag = (uint8_t *)sflag; p.hflag = (uint8_t *)hflag; p.hs = (uint32_t *)hs;
+  if( pts ) { p.pts = (int32_t *)pts; p.pflag = (uint8_t *)pflag; }
   err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, stream ? (hipStream_t)stream : e->stream );
   if( err ) return hip_fail( (hipError_t)err, "verify launch" );
   return FD_ED25519_HIP_OK;
@@ -1180,6 +1187,23 @@ fd_ed25519_hip_dropin_set_host_scalars_dbits( int dbits ) {
   dropin_hs_dbits = dbits>0 && dbits<=FD_HALF_DBITS_HOST_MAX ? dbits : 0;
 }
 
+/* Launches of at most this many host-scalar signatures also decompress A
+   and R on the calling thread (host/fd_ed25519_hip_hsdec.cc; both points
+   of a signature side by side, ~9 us a signature on one core) and launch
+   dsm16 alone: the host's scalars plus decompressions then cost less than
+   the decode blocks' ~44 us they replace.  At four signatures (~70 us of
+   host work) they would not.  Test hook: fd_ed25519_hip_dropin_set_host_decode. */
+#ifndef DROPIN_HD_MAX
+#define DROPIN_HD_MAX 2UL
+#endif
+#define DROPIN_HD_CAP 4UL   /* the hook's bound: the host arrays below */
+static unsigned long dropin_hd_max = DROPIN_HD_MAX;
+
+void
+fd_ed25519_hip_dropin_set_host_decode( unsigned long max_sigs ) {
+  dropin_hd_max = max_sigs>DROPIN_HD_CAP ? DROPIN_HD_CAP : max_sigs;
+}
+
 static pthread_once_t  dropin_once = PTHREAD_ONCE_INIT;
 static pthread_mutex_t dropin_lock = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t  dropin_cv   = PTHREAD_COND_INITIALIZER;
@@ -1340,6 +1364,7 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
      without a half-size pair (~1e-6) takes the device path from its
      digest (room for nsig digests) */
   int hsmode = nsig<=dropin_hs_max && !multi && !nsig_h;
+  int hdmode = hsmode && nsig<=dropin_hd_max;
   uint64_t ndig   = hsmode ? nsig : nsig_h;
   uint64_t o_off  = 0UL;
   uint64_t o_sz   = DROPIN_ALIGN16( o_off  + 8UL*nsig );
@@ -1355,7 +1380,8 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   uint64_t need   = o_tout + n + 16UL;
   uint64_t cap_hs = e->max_chunk;
   uint64_t o_hsf = DROPIN_ALIGN16( need ), o_hhf = DROPIN_ALIGN16( o_hsf + cap_hs ), o_hs = DROPIN_ALIGN16( o_hhf + cap_hs );
-  if( hsmode ) need = o_hs + 19UL*4UL*cap_hs;
+  uint64_t o_pts = DROPIN_ALIGN16( o_hs + 19UL*4UL*cap_hs ), o_pfl = DROPIN_ALIGN16( o_pts + 2UL*20UL*4UL*cap_hs );
+  if( hsmode ) need = hdmode ? o_pfl + 2UL*cap_hs : o_hs + 19UL*4UL*cap_hs;
   if( need>dq.blk_cap[k] ) {
     uint64_t cap = dq.blk_cap[k] ? dq.blk_cap[k] : (1UL<<20);
     while( cap<need ) cap *= 2UL;
@@ -1422,11 +1448,15 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   }
   int err = FD_ED25519_HIP_OK, hsdone = 0;
   if( direct && hsmode ) {
-    /* decompressions now; the scalars on this thread meanwhile; the group
-       equation after (a signature without a half-size pair, ~1e-6, sends
-       the launch down the device's own path instead) */
-    err = fd_ed25519_hip_private_hs_decode( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out), st );
-    if( err ) { hipStreamSynchronize( st ); return err; }
+    /* decompressions now (the device's decode blocks, or this thread's
+       after the scalars for the fewest signatures); the scalars on this
+       thread meanwhile; the group equation after (a signature without a
+       half-size pair, ~1e-6, sends the launch down the device's own path
+       instead) */
+    if( !hdmode ) {
+      err = fd_ed25519_hip_private_hs_decode( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out), st );
+      if( err ) { hipStreamSynchronize( st ); return err; }
+    }
     uint8_t *  hsf = (uint8_t *)(h + o_hsf);
     uint8_t *  hhf = (uint8_t *)(h + o_hhf);
     uint32_t * hs  = (uint32_t *)(h + o_hs);
@@ -1442,9 +1472,29 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
       hsf[ j ] = (uint8_t)rec[ 27 ];
       hhf[ j ] = (uint8_t)rec[ 28 ];
     }
+    if( all && hdmode ) {   /* A and R of each signature, side by side */
+      unsigned char const * enc[ 2UL*DROPIN_HD_CAP ];
+      int32_t       pt[ 2UL*DROPIN_HD_CAP ][ 20 ];
+      unsigned char fl[ 2UL*DROPIN_HD_CAP ];
+      t = 0UL;
+      for( dropin_req_t * r=list; r; r=r->next, t++ ) { enc[ 2UL*t ] = r->pubs; enc[ 2UL*t+1UL ] = r->sigs; }
+      fd_ed25519_hip_private_hsdec_n( enc, 2UL*nsig, !(e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE), &pt[0][0], fl );
+      int32_t * pts = (int32_t *)(h + o_pts);
+      uint8_t * pfl = (uint8_t *)(h + o_pfl);
+      t = 0UL;
+      for( dropin_req_t * r=list; r; r=r->next, t++ ) {
+        uint64_t j = tf[ t ];
+        for( uint64_t which=0UL; which<2UL; which++ ) {   /* 0: A, 1: R -- the work arrays' [2][20][cap] */
+          for( uint64_t l=0UL; l<20UL; l++ ) pts[ ( which*20UL + l )*cap_hs + j ] = pt[ 2UL*t + which ][ l ];
+          pfl[ which*cap_hs + j ] = fl[ 2UL*t + which ];
+        }
+      }
+    }
     if( all ) {
       err = fd_ed25519_hip_private_hs_dsm( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
-                                           src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs), st );
+                                           src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs),
+                                           hdmode ? (int const *)(src + o_pts) : NULL,
+                                           hdmode ? src + o_pfl : NULL, st );
     } else {   /* the device path from the digests (the messages were not staged) */
       t = 0UL;
       for( dropin_req_t * r=list; r; r=r->next, t++ )

@@ -1,0 +1,300 @@
+/* fd_ed25519_hip_hsdec.cc -- a point decompression on the calling thread,
+   for the launches of a few signatures that also take their scalars from it
+   (host/fd_ed25519_hip_hsrec.cc; host/fd_ed25519_hip_engine.c dropin_run,
+   host/fd_ed25519_hip_tile.c pipe_submit_hs).
+
+   Why on the host: a decompression is one chain of ~265 dependent field
+   operations (x = u v^3 (u v^7)^((p-5)/8)).  A row of 16 lanes runs it in
+   ~44 us on the device (prep16's decode blocks, ~300 cycles a squaring,
+   profiles/r5_lanesplit_ubench.txt); one host core with 64x64->128
+   products runs it in a few us.  For a launch of one signature that chain
+   is on the call's critical path and nothing else can hide it; for the
+   throughput path (thousands of signatures a launch) the device's decode
+   kernels stay.
+
+   Same acceptance rules and the same output as decode16_wave
+   (fd_ed25519_kernels.hip) / ge_decode (fd25519_dsm.h), the reference's
+   fd_ed25519_point_frombytes + fd_ed25519_affine_is_small_order
+   (src/ballet/ed25519/fd_curve25519.h:104-170, fd_ed25519_user.c:150-175):
+     fail  : no square root, or (the AVX-512 rule) x == 0 with the sign set
+     small : x == 0, y == 0, or y one of the order-8 points' y (canonical y)
+   and the work arrays' representation: x as fe_carry of its canonical
+   bytes with the sign applied (fd25519_fe.h's centered radix-2^25.5 limbs,
+   limb for limb what the device writes), y as fe_frombytes of the encoding
+   (bit 255 dropped, values >= p kept as they are). */
+#include <stdint.h>
+#include <string.h>
+
+namespace {
+
+typedef unsigned __int128 u128;
+const uint64_t M51 = ( 1ULL << 51 ) - 1ULL;
+
+/* GF(2^255-19) in five unsigned 51-bit limbs (carried: each < 2^52) */
+struct f51 { uint64_t v[ 5 ]; };
+
+const f51 F_D      = { { 0x34dca135978a3ULL, 0x1a8283b156ebdULL, 0x5e7a26001c029ULL, 0x739c663a03cbbULL, 0x52036cee2b6ffULL } };
+const f51 F_SQRTM1 = { { 0x61b274a0ea0b0ULL, 0xd5a5fc8f189dULL, 0x7ef5e9cbd0c60ULL, 0x78595a6804c9eULL, 0x2b8324804fc1dULL } };
+
+inline uint64_t ld64( unsigned char const * p ) { uint64_t x; memcpy( &x, p, 8 ); return x; }
+
+/* bit 255 ignored, values >= p accepted */
+f51 frombytes( unsigned char const s[ 32 ] ) {
+  uint64_t w0 = ld64( s ), w1 = ld64( s+8 ), w2 = ld64( s+16 ), w3 = ld64( s+24 );
+  f51 h;
+  h.v[ 0 ] = w0 & M51;
+  h.v[ 1 ] = ( ( w0 >> 51 ) | ( w1 << 13 ) ) & M51;
+  h.v[ 2 ] = ( ( w1 >> 38 ) | ( w2 << 26 ) ) & M51;
+  h.v[ 3 ] = ( ( w2 >> 25 ) | ( w3 << 39 ) ) & M51;
+  h.v[ 4 ] = ( w3 >> 12 ) & M51;
+  return h;
+}
+
+/* column sums (each < 2^115) -> carried limbs (< 2^51, limb 1 < 2^51 + 2^15) */
+inline f51 carry( u128 const ( &t )[ 5 ] ) {
+  f51 h;
+  u128 t1 = t[ 1 ], t2 = t[ 2 ], t3 = t[ 3 ], t4 = t[ 4 ];
+  h.v[ 0 ] = (uint64_t)t[ 0 ] & M51; t1 += t[ 0 ] >> 51;
+  h.v[ 1 ] = (uint64_t)t1 & M51;     t2 += t1 >> 51;
+  h.v[ 2 ] = (uint64_t)t2 & M51;     t3 += t2 >> 51;
+  h.v[ 3 ] = (uint64_t)t3 & M51;     t4 += t3 >> 51;
+  h.v[ 4 ] = (uint64_t)t4 & M51;
+  u128 w = (u128)h.v[ 0 ] + ( t4 >> 51 ) * 19U;
+  h.v[ 0 ] = (uint64_t)w & M51;
+  h.v[ 1 ] += (uint64_t)( w >> 51 );
+  return h;
+}
+
+f51 mul( f51 const & f, f51 const & g ) {
+  uint64_t const * a = f.v, * b = g.v;
+  uint64_t b1 = b[ 1 ]*19ULL, b2 = b[ 2 ]*19ULL, b3 = b[ 3 ]*19ULL, b4 = b[ 4 ]*19ULL;
+  u128 t[ 5 ];
+  t[ 0 ] = (u128)a[ 0 ]*b[ 0 ] + (u128)a[ 1 ]*b4 + (u128)a[ 2 ]*b3 + (u128)a[ 3 ]*b2 + (u128)a[ 4 ]*b1;
+  t[ 1 ] = (u128)a[ 0 ]*b[ 1 ] + (u128)a[ 1 ]*b[ 0 ] + (u128)a[ 2 ]*b4 + (u128)a[ 3 ]*b3 + (u128)a[ 4 ]*b2;
+  t[ 2 ] = (u128)a[ 0 ]*b[ 2 ] + (u128)a[ 1 ]*b[ 1 ] + (u128)a[ 2 ]*b[ 0 ] + (u128)a[ 3 ]*b4 + (u128)a[ 4 ]*b3;
+  t[ 3 ] = (u128)a[ 0 ]*b[ 3 ] + (u128)a[ 1 ]*b[ 2 ] + (u128)a[ 2 ]*b[ 1 ] + (u128)a[ 3 ]*b[ 0 ] + (u128)a[ 4 ]*b4;
+  t[ 4 ] = (u128)a[ 0 ]*b[ 4 ] + (u128)a[ 1 ]*b[ 3 ] + (u128)a[ 2 ]*b[ 2 ] + (u128)a[ 3 ]*b[ 1 ] + (u128)a[ 4 ]*b[ 0 ];
+  return carry( t );
+}
+
+f51 sq( f51 const & f ) {
+  uint64_t const * a = f.v;
+  uint64_t a0_2 = a[ 0 ]*2ULL, a1_2 = a[ 1 ]*2ULL, a1_38 = a[ 1 ]*38ULL, a2_38 = a[ 2 ]*38ULL,
+           a3_38 = a[ 3 ]*38ULL, a3_19 = a[ 3 ]*19ULL, a4_19 = a[ 4 ]*19ULL;
+  u128 t[ 5 ];
+  t[ 0 ] = (u128)a[ 0 ]*a[ 0 ] + (u128)a1_38*a[ 4 ] + (u128)a2_38*a[ 3 ];
+  t[ 1 ] = (u128)a0_2*a[ 1 ] + (u128)a2_38*a[ 4 ] + (u128)a3_19*a[ 3 ];
+  t[ 2 ] = (u128)a0_2*a[ 2 ] + (u128)a[ 1 ]*a[ 1 ] + (u128)a3_38*a[ 4 ];
+  t[ 3 ] = (u128)a0_2*a[ 3 ] + (u128)a1_2*a[ 2 ] + (u128)a4_19*a[ 4 ];
+  t[ 4 ] = (u128)a0_2*a[ 4 ] + (u128)a1_2*a[ 3 ] + (u128)a[ 2 ]*a[ 2 ];
+  return carry( t );
+}
+
+f51 add( f51 const & f, f51 const & g ) {
+  f51 h;
+  for( int i=0; i<5; i++ ) h.v[ i ] = f.v[ i ] + g.v[ i ];
+  return h;
+}
+
+/* f - g + 4p, limb-wise non-negative for carried g (< 2^52) */
+f51 sub( f51 const & f, f51 const & g ) {
+  const uint64_t p4_0 = 0x1fffffffffffb4ULL, p4_i = 0x1ffffffffffffcULL;
+  f51 h;
+  h.v[ 0 ] = f.v[ 0 ] + p4_0 - g.v[ 0 ];
+  for( int i=1; i<5; i++ ) h.v[ i ] = f.v[ i ] + p4_i - g.v[ i ];
+  u128 t[ 5 ] = { h.v[ 0 ], h.v[ 1 ], h.v[ 2 ], h.v[ 3 ], h.v[ 4 ] };
+  return carry( t );
+}
+
+f51 one() { f51 h = { { 1ULL, 0ULL, 0ULL, 0ULL, 0ULL } }; return h; }
+
+/* canonical little-endian words (value mod p) */
+void tobytes( uint32_t out[ 8 ], f51 const & f ) {
+  u128 t[ 5 ] = { f.v[ 0 ], f.v[ 1 ], f.v[ 2 ], f.v[ 3 ], f.v[ 4 ] };
+  f51 h = carry( t );   /* h < 2^255 + 2^67 < 2p */
+  /* q = floor(h / p) in {0, 1}: h + 19 reaches 2^255 exactly when h >= p
+     (the chain is exact carry propagation whatever the limb sizes); then
+     h + 19 q mod 2^255 = h - q p */
+  uint64_t q = ( h.v[ 0 ] + 19ULL ) >> 51;
+  q = ( h.v[ 1 ] + q ) >> 51;
+  q = ( h.v[ 2 ] + q ) >> 51;
+  q = ( h.v[ 3 ] + q ) >> 51;
+  q = ( h.v[ 4 ] + q ) >> 51;
+  h.v[ 0 ] += 19ULL * q;
+  h.v[ 1 ] += h.v[ 0 ] >> 51; h.v[ 0 ] &= M51;
+  h.v[ 2 ] += h.v[ 1 ] >> 51; h.v[ 1 ] &= M51;
+  h.v[ 3 ] += h.v[ 2 ] >> 51; h.v[ 2 ] &= M51;
+  h.v[ 4 ] += h.v[ 3 ] >> 51; h.v[ 3 ] &= M51;
+  h.v[ 4 ] &= M51;
+  uint64_t w[ 4 ] = { h.v[ 0 ] | ( h.v[ 1 ] << 51 ), ( h.v[ 1 ] >> 13 ) | ( h.v[ 2 ] << 38 ),
+                      ( h.v[ 2 ] >> 26 ) | ( h.v[ 3 ] << 25 ), ( h.v[ 3 ] >> 39 ) | ( h.v[ 4 ] << 12 ) };
+  for( int i=0; i<4; i++ ) { out[ 2*i ] = (uint32_t)w[ i ]; out[ 2*i+1 ] = (uint32_t)( w[ i ] >> 32 ); }
+}
+
+bool iszero( f51 const & f ) {
+  uint32_t b[ 8 ];
+  tobytes( b, f );
+  uint32_t z = 0u;
+  for( int i=0; i<8; i++ ) z |= b[ i ];
+  return !z;
+}
+
+/* z^(2^252 - 3) for N independent elements at once: the chain is latency
+   bound (each squaring waits for the last), so N chains side by side keep
+   the core's multipliers busy -- a launch's A and R decompress in about the
+   time of one */
+template< int N >
+void sqn_n( f51 ( &f )[ N ], int n ) {
+  for( int k=0; k<n; k++ ) for( int i=0; i<N; i++ ) f[ i ] = sq( f[ i ] );
+}
+
+template< int N >
+void mul_n( f51 ( &h )[ N ], f51 const ( &f )[ N ], f51 const ( &g )[ N ] ) {
+  for( int i=0; i<N; i++ ) h[ i ] = mul( f[ i ], g[ i ] );
+}
+
+template< int N >
+void pow22523_n( f51 ( &z )[ N ] ) {
+  f51 t0[ N ], t1[ N ], t2[ N ];
+  for( int i=0; i<N; i++ ) { t0[ i ] = sq( z[ i ] ); t1[ i ] = t0[ i ]; }   /* 2         */
+  sqn_n( t1, 2 );                                                            /* 8         */
+  mul_n( t1, z, t1 );                                                        /* 9         */
+  mul_n( t0, t0, t1 );                                                       /* 11        */
+  sqn_n( t0, 1 );                                                            /* 22        */
+  mul_n( t0, t1, t0 );                                                       /* 2^5 - 1   */
+  for( int i=0; i<N; i++ ) t1[ i ] = t0[ i ];
+  sqn_n( t1, 5 );   mul_n( t0, t1, t0 );                                     /* 2^10 - 1  */
+  for( int i=0; i<N; i++ ) t1[ i ] = t0[ i ];
+  sqn_n( t1, 10 );  mul_n( t1, t1, t0 );                                     /* 2^20 - 1  */
+  for( int i=0; i<N; i++ ) t2[ i ] = t1[ i ];
+  sqn_n( t2, 20 );  mul_n( t1, t2, t1 );                                     /* 2^40 - 1  */
+  sqn_n( t1, 10 );  mul_n( t0, t1, t0 );                                     /* 2^50 - 1  */
+  for( int i=0; i<N; i++ ) t1[ i ] = t0[ i ];
+  sqn_n( t1, 50 );  mul_n( t1, t1, t0 );                                     /* 2^100 - 1 */
+  for( int i=0; i<N; i++ ) t2[ i ] = t1[ i ];
+  sqn_n( t2, 100 ); mul_n( t1, t2, t1 );                                     /* 2^200 - 1 */
+  sqn_n( t1, 50 );  mul_n( t0, t1, t0 );                                     /* 2^250 - 1 */
+  sqn_n( t0, 2 );                                                            /* 2^252 - 4 */
+  mul_n( z, t0, z );                                                         /* 2^252 - 3 */
+}
+
+/* fd25519_fe.h fe_frombytes: limb i = bits [ceil(25.5 i), ceil(25.5 (i+1))) */
+void limbs_frombytes( int32_t h[ 10 ], uint32_t const w[ 8 ] ) {
+  uint64_t v[ 4 ];
+  for( int i=0; i<4; i++ ) v[ i ] = (uint64_t)w[ 2*i ] | ( (uint64_t)w[ 2*i+1 ] << 32 );
+  static const int off[ 10 ] = { 0, 26, 51, 77, 102, 128, 153, 179, 204, 230 };
+  for( int i=0; i<10; i++ ) {
+    int o = off[ i ], wd = ( i & 1 ) ? 25 : 26;
+    uint64_t lo = v[ o >> 6 ] >> ( o & 63 );
+    if( ( o & 63 ) + wd > 64 ) lo |= v[ ( o >> 6 ) + 1 ] << ( 64 - ( o & 63 ) );
+    h[ i ] = (int32_t)( lo & ( ( 1ULL << wd ) - 1ULL ) );
+  }
+}
+
+/* fd25519_fe.h fe_carry (fe_carry_wide on biased columns), step for step */
+void limbs_carry( int32_t h[ 10 ], int32_t const f[ 10 ] ) {
+  int64_t a[ 10 ];
+  for( int i=0; i<10; i++ ) a[ i ] = (int64_t)f[ i ] + ( ( i & 1 ) ? ( 1LL << 24 ) : ( 1LL << 25 ) );
+  const int64_t m26 = ( 1LL << 26 ) - 1, m25 = ( 1LL << 25 ) - 1;
+  int64_t c;
+  c = a[ 0 ] >> 26; a[ 1 ] += c; a[ 0 ] &= m26;
+  c = a[ 4 ] >> 26; a[ 5 ] += c; a[ 4 ] &= m26;
+  c = a[ 1 ] >> 25; a[ 2 ] += c; h[ 1 ] = (int32_t)( a[ 1 ] & m25 ) - ( 1 << 24 );
+  c = a[ 5 ] >> 25; a[ 6 ] += c; h[ 5 ] = (int32_t)( a[ 5 ] & m25 ) - ( 1 << 24 );
+  c = a[ 2 ] >> 26; a[ 3 ] += c; h[ 2 ] = (int32_t)( a[ 2 ] & m26 ) - ( 1 << 25 );
+  c = a[ 6 ] >> 26; a[ 7 ] += c; h[ 6 ] = (int32_t)( a[ 6 ] & m26 ) - ( 1 << 25 );
+  c = a[ 3 ] >> 25; a[ 4 ] += c; h[ 3 ] = (int32_t)( a[ 3 ] & m25 ) - ( 1 << 24 );
+  c = a[ 7 ] >> 25; a[ 8 ] += c; h[ 7 ] = (int32_t)( a[ 7 ] & m25 ) - ( 1 << 24 );
+  c = a[ 4 ] >> 26; h[ 5 ] += (int32_t)c; h[ 4 ] = (int32_t)( a[ 4 ] & m26 ) - ( 1 << 25 );
+  c = a[ 8 ] >> 26; a[ 9 ] += c; h[ 8 ] = (int32_t)( a[ 8 ] & m26 ) - ( 1 << 25 );
+  c = a[ 9 ] >> 25; a[ 0 ] += c * 19; h[ 9 ] = (int32_t)( a[ 9 ] & m25 ) - ( 1 << 24 );
+  c = a[ 0 ] >> 26; h[ 1 ] += (int32_t)c; h[ 0 ] = (int32_t)( a[ 0 ] & m26 ) - ( 1 << 25 );
+}
+
+const uint32_t Y0[ 8 ] = { 0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u,
+                           0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du };
+const uint32_t Y1[ 8 ] = { 0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du,
+                           0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u };
+
+/* one point's decompression around the shared exponentiation */
+struct dec_state {
+  uint32_t sign;
+  f51 y, u, v, v3;
+};
+
+void dec_pre( dec_state & d, f51 & x, unsigned char const enc[ 32 ] ) {
+  uint32_t w7;
+  memcpy( &w7, enc + 28, 4 );
+  d.sign = w7 >> 31;
+  d.y = frombytes( enc );
+  f51 u = sq( d.y );
+  d.v  = add( mul( u, F_D ), one() );          /* d y^2 + 1 */
+  d.u  = sub( u, one() );                      /* y^2 - 1   */
+  d.v3 = mul( sq( d.v ), d.v );                /* v^3       */
+  x = mul( mul( sq( d.v3 ), d.v ), d.u );      /* u v^7     */
+}
+
+unsigned dec_post( dec_state const & d, f51 x, unsigned char const enc[ 32 ], int avx_rule, int32_t pt[ 20 ] ) {
+  x = mul( mul( x, d.v3 ), d.u );              /* u v^3 (u v^7)^((p-5)/8) */
+  f51 vxx = mul( sq( x ), d.v );
+  const bool root  = iszero( sub( vxx, d.u ) );
+  const bool iroot = iszero( add( vxx, d.u ) );
+  if( !root ) x = mul( x, F_SQRTM1 );
+  uint32_t xb[ 8 ];
+  tobytes( xb, x );
+  uint32_t z = 0u;
+  for( int i=0; i<8; i++ ) z |= xb[ i ];
+  const bool x0 = !z;
+  const bool fail = !( root || iroot ) || ( avx_rule && x0 && d.sign );
+  const bool neg = ( xb[ 0 ] & 1u ) != d.sign;
+  /* small order on the canonical y */
+  uint32_t yb[ 8 ];
+  tobytes( yb, d.y );
+  uint32_t zy = 0u, e0 = 0u, e1 = 0u;
+  for( int i=0; i<8; i++ ) { zy |= yb[ i ]; e0 |= yb[ i ] ^ Y0[ i ]; e1 |= yb[ i ] ^ Y1[ i ]; }
+  const bool small = x0 || !zy || !e0 || !e1;
+  /* the device's representation (decode16_wave's stores) */
+  int32_t t[ 10 ];
+  limbs_frombytes( t, xb );
+  limbs_carry( pt, t );
+  if( neg ) for( int i=0; i<10; i++ ) pt[ i ] = -pt[ i ];
+  uint32_t ew[ 8 ];
+  memcpy( ew, enc, 32 );
+  ew[ 7 ] &= 0x7fffffffu;   /* fe_frombytes drops bit 255 (limb 9 is 25 bits wide) */
+  limbs_frombytes( pt + 10, ew );
+  return ( fail ? 1u : 0u ) | ( small ? 2u : 0u );
+}
+
+template< int N >
+void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsigned char * flags ) {
+  dec_state d[ N ];
+  f51 x[ N ];
+  for( int i=0; i<N; i++ ) dec_pre( d[ i ], x[ i ], enc[ i ] );
+  pow22523_n< N >( x );
+  for( int i=0; i<N; i++ ) flags[ i ] = (unsigned char)dec_post( d[ i ], x[ i ], enc[ i ], avx_rule, pt + 20*i );
+}
+
+} /* namespace */
+
+/* enc[i]: n 32-byte point encodings (public keys and Rs).  pt: n x 20
+   int32, the work arrays' limbs of (x, y) per point; flags[i]: 1
+   FD_PF_FAIL, 2 FD_PF_SMALL (fd_ed25519_hip_internal.h).  avx_rule: the
+   AVX-512 build's codes (an engine without
+   FD_ED25519_HIP_FLAG_CODES_PORTABLE). */
+extern "C" void
+fd_ed25519_hip_private_hsdec_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
+                                unsigned char * flags ) {
+  unsigned long i = 0UL;
+  for( ; i+4UL<=n; i+=4UL ) dec_n< 4 >( enc + i, avx_rule, pt + 20UL*i, flags + i );
+  if( n-i==3UL ) dec_n< 3 >( enc + i, avx_rule, pt + 20UL*i, flags + i );
+  if( n-i==2UL ) dec_n< 2 >( enc + i, avx_rule, pt + 20UL*i, flags + i );
+  if( n-i==1UL ) dec_n< 1 >( enc + i, avx_rule, pt + 20UL*i, flags + i );
+}
+
+/* one point: returns its flags */
+extern "C" unsigned
+fd_ed25519_hip_private_hsdec( unsigned char const enc[ 32 ], int avx_rule, int32_t pt[ 20 ] ) {
+  unsigned char f;
+  fd_ed25519_hip_private_hsdec_n( &enc, 1UL, avx_rule, pt, &f );
+  return f;
+}

@@ -214,6 +214,31 @@ fd_ed25519_hip_pipe_set_host_scalars( unsigned long max_sigs ) {
   pipe_hs_max = max_sigs;
 }
 
+/* ... and batches of at most this many also decompress A and R on the
+   submitting thread (host/fd_ed25519_hip_hsdec.cc, a few us a signature,
+   against the decode blocks' ~44 us): one launch (dsm16, reading the
+   points in place) instead of two.  At the reference tile's 95% load
+   (54K txn/s, batches of 1.3-1.7 transactions) 4 beats 2: p50 0.108 /
+   p99 0.146 ms against 0.137 / 0.239 (profiles/r6_pipe_host_decode.jsonl).
+   0 turns it off (fd_ed25519_hip_pipe_set_host_decode). */
+#ifndef PIPE_HD_MAX
+#define PIPE_HD_MAX 4UL
+#endif
+#define PIPE_HD_CAP 4UL
+static unsigned long pipe_hd_max = PIPE_HD_MAX;
+
+void
+fd_ed25519_hip_pipe_set_host_decode( unsigned long max_sigs ) {
+  pipe_hd_max = max_sigs>PIPE_HD_CAP ? PIPE_HD_CAP : max_sigs;
+}
+
+/* the page-locked host-scalar block: sflag [cap], hflag [cap], hs [19][cap]
+   words, pts [2][20][cap] words, pflag [2][cap] */
+#define HS_O_HS( cap )  ( 2UL*(cap) )
+#define HS_O_PTS( cap ) ( ( 2UL + 19UL*4UL )*(cap) )
+#define HS_O_PFL( cap ) ( ( 2UL + 19UL*4UL + 2UL*20UL*4UL )*(cap) )
+#define HS_BYTES( cap ) ( ( 2UL + 19UL*4UL + 2UL*20UL*4UL + 2UL )*(cap) )
+
 struct fd_ed25519_hip_pipe {
   int           device;
   unsigned      slot_cnt;
@@ -276,7 +301,7 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   TCHK( hipMalloc(     (void **)&s->d_in,   in_sz                        ), "hipMalloc" );
   TCHK( hipHostGetDevicePointer( (void **)&s->h_in_dev, s->h_in, 0U ), "hipHostGetDevicePointer" );
   TCHK( hipHostGetDevicePointer( (void **)&s->h_outb_dev, s->h_outb, 0U ), "hipHostGetDevicePointer" );
-  TCHK( hipHostMalloc( (void **)&s->h_hs, (2UL + 19UL*4UL)*sig_cap, hipHostMallocCoherent ), "hipHostMalloc" );
+  TCHK( hipHostMalloc( (void **)&s->h_hs, HS_BYTES( sig_cap ), hipHostMallocCoherent ), "hipHostMalloc" );
   TCHK( hipHostGetDevicePointer( (void **)&s->h_hs_dev, s->h_hs, 0U ), "hipHostGetDevicePointer" );
   TCHK( hipMalloc(     (void **)&s->d_outb, out_sz                       ), "hipMalloc" );
   p->sigs        = s->h_in + o_sigs;                   s->d_sigs   = s->d_in + o_sigs;
@@ -485,12 +510,14 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
   fd_ed25519_hip_slot_t * slot = &s->pub;
   unsigned long n = slot->sig_cnt, cap = slot->sig_cap;
   unsigned long o_sigs = (unsigned long)( slot->sigs - s->h_in ), o_pubs = (unsigned long)( slot->pubs - s->h_in );
-  int err;
-  PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_decode( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
-                                                                 (signed char *)s->h_outb_dev, st ) );
-  if( err ) return err;
+  int err, hd = n<=pipe_hd_max;
+  if( !hd ) {
+    PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_decode( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
+                                                                   (signed char *)s->h_outb_dev, st ) );
+    if( err ) return err;
+  }
   unsigned char * hsf = s->h_hs, * hhf = s->h_hs + cap;
-  uint32_t *      hs  = (uint32_t *)( s->h_hs + 2UL*cap );
+  uint32_t *      hs  = (uint32_t *)( s->h_hs + HS_O_HS( cap ) );
   int dbits = fd_ed25519_hip_private_half_dbits( s->eng );
   for( unsigned long i=0UL; i<n; i++ ) {
     uint32_t rec[ 32 ];
@@ -500,10 +527,26 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
     hsf[ i ] = (unsigned char)rec[ 27 ];
     hhf[ i ] = (unsigned char)rec[ 28 ];
   }
+  if( hd ) {   /* A and R of each signature, side by side */
+    unsigned char const * enc[ 2UL*PIPE_HD_CAP ];
+    int32_t       pt[ 2UL*PIPE_HD_CAP ][ 20 ];
+    unsigned char fl[ 2UL*PIPE_HD_CAP ];
+    for( unsigned long i=0UL; i<n; i++ ) { enc[ 2UL*i ] = slot->pubs + 32UL*i; enc[ 2UL*i+1UL ] = slot->sigs + 64UL*i; }
+    fd_ed25519_hip_private_hsdec_n( enc, 2UL*n, !fd_ed25519_hip_private_codes_portable( s->eng ), &pt[0][0], fl );
+    int32_t * pts = (int32_t *)( s->h_hs + HS_O_PTS( cap ) );
+    unsigned char * pfl = s->h_hs + HS_O_PFL( cap );
+    for( unsigned long i=0UL; i<n; i++ )
+      for( unsigned long which=0UL; which<2UL; which++ ) {   /* 0: A, 1: R */
+        for( unsigned long l=0UL; l<20UL; l++ ) pts[ ( which*20UL + l )*cap + i ] = pt[ 2UL*i + which ][ l ];
+        pfl[ which*cap + i ] = fl[ 2UL*i + which ];
+      }
+  }
   PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
                                                               (signed char *)s->h_outb_dev, s->h_hs_dev,
-                                                              s->h_hs_dev + cap, (unsigned int const *)( s->h_hs_dev + 2UL*cap ),
-                                                              st ) );
+                                                              s->h_hs_dev + cap,
+                                                              (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
+                                                              hd ? (int const *)( s->h_hs_dev + HS_O_PTS( cap ) ) : NULL,
+                                                              hd ? s->h_hs_dev + HS_O_PFL( cap ) : NULL, st ) );
   if( err ) return err;
   s->host_combine = slot->txn_cnt ? 1 : 0;
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );

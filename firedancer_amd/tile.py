@@ -322,6 +322,17 @@ def pipe_set_host_scalars(max_sigs):
     _lib.fd_ed25519_hip_pipe_set_host_scalars(int(max_sigs))
 
 
+_lib.fd_ed25519_hip_pipe_set_host_decode.argtypes = [ctypes.c_ulong]
+_lib.fd_ed25519_hip_pipe_set_host_decode.restype = None
+
+
+def pipe_set_host_decode(max_sigs):
+    """fd_ed25519_hip_pipe_set_host_decode: host-scalar batches of at most
+    max_sigs signatures also decompress A and R on the submitting thread
+    (0: never; the library's default is 4)."""
+    _lib.fd_ed25519_hip_pipe_set_host_decode(int(max_sigs))
+
+
 def latency_set_cpus(producer_cpu=-1, tile_cpu=-1):
     """fd_ed25519_hip_latency_set_cpus: pin latency_run's producer and tile
     threads (one tile) to these CPUs for each run; -1 leaves one unpinned."""
@@ -579,7 +590,7 @@ _lib.fd_ed25519_hip_vservice_run.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes
                                              ctypes.POINTER(VServiceStats)]
 # the library and these ctypes mirrors must describe the same ABI
 _lib.fd_ed25519_hip_abi_check.argtypes = [ctypes.c_uint, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong]
-ABI_VERSION = 9   # FD_ED25519_HIP_ABI_VERSION
+ABI_VERSION = 10   # FD_ED25519_HIP_ABI_VERSION
 if _lib.fd_ed25519_hip_abi_check(ABI_VERSION, ctypes.sizeof(Slot), ctypes.sizeof(__import__(
         "firedancer_amd.ed25519", fromlist=["_Info"])._Info), ctypes.sizeof(VServiceStats)) != 0:
     raise ImportError("libfd_ed25519_hip ABI mismatch: " + _lib.fd_ed25519_hip_last_error().decode())

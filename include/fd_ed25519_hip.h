@@ -115,6 +115,16 @@ fd_ed25519_hip_dropin_set_host_scalars( unsigned long max_sigs );
 void
 fd_ed25519_hip_dropin_set_host_scalars_dbits( int dbits );
 
+/* The fewest-signature host-scalar launches also decompress A and R on the
+   calling thread (a few us a point on one core, against ~44 us for the
+   GPU's decode blocks, whose one 16-lane row per point is a chain of ~265
+   dependent field operations) and launch only the group equation, which
+   reads the points in place.  Test hook: launches of at most `max_sigs`
+   signatures take that path (0: never; the default is 2; at most the host
+   scalars' bound). */
+void
+fd_ed25519_hip_dropin_set_host_decode( unsigned long max_sigs );
+
 unsigned long
 fd_ed25519_hip_dropin_device_bytes( void );
 
@@ -193,7 +203,7 @@ typedef struct fd_ed25519_hip_engine fd_ed25519_hip_engine_t;
    sizeof(fd_ed25519_hip_slot_t), sizeof(fd_ed25519_hip_info_t),
    sizeof(fd_ed25519_hip_vservice_stats_t) ) returns 0 when they agree,
    FD_ED25519_HIP_ERR_INVAL (with fd_ed25519_hip_last_error) when not. */
-#define FD_ED25519_HIP_ABI_VERSION (9U)
+#define FD_ED25519_HIP_ABI_VERSION (10U)
 
 unsigned
 fd_ed25519_hip_abi_version( void );

@@ -152,6 +152,13 @@ fd_ed25519_hip_pipe_device_bytes( fd_ed25519_hip_pipe_t const * pipe );
 void
 fd_ed25519_hip_pipe_set_host_scalars( unsigned long max_sigs );
 
+/* ... and batches of at most `max_sigs` signatures also decompress A and R
+   on the submitting thread, so that one launch (the group equation) is
+   left (0: never; default 4; at most 4 and at most the host scalars'
+   bound). */
+void
+fd_ed25519_hip_pipe_set_host_decode( unsigned long max_sigs );
+
 /* ---- txn -------------------------------------------------------------- */
 
 /* The fields of fd_txn_t (src/ballet/txn/fd_txn.h) the verify tile reads. */

@@ -1,10 +1,12 @@
 """The drop-in's host-scalar launches (fd_ed25519_hip_dropin_set_host_scalars,
 host/fd_ed25519_hip_hsrec.cc): a direct launch of a few signatures takes
 k, S < L and the half-size pair from the calling thread while the GPU
-decompresses A and R, and dsm16 reads them from the page-locked block.
-Every fixture class -- the reference's vectors, the adversarial set,
+decompresses A and R, and dsm16 reads them from the page-locked block; the
+fewest-signature launches (fd_ed25519_hip_dropin_set_host_decode,
+host/fd_ed25519_hip_hsdec.cc) decompress A and R on the calling thread too
+and launch dsm16 alone, reading the points in place.  Every fixture class -- the reference's vectors, the adversarial set,
 mixed-order points, k needing long |d| -- through fd_ed25519_verify with
-the mode on (the default) and off, code by code against the reference's
+each mode on (the default) and off, code by code against the reference's
 own codes (tests/golden/, oracle/_ref)."""
 import ctypes
 import threading
@@ -22,19 +24,22 @@ def ed():
     from firedancer_amd import ed25519
     lib = ed25519.library()
     lib.fd_ed25519_hip_dropin_set_host_scalars.argtypes = [ctypes.c_ulong]
+    lib.fd_ed25519_hip_dropin_set_host_decode.argtypes = [ctypes.c_ulong]
     yield ed25519, lib
     lib.fd_ed25519_hip_dropin_set_host_scalars(4)
+    lib.fd_ed25519_hip_dropin_set_host_decode(2)
 
 
 def _run(ed25519, d, idx):
     return np.array([ed25519.verify(*case(d, i)) for i in idx], np.int8)
 
 
-@pytest.mark.parametrize("mode", [4, 0], ids=["host-scalars", "device-scalars"])
+@pytest.mark.parametrize("mode", [(4, 2), (4, 0), (0, 0)], ids=["host-scalars-decode", "host-scalars", "device"])
 @pytest.mark.parametrize("fixture", ["vectors", "adversarial", "mixed_order", "halfsize", "longd"])
-def test_dropin_codes_both_scalar_paths(ed, request, mode, fixture):
+def test_dropin_codes_every_host_path(ed, request, mode, fixture):
     ed25519, lib = ed
-    lib.fd_ed25519_hip_dropin_set_host_scalars(mode)
+    lib.fd_ed25519_hip_dropin_set_host_scalars(mode[0])
+    lib.fd_ed25519_hip_dropin_set_host_decode(mode[1])
     d = request.getfixturevalue(fixture)
     n = len(d["msg_sz"])
     idx = list(range(0, n, 3 if n > 3000 else 1))
@@ -44,23 +49,28 @@ def test_dropin_codes_both_scalar_paths(ed, request, mode, fixture):
     assert len(bad) == 0, [(str(d["tags"][idx[i]]), int(got[i]), int(want[i])) for i in bad[:10]]
 
 
-def test_dropin_host_scalars_two_callers(ed, adversarial):
-    """Two threads calling at once: their requests may combine into one
-    launch of two signatures (still a host-scalar launch) -- codes exact."""
+@pytest.mark.parametrize("callers,hd", [(2, 2), (4, 4), (4, 0)])
+def test_dropin_host_scalars_concurrent_callers(ed, adversarial, mixed_order, callers, hd):
+    """Threads calling at once: their requests may combine into launches of
+    two to four signatures (still host-scalar launches; with the host
+    decompressions up to hd of them) -- codes exact."""
     ed25519, lib = ed
     lib.fd_ed25519_hip_dropin_set_host_scalars(4)
-    n = len(adversarial["msg_sz"])
-    out = np.zeros(n, np.int8)
+    lib.fd_ed25519_hip_dropin_set_host_decode(hd)
+    for d in (adversarial, mixed_order):
+        n = min(len(d["msg_sz"]), 2000)
+        out = np.zeros(n, np.int8)
 
-    def work(par):
-        for i in range(par, n, 2):
-            out[i] = ed25519.verify(*case(adversarial, i))
-    ths = [threading.Thread(target=work, args=(p,)) for p in range(2)]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    assert np.array_equal(out, adversarial["codes_avx512"])
+        def work(par):
+            for i in range(par, n, callers):
+                out[i] = ed25519.verify(*case(d, i))
+        ths = [threading.Thread(target=work, args=(p,)) for p in range(callers)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert np.array_equal(out, d["codes_avx512"][:n])
+    lib.fd_ed25519_hip_dropin_set_host_decode(2)
 
 
 def test_dropin_host_scalars_fallback_to_the_device_path(ed, halfsize, adversarial):

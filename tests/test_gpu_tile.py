@@ -349,15 +349,19 @@ def test_pipe_stages_in_place_and_rejects_out_of_range(tile, adversarial):
     p.close()
 
 
-@pytest.mark.parametrize("hs", [4, 0], ids=["host-scalars", "device-path"])
-def test_pipe_tiny_batches_both_paths(tile, adversarial, mixed_order, batch, hs):
+@pytest.mark.parametrize("hs,hd", [(4, 2), (4, 4), (4, 0), (0, 0)],
+                         ids=["host-scalars-decode2", "host-scalars-decode4", "host-scalars", "device-path"])
+def test_pipe_tiny_batches_every_path(tile, adversarial, mixed_order, batch, hs, hd):
     """Batches of one to four signatures (a tile at a low load), through the
     host-scalar path (prep16's decode blocks + dsm16 reading the staged
-    block in place, transaction codes combined on the host) and through the
+    block in place, transaction codes combined on the host), with the
+    decompressions on the submitting thread too for batches of at most hd
+    signatures (dsm16 alone, reading the points in place), and through the
     device path: single signatures of the adversarial and mixed-order sets,
     and the batch_single_msg transactions of one to four signatures (the
     priority rule included), against the reference's codes."""
     tile.pipe_set_host_scalars(hs)
+    tile.pipe_set_host_decode(hd)
     try:
         p = tile.Pipe(0, slot_cnt=3, sig_cap=256, msg_cap=256 * 1300, txn_cap=256)
         jobs = []   # (msgs [(bytes)], sigs, pubs, txn?, want)
@@ -420,3 +424,4 @@ def test_pipe_tiny_batches_both_paths(tile, adversarial, mixed_order, batch, hs)
         assert not bad, bad[:10]
     finally:
         tile.pipe_set_host_scalars(4)
+        tile.pipe_set_host_decode(4)

@@ -20,6 +20,9 @@ into the interpreter:
   test_mux_tile.py          the tile under fd_mux_tile: parity with the
                             reference tile, liveness, protocol violations
   test_service_lifecycle.py tiles dying, restarts, parent death, SIGTERM
+  test_hsrec.py, test_hsdec.py  the drop-in's host scalars and host
+                            decompressions on every fixture's signatures and
+                            the edge encodings
 
 Every sanitizer report goes to a log file (ASAN_OPTIONS / UBSAN_OPTIONS
 log_path), from the interpreter and from every child program, so a report
@@ -36,7 +39,8 @@ import pytest
 
 from conftest import REPO
 
-SUITES = ["test_shlink.py", "test_txn.py", "test_frag_assemble.py", "test_mux_tile.py", "test_service_lifecycle.py"]
+SUITES = ["test_shlink.py", "test_txn.py", "test_frag_assemble.py", "test_mux_tile.py", "test_service_lifecycle.py", "test_hsrec.py",
+          "test_hsdec.py"]
 # gcc's combined ASan + UBSan runtime writes UBSan's reports to stderr only
 # (log_path is ignored), so each sanitizer has a build and a run of its own
 RUNTIME = {"address": ("libasan.so", "ASAN_OPTIONS", "detect_leaks=0:halt_on_error=1"),

@@ -25,6 +25,33 @@ def pct(a):
     return {"p50_us": float(np.percentile(a, 50)), "p99_us": float(np.percentile(a, 99)), "mean_us": float(a.mean())}
 
 
+def thread_scaling(ed25519, msgs, sigs, pubs, calls):
+    """fd_ed25519_verify from 1, 2, 4, 8 threads at once (the drop-in's flat
+    combining: concurrent callers share launches); calls per second over
+    all threads and the per-call p50 / p99."""
+    import threading
+    out = {}
+    for nth in (1, 2, 4, 8):
+        per = max(50, calls // nth)
+        lat = [[] for _ in range(nth)]
+
+        def run(k):
+            for j in range(per):
+                i = (k * 31 + j) % 64
+                t = time.perf_counter()
+                assert ed25519.verify(msgs[200 * i:200 * i + 200].tobytes(), sigs[i].tobytes(), pubs[i].tobytes()) == 0
+                lat[k].append(time.perf_counter() - t)
+        th = [threading.Thread(target=run, args=(k,)) for k in range(nth)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        dt = time.perf_counter() - t0
+        out[str(nth)] = dict(pct(np.concatenate([np.asarray(x) for x in lat])), calls_per_s=nth * per / dt)
+    return out
+
+
 def large_messages(ed25519, lib, ref, sizes, reps):
     """fd_ed25519_verify on one message of each size (device SHA-512: below
     the 4 GiB host-hash limit), signed on the GPU (fd_ed25519_hip_sign_dev),
@@ -65,6 +92,9 @@ def main():
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "dropin_latency.json"))
     ap.add_argument("--host-scalars", type=int, default=None,
                     help="fd_ed25519_hip_dropin_set_host_scalars (A/B; default: the library's)")
+    ap.add_argument("--host-decode", type=int, default=None,
+                    help="fd_ed25519_hip_dropin_set_host_decode (A/B; default: the library's)")
+    ap.add_argument("--threads", action="store_true", help="also the 1/2/4/8-thread scaling")
     ap.add_argument("--large", default="16384,65376,65377,1048576,8388608",
                     help="message sizes (bytes) for the device-hashed large-message latencies")
     args = ap.parse_args()
@@ -82,6 +112,10 @@ def main():
         lib.fd_ed25519_hip_dropin_set_host_scalars.argtypes = [ctypes.c_ulong]
         lib.fd_ed25519_hip_dropin_set_host_scalars(args.host_scalars)
         res["host_scalars_max_sigs"] = args.host_scalars
+    if args.host_decode is not None:
+        lib.fd_ed25519_hip_dropin_set_host_decode.argtypes = [ctypes.c_ulong]
+        lib.fd_ed25519_hip_dropin_set_host_decode(args.host_decode)
+        res["host_decode_max_sigs"] = args.host_decode
     for _ in range(20):   # warm-up: the default engine, code objects
         ed25519.verify(msgs[:200].tobytes(), sigs[0].tobytes(), pubs[0].tobytes())
     t_one = []
@@ -93,6 +127,8 @@ def main():
         t_one.append(time.perf_counter() - t)
         assert rc == 0
     res["fd_ed25519_verify_gpu_dropin"] = pct(t_one)
+    if args.threads:
+        res["thread_scaling"] = thread_scaling(ed25519, msgs, sigs, pubs, args.calls)
     # a 4-signer transaction over one message (sign the first message with 4 keys on the device)
     ref = ctypes.CDLL(os.path.join(REPO, "oracle", "_ref", "libfdref_portable.so"))
     ref.fdref_verify.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
@@ -118,9 +154,11 @@ def main():
     res["large_messages"] = large_messages(ed25519, lib, ref, args.large, max(4, args.calls // 100))
     res["note"] = ("synchronous per-call latency through ctypes (~1 us of the GPU figure is the call itself); a call "
                    "of at most 4 single-signature requests (every case here) takes host scalars: the calling thread "
-                   "hashes R||A||M and finds the half-size scalars while prep16's decode blocks run, dsm16 reads them "
-                   "and the signature and key from the pinned block in place, no copy launches, and the host polls "
-                   "the block for the codes; the message is never staged for the device")
+                   "hashes R||A||M and finds the half-size scalars; at most 2 (the one-caller case here) also "
+                   "decompresses A and R on that thread and launches dsm16 alone, which reads the scalars, points, "
+                   "signature and key from the pinned block in place (3-4: prep16's decode blocks run meanwhile); no "
+                   "copy launches, and the host polls the block for the codes; the message is never staged for the "
+                   "device")
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
     print(json.dumps(res))

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--runs", type=int, default=3)
     ap.add_argument("--host-scalars", default=None,
                     help="comma list of fd_ed25519_hip_pipe_set_host_scalars values to sweep (default: the library's)")
+    ap.add_argument("--host-decode", default=None,
+                    help="comma list of fd_ed25519_hip_pipe_set_host_decode values to sweep (default: the library's)")
     ap.add_argument("--pin", action="store_true", help="producer and tile on two physical cores of the GPU's node")
     args = ap.parse_args()
     os.environ.setdefault("GPU_MAX_HW_QUEUES", str(args.slots))
@@ -37,9 +39,13 @@ def main():
         tile.latency_set_cpus(cores[0], cores[1])
     eng.close()
     hs_values = [None] if args.host_scalars is None else [int(x) for x in args.host_scalars.replace(":", ",").split(",")]
-    for hs, rate in [(h, float(r)) for h in hs_values for r in args.rates.replace(":", ",").split(",")]:
+    hd_values = [None] if args.host_decode is None else [int(x) for x in args.host_decode.replace(":", ",").split(",")]
+    for hs, hd, rate in [(h, d, float(r)) for h in hs_values for d in hd_values
+                         for r in args.rates.replace(":", ",").split(",")]:
         if hs is not None:
             tile.pipe_set_host_scalars(hs)
+        if hd is not None:
+            tile.pipe_set_host_decode(hd)
         pooled, batches, achieved = [], 0, []
         for _ in range(args.runs):
             n = min(args.txns, max(2000, int(rate * 0.5))) if rate > 0 else args.txns
@@ -49,7 +55,7 @@ def main():
             batches += res["batches"]
             achieved.append(res["achieved_txn_per_s"])
         ms = np.concatenate(pooled)
-        print(json.dumps({"host_scalars": hs, "rate": rate, "txns": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
+        print(json.dumps({"host_scalars": hs, "host_decode": hd, "rate": rate, "txns": int(ms.size), "p50_ms": float(np.percentile(ms, 50)),
                           "p99_ms": float(np.percentile(ms, 99)), "mean_batch": ms.size / max(batches, 1),
                           "achieved_txn_per_s": float(np.mean(achieved))}), flush=True)
 
