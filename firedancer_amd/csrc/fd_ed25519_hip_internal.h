@@ -129,12 +129,25 @@ typedef struct {
                                       its decode blocks only, and dsm16's sflag / hs /
                                       hflag point at the caller's page-locked block (the
                                       same [field][cap] layout); never a full-length item */
+  uint32_t const * go;             /* dsm16 with host scalars and points: NULL, or a
+                                      page-locked word the kernel waits on before it
+                                      reads anything else -- the launch goes ahead of
+                                      the host's work, so its dispatch overlaps it.
+                                      FD_ED25519_GO_RUN: proceed; FD_ED25519_GO_CANCEL:
+                                      exit writing nothing (the launch takes another
+                                      path); unset after FD_ED25519_GO_SPIN_MAX polls
+                                      (>= 0.1 s): exit writing nothing, which the host
+                                      reports as a launch that ended without a code */
   /* A/B build only (-DFD_ED25519_AB_LDS_BASE=1): the base
      tables staged in LDS instead, [0..256)B and [0..256)[2^136]B, 32 KiB
      each, radix-2^8 unsigned digits of s' split at 2^136 */
   int32_t const *  btab8_lo;
   int32_t const *  btab8_hi;
 } fd_ed25519_verify_params_t;
+
+#define FD_ED25519_GO_RUN      1U
+#define FD_ED25519_GO_CANCEL   2U
+#define FD_ED25519_GO_SPIN_MAX 200000U
 
 /* 0: prep16 leaves the full-length items to a flag scan after dsm16 (A/B
    build) */
@@ -179,7 +192,10 @@ int fd_ed25519_hip_launch_phase( fd_ed25519_verify_params_t const * p, int phase
    Host decompressions (host/fd_ed25519_hip_hsdec.cc) for the fewest
    signatures: hsdec_n writes each point's 20 limbs and flags as the decode
    blocks would, and hs_dsm then reads pts [2][20][cap] and pflag [2][cap]
-   in place too (pts NULL: the decode blocks' arrays on the device). */
+   in place too (pts NULL: the decode blocks' arrays on the device).  go:
+   NULL, or the page-locked word dsm16 waits on (params.go): the caller
+   launches first, writes the block, then stores FD_ED25519_GO_RUN (or
+   FD_ED25519_GO_CANCEL) -- on every path, or the kernel spins to its bound. */
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -193,7 +209,7 @@ int fd_ed25519_hip_private_hs_decode( struct fd_ed25519_hip_engine * e, unsigned
 int fd_ed25519_hip_private_hs_dsm( struct fd_ed25519_hip_engine * e, unsigned long n, unsigned char const * sigs,
                                    unsigned char const * pubs, signed char * out, unsigned char const * sflag,
                                    unsigned char const * hflag, unsigned int const * hs, int const * pts,
-                                   unsigned char const * pflag, void * stream );
+                                   unsigned char const * pflag, unsigned int const * go, void * stream );
 void fd_ed25519_hip_private_hsdec_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
                                      unsigned char * flags );
 #ifdef __cplusplus

@@ -1190,10 +1190,33 @@ FD_DEV uint32_t btab16_r16(const fe& c, const r16ctx& k) {
   return (r16_from_fe(c, k) & ~k.r3) | (r16_small(2u, k) & k.r3);
 }
 
+/* params.go: one lane of the block polls the page-locked word (a relaxed
+   atomic load at system scope: a vector load that goes to the host's
+   memory each time, never a cached copy), sleeping between polls, and
+   takes the acquire fence once it is set (one cache invalidate per block,
+   not one per poll); 0 after the bound */
+FD_DEV uint32_t wait_go(const uint32_t* go) {
+  for (uint32_t spin = 0u; spin < FD_ED25519_GO_SPIN_MAX; spin++) {
+    const uint32_t g = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (g != 0u) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      return g;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  return 0u;
+}
+
 template <int BW>
 __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify_params_t p) {
   const uint64_t j = blockIdx.x;   /* a block (two waves) per signature: every return below is block-uniform */
   if (j >= p.n) return;
+  if (p.go) {   /* launched ahead of the host's scalars and points */
+    __shared__ uint32_t go;
+    if (threadIdx.x == 0u) go = wait_go(p.go);
+    __syncthreads();
+    if (go != FD_ED25519_GO_RUN) return;
+  }
   const uint32_t hf = p.hflag[j];
   const int half = (int)(threadIdx.x >> 6);   /* 0: -A and B, 1: -+R and B' */
   /* the scalars loaded first, used after the table build: with host

@@ -746,13 +746,14 @@ int
 fd_ed25519_hip_private_hs_dsm( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned char const * sigs,
                                unsigned char const * pubs, signed char * out, unsigned char const * sflag,
                                unsigned char const * hflag, unsigned int const * hs, int const * pts,
-                               unsigned char const * pflag, void * stream ) {
+                               unsigned char const * pflag, unsigned int const * go, void * stream ) {
   fd_ed25519_verify_params_t p;
   int err = hs_params( e, &p, n, sigs, pubs, out );
   if( err ) return err;
   if( !sflag || !hflag || !hs || !pts!=!pflag ) return FD_ED25519_HIP_ERR_INVAL;
   p.sflag = (uint8_t *)sflag; p.hflag = (uint8_t *)hflag; p.hs = (uint32_t *)hs;
   if( pts ) { p.pts = (int32_t *)pts; p.pflag = (uint8_t *)pflag; }
+  p.go = (uint32_t const *)go;
   err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, stream ? (hipStream_t)stream : e->stream );
   if( err ) return hip_fail( (hipError_t)err, "verify launch" );
   return FD_ED25519_HIP_OK;
@@ -1381,7 +1382,8 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   uint64_t cap_hs = e->max_chunk;
   uint64_t o_hsf = DROPIN_ALIGN16( need ), o_hhf = DROPIN_ALIGN16( o_hsf + cap_hs ), o_hs = DROPIN_ALIGN16( o_hhf + cap_hs );
   uint64_t o_pts = DROPIN_ALIGN16( o_hs + 19UL*4UL*cap_hs ), o_pfl = DROPIN_ALIGN16( o_pts + 2UL*20UL*4UL*cap_hs );
-  if( hsmode ) need = hdmode ? o_pfl + 2UL*cap_hs : o_hs + 19UL*4UL*cap_hs;
+  uint64_t o_go  = DROPIN_ALIGN16( o_pfl + 2UL*cap_hs );
+  if( hsmode ) need = hdmode ? o_go + 16UL : o_hs + 19UL*4UL*cap_hs;
   if( need>dq.blk_cap[k] ) {
     uint64_t cap = dq.blk_cap[k] ? dq.blk_cap[k] : (1UL<<20);
     while( cap<need ) cap *= 2UL;
@@ -1448,13 +1450,25 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   }
   int err = FD_ED25519_HIP_OK, hsdone = 0;
   if( direct && hsmode ) {
-    /* decompressions now (the device's decode blocks, or this thread's
-       after the scalars for the fewest signatures); the scalars on this
-       thread meanwhile; the group equation after (a signature without a
-       half-size pair, ~1e-6, sends the launch down the device's own path
-       instead) */
+    /* the device's decompressions now and the group equation after the
+       scalars this thread computes meanwhile -- or, for the fewest
+       signatures, the group equation launched first, waiting, and this
+       thread's scalars and decompressions while it is dispatched (a
+       signature without a half-size pair, ~1e-6, sends the launch down the
+       device's own path instead) */
+    volatile uint32_t * go = (volatile uint32_t *)(h + o_go);
     if( !hdmode ) {
       err = fd_ed25519_hip_private_hs_decode( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out), st );
+      if( err ) { hipStreamSynchronize( st ); return err; }
+    } else {
+      /* dsm16 goes first and waits on the go word (params.go), so its
+         dispatch overlaps this thread's scalars and decompressions; from
+         here every path stores RUN or CANCEL */
+      *go = 0U;
+      err = fd_ed25519_hip_private_hs_dsm( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
+                                           src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs),
+                                           (int const *)(src + o_pts), src + o_pfl,
+                                           (unsigned int const *)(src + o_go), st );
       if( err ) { hipStreamSynchronize( st ); return err; }
     }
     uint8_t *  hsf = (uint8_t *)(h + o_hsf);
@@ -1490,12 +1504,12 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
         }
       }
     }
-    if( all ) {
+    if( hdmode ) __atomic_store_n( go, all ? FD_ED25519_GO_RUN : FD_ED25519_GO_CANCEL, __ATOMIC_RELEASE );
+    if( all && !hdmode ) {
       err = fd_ed25519_hip_private_hs_dsm( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
-                                           src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs),
-                                           hdmode ? (int const *)(src + o_pts) : NULL,
-                                           hdmode ? src + o_pfl : NULL, st );
-    } else {   /* the device path from the digests (the messages were not staged) */
+                                           src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs), NULL, NULL,
+                                           NULL, st );
+    } else if( !all ) {   /* the device path from the digests (the messages were not staged) */
       t = 0UL;
       for( dropin_req_t * r=list; r; r=r->next, t++ )
         fd_ed25519_hip_private_challenge( r->sigs, r->pubs, r->msg, r->msg_sz, h + o_dig + 64UL*tf[ t ] );

@@ -233,11 +233,12 @@ fd_ed25519_hip_pipe_set_host_decode( unsigned long max_sigs ) {
 }
 
 /* the page-locked host-scalar block: sflag [cap], hflag [cap], hs [19][cap]
-   words, pts [2][20][cap] words, pflag [2][cap] */
+   words, pts [2][20][cap] words, pflag [2][cap], the go word (params.go) */
 #define HS_O_HS( cap )  ( 2UL*(cap) )
 #define HS_O_PTS( cap ) ( ( 2UL + 19UL*4UL )*(cap) )
 #define HS_O_PFL( cap ) ( ( 2UL + 19UL*4UL + 2UL*20UL*4UL )*(cap) )
-#define HS_BYTES( cap ) ( ( 2UL + 19UL*4UL + 2UL*20UL*4UL + 2UL )*(cap) )
+#define HS_O_GO( cap )  ( ( ( 2UL + 19UL*4UL + 2UL*20UL*4UL + 2UL )*(cap) + 15UL ) & ~15UL )
+#define HS_BYTES( cap ) ( HS_O_GO( cap ) + 16UL )
 
 struct fd_ed25519_hip_pipe {
   int           device;
@@ -502,18 +503,34 @@ slot_check( fd_ed25519_hip_slot_t const * slot, unsigned long sig_cnt, unsigned 
 
 /* A host-scalar batch (PIPE_HS_MAX above): the decompressions launched
    first, the scalars computed meanwhile, then dsm16 writing the signature
-   codes into the page-locked output block.  1: submitted; 0: a signature
-   has no half-size pair (~1e-6), nothing but the decode launch was queued
-   and the caller takes the device's own path; < 0: a launch failed. */
+   codes into the page-locked output block -- or (PIPE_HD_MAX) dsm16
+   launched first, waiting on the go word, and the scalars and
+   decompressions computed while it is dispatched.  1: submitted; 0: a
+   signature has no half-size pair (~1e-6), nothing but the decode launch
+   (or a cancelled dsm16) was queued and the caller takes the device's own
+   path; < 0: a launch failed. */
 static int
 pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) {
   fd_ed25519_hip_slot_t * slot = &s->pub;
   unsigned long n = slot->sig_cnt, cap = slot->sig_cap;
   unsigned long o_sigs = (unsigned long)( slot->sigs - s->h_in ), o_pubs = (unsigned long)( slot->pubs - s->h_in );
   int err, hd = n<=pipe_hd_max;
+  volatile uint32_t * go = (volatile uint32_t *)( s->h_hs + HS_O_GO( cap ) );
   if( !hd ) {
     PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_decode( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
                                                                    (signed char *)s->h_outb_dev, st ) );
+    if( err ) return err;
+  } else {
+    /* dsm16 first, waiting on the go word while this thread computes
+       (params.go); every path below stores RUN or CANCEL */
+    *go = 0U;
+    PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
+                                                                (signed char *)s->h_outb_dev, s->h_hs_dev,
+                                                                s->h_hs_dev + cap,
+                                                                (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
+                                                                (int const *)( s->h_hs_dev + HS_O_PTS( cap ) ),
+                                                                s->h_hs_dev + HS_O_PFL( cap ),
+                                                                (unsigned int const *)( s->h_hs_dev + HS_O_GO( cap ) ), st ) );
     if( err ) return err;
   }
   unsigned char * hsf = s->h_hs, * hhf = s->h_hs + cap;
@@ -522,7 +539,10 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
   for( unsigned long i=0UL; i<n; i++ ) {
     uint32_t rec[ 32 ];
     if( !fd_ed25519_hip_private_hsrec( slot->sigs + 64UL*i, slot->pubs + 32UL*i, slot->msgs + slot->msg_off[ i ],
-                                       slot->msg_sz[ i ], dbits, rec ) ) return 0;
+                                       slot->msg_sz[ i ], dbits, rec ) ) {
+      if( hd ) __atomic_store_n( go, FD_ED25519_GO_CANCEL, __ATOMIC_RELEASE );
+      return 0;
+    }
     for( int w=0; w<19; w++ ) hs[ (unsigned long)w*cap + i ] = rec[ 8 + w ];
     hsf[ i ] = (unsigned char)rec[ 27 ];
     hhf[ i ] = (unsigned char)rec[ 28 ];
@@ -541,13 +561,16 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
         pfl[ which*cap + i ] = fl[ 2UL*i + which ];
       }
   }
-  PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
-                                                              (signed char *)s->h_outb_dev, s->h_hs_dev,
-                                                              s->h_hs_dev + cap,
-                                                              (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
-                                                              hd ? (int const *)( s->h_hs_dev + HS_O_PTS( cap ) ) : NULL,
-                                                              hd ? s->h_hs_dev + HS_O_PFL( cap ) : NULL, st ) );
-  if( err ) return err;
+  if( hd ) {
+    __atomic_store_n( go, FD_ED25519_GO_RUN, __ATOMIC_RELEASE );
+  } else {
+    PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
+                                                                (signed char *)s->h_outb_dev, s->h_hs_dev,
+                                                                s->h_hs_dev + cap,
+                                                                (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
+                                                                NULL, NULL, NULL, st ) );
+    if( err ) return err;
+  }
   s->host_combine = slot->txn_cnt ? 1 : 0;
   TCHK( hipEventRecord( s->ev, st ), "hipEventRecord" );
 #ifdef FD_ED25519_HIP_AB_STAGE_TRACE
