@@ -341,6 +341,43 @@ def sustained_rate(run_at, unpaced, steps=5, lo_frac=0.5, keep=0.99):
     return lo, trail
 
 
+class keep_off:
+    """For the with-block, every thread of this process (and the children
+    started with `child_mask`) off the CPUs the latency legs' spinning
+    threads are pinned to: the Python main thread and the HIP runtime's
+    helper threads float over the node otherwise, and one of them woken
+    on a spinning thread's core takes a scheduler slice from it -- a
+    stall of milliseconds in the middle of a run (one run in ~15 of the
+    deployed leg held such an episode).  Restored afterwards; a no-op with
+    --no-isolate-cores or when the node has no CPU to spare."""
+
+    def __init__(self, spin, node, enabled):
+        others = sorted(set(node) - set(spin)) if spin else []
+        self.mask = others if enabled and others else None
+        self.saved = {}
+
+    def child_mask(self, node):
+        return self.mask or node
+
+    def __enter__(self):
+        if self.mask:
+            for t in os.listdir("/proc/self/task"):
+                try:
+                    self.saved[int(t)] = os.sched_getaffinity(int(t))
+                    os.sched_setaffinity(int(t), self.mask)
+                except OSError:   # a thread that ended meanwhile
+                    pass
+        return self
+
+    def __exit__(self, *exc):
+        for t, m in self.saved.items():
+            try:
+                os.sched_setaffinity(t, m)
+            except OSError:
+                pass
+        return False
+
+
 def latency_mode(eng, args, device):
     """C5: the verify tile's latency mode.  Signed single-signer Solana
     transactions (~200-byte messages, GPU-signed) are published into a
@@ -369,9 +406,10 @@ def latency_mode(eng, args, device):
         ok &= bool((v == 0).all())
         return res["achieved_txn_per_s"]
 
+    spin = cores[:2] if args.pin_threads and len(cores) >= 2 else None
     try:
-        return latency_mode_loads(args, run_at, pay, n, device, lambda: ok,
-                                  cores[:2] if args.pin_threads and len(cores) >= 2 else None)
+        with keep_off(spin, tile.device_cpus(eng.info()), args.isolate_cores):
+            return latency_mode_loads(args, run_at, pay, n, device, lambda: ok, spin)
     finally:
         tile.latency_set_cpus(-1, -1)
 
@@ -383,6 +421,7 @@ def latency_mode_loads(args, run_at, pay, n, device, verdicts_ok, cpus):
     out = {"batch_sigs": args.latency_batch, "slots_in_flight": args.latency_slots,
            "threads": (f"producer on CPU {cpus[0]}, tile on CPU {cpus[1]} (physical cores of the GPU's node)"
                        if cpus else "unpinned"),
+           "other_threads": ("kept off those cores" if cpus and args.isolate_cores else "anywhere on the node"),
            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES") or 4), "txns_per_run": n,
            "msg_sz": 200, "peak_txn_per_s": peak, "peak": SUSTAINED_PEAK, "peak_search": trail,
            "unpaced_median_txn_per_s": float(np.median(unpaced)), "unpaced_runs_txn_per_s": unpaced,
@@ -467,9 +506,11 @@ def latency_deployed(eng, args):
     harness_cpus = ["--cpus", ",".join(map(str, cores[:3]))] if per_thread else []
     service_cpus = ["--cpus", str(cores[3])] if per_thread else []
 
+    iso = keep_off(cores[:4] if per_thread else None, node, args.isolate_cores)
+
     def pin():
         if node:
-            os.sched_setaffinity(0, node)
+            os.sched_setaffinity(0, iso.child_mask(node))
 
     def delivered(r):
         """a run's achieved rate: its frags over the span from its start to
@@ -570,11 +611,12 @@ def latency_deployed(eng, args):
                         "max_ms": float(ms.max()), "samples": int(ms.size), "percentiles": f"pooled over {runs} runs"})
         return out
     try:
-        hip = sweep("verify_hip", 5, n)
-        ref = sweep("verify", 2, n_ref)
-        rp = ref["peak_txn_per_s"]
-        matched = at_rates([(f"{f:g} x reference tile peak", f * rp) for f in (0.5, 0.8, 0.95, 10.0, 100.0)],
-                           args.deployed_matched_runs) if args.deployed_matched_runs > 0 else None
+        with iso:
+            hip = sweep("verify_hip", 5, n)
+            ref = sweep("verify", 2, n_ref)
+            rp = ref["peak_txn_per_s"]
+            matched = at_rates([(f"{f:g} x reference tile peak", f * rp) for f in (0.5, 0.8, 0.95, 10.0, 100.0)],
+                               args.deployed_matched_runs) if args.deployed_matched_runs > 0 else None
     finally:
         for f in os.listdir(tmp):
             os.unlink(os.path.join(tmp, f))
@@ -584,6 +626,7 @@ def latency_deployed(eng, args):
                 "cpus": f"{len(node)} CPUs of the GPU's NUMA node (service and harness pinned)" if node else "unpinned",
                 "threads": (f"harness producer / consumer / tile on CPUs {cores[:3]}, service link thread on CPU "
                             f"{cores[3]} (physical cores)" if per_thread else "not pinned per thread"),
+                "other_threads": "kept off those cores" if iso.mask else "anywhere on the node",
                 "service_mode": args.deployed_mode, "msg_sz": 200,
                 "path": "producer -> quic_verify mcache/dcache (reference tango) -> fd_tile_verify_hip under the "
                         "reference's fd_mux_tile, its seccomp filter installed -> shlink -> fd_verify_hip_service "
@@ -1040,6 +1083,9 @@ def main():
     ap.add_argument("--dev-kernargs", action="store_true",
                     help="leave HIP's kernel arguments in device memory (its default on this GPU; A/B)")
     ap.add_argument("--latency-txns", type=int, default=400000, help="0 disables the latency mode")
+    ap.add_argument("--no-isolate-cores", dest="isolate_cores", action="store_false",
+                    help="latency legs: leave this process's other threads and the children's unpinned ones free "
+                         "to run on the spinning threads' cores (A/B)")
     ap.add_argument("--no-pin-threads", dest="pin_threads", action="store_false",
                     help="C5 legs: leave the producer / tile / service threads unpinned (A/B)")
     ap.add_argument("--deployed-txns", type=int, default=300000,
