@@ -343,16 +343,20 @@ def sustained_rate(run_at, unpaced, steps=5, lo_frac=0.5, keep=0.99):
 
 class keep_off:
     """For the with-block, every thread of this process (and the children
-    started with `child_mask`) off the CPUs the latency legs' spinning
-    threads are pinned to: the Python main thread and the HIP runtime's
-    helper threads float over the node otherwise, and one of them woken
-    on a spinning thread's core takes a scheduler slice from it -- a
-    stall of milliseconds in the middle of a run (one run in ~15 of the
-    deployed leg held such an episode).  Restored afterwards; a no-op with
-    --no-isolate-cores or when the node has no CPU to spare."""
+    started with `child_mask`) off the physical cores the latency legs'
+    spinning threads are pinned to, SMT siblings included: the Python main
+    thread and the HIP runtime's helper threads float over the node
+    otherwise, and one of them woken on a spinning thread's CPU takes a
+    scheduler slice from it (a pause of milliseconds), or on its sibling
+    halves its speed for a while (the path delivering at half the offered
+    rate for ~10 ms: tools/episode_shape.py, profiles/r6_c5_episodes.txt).
+    Restored afterwards; a no-op with --no-isolate-cores or when the node
+    has no CPU to spare."""
 
     def __init__(self, spin, node, enabled):
-        others = sorted(set(node) - set(spin)) if spin else []
+        from firedancer_amd import tile
+        busy = set().union(*(tile.core_siblings(c) for c in spin)) if spin else set()
+        others = sorted(set(node) - busy) if spin else []
         self.mask = others if enabled and others else None
         self.saved = {}
 
@@ -421,7 +425,8 @@ def latency_mode_loads(args, run_at, pay, n, device, verdicts_ok, cpus):
     out = {"batch_sigs": args.latency_batch, "slots_in_flight": args.latency_slots,
            "threads": (f"producer on CPU {cpus[0]}, tile on CPU {cpus[1]} (physical cores of the GPU's node)"
                        if cpus else "unpinned"),
-           "other_threads": ("kept off those cores" if cpus and args.isolate_cores else "anywhere on the node"),
+           "other_threads": ("kept off those cores and their SMT siblings" if cpus and args.isolate_cores
+                             else "anywhere on the node"),
            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES") or 4), "txns_per_run": n,
            "msg_sz": 200, "peak_txn_per_s": peak, "peak": SUSTAINED_PEAK, "peak_search": trail,
            "unpaced_median_txn_per_s": float(np.median(unpaced)), "unpaced_runs_txn_per_s": unpaced,
@@ -555,6 +560,10 @@ def latency_deployed(eng, args):
         res = json.loads(p.stdout.strip().splitlines()[-1])
         lat = np.fromfile(lat_path, np.uint32).astype(np.float64) * 1e-6
         os.unlink(lat_path)
+        keep = os.environ.get("FD_BENCH_LAT_DIR")   # tail analysis (tools/episode_shape.py): every run's samples
+        if keep:
+            os.makedirs(keep, exist_ok=True)
+            np.save(os.path.join(keep, f"{kind}_{int(rate)}_{app}.npy"), lat.astype(np.float32))
         return res, lat
 
     def sweep(kind, runs, txns):
@@ -626,7 +635,7 @@ def latency_deployed(eng, args):
                 "cpus": f"{len(node)} CPUs of the GPU's NUMA node (service and harness pinned)" if node else "unpinned",
                 "threads": (f"harness producer / consumer / tile on CPUs {cores[:3]}, service link thread on CPU "
                             f"{cores[3]} (physical cores)" if per_thread else "not pinned per thread"),
-                "other_threads": "kept off those cores" if iso.mask else "anywhere on the node",
+                "other_threads": "kept off those cores and their SMT siblings" if iso.mask else "anywhere on the node",
                 "service_mode": args.deployed_mode, "msg_sz": 200,
                 "path": "producer -> quic_verify mcache/dcache (reference tango) -> fd_tile_verify_hip under the "
                         "reference's fd_mux_tile, its seccomp filter installed -> shlink -> fd_verify_hip_service "

@@ -354,6 +354,19 @@ def physical_cores(cpus):
     return out
 
 
+def core_siblings(cpu):
+    """every logical CPU of cpu's physical core (cpu itself without SMT)"""
+    try:
+        txt = open(f"/sys/devices/system/cpu/cpu{cpu}/topology/thread_siblings_list").read().strip()
+    except OSError:
+        return {cpu}
+    out = set()
+    for part in txt.split(","):
+        a, _, b = part.partition("-")
+        out.update(range(int(a), int(b or a) + 1))
+    return out or {cpu}
+
+
 def latency_run(payloads, offered_txn_per_s, device=0, slot_cnt=3, batch_sigs=256, ring_depth=4096, gpu_parse=False,
                 tiles=1):
     """Latency mode (C5): a producer thread publishes the payloads into a
