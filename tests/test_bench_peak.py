@@ -32,3 +32,42 @@ def test_sustained_rate_never_exceeds_the_unpaced_median():
 def test_sustained_rate_stays_at_the_floor_when_nothing_holds():
     rate, trail = bench.sustained_rate(lambda r: 0.5 * r, 3.0e6)
     assert rate == 1.5e6 and all(t[1] < 0.99 for t in trail)
+
+
+def test_keep_off_moves_every_thread_and_restores():
+    """bench.keep_off: inside the block every thread of this process (one
+    started before it too) runs off the spinning cores and their SMT
+    siblings, children get the same mask, and the old masks come back."""
+    import threading
+    from firedancer_amd import tile
+    node = sorted(os.sched_getaffinity(0))
+    if len(tile.physical_cores(node)) < 2:
+        import pytest
+        pytest.skip("one physical core")
+    spin = tile.physical_cores(node)[:1]
+    busy = tile.core_siblings(spin[0])
+    stop = threading.Event()
+    th = threading.Thread(target=stop.wait)
+    th.start()
+    before = {int(t): os.sched_getaffinity(int(t)) for t in os.listdir("/proc/self/task")}
+    try:
+        with bench.keep_off(spin, node, True) as iso:
+            assert iso.child_mask(node) == sorted(set(node) - busy)
+            for t in os.listdir("/proc/self/task"):
+                assert not (os.sched_getaffinity(int(t)) & busy), t
+        for t, m in before.items():
+            assert os.sched_getaffinity(t) == m
+        with bench.keep_off(spin, node, False) as iso:   # --no-isolate-cores
+            assert iso.child_mask(node) == node
+            assert os.sched_getaffinity(0) == before[os.getpid()]
+    finally:
+        stop.set()
+        th.join()
+
+
+def test_core_siblings_parses_the_topology():
+    from firedancer_amd import tile
+    for c in sorted(os.sched_getaffinity(0))[:4]:
+        sib = tile.core_siblings(c)
+        assert c in sib and all(tile.core_siblings(x) == sib for x in sib if os.path.exists(
+            f"/sys/devices/system/cpu/cpu{x}/topology/thread_siblings_list"))
