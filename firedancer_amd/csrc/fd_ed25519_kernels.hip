@@ -1298,6 +1298,125 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
 }
 
 /* ------------------------------------------------------------------------
+   dsm16q: dsm16's equation over four waves, for the launches whose points
+   the host computed (host/fd_ed25519_hip_hsdec.cc): with A' = [2^66]A and
+   R' = [2^66]R from the host too, each half-size scalar splits at bit 66,
+   c = c0 + 2^66 c1 and |d| = d0 + 2^66 d1, and s' at bits 72, 144, 216:
+
+     [c0](-A) + [c1](-A') + [d0](-+R) + [d1](-+R')
+       + [s'_0]B + [s'_1][2^72]B + [s'_2][2^144]B + [s'_3][2^216]B == 0
+
+   exactly (A' and R' are the points themselves doubled 66 times, so no
+   reduction of c or d is involved).  Wave q holds one variable-base term
+   and one base term: W = 17 windows of 4 doublings instead of 33 (|d| of
+   up to 151 bits: up to 22), the base digits radix 2^16 from the compact
+   tables at the four offsets (params.btabq), five at windows 16, 12, .., 0.
+   Waves 1-3 hand their points to wave 0 through LDS.  Inputs (host
+   memory, params.go's launch-ahead): pts [4][20][cap] (A, R, A', R'),
+   pflag [2][cap], sflag, hflag [cap], hs [24][cap]: rows 3q..3q+2 the
+   scalar of wave q (c0, c1, d0, d1), rows 12+3q..14+3q its 72-bit chunk
+   of s'. */
+__global__ void __launch_bounds__(256) fd_ed25519_dsm16q_kernel(fd_ed25519_verify_params_t p) {
+  const uint64_t j = blockIdx.x;   /* a block (four waves) per signature: every return below is block-uniform */
+  if (j >= p.n) return;
+  if (p.go) {
+    __shared__ uint32_t go;
+    if (threadIdx.x == 0u) go = wait_go(p.go);
+    __syncthreads();
+    if (go != FD_ED25519_GO_RUN) return;
+  }
+  const uint32_t hf = p.hflag[j];
+  const int q = (int)(threadIdx.x >> 6);   /* 0: c0 (-A), 1: c1 (-A'), 2: d0 (-+R), 3: d1 (-+R') */
+  uint32_t hk[5] = {0u, 0u, 0u, 0u, 0u}, hb[5] = {0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int w = 0; w < 3; w++) {
+    hk[w] = p.hs[(uint64_t)(3 * q + w) * p.cap + j];
+    hb[w] = p.hs[(uint64_t)(12 + 3 * q + w) * p.cap + j];
+  }
+  /* the block's window count: the longest of the four scalars (every wave
+     reads them all, so W is the same in each without a barrier) */
+  int W = 17;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    uint32_t x[5] = {0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int w = 0; w < 3; w++) x[w] = p.hs[(uint64_t)(3 * t + w) * p.cap + j];
+    const int wt = (fd_half_bitlen<5>(x) + 4) >> 2;
+    W = wt > W ? wt : W;
+  }
+  W = __builtin_amdgcn_readfirstlane(W);
+  r16ctx k;
+  r16_init(k);
+  const uint32_t d2 = r16_from_fe(fe{FE_D2}, k);
+  uint32_t tab[9];
+  {
+    fe x, y;
+    const int which = q == 0 ? 0 : q == 1 ? 2 : q == 2 ? 1 : 3;   /* pts rows: A, R, A', R' */
+    const int32_t* src = p.pts + (uint64_t)which * 20 * p.cap + j;
+    load_fe(x, src, p.cap);
+    load_fe(y, src + 10 * p.cap, p.cap);
+    table16_build(tab, r16_from_fe(x, k), r16_from_fe(y, k), q < 2 ? true : !(hf & FD_HF_DNEG), d2, k);
+  }
+  uint32_t sd[5], bd[5];
+  {
+    uint32_t t[5], u[5];
+    shl160<64>(u, hk);                       /* W in [17, 22]: 160 - 4W - 64 in [8, 28] */
+    shl160v(t, u, 160 - 4 * W - 64);
+    recode160<4>(sd, t);
+    shl160<80>(bd, hb);                      /* five 16-bit digits, the top one first */
+  }
+  const int32_t* btab = p.btabq[q];
+  const uint32_t one = r16_small(1u, k);
+  uint32_t P = one & k.r12;   /* identity (0, 1, 1, 0) */
+#pragma clang loop unroll(disable)
+  for (int it = W - 1; it >= 0; it--) {
+    int e = pop160<4>(sd);
+    if (it == W - 1) e &= 15;
+    e = __builtin_amdgcn_readfirstlane(e);
+    const bool badd = it <= 16 && (it & 3) == 0;
+    const uint32_t bdig = (uint32_t)__builtin_amdgcn_readfirstlane((int)(badd ? pop160u<16>(bd) : 0u));
+    const uint32_t ce = table16_at(tab, e < 0 ? -e : e);
+    fe braw;
+    if (badd) braw = btab16_fetch(btab, (int)bdig, k);
+    if (it != W - 1) {
+      P = ge16_dbl2<false, false>(P, k);
+      P = ge16_dbl2<true, false>(P, k);
+      P = ge16_dbl2<true, false>(P, k);
+      P = ge16_dbl2<true, true>(P, k);
+    }
+    uint32_t b = 0u;
+    if (badd) b = btab16_r16(braw, k);
+    if (e != 0) {
+      P = ge16_cneg4(P, k.r03, e < 0, k);
+      P = ge16_add2<true>(P, ce, e < 0, k);
+    }
+    if (badd) P = ge16_add2<true>(P, b, false, k);
+  }
+  /* waves 1-3's points as addends of wave 0's */
+  __shared__ uint32_t hand[3][64];
+  if (q) hand[q - 1][threadIdx.x & 63u] = ge16_to_qc(P, d2, k);
+  __syncthreads();
+  if (q) return;
+#pragma unroll
+  for (int t = 0; t < 3; t++) P = ge16_add2<true>(P, hand[t][threadIdx.x], false, k);
+  const uint32_t z = r16_rp<2, 2, 2, 2>(P, k);
+  const bool zero = r16_iszero(P + ((k.p4 - z) & k.r1));
+  const uint64_t bal = __ballot(zero);
+  const bool ident = (bal & 1ull) && (bal & (1ull << 16));
+  int code = precheck(p, j);
+  if (code == FD_PENDING) code = ident ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  /* the code last (dsm16's write-code-last invariant) */
+  if (threadIdx.x == 0u) p.out[p.base + j] = (int8_t)code;
+}
+
+extern "C" int fd_ed25519_hip_launch_dsm16q(const fd_ed25519_verify_params_t* p, void* stream) {
+  if (!p->n) return 0;
+  if (!p->btabq[0] || !p->btabq[1] || !p->btabq[2] || !p->btabq[3]) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(fd_ed25519_dsm16q_kernel, dim3((uint32_t)p->n), dim3(256), 0, (hipStream_t)stream, *p);
+  return (int)hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------
    prep16: the dsm16 chunks' prep, with the decompressions spread over the
    lanes as dsm16's products are.  The one-lane decode is a chain of 250
    dependent squarings (~490 cycles each, fe_sq_u); a row of 16 lanes runs

@@ -50,6 +50,7 @@ struct fd_ed25519_hip_engine {
   int32_t *    d_btab16;     /* [0..2^15]B, the verify kernels' wide B table  */
   int32_t *    d_btab8[2];   /* A/B build only (FD_ED25519_AB_LDS_BASE): the LDS-staged tables */
   int32_t *    btabw[2];    /* shared per device: [0..2^24)B, [0..2^24)[2^144]B */
+  int32_t *    btabq[4];    /* shared per device, engines with the r16 form: [0..2^16)[2^(72 q)]B (dsm16q) */
   /* Pipeline lanes: the per-chunk scratch of a chunk in flight, and the
      streams its phases run on.  Lane 0 runs on the caller's stream (or the
      engine's); the chunks of a multi-chunk call alternate between lane 0
@@ -190,12 +191,57 @@ btabw_acquire( int device, int kind, hipStream_t stream, int32_t * tab[2] ) {
   return rc;
 }
 
+/* dsm16q's four compact tables at offsets 2^0, 2^72, 2^144, 2^216 (8 MiB
+   each), shared per device like the pairs above, by every engine whose
+   launch forms include the r16 one (its host-decoded launches) */
+#define FD_ED25519_BTABQ_SHIFT 72
+static struct { int refs; int32_t * tab[4]; } btabq[ FD_ED25519_HIP_MAX_DEV ];
+
+static int
+btabq_acquire( int device, hipStream_t stream, int32_t * tab[4] ) {
+  pthread_mutex_lock( &btabw_lock );
+  int rc = FD_ED25519_HIP_OK;
+  if( !btabq[device].refs ) {
+    int32_t * t[4] = { NULL, NULL, NULL, NULL };
+    int32_t * scratch = NULL;
+    hipError_t he = hipSuccess;
+    for( int q=0; q<4 && he==hipSuccess; q++ ) he = hipMalloc( (void **)&t[q], btabw_bytes( 1 ) );
+    if( he==hipSuccess ) he = hipMalloc( (void **)&scratch, sizeof(int32_t) * (((size_t)1 << FD_ED25519_BTABC_BITS) * 10 + 64) );
+    for( int q=0; q<4 && he==hipSuccess; q++ )
+      he = (hipError_t)fd_ed25519_hip_launch_gen_btabw( t[q], FD_ED25519_BTABQ_SHIFT*q, FD_ED25519_BTABC_BITS, scratch, stream );
+    if( he==hipSuccess ) he = hipStreamSynchronize( stream );
+    hipFree( scratch );
+    if( he!=hipSuccess ) {
+      for( int q=0; q<4; q++ ) hipFree( t[q] );
+      rc = hip_fail( he, "base tables (btabq)" );
+    } else {
+      for( int q=0; q<4; q++ ) btabq[device].tab[q] = t[q];
+    }
+  }
+  if( rc==FD_ED25519_HIP_OK ) {
+    btabq[device].refs++;
+    for( int q=0; q<4; q++ ) tab[q] = btabq[device].tab[q];
+  }
+  pthread_mutex_unlock( &btabw_lock );
+  return rc;
+}
+
+static void
+btabq_release( int device ) {
+  pthread_mutex_lock( &btabw_lock );
+  if( btabq[device].refs>0 && !--btabq[device].refs ) {
+    for( int q=0; q<4; q++ ) { hipFree( btabq[device].tab[q] ); btabq[device].tab[q] = NULL; }
+  }
+  pthread_mutex_unlock( &btabw_lock );
+}
+
 unsigned long
 fd_ed25519_hip_shared_device_bytes( int device ) {
   if( device<0 || device>=FD_ED25519_HIP_MAX_DEV ) return 0UL;
   pthread_mutex_lock( &btabw_lock );
   unsigned long b = 0UL;
   for( int kind=0; kind<2; kind++ ) if( btabw[kind][device].refs ) b += 2UL*btabw_bytes( kind );
+  if( btabq[device].refs ) b += 4UL*btabw_bytes( 1 );
   pthread_mutex_unlock( &btabw_lock );
   return b;
 }
@@ -321,6 +367,7 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   hipFree( e->d_btab ); hipFree( e->d_btab16 ); hipFree( e->d_btab8[0] ); hipFree( e->d_btab8[1] );
   for( int l=0; l<2; l++ ) { hipFree( e->lane[l].d_atab ); hipFree( e->lane[l].d_work ); }
   if( e->btabw[0] ) btabw_release( e->device, engine_btab_kind( e ) );
+  if( e->btabq[0] ) btabq_release( e->device );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
   hipHostFree( e->h_msgs ); hipHostFree( e->h_off ); hipHostFree( e->h_sz ); hipHostFree( e->h_sigs );
@@ -480,6 +527,10 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   if( err ) return err;
   e->btabw[0] = tw[0];
   e->btabw[1] = tw[1];
+  if( e->r16_max ) {
+    err = btabq_acquire( e->device, e->stream, e->btabq );
+    if( err ) return err;
+  }
   return FD_ED25519_HIP_OK;
 }
 
@@ -633,6 +684,7 @@ params_tables( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p ) {
   p->bw_bits = engine_btab_kind( e ) ? FD_ED25519_BTABC_BITS : FD_ED25519_BTABW_BITS;
   p->codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   p->half_dbits     = engine_half_dbits( e );
+  for( int q=0; q<4; q++ ) p->btabq[q] = e->btabq[q];
 }
 
 /* verify_dev and verify_digests_dev: messages hashed on the device, or
@@ -757,6 +809,28 @@ fd_ed25519_hip_private_hs_dsm( fd_ed25519_hip_engine_t * e, unsigned long n, uns
   err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, stream ? (hipStream_t)stream : e->stream );
   if( err ) return hip_fail( (hipError_t)err, "verify launch" );
   return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_private_hs_dsm4( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned char const * sigs,
+                                unsigned char const * pubs, signed char * out, unsigned char const * sflag,
+                                unsigned char const * hflag, unsigned int const * hq, int const * pts4,
+                                unsigned char const * pflag, unsigned int const * go, void * stream ) {
+  fd_ed25519_verify_params_t p;
+  int err = hs_params( e, &p, n, sigs, pubs, out );
+  if( err ) return err;
+  if( !sflag || !hflag || !hq || !pts4 || !pflag || !e->btabq[0] ) return FD_ED25519_HIP_ERR_INVAL;
+  p.sflag = (uint8_t *)sflag; p.hflag = (uint8_t *)hflag; p.hs = (uint32_t *)hq;
+  p.pts = (int32_t *)pts4; p.pflag = (uint8_t *)pflag;
+  p.go = (uint32_t const *)go;
+  err = fd_ed25519_hip_launch_dsm16q( &p, stream ? (hipStream_t)stream : e->stream );
+  if( err ) return hip_fail( (hipError_t)err, "verify launch" );
+  return FD_ED25519_HIP_OK;
+}
+
+int
+fd_ed25519_hip_private_has_dsm4( fd_ed25519_hip_engine_t const * e ) {
+  return e && e->btabq[0] ? 1 : 0;
 }
 
 int
@@ -1200,6 +1274,17 @@ fd_ed25519_hip_dropin_set_host_scalars_dbits( int dbits ) {
 #define DROPIN_HD_CAP 4UL   /* the hook's bound: the host arrays below */
 static unsigned long dropin_hd_max = DROPIN_HD_MAX;
 
+/* host-decoded drop-in launches take dsm16q (four waves, the chain
+   halved) when the engine holds its tables: 82 -> 69 us p50 for one
+   caller (profiles/r6_dropin_quarter.json); 0 keeps dsm16 (test / A-B
+   hook) */
+static int dropin_quarter = 1;
+
+void
+fd_ed25519_hip_dropin_set_quarter_form( int on ) {
+  dropin_quarter = on ? 1 : 0;
+}
+
 void
 fd_ed25519_hip_dropin_set_host_decode( unsigned long max_sigs ) {
   dropin_hd_max = max_sigs>DROPIN_HD_CAP ? DROPIN_HD_CAP : max_sigs;
@@ -1381,7 +1466,10 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   uint64_t need   = o_tout + n + 16UL;
   uint64_t cap_hs = e->max_chunk;
   uint64_t o_hsf = DROPIN_ALIGN16( need ), o_hhf = DROPIN_ALIGN16( o_hsf + cap_hs ), o_hs = DROPIN_ALIGN16( o_hhf + cap_hs );
-  uint64_t o_pts = DROPIN_ALIGN16( o_hs + 19UL*4UL*cap_hs ), o_pfl = DROPIN_ALIGN16( o_pts + 2UL*20UL*4UL*cap_hs );
+  /* hs: 19 rows (dsm16) or 24 (dsm16q's split scalars); pts: A, R and,
+     for dsm16q, [2^66]A, [2^66]R */
+  int quad = hdmode && dropin_quarter && fd_ed25519_hip_private_has_dsm4( e );
+  uint64_t o_pts = DROPIN_ALIGN16( o_hs + 24UL*4UL*cap_hs ), o_pfl = DROPIN_ALIGN16( o_pts + 4UL*20UL*4UL*cap_hs );
   uint64_t o_go  = DROPIN_ALIGN16( o_pfl + 2UL*cap_hs );
   if( hsmode ) need = hdmode ? o_go + 16UL : o_hs + 19UL*4UL*cap_hs;
   if( need>dq.blk_cap[k] ) {
@@ -1465,10 +1553,16 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
          dispatch overlaps this thread's scalars and decompressions; from
          here every path stores RUN or CANCEL */
       *go = 0U;
-      err = fd_ed25519_hip_private_hs_dsm( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
-                                           src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs),
-                                           (int const *)(src + o_pts), src + o_pfl,
-                                           (unsigned int const *)(src + o_go), st );
+      if( quad )
+        err = fd_ed25519_hip_private_hs_dsm4( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
+                                              src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs),
+                                              (int const *)(src + o_pts), src + o_pfl,
+                                              (unsigned int const *)(src + o_go), st );
+      else
+        err = fd_ed25519_hip_private_hs_dsm( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
+                                             src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs),
+                                             (int const *)(src + o_pts), src + o_pfl,
+                                             (unsigned int const *)(src + o_go), st );
       if( err ) { hipStreamSynchronize( st ); return err; }
     }
     uint8_t *  hsf = (uint8_t *)(h + o_hsf);
@@ -1482,24 +1576,29 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
       all = fd_ed25519_hip_private_hsrec( r->sigs, r->pubs, r->msg, r->msg_sz, dbits, rec );
       if( !all ) break;
       uint64_t j = tf[ t ];
-      for( int w=0; w<19; w++ ) hs[ (uint64_t)w*cap_hs + j ] = rec[ 8 + w ];
+      if( quad ) fd_ed25519_hip_private_hsquad( rec, hs, cap_hs, j );
+      else for( int w=0; w<19; w++ ) hs[ (uint64_t)w*cap_hs + j ] = rec[ 8 + w ];
       hsf[ j ] = (uint8_t)rec[ 27 ];
       hhf[ j ] = (uint8_t)rec[ 28 ];
     }
-    if( all && hdmode ) {   /* A and R of each signature, side by side */
+    if( all && hdmode ) {   /* A and R of each signature, side by side (and [2^66]A, [2^66]R for dsm16q) */
       unsigned char const * enc[ 2UL*DROPIN_HD_CAP ];
-      int32_t       pt[ 2UL*DROPIN_HD_CAP ][ 20 ];
+      int32_t       pt[ 2UL*DROPIN_HD_CAP ][ 20 ], pt66[ 2UL*DROPIN_HD_CAP ][ 20 ];
       unsigned char fl[ 2UL*DROPIN_HD_CAP ];
       t = 0UL;
       for( dropin_req_t * r=list; r; r=r->next, t++ ) { enc[ 2UL*t ] = r->pubs; enc[ 2UL*t+1UL ] = r->sigs; }
-      fd_ed25519_hip_private_hsdec_n( enc, 2UL*nsig, !(e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE), &pt[0][0], fl );
+      fd_ed25519_hip_private_hsdec2_n( enc, 2UL*nsig, !(e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE), &pt[0][0],
+                                       quad ? &pt66[0][0] : NULL, fl );
       int32_t * pts = (int32_t *)(h + o_pts);
       uint8_t * pfl = (uint8_t *)(h + o_pfl);
       t = 0UL;
       for( dropin_req_t * r=list; r; r=r->next, t++ ) {
         uint64_t j = tf[ t ];
-        for( uint64_t which=0UL; which<2UL; which++ ) {   /* 0: A, 1: R -- the work arrays' [2][20][cap] */
-          for( uint64_t l=0UL; l<20UL; l++ ) pts[ ( which*20UL + l )*cap_hs + j ] = pt[ 2UL*t + which ][ l ];
+        for( uint64_t which=0UL; which<2UL; which++ ) {   /* 0: A, 1: R (2, 3: doubled) -- [4][20][cap] */
+          for( uint64_t l=0UL; l<20UL; l++ ) {
+            pts[ ( which*20UL + l )*cap_hs + j ] = pt[ 2UL*t + which ][ l ];
+            if( quad ) pts[ ( (2UL + which)*20UL + l )*cap_hs + j ] = pt66[ 2UL*t + which ][ l ];
+          }
           pfl[ which*cap_hs + j ] = fl[ 2UL*t + which ];
         }
       }

@@ -234,7 +234,8 @@ void dec_pre( dec_state & d, f51 & x, unsigned char const enc[ 32 ] ) {
   x = mul( mul( sq( d.v3 ), d.v ), d.u );      /* u v^7     */
 }
 
-unsigned dec_post( dec_state const & d, f51 x, unsigned char const enc[ 32 ], int avx_rule, int32_t pt[ 20 ] ) {
+unsigned dec_post( dec_state const & d, f51 x, unsigned char const enc[ 32 ], int avx_rule, int32_t pt[ 20 ],
+                   f51 * xs ) {
   x = mul( mul( x, d.v3 ), d.u );              /* u v^3 (u v^7)^((p-5)/8) */
   f51 vxx = mul( sq( x ), d.v );
   const bool root  = iszero( sub( vxx, d.u ) );
@@ -258,6 +259,7 @@ unsigned dec_post( dec_state const & d, f51 x, unsigned char const enc[ 32 ], in
   limbs_frombytes( t, xb );
   limbs_carry( pt, t );
   if( neg ) for( int i=0; i<10; i++ ) pt[ i ] = -pt[ i ];
+  if( xs ) *xs = neg ? sub( f51{ { 0ULL, 0ULL, 0ULL, 0ULL, 0ULL } }, x ) : x;
   uint32_t ew[ 8 ];
   memcpy( ew, enc, 32 );
   ew[ 7 ] &= 0x7fffffffu;   /* fe_frombytes drops bit 255 (limb 9 is 25 bits wide) */
@@ -265,13 +267,75 @@ unsigned dec_post( dec_state const & d, f51 x, unsigned char const enc[ 32 ], in
   return ( fail ? 1u : 0u ) | ( small ? 2u : 0u );
 }
 
+/* z^(p-2) = (z^(2^252-3))^8 z^3 for N elements at once */
 template< int N >
-void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsigned char * flags ) {
+void inv_n( f51 ( &z )[ N ] ) {
+  f51 t[ N ];
+  for( int i=0; i<N; i++ ) t[ i ] = z[ i ];
+  pow22523_n< N >( t );
+  for( int i=0; i<N; i++ ) t[ i ] = mul( sq( sq( sq( t[ i ] ) ) ), mul( sq( z[ i ] ), z[ i ] ) );
+  for( int i=0; i<N; i++ ) z[ i ] = t[ i ];
+}
+
+/* the device's limbs of an affine point given by canonical-reducible
+   (x, y): x as fe_carry of its canonical bytes, y as fe_frombytes of its
+   canonical bytes (both tight, as the decode's) */
+void limbs_point( int32_t pt[ 20 ], f51 const & x, f51 const & y ) {
+  uint32_t xb[ 8 ], yb[ 8 ];
+  int32_t t[ 10 ];
+  tobytes( xb, x );
+  tobytes( yb, y );
+  limbs_frombytes( t, xb );
+  limbs_carry( pt, t );
+  limbs_frombytes( pt + 10, yb );
+}
+
+/* [2^n](x, y) for N points at once (extended coordinates without T,
+   dbl-2008-hwcd for a = -1), then affine with one shared inversion */
+template< int N >
+void dbl_n( f51 ( &x )[ N ], f51 ( &y )[ N ], int n ) {
+  const f51 zero = { { 0ULL, 0ULL, 0ULL, 0ULL, 0ULL } };
+  f51 X[ N ], Y[ N ], Z[ N ];
+  for( int i=0; i<N; i++ ) { X[ i ] = x[ i ]; Y[ i ] = y[ i ]; Z[ i ] = one(); }
+  for( int r=0; r<n; r++ ) {
+    for( int i=0; i<N; i++ ) {
+      f51 A = sq( X[ i ] ), B = sq( Y[ i ] ), Z2 = sq( Z[ i ] );
+      f51 C = add( Z2, Z2 );
+      f51 E = sub( sub( sq( add( X[ i ], Y[ i ] ) ), A ), B );
+      f51 G = sub( B, A );                    /* D + B, D = -A */
+      f51 F = sub( G, C );
+      f51 H = sub( zero, add( A, B ) );       /* D - B         */
+      X[ i ] = mul( E, F ); Y[ i ] = mul( G, H ); Z[ i ] = mul( F, G );
+    }
+  }
+  /* 1/Z_i from one inversion: prefix products */
+  f51 pre[ N ], inv[ 1 ];
+  pre[ 0 ] = Z[ 0 ];
+  for( int i=1; i<N; i++ ) pre[ i ] = mul( pre[ i-1 ], Z[ i ] );
+  inv[ 0 ] = pre[ N-1 ];
+  inv_n< 1 >( inv );
+  f51 acc = inv[ 0 ];
+  for( int i=N-1; i>=0; i-- ) {
+    f51 zi = i ? mul( acc, pre[ i-1 ] ) : acc;
+    if( i ) acc = mul( acc, Z[ i ] );
+    x[ i ] = mul( X[ i ], zi ); y[ i ] = mul( Y[ i ], zi );
+  }
+}
+
+template< int N >
+void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsigned char * flags, int32_t * pt66 ) {
   dec_state d[ N ];
   f51 x[ N ];
   for( int i=0; i<N; i++ ) dec_pre( d[ i ], x[ i ], enc[ i ] );
   pow22523_n< N >( x );
-  for( int i=0; i<N; i++ ) flags[ i ] = (unsigned char)dec_post( d[ i ], x[ i ], enc[ i ], avx_rule, pt + 20*i );
+  f51 xs[ N ], ys[ N ];
+  for( int i=0; i<N; i++ ) {
+    flags[ i ] = (unsigned char)dec_post( d[ i ], x[ i ], enc[ i ], avx_rule, pt + 20*i, &xs[ i ] );
+    ys[ i ] = d[ i ].y;
+  }
+  if( !pt66 ) return;
+  dbl_n< N >( xs, ys, 66 );
+  for( int i=0; i<N; i++ ) limbs_point( pt66 + 20*i, xs[ i ], ys[ i ] );
 }
 
 } /* namespace */
@@ -282,13 +346,60 @@ void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsig
    AVX-512 build's codes (an engine without
    FD_ED25519_HIP_FLAG_CODES_PORTABLE). */
 extern "C" void
+fd_ed25519_hip_private_hsdec2_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
+                                 int32_t * pt66, unsigned char * flags ) {
+  unsigned long i = 0UL;
+#define HSDEC_GROUP( N ) dec_n< N >( enc + i, avx_rule, pt + 20UL*i, flags + i, pt66 ? pt66 + 20UL*i : NULL )
+  for( ; i+4UL<=n; i+=4UL ) HSDEC_GROUP( 4 );
+  if( n-i==3UL ) HSDEC_GROUP( 3 );
+  if( n-i==2UL ) HSDEC_GROUP( 2 );
+  if( n-i==1UL ) HSDEC_GROUP( 1 );
+#undef HSDEC_GROUP
+}
+
+/* pt66 (when not NULL): each point doubled 66 times, [2^66]P, affine, in
+   the same limbs -- the dsm16q form's A' and R' (a failed decode's is any
+   value: its code is the decode's) */
+extern "C" void
 fd_ed25519_hip_private_hsdec_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
                                 unsigned char * flags ) {
-  unsigned long i = 0UL;
-  for( ; i+4UL<=n; i+=4UL ) dec_n< 4 >( enc + i, avx_rule, pt + 20UL*i, flags + i );
-  if( n-i==3UL ) dec_n< 3 >( enc + i, avx_rule, pt + 20UL*i, flags + i );
-  if( n-i==2UL ) dec_n< 2 >( enc + i, avx_rule, pt + 20UL*i, flags + i );
-  if( n-i==1UL ) dec_n< 1 >( enc + i, avx_rule, pt + 20UL*i, flags + i );
+  fd_ed25519_hip_private_hsdec2_n( enc, n, avx_rule, pt, NULL, flags );
+}
+
+/* dsm16q's scalars from a host record (hsrec's layout: c rec[8..12], |d|
+   rec[13..17], s' = rec[18..22] (bits 0..143) + rec[23..26] << 144): hq
+   rows 3q..3q+2 = c0, c1, d0, d1 (c and |d| split at bit 66), rows
+   12+3q..14+3q = bits [72 q, 72 q + 72) of s', each at column j of stride
+   cap */
+extern "C" void
+fd_ed25519_hip_private_hsquad( uint32_t const rec[ 32 ], uint32_t * hq, unsigned long cap, unsigned long j ) {
+  u128 c_lo = 0, c_hi = 0, d_lo = 0, d_hi = 0;
+  uint32_t cw[ 6 ] = { rec[ 8 ], rec[ 9 ], rec[ 10 ], rec[ 11 ], rec[ 12 ], 0u };
+  uint32_t dw[ 6 ] = { rec[ 13 ], rec[ 14 ], rec[ 15 ], rec[ 16 ], rec[ 17 ], 0u };
+  /* 160-bit values as (low 66 bits, the rest) */
+  u128 cl = (u128)cw[ 0 ] | (u128)cw[ 1 ] << 32 | (u128)cw[ 2 ] << 64 | (u128)cw[ 3 ] << 96;
+  u128 dl = (u128)dw[ 0 ] | (u128)dw[ 1 ] << 32 | (u128)dw[ 2 ] << 64 | (u128)dw[ 3 ] << 96;
+  const u128 m66 = ( (u128)1 << 66 ) - 1;
+  c_lo = cl & m66; c_hi = ( cl >> 66 ) | (u128)cw[ 4 ] << 62;
+  d_lo = dl & m66; d_hi = ( dl >> 66 ) | (u128)dw[ 4 ] << 62;
+  u128 k4[ 4 ] = { c_lo, c_hi, d_lo, d_hi };
+  for( int q=0; q<4; q++ )
+    for( int w=0; w<3; w++ ) hq[ (unsigned long)( 3*q + w )*cap + j ] = (uint32_t)( k4[ q ] >> ( 32*w ) );
+  /* s' (253 bits) from its two halves */
+  uint32_t sw[ 9 ];
+  for( int w=0; w<4; w++ ) sw[ w ] = rec[ 18 + w ];
+  sw[ 4 ] = ( rec[ 22 ] & 0xffffu ) | ( rec[ 23 ] << 16 );
+  for( int w=5; w<8; w++ ) sw[ w ] = ( rec[ 18 + w ] >> 16 ) | ( rec[ 19 + w ] << 16 );
+  sw[ 8 ] = rec[ 26 ] >> 16;
+  for( int q=0; q<4; q++ ) {
+    for( int w=0; w<3; w++ ) {   /* bits 72q + 32w .. +31 of s', masked to the chunk's 72 */
+      int b = 72*q + 32*w, wi = b >> 5, sh = b & 31;
+      uint64_t v = (uint64_t)sw[ wi ] | ( wi+1<9 ? (uint64_t)sw[ wi+1 ] << 32 : 0ULL );
+      uint32_t x = (uint32_t)( v >> sh );
+      if( w==2 ) x &= 0xffu;   /* 64 + 8 bits */
+      hq[ (unsigned long)( 12 + 3*q + w )*cap + j ] = x;
+    }
+  }
 }
 
 /* one point: returns its flags */

@@ -227,17 +227,32 @@ fd_ed25519_hip_pipe_set_host_scalars( unsigned long max_sigs ) {
 #define PIPE_HD_CAP 4UL
 static unsigned long pipe_hd_max = PIPE_HD_MAX;
 
+/* ... in dsm16q's four waves (1) or dsm16's two (0, the default): the
+   four-wave form puts the 66 doublings of A and R on the submitting
+   thread, which is the tile's own -- at the reference tile's loads it
+   lost (p50 0.092 / 0.130 / 0.171 ms against 0.086 / 0.086 / 0.103 at
+   29K / 46K / 54K txn/s, the batches growing as the tile thread fell
+   behind, profiles/r6_pipe_quarter.jsonl) while the synchronous drop-in,
+   whose caller waits anyway, gains (fd_ed25519_hip_dropin_set_quarter_form) */
+static int pipe_quarter = 0;
+
+void
+fd_ed25519_hip_pipe_set_quarter_form( int on ) {
+  pipe_quarter = on ? 1 : 0;
+}
+
 void
 fd_ed25519_hip_pipe_set_host_decode( unsigned long max_sigs ) {
   pipe_hd_max = max_sigs>PIPE_HD_CAP ? PIPE_HD_CAP : max_sigs;
 }
 
-/* the page-locked host-scalar block: sflag [cap], hflag [cap], hs [19][cap]
-   words, pts [2][20][cap] words, pflag [2][cap], the go word (params.go) */
+/* the page-locked host-scalar block: sflag [cap], hflag [cap], hs [24][cap]
+   words (dsm16: 19 rows; dsm16q: 24), pts [4][20][cap] words (A, R; dsm16q
+   also [2^66]A, [2^66]R), pflag [2][cap], the go word (params.go) */
 #define HS_O_HS( cap )  ( 2UL*(cap) )
-#define HS_O_PTS( cap ) ( ( 2UL + 19UL*4UL )*(cap) )
-#define HS_O_PFL( cap ) ( ( 2UL + 19UL*4UL + 2UL*20UL*4UL )*(cap) )
-#define HS_O_GO( cap )  ( ( ( 2UL + 19UL*4UL + 2UL*20UL*4UL + 2UL )*(cap) + 15UL ) & ~15UL )
+#define HS_O_PTS( cap ) ( ( 2UL + 24UL*4UL )*(cap) )
+#define HS_O_PFL( cap ) ( ( 2UL + 24UL*4UL + 4UL*20UL*4UL )*(cap) )
+#define HS_O_GO( cap )  ( ( ( 2UL + 24UL*4UL + 4UL*20UL*4UL + 2UL )*(cap) + 15UL ) & ~15UL )
 #define HS_BYTES( cap ) ( HS_O_GO( cap ) + 16UL )
 
 struct fd_ed25519_hip_pipe {
@@ -515,6 +530,7 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
   unsigned long n = slot->sig_cnt, cap = slot->sig_cap;
   unsigned long o_sigs = (unsigned long)( slot->sigs - s->h_in ), o_pubs = (unsigned long)( slot->pubs - s->h_in );
   int err, hd = n<=pipe_hd_max;
+  int quad = hd && pipe_quarter && fd_ed25519_hip_private_has_dsm4( s->eng );
   volatile uint32_t * go = (volatile uint32_t *)( s->h_hs + HS_O_GO( cap ) );
   if( !hd ) {
     PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_decode( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
@@ -524,13 +540,23 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
     /* dsm16 first, waiting on the go word while this thread computes
        (params.go); every path below stores RUN or CANCEL */
     *go = 0U;
-    PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
-                                                                (signed char *)s->h_outb_dev, s->h_hs_dev,
-                                                                s->h_hs_dev + cap,
-                                                                (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
-                                                                (int const *)( s->h_hs_dev + HS_O_PTS( cap ) ),
-                                                                s->h_hs_dev + HS_O_PFL( cap ),
-                                                                (unsigned int const *)( s->h_hs_dev + HS_O_GO( cap ) ), st ) );
+    if( quad ) {
+      PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm4( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
+                                                                   (signed char *)s->h_outb_dev, s->h_hs_dev,
+                                                                   s->h_hs_dev + cap,
+                                                                   (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
+                                                                   (int const *)( s->h_hs_dev + HS_O_PTS( cap ) ),
+                                                                   s->h_hs_dev + HS_O_PFL( cap ),
+                                                                   (unsigned int const *)( s->h_hs_dev + HS_O_GO( cap ) ), st ) );
+    } else {
+      PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
+                                                                  (signed char *)s->h_outb_dev, s->h_hs_dev,
+                                                                  s->h_hs_dev + cap,
+                                                                  (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
+                                                                  (int const *)( s->h_hs_dev + HS_O_PTS( cap ) ),
+                                                                  s->h_hs_dev + HS_O_PFL( cap ),
+                                                                  (unsigned int const *)( s->h_hs_dev + HS_O_GO( cap ) ), st ) );
+    }
     if( err ) return err;
   }
   unsigned char * hsf = s->h_hs, * hhf = s->h_hs + cap;
@@ -543,21 +569,26 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
       if( hd ) __atomic_store_n( go, FD_ED25519_GO_CANCEL, __ATOMIC_RELEASE );
       return 0;
     }
-    for( int w=0; w<19; w++ ) hs[ (unsigned long)w*cap + i ] = rec[ 8 + w ];
+    if( quad ) fd_ed25519_hip_private_hsquad( rec, hs, cap, i );
+    else for( int w=0; w<19; w++ ) hs[ (unsigned long)w*cap + i ] = rec[ 8 + w ];
     hsf[ i ] = (unsigned char)rec[ 27 ];
     hhf[ i ] = (unsigned char)rec[ 28 ];
   }
   if( hd ) {   /* A and R of each signature, side by side */
     unsigned char const * enc[ 2UL*PIPE_HD_CAP ];
-    int32_t       pt[ 2UL*PIPE_HD_CAP ][ 20 ];
+    int32_t       pt[ 2UL*PIPE_HD_CAP ][ 20 ], pt66[ 2UL*PIPE_HD_CAP ][ 20 ];
     unsigned char fl[ 2UL*PIPE_HD_CAP ];
     for( unsigned long i=0UL; i<n; i++ ) { enc[ 2UL*i ] = slot->pubs + 32UL*i; enc[ 2UL*i+1UL ] = slot->sigs + 64UL*i; }
-    fd_ed25519_hip_private_hsdec_n( enc, 2UL*n, !fd_ed25519_hip_private_codes_portable( s->eng ), &pt[0][0], fl );
+    fd_ed25519_hip_private_hsdec2_n( enc, 2UL*n, !fd_ed25519_hip_private_codes_portable( s->eng ), &pt[0][0],
+                                     quad ? &pt66[0][0] : NULL, fl );
     int32_t * pts = (int32_t *)( s->h_hs + HS_O_PTS( cap ) );
     unsigned char * pfl = s->h_hs + HS_O_PFL( cap );
     for( unsigned long i=0UL; i<n; i++ )
-      for( unsigned long which=0UL; which<2UL; which++ ) {   /* 0: A, 1: R */
-        for( unsigned long l=0UL; l<20UL; l++ ) pts[ ( which*20UL + l )*cap + i ] = pt[ 2UL*i + which ][ l ];
+      for( unsigned long which=0UL; which<2UL; which++ ) {   /* 0: A, 1: R (2, 3: doubled, dsm16q) */
+        for( unsigned long l=0UL; l<20UL; l++ ) {
+          pts[ ( which*20UL + l )*cap + i ] = pt[ 2UL*i + which ][ l ];
+          if( quad ) pts[ ( ( 2UL + which )*20UL + l )*cap + i ] = pt66[ 2UL*i + which ][ l ];
+        }
         pfl[ which*cap + i ] = fl[ 2UL*i + which ];
       }
   }

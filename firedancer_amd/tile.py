@@ -333,6 +333,16 @@ def pipe_set_host_decode(max_sigs):
     _lib.fd_ed25519_hip_pipe_set_host_decode(int(max_sigs))
 
 
+_lib.fd_ed25519_hip_pipe_set_quarter_form.argtypes = [ctypes.c_int]
+_lib.fd_ed25519_hip_pipe_set_quarter_form.restype = None
+
+
+def pipe_set_quarter_form(on):
+    """fd_ed25519_hip_pipe_set_quarter_form: host-decoded pipe batches in
+    dsm16q's four waves (1) or dsm16's two (0, the default)."""
+    _lib.fd_ed25519_hip_pipe_set_quarter_form(1 if on else 0)
+
+
 def latency_set_cpus(producer_cpu=-1, tile_cpu=-1):
     """fd_ed25519_hip_latency_set_cpus: pin latency_run's producer and tile
     threads (one tile) to these CPUs for each run; -1 leaves one unpinned."""

@@ -159,6 +159,12 @@ fd_ed25519_hip_pipe_set_host_scalars( unsigned long max_sigs );
 void
 fd_ed25519_hip_pipe_set_host_decode( unsigned long max_sigs );
 
+/* ... and those batches in four waves (1, fd_ed25519_hip_dropin_set_
+   quarter_form's form) or two (0, the default: the extra host work sits on
+   the tile's own thread, where it costs more than the shorter chain saves). */
+void
+fd_ed25519_hip_pipe_set_quarter_form( int on );
+
 /* ---- txn -------------------------------------------------------------- */
 
 /* The fields of fd_txn_t (src/ballet/txn/fd_txn.h) the verify tile reads. */

@@ -4,7 +4,9 @@ k, S < L and the half-size pair from the calling thread while the GPU
 decompresses A and R, and dsm16 reads them from the page-locked block; the
 fewest-signature launches (fd_ed25519_hip_dropin_set_host_decode,
 host/fd_ed25519_hip_hsdec.cc) decompress A and R on the calling thread too
-and launch dsm16 alone, reading the points in place.  Every fixture class -- the reference's vectors, the adversarial set,
+and launch the group equation alone, reading the points in place -- in
+four waves on [2^66]A and [2^66]R doubled by the host too (dsm16q,
+fd_ed25519_hip_dropin_set_quarter_form) or in dsm16's two.  Every fixture class -- the reference's vectors, the adversarial set,
 mixed-order points, k needing long |d| -- through fd_ed25519_verify with
 each mode on (the default) and off, code by code against the reference's
 own codes (tests/golden/, oracle/_ref)."""
@@ -25,21 +27,25 @@ def ed():
     lib = ed25519.library()
     lib.fd_ed25519_hip_dropin_set_host_scalars.argtypes = [ctypes.c_ulong]
     lib.fd_ed25519_hip_dropin_set_host_decode.argtypes = [ctypes.c_ulong]
+    lib.fd_ed25519_hip_dropin_set_quarter_form.argtypes = [ctypes.c_int]
     yield ed25519, lib
     lib.fd_ed25519_hip_dropin_set_host_scalars(4)
     lib.fd_ed25519_hip_dropin_set_host_decode(2)
+    lib.fd_ed25519_hip_dropin_set_quarter_form(1)
 
 
 def _run(ed25519, d, idx):
     return np.array([ed25519.verify(*case(d, i)) for i in idx], np.int8)
 
 
-@pytest.mark.parametrize("mode", [(4, 2), (4, 0), (0, 0)], ids=["host-scalars-decode", "host-scalars", "device"])
+@pytest.mark.parametrize("mode", [(4, 2, 1), (4, 2, 0), (4, 0, 1), (0, 0, 1)],
+                         ids=["host-decode-quarter", "host-decode-two-wave", "host-scalars", "device"])
 @pytest.mark.parametrize("fixture", ["vectors", "adversarial", "mixed_order", "halfsize", "longd"])
 def test_dropin_codes_every_host_path(ed, request, mode, fixture):
     ed25519, lib = ed
     lib.fd_ed25519_hip_dropin_set_host_scalars(mode[0])
     lib.fd_ed25519_hip_dropin_set_host_decode(mode[1])
+    lib.fd_ed25519_hip_dropin_set_quarter_form(mode[2])
     d = request.getfixturevalue(fixture)
     n = len(d["msg_sz"])
     idx = list(range(0, n, 3 if n > 3000 else 1))
