@@ -231,6 +231,7 @@ int fd_ed25519_hip_private_hs_dsm4( struct fd_ed25519_hip_engine * e, unsigned l
                                     unsigned char const * hflag, unsigned int const * hq, int const * pts4,
                                     unsigned char const * pflag, unsigned int const * go, void * stream );
 int fd_ed25519_hip_private_has_dsm4( struct fd_ed25519_hip_engine const * e );
+int fd_ed25519_hip_private_want_dsm4( struct fd_ed25519_hip_engine * e );
 #ifdef __cplusplus
 }
 #endif

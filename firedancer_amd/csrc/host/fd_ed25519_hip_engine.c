@@ -527,10 +527,6 @@ engine_init( fd_ed25519_hip_engine_t * e, int device, uint64_t max_chunk, int fl
   if( err ) return err;
   e->btabw[0] = tw[0];
   e->btabw[1] = tw[1];
-  if( e->r16_max ) {
-    err = btabq_acquire( e->device, e->stream, e->btabq );
-    if( err ) return err;
-  }
   return FD_ED25519_HIP_OK;
 }
 
@@ -831,6 +827,19 @@ fd_ed25519_hip_private_hs_dsm4( fd_ed25519_hip_engine_t * e, unsigned long n, un
 int
 fd_ed25519_hip_private_has_dsm4( fd_ed25519_hip_engine_t const * e ) {
   return e && e->btabq[0] ? 1 : 0;
+}
+
+/* dsm16q's tables for engine e (with the lane-split form), made on first
+   use per device: the drop-in engines take them at creation, a pipe's
+   engines only when its four-wave form is asked for.  1: available. */
+int
+fd_ed25519_hip_private_want_dsm4( fd_ed25519_hip_engine_t * e ) {
+  if( !e || !e->r16_max ) return 0;
+  if( !e->btabq[0] && hipSetDevice( e->device )==hipSuccess ) {
+    int32_t * t[4] = { NULL, NULL, NULL, NULL };
+    if( !btabq_acquire( e->device, e->stream, t ) ) for( int q=0; q<4; q++ ) e->btabq[q] = t[q];
+  }
+  return e->btabq[0] ? 1 : 0;
 }
 
 int
@@ -1328,6 +1337,7 @@ dropin_engine_make( int k ) {
   dq.h_blk[k] = NULL; dq.h_dev[k] = NULL; dq.d_blk[k] = NULL; dq.blk_cap[k] = 0UL;
   dq.direct_pending[k] = 0;
   dq.eng[k] = fd_ed25519_hip_engine_new( dq.device, DROPIN_CHUNK, dq.flags );
+  if( dq.eng[k] ) fd_ed25519_hip_private_want_dsm4( dq.eng[k] );   /* without them: dsm16's two waves */
   return dq.eng[k] ? FD_ED25519_HIP_OK : FD_ED25519_HIP_ERR_INVAL;
 }
 

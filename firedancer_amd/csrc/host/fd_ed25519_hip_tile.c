@@ -530,7 +530,7 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
   unsigned long n = slot->sig_cnt, cap = slot->sig_cap;
   unsigned long o_sigs = (unsigned long)( slot->sigs - s->h_in ), o_pubs = (unsigned long)( slot->pubs - s->h_in );
   int err, hd = n<=pipe_hd_max;
-  int quad = hd && pipe_quarter && fd_ed25519_hip_private_has_dsm4( s->eng );
+  int quad = hd && pipe_quarter && fd_ed25519_hip_private_want_dsm4( s->eng );
   volatile uint32_t * go = (volatile uint32_t *)( s->h_hs + HS_O_GO( cap ) );
   if( !hd ) {
     PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_decode( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,

@@ -128,10 +128,10 @@ fd_ed25519_hip_dropin_set_host_decode( unsigned long max_sigs );
 /* Host-decoded drop-in launches run the group equation in four waves --
    the calling thread also doubles A and R 66 times and splits the
    half-size scalars at bit 66 and s' at 72-bit boundaries, so each wave's
-   chain is ~17 windows instead of 33 -- on engines that hold the four
-   compact base tables at offsets 2^0, 2^72, 2^144, 2^216 (every engine
-   with the lane-split form).  Test / A-B hook, process-wide: 0 keeps the
-   two-wave form (default 1). */
+   chain is ~17 windows instead of 33 -- from four compact base tables at
+   offsets 2^0, 2^72, 2^144, 2^216 (32 MiB per device, made with the
+   drop-in engines).  Test / A-B hook, process-wide: 0 keeps the two-wave
+   form (default 1). */
 void
 fd_ed25519_hip_dropin_set_quarter_form( int on );
 
