@@ -129,7 +129,7 @@ typedef struct {
                                       its decode blocks only, and dsm16's sflag / hs /
                                       hflag point at the caller's page-locked block (the
                                       same [field][cap] layout); never a full-length item */
-  int32_t const *  btabq[4];       /* dsm16q: compact [0..2^16)[2^(72 q)]B, q = 0..3 (shared per device) */
+  int32_t const *  btabq[8];       /* dsm16s<S>: compact [0..2^16)[2^(CB q)]B, q < S (shared per device) */
   uint32_t const * go;             /* dsm16 with host scalars and points: NULL, or a
                                       page-locked word the kernel waits on before it
                                       reads anything else -- the launch goes ahead of
@@ -181,9 +181,9 @@ int fd_ed25519_hip_launch_verify( fd_ed25519_verify_params_t const * p, uint32_t
 #define FD_ED25519_PHASE_DSM    3
 #define FD_ED25519_PHASE_CNT    4
 int fd_ed25519_hip_launch_phase( fd_ed25519_verify_params_t const * p, int phase, uint32_t grid, void * stream );
-/* dsm16q (fd_ed25519_kernels.hip): the four-wave form for launches whose
-   points and split scalars all came from the host */
-int fd_ed25519_hip_launch_dsm16q( fd_ed25519_verify_params_t const * p, void * stream );
+/* dsm16s (fd_ed25519_kernels.hip): the four- or eight-wave form for
+   launches whose points and split scalars all came from the host */
+int fd_ed25519_hip_launch_dsm16s( fd_ed25519_verify_params_t const * p, int waves, void * stream );
 
 /* Host scalars (host/fd_ed25519_hip_hsrec.cc, host/fd_ed25519_hip_engine.c):
    a launch of a few signatures whose k, S < L and half-size pair the
@@ -216,22 +216,23 @@ int fd_ed25519_hip_private_hs_dsm( struct fd_ed25519_hip_engine * e, unsigned lo
                                    unsigned char const * pflag, unsigned int const * go, void * stream );
 void fd_ed25519_hip_private_hsdec_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
                                      unsigned char * flags );
-/* The four-wave form (dsm16q) for host-decoded launches: hsquad turns one
-   signature's record and its two decoded points into the split scalars
-   and hsdec2_n the doubled points -- hq rows (24 of them, stride cap)
-   3q..3q+2 the scalar of wave q (c0, c1, d0, d1: c and |d| split at bit
-   66), 12+3q..14+3q the 72-bit chunk q of s'; pts4 rows [2] = [2^66]A,
-   [3] = [2^66]R (20 limbs each, stride cap); hs_dsm4 launches dsm16q on
-   them. */
-void fd_ed25519_hip_private_hsquad( uint32_t const rec[ 32 ], uint32_t * hq, unsigned long cap, unsigned long j );
-void fd_ed25519_hip_private_hsdec2_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
-                                      int32_t * pt66, unsigned char * flags );
-int fd_ed25519_hip_private_hs_dsm4( struct fd_ed25519_hip_engine * e, unsigned long n, unsigned char const * sigs,
-                                    unsigned char const * pubs, signed char * out, unsigned char const * sflag,
-                                    unsigned char const * hflag, unsigned int const * hq, int const * pts4,
-                                    unsigned char const * pflag, unsigned int const * go, void * stream );
-int fd_ed25519_hip_private_has_dsm4( struct fd_ed25519_hip_engine const * e );
-int fd_ed25519_hip_private_want_dsm4( struct fd_ed25519_hip_engine * e );
+/* The split forms (dsm16s<S>, S = 4 or 8 waves) for host-decoded
+   launches: hssplit turns one signature's record into the split scalars
+   and s' chunks (hq: 24 rows of stride cap, layout at the function), and
+   hsdec3_n also returns each point doubled step, 2 step, .. nx step times
+   (S = 4: nx 1, step 66; S = 8: nx 3, step 33) for pts rows 2i + side
+   (row 0 A, 1 R, 2 A_1, 3 R_1, ..); hs_dsms launches dsm16s<waves> on them
+   once want_dsms has made (or found) the engine's tables for that form. */
+void fd_ed25519_hip_private_hssplit( uint32_t const rec[ 32 ], int waves, uint32_t * hq, unsigned long cap,
+                                     unsigned long j );
+void fd_ed25519_hip_private_hsdec3_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
+                                      int32_t * ptx, int nx, int step, unsigned char * flags );
+int fd_ed25519_hip_private_hs_dsms( struct fd_ed25519_hip_engine * e, int waves, unsigned long n,
+                                    unsigned char const * sigs, unsigned char const * pubs, signed char * out,
+                                    unsigned char const * sflag, unsigned char const * hflag, unsigned int const * hq,
+                                    int const * pts, unsigned char const * pflag, unsigned int const * go,
+                                    void * stream );
+int fd_ed25519_hip_private_want_dsms( struct fd_ed25519_hip_engine * e, int waves );
 #ifdef __cplusplus
 }
 #endif

@@ -1298,26 +1298,32 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
 }
 
 /* ------------------------------------------------------------------------
-   dsm16q: dsm16's equation over four waves, for the launches whose points
-   the host computed (host/fd_ed25519_hip_hsdec.cc): with A' = [2^66]A and
-   R' = [2^66]R from the host too, each half-size scalar splits at bit 66,
-   c = c0 + 2^66 c1 and |d| = d0 + 2^66 d1, and s' at bits 72, 144, 216:
+   dsm16s<S>: dsm16's equation over S = 4 or 8 waves, for the launches
+   whose points the host computed (host/fd_ed25519_hip_hsdec.cc).  With
+   H = S/2 parts per half-size scalar, split every G = 66 (S = 4) or 33
+   (S = 8) bits -- c = sum c_i 2^(G i), |d| = sum d_i 2^(G i) -- and the
+   points doubled by the host too, A_i = [2^(G i)]A, R_i = [2^(G i)]R, and
+   s' in S chunks of CB = 72 or 32 bits:
 
-     [c0](-A) + [c1](-A') + [d0](-+R) + [d1](-+R')
-       + [s'_0]B + [s'_1][2^72]B + [s'_2][2^144]B + [s'_3][2^216]B == 0
+     sum_i [c_i](-A_i) + sum_i [d_i](-+R_i) + sum_q [s'_q][2^(CB q)]B == 0
 
-   exactly (A' and R' are the points themselves doubled 66 times, so no
-   reduction of c or d is involved).  Wave q holds one variable-base term
-   and one base term: W = 17 windows of 4 doublings instead of 33 (|d| of
-   up to 151 bits: up to 22), the base digits radix 2^16 from the compact
-   tables at the four offsets (params.btabq), five at windows 16, 12, .., 0.
-   Waves 1-3 hand their points to wave 0 through LDS.  Inputs (host
-   memory, params.go's launch-ahead): pts [4][20][cap] (A, R, A', R'),
-   pflag [2][cap], sflag, hflag [cap], hs [24][cap]: rows 3q..3q+2 the
-   scalar of wave q (c0, c1, d0, d1), rows 12+3q..14+3q its 72-bit chunk
-   of s'. */
-__global__ void __launch_bounds__(256) fd_ed25519_dsm16q_kernel(fd_ed25519_verify_params_t p) {
-  const uint64_t j = blockIdx.x;   /* a block (four waves) per signature: every return below is block-uniform */
+   exactly (A_i and R_i are the points themselves doubled, so no reduction
+   of c or d is involved).  Wave q = H side + i holds one variable-base
+   term (side 0: A, 1: R) and base chunk q: W = 17 (S = 4) or 9 (S = 8)
+   windows of 4 doublings instead of 33 (more for the rare |d| >= 2^131),
+   the base digits radix 2^16 from compact tables at offsets 2^(CB q)
+   (params.btabq), CB/16 of them (rounded up) at windows .., 4, 0.  The
+   waves' points meet in LDS by halves (log2 S rounds of additions), wave
+   0 tests the identity.  Inputs (host memory, params.go's launch-ahead):
+   pts [S][20][cap] (row 2i + side: A, R, A_1, R_1, ..), pflag [2][cap],
+   sflag, hflag [cap], hs [24][cap]: rows KW q .. KW q + KW-1 the scalar of
+   wave q (KW = 3 or 2 words), rows S KW + BWORDS q .. its chunk of s'. */
+template <int S>
+__global__ void __launch_bounds__(64 * S) fd_ed25519_dsm16s_kernel(fd_ed25519_verify_params_t p) {
+  static_assert(S == 4 || S == 8, "four or eight waves");
+  constexpr int H = S / 2, KW = S == 4 ? 3 : 2, CB = S == 4 ? 72 : 32, BWORDS = (CB + 31) / 32;
+  constexpr int NB = (CB + 15) / 16, WMIN = S == 4 ? 17 : 9, SH0 = S == 4 ? 64 : 96;
+  const uint64_t j = blockIdx.x;   /* a block (S waves) per signature: every return below is block-uniform */
   if (j >= p.n) return;
   if (p.go) {
     __shared__ uint32_t go;
@@ -1326,21 +1332,20 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm16q_kernel(fd_ed25519_verif
     if (go != FD_ED25519_GO_RUN) return;
   }
   const uint32_t hf = p.hflag[j];
-  const int q = (int)(threadIdx.x >> 6);   /* 0: c0 (-A), 1: c1 (-A'), 2: d0 (-+R), 3: d1 (-+R') */
+  const int q = (int)(threadIdx.x >> 6), side = q / H, part = q % H;
   uint32_t hk[5] = {0u, 0u, 0u, 0u, 0u}, hb[5] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int w = 0; w < 3; w++) {
-    hk[w] = p.hs[(uint64_t)(3 * q + w) * p.cap + j];
-    hb[w] = p.hs[(uint64_t)(12 + 3 * q + w) * p.cap + j];
-  }
-  /* the block's window count: the longest of the four scalars (every wave
-     reads them all, so W is the same in each without a barrier) */
-  int W = 17;
+  for (int w = 0; w < KW; w++) hk[w] = p.hs[(uint64_t)(KW * q + w) * p.cap + j];
 #pragma unroll
-  for (int t = 0; t < 4; t++) {
+  for (int w = 0; w < BWORDS; w++) hb[w] = p.hs[(uint64_t)(S * KW + BWORDS * q + w) * p.cap + j];
+  /* the block's window count: the longest of the S scalars (every wave
+     reads them all, so W is the same in each without a barrier) */
+  int W = WMIN;
+#pragma unroll
+  for (int t = 0; t < S; t++) {
     uint32_t x[5] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int w = 0; w < 3; w++) x[w] = p.hs[(uint64_t)(3 * t + w) * p.cap + j];
+    for (int w = 0; w < KW; w++) x[w] = p.hs[(uint64_t)(KW * t + w) * p.cap + j];
     const int wt = (fd_half_bitlen<5>(x) + 4) >> 2;
     W = wt > W ? wt : W;
   }
@@ -1351,19 +1356,18 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm16q_kernel(fd_ed25519_verif
   uint32_t tab[9];
   {
     fe x, y;
-    const int which = q == 0 ? 0 : q == 1 ? 2 : q == 2 ? 1 : 3;   /* pts rows: A, R, A', R' */
-    const int32_t* src = p.pts + (uint64_t)which * 20 * p.cap + j;
+    const int32_t* src = p.pts + (uint64_t)(2 * part + side) * 20 * p.cap + j;
     load_fe(x, src, p.cap);
     load_fe(y, src + 10 * p.cap, p.cap);
-    table16_build(tab, r16_from_fe(x, k), r16_from_fe(y, k), q < 2 ? true : !(hf & FD_HF_DNEG), d2, k);
+    table16_build(tab, r16_from_fe(x, k), r16_from_fe(y, k), side == 0 ? true : !(hf & FD_HF_DNEG), d2, k);
   }
   uint32_t sd[5], bd[5];
   {
     uint32_t t[5], u[5];
-    shl160<64>(u, hk);                       /* W in [17, 22]: 160 - 4W - 64 in [8, 28] */
-    shl160v(t, u, 160 - 4 * W - 64);
+    shl160<SH0>(u, hk);                      /* 160 - 4W - SH0 in [8, 28] for every W that occurs */
+    shl160v(t, u, 160 - 4 * W - SH0);
     recode160<4>(sd, t);
-    shl160<80>(bd, hb);                      /* five 16-bit digits, the top one first */
+    shl160<160 - 16 * NB>(bd, hb);           /* the chunk's 16-bit digits, the top one first */
   }
   const int32_t* btab = p.btabq[q];
   const uint32_t one = r16_small(1u, k);
@@ -1373,7 +1377,7 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm16q_kernel(fd_ed25519_verif
     int e = pop160<4>(sd);
     if (it == W - 1) e &= 15;
     e = __builtin_amdgcn_readfirstlane(e);
-    const bool badd = it <= 16 && (it & 3) == 0;
+    const bool badd = it < 4 * NB && (it & 3) == 0;
     const uint32_t bdig = (uint32_t)__builtin_amdgcn_readfirstlane((int)(badd ? pop160u<16>(bd) : 0u));
     const uint32_t ce = table16_at(tab, e < 0 ? -e : e);
     fe braw;
@@ -1392,13 +1396,17 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm16q_kernel(fd_ed25519_verif
     }
     if (badd) P = ge16_add2<true>(P, b, false, k);
   }
-  /* waves 1-3's points as addends of wave 0's */
-  __shared__ uint32_t hand[3][64];
-  if (q) hand[q - 1][threadIdx.x & 63u] = ge16_to_qc(P, d2, k);
-  __syncthreads();
-  if (q) return;
+  /* the waves' points summed by halves: waves [h, 2h) hand theirs to
+     [0, h); every wave reaches every barrier */
+  __shared__ uint32_t hand[S / 2][64];
 #pragma unroll
-  for (int t = 0; t < 3; t++) P = ge16_add2<true>(P, hand[t][threadIdx.x], false, k);
+  for (int h = S / 2; h >= 1; h >>= 1) {
+    if (q >= h && q < 2 * h) hand[q - h][threadIdx.x & 63u] = ge16_to_qc(P, d2, k);
+    __syncthreads();
+    if (q < h) P = ge16_add2<true>(P, hand[q][threadIdx.x & 63u], false, k);
+    __syncthreads();
+  }
+  if (q) return;
   const uint32_t z = r16_rp<2, 2, 2, 2>(P, k);
   const bool zero = r16_iszero(P + ((k.p4 - z) & k.r1));
   const uint64_t bal = __ballot(zero);
@@ -1409,10 +1417,15 @@ __global__ void __launch_bounds__(256) fd_ed25519_dsm16q_kernel(fd_ed25519_verif
   if (threadIdx.x == 0u) p.out[p.base + j] = (int8_t)code;
 }
 
-extern "C" int fd_ed25519_hip_launch_dsm16q(const fd_ed25519_verify_params_t* p, void* stream) {
+extern "C" int fd_ed25519_hip_launch_dsm16s(const fd_ed25519_verify_params_t* p, int waves, void* stream) {
   if (!p->n) return 0;
-  if (!p->btabq[0] || !p->btabq[1] || !p->btabq[2] || !p->btabq[3]) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(fd_ed25519_dsm16q_kernel, dim3((uint32_t)p->n), dim3(256), 0, (hipStream_t)stream, *p);
+  if (waves != 4 && waves != 8) return (int)hipErrorInvalidValue;
+  for (int q = 0; q < waves; q++)
+    if (!p->btabq[q]) return (int)hipErrorInvalidValue;
+  if (waves == 4)
+    hipLaunchKernelGGL(fd_ed25519_dsm16s_kernel<4>, dim3((uint32_t)p->n), dim3(256), 0, (hipStream_t)stream, *p);
+  else
+    hipLaunchKernelGGL(fd_ed25519_dsm16s_kernel<8>, dim3((uint32_t)p->n), dim3(512), 0, (hipStream_t)stream, *p);
   return (int)hipGetLastError();
 }
 

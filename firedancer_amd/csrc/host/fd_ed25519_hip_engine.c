@@ -50,7 +50,7 @@ struct fd_ed25519_hip_engine {
   int32_t *    d_btab16;     /* [0..2^15]B, the verify kernels' wide B table  */
   int32_t *    d_btab8[2];   /* A/B build only (FD_ED25519_AB_LDS_BASE): the LDS-staged tables */
   int32_t *    btabw[2];    /* shared per device: [0..2^24)B, [0..2^24)[2^144]B */
-  int32_t *    btabq[4];    /* shared per device, engines with the r16 form: [0..2^16)[2^(72 q)]B (dsm16q) */
+  int32_t *    btabs[2][8]; /* shared per device: dsm16s<4>'s and <8>'s compact tables, when acquired */
   /* Pipeline lanes: the per-chunk scratch of a chunk in flight, and the
      streams its phases run on.  Lane 0 runs on the caller's stream (or the
      engine's); the chunks of a multi-chunk call alternate between lane 0
@@ -191,46 +191,51 @@ btabw_acquire( int device, int kind, hipStream_t stream, int32_t * tab[2] ) {
   return rc;
 }
 
-/* dsm16q's four compact tables at offsets 2^0, 2^72, 2^144, 2^216 (8 MiB
-   each), shared per device like the pairs above, by every engine whose
-   launch forms include the r16 one (its host-decoded launches) */
-#define FD_ED25519_BTABQ_SHIFT 72
-static struct { int refs; int32_t * tab[4]; } btabq[ FD_ED25519_HIP_MAX_DEV ];
+/* dsm16s<S>'s compact tables at offsets 2^(CB q), q < S (8 MiB each; CB
+   = 72 for S = 4, 32 for S = 8), shared per device like the pairs above,
+   made with the drop-in engines (a pipe's on demand).  Set 0: S = 4, set
+   1: S = 8. */
+static struct { int refs; int32_t * tab[8]; } btabs[ 2 ][ FD_ED25519_HIP_MAX_DEV ];
+
+static int split_set( int waves ) { return waves==8 ? 1 : 0; }
+static int split_cb( int waves ) { return waves==8 ? 32 : 72; }
 
 static int
-btabq_acquire( int device, hipStream_t stream, int32_t * tab[4] ) {
+btabs_acquire( int device, int waves, hipStream_t stream, int32_t * tab[8] ) {
+  int set = split_set( waves );
   pthread_mutex_lock( &btabw_lock );
   int rc = FD_ED25519_HIP_OK;
-  if( !btabq[device].refs ) {
-    int32_t * t[4] = { NULL, NULL, NULL, NULL };
+  if( !btabs[set][device].refs ) {
+    int32_t * t[8] = { NULL };
     int32_t * scratch = NULL;
     hipError_t he = hipSuccess;
-    for( int q=0; q<4 && he==hipSuccess; q++ ) he = hipMalloc( (void **)&t[q], btabw_bytes( 1 ) );
+    for( int q=0; q<waves && he==hipSuccess; q++ ) he = hipMalloc( (void **)&t[q], btabw_bytes( 1 ) );
     if( he==hipSuccess ) he = hipMalloc( (void **)&scratch, sizeof(int32_t) * (((size_t)1 << FD_ED25519_BTABC_BITS) * 10 + 64) );
-    for( int q=0; q<4 && he==hipSuccess; q++ )
-      he = (hipError_t)fd_ed25519_hip_launch_gen_btabw( t[q], FD_ED25519_BTABQ_SHIFT*q, FD_ED25519_BTABC_BITS, scratch, stream );
+    for( int q=0; q<waves && he==hipSuccess; q++ )
+      he = (hipError_t)fd_ed25519_hip_launch_gen_btabw( t[q], split_cb( waves )*q, FD_ED25519_BTABC_BITS, scratch, stream );
     if( he==hipSuccess ) he = hipStreamSynchronize( stream );
     hipFree( scratch );
     if( he!=hipSuccess ) {
-      for( int q=0; q<4; q++ ) hipFree( t[q] );
-      rc = hip_fail( he, "base tables (btabq)" );
+      for( int q=0; q<8; q++ ) hipFree( t[q] );
+      rc = hip_fail( he, "base tables (dsm16s)" );
     } else {
-      for( int q=0; q<4; q++ ) btabq[device].tab[q] = t[q];
+      for( int q=0; q<8; q++ ) btabs[set][device].tab[q] = t[q];
     }
   }
   if( rc==FD_ED25519_HIP_OK ) {
-    btabq[device].refs++;
-    for( int q=0; q<4; q++ ) tab[q] = btabq[device].tab[q];
+    btabs[set][device].refs++;
+    for( int q=0; q<8; q++ ) tab[q] = btabs[set][device].tab[q];
   }
   pthread_mutex_unlock( &btabw_lock );
   return rc;
 }
 
 static void
-btabq_release( int device ) {
+btabs_release( int device, int waves ) {
+  int set = split_set( waves );
   pthread_mutex_lock( &btabw_lock );
-  if( btabq[device].refs>0 && !--btabq[device].refs ) {
-    for( int q=0; q<4; q++ ) { hipFree( btabq[device].tab[q] ); btabq[device].tab[q] = NULL; }
+  if( btabs[set][device].refs>0 && !--btabs[set][device].refs ) {
+    for( int q=0; q<8; q++ ) { hipFree( btabs[set][device].tab[q] ); btabs[set][device].tab[q] = NULL; }
   }
   pthread_mutex_unlock( &btabw_lock );
 }
@@ -241,7 +246,8 @@ fd_ed25519_hip_shared_device_bytes( int device ) {
   pthread_mutex_lock( &btabw_lock );
   unsigned long b = 0UL;
   for( int kind=0; kind<2; kind++ ) if( btabw[kind][device].refs ) b += 2UL*btabw_bytes( kind );
-  if( btabq[device].refs ) b += 4UL*btabw_bytes( 1 );
+  if( btabs[0][device].refs ) b += 4UL*btabw_bytes( 1 );
+  if( btabs[1][device].refs ) b += 8UL*btabw_bytes( 1 );
   pthread_mutex_unlock( &btabw_lock );
   return b;
 }
@@ -367,7 +373,8 @@ engine_free( fd_ed25519_hip_engine_t * e ) {
   hipFree( e->d_btab ); hipFree( e->d_btab16 ); hipFree( e->d_btab8[0] ); hipFree( e->d_btab8[1] );
   for( int l=0; l<2; l++ ) { hipFree( e->lane[l].d_atab ); hipFree( e->lane[l].d_work ); }
   if( e->btabw[0] ) btabw_release( e->device, engine_btab_kind( e ) );
-  if( e->btabq[0] ) btabq_release( e->device );
+  if( e->btabs[0][0] ) btabs_release( e->device, 4 );
+  if( e->btabs[1][0] ) btabs_release( e->device, 8 );
   hipFree( e->d_msgs ); hipFree( e->d_off ); hipFree( e->d_sz ); hipFree( e->d_sigs ); hipFree( e->d_pubs );
   hipFree( e->d_out );  hipFree( e->d_tfirst ); hipFree( e->d_tcnt ); hipFree( e->d_tout );
   hipHostFree( e->h_msgs ); hipHostFree( e->h_off ); hipHostFree( e->h_sz ); hipHostFree( e->h_sigs );
@@ -680,7 +687,6 @@ params_tables( fd_ed25519_hip_engine_t * e, fd_ed25519_verify_params_t * p ) {
   p->bw_bits = engine_btab_kind( e ) ? FD_ED25519_BTABC_BITS : FD_ED25519_BTABW_BITS;
   p->codes_portable = (e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE) ? 1 : 0;
   p->half_dbits     = engine_half_dbits( e );
-  for( int q=0; q<4; q++ ) p->btabq[q] = e->btabq[q];
 }
 
 /* verify_dev and verify_digests_dev: messages hashed on the device, or
@@ -808,38 +814,36 @@ fd_ed25519_hip_private_hs_dsm( fd_ed25519_hip_engine_t * e, unsigned long n, uns
 }
 
 int
-fd_ed25519_hip_private_hs_dsm4( fd_ed25519_hip_engine_t * e, unsigned long n, unsigned char const * sigs,
+fd_ed25519_hip_private_hs_dsms( fd_ed25519_hip_engine_t * e, int waves, unsigned long n, unsigned char const * sigs,
                                 unsigned char const * pubs, signed char * out, unsigned char const * sflag,
-                                unsigned char const * hflag, unsigned int const * hq, int const * pts4,
+                                unsigned char const * hflag, unsigned int const * hq, int const * pts,
                                 unsigned char const * pflag, unsigned int const * go, void * stream ) {
   fd_ed25519_verify_params_t p;
   int err = hs_params( e, &p, n, sigs, pubs, out );
   if( err ) return err;
-  if( !sflag || !hflag || !hq || !pts4 || !pflag || !e->btabq[0] ) return FD_ED25519_HIP_ERR_INVAL;
+  if( (waves!=4 && waves!=8) || !sflag || !hflag || !hq || !pts || !pflag || !e->btabs[ split_set( waves ) ][0] )
+    return FD_ED25519_HIP_ERR_INVAL;
   p.sflag = (uint8_t *)sflag; p.hflag = (uint8_t *)hflag; p.hs = (uint32_t *)hq;
-  p.pts = (int32_t *)pts4; p.pflag = (uint8_t *)pflag;
+  p.pts = (int32_t *)pts; p.pflag = (uint8_t *)pflag;
   p.go = (uint32_t const *)go;
-  err = fd_ed25519_hip_launch_dsm16q( &p, stream ? (hipStream_t)stream : e->stream );
+  for( int q=0; q<8; q++ ) p.btabq[q] = e->btabs[ split_set( waves ) ][q];
+  err = fd_ed25519_hip_launch_dsm16s( &p, waves, stream ? (hipStream_t)stream : e->stream );
   if( err ) return hip_fail( (hipError_t)err, "verify launch" );
   return FD_ED25519_HIP_OK;
 }
 
+/* dsm16s<waves>'s tables for engine e (with the lane-split form), made on
+   first use per device: the drop-in engines take them at creation, a
+   pipe's engines only when a split form is asked for.  1: available. */
 int
-fd_ed25519_hip_private_has_dsm4( fd_ed25519_hip_engine_t const * e ) {
-  return e && e->btabq[0] ? 1 : 0;
-}
-
-/* dsm16q's tables for engine e (with the lane-split form), made on first
-   use per device: the drop-in engines take them at creation, a pipe's
-   engines only when its four-wave form is asked for.  1: available. */
-int
-fd_ed25519_hip_private_want_dsm4( fd_ed25519_hip_engine_t * e ) {
-  if( !e || !e->r16_max ) return 0;
-  if( !e->btabq[0] && hipSetDevice( e->device )==hipSuccess ) {
-    int32_t * t[4] = { NULL, NULL, NULL, NULL };
-    if( !btabq_acquire( e->device, e->stream, t ) ) for( int q=0; q<4; q++ ) e->btabq[q] = t[q];
+fd_ed25519_hip_private_want_dsms( fd_ed25519_hip_engine_t * e, int waves ) {
+  if( !e || !e->r16_max || (waves!=4 && waves!=8) ) return 0;
+  int set = split_set( waves );
+  if( !e->btabs[set][0] && hipSetDevice( e->device )==hipSuccess ) {
+    int32_t * t[8] = { NULL };
+    if( !btabs_acquire( e->device, waves, e->stream, t ) ) for( int q=0; q<8; q++ ) e->btabs[set][q] = t[q];
   }
-  return e->btabq[0] ? 1 : 0;
+  return e->btabs[set][0] ? 1 : 0;
 }
 
 int
@@ -1283,15 +1287,19 @@ fd_ed25519_hip_dropin_set_host_scalars_dbits( int dbits ) {
 #define DROPIN_HD_CAP 4UL   /* the hook's bound: the host arrays below */
 static unsigned long dropin_hd_max = DROPIN_HD_MAX;
 
-/* host-decoded drop-in launches take dsm16q (four waves, the chain
-   halved) when the engine holds its tables: 82 -> 69 us p50 for one
-   caller (profiles/r6_dropin_quarter.json); 0 keeps dsm16 (test / A-B
-   hook) */
-static int dropin_quarter = 1;
+/* host-decoded drop-in launches take the split form of this many waves
+   (dsm16s: 4 or 8, the host doubling A and R and splitting the scalars;
+   2: dsm16) when the engine holds its tables: 82 -> 69 us p50 with four
+   for one caller (profiles/r6_dropin_quarter.json); test / A-B hook
+   fd_ed25519_hip_dropin_set_split_waves */
+#ifndef DROPIN_SPLIT_WAVES
+#define DROPIN_SPLIT_WAVES 8
+#endif
+static int dropin_split = DROPIN_SPLIT_WAVES;
 
 void
-fd_ed25519_hip_dropin_set_quarter_form( int on ) {
-  dropin_quarter = on ? 1 : 0;
+fd_ed25519_hip_dropin_set_split_waves( int waves ) {
+  dropin_split = waves==4 || waves==8 ? waves : 2;
 }
 
 void
@@ -1337,7 +1345,7 @@ dropin_engine_make( int k ) {
   dq.h_blk[k] = NULL; dq.h_dev[k] = NULL; dq.d_blk[k] = NULL; dq.blk_cap[k] = 0UL;
   dq.direct_pending[k] = 0;
   dq.eng[k] = fd_ed25519_hip_engine_new( dq.device, DROPIN_CHUNK, dq.flags );
-  if( dq.eng[k] ) fd_ed25519_hip_private_want_dsm4( dq.eng[k] );   /* without them: dsm16's two waves */
+  if( dq.eng[k] && dropin_split>2 ) fd_ed25519_hip_private_want_dsms( dq.eng[k], dropin_split );   /* without: dsm16 */
   return dq.eng[k] ? FD_ED25519_HIP_OK : FD_ED25519_HIP_ERR_INVAL;
 }
 
@@ -1476,10 +1484,10 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   uint64_t need   = o_tout + n + 16UL;
   uint64_t cap_hs = e->max_chunk;
   uint64_t o_hsf = DROPIN_ALIGN16( need ), o_hhf = DROPIN_ALIGN16( o_hsf + cap_hs ), o_hs = DROPIN_ALIGN16( o_hhf + cap_hs );
-  /* hs: 19 rows (dsm16) or 24 (dsm16q's split scalars); pts: A, R and,
-     for dsm16q, [2^66]A, [2^66]R */
-  int quad = hdmode && dropin_quarter && fd_ed25519_hip_private_has_dsm4( e );
-  uint64_t o_pts = DROPIN_ALIGN16( o_hs + 24UL*4UL*cap_hs ), o_pfl = DROPIN_ALIGN16( o_pts + 4UL*20UL*4UL*cap_hs );
+  /* hs: 19 rows (dsm16) or 24 (dsm16s's split scalars); pts: A, R and,
+     for dsm16s, the doubled points (up to 8 rows of 20 limbs) */
+  int split = hdmode && dropin_split>2 && fd_ed25519_hip_private_want_dsms( e, dropin_split ) ? dropin_split : 0;
+  uint64_t o_pts = DROPIN_ALIGN16( o_hs + 24UL*4UL*cap_hs ), o_pfl = DROPIN_ALIGN16( o_pts + 8UL*20UL*4UL*cap_hs );
   uint64_t o_go  = DROPIN_ALIGN16( o_pfl + 2UL*cap_hs );
   if( hsmode ) need = hdmode ? o_go + 16UL : o_hs + 19UL*4UL*cap_hs;
   if( need>dq.blk_cap[k] ) {
@@ -1563,8 +1571,8 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
          dispatch overlaps this thread's scalars and decompressions; from
          here every path stores RUN or CANCEL */
       *go = 0U;
-      if( quad )
-        err = fd_ed25519_hip_private_hs_dsm4( e, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
+      if( split )
+        err = fd_ed25519_hip_private_hs_dsms( e, split, nsig, src + o_sig, src + o_pub, (signed char *)(src + o_out),
                                               src + o_hsf, src + o_hhf, (unsigned int const *)(src + o_hs),
                                               (int const *)(src + o_pts), src + o_pfl,
                                               (unsigned int const *)(src + o_go), st );
@@ -1586,30 +1594,33 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
       all = fd_ed25519_hip_private_hsrec( r->sigs, r->pubs, r->msg, r->msg_sz, dbits, rec );
       if( !all ) break;
       uint64_t j = tf[ t ];
-      if( quad ) fd_ed25519_hip_private_hsquad( rec, hs, cap_hs, j );
+      if( split ) fd_ed25519_hip_private_hssplit( rec, split, hs, cap_hs, j );
       else for( int w=0; w<19; w++ ) hs[ (uint64_t)w*cap_hs + j ] = rec[ 8 + w ];
       hsf[ j ] = (uint8_t)rec[ 27 ];
       hhf[ j ] = (uint8_t)rec[ 28 ];
     }
-    if( all && hdmode ) {   /* A and R of each signature, side by side (and [2^66]A, [2^66]R for dsm16q) */
+    if( all && hdmode ) {   /* A and R of each signature, side by side (and doubled, for dsm16s) */
       unsigned char const * enc[ 2UL*DROPIN_HD_CAP ];
-      int32_t       pt[ 2UL*DROPIN_HD_CAP ][ 20 ], pt66[ 2UL*DROPIN_HD_CAP ][ 20 ];
+      int32_t       pt[ 2UL*DROPIN_HD_CAP ][ 20 ], ptx[ 2UL*DROPIN_HD_CAP*3UL ][ 20 ];
       unsigned char fl[ 2UL*DROPIN_HD_CAP ];
+      int nx = split ? split/2 - 1 : 0, step = split==4 ? 66 : 33;
       t = 0UL;
       for( dropin_req_t * r=list; r; r=r->next, t++ ) { enc[ 2UL*t ] = r->pubs; enc[ 2UL*t+1UL ] = r->sigs; }
-      fd_ed25519_hip_private_hsdec2_n( enc, 2UL*nsig, !(e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE), &pt[0][0],
-                                       quad ? &pt66[0][0] : NULL, fl );
+      fd_ed25519_hip_private_hsdec3_n( enc, 2UL*nsig, !(e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE), &pt[0][0],
+                                       split ? &ptx[0][0] : NULL, nx, step, fl );
       int32_t * pts = (int32_t *)(h + o_pts);
       uint8_t * pfl = (uint8_t *)(h + o_pfl);
       t = 0UL;
       for( dropin_req_t * r=list; r; r=r->next, t++ ) {
         uint64_t j = tf[ t ];
-        for( uint64_t which=0UL; which<2UL; which++ ) {   /* 0: A, 1: R (2, 3: doubled) -- [4][20][cap] */
+        for( uint64_t side=0UL; side<2UL; side++ ) {   /* rows 2i + side: A, R, A_1, R_1, .. -- [S][20][cap] */
+          uint64_t pi = 2UL*t + side;
           for( uint64_t l=0UL; l<20UL; l++ ) {
-            pts[ ( which*20UL + l )*cap_hs + j ] = pt[ 2UL*t + which ][ l ];
-            if( quad ) pts[ ( (2UL + which)*20UL + l )*cap_hs + j ] = pt66[ 2UL*t + which ][ l ];
+            pts[ ( side*20UL + l )*cap_hs + j ] = pt[ pi ][ l ];
+            for( int m=1; m<=nx; m++ )
+              pts[ ( ( 2UL*(uint64_t)m + side )*20UL + l )*cap_hs + j ] = ptx[ pi*(uint64_t)nx + (uint64_t)(m-1) ][ l ];
           }
-          pfl[ which*cap_hs + j ] = fl[ 2UL*t + which ];
+          pfl[ side*cap_hs + j ] = fl[ pi ];
         }
       }
     }

@@ -290,40 +290,47 @@ void limbs_point( int32_t pt[ 20 ], f51 const & x, f51 const & y ) {
   limbs_frombytes( pt + 10, yb );
 }
 
-/* [2^n](x, y) for N points at once (extended coordinates without T,
-   dbl-2008-hwcd for a = -1), then affine with one shared inversion */
+/* [2^(step m)](x, y) for m = 1 .. nx (nx <= 3), for N points at once
+   (extended coordinates without T, dbl-2008-hwcd for a = -1), then affine
+   with one shared inversion: ox / oy[ i nx + m-1 ] */
 template< int N >
-void dbl_n( f51 ( &x )[ N ], f51 ( &y )[ N ], int n ) {
+void dbl_n( f51 const ( &x )[ N ], f51 const ( &y )[ N ], int step, int nx, f51 * ox, f51 * oy ) {
   const f51 zero = { { 0ULL, 0ULL, 0ULL, 0ULL, 0ULL } };
   f51 X[ N ], Y[ N ], Z[ N ];
+  f51 sx[ N*3 ], sy[ N*3 ], sz[ N*3 ];
   for( int i=0; i<N; i++ ) { X[ i ] = x[ i ]; Y[ i ] = y[ i ]; Z[ i ] = one(); }
-  for( int r=0; r<n; r++ ) {
-    for( int i=0; i<N; i++ ) {
-      f51 A = sq( X[ i ] ), B = sq( Y[ i ] ), Z2 = sq( Z[ i ] );
-      f51 C = add( Z2, Z2 );
-      f51 E = sub( sub( sq( add( X[ i ], Y[ i ] ) ), A ), B );
-      f51 G = sub( B, A );                    /* D + B, D = -A */
-      f51 F = sub( G, C );
-      f51 H = sub( zero, add( A, B ) );       /* D - B         */
-      X[ i ] = mul( E, F ); Y[ i ] = mul( G, H ); Z[ i ] = mul( F, G );
+  for( int m=0; m<nx; m++ ) {
+    for( int r=0; r<step; r++ ) {
+      for( int i=0; i<N; i++ ) {
+        f51 A = sq( X[ i ] ), B = sq( Y[ i ] ), Z2 = sq( Z[ i ] );
+        f51 C = add( Z2, Z2 );
+        f51 E = sub( sub( sq( add( X[ i ], Y[ i ] ) ), A ), B );
+        f51 G = sub( B, A );                    /* D + B, D = -A */
+        f51 F = sub( G, C );
+        f51 H = sub( zero, add( A, B ) );       /* D - B         */
+        X[ i ] = mul( E, F ); Y[ i ] = mul( G, H ); Z[ i ] = mul( F, G );
+      }
     }
+    for( int i=0; i<N; i++ ) { sx[ i*nx + m ] = X[ i ]; sy[ i*nx + m ] = Y[ i ]; sz[ i*nx + m ] = Z[ i ]; }
   }
-  /* 1/Z_i from one inversion: prefix products */
-  f51 pre[ N ], inv[ 1 ];
-  pre[ 0 ] = Z[ 0 ];
-  for( int i=1; i<N; i++ ) pre[ i ] = mul( pre[ i-1 ], Z[ i ] );
-  inv[ 0 ] = pre[ N-1 ];
+  /* 1/Z from one inversion: prefix products */
+  const int T = N*nx;
+  f51 pre[ N*3 ], inv[ 1 ];
+  pre[ 0 ] = sz[ 0 ];
+  for( int t=1; t<T; t++ ) pre[ t ] = mul( pre[ t-1 ], sz[ t ] );
+  inv[ 0 ] = pre[ T-1 ];
   inv_n< 1 >( inv );
   f51 acc = inv[ 0 ];
-  for( int i=N-1; i>=0; i-- ) {
-    f51 zi = i ? mul( acc, pre[ i-1 ] ) : acc;
-    if( i ) acc = mul( acc, Z[ i ] );
-    x[ i ] = mul( X[ i ], zi ); y[ i ] = mul( Y[ i ], zi );
+  for( int t=T-1; t>=0; t-- ) {
+    f51 zi = t ? mul( acc, pre[ t-1 ] ) : acc;
+    if( t ) acc = mul( acc, sz[ t ] );
+    ox[ t ] = mul( sx[ t ], zi ); oy[ t ] = mul( sy[ t ], zi );
   }
 }
 
 template< int N >
-void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsigned char * flags, int32_t * pt66 ) {
+void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsigned char * flags, int32_t * ptx,
+            int nx, int step ) {
   dec_state d[ N ];
   f51 x[ N ];
   for( int i=0; i<N; i++ ) dec_pre( d[ i ], x[ i ], enc[ i ] );
@@ -333,9 +340,10 @@ void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsig
     flags[ i ] = (unsigned char)dec_post( d[ i ], x[ i ], enc[ i ], avx_rule, pt + 20*i, &xs[ i ] );
     ys[ i ] = d[ i ].y;
   }
-  if( !pt66 ) return;
-  dbl_n< N >( xs, ys, 66 );
-  for( int i=0; i<N; i++ ) limbs_point( pt66 + 20*i, xs[ i ], ys[ i ] );
+  if( !ptx || nx<1 ) return;
+  f51 ox[ N*3 ], oy[ N*3 ];
+  dbl_n< N >( xs, ys, step, nx, ox, oy );
+  for( int t=0; t<N*nx; t++ ) limbs_point( ptx + 20*t, ox[ t ], oy[ t ] );
 }
 
 } /* namespace */
@@ -344,12 +352,18 @@ void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsig
    int32, the work arrays' limbs of (x, y) per point; flags[i]: 1
    FD_PF_FAIL, 2 FD_PF_SMALL (fd_ed25519_hip_internal.h).  avx_rule: the
    AVX-512 build's codes (an engine without
-   FD_ED25519_HIP_FLAG_CODES_PORTABLE). */
+   FD_ED25519_HIP_FLAG_CODES_PORTABLE).  ptx (when not NULL): each point
+   also doubled step, 2 step, .. nx step times (nx <= 3), affine, in the
+   same limbs -- ptx[(i nx + m-1) 20 ..] = [2^(step m)]P_i, the split
+   forms' A_i and R_i (a failed decode's are any values: its code is the
+   decode's). */
 extern "C" void
-fd_ed25519_hip_private_hsdec2_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
-                                 int32_t * pt66, unsigned char * flags ) {
+fd_ed25519_hip_private_hsdec3_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
+                                 int32_t * ptx, int nx, int step, unsigned char * flags ) {
+  if( nx>3 ) nx = 3;
   unsigned long i = 0UL;
-#define HSDEC_GROUP( N ) dec_n< N >( enc + i, avx_rule, pt + 20UL*i, flags + i, pt66 ? pt66 + 20UL*i : NULL )
+#define HSDEC_GROUP( N ) dec_n< N >( enc + i, avx_rule, pt + 20UL*i, flags + i, \
+                                     ptx ? ptx + 20UL*(unsigned long)nx*i : NULL, nx, step )
   for( ; i+4UL<=n; i+=4UL ) HSDEC_GROUP( 4 );
   if( n-i==3UL ) HSDEC_GROUP( 3 );
   if( n-i==2UL ) HSDEC_GROUP( 2 );
@@ -357,47 +371,58 @@ fd_ed25519_hip_private_hsdec2_n( unsigned char const * const * enc, unsigned lon
 #undef HSDEC_GROUP
 }
 
-/* pt66 (when not NULL): each point doubled 66 times, [2^66]P, affine, in
-   the same limbs -- the dsm16q form's A' and R' (a failed decode's is any
-   value: its code is the decode's) */
 extern "C" void
 fd_ed25519_hip_private_hsdec_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
                                 unsigned char * flags ) {
-  fd_ed25519_hip_private_hsdec2_n( enc, n, avx_rule, pt, NULL, flags );
+  fd_ed25519_hip_private_hsdec3_n( enc, n, avx_rule, pt, NULL, 0, 0, flags );
 }
 
-/* dsm16q's scalars from a host record (hsrec's layout: c rec[8..12], |d|
-   rec[13..17], s' = rec[18..22] (bits 0..143) + rec[23..26] << 144): hq
-   rows 3q..3q+2 = c0, c1, d0, d1 (c and |d| split at bit 66), rows
-   12+3q..14+3q = bits [72 q, 72 q + 72) of s', each at column j of stride
-   cap */
+/* the split forms' scalars from a host record (hsrec's layout: c
+   rec[8..12], |d| rec[13..17], s' = rec[18..22] (bits 0..143) + rec[23..26]
+   << 144), at column j of stride cap:
+     waves 4: rows 3q..3q+2 = c0, c1, d0, d1 (c and |d| split at bit 66),
+              rows 12+3q..14+3q = bits [72 q, 72 q + 72) of s';
+     waves 8: rows 2q, 2q+1 = c0..c3, d0..d3 (split every 33 bits, the
+              last part the rest), row 16+q = bits [32 q, 32 q + 32). */
 extern "C" void
-fd_ed25519_hip_private_hsquad( uint32_t const rec[ 32 ], uint32_t * hq, unsigned long cap, unsigned long j ) {
-  u128 c_lo = 0, c_hi = 0, d_lo = 0, d_hi = 0;
-  uint32_t cw[ 6 ] = { rec[ 8 ], rec[ 9 ], rec[ 10 ], rec[ 11 ], rec[ 12 ], 0u };
-  uint32_t dw[ 6 ] = { rec[ 13 ], rec[ 14 ], rec[ 15 ], rec[ 16 ], rec[ 17 ], 0u };
-  /* 160-bit values as (low 66 bits, the rest) */
-  u128 cl = (u128)cw[ 0 ] | (u128)cw[ 1 ] << 32 | (u128)cw[ 2 ] << 64 | (u128)cw[ 3 ] << 96;
-  u128 dl = (u128)dw[ 0 ] | (u128)dw[ 1 ] << 32 | (u128)dw[ 2 ] << 64 | (u128)dw[ 3 ] << 96;
-  const u128 m66 = ( (u128)1 << 66 ) - 1;
-  c_lo = cl & m66; c_hi = ( cl >> 66 ) | (u128)cw[ 4 ] << 62;
-  d_lo = dl & m66; d_hi = ( dl >> 66 ) | (u128)dw[ 4 ] << 62;
-  u128 k4[ 4 ] = { c_lo, c_hi, d_lo, d_hi };
-  for( int q=0; q<4; q++ )
-    for( int w=0; w<3; w++ ) hq[ (unsigned long)( 3*q + w )*cap + j ] = (uint32_t)( k4[ q ] >> ( 32*w ) );
+fd_ed25519_hip_private_hssplit( uint32_t const rec[ 32 ], int waves, uint32_t * hq, unsigned long cap, unsigned long j ) {
+  const int H = waves==8 ? 4 : 2, G = waves==8 ? 33 : 66, KW = waves==8 ? 2 : 3;
+  for( int side=0; side<2; side++ ) {
+    uint32_t const * w = rec + ( side ? 13 : 8 );   /* 160 bits */
+    for( int i=0; i<H; i++ ) {
+      /* bits [G i, G (i+1)) of the value -- the last part all the rest -- as KW words */
+      for( int o=0; o<KW; o++ ) {
+        int b = G*i + 32*o;
+        uint32_t x = 0u;
+        if( b<160 ) {
+          int wi = b >> 5, sh = b & 31;
+          uint64_t v = (uint64_t)w[ wi ] | ( wi+1<5 ? (uint64_t)w[ wi+1 ] << 32 : 0ULL );
+          x = (uint32_t)( v >> sh );
+        }
+        int keep = i<H-1 ? G - 32*o : 160;   /* bits of this word that belong to the part */
+        if( keep<=0 ) x = 0u;
+        else if( keep<32 ) x &= ( 1u << keep ) - 1u;
+        hq[ (unsigned long)( KW*( H*side + i ) + o )*cap + j ] = x;
+      }
+    }
+  }
   /* s' (253 bits) from its two halves */
   uint32_t sw[ 9 ];
-  for( int w=0; w<4; w++ ) sw[ w ] = rec[ 18 + w ];
+  for( int o=0; o<4; o++ ) sw[ o ] = rec[ 18 + o ];
   sw[ 4 ] = ( rec[ 22 ] & 0xffffu ) | ( rec[ 23 ] << 16 );
-  for( int w=5; w<8; w++ ) sw[ w ] = ( rec[ 18 + w ] >> 16 ) | ( rec[ 19 + w ] << 16 );
+  for( int o=5; o<8; o++ ) sw[ o ] = ( rec[ 18 + o ] >> 16 ) | ( rec[ 19 + o ] << 16 );
   sw[ 8 ] = rec[ 26 ] >> 16;
+  if( waves==8 ) {
+    for( int q=0; q<8; q++ ) hq[ (unsigned long)( 16 + q )*cap + j ] = sw[ q ];
+    return;
+  }
   for( int q=0; q<4; q++ ) {
-    for( int w=0; w<3; w++ ) {   /* bits 72q + 32w .. +31 of s', masked to the chunk's 72 */
-      int b = 72*q + 32*w, wi = b >> 5, sh = b & 31;
+    for( int o=0; o<3; o++ ) {   /* bits 72q + 32o .. +31 of s', masked to the chunk's 72 */
+      int b = 72*q + 32*o, wi = b >> 5, sh = b & 31;
       uint64_t v = (uint64_t)sw[ wi ] | ( wi+1<9 ? (uint64_t)sw[ wi+1 ] << 32 : 0ULL );
       uint32_t x = (uint32_t)( v >> sh );
-      if( w==2 ) x &= 0xffu;   /* 64 + 8 bits */
-      hq[ (unsigned long)( 12 + 3*q + w )*cap + j ] = x;
+      if( o==2 ) x &= 0xffu;   /* 64 + 8 bits */
+      hq[ (unsigned long)( 12 + 3*q + o )*cap + j ] = x;
     }
   }
 }

@@ -227,18 +227,19 @@ fd_ed25519_hip_pipe_set_host_scalars( unsigned long max_sigs ) {
 #define PIPE_HD_CAP 4UL
 static unsigned long pipe_hd_max = PIPE_HD_MAX;
 
-/* ... in dsm16q's four waves (1) or dsm16's two (0, the default): the
-   four-wave form puts the 66 doublings of A and R on the submitting
-   thread, which is the tile's own -- at the reference tile's loads it
-   lost (p50 0.092 / 0.130 / 0.171 ms against 0.086 / 0.086 / 0.103 at
-   29K / 46K / 54K txn/s, the batches growing as the tile thread fell
-   behind, profiles/r6_pipe_quarter.jsonl) while the synchronous drop-in,
-   whose caller waits anyway, gains (fd_ed25519_hip_dropin_set_quarter_form) */
-static int pipe_quarter = 0;
+/* ... in a split form's four or eight waves (dsm16s) or dsm16's two (2,
+   the default): the split forms put the doublings of A and R on the
+   submitting thread, which is the tile's own -- at the reference tile's
+   loads four waves lost (p50 0.092 / 0.130 / 0.171 ms against 0.086 /
+   0.086 / 0.103 at 29K / 46K / 54K txn/s, the batches growing as the tile
+   thread fell behind, profiles/r6_pipe_quarter.jsonl) while the
+   synchronous drop-in, whose caller waits anyway, gains
+   (fd_ed25519_hip_dropin_set_split_waves) */
+static int pipe_split = 2;
 
 void
-fd_ed25519_hip_pipe_set_quarter_form( int on ) {
-  pipe_quarter = on ? 1 : 0;
+fd_ed25519_hip_pipe_set_split_waves( int waves ) {
+  pipe_split = waves==4 || waves==8 ? waves : 2;
 }
 
 void
@@ -247,12 +248,12 @@ fd_ed25519_hip_pipe_set_host_decode( unsigned long max_sigs ) {
 }
 
 /* the page-locked host-scalar block: sflag [cap], hflag [cap], hs [24][cap]
-   words (dsm16: 19 rows; dsm16q: 24), pts [4][20][cap] words (A, R; dsm16q
-   also [2^66]A, [2^66]R), pflag [2][cap], the go word (params.go) */
+   words (dsm16: 19 rows; dsm16s: 24), pts [8][20][cap] words (A, R; dsm16s
+   also the doubled points), pflag [2][cap], the go word (params.go) */
 #define HS_O_HS( cap )  ( 2UL*(cap) )
 #define HS_O_PTS( cap ) ( ( 2UL + 24UL*4UL )*(cap) )
-#define HS_O_PFL( cap ) ( ( 2UL + 24UL*4UL + 4UL*20UL*4UL )*(cap) )
-#define HS_O_GO( cap )  ( ( ( 2UL + 24UL*4UL + 4UL*20UL*4UL + 2UL )*(cap) + 15UL ) & ~15UL )
+#define HS_O_PFL( cap ) ( ( 2UL + 24UL*4UL + 8UL*20UL*4UL )*(cap) )
+#define HS_O_GO( cap )  ( ( ( 2UL + 24UL*4UL + 8UL*20UL*4UL + 2UL )*(cap) + 15UL ) & ~15UL )
 #define HS_BYTES( cap ) ( HS_O_GO( cap ) + 16UL )
 
 struct fd_ed25519_hip_pipe {
@@ -530,7 +531,7 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
   unsigned long n = slot->sig_cnt, cap = slot->sig_cap;
   unsigned long o_sigs = (unsigned long)( slot->sigs - s->h_in ), o_pubs = (unsigned long)( slot->pubs - s->h_in );
   int err, hd = n<=pipe_hd_max;
-  int quad = hd && pipe_quarter && fd_ed25519_hip_private_want_dsm4( s->eng );
+  int split = hd && pipe_split>2 && fd_ed25519_hip_private_want_dsms( s->eng, pipe_split ) ? pipe_split : 0;
   volatile uint32_t * go = (volatile uint32_t *)( s->h_hs + HS_O_GO( cap ) );
   if( !hd ) {
     PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_decode( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
@@ -540,8 +541,8 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
     /* dsm16 first, waiting on the go word while this thread computes
        (params.go); every path below stores RUN or CANCEL */
     *go = 0U;
-    if( quad ) {
-      PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm4( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
+    if( split ) {
+      PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsms( s->eng, split, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
                                                                    (signed char *)s->h_outb_dev, s->h_hs_dev,
                                                                    s->h_hs_dev + cap,
                                                                    (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
@@ -569,27 +570,30 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
       if( hd ) __atomic_store_n( go, FD_ED25519_GO_CANCEL, __ATOMIC_RELEASE );
       return 0;
     }
-    if( quad ) fd_ed25519_hip_private_hsquad( rec, hs, cap, i );
+    if( split ) fd_ed25519_hip_private_hssplit( rec, split, hs, cap, i );
     else for( int w=0; w<19; w++ ) hs[ (unsigned long)w*cap + i ] = rec[ 8 + w ];
     hsf[ i ] = (unsigned char)rec[ 27 ];
     hhf[ i ] = (unsigned char)rec[ 28 ];
   }
   if( hd ) {   /* A and R of each signature, side by side */
     unsigned char const * enc[ 2UL*PIPE_HD_CAP ];
-    int32_t       pt[ 2UL*PIPE_HD_CAP ][ 20 ], pt66[ 2UL*PIPE_HD_CAP ][ 20 ];
+    int32_t       pt[ 2UL*PIPE_HD_CAP ][ 20 ], ptx[ 2UL*PIPE_HD_CAP*3UL ][ 20 ];
     unsigned char fl[ 2UL*PIPE_HD_CAP ];
+    int nx = split ? split/2 - 1 : 0, step = split==4 ? 66 : 33;
     for( unsigned long i=0UL; i<n; i++ ) { enc[ 2UL*i ] = slot->pubs + 32UL*i; enc[ 2UL*i+1UL ] = slot->sigs + 64UL*i; }
-    fd_ed25519_hip_private_hsdec2_n( enc, 2UL*n, !fd_ed25519_hip_private_codes_portable( s->eng ), &pt[0][0],
-                                     quad ? &pt66[0][0] : NULL, fl );
+    fd_ed25519_hip_private_hsdec3_n( enc, 2UL*n, !fd_ed25519_hip_private_codes_portable( s->eng ), &pt[0][0],
+                                     split ? &ptx[0][0] : NULL, nx, step, fl );
     int32_t * pts = (int32_t *)( s->h_hs + HS_O_PTS( cap ) );
     unsigned char * pfl = s->h_hs + HS_O_PFL( cap );
     for( unsigned long i=0UL; i<n; i++ )
-      for( unsigned long which=0UL; which<2UL; which++ ) {   /* 0: A, 1: R (2, 3: doubled, dsm16q) */
+      for( unsigned long side=0UL; side<2UL; side++ ) {   /* rows 2i + side: A, R, A_1, R_1, .. */
+        unsigned long pi = 2UL*i + side;
         for( unsigned long l=0UL; l<20UL; l++ ) {
-          pts[ ( which*20UL + l )*cap + i ] = pt[ 2UL*i + which ][ l ];
-          if( quad ) pts[ ( ( 2UL + which )*20UL + l )*cap + i ] = pt66[ 2UL*i + which ][ l ];
+          pts[ ( side*20UL + l )*cap + i ] = pt[ pi ][ l ];
+          for( int m=1; m<=nx; m++ )
+            pts[ ( ( 2UL*(unsigned long)m + side )*20UL + l )*cap + i ] = ptx[ pi*(unsigned long)nx + (unsigned long)(m-1) ][ l ];
         }
-        pfl[ which*cap + i ] = fl[ 2UL*i + which ];
+        pfl[ side*cap + i ] = fl[ pi ];
       }
   }
   if( hd ) {

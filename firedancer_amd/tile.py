@@ -333,14 +333,14 @@ def pipe_set_host_decode(max_sigs):
     _lib.fd_ed25519_hip_pipe_set_host_decode(int(max_sigs))
 
 
-_lib.fd_ed25519_hip_pipe_set_quarter_form.argtypes = [ctypes.c_int]
-_lib.fd_ed25519_hip_pipe_set_quarter_form.restype = None
+_lib.fd_ed25519_hip_pipe_set_split_waves.argtypes = [ctypes.c_int]
+_lib.fd_ed25519_hip_pipe_set_split_waves.restype = None
 
 
-def pipe_set_quarter_form(on):
-    """fd_ed25519_hip_pipe_set_quarter_form: host-decoded pipe batches in
-    dsm16q's four waves (1) or dsm16's two (0, the default)."""
-    _lib.fd_ed25519_hip_pipe_set_quarter_form(1 if on else 0)
+def pipe_set_split_waves(waves):
+    """fd_ed25519_hip_pipe_set_split_waves: host-decoded pipe batches over
+    4 or 8 waves (dsm16s) or dsm16's 2 (the default)."""
+    _lib.fd_ed25519_hip_pipe_set_split_waves(int(waves))
 
 
 def latency_set_cpus(producer_cpu=-1, tile_cpu=-1):

@@ -125,15 +125,15 @@ fd_ed25519_hip_dropin_set_host_scalars_dbits( int dbits );
 void
 fd_ed25519_hip_dropin_set_host_decode( unsigned long max_sigs );
 
-/* Host-decoded drop-in launches run the group equation in four waves --
-   the calling thread also doubles A and R 66 times and splits the
-   half-size scalars at bit 66 and s' at 72-bit boundaries, so each wave's
-   chain is ~17 windows instead of 33 -- from four compact base tables at
-   offsets 2^0, 2^72, 2^144, 2^216 (32 MiB per device, made with the
-   drop-in engines).  Test / A-B hook, process-wide: 0 keeps the two-wave
-   form (default 1). */
+/* Host-decoded drop-in launches run the group equation split over
+   `waves` waves (4 or 8; 2: dsm16's two) -- the calling thread also
+   doubles A and R every 66 (4) or 33 (8) bits and splits the half-size
+   scalars there and s' into 72- or 32-bit chunks, so each wave's chain is
+   ~17 or ~9 windows instead of 33 -- from compact base tables at offsets
+   2^(72 q) or 2^(32 q) (32 or 64 MiB per device, made with the drop-in
+   engines).  Test / A-B hook, process-wide (default 8). */
 void
-fd_ed25519_hip_dropin_set_quarter_form( int on );
+fd_ed25519_hip_dropin_set_split_waves( int waves );
 
 unsigned long
 fd_ed25519_hip_dropin_device_bytes( void );

@@ -159,11 +159,12 @@ fd_ed25519_hip_pipe_set_host_scalars( unsigned long max_sigs );
 void
 fd_ed25519_hip_pipe_set_host_decode( unsigned long max_sigs );
 
-/* ... and those batches in four waves (1, fd_ed25519_hip_dropin_set_
-   quarter_form's form) or two (0, the default: the extra host work sits on
-   the tile's own thread, where it costs more than the shorter chain saves). */
+/* ... and those batches split over 4 or 8 waves
+   (fd_ed25519_hip_dropin_set_split_waves's forms) or dsm16's two (2, the
+   default: the extra host work sits on the tile's own thread, where it
+   costs more than the shorter chain saves). */
 void
-fd_ed25519_hip_pipe_set_quarter_form( int on );
+fd_ed25519_hip_pipe_set_split_waves( int waves );
 
 /* ---- txn -------------------------------------------------------------- */
 

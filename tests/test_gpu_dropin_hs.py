@@ -4,9 +4,10 @@ k, S < L and the half-size pair from the calling thread while the GPU
 decompresses A and R, and dsm16 reads them from the page-locked block; the
 fewest-signature launches (fd_ed25519_hip_dropin_set_host_decode,
 host/fd_ed25519_hip_hsdec.cc) decompress A and R on the calling thread too
-and launch the group equation alone, reading the points in place -- in
-four waves on [2^66]A and [2^66]R doubled by the host too (dsm16q,
-fd_ed25519_hip_dropin_set_quarter_form) or in dsm16's two.  Every fixture class -- the reference's vectors, the adversarial set,
+and launch the group equation alone, reading the points in place -- over
+eight or four waves on A and R doubled by the host every 33 or 66 bits
+(dsm16s, fd_ed25519_hip_dropin_set_split_waves) or in dsm16's two.  Every
+fixture class -- the reference's vectors, the adversarial set,
 mixed-order points, k needing long |d| -- through fd_ed25519_verify with
 each mode on (the default) and off, code by code against the reference's
 own codes (tests/golden/, oracle/_ref)."""
@@ -27,25 +28,26 @@ def ed():
     lib = ed25519.library()
     lib.fd_ed25519_hip_dropin_set_host_scalars.argtypes = [ctypes.c_ulong]
     lib.fd_ed25519_hip_dropin_set_host_decode.argtypes = [ctypes.c_ulong]
-    lib.fd_ed25519_hip_dropin_set_quarter_form.argtypes = [ctypes.c_int]
+    lib.fd_ed25519_hip_dropin_set_split_waves.argtypes = [ctypes.c_int]
     yield ed25519, lib
     lib.fd_ed25519_hip_dropin_set_host_scalars(4)
     lib.fd_ed25519_hip_dropin_set_host_decode(2)
-    lib.fd_ed25519_hip_dropin_set_quarter_form(1)
+    lib.fd_ed25519_hip_dropin_set_split_waves(8)
 
 
 def _run(ed25519, d, idx):
     return np.array([ed25519.verify(*case(d, i)) for i in idx], np.int8)
 
 
-@pytest.mark.parametrize("mode", [(4, 2, 1), (4, 2, 0), (4, 0, 1), (0, 0, 1)],
-                         ids=["host-decode-quarter", "host-decode-two-wave", "host-scalars", "device"])
+@pytest.mark.parametrize("mode", [(4, 2, 8), (4, 2, 4), (4, 2, 2), (4, 0, 8), (0, 0, 8)],
+                         ids=["host-decode-eight-waves", "host-decode-four-waves", "host-decode-two-waves",
+                              "host-scalars", "device"])
 @pytest.mark.parametrize("fixture", ["vectors", "adversarial", "mixed_order", "halfsize", "longd"])
 def test_dropin_codes_every_host_path(ed, request, mode, fixture):
     ed25519, lib = ed
     lib.fd_ed25519_hip_dropin_set_host_scalars(mode[0])
     lib.fd_ed25519_hip_dropin_set_host_decode(mode[1])
-    lib.fd_ed25519_hip_dropin_set_quarter_form(mode[2])
+    lib.fd_ed25519_hip_dropin_set_split_waves(mode[2])
     d = request.getfixturevalue(fixture)
     n = len(d["msg_sz"])
     idx = list(range(0, n, 3 if n > 3000 else 1))
@@ -55,14 +57,15 @@ def test_dropin_codes_every_host_path(ed, request, mode, fixture):
     assert len(bad) == 0, [(str(d["tags"][idx[i]]), int(got[i]), int(want[i])) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("callers,hd", [(2, 2), (4, 4), (4, 0)])
-def test_dropin_host_scalars_concurrent_callers(ed, adversarial, mixed_order, callers, hd):
+@pytest.mark.parametrize("callers,hd,waves", [(2, 2, 8), (4, 4, 8), (4, 4, 4), (4, 0, 8)])
+def test_dropin_host_scalars_concurrent_callers(ed, adversarial, mixed_order, callers, hd, waves):
     """Threads calling at once: their requests may combine into launches of
     two to four signatures (still host-scalar launches; with the host
     decompressions up to hd of them) -- codes exact."""
     ed25519, lib = ed
     lib.fd_ed25519_hip_dropin_set_host_scalars(4)
     lib.fd_ed25519_hip_dropin_set_host_decode(hd)
+    lib.fd_ed25519_hip_dropin_set_split_waves(waves)
     for d in (adversarial, mixed_order):
         n = min(len(d["msg_sz"]), 2000)
         out = np.zeros(n, np.int8)
@@ -77,6 +80,7 @@ def test_dropin_host_scalars_concurrent_callers(ed, adversarial, mixed_order, ca
             t.join()
         assert np.array_equal(out, d["codes_avx512"][:n])
     lib.fd_ed25519_hip_dropin_set_host_decode(2)
+    lib.fd_ed25519_hip_dropin_set_split_waves(8)
 
 
 def test_dropin_host_scalars_fallback_to_the_device_path(ed, halfsize, adversarial):

@@ -349,20 +349,21 @@ def test_pipe_stages_in_place_and_rejects_out_of_range(tile, adversarial):
     p.close()
 
 
-@pytest.mark.parametrize("hs,hd,quarter", [(4, 2, 0), (4, 4, 0), (4, 4, 1), (4, 0, 0), (0, 0, 0)],
-                         ids=["host-decode2", "host-decode4", "host-decode4-quarter", "host-scalars", "device-path"])
-def test_pipe_tiny_batches_every_path(tile, adversarial, mixed_order, batch, hs, hd, quarter):
+@pytest.mark.parametrize("hs,hd,waves", [(4, 2, 2), (4, 4, 2), (4, 4, 4), (4, 4, 8), (4, 0, 2), (0, 0, 2)],
+                         ids=["host-decode2", "host-decode4", "host-decode4-four-waves", "host-decode4-eight-waves",
+                              "host-scalars", "device-path"])
+def test_pipe_tiny_batches_every_path(tile, adversarial, mixed_order, batch, hs, hd, waves):
     """Batches of one to four signatures (a tile at a low load), through the
     host-scalar path (prep16's decode blocks + dsm16 reading the staged
     block in place, transaction codes combined on the host), with the
     decompressions on the submitting thread too for batches of at most hd
-    signatures (the group equation alone, reading the points in place: in
-    dsm16q's four waves or dsm16's two), and through the device path: single signatures of the adversarial and mixed-order sets,
+    signatures (the group equation alone, reading the points in place: over
+    dsm16s's four or eight waves or dsm16's two), and through the device path: single signatures of the adversarial and mixed-order sets,
     and the batch_single_msg transactions of one to four signatures (the
     priority rule included), against the reference's codes."""
     tile.pipe_set_host_scalars(hs)
     tile.pipe_set_host_decode(hd)
-    tile.pipe_set_quarter_form(quarter)
+    tile.pipe_set_split_waves(waves)
     try:
         p = tile.Pipe(0, slot_cnt=3, sig_cap=256, msg_cap=256 * 1300, txn_cap=256)
         jobs = []   # (msgs [(bytes)], sigs, pubs, txn?, want)
@@ -426,4 +427,4 @@ def test_pipe_tiny_batches_every_path(tile, adversarial, mixed_order, batch, hs,
     finally:
         tile.pipe_set_host_scalars(4)
         tile.pipe_set_host_decode(4)
-        tile.pipe_set_quarter_form(0)
+        tile.pipe_set_split_waves(2)

@@ -121,74 +121,88 @@ def _limbs_value(limbs):
 
 
 @pytest.fixture(scope="module")
-def hsdec2():
+def hsdec3():
     from firedancer_amd import ed25519
-    f = ed25519.library().fd_ed25519_hip_private_hsdec2_n
-    f.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    f = ed25519.library().fd_ed25519_hip_private_hsdec3_n
+    f.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                  ctypes.c_int, ctypes.c_void_p]
     f.restype = None
     return f
 
 
+@pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
-def test_doubled_points_for_the_quarter_form(hsdec2, adversarial, mixed_order, n):
-    """dsm16q's A' = [2^66]A and R' = [2^66]R from the host (interleaved
-    doubling chains, one shared inversion): every decodable point of the
-    fixtures, in groups of n, against Python's affine doubling; the plain
-    limbs stay the single-point function's."""
+def test_doubled_points_for_the_split_forms(hsdec3, adversarial, mixed_order, n, waves):
+    """dsm16s's A_i = [2^(G i)]A and R_i = [2^(G i)]R from the host
+    (interleaved doubling chains, one shared inversion; G = 66 for four
+    waves, 33 for eight): every decodable point of the fixtures, in groups
+    of n, against Python's affine doubling; the plain limbs stay the
+    single-point function's."""
     from conftest import case
+    nx, step = (1, 66) if waves == 4 else (3, 33)
     encs = []
     for d in (adversarial, mixed_order):
-        for i in range(0, 400):
+        for i in range(0, 200):
             _, s, p = case(d, i)
             encs += [p, s[:32]]
-    for g in range(0, 96, n):
+    for g in range(0, 48, n):
         grp = encs[g:g + n]
         bufs = [ctypes.create_string_buffer(e, 32) for e in grp]
         arr = (ctypes.c_void_p * len(grp))(*[ctypes.addressof(b) for b in bufs])
         pt = np.zeros((len(grp), 20), np.int32)
-        p66 = np.zeros((len(grp), 20), np.int32)
+        px = np.zeros((len(grp), nx, 20), np.int32)
         fl = np.zeros(len(grp), np.uint8)
-        hsdec2(ctypes.addressof(arr), len(grp), 1, pt.ctypes.data, p66.ctypes.data, fl.ctypes.data)
-        for e, a, b, f in zip(grp, pt, p66, fl):
+        hsdec3(ctypes.addressof(arr), len(grp), 1, pt.ctypes.data, px.ctypes.data, nx, step, fl.ctypes.data)
+        for e, a, bx, f in zip(grp, pt, px, fl):
             want, x, yr = expected(e, True)
             assert f == want
             if want & 1:
                 continue
-            Q = (x, yr % P)
-            for _ in range(66):
-                Q = _edwards_add(Q, Q)
             assert _limbs_value(a[:10]) == x and _limbs_value(a[10:]) == yr % P
-            assert (_limbs_value(b[:10]), _limbs_value(b[10:])) == Q, e.hex()
-            assert all(abs(int(v)) < (1 << 26) for v in b)
+            Q = (x, yr % P)
+            for m in range(nx):
+                for _ in range(step):
+                    Q = _edwards_add(Q, Q)
+                assert (_limbs_value(bx[m][:10]), _limbs_value(bx[m][10:])) == Q, (e.hex(), m)
+                assert all(abs(int(v)) < (1 << 26) for v in bx[m])
 
 
-def test_quarter_scalar_split(adversarial):
-    """hsquad: the record's c and |d| split at bit 66 (three words each) and
-    s' in four 72-bit chunks, every part summing back exactly."""
+@pytest.mark.parametrize("waves", [4, 8])
+def test_split_scalars(adversarial, halfsize, waves):
+    """hssplit: the record's c and |d| split every 66 (four waves) or 33
+    (eight) bits, the last part the rest, and s' in 72- or 32-bit chunks,
+    every part summing back exactly (long |d| included: halfsize.npz)."""
     from conftest import case
     from firedancer_amd import ed25519
     lib = ed25519.library()
     rec_f = lib.fd_ed25519_hip_private_hsrec
     rec_f.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulong, ctypes.c_int, ctypes.c_void_p]
-    q_f = lib.fd_ed25519_hip_private_hsquad
-    q_f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_ulong]
+    q_f = lib.fd_ed25519_hip_private_hssplit
+    q_f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_ulong]
     q_f.restype = None
     cap = 7
-    for dbits in (151, 131):
-        for i in range(200):
-            m, s, p = case(adversarial, i)
+    H, G, KW, CB = (2, 66, 3, 72) if waves == 4 else (4, 33, 2, 32)
+    BW = (CB + 31) // 32
+    seen_long = False
+    for d in (adversarial, halfsize):
+        for i in range(min(200, len(d["msg_sz"]))):
+            m, s, p = case(d, i)
             rec = np.zeros(32, np.uint32)
-            if not rec_f(s, p, m, len(m), dbits, rec.ctypes.data):
+            if not rec_f(s, p, m, len(m), 151, rec.ctypes.data):
                 continue
             hq = np.zeros((24, cap), np.uint32)
             j = i % cap
-            q_f(rec.ctypes.data, hq.ctypes.data, cap, j)
+            q_f(rec.ctypes.data, waves, hq.ctypes.data, cap, j)
             w = lambda a, k: sum(int(rec[a + t]) << (32 * t) for t in range(k))
             c, dm = w(8, 5), w(13, 5)
+            seen_long |= dm >= 2**131
             sp = w(18, 5) % 2**144 + (w(23, 4) << 144)
-            part = [sum(int(hq[3 * q + t, j]) << (32 * t) for t in range(3)) for q in range(4)]
-            chunk = [sum(int(hq[12 + 3 * q + t, j]) << (32 * t) for t in range(3)) for q in range(4)]
-            assert part[0] < 2**66 and part[2] < 2**66
-            assert part[0] + (part[1] << 66) == c and part[2] + (part[3] << 66) == dm
-            assert all(x < 2**72 for x in chunk)
-            assert sum(x << (72 * q) for q, x in enumerate(chunk)) == sp
+            part = [sum(int(hq[KW * q + t, j]) << (32 * t) for t in range(KW)) for q in range(waves)]
+            chunk = [sum(int(hq[waves * KW + BW * q + t, j]) << (32 * t) for t in range(BW)) for q in range(waves)]
+            for side, v in ((0, c), (1, dm)):
+                ps = part[side * H:(side + 1) * H]
+                assert all(x < 2**G for x in ps[:-1])
+                assert sum(x << (G * k) for k, x in enumerate(ps)) == v
+            assert all(x < 2**CB for x in chunk)
+            assert sum(x << (CB * q) for q, x in enumerate(chunk)) == sp
+    assert seen_long

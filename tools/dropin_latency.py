@@ -94,7 +94,7 @@ def main():
                     help="fd_ed25519_hip_dropin_set_host_scalars (A/B; default: the library's)")
     ap.add_argument("--host-decode", type=int, default=None,
                     help="fd_ed25519_hip_dropin_set_host_decode (A/B; default: the library's)")
-    ap.add_argument("--quarter", type=int, default=None, help="fd_ed25519_hip_dropin_set_quarter_form (A/B)")
+    ap.add_argument("--split", type=int, default=None, help="fd_ed25519_hip_dropin_set_split_waves (A/B: 2, 4, 8)")
     ap.add_argument("--threads", action="store_true", help="also the 1/2/4/8-thread scaling")
     ap.add_argument("--large", default="16384,65376,65377,1048576,8388608",
                     help="message sizes (bytes) for the device-hashed large-message latencies")
@@ -113,10 +113,10 @@ def main():
         lib.fd_ed25519_hip_dropin_set_host_scalars.argtypes = [ctypes.c_ulong]
         lib.fd_ed25519_hip_dropin_set_host_scalars(args.host_scalars)
         res["host_scalars_max_sigs"] = args.host_scalars
-    if args.quarter is not None:
-        lib.fd_ed25519_hip_dropin_set_quarter_form.argtypes = [ctypes.c_int]
-        lib.fd_ed25519_hip_dropin_set_quarter_form(args.quarter)
-        res["quarter_form"] = args.quarter
+    if args.split is not None:
+        lib.fd_ed25519_hip_dropin_set_split_waves.argtypes = [ctypes.c_int]
+        lib.fd_ed25519_hip_dropin_set_split_waves(args.split)
+        res["split_waves"] = args.split
     if args.host_decode is not None:
         lib.fd_ed25519_hip_dropin_set_host_decode.argtypes = [ctypes.c_ulong]
         lib.fd_ed25519_hip_dropin_set_host_decode(args.host_decode)

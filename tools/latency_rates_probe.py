@@ -28,7 +28,7 @@ def main():
                     help="comma list of fd_ed25519_hip_pipe_set_host_scalars values to sweep (default: the library's)")
     ap.add_argument("--host-decode", default=None,
                     help="comma list of fd_ed25519_hip_pipe_set_host_decode values to sweep (default: the library's)")
-    ap.add_argument("--quarter", type=int, default=None, help="fd_ed25519_hip_pipe_set_quarter_form (A/B)")
+    ap.add_argument("--split", type=int, default=None, help="fd_ed25519_hip_pipe_set_split_waves (A/B: 2, 4, 8)")
     ap.add_argument("--pin", action="store_true", help="producer and tile on two physical cores of the GPU's node")
     args = ap.parse_args()
     os.environ.setdefault("GPU_MAX_HW_QUEUES", str(args.slots))
@@ -39,8 +39,8 @@ def main():
         cores = tile.physical_cores(tile.device_cpus(eng.info()))
         tile.latency_set_cpus(cores[0], cores[1])
     eng.close()
-    if args.quarter is not None:
-        tile.pipe_set_quarter_form(args.quarter)
+    if args.split is not None:
+        tile.pipe_set_split_waves(args.split)
     hs_values = [None] if args.host_scalars is None else [int(x) for x in args.host_scalars.replace(":", ",").split(",")]
     hd_values = [None] if args.host_decode is None else [int(x) for x in args.host_decode.replace(":", ",").split(",")]
     for hs, hd, rate in [(h, d, float(r)) for h in hs_values for d in hd_values
