@@ -1289,11 +1289,13 @@ static unsigned long dropin_hd_max = DROPIN_HD_MAX;
 
 /* host-decoded drop-in launches take the split form of this many waves
    (dsm16s: 4 or 8, the host doubling A and R and splitting the scalars;
-   2: dsm16) when the engine holds its tables: 82 -> 69 us p50 with four
-   for one caller (profiles/r6_dropin_quarter.json); test / A-B hook
-   fd_ed25519_hip_dropin_set_split_waves */
+   2: dsm16) when the engine holds its tables: p50 82.3 / 68.8 / 76.2 us
+   with 2 / 4 / 8 for one caller, back to back on one box -- eight waves
+   halve the chain again but pay more host doublings, eight table builds
+   and three rounds of additions (profiles/r6_dropin_split_waves.json);
+   test / A-B hook fd_ed25519_hip_dropin_set_split_waves */
 #ifndef DROPIN_SPLIT_WAVES
-#define DROPIN_SPLIT_WAVES 8
+#define DROPIN_SPLIT_WAVES 4
 #endif
 static int dropin_split = DROPIN_SPLIT_WAVES;
 

@@ -130,8 +130,9 @@ fd_ed25519_hip_dropin_set_host_decode( unsigned long max_sigs );
    doubles A and R every 66 (4) or 33 (8) bits and splits the half-size
    scalars there and s' into 72- or 32-bit chunks, so each wave's chain is
    ~17 or ~9 windows instead of 33 -- from compact base tables at offsets
-   2^(72 q) or 2^(32 q) (32 or 64 MiB per device, made with the drop-in
-   engines).  Test / A-B hook, process-wide (default 8). */
+   2^(72 q) or 2^(32 q) (32 or 64 MiB per device, the default's made with
+   the drop-in engines).  Test / A-B hook, process-wide (default 4: eight measured
+   slower). */
 void
 fd_ed25519_hip_dropin_set_split_waves( int waves );
 

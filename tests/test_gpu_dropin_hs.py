@@ -32,7 +32,7 @@ def ed():
     yield ed25519, lib
     lib.fd_ed25519_hip_dropin_set_host_scalars(4)
     lib.fd_ed25519_hip_dropin_set_host_decode(2)
-    lib.fd_ed25519_hip_dropin_set_split_waves(8)
+    lib.fd_ed25519_hip_dropin_set_split_waves(4)
 
 
 def _run(ed25519, d, idx):
@@ -80,7 +80,7 @@ def test_dropin_host_scalars_concurrent_callers(ed, adversarial, mixed_order, ca
             t.join()
         assert np.array_equal(out, d["codes_avx512"][:n])
     lib.fd_ed25519_hip_dropin_set_host_decode(2)
-    lib.fd_ed25519_hip_dropin_set_split_waves(8)
+    lib.fd_ed25519_hip_dropin_set_split_waves(4)
 
 
 def test_dropin_host_scalars_fallback_to_the_device_path(ed, halfsize, adversarial):

@@ -129,8 +129,8 @@ def test_dropin_calls_scale_with_threads(fd):
 
 def test_dropin_only_process_device_bytes():
     """A process that only calls the drop-ins: its device memory is the four
-    drop-in engines plus the compact base tables (2 x 8 MiB, and dsm16s<8>'s
-    8 x 8 MiB), well under
+    drop-in engines plus the compact base tables (2 x 8 MiB, and dsm16s<4>'s
+    4 x 8 MiB), well under
     600 MB -- not the 2 x 2 GiB wide tables."""
     code = ("import sys; sys.path.insert(0, %r); from firedancer_amd import ed25519 as e; "
             "print(e.verify(b'', bytes(64), bytes(32)), e.dropin_device_bytes(), e.shared_device_bytes(0))" % REPO)
@@ -138,5 +138,5 @@ def test_dropin_only_process_device_bytes():
     assert r.returncode == 0, r.stderr[-2000:]
     rc, dev, shared = (int(x) for x in r.stdout.split())
     assert rc != 0   # an all-zero signature is refused
-    assert shared == 10 * (1 << 16) * 128   # the compact pair + dsm16s<8>'s eight (8 MiB each)
+    assert shared == 6 * (1 << 16) * 128   # the compact pair + dsm16s<4>'s four (8 MiB each)
     assert dev < 600 * 1000 * 1000, dev
