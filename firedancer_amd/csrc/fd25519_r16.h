@@ -401,6 +401,22 @@ FD_DEV void table16_build(uint32_t (&tab)[9], uint32_t x, uint32_t y, bool negat
   }
 }
 
+/* ... for a point given in extended coordinates: p0 is the lane's limb
+   of its row's coordinate of P (X, Y, Z, T; tight), already negated when
+   the table is for -P (ge16_cneg4 on rows 0 and 3) */
+FD_DEV void table16_build_p3(uint32_t (&tab)[9], uint32_t p0, uint32_t d2, const r16ctx& k) {
+  const uint32_t one = r16_small(1u, k);
+  tab[0] = (one & (k.r0 | k.r1)) | (r16_small(2u, k) & k.r3);
+  const uint32_t c1 = ge16_to_qc(p0, d2, k);
+  tab[1] = c1;
+  uint32_t cur = p0;
+#pragma unroll
+  for (int e = 2; e <= 8; e++) {
+    cur = ge16_add2<true>(cur, c1, false, k);
+    tab[e] = ge16_to_qc(cur, d2, k);
+  }
+}
+
 /* entry e of the table, e wave-uniform (a branch on a scalar) */
 FD_DEV uint32_t table16_at(const uint32_t (&tab)[9], int e) {
   switch (e) {

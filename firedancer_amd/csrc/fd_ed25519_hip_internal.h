@@ -220,8 +220,9 @@ void fd_ed25519_hip_private_hsdec_n( unsigned char const * const * enc, unsigned
    launches: hssplit turns one signature's record into the split scalars
    and s' chunks (hq: 24 rows of stride cap, layout at the function), and
    hsdec3_n also returns each point doubled step, 2 step, .. nx step times
-   (S = 4: nx 1, step 66; S = 8: nx 3, step 33) for pts rows 2i + side
-   (row 0 A, 1 R, 2 A_1, 3 R_1, ..); hs_dsms launches dsm16s<waves> on them
+   (S = 4: nx 1, step 66; S = 8: nx 3, step 33) in extended coordinates
+   (40 limbs) for pts rows 2i + side of 40 limbs (row 0 A, 1 R -- affine,
+   the first 20 -- 2 A_1, 3 R_1, ..); hs_dsms launches dsm16s<waves> on them
    once want_dsms has made (or found) the engine's tables for that form. */
 void fd_ed25519_hip_private_hssplit( uint32_t const rec[ 32 ], int waves, uint32_t * hq, unsigned long cap,
                                      unsigned long j );

@@ -1315,7 +1315,9 @@ __global__ void __launch_bounds__(128) fd_ed25519_dsm16_kernel(fd_ed25519_verify
    (params.btabq), CB/16 of them (rounded up) at windows .., 4, 0.  The
    waves' points meet in LDS by halves (log2 S rounds of additions), wave
    0 tests the identity.  Inputs (host memory, params.go's launch-ahead):
-   pts [S][20][cap] (row 2i + side: A, R, A_1, R_1, ..), pflag [2][cap],
+   pts [S][40][cap] (row 2i + side: A, R, A_1, R_1, ..; A and R affine
+   (x, y) in the first 20, the doubled points extended (X, Y, Z, T) -- the
+   host never inverts), pflag [2][cap],
    sflag, hflag [cap], hs [24][cap]: rows KW q .. KW q + KW-1 the scalar of
    wave q (KW = 3 or 2 words), rows S KW + BWORDS q .. its chunk of s'. */
 template <int S>
@@ -1355,11 +1357,18 @@ __global__ void __launch_bounds__(64 * S) fd_ed25519_dsm16s_kernel(fd_ed25519_ve
   const uint32_t d2 = r16_from_fe(fe{FE_D2}, k);
   uint32_t tab[9];
   {
-    fe x, y;
-    const int32_t* src = p.pts + (uint64_t)(2 * part + side) * 20 * p.cap + j;
-    load_fe(x, src, p.cap);
-    load_fe(y, src + 10 * p.cap, p.cap);
-    table16_build(tab, r16_from_fe(x, k), r16_from_fe(y, k), side == 0 ? true : !(hf & FD_HF_DNEG), d2, k);
+    const bool negate = side == 0 ? true : !(hf & FD_HF_DNEG);
+    const int32_t* src = p.pts + (uint64_t)(2 * part + side) * 40 * p.cap + j;
+    if (part == 0) {   /* A or R as decoded: affine (x, y) */
+      fe x, y;
+      load_fe(x, src, p.cap);
+      load_fe(y, src + 10 * p.cap, p.cap);
+      table16_build(tab, r16_from_fe(x, k), r16_from_fe(y, k), negate, d2, k);
+    } else {           /* doubled on the host: extended (X, Y, Z, T), no inversion; row r loads coordinate r */
+      fe c;
+      load_fe(c, src + (uint64_t)k.row * 10 * p.cap, p.cap);
+      table16_build_p3(tab, ge16_cneg4(r16_from_fe(c, k), k.r03, negate, k), d2, k);
+    }
   }
   uint32_t sd[5], bd[5];
   {

@@ -1487,9 +1487,10 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   uint64_t cap_hs = e->max_chunk;
   uint64_t o_hsf = DROPIN_ALIGN16( need ), o_hhf = DROPIN_ALIGN16( o_hsf + cap_hs ), o_hs = DROPIN_ALIGN16( o_hhf + cap_hs );
   /* hs: 19 rows (dsm16) or 24 (dsm16s's split scalars); pts: A, R and,
-     for dsm16s, the doubled points (up to 8 rows of 20 limbs) */
+     for dsm16s, the doubled points (up to 8 rows of 40 limbs: dsm16s reads
+     rows of 40, dsm16 of 20) */
   int split = hdmode && dropin_split>2 && fd_ed25519_hip_private_want_dsms( e, dropin_split ) ? dropin_split : 0;
-  uint64_t o_pts = DROPIN_ALIGN16( o_hs + 24UL*4UL*cap_hs ), o_pfl = DROPIN_ALIGN16( o_pts + 8UL*20UL*4UL*cap_hs );
+  uint64_t o_pts = DROPIN_ALIGN16( o_hs + 24UL*4UL*cap_hs ), o_pfl = DROPIN_ALIGN16( o_pts + 8UL*40UL*4UL*cap_hs );
   uint64_t o_go  = DROPIN_ALIGN16( o_pfl + 2UL*cap_hs );
   if( hsmode ) need = hdmode ? o_go + 16UL : o_hs + 19UL*4UL*cap_hs;
   if( need>dq.blk_cap[k] ) {
@@ -1603,7 +1604,7 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     }
     if( all && hdmode ) {   /* A and R of each signature, side by side (and doubled, for dsm16s) */
       unsigned char const * enc[ 2UL*DROPIN_HD_CAP ];
-      int32_t       pt[ 2UL*DROPIN_HD_CAP ][ 20 ], ptx[ 2UL*DROPIN_HD_CAP*3UL ][ 20 ];
+      int32_t       pt[ 2UL*DROPIN_HD_CAP ][ 20 ], ptx[ 2UL*DROPIN_HD_CAP*3UL ][ 40 ];
       unsigned char fl[ 2UL*DROPIN_HD_CAP ];
       int nx = split ? split/2 - 1 : 0, step = split==4 ? 66 : 33;
       t = 0UL;
@@ -1615,13 +1616,13 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
       t = 0UL;
       for( dropin_req_t * r=list; r; r=r->next, t++ ) {
         uint64_t j = tf[ t ];
-        for( uint64_t side=0UL; side<2UL; side++ ) {   /* rows 2i + side: A, R, A_1, R_1, .. -- [S][20][cap] */
+        uint64_t rs = split ? 40UL : 20UL;   /* the row stride in limbs: dsm16s's, dsm16's */
+        for( uint64_t side=0UL; side<2UL; side++ ) {   /* rows 2i + side: A, R, A_1, R_1, .. */
           uint64_t pi = 2UL*t + side;
-          for( uint64_t l=0UL; l<20UL; l++ ) {
-            pts[ ( side*20UL + l )*cap_hs + j ] = pt[ pi ][ l ];
-            for( int m=1; m<=nx; m++ )
-              pts[ ( ( 2UL*(uint64_t)m + side )*20UL + l )*cap_hs + j ] = ptx[ pi*(uint64_t)nx + (uint64_t)(m-1) ][ l ];
-          }
+          for( uint64_t l=0UL; l<20UL; l++ ) pts[ ( side*rs + l )*cap_hs + j ] = pt[ pi ][ l ];
+          for( int m=1; m<=nx; m++ )
+            for( uint64_t l=0UL; l<40UL; l++ )
+              pts[ ( ( 2UL*(uint64_t)m + side )*40UL + l )*cap_hs + j ] = ptx[ pi*(uint64_t)nx + (uint64_t)(m-1) ][ l ];
           pfl[ side*cap_hs + j ] = fl[ pi ];
         }
       }

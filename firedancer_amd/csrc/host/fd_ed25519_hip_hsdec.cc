@@ -267,37 +267,14 @@ unsigned dec_post( dec_state const & d, f51 x, unsigned char const enc[ 32 ], in
   return ( fail ? 1u : 0u ) | ( small ? 2u : 0u );
 }
 
-/* z^(p-2) = (z^(2^252-3))^8 z^3 for N elements at once */
-template< int N >
-void inv_n( f51 ( &z )[ N ] ) {
-  f51 t[ N ];
-  for( int i=0; i<N; i++ ) t[ i ] = z[ i ];
-  pow22523_n< N >( t );
-  for( int i=0; i<N; i++ ) t[ i ] = mul( sq( sq( sq( t[ i ] ) ) ), mul( sq( z[ i ] ), z[ i ] ) );
-  for( int i=0; i<N; i++ ) z[ i ] = t[ i ];
-}
-
-/* the device's limbs of an affine point given by canonical-reducible
-   (x, y): x as fe_carry of its canonical bytes, y as fe_frombytes of its
-   canonical bytes (both tight, as the decode's) */
-void limbs_point( int32_t pt[ 20 ], f51 const & x, f51 const & y ) {
-  uint32_t xb[ 8 ], yb[ 8 ];
-  int32_t t[ 10 ];
-  tobytes( xb, x );
-  tobytes( yb, y );
-  limbs_frombytes( t, xb );
-  limbs_carry( pt, t );
-  limbs_frombytes( pt + 10, yb );
-}
-
 /* [2^(step m)](x, y) for m = 1 .. nx (nx <= 3), for N points at once
-   (extended coordinates without T, dbl-2008-hwcd for a = -1), then affine
-   with one shared inversion: ox / oy[ i nx + m-1 ] */
+   (extended coordinates without T, dbl-2008-hwcd for a = -1), returned in
+   extended coordinates (X Z, Y Z, Z^2, X Y) -- no inversion: ox[ i nx +
+   m-1 ][ 4 ] */
 template< int N >
-void dbl_n( f51 const ( &x )[ N ], f51 const ( &y )[ N ], int step, int nx, f51 * ox, f51 * oy ) {
+void dbl_n( f51 const ( &x )[ N ], f51 const ( &y )[ N ], int step, int nx, f51 ( *ox )[ 4 ] ) {
   const f51 zero = { { 0ULL, 0ULL, 0ULL, 0ULL, 0ULL } };
   f51 X[ N ], Y[ N ], Z[ N ];
-  f51 sx[ N*3 ], sy[ N*3 ], sz[ N*3 ];
   for( int i=0; i<N; i++ ) { X[ i ] = x[ i ]; Y[ i ] = y[ i ]; Z[ i ] = one(); }
   for( int m=0; m<nx; m++ ) {
     for( int r=0; r<step; r++ ) {
@@ -311,21 +288,21 @@ void dbl_n( f51 const ( &x )[ N ], f51 const ( &y )[ N ], int step, int nx, f51 
         X[ i ] = mul( E, F ); Y[ i ] = mul( G, H ); Z[ i ] = mul( F, G );
       }
     }
-    for( int i=0; i<N; i++ ) { sx[ i*nx + m ] = X[ i ]; sy[ i*nx + m ] = Y[ i ]; sz[ i*nx + m ] = Z[ i ]; }
+    for( int i=0; i<N; i++ ) {
+      f51 * o = ox[ i*nx + m ];
+      o[ 0 ] = mul( X[ i ], Z[ i ] ); o[ 1 ] = mul( Y[ i ], Z[ i ] ); o[ 2 ] = sq( Z[ i ] ); o[ 3 ] = mul( X[ i ], Y[ i ] );
+    }
   }
-  /* 1/Z from one inversion: prefix products */
-  const int T = N*nx;
-  f51 pre[ N*3 ], inv[ 1 ];
-  pre[ 0 ] = sz[ 0 ];
-  for( int t=1; t<T; t++ ) pre[ t ] = mul( pre[ t-1 ], sz[ t ] );
-  inv[ 0 ] = pre[ T-1 ];
-  inv_n< 1 >( inv );
-  f51 acc = inv[ 0 ];
-  for( int t=T-1; t>=0; t-- ) {
-    f51 zi = t ? mul( acc, pre[ t-1 ] ) : acc;
-    if( t ) acc = mul( acc, sz[ t ] );
-    ox[ t ] = mul( sx[ t ], zi ); oy[ t ] = mul( sy[ t ], zi );
-  }
+}
+
+/* the device's tight limbs of one coordinate (fe_carry of its canonical
+   bytes) */
+void limbs_coord( int32_t out[ 10 ], f51 const & v ) {
+  uint32_t b[ 8 ];
+  int32_t t[ 10 ];
+  tobytes( b, v );
+  limbs_frombytes( t, b );
+  limbs_carry( out, t );
 }
 
 template< int N >
@@ -341,9 +318,9 @@ void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsig
     ys[ i ] = d[ i ].y;
   }
   if( !ptx || nx<1 ) return;
-  f51 ox[ N*3 ], oy[ N*3 ];
-  dbl_n< N >( xs, ys, step, nx, ox, oy );
-  for( int t=0; t<N*nx; t++ ) limbs_point( ptx + 20*t, ox[ t ], oy[ t ] );
+  f51 ox[ N*3 ][ 4 ];
+  dbl_n< N >( xs, ys, step, nx, ox );
+  for( int t=0; t<N*nx; t++ ) for( int c=0; c<4; c++ ) limbs_coord( ptx + 40*t + 10*c, ox[ t ][ c ] );
 }
 
 } /* namespace */
@@ -353,9 +330,10 @@ void dec_n( unsigned char const * const * enc, int avx_rule, int32_t * pt, unsig
    FD_PF_FAIL, 2 FD_PF_SMALL (fd_ed25519_hip_internal.h).  avx_rule: the
    AVX-512 build's codes (an engine without
    FD_ED25519_HIP_FLAG_CODES_PORTABLE).  ptx (when not NULL): each point
-   also doubled step, 2 step, .. nx step times (nx <= 3), affine, in the
-   same limbs -- ptx[(i nx + m-1) 20 ..] = [2^(step m)]P_i, the split
-   forms' A_i and R_i (a failed decode's are any values: its code is the
+   also doubled step, 2 step, .. nx step times (nx <= 3), in extended
+   coordinates (X, Y, Z, T: 40 limbs, each coordinate as the device's tight
+   limbs) -- ptx[(i nx + m-1) 40 ..] = [2^(step m)]P_i, the split forms'
+   A_i and R_i (a failed decode's are any values: its code is the
    decode's). */
 extern "C" void
 fd_ed25519_hip_private_hsdec3_n( unsigned char const * const * enc, unsigned long n, int avx_rule, int32_t * pt,
@@ -363,7 +341,7 @@ fd_ed25519_hip_private_hsdec3_n( unsigned char const * const * enc, unsigned lon
   if( nx>3 ) nx = 3;
   unsigned long i = 0UL;
 #define HSDEC_GROUP( N ) dec_n< N >( enc + i, avx_rule, pt + 20UL*i, flags + i, \
-                                     ptx ? ptx + 20UL*(unsigned long)nx*i : NULL, nx, step )
+                                     ptx ? ptx + 40UL*(unsigned long)nx*i : NULL, nx, step )
   for( ; i+4UL<=n; i+=4UL ) HSDEC_GROUP( 4 );
   if( n-i==3UL ) HSDEC_GROUP( 3 );
   if( n-i==2UL ) HSDEC_GROUP( 2 );

@@ -248,12 +248,13 @@ fd_ed25519_hip_pipe_set_host_decode( unsigned long max_sigs ) {
 }
 
 /* the page-locked host-scalar block: sflag [cap], hflag [cap], hs [24][cap]
-   words (dsm16: 19 rows; dsm16s: 24), pts [8][20][cap] words (A, R; dsm16s
-   also the doubled points), pflag [2][cap], the go word (params.go) */
+   words (dsm16: 19 rows; dsm16s: 24), pts [8][40][cap] words (dsm16: rows
+   of 20 limbs, A and R; dsm16s: rows of 40, the doubled points' extended
+   coordinates too), pflag [2][cap], the go word (params.go) */
 #define HS_O_HS( cap )  ( 2UL*(cap) )
 #define HS_O_PTS( cap ) ( ( 2UL + 24UL*4UL )*(cap) )
-#define HS_O_PFL( cap ) ( ( 2UL + 24UL*4UL + 8UL*20UL*4UL )*(cap) )
-#define HS_O_GO( cap )  ( ( ( 2UL + 24UL*4UL + 8UL*20UL*4UL + 2UL )*(cap) + 15UL ) & ~15UL )
+#define HS_O_PFL( cap ) ( ( 2UL + 24UL*4UL + 8UL*40UL*4UL )*(cap) )
+#define HS_O_GO( cap )  ( ( ( 2UL + 24UL*4UL + 8UL*40UL*4UL + 2UL )*(cap) + 15UL ) & ~15UL )
 #define HS_BYTES( cap ) ( HS_O_GO( cap ) + 16UL )
 
 struct fd_ed25519_hip_pipe {
@@ -577,7 +578,7 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
   }
   if( hd ) {   /* A and R of each signature, side by side */
     unsigned char const * enc[ 2UL*PIPE_HD_CAP ];
-    int32_t       pt[ 2UL*PIPE_HD_CAP ][ 20 ], ptx[ 2UL*PIPE_HD_CAP*3UL ][ 20 ];
+    int32_t       pt[ 2UL*PIPE_HD_CAP ][ 20 ], ptx[ 2UL*PIPE_HD_CAP*3UL ][ 40 ];
     unsigned char fl[ 2UL*PIPE_HD_CAP ];
     int nx = split ? split/2 - 1 : 0, step = split==4 ? 66 : 33;
     for( unsigned long i=0UL; i<n; i++ ) { enc[ 2UL*i ] = slot->pubs + 32UL*i; enc[ 2UL*i+1UL ] = slot->sigs + 64UL*i; }
@@ -585,14 +586,14 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
                                      split ? &ptx[0][0] : NULL, nx, step, fl );
     int32_t * pts = (int32_t *)( s->h_hs + HS_O_PTS( cap ) );
     unsigned char * pfl = s->h_hs + HS_O_PFL( cap );
+    unsigned long rs = split ? 40UL : 20UL;   /* the row stride in limbs: dsm16s's, dsm16's */
     for( unsigned long i=0UL; i<n; i++ )
       for( unsigned long side=0UL; side<2UL; side++ ) {   /* rows 2i + side: A, R, A_1, R_1, .. */
         unsigned long pi = 2UL*i + side;
-        for( unsigned long l=0UL; l<20UL; l++ ) {
-          pts[ ( side*20UL + l )*cap + i ] = pt[ pi ][ l ];
-          for( int m=1; m<=nx; m++ )
-            pts[ ( ( 2UL*(unsigned long)m + side )*20UL + l )*cap + i ] = ptx[ pi*(unsigned long)nx + (unsigned long)(m-1) ][ l ];
-        }
+        for( unsigned long l=0UL; l<20UL; l++ ) pts[ ( side*rs + l )*cap + i ] = pt[ pi ][ l ];
+        for( int m=1; m<=nx; m++ )
+          for( unsigned long l=0UL; l<40UL; l++ )
+            pts[ ( ( 2UL*(unsigned long)m + side )*40UL + l )*cap + i ] = ptx[ pi*(unsigned long)nx + (unsigned long)(m-1) ][ l ];
         pfl[ side*cap + i ] = fl[ pi ];
       }
   }

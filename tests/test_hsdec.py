@@ -134,10 +134,10 @@ def hsdec3():
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
 def test_doubled_points_for_the_split_forms(hsdec3, adversarial, mixed_order, n, waves):
     """dsm16s's A_i = [2^(G i)]A and R_i = [2^(G i)]R from the host
-    (interleaved doubling chains, one shared inversion; G = 66 for four
-    waves, 33 for eight): every decodable point of the fixtures, in groups
-    of n, against Python's affine doubling; the plain limbs stay the
-    single-point function's."""
+    (interleaved doubling chains, extended coordinates, no inversion; G =
+    66 for four waves, 33 for eight): every decodable point of the
+    fixtures, in groups of n, against Python's affine doubling; the plain
+    limbs stay the single-point function's."""
     from conftest import case
     nx, step = (1, 66) if waves == 4 else (3, 33)
     encs = []
@@ -150,7 +150,7 @@ def test_doubled_points_for_the_split_forms(hsdec3, adversarial, mixed_order, n,
         bufs = [ctypes.create_string_buffer(e, 32) for e in grp]
         arr = (ctypes.c_void_p * len(grp))(*[ctypes.addressof(b) for b in bufs])
         pt = np.zeros((len(grp), 20), np.int32)
-        px = np.zeros((len(grp), nx, 20), np.int32)
+        px = np.zeros((len(grp), nx, 40), np.int32)
         fl = np.zeros(len(grp), np.uint8)
         hsdec3(ctypes.addressof(arr), len(grp), 1, pt.ctypes.data, px.ctypes.data, nx, step, fl.ctypes.data)
         for e, a, bx, f in zip(grp, pt, px, fl):
@@ -163,8 +163,11 @@ def test_doubled_points_for_the_split_forms(hsdec3, adversarial, mixed_order, n,
             for m in range(nx):
                 for _ in range(step):
                     Q = _edwards_add(Q, Q)
-                assert (_limbs_value(bx[m][:10]), _limbs_value(bx[m][10:])) == Q, (e.hex(), m)
-                assert all(abs(int(v)) < (1 << 26) for v in bx[m])
+                X, Y, Z, T = (_limbs_value(bx[m][10 * c:10 * c + 10]) for c in range(4))
+                zi = pow(Z, P - 2, P)
+                assert (X * zi % P, Y * zi % P) == Q, (e.hex(), m)   # extended: x = X/Z, y = Y/Z
+                assert T * Z % P == X * Y % P
+                assert all(abs(int(v)) <= (1 << 25) + 64 for v in bx[m])   # tight (fe_carry's)
 
 
 @pytest.mark.parametrize("waves", [4, 8])
