@@ -136,7 +136,10 @@ def test_producer_stops_when_service_dies(tmp_path, how):
     tag = uuid.uuid4().hex[:12]
     txl = tile.ShLink(f"/fdt_tx_{tag}", 64, create=True)
     vdl = tile.ShLink(f"/fdt_vd_{tag}", 64, create=True)
-    proc = subprocess.Popen([tile.PRODUCER_BIN, txl.name, vdl.name, path, "--stale-ms", "300", *NO_SANDBOX],
+    # the staleness bound well above a loaded host's pauses (the fake
+    # service is Python, and under the sanitizer suites a pause of a few
+    # hundred ms would let "stale" win over the explicit failure mark)
+    proc = subprocess.Popen([tile.PRODUCER_BIN, txl.name, vdl.name, path, "--stale-ms", "1500", *NO_SANDBOX],
                             stdout=subprocess.PIPE, stderr=subprocess.PIPE)
     try:
         if how == "killed":
@@ -155,7 +158,7 @@ def test_producer_stops_when_service_dies(tmp_path, how):
         pytest.skip(f"seccomp strict mode unavailable: {err.decode()}")
     assert proc.returncode == 4, (proc.returncode, err.decode())
     assert (b"stale" if how == "killed" else b"marked a link failed") in err
-    assert dt < 5.0
+    assert dt < 8.0
 
 
 def test_link_credits_and_overrun_free():
