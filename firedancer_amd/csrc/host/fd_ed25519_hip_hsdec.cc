@@ -108,6 +108,17 @@ f51 sub( f51 const & f, f51 const & g ) {
 
 f51 one() { f51 h = { { 1ULL, 0ULL, 0ULL, 0ULL, 0ULL } }; return h; }
 
+/* f - g + 8p without the carry, for a value that only feeds mul / sq: g's
+   limbs < 2^54 - 152, the result's < f's + 2^54 (mul and sq take limbs up
+   to 2^55.5: b 19 < 2^64, five products < 2^118) */
+f51 sub_lazy( f51 const & f, f51 const & g ) {
+  const uint64_t p8_0 = 0x3fffffffffff68ULL, p8_i = 0x3ffffffffffff8ULL;
+  f51 h;
+  h.v[ 0 ] = f.v[ 0 ] + p8_0 - g.v[ 0 ];
+  for( int i=1; i<5; i++ ) h.v[ i ] = f.v[ i ] + p8_i - g.v[ i ];
+  return h;
+}
+
 /* canonical little-endian words (value mod p) */
 void tobytes( uint32_t out[ 8 ], f51 const & f ) {
   u128 t[ 5 ] = { f.v[ 0 ], f.v[ 1 ], f.v[ 2 ], f.v[ 3 ], f.v[ 4 ] };
@@ -279,12 +290,14 @@ void dbl_n( f51 const ( &x )[ N ], f51 const ( &y )[ N ], int step, int nx, f51 
   for( int m=0; m<nx; m++ ) {
     for( int r=0; r<step; r++ ) {
       for( int i=0; i<N; i++ ) {
+        /* A, B, Z2 carried (< 2^52); every difference below only feeds a
+           product, so none is carried: E, F < 2^55.2, G, H < 2^54.3 */
         f51 A = sq( X[ i ] ), B = sq( Y[ i ] ), Z2 = sq( Z[ i ] );
-        f51 C = add( Z2, Z2 );
-        f51 E = sub( sub( sq( add( X[ i ], Y[ i ] ) ), A ), B );
-        f51 G = sub( B, A );                    /* D + B, D = -A */
-        f51 F = sub( G, C );
-        f51 H = sub( zero, add( A, B ) );       /* D - B         */
+        f51 C = add( Z2, Z2 );                                      /* < 2^53   */
+        f51 E = sub_lazy( sub_lazy( sq( add( X[ i ], Y[ i ] ) ), A ), B );
+        f51 G = sub_lazy( B, A );               /* D + B, D = -A */
+        f51 F = sub_lazy( G, C );
+        f51 H = sub_lazy( zero, add( A, B ) );  /* D - B         */
         X[ i ] = mul( E, F ); Y[ i ] = mul( G, H ); Z[ i ] = mul( F, G );
       }
     }

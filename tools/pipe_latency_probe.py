@@ -4,7 +4,7 @@ from the slot's own t_submit / t_done: one batch in flight at a time, then
 slot_cnt in flight back to back -- what a verify tile's (or the GPU
 service's) batches of --batch single-signer signatures see.
 
-    python tools/pipe_latency_probe.py [--batch 4096] [--slots 3] [--reps 50]
+    python tools/pipe_latency_probe.py [--batch 4096] [--slots 3] [--reps 50] [--split 2|4|8]
 """
 import argparse
 import json
@@ -24,7 +24,10 @@ def main():
     ap.add_argument("--slots", type=int, default=3)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--msg-sz", type=int, default=200)
+    ap.add_argument("--split", type=int, default=None, help="fd_ed25519_hip_pipe_set_split_waves (A/B: 2, 4, 8)")
     args = ap.parse_args()
+    if args.split is not None:
+        tile.pipe_set_split_waves(args.split)
     n, m = args.batch, args.msg_sz
     eng = ed25519.Engine(0, max_chunk=max(n, 4096))
     wl = ed25519.DeviceWorkload(eng, n, m, m, 0, seed=77)
@@ -73,7 +76,7 @@ def main():
                                      "round_trip_ms_p90": float(np.percentile(rt, 90)),
                                      "verifies_per_s": args.reps * n / dt}
     pipe.close()
-    print(json.dumps({"batch": n, "slots": args.slots, "msg_sz": m, **res}))
+    print(json.dumps({"batch": n, "slots": args.slots, "msg_sz": m, "split_waves": args.split, **res}))
 
 
 if __name__ == "__main__":
