@@ -1462,14 +1462,16 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     if( r->hashed ) nsig_h += r->cnt; else bytes += r->msg_sz;
   }
   uint64_t nsig_m = nsig - nsig_h;
-  /* host scalars (a launch of a few single-signature requests, any message
-     size below the host-hash limit): the calling thread hashes and finds
+  /* host scalars (a launch of a few signatures -- fd_ed25519_verify calls,
+     or batch_single_msg transactions of a few signatures, whose codes are
+     then combined on the host -- any message size below the host-hash
+     limit): the calling thread hashes and finds
      the scalars, the device reads sflag / hflag [cap] and hs [19][cap] in
      the block (the work arrays' stride, the first nsig of each row
      written) and never the messages, which are not staged; a signature
      without a half-size pair (~1e-6) takes the device path from its
      digest (room for nsig digests) */
-  int hsmode = nsig<=dropin_hs_max && !multi && !nsig_h;
+  int hsmode = nsig<=dropin_hs_max && !nsig_h;
   int hdmode = hsmode && nsig<=dropin_hd_max;
   uint64_t ndig   = hsmode ? nsig : nsig_h;
   uint64_t o_off  = 0UL;
@@ -1593,32 +1595,36 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     int dbits = dropin_hs_dbits ? dropin_hs_dbits : engine_half_dbits( e );
     t = 0UL;
     for( dropin_req_t * r=list; r && all; r=r->next, t++ ) {
-      uint32_t rec[ 32 ];
-      all = fd_ed25519_hip_private_hsrec( r->sigs, r->pubs, r->msg, r->msg_sz, dbits, rec );
-      if( !all ) break;
-      uint64_t j = tf[ t ];
-      if( split ) fd_ed25519_hip_private_hssplit( rec, split, hs, cap_hs, j );
-      else for( int w=0; w<19; w++ ) hs[ (uint64_t)w*cap_hs + j ] = rec[ 8 + w ];
-      hsf[ j ] = (uint8_t)rec[ 27 ];
-      hhf[ j ] = (uint8_t)rec[ 28 ];
+      for( uint32_t i=0U; i<r->cnt && all; i++ ) {   /* a batch_single_msg request: its signatures over one message */
+        uint32_t rec[ 32 ];
+        all = fd_ed25519_hip_private_hsrec( r->sigs + 64UL*i, r->pubs + 32UL*i, r->msg, r->msg_sz, dbits, rec );
+        if( !all ) break;
+        uint64_t j = tf[ t ] + i;
+        if( split ) fd_ed25519_hip_private_hssplit( rec, split, hs, cap_hs, j );
+        else for( int w=0; w<19; w++ ) hs[ (uint64_t)w*cap_hs + j ] = rec[ 8 + w ];
+        hsf[ j ] = (uint8_t)rec[ 27 ];
+        hhf[ j ] = (uint8_t)rec[ 28 ];
+      }
     }
     if( all && hdmode ) {   /* A and R of each signature, side by side (and doubled, for dsm16s) */
       unsigned char const * enc[ 2UL*DROPIN_HD_CAP ];
       int32_t       pt[ 2UL*DROPIN_HD_CAP ][ 20 ], ptx[ 2UL*DROPIN_HD_CAP*3UL ][ 40 ];
       unsigned char fl[ 2UL*DROPIN_HD_CAP ];
       int nx = split ? split/2 - 1 : 0, step = split==4 ? 66 : 33;
+      /* signature j (the requests' signatures in order) at enc[2j], enc[2j+1] */
       t = 0UL;
-      for( dropin_req_t * r=list; r; r=r->next, t++ ) { enc[ 2UL*t ] = r->pubs; enc[ 2UL*t+1UL ] = r->sigs; }
+      for( dropin_req_t * r=list; r; r=r->next, t++ )
+        for( uint32_t i=0U; i<r->cnt; i++ ) {
+          enc[ 2UL*( tf[ t ] + i ) ] = r->pubs + 32UL*i; enc[ 2UL*( tf[ t ] + i ) + 1UL ] = r->sigs + 64UL*i;
+        }
       fd_ed25519_hip_private_hsdec3_n( enc, 2UL*nsig, !(e->flags & FD_ED25519_HIP_FLAG_CODES_PORTABLE), &pt[0][0],
                                        split ? &ptx[0][0] : NULL, nx, step, fl );
       int32_t * pts = (int32_t *)(h + o_pts);
       uint8_t * pfl = (uint8_t *)(h + o_pfl);
-      t = 0UL;
-      for( dropin_req_t * r=list; r; r=r->next, t++ ) {
-        uint64_t j = tf[ t ];
-        uint64_t rs = split ? 40UL : 20UL;   /* the row stride in limbs: dsm16s's, dsm16's */
+      uint64_t rs = split ? 40UL : 20UL;   /* the row stride in limbs: dsm16s's, dsm16's */
+      for( uint64_t j=0UL; j<nsig; j++ ) {
         for( uint64_t side=0UL; side<2UL; side++ ) {   /* rows 2i + side: A, R, A_1, R_1, .. */
-          uint64_t pi = 2UL*t + side;
+          uint64_t pi = 2UL*j + side;
           for( uint64_t l=0UL; l<20UL; l++ ) pts[ ( side*rs + l )*cap_hs + j ] = pt[ pi ][ l ];
           for( int m=1; m<=nx; m++ )
             for( uint64_t l=0UL; l<40UL; l++ )
@@ -1635,7 +1641,9 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     } else if( !all ) {   /* the device path from the digests (the messages were not staged) */
       t = 0UL;
       for( dropin_req_t * r=list; r; r=r->next, t++ )
-        fd_ed25519_hip_private_challenge( r->sigs, r->pubs, r->msg, r->msg_sz, h + o_dig + 64UL*tf[ t ] );
+        for( uint32_t i=0U; i<r->cnt; i++ )
+          fd_ed25519_hip_private_challenge( r->sigs + 64UL*i, r->pubs + 32UL*i, r->msg, r->msg_sz,
+                                            h + o_dig + 64UL*( tf[ t ] + i ) );
       err = fd_ed25519_hip_verify_digests_dev( e, nsig, src + o_dig, src + o_sig, src + o_pub,
                                                (signed char *)(src + o_out), st );
     }
@@ -1650,7 +1658,7 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
     err = fd_ed25519_hip_verify_digests_dev( e, nsig_h, src + o_dig, src + o_sig + 64UL*nsig_m,
                                              src + o_pub + 32UL*nsig_m, (signed char *)(src + o_out + nsig_m), st );
   if( err ) { hipStreamSynchronize( st ); return err; }
-  if( multi ) {
+  if( multi && !direct ) {   /* (a direct multi-signature launch is a host-scalar one: combined below) */
     err = fd_ed25519_hip_txn_combine_dev( e, n, (signed char const *)(d + o_out), (uint32_t const *)(d + o_tf),
                                           (uint32_t const *)(d + o_tc), (signed char *)(d + o_tout), st );
     if( err ) { hipStreamSynchronize( st ); return err; }
@@ -1691,6 +1699,23 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   }
   signed char const * codes = (signed char const *)(h + o_out);
   signed char const * tcode = (signed char const *)(h + o_tout);
+  if( multi && direct ) {
+    /* batch_single_msg's rule per request (fd_ed25519_user.c:231-309, the
+       device's fd_ed25519_txn_combine_kernel): the first error other than
+       ERR_MSG in signature order, else ERR_MSG if any signature had it,
+       else SUCCESS (1..16 signatures: the guard ran before submit) */
+    t = 0UL;
+    for( dropin_req_t * r=list; r; r=r->next, t++ ) {
+      int code = FD_ED25519_SUCCESS, msg_fail = 0;
+      for( uint32_t i=0U; i<r->cnt; i++ ) {
+        int c = codes[ tf[ t ] + i ];
+        if( c==FD_ED25519_ERR_MSG ) msg_fail = 1;
+        else if( c!=FD_ED25519_SUCCESS ) { code = c; break; }
+      }
+      if( code==FD_ED25519_SUCCESS && msg_fail ) code = FD_ED25519_ERR_MSG;
+      ((signed char *)(h + o_tout))[ t ] = (signed char)code;
+    }
+  }
   t = 0UL;
   for( dropin_req_t * r=list; r; r=r->next, t++ )
     r->result = (r->single || !multi) ? (int)codes[ tf[t] ] : (int)tcode[t];

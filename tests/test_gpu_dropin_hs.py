@@ -103,3 +103,36 @@ def test_dropin_host_scalars_fallback_to_the_device_path(ed, halfsize, adversari
             assert len(bad) == 0, [(str(d["tags"][i]), int(got[i]), int(d["codes_avx512"][i])) for i in bad[:10]]
     finally:
         lib.fd_ed25519_hip_dropin_set_host_scalars_dbits(0)
+
+
+@pytest.mark.parametrize("mode", [(4, 2, 4), (4, 4, 4), (4, 2, 2), (4, 0, 4), (0, 0, 4)],
+                         ids=["hs-decode2-four-waves", "hs-decode4-four-waves", "hs-decode2-two-waves", "host-scalars",
+                              "device"])
+def test_dropin_batch_single_msg_every_host_path(ed, batch, mixed_order, mode):
+    """fd_ed25519_verify_batch_single_msg: a transaction of at most 4
+    signatures over one message takes the host-scalar launch too (its
+    signatures' records from the calling thread, the decompressions as well
+    for at most hd of them), its codes combined on the host by the batch
+    rule -- every transaction of the batch fixture and the mixed-order set,
+    code for code against the reference's, in every mode."""
+    ed25519, lib = ed
+    lib.fd_ed25519_hip_dropin_set_host_scalars(mode[0])
+    lib.fd_ed25519_hip_dropin_set_host_decode(mode[1])
+    lib.fd_ed25519_hip_dropin_set_split_waves(mode[2])
+    try:
+        n_small = 0
+        for d, pre in ((batch, ""), (mixed_order, "b_")):
+            for t in range(len(d[pre + "txn_cnt"])):
+                c = int(d[pre + "txn_cnt"][t])
+                if c < 1 or c > 16:
+                    continue
+                o, z, f = int(d[pre + "txn_msg_off"][t]), int(d[pre + "txn_msg_sz"][t]), int(d[pre + "txn_first"][t])
+                got = ed25519.verify_batch_single_msg(bytes(d[pre + "msgs"][o:o + z]), d[pre + "sigs"][f:f + c].tobytes(),
+                                                      d[pre + "pubs"][f:f + c].tobytes(), c)
+                assert got == int(d[pre + "codes_avx512"][t]), (pre, t, c, got)
+                n_small += c <= 4
+        assert n_small > 100
+    finally:
+        lib.fd_ed25519_hip_dropin_set_host_scalars(4)
+        lib.fd_ed25519_hip_dropin_set_host_decode(2)
+        lib.fd_ed25519_hip_dropin_set_split_waves(4)

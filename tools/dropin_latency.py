@@ -134,6 +134,25 @@ def main():
     res["fd_ed25519_verify_gpu_dropin"] = pct(t_one)
     if args.threads:
         res["thread_scaling"] = thread_scaling(ed25519, msgs, sigs, pubs, args.calls)
+    # fd_ed25519_verify_batch_single_msg on the golden batch's valid
+    # transactions of 1, 2 and 4 signatures (one message, several signers)
+    bd = np.load(os.path.join(REPO, "tests", "golden", "batch.npz"))
+    res["batch_single_msg_gpu_dropin"] = {}
+    for want in (1, 2, 4):
+        txns = [t for t in range(len(bd["txn_cnt"])) if int(bd["txn_cnt"][t]) == want and int(bd["codes_avx512"][t]) == 0]
+        if not txns:
+            continue
+        calls = []
+        for t in txns[:16]:
+            o, z, f = int(bd["txn_msg_off"][t]), int(bd["txn_msg_sz"][t]), int(bd["txn_first"][t])
+            calls.append((bytes(bd["msgs"][o:o + z]), bd["sigs"][f:f + want].tobytes(), bd["pubs"][f:f + want].tobytes()))
+        lat = []
+        for i in range(max(200, args.calls // 4)):
+            m, s, p = calls[i % len(calls)]
+            t0 = time.perf_counter()
+            assert ed25519.verify_batch_single_msg(m, s, p, want) == 0
+            lat.append(time.perf_counter() - t0)
+        res["batch_single_msg_gpu_dropin"][f"{want}_signatures"] = pct(lat[10:])
     # a 4-signer transaction over one message (sign the first message with 4 keys on the device)
     ref = ctypes.CDLL(os.path.join(REPO, "oracle", "_ref", "libfdref_portable.so"))
     ref.fdref_verify.argtypes = [ctypes.c_char_p, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_char_p]
