@@ -146,6 +146,9 @@ typedef struct {
   int32_t const *  btab8_hi;
 } fd_ed25519_verify_params_t;
 
+/* host-decoded launches (params.pts in host memory): every host array's
+   stride (params.cap), the launch's signatures being at most this many */
+#define FD_ED25519_HS_STRIDE   8UL
 #define FD_ED25519_GO_RUN      1U
 #define FD_ED25519_GO_CANCEL   2U
 #define FD_ED25519_GO_SPIN_MAX 200000U

@@ -806,7 +806,10 @@ fd_ed25519_hip_private_hs_dsm( fd_ed25519_hip_engine_t * e, unsigned long n, uns
   if( err ) return err;
   if( !sflag || !hflag || !hs || !pts!=!pflag ) return FD_ED25519_HIP_ERR_INVAL;
   p.sflag = (uint8_t *)sflag; p.hflag = (uint8_t *)hflag; p.hs = (uint32_t *)hs;
-  if( pts ) { p.pts = (int32_t *)pts; p.pflag = (uint8_t *)pflag; }
+  if( pts ) {   /* every array the caller's: its small stride */
+    if( n>FD_ED25519_HS_STRIDE ) return FD_ED25519_HIP_ERR_INVAL;
+    p.pts = (int32_t *)pts; p.pflag = (uint8_t *)pflag; p.cap = FD_ED25519_HS_STRIDE;
+  }
   p.go = (uint32_t const *)go;
   err = fd_ed25519_hip_launch_phase( &p, FD_ED25519_PHASE_DSM, e->dsm_grid, stream ? (hipStream_t)stream : e->stream );
   if( err ) return hip_fail( (hipError_t)err, "verify launch" );
@@ -823,8 +826,9 @@ fd_ed25519_hip_private_hs_dsms( fd_ed25519_hip_engine_t * e, int waves, unsigned
   if( err ) return err;
   if( (waves!=4 && waves!=8) || !sflag || !hflag || !hq || !pts || !pflag || !e->btabs[ split_set( waves ) ][0] )
     return FD_ED25519_HIP_ERR_INVAL;
+  if( n>FD_ED25519_HS_STRIDE ) return FD_ED25519_HIP_ERR_INVAL;
   p.sflag = (uint8_t *)sflag; p.hflag = (uint8_t *)hflag; p.hs = (uint32_t *)hq;
-  p.pts = (int32_t *)pts; p.pflag = (uint8_t *)pflag;
+  p.pts = (int32_t *)pts; p.pflag = (uint8_t *)pflag; p.cap = FD_ED25519_HS_STRIDE;   /* every array the caller's */
   p.go = (uint32_t const *)go;
   for( int q=0; q<8; q++ ) p.btabq[q] = e->btabs[ split_set( waves ) ][q];
   err = fd_ed25519_hip_launch_dsm16s( &p, waves, stream ? (hipStream_t)stream : e->stream );
@@ -1486,7 +1490,9 @@ dropin_run( int k, dropin_req_t * list, unsigned long n ) {
   uint64_t o_out  = DROPIN_ALIGN16( in_sz + 16UL );
   uint64_t o_tout = o_out + nsig;
   uint64_t need   = o_tout + n + 16UL;
-  uint64_t cap_hs = e->max_chunk;
+  /* the host arrays' stride: the work arrays' when the device decodes
+     (its pts / pflag), a small one when every array is the caller's */
+  uint64_t cap_hs = hdmode ? FD_ED25519_HS_STRIDE : e->max_chunk;
   uint64_t o_hsf = DROPIN_ALIGN16( need ), o_hhf = DROPIN_ALIGN16( o_hsf + cap_hs ), o_hs = DROPIN_ALIGN16( o_hhf + cap_hs );
   /* hs: 19 rows (dsm16) or 24 (dsm16s's split scalars); pts: A, R and,
      for dsm16s, the doubled points (up to 8 rows of 40 limbs: dsm16s reads

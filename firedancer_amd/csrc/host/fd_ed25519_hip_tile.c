@@ -319,7 +319,11 @@ pipe_slot_init( pipe_slot_t * s, int device, unsigned long sig_cap, unsigned lon
   TCHK( hipMalloc(     (void **)&s->d_in,   in_sz                        ), "hipMalloc" );
   TCHK( hipHostGetDevicePointer( (void **)&s->h_in_dev, s->h_in, 0U ), "hipHostGetDevicePointer" );
   TCHK( hipHostGetDevicePointer( (void **)&s->h_outb_dev, s->h_outb, 0U ), "hipHostGetDevicePointer" );
-  TCHK( hipHostMalloc( (void **)&s->h_hs, HS_BYTES( sig_cap ), hipHostMallocCoherent ), "hipHostMalloc" );
+  /* the device-decode layout at the work arrays' stride (no points), or the
+     host-decode one at the small stride: room for the larger */
+  TCHK( hipHostMalloc( (void **)&s->h_hs, HS_O_PTS( sig_cap )>HS_BYTES( FD_ED25519_HS_STRIDE ) ? HS_O_PTS( sig_cap )
+                                                                                               : HS_BYTES( FD_ED25519_HS_STRIDE ),
+                       hipHostMallocCoherent ), "hipHostMalloc" );
   TCHK( hipHostGetDevicePointer( (void **)&s->h_hs_dev, s->h_hs, 0U ), "hipHostGetDevicePointer" );
   TCHK( hipMalloc(     (void **)&s->d_outb, out_sz                       ), "hipMalloc" );
   p->sigs        = s->h_in + o_sigs;                   s->d_sigs   = s->d_in + o_sigs;
@@ -533,7 +537,10 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
   unsigned long o_sigs = (unsigned long)( slot->sigs - s->h_in ), o_pubs = (unsigned long)( slot->pubs - s->h_in );
   int err, hd = n<=pipe_hd_max;
   int split = hd && pipe_split>2 && fd_ed25519_hip_private_want_dsms( s->eng, pipe_split ) ? pipe_split : 0;
-  volatile uint32_t * go = (volatile uint32_t *)( s->h_hs + HS_O_GO( cap ) );
+  /* the host block's stride: the work arrays' when the device decodes, a
+     small one when every array is this thread's (FD_ED25519_HS_STRIDE) */
+  unsigned long sc = hd ? FD_ED25519_HS_STRIDE : cap;
+  volatile uint32_t * go = (volatile uint32_t *)( s->h_hs + HS_O_GO( sc ) );
   if( !hd ) {
     PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_decode( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
                                                                    (signed char *)s->h_outb_dev, st ) );
@@ -545,24 +552,24 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
     if( split ) {
       PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsms( s->eng, split, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
                                                                    (signed char *)s->h_outb_dev, s->h_hs_dev,
-                                                                   s->h_hs_dev + cap,
-                                                                   (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
-                                                                   (int const *)( s->h_hs_dev + HS_O_PTS( cap ) ),
-                                                                   s->h_hs_dev + HS_O_PFL( cap ),
-                                                                   (unsigned int const *)( s->h_hs_dev + HS_O_GO( cap ) ), st ) );
+                                                                   s->h_hs_dev + sc,
+                                                                   (unsigned int const *)( s->h_hs_dev + HS_O_HS( sc ) ),
+                                                                   (int const *)( s->h_hs_dev + HS_O_PTS( sc ) ),
+                                                                   s->h_hs_dev + HS_O_PFL( sc ),
+                                                                   (unsigned int const *)( s->h_hs_dev + HS_O_GO( sc ) ), st ) );
     } else {
       PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
                                                                   (signed char *)s->h_outb_dev, s->h_hs_dev,
-                                                                  s->h_hs_dev + cap,
-                                                                  (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
-                                                                  (int const *)( s->h_hs_dev + HS_O_PTS( cap ) ),
-                                                                  s->h_hs_dev + HS_O_PFL( cap ),
-                                                                  (unsigned int const *)( s->h_hs_dev + HS_O_GO( cap ) ), st ) );
+                                                                  s->h_hs_dev + sc,
+                                                                  (unsigned int const *)( s->h_hs_dev + HS_O_HS( sc ) ),
+                                                                  (int const *)( s->h_hs_dev + HS_O_PTS( sc ) ),
+                                                                  s->h_hs_dev + HS_O_PFL( sc ),
+                                                                  (unsigned int const *)( s->h_hs_dev + HS_O_GO( sc ) ), st ) );
     }
     if( err ) return err;
   }
-  unsigned char * hsf = s->h_hs, * hhf = s->h_hs + cap;
-  uint32_t *      hs  = (uint32_t *)( s->h_hs + HS_O_HS( cap ) );
+  unsigned char * hsf = s->h_hs, * hhf = s->h_hs + sc;
+  uint32_t *      hs  = (uint32_t *)( s->h_hs + HS_O_HS( sc ) );
   int dbits = fd_ed25519_hip_private_half_dbits( s->eng );
   for( unsigned long i=0UL; i<n; i++ ) {
     uint32_t rec[ 32 ];
@@ -571,8 +578,8 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
       if( hd ) __atomic_store_n( go, FD_ED25519_GO_CANCEL, __ATOMIC_RELEASE );
       return 0;
     }
-    if( split ) fd_ed25519_hip_private_hssplit( rec, split, hs, cap, i );
-    else for( int w=0; w<19; w++ ) hs[ (unsigned long)w*cap + i ] = rec[ 8 + w ];
+    if( split ) fd_ed25519_hip_private_hssplit( rec, split, hs, sc, i );
+    else for( int w=0; w<19; w++ ) hs[ (unsigned long)w*sc + i ] = rec[ 8 + w ];
     hsf[ i ] = (unsigned char)rec[ 27 ];
     hhf[ i ] = (unsigned char)rec[ 28 ];
   }
@@ -584,17 +591,17 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
     for( unsigned long i=0UL; i<n; i++ ) { enc[ 2UL*i ] = slot->pubs + 32UL*i; enc[ 2UL*i+1UL ] = slot->sigs + 64UL*i; }
     fd_ed25519_hip_private_hsdec3_n( enc, 2UL*n, !fd_ed25519_hip_private_codes_portable( s->eng ), &pt[0][0],
                                      split ? &ptx[0][0] : NULL, nx, step, fl );
-    int32_t * pts = (int32_t *)( s->h_hs + HS_O_PTS( cap ) );
-    unsigned char * pfl = s->h_hs + HS_O_PFL( cap );
+    int32_t * pts = (int32_t *)( s->h_hs + HS_O_PTS( sc ) );
+    unsigned char * pfl = s->h_hs + HS_O_PFL( sc );
     unsigned long rs = split ? 40UL : 20UL;   /* the row stride in limbs: dsm16s's, dsm16's */
     for( unsigned long i=0UL; i<n; i++ )
       for( unsigned long side=0UL; side<2UL; side++ ) {   /* rows 2i + side: A, R, A_1, R_1, .. */
         unsigned long pi = 2UL*i + side;
-        for( unsigned long l=0UL; l<20UL; l++ ) pts[ ( side*rs + l )*cap + i ] = pt[ pi ][ l ];
+        for( unsigned long l=0UL; l<20UL; l++ ) pts[ ( side*rs + l )*sc + i ] = pt[ pi ][ l ];
         for( int m=1; m<=nx; m++ )
           for( unsigned long l=0UL; l<40UL; l++ )
-            pts[ ( ( 2UL*(unsigned long)m + side )*40UL + l )*cap + i ] = ptx[ pi*(unsigned long)nx + (unsigned long)(m-1) ][ l ];
-        pfl[ side*cap + i ] = fl[ pi ];
+            pts[ ( ( 2UL*(unsigned long)m + side )*40UL + l )*sc + i ] = ptx[ pi*(unsigned long)nx + (unsigned long)(m-1) ][ l ];
+        pfl[ side*sc + i ] = fl[ pi ];
       }
   }
   if( hd ) {
@@ -602,8 +609,8 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
   } else {
     PF_SUB( pf_sub_launch, err = fd_ed25519_hip_private_hs_dsm( s->eng, n, s->h_in_dev + o_sigs, s->h_in_dev + o_pubs,
                                                                 (signed char *)s->h_outb_dev, s->h_hs_dev,
-                                                                s->h_hs_dev + cap,
-                                                                (unsigned int const *)( s->h_hs_dev + HS_O_HS( cap ) ),
+                                                                s->h_hs_dev + sc,
+                                                                (unsigned int const *)( s->h_hs_dev + HS_O_HS( sc ) ),
                                                                 NULL, NULL, NULL, st ) );
     if( err ) return err;
   }
