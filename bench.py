@@ -411,6 +411,8 @@ def latency_mode(eng, args, device):
         return res["achieved_txn_per_s"]
 
     spin = cores[:2] if args.pin_threads and len(cores) >= 2 else None
+    if args.pipe_split_waves:
+        tile.pipe_set_split_waves(args.pipe_split_waves)
     try:
         with keep_off(spin, tile.device_cpus(eng.info()), args.isolate_cores):
             return latency_mode_loads(args, run_at, pay, n, device, lambda: ok, spin)
@@ -531,7 +533,8 @@ def latency_deployed(eng, args):
         if kind == "verify_hip":
             svc = subprocess.Popen([svc_bin, "--prefix", f"/fd_vhip_{app}_", "--tiles", "1", "--batch",
                                     str(args.latency_batch), "--slots", str(args.deployed_slots),
-                                    "--hw-queues", str(svc_queues), *svc_mode, *service_cpus],
+                                    "--hw-queues", str(svc_queues), *svc_mode, *service_cpus,
+                                    *(["--split-waves", str(args.pipe_split_waves)] if args.pipe_split_waves else [])],
                                    stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, preexec_fn=pin)
             line = svc.stdout.readline()
             if not line.startswith("ready"):
@@ -1092,6 +1095,9 @@ def main():
     ap.add_argument("--dev-kernargs", action="store_true",
                     help="leave HIP's kernel arguments in device memory (its default on this GPU; A/B)")
     ap.add_argument("--latency-txns", type=int, default=400000, help="0 disables the latency mode")
+    ap.add_argument("--pipe-split-waves", type=int, default=0,
+                    help="latency legs: small batches' group equation over 2, 4 or 8 waves "
+                         "(fd_ed25519_hip_pipe_set_split_waves, the service's --split-waves; 0: the library's)")
     ap.add_argument("--no-isolate-cores", dest="isolate_cores", action="store_false",
                     help="latency legs: leave this process's other threads and the children's unpinned ones free "
                          "to run on the spinning threads' cores (A/B)")

@@ -11,7 +11,7 @@
      fd_verify_hip_service --prefix NAME --tiles K [--gpu G] [--depth D]
                            [--slots S] [--batch B] [--gpu-parse | --zero-copy] [--codes portable|avx512]
                            [--tile-stale-ms T] [--gpu-hang-ms H] [--no-parent-watch] [--links-per-thread L]
-                           [--cpus LIST] [--hw-queues N]
+                           [--cpus LIST] [--hw-queues N] [--split-waves 2|4|8]
 
    creates, for k in [0,K), the links NAME<k>_txn (tile -> service) and
    NAME<k>_vd (service -> tile), each of D lines (default 16384), prints
@@ -114,7 +114,7 @@ static void
 usage( char const * argv0 ) {
   fprintf( stderr, "usage: %s --prefix NAME --tiles K [--gpu G] [--depth D] [--slots S] [--batch B] "
                    "[--gpu-parse | --zero-copy] [--codes portable|avx512] [--tile-stale-ms T] [--gpu-hang-ms H] "
-                   "[--no-parent-watch] [--links-per-thread L] [--cpus LIST] [--hw-queues N]\n", argv0 );
+                   "[--no-parent-watch] [--links-per-thread L] [--cpus LIST] [--hw-queues N] [--split-waves W]\n", argv0 );
 }
 
 /* "a,b,c-d" -> cpus (at most max); the count, or -1 on a malformed list */
@@ -163,6 +163,9 @@ main( int argc, char ** argv ) {
     else if( !strcmp( a, "--no-parent-watch" ) ) { parent_watch_on = 0; }
     else if( !strcmp( a, "--links-per-thread" ) && v ) { per_thread = (unsigned)strtoul( v, NULL, 0 ); i++; }
     else if( !strcmp( a, "--hw-queues" ) && v ) { hw_queues = (unsigned)strtoul( v, NULL, 0 ); i++; }
+    else if( !strcmp( a, "--split-waves" ) && v ) {   /* small batches' group equation: 2, 4 or 8 waves */
+      fd_ed25519_hip_pipe_set_split_waves( (int)strtol( v, NULL, 0 ) ); i++;
+    }
     else if( !strcmp( a, "--cpus" ) && v ) {
       cpu_cnt = parse_cpus( v, cpus, 256 );
       if( cpu_cnt<=0 ) { fprintf( stderr, "fd_verify_hip_service: bad --cpus list %s\n", v ); return 1; }
