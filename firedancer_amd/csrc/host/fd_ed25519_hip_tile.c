@@ -237,6 +237,12 @@ static unsigned long pipe_hd_max = PIPE_HD_MAX;
    (fd_ed25519_hip_dropin_set_split_waves) */
 static int pipe_split = 2;
 
+/* ... and only for batches of at most this many signatures: each one
+   more puts its doublings on the tile thread too */
+#ifndef PIPE_SPLIT_MAX_SIGS
+#define PIPE_SPLIT_MAX_SIGS 1UL
+#endif
+
 void
 fd_ed25519_hip_pipe_set_split_waves( int waves ) {
   pipe_split = waves==4 || waves==8 ? waves : 2;
@@ -536,7 +542,8 @@ pipe_submit_hs( fd_ed25519_hip_pipe_t * pipe, pipe_slot_t * s, hipStream_t st ) 
   unsigned long n = slot->sig_cnt, cap = slot->sig_cap;
   unsigned long o_sigs = (unsigned long)( slot->sigs - s->h_in ), o_pubs = (unsigned long)( slot->pubs - s->h_in );
   int err, hd = n<=pipe_hd_max;
-  int split = hd && pipe_split>2 && fd_ed25519_hip_private_want_dsms( s->eng, pipe_split ) ? pipe_split : 0;
+  int split = hd && n<=PIPE_SPLIT_MAX_SIGS && pipe_split>2 && fd_ed25519_hip_private_want_dsms( s->eng, pipe_split )
+              ? pipe_split : 0;
   /* the host block's stride: the work arrays' when the device decodes, a
      small one when every array is this thread's (FD_ED25519_HS_STRIDE) */
   unsigned long sc = hd ? FD_ED25519_HS_STRIDE : cap;
